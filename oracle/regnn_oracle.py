@@ -1,0 +1,509 @@
+"""CPU ORACLE for RE-GNN's relation-embedding message-passing hot path — TEST INFRASTRUCTURE.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+module, and only as the checker / the timed CPU baseline. The product path (``re-gnn_amd``) never
+imports it and has no CPU fallback.
+
+What it is: an independent numpy/scipy restatement (float64 by default) of the forward pass AND an
+explicit hand-derived backward (VJP) of each layer on the hot path, following the reference source:
+
+* ``REGraphConvOracle``   — layer/REGraphConv.py:52-106
+* ``REGATConvOracle``     — layer/REGATConv.py:64-100 (+ DGL ``edge_softmax`` semantics)
+* ``REMixHopConvOracle``  — layer/REMixHopConv.py:48-94
+* ``MagREGCNConvOracle``  — mag/regnn_layers.py:80-150 (self_loop_type 2, aggr='mean')
+* model wiring            — model/REGCN.py:35-46, model/REGAT.py:54-66, model/REMixHop.py:87-100
+
+Pinning: every class here is checked against golden vectors produced by running the REFERENCE's own
+layer/model source (tests/golden/make_golden.py, on a test-only DGL/PyG shim) — see
+tests/test_oracle.py. The DGL/PyG primitive semantics themselves (gspmm sum, edge_softmax,
+scatter-mean) come from their documentation: no reference test pins them.
+
+Graph convention (DGL): edge e goes src[e] -> dst[e]; messages flow src -> dst; aggregation is
+over the IN-edges of each destination; relation ids are 1-based (``table[rel - 1]``).
+"""
+import numpy as np
+import scipy.sparse as sp
+
+LRELU_SLOPE = 0.01  # nn.LeakyReLU() default, layer/REGraphConv.py:60
+
+
+# ------------------------------------------------------------------------------------------
+# primitives
+# ------------------------------------------------------------------------------------------
+def lrelu(x, slope=LRELU_SLOPE):
+    return np.where(x > 0, x, x * slope)
+
+
+def lrelu_grad(x, slope=LRELU_SLOPE):
+    # torch: d/dx = 1 if x > 0 else slope (slope at exactly 0)
+    return np.where(x > 0, 1.0, slope)
+
+
+def elu(x):
+    return np.where(x > 0, x, np.expm1(np.minimum(x, 0)))
+
+
+def elu_grad(x):
+    return np.where(x > 0, 1.0, np.exp(np.minimum(x, 0)))
+
+
+ACTS = {None: (lambda x: x, lambda x: np.ones_like(x)), "elu": (elu, elu_grad)}
+
+
+class Graph:
+    """src/dst edge lists (DGL order) + cached scipy adjacency (rows = dst, cols = src)."""
+
+    def __init__(self, src, dst, num_nodes, num_dst=None):
+        self.src = np.asarray(src, dtype=np.int64)
+        self.dst = np.asarray(dst, dtype=np.int64)
+        self.n_src = int(num_nodes)
+        self.n_dst = int(num_nodes if num_dst is None else num_dst)
+        self.E = self.src.size
+
+    def adj(self, w=None, dtype=np.float64):
+        """A[v, u] = sum of w over edges u->v (duplicates summed, = DGL gspmm u_mul_e + sum)."""
+        if w is None:
+            w = np.ones(self.E, dtype=dtype)
+        return sp.csr_matrix((np.asarray(w, dtype=dtype), (self.dst, self.src)),
+                             shape=(self.n_dst, self.n_src))
+
+    def in_sum(self, w):
+        """deg[v] = sum_{e: dst=v} w[e]   (update_all(u_mul_e('nones','ew'), sum))."""
+        return np.bincount(self.dst, weights=w, minlength=self.n_dst)
+
+    def out_sum(self, w):
+        return np.bincount(self.src, weights=w, minlength=self.n_src)
+
+    def edge_dot(self, a_dst, b_src, chunk=1 << 20):
+        """per-edge <a[dst[e]], b[src[e]]> over the trailing axis (SDDMM 'dot'), chunked."""
+        out = np.empty((self.E,) + a_dst.shape[1:-1], dtype=np.result_type(a_dst, b_src))
+        for s in range(0, self.E, chunk):
+            d, u = self.dst[s:s + chunk], self.src[s:s + chunk]
+            out[s:s + chunk] = np.einsum("e...f,e...f->e...", a_dst[d], b_src[u])
+        return out
+
+
+def rel_bins(rel, values, R):
+    """sum per relation of per-edge values; rel is 1-based. values (E,) or (E,H)."""
+    r = np.asarray(rel, dtype=np.int64) - 1
+    if values.ndim == 1:
+        return np.bincount(r, weights=values, minlength=R)[:, None]
+    return np.stack([np.bincount(r, weights=values[:, h], minlength=R)
+                     for h in range(values.shape[1])], axis=1)
+
+
+def degree_norm(g, ew):
+    """layer/REGraphConv.py:66-76: norm = clamp(in-degree weighted by ew, min=1)^-1/2."""
+    deg = g.in_sum(ew)
+    return deg, np.power(np.maximum(deg, 1.0), -0.5)
+
+
+def degree_norm_vjp(g, deg, g_norm):
+    """d norm/d ew[e] for every edge into v. clamp(min=1) passes the gradient where deg >= 1."""
+    g_deg = g_norm * (-0.5) * np.power(np.maximum(deg, 1.0), -1.5) * (deg >= 1.0)
+    return g_deg[g.dst]
+
+
+# ------------------------------------------------------------------------------------------
+# REGraphConv  (layer/REGraphConv.py:7-106)
+# ------------------------------------------------------------------------------------------
+class REGraphConvOracle:
+    def __init__(self, alpha, in_feats, out_feats, norm=True, activation=None, **_):
+        self.alpha, self.fin, self.fout = alpha, in_feats, out_feats
+        self.norm, self.act = norm, activation
+
+    def forward(self, g, feat, rel, edge_weight, weight=None, bias=None):
+        c = self.c = dict(feat=feat, weight=weight, bias=bias, rel=rel, edge_weight=edge_weight)
+        pre_tab = edge_weight * self.alpha                                  # :58
+        tab = lrelu(pre_tab)                                                # :60
+        ew = tab[np.asarray(rel) - 1, 0]                                    # :61
+        c.update(pre_tab=pre_tab, ew=ew)
+        x = feat
+        if self.norm:
+            deg, nrm = degree_norm(g, ew)                                   # :66-75
+            c.update(deg=deg, nrm=nrm)
+            x = feat * nrm[:, None]                                         # :76
+        A = g.adj(ew)
+        c["A"] = A
+        if self.fin > self.fout:                                            # :78
+            if weight is not None:
+                x = x @ weight                                              # :81
+            c["agg_in"] = x
+            rst = A @ x                                                     # :84-86
+        else:
+            c["agg_in"] = x
+            rst = A @ x                                                     # :91-93
+            c["agg_out"] = rst
+            if weight is not None:
+                rst = rst @ weight                                          # :95
+        c["pre_norm"] = rst
+        if self.norm:
+            rst = rst * c["nrm"][:, None]                                   # :98
+        if bias is not None:
+            rst = rst + bias                                                # :101
+        c["pre_act"] = rst
+        return ACTS[self.act][0](rst)                                       # :104
+
+    def backward(self, g, gout):
+        c = self.c
+        grads = {}
+        gr = gout * ACTS[self.act][1](c["pre_act"])
+        if c["bias"] is not None:
+            grads["bias"] = gr.sum(0)
+        g_nrm = None
+        if self.norm:
+            g_nrm = (gr * c["pre_norm"]).sum(1)
+            gr = gr * c["nrm"][:, None]
+        W, A = c["weight"], c["A"]
+        if self.fin > self.fout:
+            g_agg_out = gr
+        else:
+            if W is not None:
+                grads["weight"] = c["agg_out"].T @ gr
+                g_agg_out = gr @ W.T
+            else:
+                g_agg_out = gr
+        g_agg_in = A.T @ g_agg_out                                          # transposed SpMM
+        g_ew = g.edge_dot(g_agg_out, c["agg_in"])                           # SDDMM dot
+        if self.fin > self.fout and W is not None:
+            x_pre = c["feat"] * c["nrm"][:, None] if self.norm else c["feat"]
+            grads["weight"] = x_pre.T @ g_agg_in
+            g_x = g_agg_in @ W.T
+        else:
+            g_x = g_agg_in
+        if self.norm:
+            g_nrm = g_nrm + (g_x * c["feat"]).sum(1)
+            g_feat = g_x * c["nrm"][:, None]
+            g_ew = g_ew + degree_norm_vjp(g, c["deg"], g_nrm)
+        else:
+            g_feat = g_x
+        g_tab = rel_bins(c["rel"], g_ew, c["edge_weight"].shape[0])
+        grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        return g_feat, grads
+
+
+# ------------------------------------------------------------------------------------------
+# REGATConv  (layer/REGATConv.py:10-100)
+# ------------------------------------------------------------------------------------------
+def edge_softmax(g, z):
+    """per-destination softmax over in-edges, max-subtracted (DGL edge_softmax). z (E,H)."""
+    H = z.shape[1]
+    mx = np.full((g.n_dst, H), -np.inf)
+    np.maximum.at(mx, g.dst, z)
+    ex = np.exp(z - mx[g.dst])
+    s = np.zeros((g.n_dst, H))
+    np.add.at(s, g.dst, ex)
+    return ex / s[g.dst]
+
+
+class REGATConvOracle:
+    def __init__(self, alpha, in_feats, out_feats, num_heads, negative_slope=0.2,
+                 residual=False, activation=None, use_weight=True, edge_feats=True, **_):
+        self.alpha, self.fin, self.D, self.H = alpha, in_feats, out_feats, num_heads
+        self.slope, self.residual, self.act = negative_slope, residual, activation
+        self.use_weight, self.use_ee = use_weight, edge_feats
+
+    def forward(self, g, feat, rel, P):
+        """P: dict of reference parameter names -> arrays (fc.weight, attn_l, attn_r,
+        edge_weight, res_fc.weight)."""
+        N, H, D = feat.shape[0], self.H, self.D
+        c = self.c = dict(feat=feat, rel=rel, P=P)
+        ft = (feat @ P["fc.weight"].T if self.use_weight else feat).reshape(N, H, D)   # :67
+        el = (ft * P["attn_l"]).sum(-1)                                                 # :68
+        er = (ft * P["attn_r"]).sum(-1)                                                 # :69
+        s = el[g.src] + er[g.dst]                                                       # :80
+        if self.use_ee:
+            pre_tab = P["edge_weight"] * self.alpha                                     # :72
+            c["pre_tab"] = pre_tab
+            s = s + lrelu(pre_tab)[np.asarray(rel) - 1]                                 # :74-84
+        z = lrelu(s, self.slope)                                                        # :86
+        a = edge_softmax(g, z)                                                          # :88
+        out = np.zeros((g.n_dst, H, D))
+        for h in range(H):
+            out[:, h, :] = g.adj(a[:, h]) @ ft[:, h, :]                                  # :90-91
+        if self.residual:
+            if "res_fc.weight" in P:
+                res = (feat @ P["res_fc.weight"].T).reshape(N, -1, D)                   # :94
+            else:
+                res = feat.reshape(N, -1, D)
+            c["res_shape"] = res.shape
+            out = out + res
+        c.update(ft=ft, s=s, a=a, pre_act=out)
+        return ACTS[self.act][0](out)
+
+    def backward(self, g, gout):
+        c, P = self.c, self.c["P"]
+        feat, ft, a, s = c["feat"], c["ft"], c["a"], c["s"]
+        N, H, D = feat.shape[0], self.H, self.D
+        grads = {}
+        go = gout * ACTS[self.act][1](c["pre_act"])
+        g_feat = np.zeros_like(feat)
+        if self.residual:
+            if "res_fc.weight" in P:
+                gr = go.reshape(N, H * D)
+                grads["res_fc.weight"] = gr.T @ feat
+                g_feat += gr @ P["res_fc.weight"]
+            else:
+                g_feat += go.sum(1).reshape(N, -1) if c["res_shape"][1] == 1 else go.reshape(N, -1)
+        g_ft = np.zeros_like(ft)
+        g_a = np.zeros((g.E, H))
+        for h in range(H):
+            g_ft[:, h, :] = g.adj(a[:, h]).T @ go[:, h, :]
+        g_a = g.edge_dot(go, ft)                                        # (E,H)
+        t = np.zeros((g.n_dst, H))
+        np.add.at(t, g.dst, a * g_a)
+        g_z = a * (g_a - t[g.dst])                                      # softmax VJP
+        g_s = g_z * lrelu_grad(s, self.slope)
+        g_el = np.zeros((N, H))
+        np.add.at(g_el, g.src, g_s)
+        g_er = np.zeros((N, H))
+        np.add.at(g_er, g.dst, g_s)
+        if self.use_ee:
+            g_tab = rel_bins(c["rel"], g_s, P["edge_weight"].shape[0])
+            grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        g_ft += g_el[..., None] * P["attn_l"] + g_er[..., None] * P["attn_r"]
+        grads["attn_l"] = (g_el[..., None] * ft).sum(0, keepdims=True)
+        grads["attn_r"] = (g_er[..., None] * ft).sum(0, keepdims=True)
+        gf = g_ft.reshape(N, H * D)
+        if self.use_weight:
+            grads["fc.weight"] = gf.T @ feat
+            g_feat += gf @ P["fc.weight"]
+        else:
+            g_feat += gf
+        return g_feat, grads
+
+
+# ------------------------------------------------------------------------------------------
+# REMixHopConv  (layer/REMixHopConv.py:7-94)
+# ------------------------------------------------------------------------------------------
+class REMixHopConvOracle:
+    def __init__(self, alpha, in_feats, out_feats, p=(0, 1, 2), activation=None, **_):
+        self.alpha, self.p, self.act = alpha, list(p), activation
+
+    def forward(self, g, feats, rel, P):
+        c = self.c = dict(rel=rel, P=P)
+        pre_tab = P["edge_weight"] * self.alpha
+        ew = lrelu(pre_tab)[np.asarray(rel) - 1, 0]                         # :50-55
+        deg, nrm = degree_norm(g, ew)                                       # :58-64
+        A1 = g.adj(None)                                                    # copy_u: unweighted
+        fs, outs = [feats], []
+        for j in range(max(self.p) + 1):                                    # :72
+            if j in self.p:
+                outs.append(fs[-1] @ P[f"weights.{j}.weight"].T)            # :74-76
+            if j < max(self.p):   # the last propagate (:78-82) feeds nothing: skipped
+                fs.append(nrm[:, None] * (A1 @ (nrm[:, None] * fs[-1])))
+        final = np.concatenate(outs, axis=1)                                # :84
+        c.update(pre_tab=pre_tab, deg=deg, nrm=nrm, A1=A1, fs=fs, pre_act=final)
+        return ACTS[self.act][0](final)                                     # :88-90
+
+    def backward(self, g, gout):
+        c, P = self.c, self.c["P"]
+        nrm, A1, fs = c["nrm"][:, None], c["A1"], c["fs"]
+        gf_all = gout * ACTS[self.act][1](c["pre_act"])
+        grads = {}
+        width = gf_all.shape[1] // len(self.p)
+        g_f = [np.zeros_like(f) for f in fs]
+        for k, j in enumerate(self.p):
+            go = gf_all[:, k * width:(k + 1) * width]
+            grads[f"weights.{j}.weight"] = go.T @ fs[j]
+            g_f[j] += go @ P[f"weights.{j}.weight"]
+        g_nrm = np.zeros(nrm.shape[0])
+        for j in range(len(fs) - 1, 0, -1):     # f_j = nrm * A1 (nrm * f_{j-1})
+            gy = g_f[j]
+            t = A1 @ (nrm * fs[j - 1])
+            back = A1.T @ (nrm * gy)
+            g_nrm += (gy * t).sum(1) + (fs[j - 1] * back).sum(1)
+            g_f[j - 1] += nrm * back
+        g_ew = degree_norm_vjp(g, c["deg"], g_nrm)
+        g_tab = rel_bins(c["rel"], g_ew, P["edge_weight"].shape[0])
+        grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        return g_f[0], grads
+
+
+# ------------------------------------------------------------------------------------------
+# mag REGCNConv  (mag/regnn_layers.py:24-150), self_loop_type == 2, aggr='mean'
+# ------------------------------------------------------------------------------------------
+def layer_norm(x, w, b, eps=1e-5):
+    mu = x.mean(1, keepdims=True)
+    var = x.var(1, keepdims=True)
+    rstd = 1.0 / np.sqrt(var + eps)
+    xh = (x - mu) * rstd
+    return xh * w + b, (xh, rstd)
+
+
+def layer_norm_vjp(g, w, cache):
+    xh, rstd = cache
+    gxh = g * w
+    gx = rstd * (gxh - gxh.mean(1, keepdims=True) - xh * (gxh * xh).mean(1, keepdims=True))
+    return gx, (g * xh).sum(0), g.sum(0)
+
+
+class MagREGCNConvOracle:
+    def __init__(self, n_dst, num_edge_types, scaling_factor, residual=False, use_norm="ln", **_):
+        self.n_dst, self.net = n_dst, num_edge_types
+        self.alpha, self.residual, self.use_norm = scaling_factor, residual, use_norm
+
+    def block(self, src, dst, edge_type, target_node_type, n_src):
+        """append target self loops typed ntype + num_edge_types (mag/regnn_layers.py:90-96)."""
+        loop = np.arange(self.n_dst)
+        s = np.concatenate([src, loop])
+        d = np.concatenate([dst, loop])
+        t = np.concatenate([edge_type, np.asarray(target_node_type) + self.net])
+        return Graph(s, d, n_src, num_dst=self.n_dst), t
+
+    def forward(self, x, src, dst, edge_type, target_node_type, P):
+        g, et = self.block(src, dst, edge_type, target_node_type, x.shape[0])
+        W = P["weight"]
+        xs = x @ W                                                          # :102
+        xt = x[:self.n_dst] @ W                                             # :104/106
+        pre_tab = P["relation_weight"] * self.alpha                         # :110
+        ew = lrelu(pre_tab)[et]                                             # :111-113 (one-hot)
+        cnt = np.maximum(np.bincount(g.dst, minlength=self.n_dst), 1).astype(np.float64)
+        agg = (g.adj(ew) @ xs) / cnt[:, None]                               # aggr='mean' :129
+        out = agg + P["bias"]                                               # update() :148
+        if self.residual:
+            out = out + xt                                                  # :131-132
+        ln = None
+        if self.use_norm == "ln":
+            out, ln = layer_norm(out, P["norm.weight"], P["norm.bias"])     # :134-135
+        self.c = dict(g=g, et=et, x=x, xs=xs, ew=ew, cnt=cnt, pre_tab=pre_tab, ln=ln, P=P)
+        return out
+
+    def backward(self, gout):
+        c, P = self.c, self.c["P"]
+        g, W = c["g"], P["weight"]
+        grads = {}
+        if self.use_norm == "ln":
+            gout, grads["norm.weight"], grads["norm.bias"] = layer_norm_vjp(
+                gout, P["norm.weight"], c["ln"])
+        grads["bias"] = gout.sum(0)
+        gm = gout / c["cnt"][:, None]
+        g_xs = g.adj(c["ew"]).T @ gm
+        g_ew = g.edge_dot(gm, c["xs"])
+        R = P["relation_weight"].shape[0]
+        g_tab = np.bincount(c["et"], weights=g_ew, minlength=R)
+        grads["relation_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        x = c["x"]
+        gW = x.T @ g_xs
+        g_x = g_xs @ W.T
+        if self.residual:
+            gW += x[:self.n_dst].T @ gout
+            g_x[:self.n_dst] += gout @ W.T
+        grads["weight"] = gW
+        return g_x, grads
+
+
+# ------------------------------------------------------------------------------------------
+# model wiring (eval mode: dropout = identity)
+# ------------------------------------------------------------------------------------------
+class Linear:
+    def __init__(self, W, b=None):
+        self.W, self.b = W, b
+
+    def forward(self, x):
+        self.x = x
+        y = x @ self.W.T
+        return y + self.b if self.b is not None else y
+
+    def backward(self, g):
+        gr = {"weight": g.T @ self.x}
+        if self.b is not None:
+            gr["bias"] = g.sum(0)
+        return g @ self.W, gr
+
+
+def _input_proj(P, feats):
+    lins = [Linear(P[f"fc_list.{i}.weight"], P[f"fc_list.{i}.bias"]) for i in range(len(feats))]
+    return lins, np.concatenate([l.forward(f) for l, f in zip(lins, feats)], 0)
+
+
+def _input_proj_vjp(lins, feats, g, grads):
+    o = 0
+    for i, (l, f) in enumerate(zip(lins, feats)):
+        _, gr = l.backward(g[o:o + f.shape[0]])
+        o += f.shape[0]
+        grads[f"fc_list.{i}.weight"], grads[f"fc_list.{i}.bias"] = gr["weight"], gr["bias"]
+
+
+def regcn_model(g, feats, rel, P, num_layers, alpha, gout):
+    """model/REGCN.py:6-46 forward + VJP. Returns logits, embeddings, grads."""
+    lins, h = _input_proj(P, feats)
+    layers = []
+    for l in range(num_layers):
+        mid = 0 < l < num_layers - 1
+        layers.append(REGraphConvOracle(alpha, h.shape[1], h.shape[1], norm=True,
+                                        activation="elu" if mid else None))
+        h = layers[-1].forward(g, h, rel, P[f"layers.{l}.edge_weight"],
+                               P.get(f"layers.{l}.weight"), P.get(f"layers.{l}.bias"))
+    out_lin = Linear(P["out_lin.weight"], P["out_lin.bias"])
+    logits = out_lin.forward(h)
+    grads = {}
+    gh, gr = out_lin.backward(gout)
+    grads["out_lin.weight"], grads["out_lin.bias"] = gr["weight"], gr["bias"]
+    for l in range(num_layers - 1, -1, -1):
+        gh, gr = layers[l].backward(g, gh)
+        for k, v in gr.items():
+            grads[f"layers.{l}.{k}"] = v
+    _input_proj_vjp(lins, feats, gh, grads)
+    return logits, h, grads
+
+
+def regat_model(g, feats, rel, P, num_layers, heads, hidden, alpha, gout, slope=0.01):
+    """model/REGAT.py:6-66: per-type Linear, L GAT layers (ELU), last layer applied TWICE."""
+    lins, h = _input_proj(P, feats)
+
+    def params(l):
+        pre = f"gat_layers.{l}."
+        return {k[len(pre):]: v for k, v in P.items() if k.startswith(pre)}
+
+    def make(l, width):
+        if l < num_layers - 1:   # input / hidden layers: fc + ELU (model/REGAT.py:84-92)
+            return REGATConvOracle(alpha, width, hidden, heads[l], slope, residual=False,
+                                   activation="elu", use_weight=True)
+        # output layer: Identity fc, no activation, heads[-2] (model/REGAT.py:94-97)
+        return REGATConvOracle(alpha, width, hidden, heads[-2], slope, residual=False,
+                               activation=None, use_weight=False)
+
+    calls = []
+    seq = list(range(num_layers)) + [num_layers - 1]   # last layer applied twice (:61-64)
+    for i, l in enumerate(seq):
+        o = make(l, h.shape[1])
+        y = o.forward(g, h, rel, params(l))
+        calls.append((l, o))
+        h = y.reshape(h.shape[0], -1) if i < len(seq) - 1 else y
+    emb = h
+    out_lin = Linear(P["out_lin.weight"], P["out_lin.bias"])
+    logits = out_lin.forward(emb.reshape(emb.shape[0], -1))
+    grads = {}
+    gh, gr = out_lin.backward(gout)
+    grads["out_lin.weight"], grads["out_lin.bias"] = gr["weight"], gr["bias"]
+    for l, o in reversed(calls):
+        gh, gr = o.backward(g, gh.reshape(gh.shape[0], o.H, o.D))
+        for k, v in gr.items():
+            key = f"gat_layers.{l}.{k}"
+            grads[key] = grads.get(key, 0) + v
+        gh = gh.reshape(gh.shape[0], -1)
+    _input_proj_vjp(lins, feats, gh, grads)
+    return logits, emb.mean(1), grads
+
+
+def remixhop_model(g, feats, rel, P, num_layers, hidden, alpha, gout, p=(0, 1, 2)):
+    """model/REMixHop.py:19-100 (activation ELU, no batchnorm, dropout 0)."""
+    lins, h = _input_proj(P, feats)
+    layers = []
+    for l in range(num_layers):
+        o = REMixHopConvOracle(alpha, h.shape[1], hidden, p=p, activation="elu")
+        pl = {k[len(f"layers.{l}."):]: v for k, v in P.items() if k.startswith(f"layers.{l}.")}
+        h = o.forward(g, h, rel, pl)
+        layers.append(o)
+    fc = Linear(P["fc_layers.weight"])
+    logits = fc.forward(h)
+    grads = {}
+    gh, gr = fc.backward(gout)
+    grads["fc_layers.weight"] = gr["weight"]
+    for l in range(num_layers - 1, -1, -1):
+        gh, gr = layers[l].backward(g, gh)
+        for k, v in gr.items():
+            grads[f"layers.{l}.{k}"] = v
+    _input_proj_vjp(lins, feats, gh, grads)
+    return logits, h, grads

@@ -1,0 +1,318 @@
+"""Generate the golden vectors in tests/golden/*.npz by running the REFERENCE's own layer/model
+source (imported read-only from /root/reference) on a test-only pure-torch DGL/PyG shim
+(tests/golden/refshim), in float64 on the CPU of this container.
+
+This script is the ONLY place the reference is executed. It needs /root/reference and is never
+run on the GPU box (it is listed in .gpurunignore); the fixtures it writes are plain data
+(inputs + expected outputs + expected gradients) and travel with the repo.
+
+Run:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+
+Every input is drawn in float32 and widened, so the fp32 GPU path consumes bit-identical inputs;
+outputs and gradients are computed in float64 and stored rounded to float32.
+"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+SHIM = os.path.join(HERE, "refshim")
+
+
+def _purge(prefixes):
+    for name in list(sys.modules):
+        if any(name == p or name.startswith(p + ".") for p in prefixes):
+            del sys.modules[name]
+
+
+def _use_paths(paths):
+    for p in reversed(paths):
+        if p in sys.path:
+            sys.path.remove(p)
+        sys.path.insert(0, p)
+
+
+# ------------------------------------------------------------------------------------------
+# small seeded multi-relation graphs
+# ------------------------------------------------------------------------------------------
+def make_hetero_graph(rng, type_counts, n_edges, n_dup=10, isolate=5):
+    """Random typed directed graph WITHOUT self loops, then self loops appended (DGL order).
+
+    Relation id of a non-loop edge = 1 + index of its (src type, dst type) pair among the pairs
+    present; self loop of a node of type t gets ``num_etype + t + 1`` (run_regnn.py:91-98).
+    ``isolate`` nodes receive no in-edges except their self loop (deg == ew_self exercises clamp).
+    """
+    T = len(type_counts)
+    N = int(sum(type_counts))
+    ntype = np.repeat(np.arange(T), type_counts)
+    allowed_dst = np.arange(isolate, N)
+    src = rng.integers(0, N, size=n_edges)
+    dst = rng.choice(allowed_dst, size=n_edges)
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    # duplicates (multigraph edges)
+    di = rng.integers(0, src.size, size=n_dup)
+    src = np.concatenate([src, src[di]])
+    dst = np.concatenate([dst, dst[di]])
+    pairs = ntype[src] * T + ntype[dst]
+    uniq = np.unique(pairs)
+    pair_id = {int(p): i + 1 for i, p in enumerate(uniq)}
+    num_etype = len(uniq)
+    rel = np.array([pair_id[int(p)] for p in pairs], dtype=np.int64)
+    loops = np.arange(N)
+    src = np.concatenate([src, loops]).astype(np.int64)
+    dst = np.concatenate([dst, loops]).astype(np.int64)
+    rel = np.concatenate([rel, num_etype + ntype + 1]).astype(np.int64)
+    R = num_etype + T
+    return dict(src=src, dst=dst, rel=rel, N=N, R=R, ntype=ntype.astype(np.int64),
+                type_counts=np.asarray(type_counts, dtype=np.int64))
+
+
+def f32(rng, *shape, scale=1.0):
+    return (rng.standard_normal(shape) * scale).astype(np.float32)
+
+
+def _set_params(module, rng, ew_alpha=None):
+    """Overwrite every parameter with fp32-representable values (edge_weight: alpha*w in
+    U(-0.5, 1.5) so both LeakyReLU slopes and the degree clamp are exercised)."""
+    for name, p in module.named_parameters():
+        leaf = name.split(".")[-1]
+        if leaf in ("edge_weight", "relation_weight") and ew_alpha is not None:
+            v = rng.uniform(-0.5, 1.5, size=tuple(p.shape)).astype(np.float32) / np.float32(ew_alpha)
+            v = v.astype(np.float32)
+        elif leaf == "bias" or "norm" in name or leaf.startswith("bn"):
+            v = (rng.standard_normal(tuple(p.shape)) * 0.1).astype(np.float32)
+            if "norm.weight" in name:
+                v = (1.0 + v).astype(np.float32)
+        else:
+            v = f32(rng, *p.shape, scale=0.2)
+        with torch.no_grad():
+            p.copy_(torch.from_numpy(v.astype(np.float64)))
+
+
+def _pack(prefix, d, store):
+    for k, v in d.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        v = np.asarray(v)
+        if v.dtype == np.float64:
+            v = v.astype(np.float32)
+        store[prefix + k] = v
+
+
+def _params(module):
+    return {n: p.detach() for n, p in module.named_parameters()}
+
+
+def _grads(module):
+    return {n: p.grad for n, p in module.named_parameters() if p.grad is not None}
+
+
+def save(name, meta, store):
+    for k, v in list(store.items()):
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        if isinstance(v, np.ndarray) and v.dtype == np.float64:
+            v = v.astype(np.float32)
+        store[k] = v
+    store["meta"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **store)
+    print(f"wrote {path} ({os.path.getsize(path)//1024} KB)")
+
+
+# ------------------------------------------------------------------------------------------
+# full-batch layers (layer/*.py through the dgl shim)
+# ------------------------------------------------------------------------------------------
+def gen_layers():
+    _purge(["dgl", "layer", "model", "utils"])
+    _use_paths([SHIM, REF])
+    import dgl
+    layer = importlib.import_module("layer")
+    import torch.nn.functional as F
+
+    rng = np.random.default_rng(0)
+    gd = make_hetero_graph(rng, [60, 70, 40, 30], 1800)
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    e_feat = torch.from_numpy(gd["rel"])
+    N, R = gd["N"], gd["R"]
+
+    # REGraphConv variants: (tag, in, out, kwargs)
+    gcn_cases = [
+        ("norm_noweight", 64, 64, dict(norm=True, bias=False, weight=False)),
+        ("norm_weight_bias_elu", 64, 64, dict(norm=True, bias=True, weight=True, activation="elu")),
+        ("nonorm_noweight", 64, 64, dict(norm=False, bias=False, weight=False)),
+        ("norm_in_gt_out", 64, 32, dict(norm=True, bias=True, weight=True)),
+        ("nonorm_in_lt_out", 32, 64, dict(norm=False, bias=True, weight=True)),
+    ]
+    alpha = 100.0
+    for tag, fin, fout, kw in gcn_cases:
+        kw = dict(kw)
+        act = kw.pop("activation", None)
+        torch.manual_seed(1)
+        m = layer.REGraphConv(R, alpha, fin, fout, activation=F.elu if act else None, **kw)
+        _set_params(m, rng, ew_alpha=alpha)
+        feat = torch.from_numpy(f32(rng, N, fin).astype(np.float64)).requires_grad_(True)
+        out = m(g, feat, e_feat)
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = {}
+        _pack("g_", gd, st)
+        st["feat"], st["gout"], st["out"] = feat.detach().numpy().astype(np.float32), gout, out
+        st["grad_feat"] = feat.grad
+        _pack("p_", _params(m), st)
+        _pack("grad_", _grads(m), st)
+        save(f"regraphconv_{tag}", dict(layer="REGraphConv", alpha=alpha, in_feats=fin,
+                                         out_feats=fout, activation=act, **kw), st)
+
+    # REGATConv variants
+    gat_cases = [
+        ("h4_ee", 32, 32, 4, dict(residual=False, use_weight=True), True, None),
+        ("h4_noee", 32, 32, 4, dict(residual=False, use_weight=True), False, None),
+        ("h8_d64_ee_res_elu", 48, 64, 8, dict(residual=True, use_weight=True), True, "elu"),
+        ("h4_noweight_res", 128, 32, 4, dict(residual=True, use_weight=False), True, None),
+    ]
+    for tag, fin, fout, H, kw, use_ee, act in gat_cases:
+        torch.manual_seed(2)
+        m = layer.REGATConv(R, alpha, fin, fout, H, 0.0, 0.0, 0.01, kw["residual"],
+                            F.elu if act else None, use_weight=kw["use_weight"])
+        _set_params(m, rng, ew_alpha=alpha)
+        feat = torch.from_numpy(f32(rng, N, fin).astype(np.float64)).requires_grad_(True)
+        out = m(g, feat, e_feat if use_ee else None)
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = {}
+        _pack("g_", gd, st)
+        st["feat"], st["gout"], st["out"] = feat.detach().numpy().astype(np.float32), gout, out
+        st["grad_feat"] = feat.grad
+        _pack("p_", _params(m), st)
+        _pack("grad_", _grads(m), st)
+        save(f"regatconv_{tag}", dict(layer="REGATConv", alpha=alpha, in_feats=fin, out_feats=fout,
+                                       num_heads=H, negative_slope=0.01, edge_feats=use_ee,
+                                       activation=act, **kw), st)
+
+    # REMixHopConv variants
+    mix_cases = [("f64", 64, 64, None), ("f192_elu", 192, 64, "elu")]
+    for tag, fin, fout, act in mix_cases:
+        torch.manual_seed(3)
+        m = layer.REMixHopConv(R, alpha, fin, fout, p=[0, 1, 2], dropout=0,
+                               activation=F.elu if act else None, batchnorm=False)
+        _set_params(m, rng, ew_alpha=alpha)
+        feat = torch.from_numpy(f32(rng, N, fin).astype(np.float64)).requires_grad_(True)
+        out = m(g, feat, e_feat)
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = {}
+        _pack("g_", gd, st)
+        st["feat"], st["gout"], st["out"] = feat.detach().numpy().astype(np.float32), gout, out
+        st["grad_feat"] = feat.grad
+        _pack("p_", _params(m), st)
+        _pack("grad_", _grads(m), st)
+        save(f"remixhopconv_{tag}", dict(layer="REMixHopConv", alpha=alpha, in_feats=fin,
+                                          out_feats=fout, p=[0, 1, 2], activation=act), st)
+    return gd
+
+
+# ------------------------------------------------------------------------------------------
+# whole models (model/*.py), eval mode / dropout 0
+# ------------------------------------------------------------------------------------------
+def gen_models():
+    _purge(["dgl", "layer", "model", "utils"])
+    _use_paths([SHIM, REF])
+    import dgl
+    import torch.nn.functional as F
+    REGCN = importlib.import_module("model.REGCN").REGCN
+    REGAT = importlib.import_module("model.REGAT").REGAT
+    REMixHop = importlib.import_module("model.REMixHop").REMixHop
+
+    rng = np.random.default_rng(10)
+    type_counts = [50, 60, 30, 20]
+    dims = [24, 40, 12, 20]
+    gd = make_hetero_graph(rng, type_counts, 1500)
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    e_feat = torch.from_numpy(gd["rel"])
+    R = gd["R"]
+    alpha = 100.0
+    n_classes = 4
+
+    def run(tag, net, meta):
+        _set_params(net, rng, ew_alpha=alpha)
+        net.eval()
+        feats = [torch.from_numpy(f32(rng, n, d).astype(np.float64))
+                 for n, d in zip(type_counts, dims)]
+        logits, emb = net(feats, e_feat)
+        gout = f32(rng, *logits.shape)
+        logits.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = {}
+        _pack("g_", gd, st)
+        for i, f in enumerate(feats):
+            st[f"feat{i}"] = f.numpy().astype(np.float32)
+        st["gout"], st["logits"], st["emb"] = gout, logits, emb
+        _pack("p_", _params(net), st)
+        _pack("grad_", _grads(net), st)
+        meta.update(alpha=alpha, dims=dims, n_classes=n_classes)
+        save(f"model_{tag}", meta, st)
+
+    torch.manual_seed(4)
+    run("regcn2", REGCN(g, R, alpha, 64, 64, n_classes, 2, F.elu, 0.0, dims),
+        dict(model="REGCN", num_layers=2, hidden=64))
+    torch.manual_seed(5)
+    run("regcn4", REGCN(g, R, alpha, 64, 64, n_classes, 4, F.elu, 0.0, dims),
+        dict(model="REGCN", num_layers=4, hidden=64))
+    torch.manual_seed(6)
+    heads = [8, 8, 1]
+    run("regat2", REGAT(g, R, alpha, 2, 32, 32, n_classes, heads, F.elu, 0.0, 0.0, 0.01, False,
+                        dims), dict(model="REGAT", num_layers=2, hidden=32, heads=heads))
+    torch.manual_seed(7)
+    run("remixhop2", REMixHop(g, R, alpha, 64, 64, n_classes, 2, dims, input_dropout=0.0,
+                              activation=F.elu), dict(model="REMixHop", num_layers=2, hidden=64))
+
+
+# ------------------------------------------------------------------------------------------
+# mag REGCNConv (mag/regnn_layers.py) on a bipartite sampled block
+# ------------------------------------------------------------------------------------------
+def gen_mag():
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+
+    rng = np.random.default_rng(20)
+    n_src, n_dst, E = 300, 100, 1500
+    num_node_types, num_edge_types = 4, 7
+    src = rng.integers(0, n_src, size=E).astype(np.int64)
+    dst = rng.integers(0, n_dst, size=E).astype(np.int64)
+    # a few targets with no sampled in-edges (only the appended self loop)
+    dst[np.isin(dst, [3, 17, 42])] = 5
+    edge_type = rng.integers(0, num_edge_types, size=E).astype(np.int64)
+    tnt = rng.integers(0, num_node_types, size=n_dst).astype(np.int64)
+    for residual in (False, True):
+        torch.manual_seed(8)
+        conv = regnn_layers.REGCNConv(64, 64, num_node_types, num_edge_types, 10.0,
+                                      residual=residual, use_norm="ln", self_loop_type=2)
+        _set_params(conv, rng, ew_alpha=10.0)
+        x = torch.from_numpy(f32(rng, n_src, 64).astype(np.float64)).requires_grad_(True)
+        ei = torch.from_numpy(np.stack([src, dst]))
+        out = conv((x, x[:n_dst]), ei, torch.from_numpy(edge_type), torch.from_numpy(tnt))
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = dict(src=src, dst=dst, edge_type=edge_type, target_node_type=tnt,
+                  x=x.detach().numpy().astype(np.float32), gout=gout, out=out, grad_x=x.grad)
+        _pack("p_", _params(conv), st)
+        _pack("grad_", _grads(conv), st)
+        save(f"mag_regcnconv_res{int(residual)}",
+             dict(layer="mag.REGCNConv", n_src=n_src, n_dst=n_dst, num_node_types=num_node_types,
+                  num_edge_types=num_edge_types, scaling_factor=10.0, residual=residual,
+                  use_norm="ln", self_loop_type=2), st)
+
+
+if __name__ == "__main__":
+    torch.set_default_dtype(torch.float64)
+    gen_layers()
+    gen_models()
+    gen_mag()

@@ -1,0 +1,115 @@
+"""Pin the CPU oracle (oracle/regnn_oracle.py) against golden vectors produced by the REFERENCE
+source (tests/golden/make_golden.py). CPU only."""
+import numpy as np
+import pytest
+
+import _golden as G
+from oracle import regnn_oracle as O
+
+TOL = 1e-9 * 0 + 2e-6   # fixtures are fp64 results stored as fp32 -> ~1e-7 rounding
+
+
+def _graph(d):
+    return O.Graph(d["g_src"], d["g_dst"], int(d["g_N"]))
+
+
+def _check(tag, got, want, tol=TOL):
+    ok, err = G.close(got, want, tol)
+    assert ok, f"{tag}: rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("name", G.names("regraphconv_"))
+def test_regraphconv(name):
+    d = G.load(name)
+    m = d["meta"]
+    g = _graph(d)
+    P = G.sub(d, "p_")
+    o = O.REGraphConvOracle(**m)
+    out = o.forward(g, d["feat"].astype(np.float64), d["g_rel"], P["edge_weight"],
+                    P.get("weight"), P.get("bias"))
+    _check("out", out, d["out"])
+    gf, gr = o.backward(g, d["gout"].astype(np.float64))
+    _check("grad_feat", gf, d["grad_feat"])
+    for k, v in G.sub(d, "grad_").items():
+        if k == "feat":
+            continue
+        _check(k, gr[k], v)
+
+
+@pytest.mark.parametrize("name", G.names("regatconv_"))
+def test_regatconv(name):
+    d = G.load(name)
+    m = d["meta"]
+    g = _graph(d)
+    P = G.sub(d, "p_")
+    o = O.REGATConvOracle(**m)
+    out = o.forward(g, d["feat"].astype(np.float64), d["g_rel"], P)
+    _check("out", out, d["out"])
+    gf, gr = o.backward(g, d["gout"].astype(np.float64))
+    _check("grad_feat", gf, d["grad_feat"])
+    for k, v in G.sub(d, "grad_").items():
+        if k == "feat":
+            continue
+        _check(k, gr[k], v)
+
+
+@pytest.mark.parametrize("name", G.names("remixhopconv_"))
+def test_remixhopconv(name):
+    d = G.load(name)
+    m = d["meta"]
+    g = _graph(d)
+    P = G.sub(d, "p_")
+    o = O.REMixHopConvOracle(**m)
+    out = o.forward(g, d["feat"].astype(np.float64), d["g_rel"], P)
+    _check("out", out, d["out"])
+    gf, gr = o.backward(g, d["gout"].astype(np.float64))
+    _check("grad_feat", gf, d["grad_feat"])
+    for k, v in G.sub(d, "grad_").items():
+        if k == "feat":
+            continue
+        _check(k, gr[k], v)
+
+
+@pytest.mark.parametrize("name", G.names("mag_regcnconv_"))
+def test_mag_regcnconv(name):
+    d = G.load(name)
+    m = d["meta"]
+    P = G.sub(d, "p_")
+    o = O.MagREGCNConvOracle(**m)
+    out = o.forward(d["x"].astype(np.float64), d["src"], d["dst"], d["edge_type"],
+                    d["target_node_type"], P)
+    _check("out", out, d["out"])
+    gx, gr = o.backward(d["gout"].astype(np.float64))
+    _check("grad_x", gx, d["grad_x"])
+    for k, v in G.sub(d, "grad_").items():
+        if k == "x":
+            continue
+        _check(k, gr[k], v)
+
+
+def _feats(d):
+    return [d[f"feat{i}"].astype(np.float64) for i in range(len(d["meta"]["dims"]))]
+
+
+@pytest.mark.parametrize("name", G.names("model_"))
+def test_models(name):
+    d = G.load(name)
+    m = d["meta"]
+    g = _graph(d)
+    P = G.sub(d, "p_")
+    gout = d["gout"].astype(np.float64)
+    if m["model"] == "REGCN":
+        logits, emb, grads = O.regcn_model(g, _feats(d), d["g_rel"], P, m["num_layers"],
+                                           m["alpha"], gout)
+    elif m["model"] == "REGAT":
+        logits, emb, grads = O.regat_model(g, _feats(d), d["g_rel"], P, m["num_layers"],
+                                           m["heads"], m["hidden"], m["alpha"], gout)
+    else:
+        logits, emb, grads = O.remixhop_model(g, _feats(d), d["g_rel"], P, m["num_layers"],
+                                              m["hidden"], m["alpha"], gout)
+    _check("logits", logits, d["logits"])
+    _check("emb", emb, d["emb"])
+    want = G.sub(d, "grad_")
+    assert set(want) == set(grads), set(want) ^ set(grads)
+    for k, v in want.items():
+        _check(k, grads[k], v)
