@@ -1,0 +1,173 @@
+/*
+ * regnn_hip.h — C-ABI of libregnn_hip.so, the MI355X (gfx950) kernels behind RE-GNN's
+ * relation-embedding message passing.
+ *
+ * The reference has no native code of its own: its hot path calls DGL 0.7.1's gspmm / gsddmm /
+ * edge_softmax (full-batch layers) and torch_scatter / torch_sparse (ogbn-mag path) through their
+ * Python APIs. Each entry point below names the reference call sites whose arithmetic it replaces.
+ *
+ * Conventions (all entry points)
+ *  - Plain pointers + sizes; no framework types. Every buffer is device memory owned by the
+ *    caller (PyTorch's caching allocator on the Python side); the library never allocates.
+ *  - Work is enqueued on `stream` and is asynchronous; no host synchronisation, graph-capturable.
+ *  - Return 0 on success, a REGNN_E* code otherwise (invalid argument / unsupported shape /
+ *    launch failure). The Python wrapper raises RuntimeError on any non-zero return.
+ *  - Graphs are compressed segments: CSR (segment = destination, idx = source) for forward
+ *    aggregation, CSC (segment = source, idx = destination) for the transposed backward.
+ *    `rel` holds 0-based relation ids (reference e_feat - 1, layer/REGraphConv.py:61) as uint8.
+ *  - Feature rows are dense row-major [n, F]; dtype REGNN_F32 or REGNN_BF16 (storage type;
+ *    accumulation is always fp32).
+ *  - Segments with more than `split` edges are processed by the long-segment plan
+ *    (long_ids/chunk_long/chunk_off, see regnn_spmm_fwd) so hubs do not serialise one wave;
+ *    split == 0 disables splitting. Results are bitwise reproducible run to run: no float
+ *    atomics anywhere; cross-block reductions go through fixed-order slabs.
+ */
+#ifndef REGNN_HIP_H
+#define REGNN_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
+enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
+
+/* ABI version (bumped on any signature change). */
+int regnn_abi_version(void);
+
+/* Rows of the per-block relation-gradient slab that regnn_spmm_bwd / regnn_degree_bwd write
+ * (one row of n_rel (x heads) floats per block); size the slab as rows * n_rel * heads floats. */
+int64_t regnn_slab_rows(int64_t n_seg, int32_t n_chunk);
+
+/* Long-segment relation counts: segments with more than `split` in-edges (long_ids[n_long]) are
+ * not walked edge by edge in the degree kernels; long_cnt[l*n_rel + r] holds how many in-edges
+ * of segment long_ids[l] carry relation r (a static property of the graph, built once).
+ *
+ * Weighted in-degree and its power norm.
+ * Replaces: graph.update_all(fn.u_mul_e('nones','ew','m'), fn.sum('m','norm')) followed by
+ *   th.pow(norm.clamp(min=1), power)   — layer/REGraphConv.py:66-75 (power -0.5),
+ *   layer/REMixHopConv.py:58-64 (-0.5), layer/RESAGEConv.py:72-81 and REGINConv.py:162-166 (-1.0).
+ * deg[v] = sum_{e in seg v} rel_table[rel[e]];  norm[v] = max(deg[v], 1)^power.
+ * rel_table == NULL means weight 1 (unweighted in-count). */
+int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table, int64_t n_seg,
+                 float power, int32_t split, const int32_t* long_ids, int32_t n_long,
+                 const int32_t* long_cnt, int32_t n_rel, float* deg, float* norm,
+                 hipStream_t stream);
+
+/* Backward of regnn_degree w.r.t. rel_table: slab[b][r] = partial over block b of
+ *   sum_v g_norm[v] * power * max(deg,1)^(power-1) * [deg >= 1] * |{e in seg v : rel[e] = r}|.
+ * Reduce the slab with regnn_rel_reduce. Requires n_rel <= 64. */
+int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, const float* g_norm,
+                     int64_t n_seg, float power, int32_t n_rel, int32_t split,
+                     const int32_t* long_ids, int32_t n_long, const int32_t* long_cnt,
+                     float* slab, hipStream_t stream);
+
+/* Relation-embedding SpMM, forward direction.
+ * Replaces DGL gspmm for graph.update_all(fn.u_mul_e('h','ew','m'), fn.sum('m','h'))
+ *   (layer/REGraphConv.py:84-86, 91-93; with rel_table == NULL it is fn.copy_u,
+ *   layer/REMixHopConv.py:80) and torch_scatter mean aggregation of PyG propagate
+ *   (mag/regnn_layers.py:129,142-148, with out_scale = 1/in-count, bias = conv bias):
+ *   y[i] = out_scale[i] * sum_{e in seg i} w(e) * in_scale[idx[e]] * x[idx[e]] + bias
+ *   w(e) = (rel_table ? rel_table[rel[e]] : 1) * (edge_w ? edge_w[e] : 1)
+ * Any of rel_table / edge_w / in_scale / out_scale / bias may be NULL.
+ * Long-segment plan (all NULL / 0 when split == 0): long_ids[n_long] = segments with more than
+ * `split` edges; chunk c covers edges [ptr[s] + k*chunk, ...) of s = long_ids[chunk_long[c]],
+ * k = c - chunk_off[chunk_long[c]]; chunk_partial is fp32 scratch [n_chunk, F]. */
+int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w,
+                   const float* in_scale, const float* out_scale, const float* bias,
+                   const void* x, void* y, int64_t n_seg, int32_t F, int32_t dtype,
+                   int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                   const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                   float* chunk_partial, hipStream_t stream);
+
+/* Relation-embedding SpMM, fused backward over the transposed graph (CSC: segment = source u).
+ * Replaces DGL GSpMM.backward (gspmm on the reverse graph + gsddmm 'dot' for the edge weight)
+ * behind the same call sites as regnn_spmm_fwd, and the PyG/torch_scatter backward.
+ *   gx[u]  = out_scale[u] * sum_{e: u->v} w(e) * in_scale[v] * g[v]          (transposed SpMM)
+ *   slab   : per relation r, sum over edges with rel r of in_scale[v]*out_scale[u]*<g[v], x[u]>
+ *            (d loss / d rel_table[r], SDDMM 'dot' fused; only when slab != NULL)
+ *   edge_grad[e] (optional, this traversal's edge order): the same per-edge quantity
+ *   node_grad[u] (optional) = <x[u], raw[u]> + (y ? <g[u], y[u]> / in_scale[u] : 0)
+ *            with raw[u] = the sum above before out_scale: d loss / d norm[u] when
+ *            in_scale == out_scale == norm (layer/REGraphConv.py:73-76,97-98).
+ * x / y are the forward input / output rows (dtype as g). */
+int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w,
+                   const float* in_scale, const float* out_scale,
+                   const void* g, const void* x, const void* y, void* gx,
+                   float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                   int64_t n_seg, int32_t F, int32_t dtype,
+                   int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                   const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                   float* chunk_partial, hipStream_t stream);
+
+/* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order. */
+int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
+                     int32_t accumulate, hipStream_t stream);
+
+/* GAT attention, forward. Replaces apply_edges(fn.u_add_v('el','er','e')) + ee add +
+ * LeakyReLU + dgl edge_softmax (layer/REGATConv.py:80-88):
+ *   s(e,h) = el[idx[e],h] + er[v,h] + (ee_table ? ee_table[rel[e]*H + h] : 0)
+ *   z = leaky_relu(s, slope);  a(e,h) = exp(z - max_v z) / sum_v exp(z - max_v z)
+ * over the in-edges of each destination v (CSR). a is written in CSR edge order [nnz, H]. */
+int regnn_gat_softmax_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                          const float* ee_table, const float* el, const float* er,
+                          int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream);
+
+/* GAT attention, backward (edge_softmax VJP + LeakyReLU + u_add_v), per destination v (CSR):
+ *   gz = a * (ga - sum_v a*ga);  gs = gz * (s > 0 ? 1 : slope)
+ *   gs_out[e,h] = gs (CSR order); ger[v,h] = sum_v gs;  slab: per (rel, h) sums of gs
+ * (d loss / d ee_table) when slab != NULL (requires n_rel*H <= 256). */
+int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                          const float* ee_table, const float* el, const float* er,
+                          const float* a, const float* ga, int64_t n_seg, int32_t H, float slope,
+                          float* gs_out, float* ger, float* slab, int32_t n_rel,
+                          hipStream_t stream);
+
+/* Per-head weighted SpMM (GAT message passing, layer/REGATConv.py:90-91,
+ * update_all(fn.u_mul_e('ft','a','m'), fn.sum('m','ft'))):
+ *   y[v,h,:] = sum_{e in seg v} a[eid(e)*H + h] * x[idx[e],h,:],  eid(e) = perm ? perm[e] : e.
+ * Rows are H*D wide, D % 4 == 0 (fp32). */
+int regnn_spmm_heads_fwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
+                         const float* a, const void* x, void* y, int64_t n_seg, int32_t H,
+                         int32_t D, int32_t dtype, hipStream_t stream);
+
+/* Fused backward of regnn_spmm_heads_fwd over the CSC (segment = source u, perm = CSC->CSR edge):
+ *   gx[u,h,:] = sum_{e: u->v} a[perm[e],h] * g[v,h,:];   ga[perm[e],h] = <g[v,h,:], x[u,h,:]> */
+int regnn_spmm_heads_bwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
+                         const float* a, const void* g, const void* x, void* gx, float* ga,
+                         int64_t n_seg, int32_t H, int32_t D, int32_t dtype, hipStream_t stream);
+
+/* out[s,h] = sum_{e in seg s} vals[(perm ? perm[e] : e)*H + h]  (segment sum of edge values,
+ * e.g. d loss / d el over the CSC). */
+int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals, int64_t n_seg,
+                      int32_t H, float* out, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Neighbour sampler (replaces torch_sparse SparseTensor.sample_adj behind PyG NeighborSampler,
+ * mag/regnn_ns.py:206-214). Spec (this build's, documented in DESIGN.md; torch_sparse's RNG is
+ * not reproducible): for target t with in-degree d and fan-out k (k < 0: all):
+ *   d <= k or k < 0  -> all in-edges in CSR order;
+ *   else Floyd sampling of k distinct positions in [0,d) drawing
+ *        r_j = regnn_hash(seed, t_global, j) for j = d-k .. d-1, pos = (r_j * (j+1)) >> 32,
+ *   output in ascending position order.
+ * --------------------------------------------------------------------------------------- */
+
+/* counts[i] = min(deg(targets[i]), k) (or deg when k < 0). */
+int regnn_sample_count(const int32_t* ptr, const int32_t* targets, int64_t n_targets, int32_t k,
+                       int32_t* counts, hipStream_t stream);
+
+/* Fill sampled neighbours: out_src[offs[i] + q] = global source id, out_eid[...] = CSR edge id.
+ * offs = exclusive prefix sum of counts (n_targets + 1 entries). Requires k <= 64. */
+int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* targets,
+                      int64_t n_targets, int32_t k, uint64_t seed, const int32_t* offs,
+                      int32_t* out_src, int32_t* out_eid, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REGNN_HIP_H */

@@ -60,11 +60,12 @@ class Graph:
         self.n_dst = int(num_nodes if num_dst is None else num_dst)
         self.E = self.src.size
 
-    def adj(self, w=None, dtype=np.float64):
+    def adj(self, w=None, dtype=None):
         """A[v, u] = sum of w over edges u->v (duplicates summed, = DGL gspmm u_mul_e + sum)."""
         if w is None:
-            w = np.ones(self.E, dtype=dtype)
-        return sp.csr_matrix((np.asarray(w, dtype=dtype), (self.dst, self.src)),
+            w = np.ones(self.E, dtype=dtype or np.float64)
+        w = np.asarray(w, dtype=dtype) if dtype else np.asarray(w)
+        return sp.csr_matrix((w, (self.dst, self.src)),
                              shape=(self.n_dst, self.n_src))
 
     def in_sum(self, w):

@@ -1,0 +1,538 @@
+// Relation-embedding SpMM for gfx950: forward aggregation, fused transposed backward
+// (SpMM + SDDMM 'dot' + relation-bin and node-norm gradients), weighted degree / norm and its
+// backward, long-segment split path and deterministic slab reduction.
+//
+// Mapping (wave64): a segment (CSR row / CSC column) is owned by a group of LPR lanes; each lane
+// holds NV 16-byte vectors of the F-wide feature row, so one group gathers a whole neighbour row
+// per step (F=64 fp32: 16 lanes x 16 B = 256 B, four rows per wave-instruction). Neighbour ids,
+// relation weights and scales are loaded coalesced, one edge per lane, and broadcast inside the
+// group with width-LPR shuffles; UN rows are issued before any is consumed so each lane keeps
+// UN*NV 16-byte loads in flight. Relation gradients go to lane-private LDS bins
+// [n_rel][256 threads] (no cross-lane traffic per edge, no atomics) and leave the block through a
+// fixed-order slab: bitwise reproducible.
+#include "regnn_common.h"
+
+namespace regnn {
+
+struct SpmmArgs {
+    const int32_t* ptr;
+    const int32_t* idx;
+    const uint8_t* rel;
+    const float* tab;
+    const float* edge_w;
+    const float* in_scale;
+    const float* out_scale;
+    const float* bias;
+    const void* src;       // gathered rows (x in forward, g in backward)
+    void* out;             // y in forward, gx in backward
+    const void* self;      // backward: forward input x of the segment's own node
+    const void* ng_a;      // backward node grad: g rows
+    const void* ng_b;      // backward node grad: y rows
+    float* slab;
+    int32_t n_rel;
+    float* edge_grad;
+    float* node_grad;
+    int64_t n_seg;
+    int32_t F;
+    int32_t split;
+    int32_t chunk;
+    const int32_t* long_ids;
+    int32_t n_long;
+    const int32_t* chunk_long;
+    const int32_t* chunk_off;
+    int32_t n_chunk;
+    float* chunk_partial;
+    int32_t slab_row0;     // first slab row this launch writes
+};
+
+template <typename T, int LPR, int NV>
+struct Seg {
+    static constexpr int EV = Vec<T>::N;
+    static constexpr int UN = NV >= 8 ? 1 : (8 / NV);
+
+    __device__ __forceinline__ static int off(int q, int lane) { return (q * LPR + lane) * EV; }
+
+    __device__ __forceinline__ static void load_row(const T* row, int F, int lane,
+                                                    float (&v)[NV][EV]) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = off(q, lane);
+            if (o < F) {
+                Vec<T>::load(row + o, v[q]);
+            } else {
+#pragma unroll
+                for (int t = 0; t < EV; ++t) v[q][t] = 0.f;
+            }
+        }
+    }
+
+    __device__ __forceinline__ static float dot(const float (&a)[NV][EV], const float (&b)[NV][EV]) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+            for (int t = 0; t < EV; ++t) s = fmaf(a[q][t], b[q][t], s);
+        return s;
+    }
+
+    // Accumulate edges [beg, end) of one segment into acc. BWD additionally forms the per-edge
+    // SDDMM dot <src[j], self> * in_scale[j] * os into the relation bins / edge_grad.
+    template <bool BWD>
+    __device__ __forceinline__ static void accumulate(const SpmmArgs& a, int beg, int end, int lane,
+                                                      float os, const float (&sx)[NV][EV],
+                                                      float (&acc)[NV][EV], float* bins, int tid) {
+        const T* __restrict__ src = static_cast<const T*>(a.src);
+        const int F = a.F;
+        for (int e0 = beg; e0 < end; e0 += LPR) {
+            const int e = e0 + lane;
+            int j = 0, r = 0;
+            float w = 0.f, sj = 1.f;
+            if (e < end) {
+                j = a.idx[e];
+                float ww = 1.f;
+                if (a.rel) r = a.rel[e];
+                if (a.tab) ww = a.tab[r];
+                if (a.edge_w) ww *= a.edge_w[e];
+                if (a.in_scale) sj = a.in_scale[j];
+                w = ww * sj;
+            }
+            const int cnt = min(LPR, end - e0);
+            int k = 0;
+            for (; k + UN <= cnt; k += UN) {
+                int jj[UN];
+                float wk[UN];
+                float v[UN][NV][EV];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    jj[u] = __shfl(j, k + u, LPR);
+                    wk[u] = __shfl(w, k + u, LPR);
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) load_row(src + (int64_t)jj[u] * F, F, lane, v[u]);
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+#pragma unroll
+                    for (int q = 0; q < NV; ++q)
+#pragma unroll
+                        for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk[u], v[u][q][t], acc[q][t]);
+                    if constexpr (BWD) edge_dot(a, e0 + k + u, k + u, v[u], sx, sj, r, os, bins, tid, lane);
+                }
+            }
+            for (; k < cnt; ++k) {
+                const int jj = __shfl(j, k, LPR);
+                const float wk = __shfl(w, k, LPR);
+                float v[NV][EV];
+                load_row(src + (int64_t)jj * F, F, lane, v);
+#pragma unroll
+                for (int q = 0; q < NV; ++q)
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk, v[q][t], acc[q][t]);
+                if constexpr (BWD) edge_dot(a, e0 + k, k, v, sx, sj, r, os, bins, tid, lane);
+            }
+        }
+    }
+
+    __device__ __forceinline__ static void edge_dot(const SpmmArgs& a, int e, int k,
+                                                    const float (&v)[NV][EV],
+                                                    const float (&sx)[NV][EV], float sj, int r,
+                                                    float os, float* bins, int tid, int lane) {
+        if (!(a.slab || a.edge_grad)) return;
+        const float scale = __shfl(sj, k, LPR) * os;
+        const float p = dot(v, sx) * scale;
+        if (a.slab) {
+            const int rk = __shfl(r, k, LPR);
+            bins[rk * kBlock + tid] += p;
+        }
+        if (a.edge_grad) {
+            const float s = group_sum<LPR>(p);
+            if (lane == 0) a.edge_grad[e] = s;
+        }
+    }
+
+    // y = os * acc + bias; backward node grad = <self, acc> + <g_i, y_i> / in_scale[i].
+    template <bool BWD>
+    __device__ __forceinline__ static void epilogue(const SpmmArgs& a, int64_t seg, int lane,
+                                                    float os, const float (&sx)[NV][EV],
+                                                    float (&acc)[NV][EV]) {
+        const int F = a.F;
+        if constexpr (BWD) {
+            if (a.node_grad) {
+                float ng = dot(sx, acc);
+                if (a.ng_a && a.ng_b) {
+                    float ga[NV][EV], yb[NV][EV];
+                    load_row(static_cast<const T*>(a.ng_a) + seg * F, F, lane, ga);
+                    load_row(static_cast<const T*>(a.ng_b) + seg * F, F, lane, yb);
+                    const float is = a.in_scale ? a.in_scale[seg] : 1.f;
+                    ng += dot(ga, yb) / is;
+                }
+                ng = group_sum<LPR>(ng);
+                if (lane == 0) a.node_grad[seg] = ng;
+            }
+        }
+        T* __restrict__ out = static_cast<T*>(a.out) + seg * F;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = off(q, lane);
+            if (o < F) {
+                float r[EV];
+#pragma unroll
+                for (int t = 0; t < EV; ++t) {
+                    r[t] = acc[q][t] * os;
+                    if (!BWD && a.bias) r[t] += a.bias[o + t];
+                }
+                Vec<T>::store(out + o, r);
+            }
+        }
+    }
+};
+
+__device__ __forceinline__ void bins_zero(float* bins, int n_rel, int tid) {
+    for (int r = 0; r < n_rel; ++r) bins[r * kBlock + tid] = 0.f;
+}
+
+// fixed-order block reduction of the lane-private bins into slab row `row`
+__device__ __forceinline__ void bins_flush(float* bins, int n_rel, int tid, float* slab, int row) {
+    __syncthreads();
+    for (int r = tid; r < n_rel; r += kBlock) {
+        float s = 0.f;
+        for (int t = 0; t < kBlock; ++t) s += bins[r * kBlock + t];
+        slab[(int64_t)row * n_rel + r] = s;
+    }
+}
+
+template <typename T, int LPR, int NV, bool BWD>
+__global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
+    extern __shared__ float bins[];
+    using S = Seg<T, LPR, NV>;
+    constexpr int GPB = kBlock / LPR;
+    const int tid = threadIdx.x, lane = tid & (LPR - 1);
+    const bool use_bins = BWD && a.slab;
+    if (use_bins) bins_zero(bins, a.n_rel, tid);
+    const bool need_self = BWD && (a.slab || a.edge_grad || a.node_grad);
+    for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < a.n_seg;
+         seg += (int64_t)gridDim.x * GPB) {
+        const int beg = a.ptr[seg], end = a.ptr[seg + 1];
+        if (a.split > 0 && end - beg > a.split) continue;   // long-segment path
+        float acc[NV][S::EV] = {};
+        float sx[NV][S::EV] = {};
+        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        const float os = a.out_scale ? a.out_scale[seg] : 1.f;
+        S::template accumulate<BWD>(a, beg, end, lane, os, sx, acc, bins, tid);
+        S::template epilogue<BWD>(a, seg, lane, os, sx, acc);
+    }
+    if (use_bins) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
+}
+
+// one group per chunk of a long segment: raw partial sums (fp32) -> chunk_partial
+template <typename T, int LPR, int NV, bool BWD>
+__global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
+    extern __shared__ float bins[];
+    using S = Seg<T, LPR, NV>;
+    constexpr int GPB = kBlock / LPR;
+    const int tid = threadIdx.x, lane = tid & (LPR - 1);
+    const bool use_bins = BWD && a.slab;
+    if (use_bins) bins_zero(bins, a.n_rel, tid);
+    const bool need_self = BWD && (a.slab || a.edge_grad || a.node_grad);
+    for (int64_t c = (int64_t)blockIdx.x * GPB + tid / LPR; c < a.n_chunk;
+         c += (int64_t)gridDim.x * GPB) {
+        const int l = a.chunk_long[c];
+        const int64_t seg = a.long_ids[l];
+        const int k = int(c) - a.chunk_off[l];
+        const int s0 = a.ptr[seg], s1 = a.ptr[seg + 1];
+        const int beg = s0 + k * a.chunk;
+        const int end = min(s1, beg + a.chunk);
+        float acc[NV][S::EV] = {};
+        float sx[NV][S::EV] = {};
+        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        const float os = a.out_scale ? a.out_scale[seg] : 1.f;
+        S::template accumulate<BWD>(a, beg, end, lane, os, sx, acc, bins, tid);
+        float* part = a.chunk_partial + c * a.F;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = S::off(q, lane);
+            if (o < a.F) {
+#pragma unroll
+                for (int t = 0; t < S::EV; ++t) part[o + t] = acc[q][t];
+            }
+        }
+    }
+    if (use_bins) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
+}
+
+// one group per long segment: fixed-order sum of its chunk partials, then the epilogue
+template <typename T, int LPR, int NV, bool BWD>
+__global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a) {
+    using S = Seg<T, LPR, NV>;
+    constexpr int GPB = kBlock / LPR;
+    const int tid = threadIdx.x, lane = tid & (LPR - 1);
+    const bool need_self = BWD && a.node_grad;
+    for (int64_t l = (int64_t)blockIdx.x * GPB + tid / LPR; l < a.n_long;
+         l += (int64_t)gridDim.x * GPB) {
+        const int64_t seg = a.long_ids[l];
+        float acc[NV][S::EV] = {};
+        float sx[NV][S::EV] = {};
+        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        for (int c = a.chunk_off[l]; c < a.chunk_off[l + 1]; ++c) {
+            const float* part = a.chunk_partial + (int64_t)c * a.F;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int o = S::off(q, lane);
+                if (o < a.F) {
+#pragma unroll
+                    for (int t = 0; t < S::EV; ++t) acc[q][t] += part[o + t];
+                }
+            }
+        }
+        const float os = a.out_scale ? a.out_scale[seg] : 1.f;
+        S::template epilogue<BWD>(a, seg, lane, os, sx, acc);
+    }
+}
+
+template <typename T, int LPR, int NV, bool BWD>
+int launch_spmm(SpmmArgs a, hipStream_t stream) {
+    constexpr int GPB = kBlock / LPR;
+    const size_t lds = (BWD && a.slab) ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
+    const int g1 = grid_for(a.n_seg, GPB);
+    a.slab_row0 = 0;
+    hipLaunchKernelGGL((spmm_main<T, LPR, NV, BWD>), dim3(g1), dim3(kBlock), lds, stream, a);
+    REGNN_LAUNCH_CHECK();
+    if (a.split > 0 && a.n_chunk > 0) {
+        a.slab_row0 = kMaxGrid;
+        const int g2 = grid_for(a.n_chunk, GPB);
+        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, BWD>), dim3(g2), dim3(kBlock), lds, stream, a);
+        REGNN_LAUNCH_CHECK();
+        const int g3 = grid_for(a.n_long, GPB);
+        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, BWD>), dim3(g3), dim3(kBlock), 0, stream, a);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
+// (lanes per segment, vectors per lane) for a row of nvec 16-byte vectors
+template <typename T, bool BWD>
+int dispatch(SpmmArgs a, hipStream_t stream) {
+    constexpr int EV = Vec<T>::N;
+    if (a.F <= 0 || a.F % EV) return REGNN_EUNSUPPORTED;
+    const int nvec = a.F / EV;
+    if (nvec <= 4) return launch_spmm<T, 4, 1, BWD>(a, stream);
+    if (nvec <= 8) return launch_spmm<T, 8, 1, BWD>(a, stream);
+    if (nvec <= 16) return launch_spmm<T, 16, 1, BWD>(a, stream);
+    if (nvec <= 32) return launch_spmm<T, 16, 2, BWD>(a, stream);
+    if (nvec <= 48) return launch_spmm<T, 16, 3, BWD>(a, stream);
+    if (nvec <= 64) return launch_spmm<T, 16, 4, BWD>(a, stream);
+    if (nvec <= 128) return launch_spmm<T, 64, 2, BWD>(a, stream);
+    if (nvec <= 256) return launch_spmm<T, 64, 4, BWD>(a, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+// ---------------------------------------------------------------------------------------------
+// degree / norm
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock)
+degree_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ rel,
+              const float* __restrict__ tab, int64_t n_seg, float power, int32_t split,
+              float* __restrict__ deg, float* __restrict__ norm) {
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n_seg;
+         v += (int64_t)gridDim.x * kBlock) {
+        const int b = ptr[v], e = ptr[v + 1];
+        if (split > 0 && e - b > split) continue;
+        float d;
+        if (tab) {
+            d = 0.f;
+            for (int k = b; k < e; ++k) d += tab[rel[k]];
+        } else {
+            d = float(e - b);
+        }
+        deg[v] = d;
+        if (norm) norm[v] = powf(fmaxf(d, 1.f), power);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+degree_long_kernel(const int32_t* __restrict__ ptr, const float* __restrict__ tab,
+                   const int32_t* __restrict__ long_ids, int32_t n_long,
+                   const int32_t* __restrict__ long_cnt, int32_t n_rel, float power,
+                   float* __restrict__ deg, float* __restrict__ norm) {
+    for (int l = blockIdx.x * kBlock + threadIdx.x; l < n_long; l += gridDim.x * kBlock) {
+        const int64_t v = long_ids[l];
+        float d;
+        if (tab) {
+            d = 0.f;
+            for (int r = 0; r < n_rel; ++r) d += tab[r] * float(long_cnt[(int64_t)l * n_rel + r]);
+        } else {
+            d = float(ptr[v + 1] - ptr[v]);
+        }
+        deg[v] = d;
+        if (norm) norm[v] = powf(fmaxf(d, 1.f), power);
+    }
+}
+
+__device__ __forceinline__ float dnorm_ddeg(float d, float g, float power) {
+    // d/d deg of max(deg,1)^power with torch clamp semantics (gradient passes where deg >= 1)
+    return d >= 1.f ? g * power * powf(d, power - 1.f) : 0.f;
+}
+
+__global__ void __launch_bounds__(kBlock)
+degree_bwd_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ rel,
+                  const float* __restrict__ deg, const float* __restrict__ g_norm, int64_t n_seg,
+                  float power, int32_t n_rel, int32_t split, const int32_t* __restrict__ long_ids,
+                  int32_t n_long, const int32_t* __restrict__ long_cnt, float* __restrict__ slab) {
+    extern __shared__ float bins[];
+    const int tid = threadIdx.x;
+    bins_zero(bins, n_rel, tid);
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + tid; v < n_seg;
+         v += (int64_t)gridDim.x * kBlock) {
+        const int b = ptr[v], e = ptr[v + 1];
+        if (split > 0 && e - b > split) continue;
+        const float gd = dnorm_ddeg(deg[v], g_norm[v], power);
+        for (int k = b; k < e; ++k) bins[rel[k] * kBlock + tid] += gd;
+    }
+    for (int l = blockIdx.x * kBlock + tid; l < n_long; l += gridDim.x * kBlock) {
+        const int64_t v = long_ids[l];
+        const float gd = dnorm_ddeg(deg[v], g_norm[v], power);
+        for (int r = 0; r < n_rel; ++r)
+            bins[r * kBlock + tid] += gd * float(long_cnt[(int64_t)l * n_rel + r]);
+    }
+    bins_flush(bins, n_rel, tid, slab, blockIdx.x);
+}
+
+// one wave per output column k: fixed-order sum over slab rows
+__global__ void __launch_bounds__(64)
+rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
+                  float* __restrict__ out, int32_t accumulate) {
+    const int k = blockIdx.x, lane = threadIdx.x;
+    float s = 0.f;
+    for (int64_t r = lane; r < n_rows; r += 64) s += slab[r * width + k];
+    s = group_sum<64>(s);
+    if (lane == 0) out[k] = accumulate ? out[k] + s : s;
+}
+
+}  // namespace regnn
+
+using namespace regnn;
+
+extern "C" {
+
+int regnn_abi_version(void) { return 1; }
+
+int64_t regnn_slab_rows(int64_t, int32_t) { return 2 * int64_t(kMaxGrid); }
+
+static SpmmArgs make_args(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                          const float* tab, const float* edge_w, const float* in_scale,
+                          const float* out_scale, int64_t n_seg, int32_t F, int32_t split,
+                          int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                          const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                          float* chunk_partial) {
+    SpmmArgs a{};
+    a.ptr = ptr; a.idx = idx; a.rel = rel; a.tab = tab; a.edge_w = edge_w;
+    a.in_scale = in_scale; a.out_scale = out_scale; a.n_seg = n_seg; a.F = F;
+    a.split = split; a.chunk = chunk; a.long_ids = long_ids; a.n_long = n_long;
+    a.chunk_long = chunk_long; a.chunk_off = chunk_off; a.n_chunk = n_chunk;
+    a.chunk_partial = chunk_partial;
+    return a;
+}
+
+static int check_common(const int32_t* ptr, const int32_t* idx, const void* src, const void* out,
+                        int64_t n_seg, int32_t split, int32_t chunk, const int32_t* long_ids,
+                        int32_t n_long, const int32_t* chunk_long, const int32_t* chunk_off,
+                        int32_t n_chunk, const float* chunk_partial, const uint8_t* rel,
+                        const float* tab) {
+    if (n_seg < 0 || !ptr || (n_seg > 0 && (!idx || !src || !out))) return REGNN_EINVAL;
+    if (tab && !rel) return REGNN_EINVAL;
+    if (split < 0) return REGNN_EINVAL;
+    if (split > 0 && n_long > 0 &&
+        (chunk <= 0 || !long_ids || !chunk_long || !chunk_off || !chunk_partial || n_chunk <= 0))
+        return REGNN_EINVAL;
+    return REGNN_OK;
+}
+
+int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w, const float* in_scale,
+                   const float* out_scale, const float* bias, const void* x, void* y,
+                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   hipStream_t stream) {
+    int st = check_common(ptr, idx, x, y, n_seg, split, chunk, long_ids, n_long, chunk_long,
+                          chunk_off, n_chunk, chunk_partial, rel, rel_table);
+    if (st) return st;
+    if (n_seg == 0) return REGNN_OK;
+    if (n_long == 0) { split = 0; n_chunk = 0; }
+    SpmmArgs a = make_args(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, n_seg, F, split,
+                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial);
+    a.bias = bias; a.src = x; a.out = y;
+    if (dtype == REGNN_F32) return dispatch<float, false>(a, stream);
+    if (dtype == REGNN_BF16) return dispatch<bf16_t, false>(a, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w, const float* in_scale,
+                   const float* out_scale, const void* g, const void* x, const void* y, void* gx,
+                   float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   hipStream_t stream) {
+    int st = check_common(ptr, idx, g, gx, n_seg, split, chunk, long_ids, n_long, chunk_long,
+                          chunk_off, n_chunk, chunk_partial, rel, rel_table);
+    if (st) return st;
+    if (slab && (!rel || n_rel <= 0 || n_rel > 64)) return REGNN_EINVAL;
+    if ((slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    if (n_long == 0) { split = 0; n_chunk = 0; }
+    SpmmArgs a = make_args(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, n_seg, F, split,
+                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial);
+    a.src = g; a.out = gx; a.self = x; a.ng_a = y ? g : nullptr; a.ng_b = y;
+    a.slab = slab; a.n_rel = n_rel; a.edge_grad = edge_grad; a.node_grad = node_grad;
+    if (dtype == REGNN_F32) return dispatch<float, true>(a, stream);
+    if (dtype == REGNN_BF16) return dispatch<bf16_t, true>(a, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table, int64_t n_seg,
+                 float power, int32_t split, const int32_t* long_ids, int32_t n_long,
+                 const int32_t* long_cnt, int32_t n_rel, float* deg, float* norm,
+                 hipStream_t stream) {
+    if (!ptr || !deg || n_seg < 0 || (rel_table && !rel)) return REGNN_EINVAL;
+    if (split > 0 && n_long > 0 && (!long_ids || (rel_table && !long_cnt))) return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    if (n_long == 0) split = 0;
+    hipLaunchKernelGGL(degree_kernel, dim3(grid_for(n_seg, kBlock)), dim3(kBlock), 0, stream, ptr,
+                       rel, rel_table, n_seg, power, split, deg, norm);
+    REGNN_LAUNCH_CHECK();
+    if (split > 0) {
+        hipLaunchKernelGGL(degree_long_kernel, dim3(grid_for(n_long, kBlock)), dim3(kBlock), 0,
+                           stream, ptr, rel_table, long_ids, n_long, long_cnt, n_rel, power, deg,
+                           norm);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
+int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, const float* g_norm,
+                     int64_t n_seg, float power, int32_t n_rel, int32_t split,
+                     const int32_t* long_ids, int32_t n_long, const int32_t* long_cnt,
+                     float* slab, hipStream_t stream) {
+    if (!ptr || !rel || !deg || !g_norm || !slab || n_rel <= 0 || n_rel > 64) return REGNN_EINVAL;
+    if (split > 0 && n_long > 0 && (!long_ids || !long_cnt)) return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    if (n_long == 0) split = 0;
+    const size_t lds = size_t(n_rel) * kBlock * sizeof(float);
+    hipLaunchKernelGGL(degree_bwd_kernel, dim3(grid_for(n_seg, kBlock)), dim3(kBlock), lds, stream,
+                       ptr, rel, deg, g_norm, n_seg, power, n_rel, split, long_ids,
+                       split > 0 ? n_long : 0, long_cnt, slab);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
+                     int32_t accumulate, hipStream_t stream) {
+    if (!slab || !out || width <= 0 || n_rows < 0) return REGNN_EINVAL;
+    hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(64), 0, stream, slab, n_rows, width,
+                       out, accumulate);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+}  // extern "C"

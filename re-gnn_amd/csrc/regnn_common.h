@@ -1,0 +1,75 @@
+// Shared device helpers for the gfx950 RE-GNN kernels (wave64, 16-byte row vectors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "../../include/regnn_hip.h"
+
+namespace regnn {
+
+constexpr int kBlock = 256;       // 4 waves of 64
+constexpr int kMaxGrid = 2048;    // grid-stride cap (8 blocks per CU); bounds the slab rows
+
+using bf16_t = uint16_t;          // storage type for REGNN_BF16 rows
+
+// fp32 <-> bf16 (round to nearest even via the gfx950 conversion instruction)
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    __hip_bfloat16 h = __float2bfloat16(f);
+    return *reinterpret_cast<uint16_t*>(&h);
+}
+
+// One 16-byte vector of a feature row, widened to fp32.
+template <typename T> struct Vec;
+
+template <> struct Vec<float> {
+    static constexpr int N = 4;
+    __device__ __forceinline__ static void load(const float* p, float (&v)[4]) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+    __device__ __forceinline__ static void store(float* p, const float (&v)[4]) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+
+template <> struct Vec<bf16_t> {
+    static constexpr int N = 8;
+    __device__ __forceinline__ static void load(const bf16_t* p, float (&v)[8]) {
+        const uint4 t = *reinterpret_cast<const uint4*>(p);
+        const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    }
+    __device__ __forceinline__ static void store(bf16_t* p, const float (&v)[8]) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+};
+
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+    return v;
+}
+
+inline int grid_for(int64_t units, int per_block) {
+    int64_t g = (units + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    return int(g < kMaxGrid ? g : kMaxGrid);
+}
+
+}  // namespace regnn
+
+#define REGNN_LAUNCH_CHECK()                                        \
+    do {                                                            \
+        if (hipGetLastError() != hipSuccess) return REGNN_ELAUNCH;  \
+    } while (0)

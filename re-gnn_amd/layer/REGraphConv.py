@@ -1,0 +1,63 @@
+"""REGraphConv on MI355X — drop-in for layer/REGraphConv.py:7-106 (same constructor, forward
+signature, parameters and state_dict keys). The weighted degree, the normalised relation-weighted
+SpMM and their backward run as HIP kernels (regnn_hip.ops); torch does the R-sized relation table
+and the optional dense projection (hipBLASLt)."""
+import torch as th
+from torch import nn
+from torch.nn import init
+
+from regnn_hip import ops
+
+from ._common import relgraph, relation_table
+
+
+class REGraphConv(nn.Module):
+    def __init__(self, num_etypes, scaling_factor, in_feats, out_feats, norm=True, bias=True,
+                 activation=None, weight=True, dropout=0.):
+        super().__init__()
+        self.in_feats = in_feats
+        self.out_feats = out_feats
+        self.norm = norm
+        self.dropout = dropout
+        self.edge_weight = nn.Parameter(th.Tensor(num_etypes, 1), requires_grad=True)
+        self.alpha = scaling_factor
+        if weight:
+            self.weight = nn.Parameter(th.Tensor(in_feats, out_feats))
+        else:
+            self.register_parameter('weight', None)
+        if bias:
+            self.bias = nn.Parameter(th.Tensor(out_feats))
+        else:
+            self.register_parameter('bias', None)
+        self.reset_parameters()
+        self.feat_dropout = nn.Dropout(p=self.dropout)
+        self.activation = activation
+
+    def reset_parameters(self):
+        if self.weight is not None:
+            init.xavier_uniform_(self.weight)
+        if self.bias is not None:
+            init.zeros_(self.bias)
+        init.constant_(self.edge_weight, 1.0 / self.alpha)
+
+    def forward(self, graph, feat, e_feat, return_embedding=False):
+        rg = relgraph(graph, feat.device)
+        pack = rg.rel_pack(e_feat, num_rel=self.edge_weight.shape[0])
+        feat = self.feat_dropout(feat)                                   # :56
+        tab = relation_table(self.edge_weight, self.alpha)               # :58-61 (folded: no E-sized ew)
+        norm = ops.degree_norm(rg, pack, tab) if self.norm else None     # :66-75
+        if self.in_feats > self.out_feats:                               # :78
+            if self.weight is not None:
+                feat = th.matmul(feat, self.weight)                      # :81
+            rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm,  # :76,84-86,97-101
+                              bias=self.bias)
+        elif self.weight is None:
+            rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm, bias=self.bias)
+        else:
+            # diag(norm) (A X) W == (diag(norm) A X) W: post-scale fused into the SpMM epilogue
+            rst = th.matmul(ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm), self.weight)
+            if self.bias is not None:
+                rst = rst + self.bias
+        if self.activation is not None:
+            rst = self.activation(rst)                                   # :103-104
+        return rst

@@ -1,0 +1,91 @@
+"""ctypes binding of libregnn_hip.so (C-ABI declared in include/regnn_hip.h).
+
+There is no CPU fallback: if the library is missing this module raises at import, and every
+wrapper refuses non-ROCm tensors. Pointers are passed as integers from ``Tensor.data_ptr()``;
+the stream is torch's current HIP stream, so kernels order with surrounding torch work.
+"""
+import ctypes
+import os
+
+import torch
+
+from .build import LIB
+
+if not os.path.exists(LIB):
+    raise ImportError(
+        f"regnn_hip: native library {LIB} is missing — build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+        "There is no CPU fallback.")
+
+_so = ctypes.CDLL(LIB)
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F32 = ctypes.c_float
+
+_SIG = {
+    "regnn_abi_version": ([], ctypes.c_int),
+    "regnn_slab_rows": ([I64, I32], I64),
+    "regnn_degree": ([P, P, P, I64, F32, I32, P, I32, P, I32, P, P, P], ctypes.c_int),
+    "regnn_degree_bwd": ([P, P, P, P, I64, F32, I32, I32, P, I32, P, P, P], ctypes.c_int),
+    "regnn_spmm_fwd": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P, P, I32,
+                        P, P], ctypes.c_int),
+    "regnn_spmm_bwd": ([P, P, P, P, P, P, P, P, P, P, P, P, I32, P, P, I64, I32, I32, I32, I32, P,
+                        I32, P, P, I32, P, P], ctypes.c_int),
+    "regnn_rel_reduce": ([P, I64, I32, P, I32, P], ctypes.c_int),
+    "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
+    "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P],
+                              ctypes.c_int),
+    "regnn_spmm_heads_fwd": ([P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
+    "regnn_spmm_heads_bwd": ([P, P, P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
+    "regnn_segment_sum": ([P, P, P, I64, I32, P, P], ctypes.c_int),
+    "regnn_sample_count": ([P, P, I64, I32, P, P], ctypes.c_int),
+    "regnn_sample_fill": ([P, P, P, I64, I32, U64, P, P, P, P], ctypes.c_int),
+}
+
+for _name, (_args, _ret) in _SIG.items():
+    _f = getattr(_so, _name)
+    _f.argtypes = _args
+    _f.restype = _ret
+
+EXPORTED = tuple(_SIG)
+ABI_VERSION = 1
+if _so.regnn_abi_version() != ABI_VERSION:
+    raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
+                      "rebuild the library")
+
+F32_CODE, BF16_CODE = 0, 1
+_ERR = {1: "invalid argument", 2: "unsupported shape/dtype", 3: "kernel launch failed"}
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32_CODE
+    if t.dtype == torch.bfloat16:
+        return BF16_CODE
+    raise TypeError(f"regnn_hip: unsupported feature dtype {t.dtype} (float32 / bfloat16)")
+
+
+def ptr(t):
+    """device pointer of a tensor (None -> NULL); refuses CPU tensors: no CPU fallback."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("regnn_hip kernels need ROCm device tensors (there is no CPU path)")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name, *args):
+    rc = getattr(_so, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"regnn_hip.{name} failed: {_ERR.get(rc, rc)}")
+
+
+def slab_rows():
+    return int(_so.regnn_slab_rows(0, 0))

@@ -1,0 +1,136 @@
+"""Device-resident multi-relation graph layout for the HIP kernels.
+
+HBM layout (built once per graph per device, int32 indices, uint8 relation ids):
+  CSR by destination   csr_ptr [N+1], csr_idx [E] (source ids), csr_eid [E] (original edge id)
+  CSC by source        csc_ptr [N+1], csc_idx [E] (destination ids), csc_eid [E], csc2csr [E]
+  relation ids         per e_feat tensor: rel_csr / rel_csc uint8 [E] (0-based = e_feat - 1)
+  long-segment plans   segments with > split edges are cut into `chunk`-edge pieces
+                       (hub rows of power-law graphs would otherwise serialise one wave)
+
+Edge ids are the caller's (DGL) edge order; within a CSR row edges stay in edge-id order
+(stable sort), which is the summation order of DGL's own CSR gspmm.
+"""
+import torch
+
+SPLIT = 256      # segments with more edges than this go through the chunked path
+CHUNK = 256      # edges per chunk
+
+
+class SegPlan:
+    """Long-segment split plan for one orientation (see regnn_spmm_fwd in regnn_hip.h)."""
+
+    def __init__(self, ptr, split=SPLIT, chunk=CHUNK):
+        deg = (ptr[1:] - ptr[:-1]).to(torch.int64)
+        long_ids = torch.nonzero(deg > split).flatten()
+        self.split, self.chunk = split, chunk
+        self.n_long = int(long_ids.numel())
+        if self.n_long == 0:
+            self.split = 0
+            self.long_ids = self.chunk_long = self.chunk_off = None
+            self.n_chunk = 0
+            return
+        nch = (deg[long_ids] + chunk - 1) // chunk
+        self.long_ids = long_ids.to(torch.int32)
+        self.chunk_off = torch.cat([nch.new_zeros(1), torch.cumsum(nch, 0)]).to(torch.int32)
+        self.chunk_long = torch.repeat_interleave(
+            torch.arange(self.n_long, device=ptr.device, dtype=torch.int32), nch)
+        self.n_chunk = int(self.chunk_off[-1].item())
+
+    def partial(self, F, device):
+        if self.n_chunk == 0:
+            return None
+        return torch.empty(self.n_chunk, F, dtype=torch.float32, device=device)
+
+
+class RelPack:
+    """Relation ids of one e_feat tensor laid out for both orientations (+ long-row counts)."""
+
+    def __init__(self, rg, e_feat, num_rel=None):
+        e = e_feat.to(rg.device).reshape(-1).to(torch.int64)
+        if e.numel() != rg.E:
+            raise ValueError(f"e_feat has {e.numel()} entries, graph has {rg.E} edges")
+        if e.numel():
+            lo, hi = int(e.min().item()), int(e.max().item())
+            # reference indexes table[e_feat - 1] (layer/REGraphConv.py:61): ids must be 1..R
+            if lo < 1 or hi > 256 or (num_rel is not None and hi > num_rel):
+                raise ValueError(f"relation ids must lie in [1, {num_rel or 256}], got [{lo}, {hi}]")
+        self.max_rel = int(e.max().item()) if e.numel() else 0
+        r = (e - 1).to(torch.uint8)
+        self.rel_csr = r[rg.csr_eid].contiguous()
+        self.rel_csc = r[rg.csc_eid].contiguous()
+        self._cnt = {}
+        self.rg = rg
+
+    def long_cnt(self, n_rel):
+        """[n_long, n_rel] int32 relation histogram of every long CSR row."""
+        plan = self.rg.csr_plan
+        if plan.n_long == 0:
+            return None
+        if n_rel not in self._cnt:
+            rg = self.rg
+            deg = (rg.csr_ptr[1:] - rg.csr_ptr[:-1]).to(torch.int64)
+            lids = plan.long_ids.to(torch.int64)
+            row_of = torch.repeat_interleave(torch.arange(plan.n_long, device=rg.device),
+                                             deg[lids])
+            starts = rg.csr_ptr[lids].to(torch.int64)
+            offs = torch.cat([deg.new_zeros(1), torch.cumsum(deg[lids], 0)])[:-1]
+            pos = torch.arange(row_of.numel(), device=rg.device) - offs[row_of] + starts[row_of]
+            key = row_of * n_rel + self.rel_csr[pos].to(torch.int64)
+            cnt = torch.bincount(key, minlength=plan.n_long * n_rel)
+            self._cnt[n_rel] = cnt.view(plan.n_long, n_rel).to(torch.int32).contiguous()
+        return self._cnt[n_rel]
+
+
+class RelGraph:
+    """CSR (by destination) + CSC (by source) of a directed multigraph on one device."""
+
+    def __init__(self, src, dst, num_nodes, device, num_dst=None, split=SPLIT, chunk=CHUNK):
+        src = torch.as_tensor(src).to(device=device, dtype=torch.int64).reshape(-1)
+        dst = torch.as_tensor(dst).to(device=device, dtype=torch.int64).reshape(-1)
+        self.device = torch.device(device)
+        self.n_src = int(num_nodes)
+        self.n_dst = int(num_nodes if num_dst is None else num_dst)
+        self.E = int(src.numel())
+        if self.E >= 2 ** 31 or max(self.n_src, self.n_dst) >= 2 ** 31:
+            raise ValueError("graphs with >= 2^31 edges or nodes need 64-bit offsets (not built)")
+        _, csr_eid = torch.sort(dst, stable=True)
+        _, csc_eid = torch.sort(src, stable=True)
+        self.csr_eid = csr_eid
+        self.csc_eid = csc_eid
+        self.csr_idx = src[csr_eid].to(torch.int32).contiguous()
+        self.csc_idx = dst[csc_eid].to(torch.int32).contiguous()
+        self.csr_ptr = self._ptr(dst, self.n_dst)
+        self.csc_ptr = self._ptr(src, self.n_src)
+        inv = torch.empty_like(csr_eid)
+        inv[csr_eid] = torch.arange(self.E, device=self.device)
+        self.csc2csr = inv[csc_eid].to(torch.int32).contiguous()
+        self.csr_plan = SegPlan(self.csr_ptr, split, chunk)
+        self.csc_plan = SegPlan(self.csc_ptr, split, chunk)
+        self._packs = {}
+        self._inv_cnt = None
+
+    def _ptr(self, keys, n):
+        cnt = torch.bincount(keys, minlength=n)
+        return torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0)]).to(torch.int32).contiguous()
+
+    def in_degree(self):
+        return (self.csr_ptr[1:] - self.csr_ptr[:-1])
+
+    def inv_in_count(self):
+        """1 / max(in-count, 1) per destination (torch_scatter 'mean' divisor)."""
+        if self._inv_cnt is None:
+            self._inv_cnt = (1.0 / self.in_degree().clamp(min=1).to(torch.float32)).contiguous()
+        return self._inv_cnt
+
+    def rel_pack(self, e_feat, num_rel=None):
+        """RelPack for an e_feat tensor, cached on (storage, version, shape)."""
+        key = (e_feat.data_ptr(), getattr(e_feat, "_version", 0), tuple(e_feat.shape),
+               str(e_feat.device))
+        pack = self._packs.get(key)
+        if pack is None:
+            if len(self._packs) > 8:
+                self._packs.clear()
+            pack = RelPack(self, e_feat, num_rel)
+            pack._keepalive = e_feat
+            self._packs[key] = pack
+        return pack

@@ -1,0 +1,105 @@
+"""Model wiring over the drop-in layers, for tests and bench.py.
+
+The reference's own ``model/REGCN.py``, ``model/REGAT.py`` and ``model/REMixHop.py`` import the
+``layer`` package and run unchanged on this build; these classes restate the same wiring (same
+constructor arguments, parameter names and forward contract) so the repo can exercise the full
+models without shipping reference source.
+"""
+import torch
+import torch.nn as nn
+
+from layer import REGATConv, REGraphConv, REMixHopConv
+
+
+def _input_proj(feats_dim_list, width):
+    fcs = nn.ModuleList([nn.Linear(d, width, bias=True) for d in feats_dim_list])
+    for fc in fcs:
+        nn.init.xavier_normal_(fc.weight, gain=1.414)
+    return fcs
+
+
+class REGCN(nn.Module):
+    """model/REGCN.py:6-46: per-type Linear -> L x REGraphConv (first/last weightless) -> out_lin."""
+
+    def __init__(self, g, num_etypes, R, in_feats, n_hidden, n_classes, n_layers, activation,
+                 dropout, feats_dim_list):
+        super().__init__()
+        self.g = g
+        self.num_layers = n_layers
+        self.fc_list = _input_proj(feats_dim_list, in_feats)
+        self.layers = nn.ModuleList()
+        self.layers.append(REGraphConv(num_etypes, R, in_feats, n_hidden, bias=False,
+                                       activation=None, dropout=dropout, weight=False))
+        for _ in range(1, n_layers - 1):
+            self.layers.append(REGraphConv(num_etypes, R, n_hidden, n_hidden,
+                                           activation=activation, dropout=dropout))
+        self.layers.append(REGraphConv(num_etypes, R, n_hidden, n_classes, bias=False,
+                                       dropout=dropout, weight=False))
+        self.out_lin = nn.Linear(n_hidden, n_classes, bias=True)
+        self.dropout = nn.Dropout(p=dropout)
+
+    def forward(self, features_list, e_feat):
+        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = self.layers[0](self.g, h, e_feat)
+        for layer in self.layers[1:]:
+            h = layer(self.g, self.dropout(h), e_feat)
+        return self.out_lin(h), h
+
+
+class REGAT(nn.Module):
+    """model/REGAT.py:6-66 (the output layer is applied twice, as in the reference :61-64)."""
+
+    def __init__(self, g, num_etypes, R, num_layers, in_dim, num_hidden, num_classes, heads,
+                 activation, feat_drop, attn_drop, negative_slope, residual, feats_dim_list):
+        super().__init__()
+        self.g = g
+        self.num_layers = num_layers
+        self.fc_list = _input_proj(feats_dim_list, num_hidden)
+        self.gat_layers = nn.ModuleList()
+        self.gat_layers.append(REGATConv(num_etypes, R, in_dim, num_hidden, heads[0], feat_drop,
+                                         attn_drop, negative_slope, False, activation))
+        for l in range(1, num_layers - 1):
+            self.gat_layers.append(REGATConv(num_etypes, R, num_hidden * heads[l - 1], num_hidden,
+                                             heads[l], feat_drop, attn_drop, negative_slope,
+                                             residual, activation))
+        self.gat_layers.append(REGATConv(num_etypes, R, num_hidden * heads[-2], num_hidden,
+                                         heads[-2], feat_drop, attn_drop, negative_slope,
+                                         residual, None, use_weight=False))
+        self.out_lin = nn.Linear(num_hidden * heads[-2], num_classes)
+
+    def forward(self, features_list, e_feat):
+        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = self.gat_layers[0](self.g, h, e_feat).flatten(1)
+        for l in range(1, self.num_layers):
+            h = self.gat_layers[l](self.g, h, e_feat).flatten(1)
+        emb = self.gat_layers[-1](self.g, h, e_feat)
+        return self.out_lin(emb.flatten(1)), emb.mean(1)
+
+
+class REMixHop(nn.Module):
+    """model/REMixHop.py:19-100."""
+
+    def __init__(self, g, num_etypes, R, in_dim, hid_dim, out_dim, num_layers, feats_dim_list,
+                 p=(0, 1, 2), input_dropout=0.0, layer_dropout=0.0, activation=None,
+                 batchnorm=False):
+        super().__init__()
+        self.g = g
+        self.num_layers = num_layers
+        p = list(p)
+        self.dropout = nn.Dropout(input_dropout)
+        self.fc_list = _input_proj(feats_dim_list, in_dim)
+        self.layers = nn.ModuleList([REMixHopConv(num_etypes, R, in_dim, hid_dim, p=p,
+                                                  dropout=input_dropout, activation=activation,
+                                                  batchnorm=batchnorm)])
+        for _ in range(num_layers - 1):
+            self.layers.append(REMixHopConv(num_etypes, R, hid_dim * len(p), hid_dim, p=p,
+                                            dropout=layer_dropout, activation=activation,
+                                            batchnorm=batchnorm))
+        self.fc_layers = nn.Linear(hid_dim * len(p), out_dim, bias=False)
+
+    def forward(self, features_list, e_feat):
+        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = self.layers[0](self.g, h, e_feat)
+        for layer in self.layers[1:]:
+            h = layer(self.g, self.dropout(h), e_feat)
+        return self.fc_layers(h), h

@@ -1,0 +1,277 @@
+"""Autograd operators over the C-ABI (include/regnn_hip.h). Every forward and backward runs in the
+HIP library on torch's current stream; torch only allocates buffers and does the R-sized table
+math (LeakyReLU of the relation embedding) and dense projections.
+
+* degree_norm(rg, pack, tab, power)           layer/REGraphConv.py:66-75
+* re_spmm(rg, x, tab, pack, pre, post)         layer/REGraphConv.py:76,84-98 / REMixHopConv.py:78-82
+                                               / mag/regnn_layers.py:129,142-148
+* edge_spmm(rg, x, ew)                         generic fn.u_mul_e(h, ew) + fn.sum, ew per edge
+* gat_attention(rg, el, er, ee_tab, pack, s)   layer/REGATConv.py:80-88
+* head_spmm(rg, a, ft)                         layer/REGATConv.py:90-91
+"""
+import torch
+
+from . import _lib as L
+from .profile import timed
+
+_SLAB = None
+
+
+def _slab(width, device):
+    return torch.zeros(L.slab_rows(), width, dtype=torch.float32, device=device)
+
+
+def _reduce(slab, width, out=None, accumulate=False):
+    if out is None:
+        out = torch.empty(width, dtype=torch.float32, device=slab.device)
+    L.call("regnn_rel_reduce", L.ptr(slab), slab.shape[0], width, L.ptr(out), int(accumulate),
+           L.stream())
+    return out
+
+
+def _plan_args(plan, F, device):
+    if plan.n_chunk == 0:
+        return (0, 0, None, 0, None, None, 0, None), None
+    part = plan.partial(F, device)
+    return (plan.split, plan.chunk, L.ptr(plan.long_ids), plan.n_long, L.ptr(plan.chunk_long),
+            L.ptr(plan.chunk_off), plan.n_chunk, L.ptr(part)), part
+
+
+def _flat_table(tab):
+    return None if tab is None else tab.detach().reshape(-1).to(torch.float32).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------
+class _DegreeNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tab, rg, pack, power):
+        dev = rg.device
+        deg = torch.empty(rg.n_dst, dtype=torch.float32, device=dev)
+        norm = torch.empty_like(deg)
+        t = _flat_table(tab)
+        n_rel = t.numel() if t is not None else 0
+        plan = rg.csr_plan
+        cnt = pack.long_cnt(n_rel) if (t is not None and plan.n_long) else None
+        with timed("degree"):
+            L.call("regnn_degree", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr if pack else None),
+                   L.ptr(t), rg.n_dst, float(power), plan.split,
+                   L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), n_rel, L.ptr(deg), L.ptr(norm),
+                   L.stream())
+        ctx.rg, ctx.pack, ctx.power, ctx.n_rel, ctx.shape = rg, pack, power, n_rel, tab.shape
+        ctx.save_for_backward(deg)
+        ctx.mark_non_differentiable(deg)
+        return norm, deg
+
+    @staticmethod
+    def backward(ctx, g_norm, _g_deg):
+        if not ctx.needs_input_grad[0] or g_norm is None:
+            return None, None, None, None
+        (deg,) = ctx.saved_tensors
+        rg, pack, n_rel = ctx.rg, ctx.pack, ctx.n_rel
+        plan = rg.csr_plan
+        slab = _slab(n_rel, rg.device)
+        cnt = pack.long_cnt(n_rel) if plan.n_long else None
+        with timed("degree_bwd"):
+            L.call("regnn_degree_bwd", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr), L.ptr(deg),
+                   L.ptr(g_norm.contiguous().float()), rg.n_dst, float(ctx.power), n_rel,
+                   plan.split, L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), L.ptr(slab),
+                   L.stream())
+        g = _reduce(slab, n_rel)
+        return g.view(ctx.shape), None, None, None
+
+
+def degree_norm(rg, pack, tab, power=-0.5):
+    """norm[v] = max(sum_{e->v} tab[rel_e], 1)^power  (differentiable in tab)."""
+    norm, _ = _DegreeNorm.apply(tab, rg, pack, power)
+    return norm
+
+
+def in_count_norm(rg, power=-0.5):
+    """unweighted variant (copy_u degree)."""
+    deg = rg.in_degree().to(torch.float32)
+    return deg.clamp(min=1).pow(power)
+
+
+# ---------------------------------------------------------------------------------------------
+class _ReSpmm(torch.autograd.Function):
+    """y = post * (A_tab (pre * x)), A_tab[v,u] = sum over edges u->v of tab[rel_e]."""
+
+    @staticmethod
+    def forward(ctx, x, tab, pre, post, bias, rg, pack):
+        x = x.contiguous()
+        F = x.shape[1]
+        y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
+        t = _flat_table(tab)
+        plan_args, part = _plan_args(rg.csr_plan, F, x.device)
+        with timed("spmm_fwd"):
+            L.call("regnn_spmm_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                   L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
+                   L.ptr(t), None, L.ptr(pre), L.ptr(post),
+                   L.ptr(None if bias is None else bias.detach().float().contiguous()),
+                   L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args, L.stream())
+        ctx.rg, ctx.pack, ctx.tab_shape = rg, pack, None if tab is None else tab.shape
+        ctx.same_scale = pre is not None and pre is post and rg.n_src == rg.n_dst
+        ctx.save_for_backward(x, y, t, pre, post)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, t, pre, post = ctx.saved_tensors
+        rg, pack = ctx.rg, ctx.pack
+        need_x, need_tab, need_pre, need_post, need_bias = ctx.needs_input_grad[:5]
+        gy = gy.contiguous().to(x.dtype)
+        F = x.shape[1]
+        gx = torch.empty(rg.n_src, F, dtype=x.dtype, device=x.device)
+        n_rel = t.numel() if t is not None else 0
+        slab = _slab(n_rel, x.device) if (need_tab and t is not None) else None
+        node = None
+        if ctx.same_scale and (need_pre or need_post):
+            node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
+        elif need_pre:
+            node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
+        plan_args, part = _plan_args(rg.csc_plan, F, x.device)
+        with timed("spmm_bwd"):
+            L.call("regnn_spmm_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                   L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
+                   L.ptr(t), None, L.ptr(post), L.ptr(pre), L.ptr(gy), L.ptr(x),
+                   L.ptr(y if ctx.same_scale and node is not None else None), L.ptr(gx),
+                   L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F, L.dtype_code(x),
+                   *plan_args, L.stream())
+        g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
+        g_pre = g_post = None
+        if ctx.same_scale:
+            g_pre = node
+        else:
+            if need_pre:
+                g_pre = node
+            if need_post:
+                yf, gf = y.float(), gy.float()
+                g_post = (gf * yf).sum(1) / post
+        g_bias = gy.float().sum(0) if need_bias else None
+        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None
+
+
+def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None):
+    """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * x[u] + bias  (HIP)."""
+    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack)
+
+
+# ---------------------------------------------------------------------------------------------
+class _EdgeSpmm(torch.autograd.Function):
+    """y[v] = sum_{e: u->v} ew[e] * x[u]; ew per edge in the caller's edge order."""
+
+    @staticmethod
+    def forward(ctx, x, ew, rg):
+        x = x.contiguous()
+        F = x.shape[1]
+        ewf = ew.detach().reshape(-1).float()
+        w_csr = ewf[rg.csr_eid].contiguous()
+        y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
+        plan_args, part = _plan_args(rg.csr_plan, F, x.device)
+        L.call("regnn_spmm_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), None, None, L.ptr(w_csr),
+               None, None, None, L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args,
+               L.stream())
+        ctx.rg, ctx.ew_shape = rg, ew.shape
+        ctx.save_for_backward(x, ewf)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, ewf = ctx.saved_tensors
+        rg = ctx.rg
+        gy = gy.contiguous().to(x.dtype)
+        F = x.shape[1]
+        gx = torch.empty(rg.n_src, F, dtype=x.dtype, device=x.device)
+        w_csc = ewf[rg.csc_eid].contiguous()
+        eg = torch.empty(rg.E, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[1] else None
+        plan_args, part = _plan_args(rg.csc_plan, F, x.device)
+        L.call("regnn_spmm_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx), None, None, L.ptr(w_csc),
+               None, None, L.ptr(gy), L.ptr(x), None, L.ptr(gx), None, 0, L.ptr(eg), None,
+               rg.n_src, F, L.dtype_code(x), *plan_args, L.stream())
+        g_ew = None
+        if eg is not None:
+            g_ew = torch.empty_like(eg)
+            g_ew[rg.csc_eid] = eg
+            g_ew = g_ew.view(ctx.ew_shape)
+        return gx, g_ew, None
+
+
+def edge_spmm(rg, x, ew):
+    return _EdgeSpmm.apply(x, ew, rg)
+
+
+# ---------------------------------------------------------------------------------------------
+class _GatAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, el, er, ee_tab, rg, pack, slope):
+        el, er = el.contiguous().float(), er.contiguous().float()
+        H = el.shape[1]
+        a = torch.empty(rg.E, H, dtype=torch.float32, device=el.device)
+        t = None if ee_tab is None else ee_tab.detach().float().contiguous()
+        with timed("gat_softmax_fwd"):
+            L.call("regnn_gat_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                   L.ptr(pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
+                   L.ptr(er), rg.n_dst, H, float(slope), L.ptr(a), L.stream())
+        ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
+        ctx.tab_shape = None if ee_tab is None else ee_tab.shape
+        ctx.save_for_backward(el, er, t, a)
+        return a
+
+    @staticmethod
+    def backward(ctx, ga):
+        el, er, t, a = ctx.saved_tensors
+        rg, H = ctx.rg, el.shape[1]
+        ga = ga.contiguous().float()
+        gs = torch.empty_like(a)
+        ger = torch.empty_like(er)
+        n_rel = t.shape[0] if t is not None else 0
+        slab = _slab(n_rel * H, el.device) if (t is not None and ctx.needs_input_grad[2]) else None
+        with timed("gat_softmax_bwd"):
+            L.call("regnn_gat_softmax_bwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                   L.ptr(ctx.pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
+                   L.ptr(er), L.ptr(a), L.ptr(ga), rg.n_dst, H, float(ctx.slope), L.ptr(gs),
+                   L.ptr(ger), L.ptr(slab), n_rel, L.stream())
+        gel = torch.empty(rg.n_src, H, dtype=torch.float32, device=el.device)
+        L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
+               L.ptr(gel), L.stream())
+        g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
+        return gel, ger, g_tab, None, None, None
+
+
+def gat_attention(rg, el, er, ee_tab=None, pack=None, slope=0.2):
+    """a[e,h] (CSR edge order) = edge_softmax(leaky_relu(el[u]+er[v]+ee[rel_e], slope))."""
+    return _GatAttention.apply(el, er, ee_tab, rg, pack, slope)
+
+
+class _HeadSpmm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, ft, rg):
+        N, H, D = ft.shape
+        ft = ft.contiguous()
+        a = a.contiguous().float()
+        y = torch.empty(rg.n_dst, H, D, dtype=ft.dtype, device=ft.device)
+        with timed("spmm_heads_fwd"):
+            L.call("regnn_spmm_heads_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), None, L.ptr(a),
+                   L.ptr(ft), L.ptr(y), rg.n_dst, H, D, L.dtype_code(ft), L.stream())
+        ctx.rg = rg
+        ctx.save_for_backward(a, ft)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        a, ft = ctx.saved_tensors
+        rg = ctx.rg
+        N, H, D = ft.shape
+        gy = gy.contiguous().to(ft.dtype)
+        gft = torch.empty_like(ft)
+        ga = torch.empty_like(a)
+        with timed("spmm_heads_bwd"):
+            L.call("regnn_spmm_heads_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                   L.ptr(rg.csc2csr), L.ptr(a), L.ptr(gy), L.ptr(ft), L.ptr(gft), L.ptr(ga),
+                   rg.n_src, H, D, L.dtype_code(ft), L.stream())
+        return ga, gft, None
+
+
+def head_spmm(rg, a, ft):
+    """out[v,h,:] = sum_{e: u->v} a[e,h] * ft[u,h,:]   (a in CSR edge order)."""
+    return _HeadSpmm.apply(a, ft, rg)
