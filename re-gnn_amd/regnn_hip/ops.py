@@ -152,7 +152,12 @@ class _ReSpmm(torch.autograd.Function):
 
 
 def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None):
-    """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * x[u] + bias  (HIP)."""
+    """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * x[u] + bias  (HIP).
+
+    The bias is fused into the kernel epilogue unless the backward needs the pre-bias output
+    (differentiable post-scale: the node-norm gradient reads <g, y> / post)."""
+    if bias is not None and post is not None and post.requires_grad:
+        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack) + bias
     return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack)
 
 
