@@ -6,8 +6,3 @@ the ctypes boundary to libregnn_hip.so and the autograd operators.
 """
 from .graph import RelGraph, RelPack, SegPlan  # noqa: F401
 
-
-def ops():
-    """import the native operators (raises if libregnn_hip.so is missing: no CPU fallback)."""
-    from . import ops as _ops
-    return _ops
