@@ -1,0 +1,162 @@
+"""ogbn-mag neighbour-sampled path on MI355X: mag ``REGCNConv`` (mag/regnn_layers.py:24-150), the
+``REGNN`` model (mag/regnn_ns.py:216-369) and a data-parallel train step with a flat-bucket RCCL
+gradient all-reduce (inserted between mag/regnn_ns.py:406 and :407).
+
+The sampled block's aggregation (PyG propagate with aggr='mean', message ew * x_j, update +bias)
+runs as one HIP SpMM with the relation table, the 1/in-count scale and the bias fused; its
+backward is the fused transposed SpMM + relation-bin SDDMM.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch.nn import Linear, ModuleDict, ModuleList, Parameter, init
+
+from . import ops
+from .graph import RelGraph
+
+
+def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_types,
+               self_loop_type=2):
+    """device CSR/CSC of a sampled bipartite block, self loops appended for the targets with
+    type ntype + num_edge_types (mag/regnn_layers.py:90-96). Returns (RelGraph, RelPack)."""
+    src, dst = edge_index[0].to(torch.int64), edge_index[1].to(torch.int64)
+    et = edge_type.to(torch.int64)
+    if self_loop_type == 2:
+        loop = torch.arange(n_dst, device=src.device)
+        src = torch.cat([src, loop])
+        dst = torch.cat([dst, loop])
+        et = torch.cat([et, target_node_type.to(torch.int64) + num_edge_types])
+    rg = RelGraph(src, dst, n_src, src.device, num_dst=n_dst)
+    pack = rg.rel_pack(et + 1)
+    return rg, pack
+
+
+class REGCNConv(torch.nn.Module):
+    """mag/regnn_layers.py:24-150 (same constructor, parameters and forward signature)."""
+
+    def __init__(self, in_channels, out_channels, num_node_types, num_edge_types,
+                 scaling_factor=100., dropout=0., use_softmax=False, residual=False,
+                 use_norm=None, self_loop_type=1, no_re=False):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.num_node_types, self.num_edge_types = num_node_types, num_edge_types
+        self.use_softmax = use_softmax
+        self.dropout, self.residual, self.use_norm = dropout, residual, use_norm
+        self.self_loop_type = self_loop_type
+        self.weight = Parameter(torch.Tensor(in_channels, out_channels))
+        if self.residual:
+            self.weight_root = self.weight        # shared, as in the reference (:51)
+        self.bias = Parameter(torch.Tensor(out_channels))
+        rw_dim = num_edge_types if self_loop_type in (1, 3) else num_edge_types + num_node_types
+        self.relation_weight = Parameter(torch.Tensor(rw_dim), requires_grad=not no_re)
+        self.scaling_factor = scaling_factor
+        if self.use_norm == 'bn':
+            self.norm = torch.nn.BatchNorm1d(out_channels)
+        elif self.use_norm == 'ln':
+            self.norm = torch.nn.LayerNorm(out_channels)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        init.xavier_uniform_(self.weight)
+        init.zeros_(self.bias)
+        init.constant_(self.relation_weight, 1.0 / self.scaling_factor)
+        if self.use_norm in ('bn', 'ln'):
+            self.norm.reset_parameters()
+
+    def forward(self, x, edge_index, edge_type=None, target_node_type=None,
+                return_weights=False):
+        if self.use_softmax:
+            raise NotImplementedError("use_softmax=True (global-max softmax) is not on the HIP path")
+        x_src, x_target = x
+        if isinstance(edge_index, tuple):           # pre-built (RelGraph, RelPack) block
+            rg, pack = edge_index
+        else:
+            rg, pack = make_block(edge_index, edge_type, target_node_type, x_src.shape[0],
+                                  x_target.shape[0], self.num_edge_types, self.self_loop_type)
+        xs = torch.matmul(x_src, self.weight)                                    # :102
+        tab = F.leaky_relu(self.relation_weight * self.scaling_factor)           # :110-111
+        # mean of ew * x_j over in-edges incl. self loops, + bias (:113,129,142-148)
+        out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
+        if self.residual:
+            out = out + torch.matmul(x_target, self.weight)                      # :104,131-132
+        if self.use_norm in ('bn', 'ln'):
+            out = self.norm(out)                                                 # :134-135
+        if return_weights:
+            return out, None, tab
+        return out
+
+
+class REGNN(torch.nn.Module):
+    """mag/regnn_ns.py:216-369 for model 'regcn' (feats_type != 2)."""
+
+    def __init__(self, in_channels, hidden_channels, out_channels, num_layers, scaling_factor,
+                 dropout, num_feature_dict, num_edge_types, residual=False, no_re=False,
+                 use_norm='ln', self_loop_type=2):
+        super().__init__()
+        self.hidden_dim = hidden_channels
+        self.num_layers, self.dropout = num_layers, dropout
+        self.num_node_types = len(num_feature_dict)
+        self.num_edge_types = num_edge_types
+        self.self_loop_type = self_loop_type
+        self.lins = ModuleDict({str(k): Linear(d, hidden_channels)
+                                for k, d in num_feature_dict.items()})
+        self.convs = ModuleList([
+            REGCNConv(hidden_channels, hidden_channels, self.num_node_types, num_edge_types,
+                      scaling_factor, dropout=dropout, residual=residual, use_norm=use_norm,
+                      self_loop_type=self_loop_type, no_re=no_re)
+            for _ in range(num_layers)])
+        self.out_lin = Linear(hidden_channels, out_channels)
+        if use_norm == 'ln':
+            self.norm = torch.nn.LayerNorm(hidden_channels)   # declared, unused in forward
+        elif use_norm == 'bn':
+            self.norm = torch.nn.BatchNorm1d(hidden_channels)
+
+    def group_input(self, x_dict, node_type, local_node_idx, n_id=None):
+        if n_id is not None:
+            node_type, local_node_idx = node_type[n_id], local_node_idx[n_id]
+        h = torch.zeros(node_type.numel(), self.hidden_dim, device=node_type.device)
+        for key, x in x_dict.items():
+            mask = node_type == key
+            h[mask] = self.lins[str(key)](x[local_node_idx[mask]])
+        return h
+
+    def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
+        x = self.group_input(x_dict, node_type, local_node_idx, n_id)
+        ntype = node_type[n_id]
+        for i, adj in enumerate(adjs):
+            edge_index, e_id, size = adj
+            x_target = x[:size[1]]
+            ntype = ntype[:size[1]]
+            x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
+            x = F.relu(x)
+            x = F.dropout(x, p=self.dropout, training=self.training)
+        return self.out_lin(x).log_softmax(dim=-1)
+
+
+def flat_grad_allreduce(params, world):
+    """one SUM all-reduce of every gradient in a flat fp32 bucket, then / world (RCCL over xGMI
+    on ROCm devices; gloo on CPU). Sized 0.26-4 MB for the mag configs: latency-bound, one call."""
+    grads = [p.grad for p in params if p.grad is not None]
+    if world <= 1 or not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    flat /= world
+    o = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[o:o + n].view_as(g))
+        o += n
+
+
+def train_step(model, opt, batch, x_dict, edge_type, node_type, local_node_idx, y_global, world):
+    """mag/regnn_ns.py:399-407 with the gradient all-reduce between backward and step."""
+    batch_size, n_id, adjs = batch
+    opt.zero_grad(set_to_none=True)
+    out = model(n_id, x_dict, adjs, edge_type, node_type, local_node_idx)
+    y = y_global[n_id][:batch_size].squeeze(-1)
+    loss = F.nll_loss(out, y)
+    loss.backward()
+    flat_grad_allreduce(list(model.parameters()), world)
+    opt.step()
+    return loss
