@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change). */
+/* ABI version (bumped on any signature change; currently 2). */
 int regnn_abi_version(void);
 
 /* Rows of the per-block relation-gradient slab that regnn_spmm_bwd / regnn_degree_bwd write
@@ -75,14 +75,20 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
  * Any of rel_table / edge_w / in_scale / out_scale / bias may be NULL.
  * Long-segment plan (all NULL / 0 when split == 0): long_ids[n_long] = segments with more than
  * `split` edges; chunk c covers edges [ptr[s] + k*chunk, ...) of s = long_ids[chunk_long[c]],
- * k = c - chunk_off[chunk_long[c]]; chunk_partial is fp32 scratch [n_chunk, F]. */
+ * k = c - chunk_off[chunk_long[c]]. Chunk partial sums are combined by a fixed-order tree:
+ * level k (k < n_levels) reduces partial rows [sb[p], sb[p+1]) (sb = level_sb + desc[k][0],
+ * p < desc[k][1]) into row desc[k][2] + p; the last level leaves row desc[n-1][2] + l for long
+ * segment l (n_levels == 0: row chunk_off[l]). level_desc is a HOST array [n_levels][3]
+ * (int64: sb offset, n_out, output row base); chunk_partial is fp32 scratch
+ * [n_chunk + sum n_out, F]. Deterministic for any chunk count (hub rows of 10^7 edges). */
 int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    const float* rel_table, const float* edge_w,
                    const float* in_scale, const float* out_scale, const float* bias,
                    const void* x, void* y, int64_t n_seg, int32_t F, int32_t dtype,
                    int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
                    const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
-                   float* chunk_partial, hipStream_t stream);
+                   float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                   const int64_t* level_desc, hipStream_t stream);
 
 /* Relation-embedding SpMM, fused backward over the transposed graph (CSC: segment = source u).
  * Replaces DGL GSpMM.backward (gspmm on the reverse graph + gsddmm 'dot' for the edge weight)
@@ -103,7 +109,8 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    int64_t n_seg, int32_t F, int32_t dtype,
                    int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
                    const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
-                   float* chunk_partial, hipStream_t stream);
+                   float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                   const int64_t* level_desc, hipStream_t stream);
 
 /* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order. */
 int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,

@@ -42,6 +42,9 @@ struct SpmmArgs {
     const int32_t* chunk_off;
     int32_t n_chunk;
     float* chunk_partial;
+    const int32_t* level_sb;     // tree reduction of chunk partials (see regnn_spmm_fwd)
+    int32_t n_levels;
+    const int64_t* level_desc;   // HOST [n_levels][3]: sb offset, n_out, partial row base
     int32_t slab_row0;     // first slab row this launch writes
 };
 
@@ -259,9 +262,44 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
     if (use_bins) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
 }
 
-// one group per long segment: fixed-order sum of its chunk partials, then the epilogue
+// one level of the fixed-order tree over chunk partials: output row p = sum of input rows
+// [sb[p], sb[p+1]) in order (consecutive rows of one long segment), one group per output row
+template <int LPR>
+__global__ void __launch_bounds__(kBlock)
+partial_reduce(const float* __restrict__ in, const int32_t* __restrict__ sb, int64_t n_out, int F,
+               float* __restrict__ out) {
+    constexpr int GPB = kBlock / LPR;
+    const int tid = threadIdx.x, lane = tid & (LPR - 1);
+    const int nv = F / 4;
+    for (int64_t p = (int64_t)blockIdx.x * GPB + tid / LPR; p < n_out;
+         p += (int64_t)gridDim.x * GPB) {
+        const int b = sb[p], e = sb[p + 1];
+        for (int v = lane; v < nv; v += LPR) {
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            int r = b;
+            for (; r + 4 <= e; r += 4) {
+                float x[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) Vec<float>::load(in + (int64_t)(r + u) * F + 4 * v, x[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t] += x[u][t];
+            }
+            for (; r < e; ++r) {
+                float x[4];
+                Vec<float>::load(in + (int64_t)r * F + 4 * v, x);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t] += x[t];
+            }
+            Vec<float>::store(out + p * F + 4 * v, acc);
+        }
+    }
+}
+
+// one group per long segment: its fully reduced partial row, then the epilogue
 template <typename T, int LPR, int NV, bool BWD>
-__global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a) {
+__global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_base) {
     using S = Seg<T, LPR, NV>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
@@ -272,15 +310,14 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a) {
         float acc[NV][S::EV] = {};
         float sx[NV][S::EV] = {};
         if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
-        for (int c = a.chunk_off[l]; c < a.chunk_off[l + 1]; ++c) {
-            const float* part = a.chunk_partial + (int64_t)c * a.F;
+        const int64_t row = final_base >= 0 ? final_base + l : a.chunk_off[l];
+        const float* part = a.chunk_partial + row * a.F;
 #pragma unroll
-            for (int q = 0; q < NV; ++q) {
-                const int o = S::off(q, lane);
-                if (o < a.F) {
+        for (int q = 0; q < NV; ++q) {
+            const int o = S::off(q, lane);
+            if (o < a.F) {
 #pragma unroll
-                    for (int t = 0; t < S::EV; ++t) acc[q][t] += part[o + t];
-                }
+                for (int t = 0; t < S::EV; ++t) acc[q][t] = part[o + t];
             }
         }
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
@@ -301,8 +338,20 @@ int launch_spmm(SpmmArgs a, hipStream_t stream) {
         const int g2 = grid_for(a.n_chunk, GPB);
         hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, BWD>), dim3(g2), dim3(kBlock), lds, stream, a);
         REGNN_LAUNCH_CHECK();
+        int64_t base_in = 0, final_base = -1;
+        for (int k = 0; k < a.n_levels; ++k) {
+            const int64_t sb_off = a.level_desc[3 * k], n_out = a.level_desc[3 * k + 1];
+            const int64_t base_out = a.level_desc[3 * k + 2];
+            hipLaunchKernelGGL((partial_reduce<16>), dim3(grid_for(n_out, kBlock / 16)),
+                               dim3(kBlock), 0, stream, a.chunk_partial + base_in * a.F,
+                               a.level_sb + sb_off, n_out, a.F, a.chunk_partial + base_out * a.F);
+            REGNN_LAUNCH_CHECK();
+            base_in = base_out;
+            final_base = base_out;
+        }
         const int g3 = grid_for(a.n_long, GPB);
-        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, BWD>), dim3(g3), dim3(kBlock), 0, stream, a);
+        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, BWD>), dim3(g3), dim3(kBlock), 0, stream, a,
+                           final_base);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
@@ -413,7 +462,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 1; }
+int regnn_abi_version(void) { return 2; }
 
 int64_t regnn_slab_rows(int64_t, int32_t) { return 2 * int64_t(kMaxGrid); }
 
@@ -422,13 +471,15 @@ static SpmmArgs make_args(const int32_t* ptr, const int32_t* idx, const uint8_t*
                           const float* out_scale, int64_t n_seg, int32_t F, int32_t split,
                           int32_t chunk, const int32_t* long_ids, int32_t n_long,
                           const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
-                          float* chunk_partial) {
+                          float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                          const int64_t* level_desc) {
     SpmmArgs a{};
     a.ptr = ptr; a.idx = idx; a.rel = rel; a.tab = tab; a.edge_w = edge_w;
     a.in_scale = in_scale; a.out_scale = out_scale; a.n_seg = n_seg; a.F = F;
     a.split = split; a.chunk = chunk; a.long_ids = long_ids; a.n_long = n_long;
     a.chunk_long = chunk_long; a.chunk_off = chunk_off; a.n_chunk = n_chunk;
     a.chunk_partial = chunk_partial;
+    a.level_sb = level_sb; a.n_levels = n_levels; a.level_desc = level_desc;
     return a;
 }
 
@@ -452,14 +503,17 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
                    const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
                    const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
                    hipStream_t stream) {
     int st = check_common(ptr, idx, x, y, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
     if (st) return st;
     if (n_seg == 0) return REGNN_OK;
-    if (n_long == 0) { split = 0; n_chunk = 0; }
+    if (n_levels < 0 || (n_levels > 0 && (!level_sb || !level_desc))) return REGNN_EINVAL;
+    if (n_long == 0) { split = 0; n_chunk = 0; n_levels = 0; }
     SpmmArgs a = make_args(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, n_seg, F, split,
-                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial);
+                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial,
+                           level_sb, n_levels, level_desc);
     a.bias = bias; a.src = x; a.out = y;
     if (dtype == REGNN_F32) return dispatch<float, false>(a, stream);
     if (dtype == REGNN_BF16) return dispatch<bf16_t, false>(a, stream);
@@ -473,6 +527,7 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
                    const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
                    const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
                    hipStream_t stream) {
     int st = check_common(ptr, idx, g, gx, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
@@ -480,9 +535,11 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
     if (slab && (!rel || n_rel <= 0 || n_rel > 64)) return REGNN_EINVAL;
     if ((slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
-    if (n_long == 0) { split = 0; n_chunk = 0; }
+    if (n_levels < 0 || (n_levels > 0 && (!level_sb || !level_desc))) return REGNN_EINVAL;
+    if (n_long == 0) { split = 0; n_chunk = 0; n_levels = 0; }
     SpmmArgs a = make_args(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, n_seg, F, split,
-                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial);
+                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial,
+                           level_sb, n_levels, level_desc);
     a.src = g; a.out = gx; a.self = x; a.ng_a = y ? g : nullptr; a.ng_b = y;
     a.slab = slab; a.n_rel = n_rel; a.edge_grad = edge_grad; a.node_grad = node_grad;
     if (dtype == REGNN_F32) return dispatch<float, true>(a, stream);

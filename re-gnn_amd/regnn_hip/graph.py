@@ -10,10 +10,13 @@ HBM layout (built once per graph per device, int32 indices, uint8 relation ids):
 Edge ids are the caller's (DGL) edge order; within a CSR row edges stay in edge-id order
 (stable sort), which is the summation order of DGL's own CSR gspmm.
 """
+import ctypes
+
 import torch
 
 SPLIT = 256      # segments with more edges than this go through the chunked path
 CHUNK = 256      # edges per chunk
+FANIN = 64       # chunk partials summed per node of the reduction tree
 
 
 class SegPlan:
@@ -27,19 +30,46 @@ class SegPlan:
         if self.n_long == 0:
             self.split = 0
             self.long_ids = self.chunk_long = self.chunk_off = None
-            self.n_chunk = 0
+            self.n_chunk = self.n_levels = self.partial_rows = 0
+            self.level_sb, self.level_desc = None, None
             return
         nch = (deg[long_ids] + chunk - 1) // chunk
         self.long_ids = long_ids.to(torch.int32)
-        self.chunk_off = torch.cat([nch.new_zeros(1), torch.cumsum(nch, 0)]).to(torch.int32)
+        off = torch.cat([nch.new_zeros(1), torch.cumsum(nch, 0)])
+        self.chunk_off = off.to(torch.int32)
         self.chunk_long = torch.repeat_interleave(
             torch.arange(self.n_long, device=ptr.device, dtype=torch.int32), nch)
-        self.n_chunk = int(self.chunk_off[-1].item())
+        self.n_chunk = int(off[-1].item())
+        self._tree(nch, off)
+
+    def _tree(self, counts, in_off, fanin=FANIN):
+        """fixed-order reduction tree over each long segment's chunk partials (<= fanin inputs
+        per node): level k turns partial rows [sb[p], sb[p+1]) into row base_k + p."""
+        dev = counts.device
+        rows = torch.arange(self.n_long, device=dev)
+        sbs, desc = [], []
+        sb_total, base, total_in = 0, self.n_chunk, self.n_chunk
+        while int(counts.max().item()) > 1:
+            n_out = (counts + fanin - 1) // fanin
+            out_off = torch.cat([n_out.new_zeros(1), torch.cumsum(n_out, 0)])
+            P = int(out_off[-1].item())
+            l = torch.repeat_interleave(rows, n_out)
+            j = torch.arange(P, device=dev) - out_off[l]
+            sb = torch.cat([in_off[l] + j * fanin, in_off.new_tensor([total_in])])
+            sbs.append(sb.to(torch.int32))
+            desc += [sb_total, P, base]
+            sb_total += P + 1
+            base += P
+            counts, in_off, total_in = n_out, out_off, P
+        self.n_levels = len(sbs)
+        self.level_sb = torch.cat(sbs).contiguous() if sbs else None
+        self.level_desc = (ctypes.c_int64 * max(1, len(desc)))(*desc)
+        self.partial_rows = base
 
     def partial(self, F, device):
         if self.n_chunk == 0:
             return None
-        return torch.empty(self.n_chunk, F, dtype=torch.float32, device=device)
+        return torch.empty(self.partial_rows, F, dtype=torch.float32, device=device)
 
 
 class RelPack:

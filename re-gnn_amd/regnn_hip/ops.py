@@ -9,6 +9,8 @@ math (LeakyReLU of the relation embedding) and dense projections.
 * gat_attention(rg, el, er, ee_tab, pack, s)   layer/REGATConv.py:80-88
 * head_spmm(rg, a, ft)                         layer/REGATConv.py:90-91
 """
+import ctypes
+
 import torch
 
 from . import _lib as L
@@ -31,10 +33,11 @@ def _reduce(slab, width, out=None, accumulate=False):
 
 def _plan_args(plan, F, device):
     if plan.n_chunk == 0:
-        return (0, 0, None, 0, None, None, 0, None), None
+        return (0, 0, None, 0, None, None, 0, None, None, 0, None), None
     part = plan.partial(F, device)
     return (plan.split, plan.chunk, L.ptr(plan.long_ids), plan.n_long, L.ptr(plan.chunk_long),
-            L.ptr(plan.chunk_off), plan.n_chunk, L.ptr(part)), part
+            L.ptr(plan.chunk_off), plan.n_chunk, L.ptr(part), L.ptr(plan.level_sb),
+            plan.n_levels, ctypes.cast(plan.level_desc, ctypes.c_void_p)), part
 
 
 def _flat_table(tab):

@@ -37,7 +37,7 @@ def test_invalid_arguments_rejected_without_gpu():
     """argument validation happens before any launch: NULL ptr array -> EINVAL (1)."""
     from regnn_hip import _lib
     rc = _lib._so.regnn_spmm_fwd(None, None, None, None, None, None, None, None, None, None,
-                                 10, 64, 0, 0, 0, None, 0, None, None, 0, None, None)
+                                 10, 64, 0, 0, 0, None, 0, None, None, 0, None, None, 0, None, None)
     assert rc == 1
     rc = _lib._so.regnn_degree_bwd(None, None, None, None, 5, -0.5, 100, 0, None, 0, None, None,
                                    None)
