@@ -79,7 +79,10 @@ def build_workload(args, dev):
 def train_step(w):
     net, opt = w["net"], w["opt"]
     logits, _ = net(w["feats"], w["e_feat"])
-    loss = F.cross_entropy(logits[: w["labels"].numel()], w["labels"])
+    # = F.cross_entropy(logits[train], y) (run_regnn.py:147); gather form: torch's nll_loss
+    # reduction is a single-block kernel (17 ms at 7.4M rows, profiled)
+    logp = F.log_softmax(logits[: w["labels"].numel()], dim=1)
+    loss = -logp.gather(1, w["labels"].unsqueeze(1)).mean()
     opt.zero_grad(set_to_none=True)
     loss.backward()
     opt.step()

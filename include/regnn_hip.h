@@ -154,6 +154,13 @@ int regnn_spmm_heads_bwd(const int32_t* ptr, const int32_t* idx, const int32_t* 
 int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals, int64_t n_seg,
                       int32_t H, float* out, hipStream_t stream);
 
+/* Column sum of a row-major fp32 [rows, cols] matrix into per-block partial rows:
+ * slab[b][c] = sum of column c over block b's row range (at most regnn_slab_rows()/2 blocks;
+ * zero the slab first, then regnn_rel_reduce(slab, rows_of_slab, cols, out, 0)).
+ * Replaces torch's grad.sum(0) for the bias gradient of nn.Linear heads over all nodes
+ * (model/REGCN.py:32,45 out_lin), which ran far below HBM rate for N ~ 1e7 rows. */
+int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Neighbour sampler (replaces torch_sparse SparseTensor.sample_adj behind PyG NeighborSampler,
  * mag/regnn_ns.py:206-214). Spec (this build's, documented in DESIGN.md; torch_sparse's RNG is

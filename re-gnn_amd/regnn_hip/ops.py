@@ -283,3 +283,13 @@ class _HeadSpmm(torch.autograd.Function):
 def head_spmm(rg, a, ft):
     """out[v,h,:] = sum_{e: u->v} a[e,h] * ft[u,h,:]   (a in CSR edge order)."""
     return _HeadSpmm.apply(a, ft, rg)
+
+
+# ---------------------------------------------------------------------------------------------
+def col_sum(x):
+    """x.sum(0) for a tall row-major fp32 matrix, deterministic (HIP col_sum + slab reduce)."""
+    x = x.contiguous().float()
+    rows, cols = x.shape
+    slab = torch.zeros(L.slab_rows() // 2, cols, dtype=torch.float32, device=x.device)
+    L.call("regnn_col_sum", L.ptr(x), rows, cols, L.ptr(slab), L.stream())
+    return _reduce(slab, cols)
