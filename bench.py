@@ -179,11 +179,16 @@ def main():
     launches, mean_ms, _ = cand[dom]
     byts = spmm_bytes(rg.E, rg.n_dst, F_, s, dom)
     achieved = byts / (mean_ms / 1e3) / 1e9
+    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/gpu_pmc.sh:
+    # FETCH_SIZE and WRITE_SIZE in separate runs, calibrated on a 4 GiB copy), valid only for the
+    # exact graph it was measured on
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{dom}.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("bytes_per_launch")
+            rec = json.load(f)
+        if rec.get("graph") == {"N": rg.n_dst, "E": rg.E} and dom in rec:
+            traffic = rec[dom]["bytes_per_launch"]
 
     result = {
         "metric": "aggregated edges/sec per GPU (REGCN fwd+bwd, hidden=64); % HBM roofline",

@@ -70,7 +70,8 @@ class NeighborSampler:
             return self.node_idx
         g = torch.Generator()
         g.manual_seed(self.seed * 1_000_003 + self.epoch)
-        return self.node_idx[torch.randperm(self.node_idx.numel(), generator=g).to(self.rg.device)]
+        perm = torch.randperm(self.node_idx.numel(), generator=g)
+        return self.node_idx[perm.to(self.node_idx.device)]
 
     def num_batches(self):
         n = self.node_idx.numel()
@@ -80,12 +81,16 @@ class NeighborSampler:
     def __len__(self):
         return self.num_batches()
 
-    def __iter__(self):
+    def batches(self):
+        """(global batch index, target nodes) of this rank for the current epoch."""
         order = self._order()
         n = order.numel()
         nb = n // self.batch_size if self.drop_last else -(-n // self.batch_size)
         for b in range(self.rank, nb, self.world):
-            batch = order[b * self.batch_size:(b + 1) * self.batch_size]
+            yield b, order[b * self.batch_size:(b + 1) * self.batch_size]
+
+    def __iter__(self):
+        for b, batch in self.batches():
             yield self.sample(batch, b)
 
     def sample(self, batch, batch_idx=0):

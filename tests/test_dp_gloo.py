@@ -1,0 +1,68 @@
+"""Multi-process (world_size 2, gloo, CPU) checks of the data-parallel machinery of the
+neighbour-sampled path: batch dealing across ranks and the flat-bucket gradient all-reduce
+(regnn_hip.mag.flat_grad_allreduce, mag/regnn_ns.py:406-407)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _StubGraph:
+    def __init__(self, n):
+        self.n_dst, self.device = n, torch.device("cpu")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from regnn_hip.mag import flat_grad_allreduce
+    from regnn_hip.sampler import NeighborSampler
+    # 1. batch dealing: shared permutation, rank r takes global batches r, r+W, ...
+    smp = NeighborSampler(_StubGraph(1000), torch.arange(1000), [25, 20], batch_size=64,
+                          shuffle=True, seed=5, rank=rank, world_size=world)
+    smp.set_epoch(2)
+    mine = [(b, t.tolist()) for b, t in smp.batches()]
+    # 2. gradient all-reduce: each rank the mean loss of its half of a global batch
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(64, 8, generator=g)
+    Y = torch.randint(0, 3, (64,), generator=g)
+    part = slice(rank * 32, (rank + 1) * 32)
+    loss = torch.nn.functional.cross_entropy(model(X[part]), Y[part])
+    loss.backward()
+    flat_grad_allreduce(list(model.parameters()), world)
+    out[rank] = {"batches": mine, "grads": [p.grad.clone() for p in model.parameters()]}
+    dist.destroy_process_group()
+
+
+def test_dp_two_ranks():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b0, b1 = out[0]["batches"], out[1]["batches"]
+    assert all(b % 2 == 0 for b, _ in b0) and all(b % 2 == 1 for b, _ in b1)
+    nodes = [x for _, t in b0 + b1 for x in t]
+    assert sorted(nodes) == list(range(1000))            # disjoint cover of the train nodes
+    # single-process reference: mean loss over the whole global batch
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(64, 8, generator=g)
+    Y = torch.randint(0, 3, (64,), generator=g)
+    torch.nn.functional.cross_entropy(model(X), Y).backward()
+    for r in range(world):
+        for got, p in zip(out[r]["grads"], model.parameters()):
+            assert torch.allclose(got, p.grad, atol=1e-6, rtol=1e-5)
