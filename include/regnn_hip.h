@@ -35,8 +35,14 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change; currently 2). */
+/* ABI version (bumped on any signature change; currently 3). */
 int regnn_abi_version(void);
+
+/* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
+ * key 1: grid cap of the grid-stride gather kernels (0 = resident capacity from the occupancy
+ * API, the default; > 0 = fixed block count, at most 2048). Returns the previous value, -1 for
+ * an unknown key. */
+int64_t regnn_tune(int32_t key, int64_t value);
 
 /* Rows of the per-block relation-gradient slab that regnn_spmm_bwd / regnn_degree_bwd write
  * (one row of n_rel (x heads) floats per block); size the slab as rows * n_rel * heads floats. */

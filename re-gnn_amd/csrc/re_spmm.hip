@@ -10,6 +10,8 @@
 // UN*NV 16-byte loads in flight. Relation gradients go to lane-private LDS bins
 // [n_rel][256 threads] (no cross-lane traffic per edge, no atomics) and leave the block through a
 // fixed-order slab: bitwise reproducible.
+#include <mutex>
+
 #include "regnn_common.h"
 
 namespace regnn {
@@ -329,13 +331,13 @@ template <typename T, int LPR, int NV, bool BWD>
 int launch_spmm(SpmmArgs a, hipStream_t stream) {
     constexpr int GPB = kBlock / LPR;
     const size_t lds = (BWD && a.slab) ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
-    const int g1 = grid_for(a.n_seg, GPB);
+    const int g1 = grid_resident(spmm_main<T, LPR, NV, BWD>, a.n_seg, GPB, lds);
     a.slab_row0 = 0;
     hipLaunchKernelGGL((spmm_main<T, LPR, NV, BWD>), dim3(g1), dim3(kBlock), lds, stream, a);
     REGNN_LAUNCH_CHECK();
     if (a.split > 0 && a.n_chunk > 0) {
         a.slab_row0 = kMaxGrid;
-        const int g2 = grid_for(a.n_chunk, GPB);
+        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, BWD>, a.n_chunk, GPB, lds);
         hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, BWD>), dim3(g2), dim3(kBlock), lds, stream, a);
         REGNN_LAUNCH_CHECK();
         int64_t base_in = 0, final_base = -1;
@@ -456,13 +458,48 @@ rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
     if (lane == 0) out[k] = accumulate ? out[k] + s : s;
 }
 
+int64_t g_tune_grid_cap = 0;
+
+int resident_blocks(const void* kernel, size_t lds) {
+    struct Entry { const void* k; size_t lds; int blocks; };
+    static std::mutex mu;
+    static Entry cache[64];
+    static int n_cache = 0;
+    static int n_cu = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    for (int i = 0; i < n_cache; ++i)
+        if (cache[i].k == kernel && cache[i].lds == lds) return cache[i].blocks;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n_cu = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 4;
+    const int blocks = per_cu * n_cu;
+    if (n_cache < 64) cache[n_cache++] = {kernel, lds, blocks};
+    return blocks;
+}
+
 }  // namespace regnn
 
 using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 2; }
+int regnn_abi_version(void) { return 3; }
+
+int64_t regnn_tune(int32_t key, int64_t value) {
+    if (key == 1) {
+        const int64_t old = g_tune_grid_cap;
+        g_tune_grid_cap = value < 0 ? 0 : value;
+        return old;
+    }
+    return -1;
+}
 
 int64_t regnn_slab_rows(int64_t, int32_t) { return 2 * int64_t(kMaxGrid); }
 
@@ -555,7 +592,8 @@ int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table,
     if (split > 0 && n_long > 0 && (!long_ids || (rel_table && !long_cnt))) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (n_long == 0) split = 0;
-    hipLaunchKernelGGL(degree_kernel, dim3(grid_for(n_seg, kBlock)), dim3(kBlock), 0, stream, ptr,
+    hipLaunchKernelGGL(degree_kernel, dim3(grid_resident(degree_kernel, n_seg, kBlock, 0)),
+                       dim3(kBlock), 0, stream, ptr,
                        rel, rel_table, n_seg, power, split, deg, norm);
     REGNN_LAUNCH_CHECK();
     if (split > 0) {
@@ -576,7 +614,8 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
     if (n_seg == 0) return REGNN_OK;
     if (n_long == 0) split = 0;
     const size_t lds = size_t(n_rel) * kBlock * sizeof(float);
-    hipLaunchKernelGGL(degree_bwd_kernel, dim3(grid_for(n_seg, kBlock)), dim3(kBlock), lds, stream,
+    hipLaunchKernelGGL(degree_bwd_kernel, dim3(grid_resident(degree_bwd_kernel, n_seg, kBlock, lds)),
+                       dim3(kBlock), lds, stream,
                        ptr, rel, deg, g_norm, n_seg, power, n_rel, split, long_ids,
                        split > 0 ? n_long : 0, long_cnt, slab);
     REGNN_LAUNCH_CHECK();

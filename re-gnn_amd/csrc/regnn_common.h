@@ -67,6 +67,25 @@ inline int grid_for(int64_t units, int per_block) {
     return int(g < kMaxGrid ? g : kMaxGrid);
 }
 
+// Tuning knobs (regnn_tune): grid cap of the grid-stride gather kernels. 0 = the kernel's
+// resident capacity (occupancy API x CUs: every block in the first dispatch round, so the
+// grid-stride loop has no partial last round), > 0 = a fixed cap.
+extern int64_t g_tune_grid_cap;
+
+int resident_blocks(const void* kernel, size_t lds);   // blocks per CU x CUs, cached
+
+// grid for a grid-stride gather kernel: one round of resident blocks (<= kMaxGrid)
+template <typename K>
+inline int grid_resident(K kernel, int64_t units, int per_block, size_t lds) {
+    int64_t g = (units + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    int64_t cap = g_tune_grid_cap > 0 ? g_tune_grid_cap
+                                      : resident_blocks(reinterpret_cast<const void*>(kernel), lds);
+    if (cap > kMaxGrid) cap = kMaxGrid;
+    if (cap < 1) cap = kMaxGrid;
+    return int(g < cap ? g : cap);
+}
+
 }  // namespace regnn
 
 #define REGNN_LAUNCH_CHECK()                                        \

@@ -28,6 +28,7 @@ F32 = ctypes.c_float
 _SIG = {
     "regnn_abi_version": ([], ctypes.c_int),
     "regnn_slab_rows": ([I64, I32], I64),
+    "regnn_tune": ([I32, I64], I64),
     "regnn_degree": ([P, P, P, I64, F32, I32, P, I32, P, I32, P, P, P], ctypes.c_int),
     "regnn_degree_bwd": ([P, P, P, P, I64, F32, I32, I32, P, I32, P, P, P], ctypes.c_int),
     "regnn_spmm_fwd": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P, P, I32,
@@ -52,7 +53,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 2
+ABI_VERSION = 3
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")
