@@ -50,25 +50,45 @@ struct SpmmArgs {
     int32_t slab_row0;     // first slab row this launch writes
 };
 
-template <typename T, int LPR, int NV>
+// Backward per-edge dot products (SDDMM 'dot'), compile-time so the gather loop has no
+// run-time branches: MODE 0 forward; 1 backward without per-edge dots; 2 relation bins (slab);
+// 3 per-edge gradient; 4 both.
+enum { kFwd = 0, kBwd = 1, kBwdSlab = 2, kBwdEdge = 3, kBwdBoth = 4 };
+
+__device__ const float kOneF[1] = {1.f};
+__device__ const uint8_t kZeroU8[4] = {0, 0, 0, 0};
+
+template <typename T, int LPR, int NV, int MODE>
 struct Seg {
     static constexpr int EV = Vec<T>::N;
-    static constexpr int UN = NV >= 8 ? 1 : (8 / NV);
+    static constexpr bool BWD = MODE != kFwd;
+    static constexpr bool SLAB = MODE == kBwdSlab || MODE == kBwdBoth;
+    static constexpr bool EDGE = MODE == kBwdEdge || MODE == kBwdBoth;
+    // rows gathered per step: 8 x 16-byte loads in flight per lane (NV vectors per row)
+    static constexpr int UN0 = NV >= 8 ? 1 : (8 / NV);
+    static constexpr int UN = UN0 < LPR ? UN0 : LPR;
 
     __device__ __forceinline__ static int off(int q, int lane) { return (q * LPR + lane) * EV; }
 
-    __device__ __forceinline__ static void load_row(const T* row, int F, int lane,
-                                                    float (&v)[NV][EV]) {
+    // Branch-free: the address is clamped into the row and out-of-row lanes are zeroed with a
+    // select afterwards. A guarded load makes hipcc branch around it and wait vmcnt(0) right
+    // after, serialising every gather of the unrolled batch (seen in the ISA).
+    __device__ __forceinline__ static void load_raw(const T* row, int F, int lane, uint4 (&v)[NV]) {
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int o = off(q, lane);
-            if (o < F) {
-                Vec<T>::load(row + o, v[q]);
-            } else {
-#pragma unroll
-                for (int t = 0; t < EV; ++t) v[q][t] = 0.f;
-            }
+            const bool in = o < F;
+            const uint4 r = load16(row + (in ? o : 0));
+            v[q] = make_uint4(in ? r.x : 0u, in ? r.y : 0u, in ? r.z : 0u, in ? r.w : 0u);
         }
+    }
+
+    __device__ __forceinline__ static void load_row(const T* row, int F, int lane,
+                                                    float (&v)[NV][EV]) {
+        uint4 r[NV];
+        load_raw(row, F, lane, r);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) unpack<T>(r[q], v[q]);
     }
 
     __device__ __forceinline__ static float dot(const float (&a)[NV][EV], const float (&b)[NV][EV]) {
@@ -80,82 +100,79 @@ struct Seg {
         return s;
     }
 
-    // Accumulate edges [beg, end) of one segment into acc. BWD additionally forms the per-edge
-    // SDDMM dot <src[j], self> * in_scale[j] * os into the relation bins / edge_grad.
-    template <bool BWD>
+    // Accumulate edges [beg, end) (beg < end) of one segment into acc. The backward modes also
+    // form the per-edge dot <src[j], self> * in_scale[j] * os (relation bins / edge_grad).
+    //
+    // Per-edge metadata is software-pipelined over batches of LPR edges (one edge per lane): while
+    // batch b is gathered, the in_scale / relation-table lookups of batch b+1 (ids loaded one
+    // iteration earlier) and the id / relation loads of batch b+2 are in flight. Every load is
+    // unconditional: edge indices are clamped to the segment, absent optional arrays read one
+    // constant (kOneF / kZeroU8), and a batch tail is processed as a full step with weight 0 and
+    // the dot scale 0, so no run-time branch forces a vmcnt(0) inside the loop.
     __device__ __forceinline__ static void accumulate(const SpmmArgs& a, int beg, int end, int lane,
                                                       float os, const float (&sx)[NV][EV],
                                                       float (&acc)[NV][EV], float* bins, int tid) {
         const T* __restrict__ src = static_cast<const T*>(a.src);
         const int F = a.F;
+        const int last = end - 1;
+        const float* tabp = a.tab ? a.tab : kOneF;
+        const float* scp = a.in_scale ? a.in_scale : kOneF;
+        const float* ewp = a.edge_w ? a.edge_w : kOneF;
+        const uint8_t* relp = a.rel ? a.rel : kZeroU8;
+        const int tm = a.tab ? 0xff : 0, sm = a.in_scale ? -1 : 0;
+        const int em = a.edge_w ? -1 : 0, rm = a.rel ? -1 : 0;
+
+        int ec = min(beg + lane, last);
+        int j0 = a.idx[ec], r0 = relp[ec & rm];
+        float ew0 = ewp[ec & em];
+        float s0 = scp[j0 & sm], t0 = tabp[r0 & tm];
+        ec = min(beg + LPR + lane, last);
+        int j1 = a.idx[ec], r1 = relp[ec & rm];
+        float ew1 = ewp[ec & em];
         for (int e0 = beg; e0 < end; e0 += LPR) {
-            const int e = e0 + lane;
-            int j = 0, r = 0;
-            float w = 0.f, sj = 1.f;
-            if (e < end) {
-                j = a.idx[e];
-                float ww = 1.f;
-                if (a.rel) r = a.rel[e];
-                if (a.tab) ww = a.tab[r];
-                if (a.edge_w) ww *= a.edge_w[e];
-                if (a.in_scale) sj = a.in_scale[j];
-                w = ww * sj;
-            }
+            const float s1 = scp[j1 & sm], t1 = tabp[r1 & tm];        // lookups, batch b+1
+            const int e2 = min(e0 + 2 * LPR + lane, last);            // ids, batch b+2
+            const int j2 = a.idx[e2], r2 = relp[e2 & rm];
+            const float ew2 = ewp[e2 & em];
+            const bool live = e0 + lane < end;
+            const float w0 = live ? t0 * ew0 * s0 : 0.f;
+            const float d0 = live ? s0 * os : 0.f;                   // dot scale (backward)
             const int cnt = min(LPR, end - e0);
-            int k = 0;
-            for (; k + UN <= cnt; k += UN) {
+            for (int k = 0; k < cnt; k += UN) {
                 int jj[UN];
                 float wk[UN];
-                float v[UN][NV][EV];
+                uint4 raw[UN][NV];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) jj[u] = __shfl(j0, k + u, LPR);
+#pragma unroll
+                for (int u = 0; u < UN; ++u) load_raw(src + (int64_t)jj[u] * F, F, lane, raw[u]);
+#pragma unroll
+                for (int u = 0; u < UN; ++u) wk[u] = __shfl(w0, k + u, LPR);
 #pragma unroll
                 for (int u = 0; u < UN; ++u) {
-                    jj[u] = __shfl(j, k + u, LPR);
-                    wk[u] = __shfl(w, k + u, LPR);
-                }
+                    float v[NV][EV];
 #pragma unroll
-                for (int u = 0; u < UN; ++u) load_row(src + (int64_t)jj[u] * F, F, lane, v[u]);
-#pragma unroll
-                for (int u = 0; u < UN; ++u) {
+                    for (int q = 0; q < NV; ++q) unpack<T>(raw[u][q], v[q]);
 #pragma unroll
                     for (int q = 0; q < NV; ++q)
 #pragma unroll
-                        for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk[u], v[u][q][t], acc[q][t]);
-                    if constexpr (BWD) edge_dot(a, e0 + k + u, k + u, v[u], sx, sj, r, os, bins, tid, lane);
+                        for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk[u], v[q][t], acc[q][t]);
+                    if constexpr (SLAB || EDGE) {
+                        const float p = dot(v, sx) * __shfl(d0, k + u, LPR);
+                        if constexpr (SLAB) bins[__shfl(r0, k + u, LPR) * kBlock + tid] += p;
+                        if constexpr (EDGE) {
+                            const float sum = group_sum<LPR>(p);
+                            if (lane == 0 && k + u < cnt) a.edge_grad[e0 + k + u] = sum;
+                        }
+                    }
                 }
             }
-            for (; k < cnt; ++k) {
-                const int jj = __shfl(j, k, LPR);
-                const float wk = __shfl(w, k, LPR);
-                float v[NV][EV];
-                load_row(src + (int64_t)jj * F, F, lane, v);
-#pragma unroll
-                for (int q = 0; q < NV; ++q)
-#pragma unroll
-                    for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk, v[q][t], acc[q][t]);
-                if constexpr (BWD) edge_dot(a, e0 + k, k, v, sx, sj, r, os, bins, tid, lane);
-            }
-        }
-    }
-
-    __device__ __forceinline__ static void edge_dot(const SpmmArgs& a, int e, int k,
-                                                    const float (&v)[NV][EV],
-                                                    const float (&sx)[NV][EV], float sj, int r,
-                                                    float os, float* bins, int tid, int lane) {
-        if (!(a.slab || a.edge_grad)) return;
-        const float scale = __shfl(sj, k, LPR) * os;
-        const float p = dot(v, sx) * scale;
-        if (a.slab) {
-            const int rk = __shfl(r, k, LPR);
-            bins[rk * kBlock + tid] += p;
-        }
-        if (a.edge_grad) {
-            const float s = group_sum<LPR>(p);
-            if (lane == 0) a.edge_grad[e] = s;
+            j0 = j1; r0 = r1; ew0 = ew1; s0 = s1; t0 = t1;
+            j1 = j2; r1 = r2; ew1 = ew2;
         }
     }
 
     // y = os * acc + bias; backward node grad = <self, acc> + <g_i, y_i> / in_scale[i].
-    template <bool BWD>
     __device__ __forceinline__ static void epilogue(const SpmmArgs& a, int64_t seg, int lane,
                                                     float os, const float (&sx)[NV][EV],
                                                     float (&acc)[NV][EV]) {
@@ -205,15 +222,14 @@ __device__ __forceinline__ void bins_flush(float* bins, int n_rel, int tid, floa
     }
 }
 
-template <typename T, int LPR, int NV, bool BWD>
+template <typename T, int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV>;
+    using S = Seg<T, LPR, NV, MODE>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
-    const bool use_bins = BWD && a.slab;
-    if (use_bins) bins_zero(bins, a.n_rel, tid);
-    const bool need_self = BWD && (a.slab || a.edge_grad || a.node_grad);
+    if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
+    const bool need_self = S::SLAB || S::EDGE || (S::BWD && a.node_grad);
     for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < a.n_seg;
          seg += (int64_t)gridDim.x * GPB) {
         const int beg = a.ptr[seg], end = a.ptr[seg + 1];
@@ -222,22 +238,20 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
         float sx[NV][S::EV] = {};
         if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        S::template accumulate<BWD>(a, beg, end, lane, os, sx, acc, bins, tid);
-        S::template epilogue<BWD>(a, seg, lane, os, sx, acc);
+        if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
+        S::epilogue(a, seg, lane, os, sx, acc);
     }
-    if (use_bins) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
+    if constexpr (S::SLAB) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
 }
 
 // one group per chunk of a long segment: raw partial sums (fp32) -> chunk_partial
-template <typename T, int LPR, int NV, bool BWD>
+template <typename T, int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV>;
+    using S = Seg<T, LPR, NV, MODE>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
-    const bool use_bins = BWD && a.slab;
-    if (use_bins) bins_zero(bins, a.n_rel, tid);
-    const bool need_self = BWD && (a.slab || a.edge_grad || a.node_grad);
+    if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
     for (int64_t c = (int64_t)blockIdx.x * GPB + tid / LPR; c < a.n_chunk;
          c += (int64_t)gridDim.x * GPB) {
         const int l = a.chunk_long[c];
@@ -248,9 +262,10 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
         const int end = min(s1, beg + a.chunk);
         float acc[NV][S::EV] = {};
         float sx[NV][S::EV] = {};
-        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        if constexpr (S::SLAB || S::EDGE)
+            S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        S::template accumulate<BWD>(a, beg, end, lane, os, sx, acc, bins, tid);
+        if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
         float* part = a.chunk_partial + c * a.F;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -261,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
             }
         }
     }
-    if (use_bins) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
+    if constexpr (S::SLAB) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
 }
 
 // one level of the fixed-order tree over chunk partials: output row p = sum of input rows
@@ -300,12 +315,12 @@ partial_reduce(const float* __restrict__ in, const int32_t* __restrict__ sb, int
 }
 
 // one group per long segment: its fully reduced partial row, then the epilogue
-template <typename T, int LPR, int NV, bool BWD>
+template <typename T, int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_base) {
-    using S = Seg<T, LPR, NV>;
+    using S = Seg<T, LPR, NV, MODE>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
-    const bool need_self = BWD && a.node_grad;
+    const bool need_self = S::BWD && a.node_grad;
     for (int64_t l = (int64_t)blockIdx.x * GPB + tid / LPR; l < a.n_long;
          l += (int64_t)gridDim.x * GPB) {
         const int64_t seg = a.long_ids[l];
@@ -323,22 +338,23 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
             }
         }
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        S::template epilogue<BWD>(a, seg, lane, os, sx, acc);
+        S::epilogue(a, seg, lane, os, sx, acc);
     }
 }
 
-template <typename T, int LPR, int NV, bool BWD>
+template <typename T, int LPR, int NV, int MODE>
 int launch_spmm(SpmmArgs a, hipStream_t stream) {
+    using S = Seg<T, LPR, NV, MODE>;
     constexpr int GPB = kBlock / LPR;
-    const size_t lds = (BWD && a.slab) ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
-    const int g1 = grid_resident(spmm_main<T, LPR, NV, BWD>, a.n_seg, GPB, lds);
+    const size_t lds = S::SLAB ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
+    const int g1 = grid_resident(spmm_main<T, LPR, NV, MODE>, a.n_seg, GPB, lds);
     a.slab_row0 = 0;
-    hipLaunchKernelGGL((spmm_main<T, LPR, NV, BWD>), dim3(g1), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL((spmm_main<T, LPR, NV, MODE>), dim3(g1), dim3(kBlock), lds, stream, a);
     REGNN_LAUNCH_CHECK();
     if (a.split > 0 && a.n_chunk > 0) {
         a.slab_row0 = kMaxGrid;
-        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, BWD>, a.n_chunk, GPB, lds);
-        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, BWD>), dim3(g2), dim3(kBlock), lds, stream, a);
+        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, MODE>, a.n_chunk, GPB, lds);
+        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, MODE>), dim3(g2), dim3(kBlock), lds, stream, a);
         REGNN_LAUNCH_CHECK();
         int64_t base_in = 0, final_base = -1;
         for (int k = 0; k < a.n_levels; ++k) {
@@ -352,27 +368,38 @@ int launch_spmm(SpmmArgs a, hipStream_t stream) {
             final_base = base_out;
         }
         const int g3 = grid_for(a.n_long, GPB);
-        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, BWD>), dim3(g3), dim3(kBlock), 0, stream, a,
+        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, MODE>), dim3(g3), dim3(kBlock), 0, stream, a,
                            final_base);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
 }
 
+template <typename T, int LPR, int NV>
+int launch_mode(SpmmArgs a, int mode, hipStream_t stream) {
+    switch (mode) {
+        case kFwd: return launch_spmm<T, LPR, NV, kFwd>(a, stream);
+        case kBwd: return launch_spmm<T, LPR, NV, kBwd>(a, stream);
+        case kBwdSlab: return launch_spmm<T, LPR, NV, kBwdSlab>(a, stream);
+        case kBwdEdge: return launch_spmm<T, LPR, NV, kBwdEdge>(a, stream);
+        default: return launch_spmm<T, LPR, NV, kBwdBoth>(a, stream);
+    }
+}
+
 // (lanes per segment, vectors per lane) for a row of nvec 16-byte vectors
-template <typename T, bool BWD>
-int dispatch(SpmmArgs a, hipStream_t stream) {
+template <typename T>
+int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
     constexpr int EV = Vec<T>::N;
     if (a.F <= 0 || a.F % EV) return REGNN_EUNSUPPORTED;
     const int nvec = a.F / EV;
-    if (nvec <= 4) return launch_spmm<T, 4, 1, BWD>(a, stream);
-    if (nvec <= 8) return launch_spmm<T, 8, 1, BWD>(a, stream);
-    if (nvec <= 16) return launch_spmm<T, 16, 1, BWD>(a, stream);
-    if (nvec <= 32) return launch_spmm<T, 16, 2, BWD>(a, stream);
-    if (nvec <= 48) return launch_spmm<T, 16, 3, BWD>(a, stream);
-    if (nvec <= 64) return launch_spmm<T, 16, 4, BWD>(a, stream);
-    if (nvec <= 128) return launch_spmm<T, 64, 2, BWD>(a, stream);
-    if (nvec <= 256) return launch_spmm<T, 64, 4, BWD>(a, stream);
+    if (nvec <= 4) return launch_mode<T, 4, 1>(a, mode, stream);
+    if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
+    if (nvec <= 16) return launch_mode<T, 16, 1>(a, mode, stream);
+    if (nvec <= 32) return launch_mode<T, 16, 2>(a, mode, stream);
+    if (nvec <= 48) return launch_mode<T, 16, 3>(a, mode, stream);
+    if (nvec <= 64) return launch_mode<T, 16, 4>(a, mode, stream);
+    if (nvec <= 128) return launch_mode<T, 64, 2>(a, mode, stream);
+    if (nvec <= 256) return launch_mode<T, 64, 4>(a, mode, stream);
     return REGNN_EUNSUPPORTED;
 }
 
@@ -552,8 +579,8 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial,
                            level_sb, n_levels, level_desc);
     a.bias = bias; a.src = x; a.out = y;
-    if (dtype == REGNN_F32) return dispatch<float, false>(a, stream);
-    if (dtype == REGNN_BF16) return dispatch<bf16_t, false>(a, stream);
+    if (dtype == REGNN_F32) return dispatch<float>(a, kFwd, stream);
+    if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, kFwd, stream);
     return REGNN_EUNSUPPORTED;
 }
 
@@ -579,8 +606,9 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            level_sb, n_levels, level_desc);
     a.src = g; a.out = gx; a.self = x; a.ng_a = y ? g : nullptr; a.ng_b = y;
     a.slab = slab; a.n_rel = n_rel; a.edge_grad = edge_grad; a.node_grad = node_grad;
-    if (dtype == REGNN_F32) return dispatch<float, true>(a, stream);
-    if (dtype == REGNN_BF16) return dispatch<bf16_t, true>(a, stream);
+    const int mode = slab ? (edge_grad ? kBwdBoth : kBwdSlab) : (edge_grad ? kBwdEdge : kBwd);
+    if (dtype == REGNN_F32) return dispatch<float>(a, mode, stream);
+    if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, mode, stream);
     return REGNN_EUNSUPPORTED;
 }
 

@@ -54,6 +54,28 @@ template <> struct Vec<bf16_t> {
     }
 };
 
+// raw 16-byte vector load (kept packed in 4 VGPRs until use) and its widening to fp32
+__device__ __forceinline__ uint4 load16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+
+template <typename T>
+__device__ __forceinline__ void unpack(const uint4& r, float (&v)[Vec<T>::N]);
+
+template <>
+__device__ __forceinline__ void unpack<float>(const uint4& r, float (&v)[4]) {
+    v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y);
+    v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
+}
+
+template <>
+__device__ __forceinline__ void unpack<bf16_t>(const uint4& r, float (&v)[8]) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
