@@ -40,8 +40,9 @@ int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
  * key 1: grid cap of the grid-stride gather kernels (0 = resident capacity from the occupancy
- * API, the default; > 0 = fixed block count, at most 2048). Returns the previous value, -1 for
- * an unknown key. */
+ * API, the default; > 0 = fixed block count, at most 2048). key 2: rows gathered per lane per
+ * step for 16-vector rows (F=64 fp32 / F=128 bf16): 0 = default (8), 4 or 16. Returns the
+ * previous value, -1 for an unknown key. */
 int64_t regnn_tune(int32_t key, int64_t value);
 
 /* Rows of the per-block relation-gradient slab that regnn_spmm_bwd / regnn_degree_bwd write

@@ -58,14 +58,14 @@ enum { kFwd = 0, kBwd = 1, kBwdSlab = 2, kBwdEdge = 3, kBwdBoth = 4 };
 __device__ const float kOneF[1] = {1.f};
 __device__ const uint8_t kZeroU8[4] = {0, 0, 0, 0};
 
-template <typename T, int LPR, int NV, int MODE>
+template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false>
 struct Seg {
     static constexpr int EV = Vec<T>::N;
     static constexpr bool BWD = MODE != kFwd;
     static constexpr bool SLAB = MODE == kBwdSlab || MODE == kBwdBoth;
     static constexpr bool EDGE = MODE == kBwdEdge || MODE == kBwdBoth;
     // rows gathered per step: 8 x 16-byte loads in flight per lane (NV vectors per row)
-    static constexpr int UN0 = NV >= 8 ? 1 : (8 / NV);
+    static constexpr int UN0 = UNT > 0 ? UNT : (NV >= 8 ? 1 : (8 / NV));
     static constexpr int UN = UN0 < LPR ? UN0 : LPR;
 
     __device__ __forceinline__ static int off(int q, int lane) { return (q * LPR + lane) * EV; }
@@ -77,9 +77,13 @@ struct Seg {
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int o = off(q, lane);
-            const bool in = o < F;
-            const uint4 r = load16(row + (in ? o : 0));
-            v[q] = make_uint4(in ? r.x : 0u, in ? r.y : 0u, in ? r.z : 0u, in ? r.w : 0u);
+            if constexpr (FULL) {           // F == LPR * NV * EV: every lane is inside the row
+                v[q] = load16(row + o);
+            } else {
+                const bool in = o < F;
+                const uint4 r = load16(row + (in ? o : 0));
+                v[q] = make_uint4(in ? r.x : 0u, in ? r.y : 0u, in ? r.z : 0u, in ? r.w : 0u);
+            }
         }
     }
 
@@ -222,10 +226,10 @@ __device__ __forceinline__ void bins_flush(float* bins, int n_rel, int tid, floa
     }
 }
 
-template <typename T, int LPR, int NV, int MODE>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV, MODE>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
@@ -245,10 +249,10 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
 }
 
 // one group per chunk of a long segment: raw partial sums (fp32) -> chunk_partial
-template <typename T, int LPR, int NV, int MODE>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV, MODE>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
@@ -315,9 +319,9 @@ partial_reduce(const float* __restrict__ in, const int32_t* __restrict__ sb, int
 }
 
 // one group per long segment: its fully reduced partial row, then the epilogue
-template <typename T, int LPR, int NV, int MODE>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_base) {
-    using S = Seg<T, LPR, NV, MODE>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     const bool need_self = S::BWD && a.node_grad;
@@ -342,19 +346,19 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
     }
 }
 
-template <typename T, int LPR, int NV, int MODE>
+template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false>
 int launch_spmm(SpmmArgs a, hipStream_t stream) {
-    using S = Seg<T, LPR, NV, MODE>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
     constexpr int GPB = kBlock / LPR;
     const size_t lds = S::SLAB ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
-    const int g1 = grid_resident(spmm_main<T, LPR, NV, MODE>, a.n_seg, GPB, lds);
+    const int g1 = grid_resident(spmm_main<T, LPR, NV, MODE, UNT, FULL>, a.n_seg, GPB, lds);
     a.slab_row0 = 0;
-    hipLaunchKernelGGL((spmm_main<T, LPR, NV, MODE>), dim3(g1), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL((spmm_main<T, LPR, NV, MODE, UNT, FULL>), dim3(g1), dim3(kBlock), lds, stream, a);
     REGNN_LAUNCH_CHECK();
     if (a.split > 0 && a.n_chunk > 0) {
         a.slab_row0 = kMaxGrid;
-        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, MODE>, a.n_chunk, GPB, lds);
-        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, MODE>), dim3(g2), dim3(kBlock), lds, stream, a);
+        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, MODE, UNT, FULL>, a.n_chunk, GPB, lds);
+        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, MODE, UNT, FULL>), dim3(g2), dim3(kBlock), lds, stream, a);
         REGNN_LAUNCH_CHECK();
         int64_t base_in = 0, final_base = -1;
         for (int k = 0; k < a.n_levels; ++k) {
@@ -368,22 +372,31 @@ int launch_spmm(SpmmArgs a, hipStream_t stream) {
             final_base = base_out;
         }
         const int g3 = grid_for(a.n_long, GPB);
-        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, MODE>), dim3(g3), dim3(kBlock), 0, stream, a,
+        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, MODE, UNT, FULL>), dim3(g3), dim3(kBlock), 0, stream, a,
                            final_base);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
 }
 
-template <typename T, int LPR, int NV>
+template <typename T, int LPR, int NV, int UNT = 0, bool FULL = false>
 int launch_mode(SpmmArgs a, int mode, hipStream_t stream) {
     switch (mode) {
-        case kFwd: return launch_spmm<T, LPR, NV, kFwd>(a, stream);
-        case kBwd: return launch_spmm<T, LPR, NV, kBwd>(a, stream);
-        case kBwdSlab: return launch_spmm<T, LPR, NV, kBwdSlab>(a, stream);
-        case kBwdEdge: return launch_spmm<T, LPR, NV, kBwdEdge>(a, stream);
-        default: return launch_spmm<T, LPR, NV, kBwdBoth>(a, stream);
+        case kFwd: return launch_spmm<T, LPR, NV, kFwd, UNT, FULL>(a, stream);
+        case kBwd: return launch_spmm<T, LPR, NV, kBwd, UNT, FULL>(a, stream);
+        case kBwdSlab: return launch_spmm<T, LPR, NV, kBwdSlab, UNT, FULL>(a, stream);
+        case kBwdEdge: return launch_spmm<T, LPR, NV, kBwdEdge, UNT, FULL>(a, stream);
+        default: return launch_spmm<T, LPR, NV, kBwdBoth, UNT, FULL>(a, stream);
     }
+}
+
+// F = 16 vectors (F=64 fp32 / F=128 bf16), the BASELINE hidden size: exact fit (no lane masking)
+// and a tunable number of rows in flight per lane (regnn_tune key 2: 0 = 8, or 4 / 16)
+template <typename T>
+int launch_f16v(SpmmArgs a, int mode, hipStream_t stream) {
+    if (g_tune_un == 4) return launch_mode<T, 16, 1, 4, true>(a, mode, stream);
+    if (g_tune_un == 16) return launch_mode<T, 16, 1, 16, true>(a, mode, stream);
+    return launch_mode<T, 16, 1, 8, true>(a, mode, stream);
 }
 
 // (lanes per segment, vectors per lane) for a row of nvec 16-byte vectors
@@ -394,6 +407,7 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
     const int nvec = a.F / EV;
     if (nvec <= 4) return launch_mode<T, 4, 1>(a, mode, stream);
     if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
+    if (nvec == 16) return launch_f16v<T>(a, mode, stream);
     if (nvec <= 16) return launch_mode<T, 16, 1>(a, mode, stream);
     if (nvec <= 32) return launch_mode<T, 16, 2>(a, mode, stream);
     if (nvec <= 48) return launch_mode<T, 16, 3>(a, mode, stream);
@@ -486,6 +500,7 @@ rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
 }
 
 int64_t g_tune_grid_cap = 0;
+int64_t g_tune_un = 0;
 
 int resident_blocks(const void* kernel, size_t lds) {
     struct Entry { const void* k; size_t lds; int blocks; };
@@ -523,6 +538,11 @@ int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
         const int64_t old = g_tune_grid_cap;
         g_tune_grid_cap = value < 0 ? 0 : value;
+        return old;
+    }
+    if (key == 2) {
+        const int64_t old = g_tune_un;
+        g_tune_un = value;
         return old;
     }
     return -1;

@@ -93,6 +93,7 @@ inline int grid_for(int64_t units, int per_block) {
 // resident capacity (occupancy API x CUs: every block in the first dispatch round, so the
 // grid-stride loop has no partial last round), > 0 = a fixed cap.
 extern int64_t g_tune_grid_cap;
+extern int64_t g_tune_un;        // rows in flight per lane for F = 16 vectors (0 = 8)
 
 int resident_blocks(const void* kernel, size_t lds);   // blocks per CU x CUs, cached
 

@@ -37,19 +37,22 @@ def main():
     graphs = {}
     variants = []
     for v in args.variants.split(","):
-        cap, split, chunk = v.split(":")
+        parts = v.split(":")
+        cap, split, chunk = parts[:3]
+        un = int(parts[3]) if len(parts) > 3 else 0
         key = (int(split), int(chunk))
         if key not in graphs:
             graphs[key] = RelGraph(gd["src"], gd["dst"], gd["N"], dev, split=key[0], chunk=key[1])
-        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key]))
+        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key], un))
     E, N = graphs[next(iter(graphs))].E, gd["N"]
     F = args.F
     fwd_b = E * (F * s + 9) + N * (F * s + 8)
     bwd_b = E * (F * s + 9) + N * (3 * F * s + 12)
     res = {v[0]: {"fwd": [], "bwd": []} for v in variants}
     for r in range(args.rounds + 1):
-        for name, cap, rg in variants:
+        for name, cap, rg, un in variants:
             L._so.regnn_tune(1, cap)
+            L._so.regnn_tune(2, un)
             pack = rg.rel_pack(e_feat, 11)
             tab = torch.full((11, 1), 0.9, device=dev, requires_grad=True)
             x = x0.clone().requires_grad_(True)
@@ -65,6 +68,7 @@ def main():
                 res[name]["bwd"].append(st["spmm_bwd"][1])
             del x, y, norm
     L._so.regnn_tune(1, 0)
+    L._so.regnn_tune(2, 0)
     out = {}
     for name, d in res.items():
         f, b = statistics.median(d["fwd"]), statistics.median(d["bwd"])
