@@ -45,57 +45,123 @@ def setup_dist(n):
     return rank, world, torch.device("cuda", local)
 
 
-def build_workload(args, dev):
+def _full_graph(gd, dev):
     import dgl
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    return g, g.relgraph(dev), gd["rel"].to(torch.int64)
+
+
+def build_workload(args, dev):
+    """-> dict(step=callable, edges_per_step=int|callable, rg=RelGraph, kernels=[...], ...)."""
     from regnn_hip import nets, synth
     t0 = time.time()
-    if args.workload == "mag":
-        gd = synth.mag_like(args.scale, seed=0, device=dev)
-        dims = {t: 128 for t in synth.NTYPES}
-        feats = synth.type_features(gd["counts"], dims, seed=1, device=dev, kind="mag")
-        n_classes = 349
-        train_nodes = gd["counts"]["paper"]
-    else:
-        gd = synth.dblp_like(seed=0, device=dev)
-        feats = synth.type_features(gd["counts"], synth.DBLP_DIMS, seed=1, device=dev, kind="dblp")
-        n_classes = 4
-        train_nodes = gd["counts"]["A"]
-    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
-    e_feat = gd["rel"].to(torch.int64)
-    rg = g.relgraph(dev)
+    wl = args.workload
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
-    labels = torch.randint(0, n_classes, (train_nodes,), generator=gen, device=dev)
     torch.manual_seed(3)
-    net = nets.REGCN(g, gd["R"], 100.0, 64, 64, n_classes, 2, F.elu, args.dropout,
-                     [f.shape[1] for f in feats]).to(dev)
+    if wl in ("mag", "dblp"):
+        if wl == "mag":
+            gd = synth.mag_like(args.scale, seed=0, device=dev)
+            feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1,
+                                        device=dev, kind="mag")
+            n_classes, train_nodes = 349, gd["counts"]["paper"]
+        else:
+            gd = synth.dblp_like(seed=0, device=dev)
+            feats = synth.type_features(gd["counts"], synth.DBLP_DIMS, seed=1, device=dev,
+                                        kind="dblp")
+            n_classes, train_nodes = 4, gd["counts"]["A"]
+        g, rg, e_feat = _full_graph(gd, dev)
+        net = nets.REGCN(g, gd["R"], 100.0, 64, 64, n_classes, 2, F.elu, args.dropout,
+                         [f.shape[1] for f in feats]).to(dev)
+        convs, kern = 2, ("spmm_fwd", "spmm_bwd")
+    elif wl == "acm":
+        gd = synth.acm_like(seed=0, device=dev)
+        feats = synth.type_features(gd["counts"], synth.ACM_DIMS, seed=1, device=dev, kind="target")
+        n_classes, train_nodes = 3, gd["counts"]["P"]
+        g, rg, e_feat = _full_graph(gd, dev)
+        net = nets.REGAT(g, gd["R"], 100.0, 2, 64, 64, n_classes, [8, 8, 1], F.elu, args.dropout,
+                         args.dropout, 0.01, False, [f.shape[1] for f in feats]).to(dev)
+        convs, kern = 3, ("spmm_heads_fwd", "spmm_heads_bwd", "gat_softmax_fwd", "gat_softmax_bwd")
+    elif wl == "imdb":
+        gd = synth.imdb_like(seed=0, device=dev)
+        feats = synth.type_features(gd["counts"], synth.IMDB_DIMS, seed=1, device=dev, kind="target")
+        n_classes, train_nodes = 3, gd["counts"]["M"]
+        g, rg, e_feat = _full_graph(gd, dev)
+        net = nets.REMixHop(g, gd["R"], 100.0, 64, 64, n_classes, 2, [f.shape[1] for f in feats],
+                            input_dropout=args.dropout, activation=F.elu).to(dev)
+        convs, kern = 4, ("spmm_fwd", "spmm_bwd")        # 2 live hops x 2 layers
+    else:
+        return build_ns(args, dev, t0)
+    labels = torch.randint(0, n_classes, (train_nodes,), generator=gen, device=dev)
     opt = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=1e-3)
+
+    def step():
+        logits, _ = net(feats, e_feat)
+        # = F.cross_entropy(logits[train], y) (run_regnn.py:147); gather form: torch's nll_loss
+        # reduction is a single-block kernel (17 ms at 7.4M rows, profiled)
+        logp = F.log_softmax(logits[: labels.numel()], dim=1)
+        loss = -logp.gather(1, labels.unsqueeze(1)).mean()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+
     torch.cuda.synchronize()
-    log(f"[bench] {args.workload}: N={gd['N']:,} E={rg.E:,} R={gd['R']} built in "
-        f"{time.time() - t0:.1f}s; long rows csr={rg.csr_plan.n_long} csc={rg.csc_plan.n_long}")
-    return dict(g=g, rg=rg, net=net, opt=opt, feats=feats, e_feat=e_feat, labels=labels, gd=gd)
+    log(f"[bench] {wl}: N={gd['N']:,} E={rg.E:,} R={gd['R']} built in {time.time() - t0:.1f}s; "
+        f"long rows csr={rg.csr_plan.n_long} csc={rg.csc_plan.n_long}")
+    return dict(step=step, edges_per_step=convs * rg.E, rg=rg, R=gd["R"], kernels=kern,
+                convs=convs, N=rg.n_dst, E=rg.E)
 
 
-def train_step(w):
-    net, opt = w["net"], w["opt"]
-    logits, _ = net(w["feats"], w["e_feat"])
-    # = F.cross_entropy(logits[train], y) (run_regnn.py:147); gather form: torch's nll_loss
-    # reduction is a single-block kernel (17 ms at 7.4M rows, profiled)
-    logp = F.log_softmax(logits[: w["labels"].numel()], dim=1)
-    loss = -logp.gather(1, w["labels"].unsqueeze(1)).mean()
-    opt.zero_grad(set_to_none=True)
-    loss.backward()
-    opt.step()
-    return loss
+def build_ns(args, dev, t0):
+    """config 5: mag/regnn_ns.py REGCN neighbour-sampled training step (sample + fwd/bwd + Adam),
+    data-parallel over ranks with the flat-bucket gradient all-reduce."""
+    from regnn_hip import mag, synth
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.sampler import NeighborSampler
+    gd = synth.mag_like(args.scale, seed=0, device=dev)
+    keep = gd["rel"] <= 7                                  # the raw 7 edge types, no loops
+    src, dst = gd["src"][keep], gd["dst"][keep]
+    edge_type = (gd["rel"][keep].to(torch.int64) - 1)
+    rg = RelGraph(src, dst, gd["N"], dev)
+    node_type = gd["ntype"]
+    offs = torch.tensor([gd["type_offsets"][t] for t in synth.NTYPES], device=dev)
+    local_node_idx = torch.arange(gd["N"], device=dev) - offs[node_type]
+    feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1, device=dev)
+    x_dict = {k: f for k, f in enumerate(feats)}
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    torch.manual_seed(3)
+    model = mag.REGNN(128, 64, 349, 2, 10.0, args.dropout, {k: 128 for k in x_dict}, 7,
+                      use_norm="ln", self_loop_type=2).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    n_paper = gd["counts"]["paper"]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    y_global = torch.full((gd["N"], 1), -1, dtype=torch.int64, device=dev)
+    y_global[:n_paper, 0] = torch.randint(0, 349, (n_paper,), generator=gen, device=dev)
+    sampler = NeighborSampler(rg, torch.arange(n_paper, device=dev), [25, 20], args.batch,
+                              shuffle=True, seed=123, rank=rank, world_size=world)
+    state = {"it": iter(sampler), "epoch": 0, "edges": 0}
 
+    def step():
+        try:
+            batch = next(state["it"])
+        except StopIteration:
+            state["epoch"] += 1
+            sampler.set_epoch(state["epoch"])
+            state["it"] = iter(sampler)
+            batch = next(state["it"])
+        _, n_id, adjs = batch
+        state["edges"] += sum(a.edge_index.shape[1] + a.size[1] for a in adjs)  # + self loops
+        mag.train_step(model, opt, batch, x_dict, edge_type, node_type, local_node_idx,
+                       y_global, world)
 
-def spmm_bytes(E, N, F, s, kind):
-    """algorithmic HBM bytes of one launch: int32 idx, uint8 rel, fp32 norm."""
-    if kind == "spmm_fwd":      # gather row + idx 4 + rel 1 + norm[src] 4; ptr 8, norm 4, out row
-        return E * (F * s + 9) + N * (F * s + 8)
-    if kind == "spmm_bwd":      # gather g row + idx + rel + norm; per node x, g, out rows + misc
-        return E * (F * s + 9) + N * (3 * F * s + 12)
-    raise KeyError(kind)
+    torch.cuda.synchronize()
+    log(f"[bench] ns: N={gd['N']:,} E={rg.E:,} built in {time.time() - t0:.1f}s; "
+        f"{len(sampler)} batches/epoch/rank")
+    return dict(step=step, edges_per_step=lambda: state["edges"], reset=lambda: state.update(edges=0),
+                rg=rg, R=11, kernels=("spmm_fwd", "spmm_bwd"), convs=2, N=gd["N"], E=rg.E,
+                ns=True)
 
 
 def cpu_baseline(budget_s=20.0):
@@ -135,8 +201,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["mag", "dblp"], default="mag")
+    ap.add_argument("--workload", choices=["mag", "dblp", "acm", "imdb", "ns"], default="mag")
     ap.add_argument("--scale", type=float, default=10.0)
+    ap.add_argument("--batch", type=int, default=512, help="ns: target papers per rank")
     ap.add_argument("--dropout", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -147,8 +214,10 @@ def main():
     w = build_workload(args, dev)
     rg = w["rg"]
     for _ in range(args.warmup):
-        train_step(w)
+        w["step"]()
     torch.cuda.synchronize()
+    if "reset" in w:
+        w["reset"]()
 
     profile.enable(True)
     if world > 1:
@@ -156,29 +225,31 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        train_step(w)
+        w["step"]()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kstats = profile.summary()
     profile.enable(False)
+    eps = w["edges_per_step"]
+    edges = eps() if callable(eps) else eps * args.steps
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
+        e = torch.tensor([float(edges)], device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        edges = float(e.item())
     ms = elapsed / args.steps * 1e3
-    L = 2
-    value = world * L * rg.E / (ms / 1e3)
+    value = edges / elapsed if world > 1 else edges / elapsed
 
-    # dominant HIP kernel and its roofline
-    F_, s = 64, 4
-    cand = {k: v for k, v in kstats.items() if k in ("spmm_fwd", "spmm_bwd")}
+    # dominant HIP op (largest device time in the timed region) and its HBM roofline:
+    # achieved = algorithmic bytes of its launches / their HIP-event durations
+    cand = {k: v for k, v in kstats.items() if k in w["kernels"]}
     dom = max(cand, key=lambda k: cand[k][2])
-    launches, mean_ms, _ = cand[dom]
-    byts = spmm_bytes(rg.E, rg.n_dst, F_, s, dom)
-    achieved = byts / (mean_ms / 1e3) / 1e9
+    launches, mean_ms, total_ms, total_bytes = cand[dom]
+    achieved = total_bytes / (total_ms / 1e3) / 1e9
     # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/gpu_pmc.sh:
     # FETCH_SIZE and WRITE_SIZE in separate runs, calibrated on a 4 GiB copy), valid only for the
     # exact graph it was measured on
@@ -190,6 +261,15 @@ def main():
         if rec.get("graph") == {"N": rg.n_dst, "E": rg.E} and dom in rec:
             traffic = rec[dom]["bytes_per_launch"]
 
+    desc = {
+        "mag": f"REGCN 2-layer hidden=64 full-graph train step (input Linear, 2x REGraphConv "
+               f"fwd+bwd, out_lin 349 classes, CE, Adam) on mag_like(scale={args.scale})",
+        "dblp": "REGCN 2-layer hidden=64 full-graph train step on dblp_like (configs[1] shape)",
+        "acm": "REGAT 2-layer hidden=64 heads [8,8,1] (last layer twice) train step on acm_like",
+        "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 train step on imdb_like",
+        "ns": f"mag/regnn_ns.py REGCN-NS train step (sample [25,20] x {args.batch} papers/rank, "
+              f"group_input, 2x REGCNConv+LN, Adam, grad all-reduce) on mag_like(scale={args.scale})",
+    }[args.workload]
     result = {
         "metric": "aggregated edges/sec per GPU (REGCN fwd+bwd, hidden=64); % HBM roofline",
         "value": value,
@@ -202,26 +282,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (seeded ogbn-mag-shaped multi-relation graph, random features/labels)",
+        "data": "synthetic (seeded multi-relation graph of the BASELINE shape, random features/labels)",
         "config": {
-            "workload": (f"REGCN 2-layer hidden=64 full-graph train step (input Linear, "
-                         f"2x REGraphConv fwd+bwd, out_lin, CE, Adam) on mag_like(scale="
-                         f"{args.scale})" if args.workload == "mag" else
-                         "REGCN 2-layer hidden=64 full-graph train step on dblp_like"),
-            "nodes": rg.n_dst, "edges": rg.E, "relations": w["gd"]["R"], "layers": L,
-            "hidden": 64, "parallelism": f"replicas x{world}",
+            "workload": desc, "nodes": w["N"], "edges": w["E"], "relations": w["R"],
+            "conv_applications_per_step": w["convs"], "hidden": 64,
+            "parallelism": (f"data-parallel x{world} (RCCL grad all-reduce)" if w.get("ns")
+                            else f"replicas x{world}"),
         },
         "roofline": {
             "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "launch_ms": mean_ms, "launches": launches, "algorithmic_bytes_per_launch": byts,
+            "launch_ms": mean_ms, "launches": launches,
+            "algorithmic_bytes_per_launch": total_bytes / launches,
         },
         "kernels_ms": {k: round(v[1], 4) for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, desc = cpu_baseline()
+        v, sample = cpu_baseline()
         result["cpu_baseline"] = {"value": v, "unit": "edges/s", "cores": 1, "kind": "port",
-                                  "sample": desc + " (oracle/regnn_oracle.py numpy/scipy fp32)"}
+                                  "sample": sample + " (oracle/regnn_oracle.py numpy/scipy fp32)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

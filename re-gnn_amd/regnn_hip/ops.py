@@ -40,6 +40,16 @@ def _plan_args(plan, F, device):
             plan.n_levels, ctypes.cast(plan.level_desc, ctypes.c_void_p)), part
 
 
+def spmm_bytes(E, n_dst, n_src, F, s, kind):
+    """algorithmic HBM bytes of one SpMM launch: int32 ids, uint8 relation ids,
+    fp32 norms. fwd: gather row + id + rel + norm[src] per edge; ptr, norm, out row per node.
+    bwd: gather g row + id + rel + norm per edge; x, g, gx rows + ptr, norm, node grad per node
+    (the kernel also reads y when forming the norm gradient: not credited)."""
+    if kind == "spmm_fwd":
+        return E * (F * s + 9) + n_dst * (F * s + 8)
+    return E * (F * s + 9) + n_src * (3 * F * s + 12)
+
+
 def _flat_table(tab):
     return None if tab is None else tab.detach().reshape(-1).to(torch.float32).contiguous()
 
@@ -55,7 +65,7 @@ class _DegreeNorm(torch.autograd.Function):
         n_rel = t.numel() if t is not None else 0
         plan = rg.csr_plan
         cnt = pack.long_cnt(n_rel) if (t is not None and plan.n_long) else None
-        with timed("degree"):
+        with timed("degree", rg.E + rg.n_dst * 16):
             L.call("regnn_degree", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr if pack else None),
                    L.ptr(t), rg.n_dst, float(power), plan.split,
                    L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), n_rel, L.ptr(deg), L.ptr(norm),
@@ -74,7 +84,7 @@ class _DegreeNorm(torch.autograd.Function):
         plan = rg.csr_plan
         slab = _slab(n_rel, rg.device)
         cnt = pack.long_cnt(n_rel) if plan.n_long else None
-        with timed("degree_bwd"):
+        with timed("degree_bwd", rg.E + rg.n_dst * 16):
             L.call("regnn_degree_bwd", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr), L.ptr(deg),
                    L.ptr(g_norm.contiguous().float()), rg.n_dst, float(ctx.power), n_rel,
                    plan.split, L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), L.ptr(slab),
@@ -106,7 +116,8 @@ class _ReSpmm(torch.autograd.Function):
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
         t = _flat_table(tab)
         plan_args, part = _plan_args(rg.csr_plan, F, x.device)
-        with timed("spmm_fwd"):
+        with timed("spmm_fwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
+                                          "spmm_fwd")):
             L.call("regnn_spmm_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
                    L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
                    L.ptr(t), None, L.ptr(pre), L.ptr(post),
@@ -133,7 +144,8 @@ class _ReSpmm(torch.autograd.Function):
         elif need_pre:
             node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
         plan_args, part = _plan_args(rg.csc_plan, F, x.device)
-        with timed("spmm_bwd"):
+        with timed("spmm_bwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
+                                          "spmm_bwd")):
             L.call("regnn_spmm_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
                    L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
                    L.ptr(t), None, L.ptr(post), L.ptr(pre), L.ptr(gy), L.ptr(x),
@@ -216,7 +228,7 @@ class _GatAttention(torch.autograd.Function):
         H = el.shape[1]
         a = torch.empty(rg.E, H, dtype=torch.float32, device=el.device)
         t = None if ee_tab is None else ee_tab.detach().float().contiguous()
-        with timed("gat_softmax_fwd"):
+        with timed("gat_softmax_fwd", rg.E * (5 + 12 * H) + rg.n_dst * 8 * H):
             L.call("regnn_gat_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
                    L.ptr(pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
                    L.ptr(er), rg.n_dst, H, float(slope), L.ptr(a), L.stream())
@@ -234,7 +246,7 @@ class _GatAttention(torch.autograd.Function):
         ger = torch.empty_like(er)
         n_rel = t.shape[0] if t is not None else 0
         slab = _slab(n_rel * H, el.device) if (t is not None and ctx.needs_input_grad[2]) else None
-        with timed("gat_softmax_bwd"):
+        with timed("gat_softmax_bwd", rg.E * (5 + 16 * H) + rg.n_dst * 12 * H):
             L.call("regnn_gat_softmax_bwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
                    L.ptr(ctx.pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
                    L.ptr(er), L.ptr(a), L.ptr(ga), rg.n_dst, H, float(ctx.slope), L.ptr(gs),
@@ -258,7 +270,8 @@ class _HeadSpmm(torch.autograd.Function):
         ft = ft.contiguous()
         a = a.contiguous().float()
         y = torch.empty(rg.n_dst, H, D, dtype=ft.dtype, device=ft.device)
-        with timed("spmm_heads_fwd"):
+        s_ = ft.element_size()
+        with timed("spmm_heads_fwd", rg.E * (H * D * s_ + 4 * H + 4) + rg.n_dst * (H * D * s_ + 4)):
             L.call("regnn_spmm_heads_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), None, L.ptr(a),
                    L.ptr(ft), L.ptr(y), rg.n_dst, H, D, L.dtype_code(ft), L.stream())
         ctx.rg = rg
@@ -273,7 +286,9 @@ class _HeadSpmm(torch.autograd.Function):
         gy = gy.contiguous().to(ft.dtype)
         gft = torch.empty_like(ft)
         ga = torch.empty_like(a)
-        with timed("spmm_heads_bwd"):
+        s_ = ft.element_size()
+        with timed("spmm_heads_bwd",
+                   rg.E * (H * D * s_ + 8 * H + 8) + rg.n_src * (2 * H * D * s_ + 4)):
             L.call("regnn_spmm_heads_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
                    L.ptr(rg.csc2csr), L.ptr(a), L.ptr(gy), L.ptr(ft), L.ptr(gft), L.ptr(ga),
                    rg.n_src, H, D, L.dtype_code(ft), L.stream())

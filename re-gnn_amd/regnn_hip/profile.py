@@ -19,7 +19,8 @@ def enable(on=True):
 
 
 @contextlib.contextmanager
-def timed(name):
+def timed(name, nbytes=0):
+    """nbytes = the launch's ALGORITHMIC HBM bytes (SURVEY.md §8d accounting), for the roofline."""
     if not _enabled:
         yield
         return
@@ -28,13 +29,13 @@ def timed(name):
     s.record()
     yield
     e.record()
-    _events.setdefault(name, []).append((s, e))
+    _events.setdefault(name, []).append((s, e, nbytes))
 
 
 def summary():
-    """{name: (launches, mean_ms, total_ms)} — call after torch.cuda.synchronize()."""
+    """{name: (launches, mean_ms, total_ms, total_bytes)} — call after torch.cuda.synchronize()."""
     out = {}
     for name, evs in _events.items():
-        ms = [s.elapsed_time(e) for s, e in evs]
-        out[name] = (len(ms), sum(ms) / len(ms), sum(ms))
+        ms = [s.elapsed_time(e) for s, e, _ in evs]
+        out[name] = (len(ms), sum(ms) / len(ms), sum(ms), sum(b for _, _, b in evs))
     return out

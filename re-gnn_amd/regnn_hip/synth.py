@@ -108,6 +108,55 @@ def dblp_like(seed=0, device="cuda"):
                 N=N, R=10, counts=dict(DBLP_NODES), type_offsets=off)
 
 
+def _bipartite_hetero(spec, counts, seed, device):
+    """node types in `counts` order; spec = [(src type, dst type, n_edges, one_per_src)];
+    relation ids: 2k+1 for spec k forward, 2k+2 reversed; self loops num_etype + ntype + 1."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    order = list(counts)
+    off, o = {}, 0
+    for t in order:
+        off[t] = o
+        o += counts[t]
+    N = o
+    srcs, dsts, rels = [], [], []
+    for k, (st, dt, m, one) in enumerate(spec):
+        a = (torch.arange(counts[st], device=device) if one else
+             torch.randint(0, counts[st], (m,), generator=gen, device=device)) + off[st]
+        b = torch.randint(0, counts[dt], (a.numel(),), generator=gen, device=device) + off[dt]
+        srcs += [a, b]; dsts += [b, a]
+        rels += [torch.full((a.numel(),), 2 * k + 1, dtype=torch.uint8, device=device),
+                 torch.full((a.numel(),), 2 * k + 2, dtype=torch.uint8, device=device)]
+    n_et = 2 * len(spec)
+    ntype = torch.cat([torch.full((counts[t],), i, dtype=torch.int64, device=device)
+                       for i, t in enumerate(order)])
+    loops = torch.arange(N, device=device)
+    srcs.append(loops); dsts.append(loops)
+    rels.append((n_et + 1 + ntype).to(torch.uint8))
+    return dict(src=torch.cat(srcs), dst=torch.cat(dsts), rel=torch.cat(rels), ntype=ntype, N=N,
+                R=n_et + len(order), counts=dict(counts), type_offsets=off)
+
+
+ACM_NODES = {"P": 4_019, "A": 7_167, "S": 60}
+ACM_DIMS = {"P": 1_902, "A": 10, "S": 10}
+IMDB_NODES = {"M": 4_278, "D": 2_081, "A": 5_257}
+IMDB_DIMS = {"M": 3_066, "D": 10, "A": 10}
+
+
+def acm_like(seed=0, device="cuda"):
+    """ACM shape: P-A 13,407 and P-S (one subject per paper), both
+    directions + self loops, R = 4 + 3 = 7."""
+    return _bipartite_hetero([("P", "A", 13_407, False), ("P", "S", 4_019, True)], ACM_NODES,
+                             seed, device)
+
+
+def imdb_like(seed=0, device="cuda"):
+    """IMDB shape: M-D (one director per movie) and M-A 12,828, both
+    directions + self loops, R = 4 + 3 = 7."""
+    return _bipartite_hetero([("M", "D", 4_278, True), ("M", "A", 12_828, False)], IMDB_NODES,
+                             seed, device)
+
+
 def type_features(counts, dims, seed=1, device="cuda", kind="mag"):
     """per-type dense input features (feats_type 3 for mag: paper N(0,1), others U(-0.5,0.5))."""
     gen = torch.Generator(device=device)
@@ -120,6 +169,9 @@ def type_features(counts, dims, seed=1, device="cuda", kind="mag"):
                 f = torch.randn(n, d, generator=gen, device=device)
             else:
                 f = torch.rand(n, d, generator=gen, device=device) - 0.5
+        elif kind == "target":   # feats_type 1: target type bag-of-words, zeros(10) for others
+            f = ((torch.rand(n, d, generator=gen, device=device) < 0.01).float() if i == 0
+                 else torch.zeros(n, d, device=device))
         else:  # dblp: binary bag-of-words A/P, gaussian T, identity V (utils/data.py:163-167)
             if t in ("A", "P"):
                 f = (torch.rand(n, d, generator=gen, device=device) < 0.01).float()
