@@ -93,7 +93,8 @@ def build_workload(args, dev):
     else:
         return build_ns(args, dev, t0)
     labels = torch.randint(0, n_classes, (train_nodes,), generator=gen, device=dev)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=1e-3)
+    # capturable: Adam's step counters live on the device so the step can be HIP-graph captured
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=1e-3, capturable=True)
 
     def step():
         logits, _ = net(feats, e_feat)
@@ -109,7 +110,7 @@ def build_workload(args, dev):
     log(f"[bench] {wl}: N={gd['N']:,} E={rg.E:,} R={gd['R']} built in {time.time() - t0:.1f}s; "
         f"long rows csr={rg.csr_plan.n_long} csc={rg.csc_plan.n_long}")
     return dict(step=step, edges_per_step=convs * rg.E, rg=rg, R=gd["R"], kernels=kern,
-                convs=convs, N=rg.n_dst, E=rg.E)
+                convs=convs, N=rg.n_dst, E=rg.E, opt=opt)
 
 
 def build_ns(args, dev, t0):
@@ -205,6 +206,9 @@ def main():
     ap.add_argument("--scale", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=512, help="ns: target papers per rank")
     ap.add_argument("--dropout", type=float, default=0.5)
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="capture the whole train step in a HIP graph and replay it "
+                         "(auto: on for the launch-bound small graphs dblp/acm/imdb)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -213,25 +217,54 @@ def main():
 
     w = build_workload(args, dev)
     rg = w["rg"]
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.workload in ("dblp", "acm", "imdb"))
+    if use_graph and w.get("ns"):
+        raise SystemExit("--graph: the sampled path has data-dependent shapes (not capturable)")
     for _ in range(args.warmup):
         w["step"]()
     torch.cuda.synchronize()
     if "reset" in w:
         w["reset"]()
+    kstats = None
+    run = w["step"]
+    if use_graph:
+        # per-op device times from eager profiled steps (events cannot sit inside a graph)
+        profile.enable(True)
+        for _ in range(min(args.steps, 10)):
+            w["step"]()
+        torch.cuda.synchronize()
+        kstats = profile.summary()
+        profile.enable(False)
+        # capture one full train step (fwd + bwd + Adam) on a side stream, replay it K times
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                w["step"]()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            w["step"]()
+        torch.cuda.synchronize()
+        run = graph.replay
+        run()
+        torch.cuda.synchronize()
 
-    profile.enable(True)
+    if not use_graph:
+        profile.enable(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        w["step"]()
+        run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kstats = profile.summary()
-    profile.enable(False)
+    if not use_graph:
+        kstats = profile.summary()
+        profile.enable(False)
     eps = w["edges_per_step"]
     edges = eps() if callable(eps) else eps * args.steps
     if world > 1:
@@ -288,6 +321,7 @@ def main():
             "conv_applications_per_step": w["convs"], "hidden": 64,
             "parallelism": (f"data-parallel x{world} (RCCL grad all-reduce)" if w.get("ns")
                             else f"replicas x{world}"),
+            "hip_graph": use_graph,
         },
         "roofline": {
             "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
