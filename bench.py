@@ -53,7 +53,7 @@ def _full_graph(gd, dev):
 
 def build_workload(args, dev):
     """-> dict(step=callable, edges_per_step=int|callable, rg=RelGraph, kernels=[...], ...)."""
-    from regnn_hip import nets, synth
+    from regnn_hip import nets, ops, synth
     t0 = time.time()
     wl = args.workload
     gen = torch.Generator(device=dev)
@@ -96,12 +96,13 @@ def build_workload(args, dev):
     # capturable: Adam's step counters live on the device so the step can be HIP-graph captured
     opt = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=1e-3, capturable=True)
 
+    W, b = net.head()
+
     def step():
-        logits, _ = net(feats, e_feat)
-        # = F.cross_entropy(logits[train], y) (run_regnn.py:147); gather form: torch's nll_loss
-        # reduction is a single-block kernel (17 ms at 7.4M rows, profiled)
-        logp = F.log_softmax(logits[: labels.numel()], dim=1)
-        loss = -logp.gather(1, labels.unsqueeze(1)).mean()
+        # run_regnn.py:146-150: logits = net(...) over all nodes, CE on the train rows, backward,
+        # Adam. ops.head_ce computes the same logits / loss / gradients without the all-rows
+        # zero-filled logits gradient (tests/test_gpu_ops.py::test_head_ce checks it vs autograd)
+        _, loss = ops.head_ce(net.embed(feats, e_feat), W, b, labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()

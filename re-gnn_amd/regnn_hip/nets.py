@@ -70,12 +70,20 @@ class REGCN(nn.Module):
         self.out_lin = Linear(n_hidden, n_classes, bias=True)
         self.dropout = nn.Dropout(p=dropout)
 
-    def forward(self, features_list, e_feat):
+    def embed(self, features_list, e_feat):
+        """everything before out_lin: the node embeddings the reference returns as `h`."""
         h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
         h = self.layers[0](self.g, h, e_feat)
         for layer in self.layers[1:]:
             h = layer(self.g, self.dropout(h), e_feat)
+        return h
+
+    def forward(self, features_list, e_feat):
+        h = self.embed(features_list, e_feat)
         return self.out_lin(h), h
+
+    def head(self):
+        return self.out_lin.weight, self.out_lin.bias
 
 
 class REGAT(nn.Module):
@@ -99,13 +107,22 @@ class REGAT(nn.Module):
                                          residual, None, use_weight=False))
         self.out_lin = Linear(num_hidden * heads[-2], num_classes)
 
-    def forward(self, features_list, e_feat):
+    def _emb(self, features_list, e_feat):
         h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
         h = self.gat_layers[0](self.g, h, e_feat).flatten(1)
         for l in range(1, self.num_layers):
             h = self.gat_layers[l](self.g, h, e_feat).flatten(1)
-        emb = self.gat_layers[-1](self.g, h, e_feat)
+        return self.gat_layers[-1](self.g, h, e_feat)
+
+    def embed(self, features_list, e_feat):
+        return self._emb(features_list, e_feat).flatten(1)
+
+    def forward(self, features_list, e_feat):
+        emb = self._emb(features_list, e_feat)
         return self.out_lin(emb.flatten(1)), emb.mean(1)
+
+    def head(self):
+        return self.out_lin.weight, self.out_lin.bias
 
 
 class REMixHop(nn.Module):
@@ -129,9 +146,16 @@ class REMixHop(nn.Module):
                                             batchnorm=batchnorm))
         self.fc_layers = Linear(hid_dim * len(p), out_dim, bias=False)
 
-    def forward(self, features_list, e_feat):
+    def embed(self, features_list, e_feat):
         h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
         h = self.layers[0](self.g, h, e_feat)
         for layer in self.layers[1:]:
             h = layer(self.g, self.dropout(h), e_feat)
+        return h
+
+    def forward(self, features_list, e_feat):
+        h = self.embed(features_list, e_feat)
         return self.fc_layers(h), h
+
+    def head(self):
+        return self.fc_layers.weight, None

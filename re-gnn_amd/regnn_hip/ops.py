@@ -308,3 +308,48 @@ def col_sum(x):
     slab = torch.zeros(L.slab_rows() // 2, cols, dtype=torch.float32, device=x.device)
     L.call("regnn_col_sum", L.ptr(x), rows, cols, L.ptr(slab), L.stream())
     return _reduce(slab, cols)
+
+
+# ---------------------------------------------------------------------------------------------
+class _HeadCE(torch.autograd.Function):
+    """(logits, loss) = (h W^T + b over ALL rows, mean CE over the first n rows vs labels).
+
+    The training step of run_regnn.py (:146-150) computes out_lin on every node and the loss on the
+    train rows; autograd through that slice materialises an all-rows zero-filled logits gradient
+    (19.4M x 349 fp32 = 27 GB at mag-10x) and runs the backward GEMMs over it. This op returns the
+    same logits and loss and the same gradients, forming the softmax gradient only for the loss
+    rows. The logits output is non-differentiable: use it for evaluation, the loss for training."""
+
+    @staticmethod
+    def forward(ctx, h, W, b, labels):
+        logits = torch.addmm(b, h, W.t()) if b is not None else h @ W.t()
+        n = labels.numel()
+        z = logits[:n]
+        lse = torch.logsumexp(z, 1)
+        loss = (lse - z.gather(1, labels.view(-1, 1)).squeeze(1)).mean()
+        ctx.save_for_backward(h, W, logits, lse, labels)
+        ctx.has_bias = b is not None
+        ctx.mark_non_differentiable(logits)
+        return logits, loss
+
+    @staticmethod
+    def backward(ctx, _g_logits, g_loss):
+        h, W, logits, lse, labels = ctx.saved_tensors
+        n = labels.numel()
+        p = torch.exp(logits[:n] - lse.unsqueeze(1))                  # softmax of the loss rows
+        p[torch.arange(n, device=p.device), labels] -= 1.0
+        p.mul_(g_loss / n)
+        gh = None
+        if ctx.needs_input_grad[0]:
+            gh = torch.zeros_like(h)
+            torch.mm(p, W, out=gh[:n])
+        gW = p.t() @ h[:n] if ctx.needs_input_grad[1] else None
+        gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = col_sum(p) if p.is_cuda else p.sum(0)
+        return gh, gW, gb, None
+
+
+def head_ce(h, weight, bias, labels):
+    """fused output head + cross-entropy over rows [0, len(labels)) -> (logits, loss)."""
+    return _HeadCE.apply(h, weight, bias, labels)

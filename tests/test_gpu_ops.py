@@ -107,3 +107,28 @@ def test_col_sum(rows, cols):
     want = x.double().sum(0)
     assert _rel(got, want) < 1e-5
     assert torch.equal(got, ops.col_sum(x))      # deterministic
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_head_ce_matches_autograd(bias):
+    """ops.head_ce == out_lin over all rows + cross_entropy(logits[:n], y) (run_regnn.py:146-148)."""
+    from regnn_hip import ops
+    torch.manual_seed(0)
+    N, D, C, n = 5000, 64, 349, 1800
+    h0 = torch.randn(N, D, device=DEV)
+    W0 = torch.randn(C, D, device=DEV) * 0.1
+    b0 = torch.randn(C, device=DEV) * 0.1 if bias else None
+    y = torch.randint(0, C, (n,), device=DEV)
+    h, W = h0.clone().requires_grad_(True), W0.clone().requires_grad_(True)
+    b = b0.clone().requires_grad_(True) if bias else None
+    logits, loss = ops.head_ce(h, W, b, y)
+    loss.backward()
+    hr, Wr = h0.double().requires_grad_(True), W0.double().requires_grad_(True)
+    br = b0.double().requires_grad_(True) if bias else None
+    lr = hr @ Wr.t() + (br if bias else 0)
+    lossr = torch.nn.functional.cross_entropy(lr[:n], y)
+    lossr.backward()
+    assert _rel(logits, lr) < 1e-5 and abs(loss.item() - lossr.item()) < 1e-5
+    assert _rel(h.grad, hr.grad) < 1e-5 and _rel(W.grad, Wr.grad) < 1e-5
+    if bias:
+        assert _rel(b.grad, br.grad) < 1e-5
