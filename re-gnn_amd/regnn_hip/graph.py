@@ -22,6 +22,16 @@ FANIN = 64       # chunk partials summed per node of the reduction tree
 class SegPlan:
     """Long-segment split plan for one orientation (see regnn_spmm_fwd in regnn_hip.h)."""
 
+    @classmethod
+    def none(cls):
+        """plan of an orientation whose segments are known to be short (no host sync)."""
+        plan = cls.__new__(cls)
+        plan.split, plan.chunk, plan.n_long = 0, CHUNK, 0
+        plan.long_ids = plan.chunk_long = plan.chunk_off = None
+        plan.n_chunk = plan.n_levels = plan.partial_rows = 0
+        plan.level_sb, plan.level_desc = None, None
+        return plan
+
     def __init__(self, ptr, split=SPLIT, chunk=CHUNK):
         deg = (ptr[1:] - ptr[:-1]).to(torch.int64)
         long_ids = torch.nonzero(deg > split).flatten()

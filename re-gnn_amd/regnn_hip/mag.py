@@ -12,7 +12,7 @@ import torch.nn.functional as F
 from torch.nn import Linear, ModuleDict, ModuleList, Parameter, init
 
 from . import ops
-from .graph import RelGraph
+from .graph import RelGraph, SegPlan
 
 
 def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_types,
@@ -29,6 +29,52 @@ def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_t
     rg = RelGraph(src, dst, n_src, src.device, num_dst=n_dst)
     pack = rg.rel_pack(et + 1)
     return rg, pack
+
+
+class _Block:
+    """CSR/CSC of one sampled block built from the sampler's dst-major output without sorting the
+    CSR side and with host syncs only for the CSC long-segment plan (RelGraph-compatible for
+    ops.re_spmm). Self loops are placed last in every target row (mag/regnn_layers.py:90-96)."""
+
+    def __init__(self, adj, edge_type, target_node_type, num_edge_types):
+        (ei, _, (n_src, n_dst)) = adj.edge_index, adj.e_id, adj.size
+        src_l, dst_l = ei[0], ei[1]
+        dev = src_l.device
+        M = src_l.numel()
+        self.device, self.n_src, self.n_dst, self.E = dev, n_src, n_dst, M + n_dst
+        cnt = adj.counts.to(torch.int64) + 1
+        ptr = torch.zeros(n_dst + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(cnt, 0, out=ptr[1:])
+        posn = torch.arange(M, device=dev) + dst_l          # rows keep the sampled order
+        loop_pos = ptr[1:] - 1
+        ar = torch.arange(n_dst, device=dev)
+        idx = torch.empty(self.E, dtype=torch.int64, device=dev)
+        idx[posn] = src_l
+        idx[loop_pos] = ar
+        dst_all = torch.empty_like(idx)
+        dst_all[posn] = dst_l
+        dst_all[loop_pos] = ar
+        rel = torch.empty(self.E, dtype=torch.uint8, device=dev)
+        rel[posn] = edge_type.to(torch.uint8)
+        rel[loop_pos] = (target_node_type + num_edge_types).to(torch.uint8)
+        self.csr_ptr = ptr.to(torch.int32)
+        self.csr_idx = idx.to(torch.int32)
+        perm = torch.sort(idx, stable=True)[1]
+        self.csc_idx = dst_all[perm].to(torch.int32)
+        ccnt = torch.zeros(n_src, dtype=torch.int64, device=dev).index_add_(
+            0, idx, torch.ones_like(idx))
+        cptr = torch.zeros(n_src + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(ccnt, 0, out=cptr[1:])
+        self.csc_ptr = cptr.to(torch.int32)
+        self.csr_plan = SegPlan.none()                       # rows <= fan-out + 1
+        self.csc_plan = SegPlan(self.csc_ptr)
+        self.pack = type("BlockPack", (), {})()
+        self.pack.rel_csr = rel
+        self.pack.rel_csc = rel[perm].contiguous()
+        self._inv = (1.0 / cnt.to(torch.float32)).contiguous()
+
+    def inv_in_count(self):
+        return self._inv
 
 
 class REGCNConv(torch.nn.Module):
@@ -112,13 +158,35 @@ class REGNN(torch.nn.Module):
             self.norm = torch.nn.BatchNorm1d(hidden_channels)
 
     def group_input(self, x_dict, node_type, local_node_idx, n_id=None):
+        """mag/regnn_ns.py:300-326. When every type has the same feature width the per-type
+        Linear is one GEMM against all types' weights + a per-node pick (no boolean-mask syncs);
+        each node still gets exactly its own type's projection."""
         if n_id is not None:
             node_type, local_node_idx = node_type[n_id], local_node_idx[n_id]
+        keys = sorted(x_dict)
+        dims = {x_dict[k].shape[1] for k in keys}
+        if len(dims) == 1 and keys == list(range(len(keys))):
+            table, offs = self._feature_table(x_dict, keys)
+            X = table[offs[node_type] + local_node_idx]
+            Wc = torch.cat([self.lins[str(k)].weight for k in keys], 0)
+            bc = torch.cat([self.lins[str(k)].bias for k in keys], 0)
+            Y = torch.addmm(bc, X, Wc.t()).view(X.shape[0], len(keys), self.hidden_dim)
+            return Y[torch.arange(X.shape[0], device=X.device), node_type]
         h = torch.zeros(node_type.numel(), self.hidden_dim, device=node_type.device)
         for key, x in x_dict.items():
             mask = node_type == key
             h[mask] = self.lins[str(key)](x[local_node_idx[mask]])
         return h
+
+    def _feature_table(self, x_dict, keys):
+        sig = tuple((k, x_dict[k].data_ptr(), x_dict[k].shape[0]) for k in keys)
+        cache = getattr(self, "_ftab", None)
+        if cache is None or cache[0] != sig:
+            table = torch.cat([x_dict[k] for k in keys], 0)
+            sizes = torch.tensor([0] + [x_dict[k].shape[0] for k in keys[:-1]])
+            offs = torch.cumsum(sizes, 0).to(table.device)
+            self._ftab = cache = (sig, table, offs)
+        return cache[1], cache[2]
 
     def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
         x = self.group_input(x_dict, node_type, local_node_idx, n_id)
@@ -127,7 +195,11 @@ class REGNN(torch.nn.Module):
             edge_index, e_id, size = adj
             x_target = x[:size[1]]
             ntype = ntype[:size[1]]
-            x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
+            if getattr(adj, "counts", None) is not None and self.self_loop_type == 2:
+                blk = _Block(adj, edge_type[e_id], ntype, self.num_edge_types)
+                x = self.convs[i]((x, x_target), (blk, blk.pack))
+            else:
+                x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
             x = F.relu(x)
             x = F.dropout(x, p=self.dropout, training=self.training)
         return self.out_lin(x).log_softmax(dim=-1)

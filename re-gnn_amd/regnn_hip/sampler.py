@@ -34,8 +34,9 @@ class Adj:
     edge_index = [src_local, dst_local] (dst-major: rows already grouped by target),
     e_id = original edge ids, size = (n_src, n_dst); ``rel`` = 0-based relation of every edge."""
 
-    def __init__(self, edge_index, e_id, size, csr_pos):
+    def __init__(self, edge_index, e_id, size, csr_pos, counts=None):
         self.edge_index, self.e_id, self.size, self.csr_pos = edge_index, e_id, size, csr_pos
+        self.counts = counts       # sampled in-edges per target (int32), dst-major order
 
     def __iter__(self):
         return iter((self.edge_index, self.e_id, self.size))
@@ -99,9 +100,9 @@ class NeighborSampler:
         for hop, k in enumerate(self.sizes):
             seed = hop_seed(self.seed, self.epoch, batch_idx, hop)
             n_dst = n_id.numel()
-            n_id, src_l, dst_l, pos = self.sample_hop(n_id, k, seed)
+            n_id, src_l, dst_l, pos, counts = self.sample_hop(n_id, k, seed)
             e_id = self.rg.csr_eid[pos]
-            adjs.append(Adj(torch.stack([src_l, dst_l]), e_id, (n_id.numel(), n_dst), pos))
+            adjs.append(Adj(torch.stack([src_l, dst_l]), e_id, (n_id.numel(), n_dst), pos, counts))
         return batch.numel(), n_id, adjs[0] if len(adjs) == 1 else adjs[::-1]
 
     def sample_hop(self, targets, k, seed):
@@ -132,4 +133,4 @@ class NeighborSampler:
         n_id = torch.cat([targets, new_nodes])
         g2l[n_id] = -1
         first[cand] = 1 << 62
-        return n_id, src_l, dst_l, pos.to(torch.int64)
+        return n_id, src_l, dst_l, pos.to(torch.int64), counts
