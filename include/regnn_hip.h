@@ -168,6 +168,21 @@ int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals
  * (model/REGCN.py:32,45 out_lin), which ran far below HBM rate for N ~ 1e7 rows. */
 int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipStream_t stream);
 
+/* Row-wise softmax cross-entropy of the output head over `rows` logit rows (stride ld):
+ * loss_rows[r] = logsumexp(z_r) - z_r[labels[r]];  p[r, c] = scale * (softmax(z_r)_c - [c == y_r])
+ * (p dense [rows, cols]); the CE of run_regnn.py:147 and its gradient in one pass. */
+int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t ld,
+                       const int64_t* labels, float scale, float* p, float* loss_rows,
+                       hipStream_t stream);
+
+/* Fused output head (run_regnn.py:146-148: out_lin over all nodes, log_softmax + nll over the
+ * train rows): logits[rows, C] = h[rows, K] W[C, K]^T + b  (b may be NULL), and for the first
+ * n_loss rows loss_rows / p exactly as regnn_softmax_xent. fp32 MFMA; K must be 64 and
+ * C <= 384 (else REGNN_EINVAL: use a GEMM + regnn_softmax_xent); h 16-byte aligned. */
+int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+                   int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
+                   float* p, float* loss_rows, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Neighbour sampler (replaces torch_sparse SparseTensor.sample_adj behind PyG NeighborSampler,
  * mag/regnn_ns.py:206-214). Spec (this build's, documented in DESIGN.md; torch_sparse's RNG is

@@ -1,5 +1,6 @@
-// Dense helpers of the training step on gfx950: a deterministic column sum of a tall row-major
-// matrix (bias gradients of the per-node Linear heads, N up to ~2e7 rows). Each block owns a
+// Dense helpers of the training step on gfx950: the fused output head (MFMA logits + softmax
+// cross-entropy), a row-wise softmax-xent for other widths, and a deterministic column sum of a
+// tall row-major matrix (bias gradients of the per-node Linear heads, N up to ~2e7 rows). Each block owns a
 // contiguous row range and keeps one partial per column per thread; block partials leave through
 // a fixed-order slab (regnn_rel_reduce) — no atomics, rows read coalesced.
 #include "regnn_common.h"
@@ -25,6 +26,170 @@ col_sum_kernel(const float* __restrict__ x, int64_t rows, int cols, int64_t rows
     }
 }
 
+// One wave per row of a [rows, cols] logits matrix (row stride ld): log-sum-exp, the row's
+// cross-entropy term and the scaled softmax gradient p = scale * (softmax(z) - onehot(label)),
+// written once. Replaces torch's logsumexp / exp / sub / index_put chain, which splits >2^31-
+// element tensors into 32-bit chunks and re-reads the logits ~6 times.
+__global__ void __launch_bounds__(kBlock)
+softmax_xent_kernel(const float* __restrict__ z, int64_t rows, int cols, int64_t ld,
+                    const int64_t* __restrict__ labels, float scale, float* __restrict__ p,
+                    float* __restrict__ loss_rows) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wpb = kBlock / 64;
+    for (int64_t r = (int64_t)blockIdx.x * wpb + threadIdx.x / 64; r < rows;
+         r += (int64_t)gridDim.x * wpb) {
+        const float* zr = z + r * ld;
+        float m = -INFINITY;
+        for (int c = lane; c < cols; c += 64) m = fmaxf(m, zr[c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        float s = 0.f;
+        for (int c = lane; c < cols; c += 64) s += __expf(zr[c] - m);
+        s = group_sum<64>(s);
+        const float lse = m + __logf(s);
+        const int64_t y = labels[r];
+        float* pr = p + r * (int64_t)cols;
+        for (int c = lane; c < cols; c += 64) {
+            const float v = __expf(zr[c] - lse);
+            pr[c] = scale * (c == y ? v - 1.f : v);
+        }
+        if (lane == 0) loss_rows[r] = lse - zr[y];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused output head: logits = h W^T + b over every row, and for the first n_loss rows the CE
+// term lse - z[y] and the scaled softmax gradient p = scale * (softmax(z) - onehot(y)), from the
+// accumulators (run_regnn.py:146-148 out_lin + log_softmax + nll over the train rows).
+//
+// fp32 MFMA v_mfma_f32_16x16x4_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD). One wave owns a
+// 16-row tile and all NT x 16 columns (NT accumulators of 4 regs: 88 for 349 classes, so two
+// waves per SIMD fit without spills); W^T lives in LDS for the whole persistent block (8 waves
+// share one copy). The K = 64 reduction is split by lane quarter: quarter q supplies
+// k = 16 q + s at k-step s, so each lane reads 16 contiguous floats of its row.
+// C/D layout (16x16): col = lane & 15, row = 4 * (lane >> 4) + reg, so a row's columns sit on
+// the 16 lanes of one quarter: row reductions are 4 xor-shuffles.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kHeadK = 64;
+constexpr int kHeadBlock = 512;
+constexpr int kHeadMaxC = 24 * 16;
+
+template <int NT>
+__global__ void __launch_bounds__(kHeadBlock)
+head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
+                const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
+                int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
+                float* __restrict__ loss_rows) {
+    constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;   // +1: the four lane quarters read
+    extern __shared__ float Wl[];                           // rows 16 apart -> other banks
+    for (int idx = threadIdx.x; idx < CP * K; idx += blockDim.x) {
+        const int j = idx / K, k = idx - j * K;
+        Wl[k * LDW + j] = j < C ? W[(int64_t)j * K + k] : 0.f;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int wpb = blockDim.x >> 6;
+    const int64_t n_tiles = (rows + 15) / 16;
+    const float* wq = Wl + (16 * q) * LDW + c;
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
+         tile += (int64_t)gridDim.x * wpb) {
+        const int64_t row0 = tile * 16;
+        const int64_t arow = min(row0 + c, rows - 1);
+        const float4* hp = reinterpret_cast<const float4*>(h + arow * K + 16 * q);
+        float a[16];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float4 x = hp[v];
+            a[4 * v] = x.x; a[4 * v + 1] = x.y; a[4 * v + 2] = x.z; a[4 * v + 3] = x.w;
+        }
+        f32x4 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int col = t * 16 + c;
+            const float bc = (bias != nullptr && col < C) ? bias[col] : 0.f;
+            acc[t] = f32x4{bc, bc, bc, bc};
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            float bw[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bw[t] = wq[s * LDW + t * 16];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[t], acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);      // one k-step's B operands live at a time
+        }
+        // ---- logits of every valid row ----
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t row = row0 + 4 * q + i;
+            if (row < rows) {
+                float* lr = logits + row * C + c;
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    if (t < NT - 1 || t * 16 + c < C) lr[t * 16] = acc[t][i];
+            }
+        }
+        if (row0 >= n_loss) continue;                       // wave-uniform
+        // ---- loss rows: log-sum-exp, CE term, scaled softmax gradient ----
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t row = row0 + 4 * q + i;
+            float m = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                if (t < NT - 1 || t * 16 + c < C) m = fmaxf(m, acc[t][i]);
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            float se = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                if (t < NT - 1 || t * 16 + c < C) se += __expf(acc[t][i] - m);
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
+            const float lse = m + __logf(se);
+            if (row < n_loss) {
+                const int64_t y = labels[row];
+                float* pr = p + row * C;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const int col = t * 16 + c;
+                    if (t < NT - 1 || col < C) {
+                        const float z = acc[t][i];
+                        const float v = __expf(z - lse) * scale;
+                        pr[col] = col == y ? v - scale : v;
+                        if (col == y) loss_rows[row] = lse - z;
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int NT>
+int launch_head(const float* h, int64_t rows, const float* W, const float* b, int C,
+                const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
+                float* loss_rows, hipStream_t stream) {
+    const size_t lds = (size_t)kHeadK * (NT * 16 + 1) * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return REGNN_ELAUNCH;
+        attr = true;
+    }
+    const int64_t tiles = (rows + 15) / 16;
+    int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT>), lds,
+                                    kHeadBlock);
+    if (grid > cap) grid = cap;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(head_fwd_kernel<NT>, dim3((unsigned)grid), dim3(kHeadBlock), lds, stream,
+                       h, rows, W, b, C, labels, n_loss, scale, logits, p, loss_rows);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -39,6 +204,39 @@ int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipSt
                        rpb > 0 ? rpb : 1, slab);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
+}
+
+int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t ld,
+                       const int64_t* labels, float scale, float* p, float* loss_rows,
+                       hipStream_t stream) {
+    if (!logits || !labels || !p || !loss_rows || rows < 0 || cols <= 0 || ld < cols)
+        return REGNN_EINVAL;
+    if (rows == 0) return REGNN_OK;
+    hipLaunchKernelGGL(softmax_xent_kernel, dim3(grid_for(rows, kBlock / 64)), dim3(kBlock), 0,
+                       stream, logits, rows, cols, ld, labels, scale, p, loss_rows);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+                   int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
+                   float* p, float* loss_rows, hipStream_t stream) {
+    if (!h || !W || !logits || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC ||
+        n_loss < 0 || n_loss > rows || (n_loss > 0 && (!labels || !p || !loss_rows)) ||
+        (reinterpret_cast<uintptr_t>(h) & 15))
+        return REGNN_EINVAL;
+    if (rows == 0) return REGNN_OK;
+    switch ((C + 15) / 16) {
+#define HEAD_CASE(nt) \
+        case nt: return launch_head<nt>(h, rows, W, b, C, labels, n_loss, scale, logits, p, \
+                                        loss_rows, stream);
+        HEAD_CASE(1) HEAD_CASE(2) HEAD_CASE(3) HEAD_CASE(4) HEAD_CASE(5) HEAD_CASE(6)
+        HEAD_CASE(7) HEAD_CASE(8) HEAD_CASE(9) HEAD_CASE(10) HEAD_CASE(11) HEAD_CASE(12)
+        HEAD_CASE(13) HEAD_CASE(14) HEAD_CASE(15) HEAD_CASE(16) HEAD_CASE(17) HEAD_CASE(18)
+        HEAD_CASE(19) HEAD_CASE(20) HEAD_CASE(21) HEAD_CASE(22) HEAD_CASE(23) HEAD_CASE(24)
+#undef HEAD_CASE
+        default: return REGNN_EINVAL;
+    }
 }
 
 }  // extern "C"

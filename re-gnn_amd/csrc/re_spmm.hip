@@ -502,15 +502,16 @@ rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
 int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
 
-int resident_blocks(const void* kernel, size_t lds) {
-    struct Entry { const void* k; size_t lds; int blocks; };
+int resident_blocks(const void* kernel, size_t lds, int block) {
+    struct Entry { const void* k; size_t lds; int block; int blocks; };
     static std::mutex mu;
     static Entry cache[64];
     static int n_cache = 0;
     static int n_cu = 0;
     std::lock_guard<std::mutex> lock(mu);
     for (int i = 0; i < n_cache; ++i)
-        if (cache[i].k == kernel && cache[i].lds == lds) return cache[i].blocks;
+        if (cache[i].k == kernel && cache[i].lds == lds && cache[i].block == block)
+            return cache[i].blocks;
     if (n_cu == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -518,11 +519,11 @@ int resident_blocks(const void* kernel, size_t lds) {
             n_cu = 256;
     }
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 4;
     const int blocks = per_cu * n_cu;
-    if (n_cache < 64) cache[n_cache++] = {kernel, lds, blocks};
+    if (n_cache < 64) cache[n_cache++] = {kernel, lds, block, blocks};
     return blocks;
 }
 

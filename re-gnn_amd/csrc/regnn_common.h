@@ -95,7 +95,7 @@ inline int grid_for(int64_t units, int per_block) {
 extern int64_t g_tune_grid_cap;
 extern int64_t g_tune_un;        // rows in flight per lane for F = 16 vectors (0 = 8)
 
-int resident_blocks(const void* kernel, size_t lds);   // blocks per CU x CUs, cached
+int resident_blocks(const void* kernel, size_t lds, int block = kBlock);  // per CU x CUs, cached
 
 // grid for a grid-stride gather kernel: one round of resident blocks (<= kMaxGrid)
 template <typename K>

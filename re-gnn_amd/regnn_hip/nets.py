@@ -29,7 +29,7 @@ class _LinearFn(torch.autograd.Function):
         x, W = ctx.saved_tensors
         g = g.contiguous()
         gx = g @ W if ctx.needs_input_grad[0] else None
-        gW = g.t() @ x if ctx.needs_input_grad[1] else None
+        gW = ops.batched_wgrad(g, x) if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = ops.col_sum(g) if g.is_cuda else g.sum(0)

@@ -58,6 +58,7 @@ def _flat_table(tab):
 class _DegreeNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tab, rg, pack, power):
+        ctx.set_materialize_grads(False)
         dev = rg.device
         deg = torch.empty(rg.n_dst, dtype=torch.float32, device=dev)
         norm = torch.empty_like(deg)
@@ -317,37 +318,74 @@ class _HeadCE(torch.autograd.Function):
     The training step of run_regnn.py (:146-150) computes out_lin on every node and the loss on the
     train rows; autograd through that slice materialises an all-rows zero-filled logits gradient
     (19.4M x 349 fp32 = 27 GB at mag-10x) and runs the backward GEMMs over it. This op returns the
-    same logits and loss and the same gradients, forming the softmax gradient only for the loss
-    rows. The logits output is non-differentiable: use it for evaluation, the loss for training."""
+    same logits and loss and the same gradients: one HIP pass (regnn_softmax_xent) forms the loss
+    rows and the scaled softmax gradient of the loss rows only. The logits output is
+    non-differentiable: use it for evaluation, the loss for training."""
 
     @staticmethod
     def forward(ctx, h, W, b, labels):
-        logits = torch.addmm(b, h, W.t()) if b is not None else h @ W.t()
-        n = labels.numel()
-        z = logits[:n]
-        lse = torch.logsumexp(z, 1)
-        loss = (lse - z.gather(1, labels.view(-1, 1)).squeeze(1)).mean()
-        ctx.save_for_backward(h, W, logits, lse, labels)
+        ctx.set_materialize_grads(False)          # no all-rows zero gradient for `logits`
+        n, C = labels.numel(), W.shape[0]
+        dev = h.device
+        p = torch.empty(n, C, dtype=torch.float32, device=dev)
+        loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
+        lab = labels.to(torch.int64).contiguous()
+        if head_fused(h.shape[1], C) and h.dtype == torch.float32:
+            h = h.contiguous()
+            Wc = W.detach().contiguous()
+            logits = torch.empty(h.shape[0], C, dtype=torch.float32, device=dev)
+            nbytes = 4 * (h.numel() + logits.numel() + p.numel() + n) + 8 * n
+            with timed("head_fwd", nbytes):
+                L.call("regnn_head_fwd", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc),
+                       L.ptr(b.detach().contiguous()) if b is not None else None, C, L.ptr(lab),
+                       n, 1.0 / n, L.ptr(logits), L.ptr(p), L.ptr(loss_rows), L.stream())
+        else:
+            logits = torch.addmm(b, h, W.t()) if b is not None else h @ W.t()
+            with timed("softmax_xent", n * C * 8):
+                L.call("regnn_softmax_xent", L.ptr(logits), n, C, logits.stride(0), L.ptr(lab),
+                       1.0 / n, L.ptr(p), L.ptr(loss_rows), L.stream())
+        loss = loss_rows.sum() / n
+        ctx.save_for_backward(h, W, p)
         ctx.has_bias = b is not None
         ctx.mark_non_differentiable(logits)
         return logits, loss
 
     @staticmethod
     def backward(ctx, _g_logits, g_loss):
-        h, W, logits, lse, labels = ctx.saved_tensors
-        n = labels.numel()
-        p = torch.exp(logits[:n] - lse.unsqueeze(1))                  # softmax of the loss rows
-        p[torch.arange(n, device=p.device), labels] -= 1.0
-        p.mul_(g_loss / n)
-        gh = None
+        h, W, p = ctx.saved_tensors
+        n = p.shape[0]
+        gh = gW = gb = None
+        if g_loss is None:
+            return None, None, None, None
         if ctx.needs_input_grad[0]:
-            gh = torch.zeros_like(h)
-            torch.mm(p, W, out=gh[:n])
-        gW = p.t() @ h[:n] if ctx.needs_input_grad[1] else None
-        gb = None
+            gh = torch.empty_like(h)
+            gh[n:].zero_()
+            torch.mm(p, W * g_loss, out=gh[:n])      # g_loss folded into the C x K weight
+        if ctx.needs_input_grad[1]:
+            gW = batched_wgrad(p, h[:n]) * g_loss
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = col_sum(p) if p.is_cuda else p.sum(0)
+            gb = col_sum(p) * g_loss
         return gh, gW, gb, None
+
+
+def head_fused(K, C):
+    """shapes regnn_head_fwd takes (include/regnn_hip.h): K = 64, C <= 384."""
+    return K == 64 and 0 < C <= 384
+
+
+def batched_wgrad(g, x, chunk=1 << 15):
+    """g^T x for tall g [rows, m], x [rows, k]: a batched GEMM over row chunks + a fixed-order
+    sum (one (m, k) GEMM with K = rows ~ 1e7 ran at ~1 TB/s in hipBLASLt, profiled)."""
+    rows = g.shape[0]
+    nb = rows // chunk
+    if nb < 2:
+        return g.t() @ x
+    main = nb * chunk
+    part = torch.bmm(g[:main].view(nb, chunk, -1).transpose(1, 2), x[:main].view(nb, chunk, -1))
+    out = part.sum(0)
+    if main < rows:
+        out = out + g[main:].t() @ x[main:]
+    return out
 
 
 def head_ce(h, weight, bias, labels):

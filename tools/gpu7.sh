@@ -4,4 +4,4 @@ tail -2 gpurun_out/pytest_gpu.log &&
 tools/gpu_step.sh 900 gpurun_out/bench_mag.log python bench.py --no-cpu-baseline &&
 tools/gpu_step.sh 900 gpurun_out/prof_s10.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_s10 -o run -- python bench.py --steps 4 --warmup 1 --no-cpu-baseline &&
 tools/gpu_step.sh 600 gpurun_out/prof_dblp.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dblp -o run -- python bench.py --workload dblp --steps 50 --warmup 3 --no-cpu-baseline --graph off &&
-tail -1 gpurun_out/bench_mag.log | cut -c1-400
+tail -1 gpurun_out/bench_mag.log | cut -c1-400 && tools/gpu_step.sh 900 gpurun_out/bench_ns.log python bench.py --workload ns --steps 30 --warmup 5 --no-cpu-baseline && tail -1 gpurun_out/bench_ns.log | cut -c1-300
