@@ -41,8 +41,9 @@ int regnn_abi_version(void);
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
  * key 1: grid cap of the grid-stride gather kernels (0 = resident capacity from the occupancy
  * API, the default; > 0 = fixed block count, at most 2048). key 2: rows gathered per lane per
- * step for 16-vector rows (F=64 fp32 / F=128 bf16): 0 = default (8), 4 or 16. Returns the
- * previous value, -1 for an unknown key. */
+ * step for 16-vector rows (F=64 fp32 / F=128 bf16): 0 = default (8), 4 or 16. key 3: fused
+ * head variant (0 = next tile / next k-step operands prefetched, the default; 1 = plain).
+ * Returns the previous value, -1 for an unknown key. */
 int64_t regnn_tune(int32_t key, int64_t value);
 
 /* Rows of the per-block relation-gradient slab that regnn_spmm_bwd / regnn_degree_bwd write
@@ -182,6 +183,18 @@ int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t 
 int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
                    int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
                    float* p, float* loss_rows, hipStream_t stream);
+
+/* GAT attention logits (layer/REGATConv.py:68-69 el = (ft * attn_l).sum(-1), er likewise):
+ * ft [N, H, D], attn_l / attn_r [H, D] -> el, er [N, H]. */
+int regnn_attn_dots_fwd(const float* ft, const float* attn_l, const float* attn_r, int64_t N,
+                        int32_t H, int32_t D, float* el, float* er, hipStream_t stream);
+
+/* Backward of regnn_attn_dots_fwd: gft[n,h,:] = gel[n,h] attn_l[h,:] + ger[n,h] attn_r[h,:]
+ * (written, not accumulated), and slab [slab_rows, 2*H*D] of per-block partial sums whose
+ * column sums (regnn_rel_reduce, width 2*H*D) are [d attn_l | d attn_r]. Every row is written. */
+int regnn_attn_dots_bwd(const float* ft, const float* attn_l, const float* attn_r,
+                        const float* gel, const float* ger, int64_t N, int32_t H, int32_t D,
+                        float* gft, float* slab, int32_t slab_rows, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Neighbour sampler (replaces torch_sparse SparseTensor.sample_adj behind PyG NeighborSampler,

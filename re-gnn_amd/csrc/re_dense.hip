@@ -62,132 +62,188 @@ softmax_xent_kernel(const float* __restrict__ z, int64_t rows, int cols, int64_t
 // term lse - z[y] and the scaled softmax gradient p = scale * (softmax(z) - onehot(y)), from the
 // accumulators (run_regnn.py:146-148 out_lin + log_softmax + nll over the train rows).
 //
-// fp32 MFMA v_mfma_f32_16x16x4_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD). One wave owns a
-// 16-row tile and all NT x 16 columns (NT accumulators of 4 regs: 88 for 349 classes, so two
-// waves per SIMD fit without spills); W^T lives in LDS for the whole persistent block (8 waves
-// share one copy). The K = 64 reduction is split by lane quarter: quarter q supplies
-// k = 16 q + s at k-step s, so each lane reads 16 contiguous floats of its row.
-// C/D layout (16x16): col = lane & 15, row = 4 * (lane >> 4) + reg, so a row's columns sit on
-// the 16 lanes of one quarter: row reductions are 4 xor-shuffles.
+// fp32 MFMA v_mfma_f32_16x16x4_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD) computing the tile
+// TRANSPOSED, logits^T = W h^T: A = W (class on lane & 15), B = h^T (node on lane & 15). The
+// C/D layout (col = lane & 15, row = 4 * (lane >> 4) + reg) then gives lane (q, c) node c and the
+// 4 consecutive classes 16 t + 4 q + 0..3 of every 16-class tile t: one 16-byte store per tile
+// and lane, and a node's softmax reductions are in-lane over 4 NT values plus 2 xor-shuffles
+// across the quarters. One wave owns 16 nodes and all NT x 16 classes (NT accumulators of
+// 4 regs: 88 for 349 classes; 2 waves per SIMD without spills); W^T lives in LDS for the whole
+// persistent block (8 waves share one copy). The K = 64 reduction is split by lane quarter:
+// quarter q supplies k = 16 q + s at k-step s, so each lane reads 16 contiguous floats of its row.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4_u __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned rows
 constexpr int kHeadK = 64;
 constexpr int kHeadBlock = 512;
 constexpr int kHeadMaxC = 24 * 16;
 
-template <int NT>
+// FL: diagnostic variant bits for A/B timing only (regnn_tune key 3): 1 = no prefetch,
+// 2 = no logits stores, 4 = no loss-row epilogue. Shipped variant: FL = 0.
+template <int NT, int FL>
 __global__ void __launch_bounds__(kHeadBlock)
 head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
                 const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
                 int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
                 float* __restrict__ loss_rows) {
+    constexpr bool PIPE = !(FL & 1);
     constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;   // +1: the four lane quarters read
+    static_assert((K * LDW) % 4 == 0, "bias slot must be 16-byte aligned");
     extern __shared__ float Wl[];                           // rows 16 apart -> other banks
     for (int idx = threadIdx.x; idx < CP * K; idx += blockDim.x) {
         const int j = idx / K, k = idx - j * K;
         Wl[k * LDW + j] = j < C ? W[(int64_t)j * K + k] : 0.f;
     }
+    float* bl = Wl + K * LDW;                               // bias after W^T (16-B aligned)
+    for (int j = threadIdx.x; j < CP; j += blockDim.x) bl[j] = (bias && j < C) ? bias[j] : 0.f;
     __syncthreads();
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
     const int wpb = blockDim.x >> 6;
     const int64_t n_tiles = (rows + 15) / 16;
     const float* wq = Wl + (16 * q) * LDW + c;
-    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
-         tile += (int64_t)gridDim.x * wpb) {
-        const int64_t row0 = tile * 16;
-        const int64_t arow = min(row0 + c, rows - 1);
+    const f32x4* bl4 = reinterpret_cast<const f32x4*>(Wl + K * LDW) + q;   // bias[16 t + 4 q]
+    auto load_a = [&](int64_t tile, float* a) {
+        const int64_t arow = min(tile * 16 + c, rows - 1);
         const float4* hp = reinterpret_cast<const float4*>(h + arow * K + 16 * q);
-        float a[16];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const float4 x = hp[v];
             a[4 * v] = x.x; a[4 * v + 1] = x.y; a[4 * v + 2] = x.z; a[4 * v + 3] = x.w;
         }
+    };
+    const int64_t tstride = (int64_t)gridDim.x * wpb;
+    int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+    float a[16], an[16];
+    if (PIPE && tile < n_tiles) load_a(tile, an);
+    for (; tile < n_tiles; tile += tstride) {
+        const int64_t node = tile * 16 + c;
+        if (PIPE) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) a[k] = an[k];
+            if (tile + tstride < n_tiles) load_a(tile + tstride, an);   // next tile in flight
+        } else {
+            load_a(tile, a);
+        }
         f32x4 acc[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int col = t * 16 + c;
-            const float bc = (bias != nullptr && col < C) ? bias[col] : 0.f;
-            acc[t] = f32x4{bc, bc, bc, bc};
-        }
+        for (int t = 0; t < NT; ++t) acc[t] = bl4[4 * t];
+        {
+            float bw[NT], bn[NT];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            float bw[NT];
+            for (int t = 0; t < NT; ++t) bw[t] = wq[t * 16];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) bw[t] = wq[s * LDW + t * 16];
+            for (int s = 0; s < 16; ++s) {
+                if (s + 1 < 16) {
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[t], acc[t], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);      // one k-step's B operands live at a time
-        }
-        // ---- logits of every valid row ----
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t row = row0 + 4 * q + i;
-            if (row < rows) {
-                float* lr = logits + row * C + c;
+                    for (int t = 0; t < NT; ++t) bn[t] = wq[(s + 1) * LDW + t * 16];
+                }
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
-                    if (t < NT - 1 || t * 16 + c < C) lr[t * 16] = acc[t][i];
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[t], a[s], acc[t], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);  // step s+1's B reads overlap step s's MFMAs
+#pragma unroll
+                for (int t = 0; t < NT; ++t) bw[t] = bn[t];
             }
         }
-        if (row0 >= n_loss) continue;                       // wave-uniform
+        const bool valid = node < rows;
+        // ---- logits of every valid node: one 16-byte store per class tile ----
+        if (!(FL & 2) && valid) {
+            float* lr = logits + node * C + 4 * q;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (16 * t + 16 <= C) {
+                    *reinterpret_cast<f32x4_u*>(lr + 16 * t) = acc[t];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (16 * t + 4 * q + i < C) lr[16 * t + i] = acc[t][i];
+                }
+            }
+        }
+        if ((FL & 4) || tile * 16 >= n_loss) continue;      // wave-uniform
         // ---- loss rows: log-sum-exp, CE term, scaled softmax gradient ----
+        float m = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t row = row0 + 4 * q + i;
-            float m = -INFINITY;
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-                if (t < NT - 1 || t * 16 + c < C) m = fmaxf(m, acc[t][i]);
+            for (int i = 0; i < 4; ++i)
+                if (16 * t + 16 <= C || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        float se = 0.f;
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-            float se = 0.f;
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-                if (t < NT - 1 || t * 16 + c < C) se += __expf(acc[t][i] - m);
+            for (int i = 0; i < 4; ++i)
+                if (16 * t + 16 <= C || 16 * t + 4 * q + i < C) se += __expf(acc[t][i] - m);
+        se += __shfl_xor(se, 16, 64);
+        se += __shfl_xor(se, 32, 64);
+        const float lse = m + __logf(se);
+        if (node < n_loss) {
+            const int y = (int)labels[node];
+            float* pr = p + node * C + 4 * q;
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
-            const float lse = m + __logf(se);
-            if (row < n_loss) {
-                const int64_t y = labels[row];
-                float* pr = p + row * C;
+            for (int t = 0; t < NT; ++t) {
+                f32x4 v;
 #pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const int col = t * 16 + c;
-                    if (t < NT - 1 || col < C) {
-                        const float z = acc[t][i];
-                        const float v = __expf(z - lse) * scale;
-                        pr[col] = col == y ? v - scale : v;
-                        if (col == y) loss_rows[row] = lse - z;
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    const int cls = 16 * t + 4 * q + i;
+                    const float e = __expf(acc[t][i] - lse) * scale;
+                    v[i] = cls == y ? e - scale : e;
+                    if (cls == y) loss_rows[node] = lse - acc[t][i];
+                }
+                if (16 * t + 16 <= C) {
+                    *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
                 }
             }
         }
     }
 }
 
-template <int NT>
-int launch_head(const float* h, int64_t rows, const float* W, const float* b, int C,
+template <int NT, int FL>
+int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, int C,
                 const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                 float* loss_rows, hipStream_t stream) {
-    const size_t lds = (size_t)kHeadK * (NT * 16 + 1) * sizeof(float);
+    const size_t lds = ((size_t)kHeadK * (NT * 16 + 1) + NT * 16) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return REGNN_ELAUNCH;
         attr = true;
     }
     const int64_t tiles = (rows + 15) / 16;
     int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
-    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT>), lds,
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL>), lds,
                                     kHeadBlock);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(head_fwd_kernel<NT>, dim3((unsigned)grid), dim3(kHeadBlock), lds, stream,
-                       h, rows, W, b, C, labels, n_loss, scale, logits, p, loss_rows);
+    auto kern = &head_fwd_kernel<NT, FL>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kHeadBlock), lds, stream, h, rows, W, b,
+                       C, labels, n_loss, scale, logits, p, loss_rows);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
+}
+
+template <int NT>
+int launch_head(const float* h, int64_t rows, const float* W, const float* b, int C,
+                const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
+                float* loss_rows, hipStream_t stream) {
+#define HEAD_V(fl) launch_head_v<NT, fl>(h, rows, W, b, C, labels, n_loss, scale, logits, p, \
+                                            loss_rows, stream)
+    if (NT == 22 && g_tune_head != 0) {
+        switch (g_tune_head) {
+            case 1: return HEAD_V(1);
+            case 2: return HEAD_V(2);
+            case 4: return HEAD_V(4);
+            default: break;
+        }
+    }
+    return HEAD_V(0);
+#undef HEAD_V
 }
 
 }  // namespace regnn

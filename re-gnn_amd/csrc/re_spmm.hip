@@ -488,19 +488,36 @@ degree_bwd_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ r
     bins_flush(bins, n_rel, tid, slab, blockIdx.x);
 }
 
-// one wave per output column k: fixed-order sum over slab rows
-__global__ void __launch_bounds__(64)
+// one block per output column k: fixed-order sum over slab rows
+__global__ void __launch_bounds__(kBlock)
 rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
                   float* __restrict__ out, int32_t accumulate) {
-    const int k = blockIdx.x, lane = threadIdx.x;
-    float s = 0.f;
-    for (int64_t r = lane; r < n_rows; r += 64) s += slab[r * width + k];
-    s = group_sum<64>(s);
-    if (lane == 0) out[k] = accumulate ? out[k] + s : s;
+    // one block per column; thread t sums rows t, t + kBlock, ... (4 independent partials in
+    // flight), then the waves combine in a fixed order: deterministic
+    __shared__ float part[kBlock / 64];
+    const int k = blockIdx.x, tid = threadIdx.x;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = tid;
+    for (; r + 3 * kBlock < n_rows; r += 4 * kBlock) {
+        s0 += slab[r * width + k];
+        s1 += slab[(r + kBlock) * width + k];
+        s2 += slab[(r + 2 * kBlock) * width + k];
+        s3 += slab[(r + 3 * kBlock) * width + k];
+    }
+    for (; r < n_rows; r += kBlock) s0 += slab[r * width + k];
+    float s = group_sum<64>((s0 + s1) + (s2 + s3));
+    if ((tid & 63) == 0) part[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+        out[k] = accumulate ? out[k] + t : t;
+    }
 }
 
 int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
+int64_t g_tune_head = 0;
 
 int resident_blocks(const void* kernel, size_t lds, int block) {
     struct Entry { const void* k; size_t lds; int block; int blocks; };
@@ -544,6 +561,11 @@ int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 2) {
         const int64_t old = g_tune_un;
         g_tune_un = value;
+        return old;
+    }
+    if (key == 3) {
+        const int64_t old = g_tune_head;
+        g_tune_head = value;
         return old;
     }
     return -1;
@@ -674,7 +696,7 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
 int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
                      int32_t accumulate, hipStream_t stream) {
     if (!slab || !out || width <= 0 || n_rows < 0) return REGNN_EINVAL;
-    hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(64), 0, stream, slab, n_rows, width,
+    hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(kBlock), 0, stream, slab, n_rows, width,
                        out, accumulate);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;

@@ -1,6 +1,6 @@
 """REGATConv on MI355X — drop-in for layer/REGATConv.py:10-100. The u_add_v SDDMM + relation bias +
 LeakyReLU + per-destination edge softmax is one HIP kernel (forward and backward), the per-head
-aggregation another; torch does the fc projection (hipBLASLt) and the per-head el/er dots."""
+aggregation another, the per-head el/er dots a third; torch does the fc projection (hipBLASLt)."""
 import torch as th
 from torch import nn
 from torch.nn import init
@@ -57,8 +57,7 @@ class REGATConv(nn.Module):
         rg = relgraph(graph, feat.device)
         h = self.feat_drop(feat)                                                   # :66
         ft = self.fc(h).view(-1, self.num_heads, self.out_feats)                   # :67
-        el = (ft * self.attn_l).sum(dim=-1)                                        # :68
-        er = (ft * self.attn_r).sum(dim=-1)                                        # :69
+        el, er = ops.attn_dots(ft, self.attn_l, self.attn_r)                       # :68-69
         tab = pack = None
         if edge_feats is not None:
             tab = relation_table(self.edge_weight, self.alpha)                     # :72-74

@@ -44,6 +44,8 @@ _SIG = {
     "regnn_segment_sum": ([P, P, P, I64, I32, P, P], ctypes.c_int),
     "regnn_col_sum": ([P, I64, I32, P, P], ctypes.c_int),
     "regnn_softmax_xent": ([P, I64, I32, I64, P, F32, P, P, P], ctypes.c_int),
+    "regnn_attn_dots_fwd": ([P, P, P, I64, I32, I32, P, P, P], ctypes.c_int),
+    "regnn_attn_dots_bwd": ([P, P, P, P, P, I64, I32, I32, P, P, I32, P], ctypes.c_int),
     "regnn_head_fwd": ([P, I64, I32, P, P, I32, P, I64, F32, P, P, P, P], ctypes.c_int),
     "regnn_sample_count": ([P, P, I64, I32, P, P], ctypes.c_int),
     "regnn_sample_fill": ([P, P, P, I64, I32, U64, P, P, P, P], ctypes.c_int),

@@ -36,6 +36,51 @@ class _LinearFn(torch.autograd.Function):
         return gx, gW, gb
 
 
+class _TypeProjFn(torch.autograd.Function):
+    """cat([x_t W_t^T + b_t for each node type t], 0) with every GEMM writing its own row range of
+    one output (no torch.cat pass over the N x width result; model/REGCN.py:31-35)."""
+
+    @staticmethod
+    def forward(ctx, n, *args):
+        xs, Ws, bs = args[:n], args[n:2 * n], args[2 * n:]
+        rows = [x.shape[0] for x in xs]
+        out = torch.empty(sum(rows), Ws[0].shape[0], dtype=xs[0].dtype, device=xs[0].device)
+        o = 0
+        for x, W, b, r in zip(xs, Ws, bs, rows):
+            torch.addmm(b, x, W.t(), out=out[o:o + r])
+            o += r
+        ctx.n, ctx.rows = n, rows
+        ctx.save_for_backward(*xs, *Ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        xs, Ws = saved[:n], saved[n:]
+        g = g.contiguous()
+        gx, gW, gb = [None] * n, [None] * n, [None] * n
+        o = 0
+        for t, r in enumerate(ctx.rows):
+            gt = g[o:o + r]
+            o += r
+            if ctx.needs_input_grad[1 + t]:
+                gx[t] = gt @ Ws[t]
+            if ctx.needs_input_grad[1 + n + t]:
+                gW[t] = ops.batched_wgrad(gt, xs[t])
+            if ctx.needs_input_grad[1 + 2 * n + t]:
+                gb[t] = ops.col_sum(gt) if gt.is_cuda else gt.sum(0)
+        return (None, *gx, *gW, *gb)
+
+
+def type_project(fcs, feats):
+    """the per-type input Linear layers of every model, concatenated over node types."""
+    if not all(fc.bias is not None for fc in fcs):
+        return torch.cat([fc(f) for fc, f in zip(fcs, feats)], 0)
+    return _TypeProjFn.apply(len(fcs), *feats, *[fc.weight for fc in fcs],
+                             *[fc.bias for fc in fcs])
+
+
 class Linear(nn.Linear):
     """nn.Linear (same parameters / state_dict) with the GEMV bias gradient."""
 
@@ -72,7 +117,7 @@ class REGCN(nn.Module):
 
     def embed(self, features_list, e_feat):
         """everything before out_lin: the node embeddings the reference returns as `h`."""
-        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = type_project(self.fc_list, features_list)
         h = self.layers[0](self.g, h, e_feat)
         for layer in self.layers[1:]:
             h = layer(self.g, self.dropout(h), e_feat)
@@ -108,7 +153,7 @@ class REGAT(nn.Module):
         self.out_lin = Linear(num_hidden * heads[-2], num_classes)
 
     def _emb(self, features_list, e_feat):
-        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = type_project(self.fc_list, features_list)
         h = self.gat_layers[0](self.g, h, e_feat).flatten(1)
         for l in range(1, self.num_layers):
             h = self.gat_layers[l](self.g, h, e_feat).flatten(1)
@@ -147,7 +192,7 @@ class REMixHop(nn.Module):
         self.fc_layers = Linear(hid_dim * len(p), out_dim, bias=False)
 
     def embed(self, features_list, e_feat):
-        h = torch.cat([fc(f) for fc, f in zip(self.fc_list, features_list)], 0)
+        h = type_project(self.fc_list, features_list)
         h = self.layers[0](self.g, h, e_feat)
         for layer in self.layers[1:]:
             h = layer(self.g, self.dropout(h), e_feat)

@@ -264,6 +264,46 @@ def gat_attention(rg, el, er, ee_tab=None, pack=None, slope=0.2):
     return _GatAttention.apply(el, er, ee_tab, rg, pack, slope)
 
 
+class _AttnDots(torch.autograd.Function):
+    """(el, er) = ((ft * attn_l).sum(-1), (ft * attn_r).sum(-1))  — layer/REGATConv.py:68-69."""
+
+    @staticmethod
+    def forward(ctx, ft, attn_l, attn_r):
+        N, H, D = ft.shape
+        ft = ft.contiguous().float()
+        al = attn_l.detach().reshape(H, D).contiguous().float()
+        ar = attn_r.detach().reshape(H, D).contiguous().float()
+        el = torch.empty(N, H, dtype=torch.float32, device=ft.device)
+        er = torch.empty_like(el)
+        with timed("attn_dots_fwd", 4 * (N * H * D + 2 * N * H)):
+            L.call("regnn_attn_dots_fwd", L.ptr(ft), L.ptr(al), L.ptr(ar), N, H, D, L.ptr(el),
+                   L.ptr(er), L.stream())
+        ctx.save_for_backward(ft, al, ar)
+        ctx.shape = attn_l.shape
+        return el, er
+
+    @staticmethod
+    def backward(ctx, gel, ger):
+        ft, al, ar = ctx.saved_tensors
+        N, H, D = ft.shape
+        gel = torch.zeros(N, H, device=ft.device) if gel is None else gel.contiguous().float()
+        ger = torch.zeros(N, H, device=ft.device) if ger is None else ger.contiguous().float()
+        gft = torch.empty_like(ft)
+        rows = max(1, min(256, N))
+        slab = torch.empty(rows, 2 * H * D, dtype=torch.float32, device=ft.device)
+        with timed("attn_dots_bwd", 4 * (2 * N * H * D + 2 * N * H)):
+            L.call("regnn_attn_dots_bwd", L.ptr(ft), L.ptr(al), L.ptr(ar), L.ptr(gel), L.ptr(ger),
+                   N, H, D, L.ptr(gft), L.ptr(slab), rows, L.stream())
+        g = _reduce(slab, 2 * H * D)
+        F = H * D
+        return gft, g[:F].view(ctx.shape), g[F:].view(ctx.shape)
+
+
+def attn_dots(ft, attn_l, attn_r):
+    """el, er [N, H] of the GAT attention (ft [N, H, D], attn_* [1, H, D])."""
+    return _AttnDots.apply(ft, attn_l, attn_r)
+
+
 class _HeadSpmm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, ft, rg):

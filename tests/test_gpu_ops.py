@@ -136,3 +136,23 @@ def test_head_ce_matches_autograd(bias, N, D, C, n):
     assert _rel(h.grad, hr.grad) < 1e-5 and _rel(W.grad, Wr.grad) < 1e-5
     if bias:
         assert _rel(b.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,D", [(1000, 8, 64), (77, 1, 3), (300, 4, 20)])
+def test_attn_dots_matches_autograd(N, H, D):
+    """ops.attn_dots == ((ft * attn_l).sum(-1), (ft * attn_r).sum(-1)) (layer/REGATConv.py:68-69),
+    values and gradients of ft / attn_l / attn_r."""
+    from regnn_hip import ops
+    torch.manual_seed(1)
+    ft0 = torch.randn(N, H, D, device=DEV)
+    al0, ar0 = torch.randn(1, H, D, device=DEV), torch.randn(1, H, D, device=DEV)
+    ft, al, ar = (t.clone().requires_grad_(True) for t in (ft0, al0, ar0))
+    el, er = ops.attn_dots(ft, al, ar)
+    gl, gr = torch.randn(N, H, device=DEV), torch.randn(N, H, device=DEV)
+    (el * gl + er * gr).sum().backward()
+    ftr, alr, arr = (t.double().requires_grad_(True) for t in (ft0, al0, ar0))
+    elr, err = (ftr * alr).sum(-1), (ftr * arr).sum(-1)
+    (elr * gl.double() + err * gr.double()).sum().backward()
+    assert _rel(el, elr) < 1e-5 and _rel(er, err) < 1e-5
+    assert _rel(ft.grad, ftr.grad) < 1e-5
+    assert _rel(al.grad, alr.grad) < 1e-5 and _rel(ar.grad, arr.grad) < 1e-5
