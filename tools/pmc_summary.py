@@ -19,12 +19,17 @@ def load(d):
 
 
 def group(name):
+    """logical op of a kernel: spmm_main / spmm_chunks / spmm_fixup<T, LPR, NV, MODE, ...> with
+    MODE 0 = forward, 1..4 = backward variants (re_spmm.hip); the shared partial-sum tree; the
+    fused output head."""
     if "regnn::" not in name:
         return None
-    bwd = ", true>" in name or "true>(" in name
+    if "head_fwd_kernel" in name:
+        return "head_fwd"
     for k in ("spmm_main", "spmm_chunks", "spmm_fixup"):
         if k in name:
-            return "spmm_bwd" if bwd else "spmm_fwd"
+            targs = name[name.index("<") + 1:name.index(">")].split(",")
+            return "spmm_fwd" if int(targs[3]) == 0 else "spmm_bwd"
     if "partial_reduce" in name:
         return "spmm_tree"
     return None
@@ -38,13 +43,16 @@ def main():
     true_bytes = 4 * (1 << 30)
     f_scale, w_scale = true_bytes / cal_f, true_bytes / cal_w
     res = {}
-    for op in ("spmm_fwd", "spmm_bwd"):
+    for op in ("spmm_fwd", "spmm_bwd", "head_fwd"):
         fk = {k: v for k, v in fetch.items() if group(k) == op}
+        if not fk:
+            continue
         wk = {k: v for k, v in write.items() if group(k) == op}
         launches = max(len(v) for v in fk.values())
         # tree kernels are shared by fwd/bwd; split them evenly per launch (small)
-        tf = sum(sum(v) for k, v in fetch.items() if group(k) == "spmm_tree")
-        tw = sum(sum(v) for k, v in write.items() if group(k) == "spmm_tree")
+        spmm = op.startswith("spmm")
+        tf = sum(sum(v) for k, v in fetch.items() if group(k) == "spmm_tree") if spmm else 0
+        tw = sum(sum(v) for k, v in write.items() if group(k) == "spmm_tree") if spmm else 0
         fb = (sum(sum(v) for v in fk.values()) + tf / 2) * 1024 / launches
         wb = (sum(sum(v) for v in wk.values()) + tw / 2) * 1024 / launches
         res[op] = {"fetch_bytes_raw": fb, "write_bytes_raw": wb,
@@ -55,7 +63,7 @@ def main():
                           "WRITE_SIZE_bytes": cal_w}
     res["graph"] = {"N": int(N), "E": int(E)}
     json.dump(res, open(out_json, "w"), indent=1)
-    for op in ("spmm_fwd", "spmm_bwd"):
+    for op in [o for o in ("spmm_fwd", "spmm_bwd", "head_fwd") if o in res]:
         with open(out_json.replace("pmc_mag.json", f"pmc_mag_{op}.json"), "w") as f:
             json.dump(res[op] | {"calibration": res["calibration"]}, f, indent=1)
     print(json.dumps({k: v.get("bytes_per_launch") if isinstance(v, dict) else v
