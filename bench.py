@@ -90,6 +90,8 @@ def build_workload(args, dev):
         net = nets.REMixHop(g, gd["R"], 100.0, 64, 64, n_classes, 2, [f.shape[1] for f in feats],
                             input_dropout=args.dropout, activation=F.elu).to(dev)
         convs, kern = 4, ("spmm_fwd", "spmm_bwd")        # 2 live hops x 2 layers
+    elif wl == "ns_infer":
+        return build_ns_infer(args, dev, t0)
     else:
         return build_ns(args, dev, t0)
     labels = torch.randint(0, n_classes, (train_nodes,), generator=gen, device=dev)
@@ -166,6 +168,42 @@ def build_ns(args, dev, t0):
                 ns=True)
 
 
+def build_ns_infer(args, dev, t0):
+    """mag/regnn_ns.py:348-369 layer-wise full-neighbour inference (2 x REGCNConv + LN + relu,
+    out_lin), destination rows sharded over ranks with one all-gather per layer (strong
+    scaling: the whole graph is one step's work, split across ranks)."""
+    from regnn_hip import mag, synth
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.inference import ShardedInference
+    gd = synth.mag_like(args.scale, seed=0, device=dev)
+    keep = gd["rel"] <= 7
+    rg = RelGraph(gd["src"][keep], gd["dst"][keep], gd["N"], dev)
+    edge_type = gd["rel"][keep].to(torch.int64) - 1
+    del keep, gd["src"], gd["dst"], gd["rel"]
+    node_type = gd["ntype"]
+    offs = torch.tensor([gd["type_offsets"][t] for t in synth.NTYPES], device=dev)
+    local_node_idx = torch.arange(gd["N"], device=dev) - offs[node_type]
+    feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1, device=dev)
+    x_dict = {k: f for k, f in enumerate(feats)}
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    torch.manual_seed(3)
+    model = mag.REGNN(128, 64, 349, 2, 10.0, 0.0, {k: 128 for k in x_dict}, 7,
+                      use_norm="ln", self_loop_type=2).to(dev).eval()
+    si = ShardedInference(model, rg, edge_type, node_type, local_node_idx, rank, world)
+    del rg, edge_type
+    torch.cuda.empty_cache()
+
+    def step():
+        si.run(x_dict, gather="argmax")
+
+    torch.cuda.synchronize()
+    log(f"[bench] ns_infer: N={gd['N']:,} rows {si.r0:,}..{si.r1:,} block E={si.block.E:,} "
+        f"built in {time.time() - t0:.1f}s")
+    return dict(step=step, edges_per_step=2 * si.block.E, rg=si.block, R=11,
+                kernels=("spmm_fwd",), convs=2, N=gd["N"], E=si.block.E, scaling="strong")
+
+
 def cpu_baseline(budget_s=20.0):
     """oracle ("port": numpy/scipy restatement) REGCN-2 fwd+bwd, hidden 64, on a bounded
     mag-shaped sample, single thread; returns (edges/s, sample description)."""
@@ -203,7 +241,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["mag", "dblp", "acm", "imdb", "ns"], default="mag")
+    ap.add_argument("--workload", choices=["mag", "dblp", "acm", "imdb", "ns", "ns_infer"], default="mag")
     ap.add_argument("--scale", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=512, help="ns: target papers per rank")
     ap.add_argument("--dropout", type=float, default=0.5)
@@ -303,6 +341,9 @@ def main():
         "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 train step on imdb_like",
         "ns": f"mag/regnn_ns.py REGCN-NS train step (sample [25,20] x {args.batch} papers/rank, "
               f"group_input, 2x REGCNConv+LN, Adam, grad all-reduce) on mag_like(scale={args.scale})",
+        "ns_infer": f"mag/regnn_ns.py layer-wise full-neighbour inference (2x REGCNConv+LN+relu, "
+                    f"out_lin, argmax) on mag_like(scale={args.scale}), rows sharded over ranks, "
+                    f"one all-gather per layer",
     }[args.workload]
     result = {
         "metric": "aggregated edges/sec per GPU (REGCN fwd+bwd, hidden=64); % HBM roofline",
@@ -313,7 +354,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": w.get("scaling", "weak"),
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (seeded multi-relation graph of the BASELINE shape, random features/labels)",
@@ -321,7 +362,8 @@ def main():
             "workload": desc, "nodes": w["N"], "edges": w["E"], "relations": w["R"],
             "conv_applications_per_step": w["convs"], "hidden": 64,
             "parallelism": (f"data-parallel x{world} (RCCL grad all-reduce)" if w.get("ns")
-                            else f"replicas x{world}"),
+                            else f"row-sharded x{world} (RCCL all-gather per layer)"
+                            if w.get("scaling") == "strong" else f"replicas x{world}"),
             "hip_graph": use_graph,
         },
         "roofline": {

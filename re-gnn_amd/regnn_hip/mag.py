@@ -204,6 +204,32 @@ class REGNN(torch.nn.Module):
             x = F.dropout(x, p=self.dropout, training=self.training)
         return self.out_lin(x).log_softmax(dim=-1)
 
+    @torch.no_grad()
+    def inference(self, x_dict, subgraph_loader, edge_type, node_type, local_node_idx,
+                  device=None):
+        """mag/regnn_ns.py:348-369: layer-wise full-neighbour inference -> logits of every node.
+
+        ``subgraph_loader`` is the reference's full-neighbour loader (a NeighborSampler with
+        sizes=[-1] over all nodes) or the global RelGraph itself. Its batches are row ranges of
+        the full graph, so each layer runs as one full-graph aggregation with the layer input
+        resident in HBM (regnn_hip/inference.py); ``inference_sharded`` splits the rows over
+        data-parallel ranks."""
+        rg = getattr(subgraph_loader, "rg", subgraph_loader)
+        sizes = getattr(subgraph_loader, "sizes", [-1])
+        if list(sizes) != [-1]:
+            raise ValueError(f"inference expects a full-neighbour loader (sizes=[-1]), got {sizes}")
+        from .inference import ShardedInference
+        return ShardedInference(self, rg, edge_type, node_type, local_node_idx).run(x_dict)
+
+    @torch.no_grad()
+    def inference_sharded(self, x_dict, rg, edge_type, node_type, local_node_idx, rank, world,
+                          gather="logits", group=None):
+        """inference() with the destination rows split over ``world`` ranks and one all-gather
+        per layer (RCCL over xGMI); gather=None returns only this rank's rows."""
+        from .inference import ShardedInference
+        return ShardedInference(self, rg, edge_type, node_type, local_node_idx, rank,
+                                world).run(x_dict, gather=gather, group=group)
+
 
 def flat_grad_allreduce(params, world):
     """one SUM all-reduce of every gradient in a flat fp32 bucket, then / world (RCCL over xGMI

@@ -52,6 +52,8 @@ class NeighborSampler:
     def __init__(self, rg, node_idx, sizes, batch_size, shuffle=True, seed=0, rank=0,
                  world_size=1, drop_last=False):
         self.rg = rg
+        if node_idx is None:                       # PyG: every node is a target
+            node_idx = torch.arange(rg.n_dst, device=rg.device)
         self.node_idx = torch.as_tensor(node_idx).to(rg.device, torch.int64)
         self.sizes = list(sizes)
         self.batch_size = int(batch_size)
