@@ -10,6 +10,9 @@ explicit hand-derived backward (VJP) of each layer on the hot path, following th
 * ``REGraphConvOracle``   — layer/REGraphConv.py:52-106
 * ``REGATConvOracle``     — layer/REGATConv.py:64-100 (+ DGL ``edge_softmax`` semantics)
 * ``REMixHopConvOracle``  — layer/REMixHopConv.py:48-94
+* ``RESAGEConvOracle``    — layer/RESAGEConv.py:55-114
+* ``REGINConvOracle``     — layer/REGINConv.py:39-66
+* ``REGATv2ConvOracle``   — layer/REGATv2Conv.py:103-163
 * ``MagREGCNConvOracle``  — mag/regnn_layers.py:80-150 (self_loop_type 2, aggr='mean')
 * model wiring            — model/REGCN.py:35-46, model/REGAT.py:54-66, model/REMixHop.py:87-100
 
@@ -319,6 +322,214 @@ class REMixHopConvOracle:
         g_tab = rel_bins(c["rel"], g_ew, P["edge_weight"].shape[0])
         grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
         return g_f[0], grads
+
+
+# ------------------------------------------------------------------------------------------
+# RESAGEConv / REGINConv (layer/RESAGEConv.py:55-114, layer/REGINConv.py:39-66): deg^-1 norm
+# ------------------------------------------------------------------------------------------
+def degree_norm_pow(g, ew, power):
+    deg = g.in_sum(ew)
+    return deg, np.power(np.maximum(deg, 1.0), power)
+
+
+def degree_norm_pow_vjp(g, deg, g_norm, power):
+    g_deg = g_norm * power * np.power(np.maximum(deg, 1.0), power - 1.0) * (deg >= 1.0)
+    return g_deg[g.dst]
+
+
+class RESAGEConvOracle:
+    """deg^-1 pre-norm of the aggregated features, no post-norm, root term feat @ weight (the
+    reference's forward uses ``self.weight`` for the root, :60-61; ``weight_root`` is unused)."""
+
+    def __init__(self, alpha, in_feats, out_feats, norm=True, activation=None, **_):
+        self.alpha, self.fin, self.fout = alpha, in_feats, out_feats
+        self.norm, self.act = norm, activation
+
+    def forward(self, g, feat, rel, P):
+        W, b = P.get("weight"), P.get("bias")
+        c = self.c = dict(feat=feat, rel=rel, P=P)
+        pre_tab = P["edge_weight"] * self.alpha                             # :65
+        ew = lrelu(pre_tab)[np.asarray(rel) - 1, 0]                         # :67-68
+        root = feat @ W if W is not None else feat                          # :60-63
+        x = feat
+        if self.norm:
+            deg, nrm = degree_norm_pow(g, ew, -1.0)                         # :73-80
+            c.update(deg=deg, nrm=nrm)
+            x = feat * nrm[:, None]                                         # :83
+        A = g.adj(ew)
+        if self.fin > self.fout:                                            # :85
+            agg_in = x @ W if W is not None else x                          # :88
+            rst = A @ agg_in
+        else:
+            agg_in = x
+            rst = A @ x                                                     # :98-101
+            c["agg_out"] = rst
+            if W is not None:
+                rst = rst @ W                                               # :103
+        rst = rst + root                                                    # :109
+        if b is not None:
+            rst = rst + b                                                   # :112
+        c.update(pre_tab=pre_tab, A=A, x=x, agg_in=agg_in, pre_act=rst)
+        return ACTS[self.act][0](rst)
+
+    def backward(self, g, gout):
+        c, P = self.c, self.c["P"]
+        W, A, feat = P.get("weight"), c["A"], c["feat"]
+        grads = {}
+        gr = gout * ACTS[self.act][1](c["pre_act"])
+        if P.get("bias") is not None:
+            grads["bias"] = gr.sum(0)
+        if W is not None:
+            grads["weight"] = feat.T @ gr
+            g_feat = gr @ W.T
+        else:
+            g_feat = gr.copy()
+        if self.fin > self.fout:
+            g_agg_in = A.T @ gr
+            g_ew = g.edge_dot(gr, c["agg_in"])
+            if W is not None:
+                grads["weight"] = grads["weight"] + c["x"].T @ g_agg_in
+                g_x = g_agg_in @ W.T
+            else:
+                g_x = g_agg_in
+        else:
+            if W is not None:
+                grads["weight"] = grads["weight"] + c["agg_out"].T @ gr
+                g_out = gr @ W.T
+            else:
+                g_out = gr
+            g_x = A.T @ g_out
+            g_ew = g.edge_dot(g_out, c["x"])
+        if self.norm:
+            g_nrm = (g_x * feat).sum(1)
+            g_feat = g_feat + g_x * c["nrm"][:, None]
+            g_ew = g_ew + degree_norm_pow_vjp(g, c["deg"], g_nrm, -1.0)
+        else:
+            g_feat = g_feat + g_x
+        g_tab = rel_bins(c["rel"], g_ew, P["edge_weight"].shape[0])
+        grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        return g_feat, grads
+
+
+class REGINConvOracle:
+    """rst = deg^-1 * sum ew * feat[u], then apply_func (a Linear here) and activation. The
+    reference always reduces with sum whatever ``aggregator_type`` says (``_reducer`` unused)."""
+
+    def __init__(self, alpha, apply_linear=None, activation=None, **_):
+        self.alpha, self.lin, self.act = alpha, apply_linear, activation
+
+    def forward(self, g, feat, rel, P):
+        c = self.c = dict(feat=feat, rel=rel, P=P)
+        pre_tab = P["edge_weight"] * self.alpha                             # :42-44
+        ew = lrelu(pre_tab)[np.asarray(rel) - 1, 0]                         # :45
+        deg, nrm = degree_norm_pow(g, ew, -1.0)                             # :48-54
+        A = g.adj(ew)
+        agg = A @ feat                                                      # :58-60
+        rst = agg * nrm[:, None]                                            # :62
+        c.update(pre_tab=pre_tab, deg=deg, nrm=nrm, A=A, agg=agg, rst=rst)
+        if self.lin:
+            rst = rst @ P["apply_func.weight"].T + P["apply_func.bias"]      # :63-64
+        c["pre_act"] = rst
+        return ACTS[self.act][0](rst)
+
+    def backward(self, g, gout):
+        c, P = self.c, self.c["P"]
+        grads = {}
+        gr = gout * ACTS[self.act][1](c["pre_act"])
+        if self.lin:
+            grads["apply_func.weight"] = gr.T @ c["rst"]
+            grads["apply_func.bias"] = gr.sum(0)
+            gr = gr @ P["apply_func.weight"]
+        g_nrm = (gr * c["agg"]).sum(1)
+        g_agg = gr * c["nrm"][:, None]
+        g_feat = c["A"].T @ g_agg
+        g_ew = g.edge_dot(g_agg, c["feat"]) + degree_norm_pow_vjp(g, c["deg"], g_nrm, -1.0)
+        g_tab = rel_bins(c["rel"], g_ew, P["edge_weight"].shape[0])
+        grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        return g_feat, grads
+
+
+# ------------------------------------------------------------------------------------------
+# REGATv2Conv (layer/REGATv2Conv.py:103-163): score = attn . LeakyReLU(fs[u] + fd[v])
+# ------------------------------------------------------------------------------------------
+class REGATv2ConvOracle:
+    def __init__(self, alpha, in_feats, out_feats, num_heads, negative_slope=0.2,
+                 residual=False, activation=None, share_weights=False, edge_feats=True, **_):
+        self.alpha, self.fin, self.D, self.H = alpha, in_feats, out_feats, num_heads
+        self.slope, self.residual, self.act = negative_slope, residual, activation
+        self.share, self.use_ee = share_weights, edge_feats
+
+    def forward(self, g, feat, rel, P):
+        N, H, D = feat.shape[0], self.H, self.D
+        c = self.c = dict(feat=feat, rel=rel, P=P)
+        fs = (feat @ P["fc_src.weight"].T + P["fc_src.bias"]).reshape(N, H, D)   # :127-129
+        if self.share:
+            fd = fs                                                             # :131
+        else:
+            fd = (feat @ P["fc_dst.weight"].T + P["fc_dst.bias"]).reshape(N, H, D)  # :133-134
+        pre = fs[g.src] + fd[g.dst]                                             # :139
+        z = lrelu(pre, self.slope)                                              # :140
+        e = (z * P["attn"]).sum(-1)                                             # :141
+        if self.use_ee:
+            pre_tab = P["edge_weight"] * self.alpha                             # :144
+            c["pre_tab"] = pre_tab
+            e = e + lrelu(pre_tab)[np.asarray(rel) - 1]                         # :146-149
+        a = edge_softmax(g, e)                                                  # :152
+        out = np.zeros((g.n_dst, H, D))
+        for h in range(H):
+            out[:, h, :] = g.adj(a[:, h]) @ fs[:, h, :]                         # :154-156
+        if self.residual:
+            if "res_fc.weight" in P:
+                res = (feat @ P["res_fc.weight"].T + P["res_fc.bias"]).reshape(N, -1, D)
+            else:
+                res = feat.reshape(N, -1, D)                                    # Identity
+            c["res_shape"] = res.shape
+            out = out + res                                                     # :158-160
+        c.update(fs=fs, pre=pre, z=z, a=a, pre_act=out)
+        return ACTS[self.act][0](out)
+
+    def backward(self, g, gout):
+        c, P = self.c, self.c["P"]
+        feat, fs, a, pre, z = c["feat"], c["fs"], c["a"], c["pre"], c["z"]
+        N, H, D = feat.shape[0], self.H, self.D
+        grads = {}
+        go = gout * ACTS[self.act][1](c["pre_act"])
+        g_feat = np.zeros_like(feat)
+        if self.residual:
+            if "res_fc.weight" in P:
+                gr = go.reshape(N, H * D)
+                grads["res_fc.weight"] = gr.T @ feat
+                grads["res_fc.bias"] = gr.sum(0)
+                g_feat += gr @ P["res_fc.weight"]
+            else:
+                g_feat += go.sum(1).reshape(N, -1) if c["res_shape"][1] == 1 else go.reshape(N, -1)
+        g_fs = np.zeros_like(fs)
+        for h in range(H):
+            g_fs[:, h, :] = g.adj(a[:, h]).T @ go[:, h, :]
+        g_a = g.edge_dot(go, fs)                                                # (E,H)
+        t = np.zeros((g.n_dst, H))
+        np.add.at(t, g.dst, a * g_a)
+        g_e = a * (g_a - t[g.dst])                                              # softmax VJP
+        if self.use_ee:
+            g_tab = rel_bins(c["rel"], g_e, P["edge_weight"].shape[0])
+            grads["edge_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        grads["attn"] = (g_e[..., None] * z).sum(0, keepdims=True)
+        g_pre = g_e[..., None] * P["attn"] * lrelu_grad(pre, self.slope)        # (E,H,D)
+        np.add.at(g_fs, g.src, g_pre)
+        g_fd = np.zeros_like(fs)
+        np.add.at(g_fd, g.dst, g_pre)
+        if self.share:
+            g_fs = g_fs + g_fd
+        gfs = g_fs.reshape(N, H * D)
+        grads["fc_src.weight"] = gfs.T @ feat
+        grads["fc_src.bias"] = gfs.sum(0)
+        g_feat += gfs @ P["fc_src.weight"]
+        if not self.share:
+            gfd = g_fd.reshape(N, H * D)
+            grads["fc_dst.weight"] = gfd.T @ feat
+            grads["fc_dst.bias"] = gfd.sum(0)
+            g_feat += gfd @ P["fc_dst.weight"]
+        return g_feat, grads
 
 
 # ------------------------------------------------------------------------------------------

@@ -31,9 +31,8 @@ class REGINConv(nn.Module):
         nn.init.constant_(self.edge_weight, 1.0 / self.alpha)
 
     def forward(self, graph, feat, e_feat):
-        if self._aggregator_type != 'sum':
-            raise NotImplementedError(f"REGINConv aggregator '{self._aggregator_type}' "
-                                      "(only 'sum' runs on the HIP path)")
+        # the reference reduces with fn.sum whatever aggregator_type names: its `_reducer`
+        # (layer/REGINConv.py:40) is never used, so 'max' / 'mean' also sum here
         rg = relgraph(graph, feat.device)
         pack = rg.rel_pack(e_feat, num_rel=self.edge_weight.shape[0])
         tab = relation_table(self.edge_weight, self.alpha)

@@ -311,8 +311,84 @@ def gen_mag():
                   use_norm="ln", self_loop_type=2), st)
 
 
+# ------------------------------------------------------------------------------------------
+# the other RE layers (layer/RESAGEConv.py, REGINConv.py, REGATv2Conv.py)
+# ------------------------------------------------------------------------------------------
+def gen_layers_extra():
+    _purge(["dgl", "layer", "model", "utils"])
+    _use_paths([SHIM, REF])
+    import dgl
+    layer = importlib.import_module("layer")
+    import torch.nn.functional as F
+
+    rng = np.random.default_rng(30)
+    gd = make_hetero_graph(rng, [50, 60, 45, 25], 1600)
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    e_feat = torch.from_numpy(gd["rel"])
+    N, R = gd["N"], gd["R"]
+    alpha = 100.0
+
+    def record(name, m, fin, meta, call):
+        feat = torch.from_numpy(f32(rng, N, fin).astype(np.float64)).requires_grad_(True)
+        out = call(m, feat)
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = {}
+        _pack("g_", gd, st)
+        st["feat"], st["gout"], st["out"] = feat.detach().numpy().astype(np.float32), gout, out
+        st["grad_feat"] = feat.grad
+        _pack("p_", _params(m), st)
+        _pack("grad_", _grads(m), st)
+        save(name, dict(alpha=alpha, in_feats=fin, **meta), st)
+
+    sage_cases = [
+        ("norm_weight_bias", 64, 64, dict(norm=True, bias=True, weight=True)),
+        ("norm_in_gt_out_elu", 64, 32, dict(norm=True, bias=True, weight=True, activation="elu")),
+        ("nonorm_noweight", 48, 48, dict(norm=False, bias=False, weight=False)),
+    ]
+    for tag, fin, fout, kw in sage_cases:
+        kw = dict(kw)
+        act = kw.pop("activation", None)
+        torch.manual_seed(11)
+        m = layer.RESAGEConv(R, alpha, fin, fout, activation=F.elu if act else None, **kw)
+        _set_params(m, rng, ew_alpha=alpha)
+        record(f"resageconv_{tag}", m, fin,
+               dict(layer="RESAGEConv", out_feats=fout, activation=act, **kw),
+               lambda m, f: m(g, f, e_feat))
+
+    for tag, agg, lin in (("sum_linear", "sum", True), ("mean_nofunc", "mean", False)):
+        torch.manual_seed(12)
+        apply = torch.nn.Linear(64, 32) if lin else None
+        m = layer.REGINConv(R, alpha, apply_func=apply, aggregator_type=agg)
+        _set_params(m, rng, ew_alpha=alpha)
+        record(f"reginconv_{tag}", m, 64, dict(layer="REGINConv", aggregator_type=agg,
+                                               apply_linear=[64, 32] if lin else None),
+               lambda m, f: m(g, f, e_feat))
+
+    v2_cases = [
+        ("h4_ee", 32, 16, 4, dict(residual=False, share_weights=False), True, None),
+        ("h4_noee_share", 32, 16, 4, dict(residual=False, share_weights=True), False, None),
+        ("h2_ee_res_elu", 24, 16, 2, dict(residual=True, share_weights=False), True, "elu"),
+    ]
+    for tag, fin, fout, H, kw, use_ee, act in v2_cases:
+        torch.manual_seed(13)
+        m = layer.REGATv2Conv(R, alpha, fin, fout, H, 0.0, 0.0, 0.2, kw["residual"],
+                              F.elu if act else None, share_weights=kw["share_weights"])
+        _set_params(m, rng, ew_alpha=alpha)
+        record(f"regatv2conv_{tag}", m, fin,
+               dict(layer="REGATv2Conv", out_feats=fout, num_heads=H, negative_slope=0.2,
+                    edge_feats=use_ee, activation=act, **kw),
+               lambda m, f: m(g, f, e_feat if use_ee else None))
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float64)
-    gen_layers()
-    gen_models()
-    gen_mag()
+    which = sys.argv[1:] or ["layers", "models", "mag", "extra"]
+    if "layers" in which:
+        gen_layers()
+    if "models" in which:
+        gen_models()
+    if "mag" in which:
+        gen_mag()
+    if "extra" in which:
+        gen_layers_extra()

@@ -142,3 +142,56 @@ def test_determinism_regraphconv():
         res.append([out, gfeat] + [p.grad for p in mod.parameters()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def _check_all(mod, d, out, gfeat):
+    _check("out", out, d["out"])
+    _check("grad_feat", gfeat, d["grad_feat"])
+    want = {k: v for k, v in G.sub(d, "grad_").items() if k != "feat"}
+    got = _grads(mod)
+    assert set(got) == set(want), set(got) ^ set(want)
+    for k, v in want.items():
+        _check(k, got[k], v)
+
+
+@pytest.mark.parametrize("name", G.names("resageconv_"))
+def test_resageconv(name):
+    """layer/RESAGEConv.py: deg^-1 pre-norm + root term, HIP degree/SpMM."""
+    from layer import RESAGEConv
+    d = G.load(name)
+    m = d["meta"]
+    mod = _load(RESAGEConv(int(d["g_R"]), m["alpha"], m["in_feats"], m["out_feats"],
+                           norm=m["norm"], bias=m["bias"], weight=m["weight"],
+                           activation=F.elu if m["activation"] else None), d)
+    e_feat = torch.from_numpy(d["g_rel"]).to(DEV)
+    out, gfeat = _run(mod, _graph(d), d["feat"], d["gout"], lambda mo, gg, f: mo(gg, f, e_feat))
+    _check_all(mod, d, out, gfeat)
+
+
+@pytest.mark.parametrize("name", G.names("reginconv_"))
+def test_reginconv(name):
+    """layer/REGINConv.py: sum aggregation (whatever aggregator_type says) + deg^-1 post-norm."""
+    from layer import REGINConv
+    d = G.load(name)
+    m = d["meta"]
+    lin = torch.nn.Linear(*m["apply_linear"]) if m["apply_linear"] else None
+    mod = _load(REGINConv(int(d["g_R"]), m["alpha"], apply_func=lin,
+                          aggregator_type=m["aggregator_type"]), d)
+    e_feat = torch.from_numpy(d["g_rel"]).to(DEV)
+    out, gfeat = _run(mod, _graph(d), d["feat"], d["gout"], lambda mo, gg, f: mo(gg, f, e_feat))
+    _check_all(mod, d, out, gfeat)
+
+
+@pytest.mark.parametrize("name", G.names("regatv2conv_"))
+def test_regatv2conv(name):
+    """layer/REGATv2Conv.py: attn . LeakyReLU(fs[u] + fd[v]) scores, edge softmax, head SpMM."""
+    from layer import REGATv2Conv
+    d = G.load(name)
+    m = d["meta"]
+    mod = _load(REGATv2Conv(int(d["g_R"]), m["alpha"], m["in_feats"], m["out_feats"],
+                            m["num_heads"], 0.0, 0.0, m["negative_slope"], m["residual"],
+                            F.elu if m["activation"] else None,
+                            share_weights=m["share_weights"]), d)
+    e_feat = torch.from_numpy(d["g_rel"]).to(DEV) if m["edge_feats"] else None
+    out, gfeat = _run(mod, _graph(d), d["feat"], d["gout"], lambda mo, gg, f: mo(gg, f, e_feat))
+    _check_all(mod, d, out, gfeat)

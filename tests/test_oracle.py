@@ -70,6 +70,28 @@ def test_remixhopconv(name):
         _check(k, gr[k], v)
 
 
+_EXTRA = {"resageconv_": O.RESAGEConvOracle, "reginconv_": O.REGINConvOracle,
+          "regatv2conv_": O.REGATv2ConvOracle}
+
+
+@pytest.mark.parametrize("name", [n for p in _EXTRA for n in G.names(p)])
+def test_other_re_layers(name):
+    """RESAGEConv / REGINConv / REGATv2Conv."""
+    d = G.load(name)
+    cls = next(c for p, c in _EXTRA.items() if name.startswith(p))
+    g = _graph(d)
+    P = G.sub(d, "p_")
+    o = cls(**d["meta"])
+    out = o.forward(g, d["feat"].astype(np.float64), d["g_rel"], P)
+    _check("out", out, d["out"])
+    gf, gr = o.backward(g, d["gout"].astype(np.float64))
+    _check("grad_feat", gf, d["grad_feat"])
+    want = {k: v for k, v in G.sub(d, "grad_").items() if k != "feat"}
+    assert set(want) == set(gr), set(want) ^ set(gr)
+    for k, v in want.items():
+        _check(k, gr[k], v)
+
+
 @pytest.mark.parametrize("name", G.names("mag_regcnconv_"))
 def test_mag_regcnconv(name):
     d = G.load(name)
