@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change; currently 3). */
+/* ABI version (bumped on any signature change or addition; currently 4). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -98,6 +98,31 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                    const int64_t* level_desc, hipStream_t stream);
 
+/* regnn_spmm_fwd with a fused dropout of the gathered input rows. Replaces the nn.Dropout in
+ * front of the aggregation (layer/REGraphConv.py:56 feat_dropout, and with it the model dropout
+ * between layers, model/REGCN.py:43, when both precede the same aggregation): the rows are read
+ * undropped and every gathered element is masked on the fly, so no dropped copy or mask tensor
+ * is written. Mask spec (this build's; torch's Philox stream is not reproduced): per call a
+ * 64-bit seed s read from device memory (*drop_seed, so a captured graph sees a new seed per
+ * replay), key = fmix32(lo32(s) ^ fmix32(hi32(s) ^ 0x5BD1E995)) with fmix32 the murmur3
+ * finaliser; element (row, f) lies in 16-byte vector v = f / EV (EV = 4 fp32, 8 bf16) of
+ * nvec = F / EV; c = row * nvec + v; h_0 = fmix32(lo32(c) ^ key ^ rotl16(hi32(c))),
+ * h_k = fmix32(h_{k-1} + 0x9E3779B9). 16-bit draws: feature f = v*EV + 2k + b keeps iff 16-bit
+ * half b of h_k is < drop_keep16 (keep probability drop_keep16 / 65536). When drop_keep16 is a
+ * multiple of 256 (p = 0.5, 0.25, ...), 8-bit draws: f = v*EV + 4k + b keeps iff byte b of h_k
+ * is < drop_keep16 / 256 (same keep probability, half the hashing). Kept values are scaled by
+ * drop_scale.
+ * Rows must be 16 vectors (F = 64 fp32 / 128 bf16), else REGNN_EUNSUPPORTED. */
+int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const float* rel_table, const float* edge_w,
+                           const float* in_scale, const float* out_scale, const float* bias,
+                           const void* x, void* y, int64_t n_seg, int32_t F, int32_t dtype,
+                           int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                           const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                           float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                           const int64_t* level_desc, const uint64_t* drop_seed,
+                           uint32_t drop_keep16, float drop_scale, hipStream_t stream);
+
 /* Relation-embedding SpMM, fused backward over the transposed graph (CSC: segment = source u).
  * Replaces DGL GSpMM.backward (gspmm on the reverse graph + gsddmm 'dot' for the edge weight)
  * behind the same call sites as regnn_spmm_fwd, and the PyG/torch_scatter backward.
@@ -119,6 +144,21 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
                    float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                    const int64_t* level_desc, hipStream_t stream);
+
+/* regnn_spmm_bwd through the fused dropout of regnn_spmm_fwd_dropout (same seed, threshold and
+ * scale): x (the undropped forward input) is masked where the kernel reads it (relation bins,
+ * edge and node gradients) and gx is the gradient w.r.t. the undropped rows (masked, scaled). */
+int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const float* rel_table, const float* edge_w,
+                           const float* in_scale, const float* out_scale,
+                           const void* g, const void* x, const void* y, void* gx,
+                           float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                           int64_t n_seg, int32_t F, int32_t dtype,
+                           int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                           const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                           float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                           const int64_t* level_desc, const uint64_t* drop_seed,
+                           uint32_t drop_keep16, float drop_scale, hipStream_t stream);
 
 /* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order. */
 int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,

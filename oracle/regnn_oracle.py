@@ -719,3 +719,43 @@ def remixhop_model(g, feats, rel, P, num_layers, hidden, alpha, gout, p=(0, 1, 2
             grads[f"layers.{l}.{k}"] = v
     _input_proj_vjp(lins, feats, gh, grads)
     return logits, h, grads
+
+
+# ------------------------------------------------------------------------------------------
+# fused-dropout mask of regnn_spmm_fwd_dropout (this build's spec, include/regnn_hip.h)
+# ------------------------------------------------------------------------------------------
+def _fmix32(h):
+    h = np.asarray(h, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x85EBCA6B)
+        h = h ^ (h >> np.uint32(13))
+        h = h * np.uint32(0xC2B2AE35)
+        h = h ^ (h >> np.uint32(16))
+    return h
+
+
+def dropout_mask(seed, rows, F, ev, keep16):
+    """0/1 keep mask [rows, F] of the fused dropout for a 64-bit seed (ev = features per 16-byte
+    vector: 4 fp32, 8 bf16)."""
+    seed = int(seed) & ((1 << 64) - 1)
+    lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    key = _fmix32(lo ^ _fmix32(hi ^ np.uint32(0x5BD1E995)))
+    nvec = F // ev
+    c = (np.arange(rows, dtype=np.uint64)[:, None] * np.uint64(nvec)
+         + np.arange(nvec, dtype=np.uint64)[None, :])
+    hi = (c >> np.uint64(32)).astype(np.uint32)
+    bits = 8 if keep16 % 256 == 0 else 16
+    per = 32 // bits
+    with np.errstate(over="ignore"):
+        h = _fmix32((c & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ key
+                    ^ ((hi << np.uint32(16)) | (hi >> np.uint32(16))))
+        keep = np.empty((rows, nvec, ev), dtype=bool)
+        lim = np.uint32(keep16 >> 8) if bits == 8 else np.uint32(keep16)
+        mask = np.uint32((1 << bits) - 1)
+        for k in range(ev // per):
+            if k:
+                h = _fmix32(h + np.uint32(0x9E3779B9))
+            for b in range(per):
+                keep[:, :, per * k + b] = ((h >> np.uint32(bits * b)) & mask) < lim
+    return keep.reshape(rows, F).astype(np.float64)

@@ -48,6 +48,9 @@ struct SpmmArgs {
     int32_t n_levels;
     const int64_t* level_desc;   // HOST [n_levels][3]: sb offset, n_out, partial row base
     int32_t slab_row0;     // first slab row this launch writes
+    const uint64_t* drop_seed;   // fused dropout of the gathered rows (DROP kernels only)
+    uint32_t drop_thresh;
+    float drop_scale;
 };
 
 // Backward per-edge dot products (SDDMM 'dot'), compile-time so the gather loop has no
@@ -58,7 +61,8 @@ enum { kFwd = 0, kBwd = 1, kBwdSlab = 2, kBwdEdge = 3, kBwdBoth = 4 };
 __device__ const float kOneF[1] = {1.f};
 __device__ const uint8_t kZeroU8[4] = {0, 0, 0, 0};
 
-template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false>
+// DROP: fused dropout of the forward input rows, 0 = none, 16 / 8 = bits per feature draw
+template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false, int DROP = 0>
 struct Seg {
     static constexpr int EV = Vec<T>::N;
     static constexpr bool BWD = MODE != kFwd;
@@ -67,6 +71,7 @@ struct Seg {
     // rows gathered per step: 8 x 16-byte loads in flight per lane (NV vectors per row)
     static constexpr int UN0 = UNT > 0 ? UNT : (NV >= 8 ? 1 : (8 / NV));
     static constexpr int UN = UN0 < LPR ? UN0 : LPR;
+    static constexpr int NVEC = LPR * NV;    // 16-byte vectors per row (FULL rows)
 
     __device__ __forceinline__ static int off(int q, int lane) { return (q * LPR + lane) * EV; }
 
@@ -93,6 +98,18 @@ struct Seg {
         load_raw(row, F, lane, r);
 #pragma unroll
         for (int q = 0; q < NV; ++q) unpack<T>(r[q], v[q]);
+    }
+
+    // the forward input row of the segment's own node (backward); with DROP the dropped row
+    __device__ __forceinline__ static void load_self(const SpmmArgs& a, int64_t seg, int lane,
+                                                     float (&v)[NV][EV]) {
+        load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, v);
+        if constexpr (DROP) {
+            const uint32_t key = drop_key(a.drop_seed);
+#pragma unroll
+            for (int q = 0; q < NV; ++q)
+                drop_apply<EV, DROP>(key, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane, v[q]);
+        }
     }
 
     __device__ __forceinline__ static float dot(const float (&a)[NV][EV], const float (&b)[NV][EV]) {
@@ -125,6 +142,8 @@ struct Seg {
         const uint8_t* relp = a.rel ? a.rel : kZeroU8;
         const int tm = a.tab ? 0xff : 0, sm = a.in_scale ? -1 : 0;
         const int em = a.edge_w ? -1 : 0, rm = a.rel ? -1 : 0;
+        uint32_t dkey = 0;
+        if constexpr (DROP && !BWD) dkey = drop_key(a.drop_seed);
 
         int ec = min(beg + lane, last);
         int j0 = a.idx[ec], r0 = relp[ec & rm];
@@ -157,6 +176,12 @@ struct Seg {
                     float v[NV][EV];
 #pragma unroll
                     for (int q = 0; q < NV; ++q) unpack<T>(raw[u][q], v[q]);
+                    if constexpr (DROP && !BWD) {
+#pragma unroll
+                        for (int q = 0; q < NV; ++q)
+                            drop_apply<EV, DROP>(dkey, a.drop_thresh, a.drop_scale, jj[u], NVEC,
+                                           q * LPR + lane, v[q]);
+                    }
 #pragma unroll
                     for (int q = 0; q < NV; ++q)
 #pragma unroll
@@ -196,6 +221,8 @@ struct Seg {
             }
         }
         T* __restrict__ out = static_cast<T*>(a.out) + seg * F;
+        uint32_t dkey = 0;
+        if constexpr (DROP && BWD) dkey = drop_key(a.drop_seed);
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int o = off(q, lane);
@@ -206,6 +233,9 @@ struct Seg {
                     r[t] = acc[q][t] * os;
                     if (!BWD && a.bias) r[t] += a.bias[o + t];
                 }
+                // backward through the fused dropout of the forward input rows
+                if constexpr (DROP && BWD)
+                    drop_apply<EV, DROP>(dkey, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane, r);
                 Vec<T>::store(out + o, r);
             }
         }
@@ -226,10 +256,10 @@ __device__ __forceinline__ void bins_flush(float* bins, int n_rel, int tid, floa
     }
 }
 
-template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL, int DROP>
 __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL, DROP>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
@@ -240,7 +270,7 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
         if (a.split > 0 && end - beg > a.split) continue;   // long-segment path
         float acc[NV][S::EV] = {};
         float sx[NV][S::EV] = {};
-        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        if (need_self) S::load_self(a, seg, lane, sx);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
         if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
         S::epilogue(a, seg, lane, os, sx, acc);
@@ -249,10 +279,10 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
 }
 
 // one group per chunk of a long segment: raw partial sums (fp32) -> chunk_partial
-template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL, int DROP>
 __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
     extern __shared__ float bins[];
-    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL, DROP>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
@@ -266,8 +296,7 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
         const int end = min(s1, beg + a.chunk);
         float acc[NV][S::EV] = {};
         float sx[NV][S::EV] = {};
-        if constexpr (S::SLAB || S::EDGE)
-            S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        if constexpr (S::SLAB || S::EDGE) S::load_self(a, seg, lane, sx);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
         if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
         float* part = a.chunk_partial + c * a.F;
@@ -319,9 +348,9 @@ partial_reduce(const float* __restrict__ in, const int32_t* __restrict__ sb, int
 }
 
 // one group per long segment: its fully reduced partial row, then the epilogue
-template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL>
+template <typename T, int LPR, int NV, int MODE, int UNT, bool FULL, int DROP>
 __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_base) {
-    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL, DROP>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     const bool need_self = S::BWD && a.node_grad;
@@ -330,7 +359,7 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
         const int64_t seg = a.long_ids[l];
         float acc[NV][S::EV] = {};
         float sx[NV][S::EV] = {};
-        if (need_self) S::load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, sx);
+        if (need_self) S::load_self(a, seg, lane, sx);
         const int64_t row = final_base >= 0 ? final_base + l : a.chunk_off[l];
         const float* part = a.chunk_partial + row * a.F;
 #pragma unroll
@@ -346,19 +375,22 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
     }
 }
 
-template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false>
+template <typename T, int LPR, int NV, int MODE, int UNT = 0, bool FULL = false, int DROP = 0>
 int launch_spmm(SpmmArgs a, hipStream_t stream) {
-    using S = Seg<T, LPR, NV, MODE, UNT, FULL>;
+    using S = Seg<T, LPR, NV, MODE, UNT, FULL, DROP>;
     constexpr int GPB = kBlock / LPR;
     const size_t lds = S::SLAB ? size_t(a.n_rel) * kBlock * sizeof(float) : 0;
-    const int g1 = grid_resident(spmm_main<T, LPR, NV, MODE, UNT, FULL>, a.n_seg, GPB, lds);
+    const int g1 = grid_resident(spmm_main<T, LPR, NV, MODE, UNT, FULL, DROP>, a.n_seg, GPB, lds);
     a.slab_row0 = 0;
-    hipLaunchKernelGGL((spmm_main<T, LPR, NV, MODE, UNT, FULL>), dim3(g1), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL((spmm_main<T, LPR, NV, MODE, UNT, FULL, DROP>), dim3(g1), dim3(kBlock), lds,
+                       stream, a);
     REGNN_LAUNCH_CHECK();
     if (a.split > 0 && a.n_chunk > 0) {
         a.slab_row0 = kMaxGrid;
-        const int g2 = grid_resident(spmm_chunks<T, LPR, NV, MODE, UNT, FULL>, a.n_chunk, GPB, lds);
-        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, MODE, UNT, FULL>), dim3(g2), dim3(kBlock), lds, stream, a);
+        const int g2 =
+            grid_resident(spmm_chunks<T, LPR, NV, MODE, UNT, FULL, DROP>, a.n_chunk, GPB, lds);
+        hipLaunchKernelGGL((spmm_chunks<T, LPR, NV, MODE, UNT, FULL, DROP>), dim3(g2), dim3(kBlock),
+                           lds, stream, a);
         REGNN_LAUNCH_CHECK();
         int64_t base_in = 0, final_base = -1;
         for (int k = 0; k < a.n_levels; ++k) {
@@ -372,21 +404,21 @@ int launch_spmm(SpmmArgs a, hipStream_t stream) {
             final_base = base_out;
         }
         const int g3 = grid_for(a.n_long, GPB);
-        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, MODE, UNT, FULL>), dim3(g3), dim3(kBlock), 0, stream, a,
-                           final_base);
+        hipLaunchKernelGGL((spmm_fixup<T, LPR, NV, MODE, UNT, FULL, DROP>), dim3(g3), dim3(kBlock),
+                           0, stream, a, final_base);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
 }
 
-template <typename T, int LPR, int NV, int UNT = 0, bool FULL = false>
+template <typename T, int LPR, int NV, int UNT = 0, bool FULL = false, int DROP = 0>
 int launch_mode(SpmmArgs a, int mode, hipStream_t stream) {
     switch (mode) {
-        case kFwd: return launch_spmm<T, LPR, NV, kFwd, UNT, FULL>(a, stream);
-        case kBwd: return launch_spmm<T, LPR, NV, kBwd, UNT, FULL>(a, stream);
-        case kBwdSlab: return launch_spmm<T, LPR, NV, kBwdSlab, UNT, FULL>(a, stream);
-        case kBwdEdge: return launch_spmm<T, LPR, NV, kBwdEdge, UNT, FULL>(a, stream);
-        default: return launch_spmm<T, LPR, NV, kBwdBoth, UNT, FULL>(a, stream);
+        case kFwd: return launch_spmm<T, LPR, NV, kFwd, UNT, FULL, DROP>(a, stream);
+        case kBwd: return launch_spmm<T, LPR, NV, kBwd, UNT, FULL, DROP>(a, stream);
+        case kBwdSlab: return launch_spmm<T, LPR, NV, kBwdSlab, UNT, FULL, DROP>(a, stream);
+        case kBwdEdge: return launch_spmm<T, LPR, NV, kBwdEdge, UNT, FULL, DROP>(a, stream);
+        default: return launch_spmm<T, LPR, NV, kBwdBoth, UNT, FULL, DROP>(a, stream);
     }
 }
 
@@ -394,6 +426,10 @@ int launch_mode(SpmmArgs a, int mode, hipStream_t stream) {
 // and a tunable number of rows in flight per lane (regnn_tune key 2: 0 = 8, or 4 / 16)
 template <typename T>
 int launch_f16v(SpmmArgs a, int mode, hipStream_t stream) {
+    if (a.drop_seed) {
+        if ((a.drop_thresh & 0xFFu) == 0) return launch_mode<T, 16, 1, 8, true, 8>(a, mode, stream);
+        return launch_mode<T, 16, 1, 8, true, 16>(a, mode, stream);
+    }
     if (g_tune_un == 4) return launch_mode<T, 16, 1, 4, true>(a, mode, stream);
     if (g_tune_un == 16) return launch_mode<T, 16, 1, 16, true>(a, mode, stream);
     return launch_mode<T, 16, 1, 8, true>(a, mode, stream);
@@ -405,6 +441,7 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
     constexpr int EV = Vec<T>::N;
     if (a.F <= 0 || a.F % EV) return REGNN_EUNSUPPORTED;
     const int nvec = a.F / EV;
+    if (a.drop_seed && nvec != 16) return REGNN_EUNSUPPORTED;   // fused dropout: 256-byte rows
     if (nvec <= 4) return launch_mode<T, 4, 1>(a, mode, stream);
     if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
     if (nvec == 16) return launch_f16v<T>(a, mode, stream);
@@ -550,7 +587,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 3; }
+int regnn_abi_version(void) { return 4; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -604,14 +641,15 @@ static int check_common(const int32_t* ptr, const int32_t* idx, const void* src,
     return REGNN_OK;
 }
 
-int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
-                   const float* rel_table, const float* edge_w, const float* in_scale,
-                   const float* out_scale, const float* bias, const void* x, void* y,
-                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
-                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
-                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
-                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
-                   hipStream_t stream) {
+static int spmm_fwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                         const float* rel_table, const float* edge_w, const float* in_scale,
+                         const float* out_scale, const float* bias, const void* x, void* y,
+                         int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                         const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                         const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                         const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                         const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                         hipStream_t stream) {
     int st = check_common(ptr, idx, x, y, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
     if (st) return st;
@@ -622,20 +660,22 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial,
                            level_sb, n_levels, level_desc);
     a.bias = bias; a.src = x; a.out = y;
+    a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
     if (dtype == REGNN_F32) return dispatch<float>(a, kFwd, stream);
     if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, kFwd, stream);
     return REGNN_EUNSUPPORTED;
 }
 
-int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
-                   const float* rel_table, const float* edge_w, const float* in_scale,
-                   const float* out_scale, const void* g, const void* x, const void* y, void* gx,
-                   float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
-                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
-                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
-                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
-                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
-                   hipStream_t stream) {
+static int spmm_bwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                         const float* rel_table, const float* edge_w, const float* in_scale,
+                         const float* out_scale, const void* g, const void* x, const void* y,
+                         void* gx, float* slab, int32_t n_rel, float* edge_grad,
+                         float* node_grad, int64_t n_seg, int32_t F, int32_t dtype, int32_t split,
+                         int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                         const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                         float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                         const int64_t* level_desc, const uint64_t* drop_seed,
+                         uint32_t drop_keep16, float drop_scale, hipStream_t stream) {
     int st = check_common(ptr, idx, g, gx, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
     if (st) return st;
@@ -649,10 +689,73 @@ int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            level_sb, n_levels, level_desc);
     a.src = g; a.out = gx; a.self = x; a.ng_a = y ? g : nullptr; a.ng_b = y;
     a.slab = slab; a.n_rel = n_rel; a.edge_grad = edge_grad; a.node_grad = node_grad;
+    a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
+    if (drop_seed && (slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
     const int mode = slab ? (edge_grad ? kBwdBoth : kBwdSlab) : (edge_grad ? kBwdEdge : kBwd);
     if (dtype == REGNN_F32) return dispatch<float>(a, mode, stream);
     if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, mode, stream);
     return REGNN_EUNSUPPORTED;
+}
+
+int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w, const float* in_scale,
+                   const float* out_scale, const float* bias, const void* x, void* y,
+                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                   hipStream_t stream) {
+    return spmm_fwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y, n_seg,
+                         F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
+                         chunk_partial, level_sb, n_levels, level_desc, nullptr, 0, 1.f, stream);
+}
+
+int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const float* rel_table, const float* edge_w, const float* in_scale,
+                           const float* out_scale, const float* bias, const void* x, void* y,
+                           int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                           const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                           const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                           const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                           const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                           hipStream_t stream) {
+    if (!drop_seed || drop_keep16 > 65536u) return REGNN_EINVAL;
+    return spmm_fwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y, n_seg,
+                         F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
+                         chunk_partial, level_sb, n_levels, level_desc, drop_seed, drop_keep16,
+                         drop_scale, stream);
+}
+
+int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                   const float* rel_table, const float* edge_w, const float* in_scale,
+                   const float* out_scale, const void* g, const void* x, const void* y, void* gx,
+                   float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                   int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                   const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                   const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                   const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                   hipStream_t stream) {
+    return spmm_bwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, g, x, y, gx, slab,
+                         n_rel, edge_grad, node_grad, n_seg, F, dtype, split, chunk, long_ids,
+                         n_long, chunk_long, chunk_off, n_chunk, chunk_partial, level_sb,
+                         n_levels, level_desc, nullptr, 0, 1.f, stream);
+}
+
+int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const float* rel_table, const float* edge_w, const float* in_scale,
+                           const float* out_scale, const void* g, const void* x, const void* y,
+                           void* gx, float* slab, int32_t n_rel, float* edge_grad,
+                           float* node_grad, int64_t n_seg, int32_t F, int32_t dtype,
+                           int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                           const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                           float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                           const int64_t* level_desc, const uint64_t* drop_seed,
+                           uint32_t drop_keep16, float drop_scale, hipStream_t stream) {
+    if (!drop_seed || drop_keep16 > 65536u) return REGNN_EINVAL;
+    return spmm_bwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, g, x, y, gx, slab,
+                         n_rel, edge_grad, node_grad, n_seg, F, dtype, split, chunk, long_ids,
+                         n_long, chunk_long, chunk_off, n_chunk, chunk_partial, level_sb,
+                         n_levels, level_desc, drop_seed, drop_keep16, drop_scale, stream);
 }
 
 int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table, int64_t n_seg,

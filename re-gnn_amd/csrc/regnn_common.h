@@ -76,6 +76,49 @@ __device__ __forceinline__ void unpack<bf16_t>(const uint4& r, float (&v)[8]) {
     }
 }
 
+// Fused dropout keep mask (spec in regnn_hip.h, regnn_spmm_fwd_dropout): the murmur3 finaliser
+// over a per-call key and the element's 16-byte-vector counter, 16 bits per feature.
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t drop_key(const uint64_t* seed) {
+    const uint64_t s = *seed;
+    return fmix32(uint32_t(s) ^ fmix32(uint32_t(s >> 32) ^ 0x5BD1E995u));
+}
+
+// v[t] *= keep(t) ? scale : 0 for feature vector `vec` (of nvec per row) of row `row`.
+// BITS = 16: two features per 32-bit draw; BITS = 8 (keep16 a multiple of 256): four.
+template <int EV, int BITS>
+__device__ __forceinline__ void drop_apply(uint32_t key, uint32_t thresh, float scale, int64_t row,
+                                           int nvec, int vec, float (&v)[EV]) {
+    const uint64_t c = uint64_t(row) * uint64_t(nvec) + uint64_t(vec);
+    const uint32_t hi = uint32_t(c >> 32);
+    uint32_t h = fmix32(uint32_t(c) ^ key ^ ((hi << 16) | (hi >> 16)));
+    if constexpr (BITS == 16) {
+#pragma unroll
+        for (int k = 0; k < EV / 2; ++k) {
+            if (k) h = fmix32(h + 0x9E3779B9u);
+            v[2 * k] = (h & 0xFFFFu) < thresh ? v[2 * k] * scale : 0.f;
+            v[2 * k + 1] = (h >> 16) < thresh ? v[2 * k + 1] * scale : 0.f;
+        }
+    } else {
+        const uint32_t t8 = thresh >> 8;
+#pragma unroll
+        for (int k = 0; k < EV / 4; ++k) {
+            if (k) h = fmix32(h + 0x9E3779B9u);
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                v[4 * k + b] = ((h >> (8 * b)) & 0xFFu) < t8 ? v[4 * k + b] * scale : 0.f;
+        }
+    }
+}
+
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll

@@ -40,22 +40,37 @@ class REGraphConv(nn.Module):
             init.zeros_(self.bias)
         init.constant_(self.edge_weight, 1.0 / self.alpha)
 
-    def forward(self, graph, feat, e_feat, return_embedding=False):
+    def forward(self, graph, feat, e_feat, return_embedding=False, pre_dropout=0.0):
+        """``pre_dropout`` (not in the reference signature, default off): the probability of a
+        caller's nn.Dropout applied to ``feat`` just before this layer (model/REGCN.py:43), so
+        both dropouts fuse into the aggregation's gather when it reads ``feat`` directly."""
         rg = relgraph(graph, feat.device)
         pack = rg.rel_pack(e_feat, num_rel=self.edge_weight.shape[0])
-        feat = self.feat_dropout(feat)                                   # :56
+        keep = 1.0
+        if self.training:
+            keep = (1.0 - self.feat_dropout.p) * (1.0 - pre_dropout)
+        direct = self.weight is None or self.in_feats <= self.out_feats  # SpMM reads feat as is
+        p_drop = 0.0
+        if keep < 1.0 and keep > 0.0 and direct and ops.dropout_fusable(feat):
+            p_drop = 1.0 - keep                                          # :56 fused in the gather
+        else:
+            if self.training and pre_dropout:
+                feat = th.nn.functional.dropout(feat, pre_dropout, training=True)
+            feat = self.feat_dropout(feat)                               # :56
         tab = relation_table(self.edge_weight, self.alpha)               # :58-61 (folded: no E-sized ew)
         norm = ops.degree_norm(rg, pack, tab) if self.norm else None     # :66-75
         if self.in_feats > self.out_feats:                               # :78
             if self.weight is not None:
                 feat = th.matmul(feat, self.weight)                      # :81
             rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm,  # :76,84-86,97-101
-                              bias=self.bias)
+                              bias=self.bias, dropout=p_drop)
         elif self.weight is None:
-            rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm, bias=self.bias)
+            rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm, bias=self.bias,
+                              dropout=p_drop)
         else:
             # diag(norm) (A X) W == (diag(norm) A X) W: post-scale fused into the SpMM epilogue
-            rst = th.matmul(ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm), self.weight)
+            rst = th.matmul(ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm,
+                                        dropout=p_drop), self.weight)
             if self.bias is not None:
                 rst = rst + self.bias
         if self.activation is not None:

@@ -35,6 +35,11 @@ _SIG = {
                         P, P, I32, P, P], ctypes.c_int),
     "regnn_spmm_bwd": ([P, P, P, P, P, P, P, P, P, P, P, P, I32, P, P, I64, I32, I32, I32, I32, P,
                         I32, P, P, I32, P, P, I32, P, P], ctypes.c_int),
+    "regnn_spmm_fwd_dropout": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P,
+                                P, I32, P, P, I32, P, P, ctypes.c_uint32, F32, P], ctypes.c_int),
+    "regnn_spmm_bwd_dropout": ([P, P, P, P, P, P, P, P, P, P, P, P, I32, P, P, I64, I32, I32, I32,
+                                I32, P, I32, P, P, I32, P, P, I32, P, P, ctypes.c_uint32, F32, P],
+                               ctypes.c_int),
     "regnn_rel_reduce": ([P, I64, I32, P, I32, P], ctypes.c_int),
     "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P],
@@ -57,7 +62,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 3
+ABI_VERSION = 4
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -119,8 +119,11 @@ class REGCN(nn.Module):
         """everything before out_lin: the node embeddings the reference returns as `h`."""
         h = type_project(self.fc_list, features_list)
         h = self.layers[0](self.g, h, e_feat)
+        p = self.dropout.p if self.training else 0.0
         for layer in self.layers[1:]:
-            h = layer(self.g, self.dropout(h), e_feat)
+            # model dropout (model/REGCN.py:43) handed to the layer: fused with its own
+            # feat_dropout into the aggregation's gather when the layer reads h directly
+            h = layer(self.g, h, e_feat, pre_dropout=p)
         return h
 
     def forward(self, features_list, e_feat):

@@ -107,23 +107,55 @@ def in_count_norm(rg, power=-0.5):
 
 
 # ---------------------------------------------------------------------------------------------
+_DROP_CTR = {}
+
+
+def dropout_fusable(x):
+    """the fused-dropout SpMM kernels take 256-byte rows (F = 64 fp32 / 128 bf16)."""
+    return x.is_cuda and x.dim() == 2 and x.shape[1] * x.element_size() == 256
+
+
+def drop_request(p, device, seed=None):
+    """one fused-dropout call: (seed tensor on the device, 16-bit keep threshold, scale).
+
+    The seed is a fresh device scalar per call, derived from a per-device counter whose base is
+    drawn from torch's CPU generator (so torch.manual_seed makes runs repeatable); the counter
+    increment is a device op, so a captured HIP graph draws a new mask on every replay."""
+    keep = 1.0 - float(p)
+    if seed is None:
+        ctr = _DROP_CTR.get(device)
+        if ctr is None:
+            base = int(torch.randint(1, 2 ** 62, (1,)).item())
+            ctr = _DROP_CTR[device] = torch.tensor([base], dtype=torch.int64, device=device)
+        ctr.add_(1)
+        seed = ctr.clone()
+    return seed, int(round(keep * 65536)), 1.0 / keep
+
+
 class _ReSpmm(torch.autograd.Function):
-    """y = post * (A_tab (pre * x)), A_tab[v,u] = sum over edges u->v of tab[rel_e]."""
+    """y = post * (A_tab (pre * drop(x))) + bias, A_tab[v,u] = sum over edges u->v of tab[rel_e];
+    drop = the optional fused dropout of the gathered rows (regnn_spmm_fwd_dropout)."""
 
     @staticmethod
-    def forward(ctx, x, tab, pre, post, bias, rg, pack):
+    def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None):
         x = x.contiguous()
         F = x.shape[1]
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
         t = _flat_table(tab)
         plan_args, part = _plan_args(rg.csr_plan, F, x.device)
+        args = (L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
+                L.ptr(t), None, L.ptr(pre), L.ptr(post),
+                L.ptr(None if bias is None else bias.detach().float().contiguous()),
+                L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args)
         with timed("spmm_fwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_fwd")):
-            L.call("regnn_spmm_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
-                   L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
-                   L.ptr(t), None, L.ptr(pre), L.ptr(post),
-                   L.ptr(None if bias is None else bias.detach().float().contiguous()),
-                   L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args, L.stream())
+            if drop is None:
+                L.call("regnn_spmm_fwd", *args, L.stream())
+            else:
+                L.call("regnn_spmm_fwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
+                       L.stream())
+        ctx.drop = drop
         ctx.rg, ctx.pack, ctx.tab_shape = rg, pack, None if tab is None else tab.shape
         ctx.same_scale = pre is not None and pre is post and rg.n_src == rg.n_dst
         ctx.save_for_backward(x, y, t, pre, post)
@@ -145,14 +177,19 @@ class _ReSpmm(torch.autograd.Function):
         elif need_pre:
             node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
         plan_args, part = _plan_args(rg.csc_plan, F, x.device)
+        args = (L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
+                L.ptr(t), None, L.ptr(post), L.ptr(pre), L.ptr(gy), L.ptr(x),
+                L.ptr(y if ctx.same_scale and node is not None else None), L.ptr(gx),
+                L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F, L.dtype_code(x), *plan_args)
+        drop = ctx.drop
         with timed("spmm_bwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_bwd")):
-            L.call("regnn_spmm_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
-                   L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
-                   L.ptr(t), None, L.ptr(post), L.ptr(pre), L.ptr(gy), L.ptr(x),
-                   L.ptr(y if ctx.same_scale and node is not None else None), L.ptr(gx),
-                   L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F, L.dtype_code(x),
-                   *plan_args, L.stream())
+            if drop is None:
+                L.call("regnn_spmm_bwd", *args, L.stream())
+            else:
+                L.call("regnn_spmm_bwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
+                       L.stream())
         g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
         g_pre = g_post = None
         if ctx.same_scale:
@@ -164,17 +201,26 @@ class _ReSpmm(torch.autograd.Function):
                 yf, gf = y.float(), gy.float()
                 g_post = (gf * yf).sum(1) / post
         g_bias = gy.float().sum(0) if need_bias else None
-        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None
+        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None
 
 
-def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None):
-    """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * x[u] + bias  (HIP).
+def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=0.0,
+            drop_seed=None):
+    """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * drop(x)[u] + bias  (HIP).
 
+    dropout: probability of an nn.Dropout applied to x in front of the aggregation; fused into
+    the gather for 256-byte rows (no dropped copy, no mask tensor), a torch dropout otherwise.
     The bias is fused into the kernel epilogue unless the backward needs the pre-bias output
     (differentiable post-scale: the node-norm gradient reads <g, y> / post)."""
+    drop = None
+    if dropout:
+        if dropout < 1.0 and dropout_fusable(x):
+            drop = drop_request(dropout, x.device, drop_seed)
+        else:
+            x = torch.nn.functional.dropout(x, dropout, training=True)
     if bias is not None and post is not None and post.requires_grad:
-        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack) + bias
-    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack)
+        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop) + bias
+    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -135,3 +135,18 @@ def test_models(name):
     assert set(want) == set(grads), set(want) ^ set(grads)
     for k, v in want.items():
         _check(k, grads[k], v)
+
+
+@pytest.mark.parametrize("keep16,ev", [(32768, 4), (16384, 8), (int(0.7 * 65536), 4),
+                                       (int(0.9 * 65536), 8)])
+def test_dropout_mask_spec(keep16, ev):
+    """the fused-dropout mask restatement (include/regnn_hip.h regnn_spmm_fwd_dropout): keep rate,
+    no correlation between neighbouring features / rows, a different mask per seed."""
+    m = O.dropout_mask(0xDEADBEEF12345, 4000, 16 * ev, ev, keep16)
+    keep = keep16 / 65536
+    assert abs(m.mean() - keep) < 0.005
+    c = m - m.mean()
+    assert abs((c[:, 1:] * c[:, :-1]).mean()) < 0.01 * keep
+    assert abs((c[1:] * c[:-1]).mean()) < 0.01 * keep
+    m2 = O.dropout_mask(0xDEADBEEF12346, 4000, 16 * ev, ev, keep16)
+    assert abs((m == m2).mean() - (keep ** 2 + (1 - keep) ** 2)) < 0.01
