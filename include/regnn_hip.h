@@ -98,6 +98,23 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                    const int64_t* level_desc, hipStream_t stream);
 
+/* regnn_spmm_fwd with a fused forward epilogue (the mag REGCNConv tail, forward only, e.g.
+ * layer-wise inference, mag/regnn_ns.py:348-369):
+ *   r = out_scale[i] * sum(...) + bias + (residual ? residual[i] : 0)
+ *   (epi & 1) r = (r - mean(r)) / sqrt(var(r) + ln_eps) * ln_w + ln_b   (LayerNorm over the row,
+ *             biased variance; ln_w / ln_b may be NULL; mag/regnn_layers.py:134-135)
+ *   (epi & 2) r = max(r, 0)                                             (mag/regnn_ns.py:362)
+ * residual rows have the dtype of y. */
+int regnn_spmm_fwd_fused(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                         const float* rel_table, const float* edge_w,
+                         const float* in_scale, const float* out_scale, const float* bias,
+                         const void* x, void* y, int64_t n_seg, int32_t F, int32_t dtype,
+                         int32_t split, int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                         const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
+                         float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
+                         const int64_t* level_desc, const void* residual, const float* ln_w,
+                         const float* ln_b, float ln_eps, int32_t epi, hipStream_t stream);
+
 /* regnn_spmm_fwd with a fused dropout of the gathered input rows. Replaces the nn.Dropout in
  * front of the aggregation (layer/REGraphConv.py:56 feat_dropout, and with it the model dropout
  * between layers, model/REGCN.py:43, when both precede the same aggregation): the rows are read
@@ -223,6 +240,12 @@ int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t 
 int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
                    int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
                    float* p, float* loss_rows, hipStream_t stream);
+
+/* Inference head (mag/regnn_ns.py:367 out_lin over every node, then the caller's argmax,
+ * regnn_ns.py:379): out[r] = argmax_c (h[r] W^T + b)[c] (first maximal class, as torch.argmax),
+ * fp32 MFMA as regnn_head_fwd, without writing the [rows, C] logits. K must be 64, C <= 384. */
+int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+                      int32_t C, int64_t* out, hipStream_t stream);
 
 /* GAT attention logits (layer/REGATConv.py:68-69 el = (ft * attn_l).sum(-1), er likewise):
  * ft [N, H, D], attn_l / attn_r [H, D] -> el, er [N, H]. */

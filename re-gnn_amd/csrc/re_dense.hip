@@ -79,12 +79,14 @@ constexpr int kHeadMaxC = 24 * 16;
 
 // FL: diagnostic variant bits for A/B timing only (regnn_tune key 3): 1 = no prefetch,
 // 2 = no logits stores, 4 = no loss-row epilogue. Shipped variant: FL = 0.
-template <int NT, int FL>
+// AMAX: inference variant (mag/regnn_ns.py:367 out_lin + the caller's argmax): no logits
+// stores and no loss rows; amax[node] = first class of maximal logit (torch.argmax ties).
+template <int NT, int FL, bool AMAX = false>
 __global__ void __launch_bounds__(kHeadBlock)
 head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
                 const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
                 int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
-                float* __restrict__ loss_rows) {
+                float* __restrict__ loss_rows, int64_t* __restrict__ amax) {
     constexpr bool PIPE = !(FL & 1);
     constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;   // +1: the four lane quarters read
     static_assert((K * LDW) % 4 == 0, "bias slot must be 16-byte aligned");
@@ -145,6 +147,28 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
             }
         }
         const bool valid = node < rows;
+        if constexpr (AMAX) {
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int cls = 16 * t + 4 * q + i;
+                    if (cls < C && (acc[t][i] > bv || (acc[t][i] == bv && cls < bi))) {
+                        bv = acc[t][i];
+                        bi = cls;
+                    }
+                }
+#pragma unroll
+            for (int o = 16; o <= 32; o <<= 1) {
+                const float ov = __shfl_xor(bv, o, 64);
+                const int oi = __shfl_xor(bi, o, 64);
+                if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+            }
+            if (valid && q == 0) amax[node] = bi;
+            continue;
+        }
         // ---- logits of every valid node: one 16-byte store per class tile ----
         if (!(FL & 2) && valid) {
             float* lr = logits + node * C + 4 * q;
@@ -203,27 +227,27 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
     }
 }
 
-template <int NT, int FL>
+template <int NT, int FL, bool AMAX = false>
 int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, int C,
                 const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
-                float* loss_rows, hipStream_t stream) {
+                float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
     const size_t lds = ((size_t)kHeadK * (NT * 16 + 1) + NT * 16) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return REGNN_ELAUNCH;
         attr = true;
     }
     const int64_t tiles = (rows + 15) / 16;
     int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
-    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL>), lds,
-                                    kHeadBlock);
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX>),
+                                    lds, kHeadBlock);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
-    auto kern = &head_fwd_kernel<NT, FL>;
+    auto kern = &head_fwd_kernel<NT, FL, AMAX>;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kHeadBlock), lds, stream, h, rows, W, b,
-                       C, labels, n_loss, scale, logits, p, loss_rows);
+                       C, labels, n_loss, scale, logits, p, loss_rows, amax);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
@@ -291,6 +315,25 @@ int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, cons
         HEAD_CASE(13) HEAD_CASE(14) HEAD_CASE(15) HEAD_CASE(16) HEAD_CASE(17) HEAD_CASE(18)
         HEAD_CASE(19) HEAD_CASE(20) HEAD_CASE(21) HEAD_CASE(22) HEAD_CASE(23) HEAD_CASE(24)
 #undef HEAD_CASE
+        default: return REGNN_EINVAL;
+    }
+}
+
+int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+                      int32_t C, int64_t* out, hipStream_t stream) {
+    if (!h || !W || !out || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC ||
+        (reinterpret_cast<uintptr_t>(h) & 15))
+        return REGNN_EINVAL;
+    if (rows == 0) return REGNN_OK;
+    switch ((C + 15) / 16) {
+#define AMAX_CASE(nt) \
+        case nt: return launch_head_v<nt, 0, true>(h, rows, W, b, C, nullptr, 0, 1.f, nullptr, \
+                                                   nullptr, nullptr, stream, out);
+        AMAX_CASE(1) AMAX_CASE(2) AMAX_CASE(3) AMAX_CASE(4) AMAX_CASE(5) AMAX_CASE(6)
+        AMAX_CASE(7) AMAX_CASE(8) AMAX_CASE(9) AMAX_CASE(10) AMAX_CASE(11) AMAX_CASE(12)
+        AMAX_CASE(13) AMAX_CASE(14) AMAX_CASE(15) AMAX_CASE(16) AMAX_CASE(17) AMAX_CASE(18)
+        AMAX_CASE(19) AMAX_CASE(20) AMAX_CASE(21) AMAX_CASE(22) AMAX_CASE(23) AMAX_CASE(24)
+#undef AMAX_CASE
         default: return REGNN_EINVAL;
     }
 }

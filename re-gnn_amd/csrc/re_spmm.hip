@@ -51,7 +51,14 @@ struct SpmmArgs {
     const uint64_t* drop_seed;   // fused dropout of the gathered rows (DROP kernels only)
     uint32_t drop_thresh;
     float drop_scale;
+    const void* residual;  // forward epilogue: + residual row (dtype as out)
+    const float* ln_w;     // forward epilogue: LayerNorm over the row (epi & kEpiLN)
+    const float* ln_b;
+    float ln_eps;
+    int32_t epi;           // kEpiLN | kEpiReLU
 };
+
+enum { kEpiLN = 1, kEpiReLU = 2 };
 
 // Backward per-edge dot products (SDDMM 'dot'), compile-time so the gather loop has no
 // run-time branches: MODE 0 forward; 1 backward without per-edge dots; 2 relation bins (slab);
@@ -201,6 +208,69 @@ struct Seg {
         }
     }
 
+    // y = act(LN(os * acc + bias + residual)) (mag/regnn_layers.py:146-150 update() + residual
+    // + self.norm, then the caller's F.relu, mag/regnn_ns.py:361-362): the row's mean and
+    // variance are LPR-lane group sums, two passes like torch's LayerNorm (biased variance).
+    __device__ __forceinline__ static void epilogue_fused(const SpmmArgs& a, int64_t seg, int lane,
+                                                          float os, const float (&acc)[NV][EV],
+                                                          T* __restrict__ out) {
+        const int F = a.F;
+        float r[NV][EV], res[NV][EV];
+        if (a.residual) load_row(static_cast<const T*>(a.residual) + seg * F, F, lane, res);
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = off(q, lane);
+            const bool in = o < F;
+#pragma unroll
+            for (int t = 0; t < EV; ++t) {
+                float v = acc[q][t] * os;
+                if (a.bias && in) v += a.bias[o + t];
+                if (a.residual) v += res[q][t];
+                r[q][t] = in ? v : 0.f;
+                s += r[q][t];
+            }
+        }
+        if (a.epi & kEpiLN) {
+            const float mean = group_sum<LPR>(s) / float(F);
+            float s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const bool in = off(q, lane) < F;
+#pragma unroll
+                for (int t = 0; t < EV; ++t) {
+                    const float d = r[q][t] - mean;
+                    s2 += in ? d * d : 0.f;
+                }
+            }
+            const float rstd = rsqrtf(group_sum<LPR>(s2) / float(F) + a.ln_eps);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int o = off(q, lane);
+                if (o < F) {
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) {
+                        float v = (r[q][t] - mean) * rstd;
+                        if (a.ln_w) v *= a.ln_w[o + t];
+                        if (a.ln_b) v += a.ln_b[o + t];
+                        r[q][t] = v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = off(q, lane);
+            if (o < F) {
+                if (a.epi & kEpiReLU) {
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) r[q][t] = fmaxf(r[q][t], 0.f);
+                }
+                Vec<T>::store(out + o, r[q]);
+            }
+        }
+    }
+
     // y = os * acc + bias; backward node grad = <self, acc> + <g_i, y_i> / in_scale[i].
     __device__ __forceinline__ static void epilogue(const SpmmArgs& a, int64_t seg, int lane,
                                                     float os, const float (&sx)[NV][EV],
@@ -221,6 +291,12 @@ struct Seg {
             }
         }
         T* __restrict__ out = static_cast<T*>(a.out) + seg * F;
+        if constexpr (!BWD) {
+            if (a.residual || a.epi) {          // wave-uniform: fused forward epilogue
+                epilogue_fused(a, seg, lane, os, acc, out);
+                return;
+            }
+        }
         uint32_t dkey = 0;
         if constexpr (DROP && BWD) dkey = drop_key(a.drop_seed);
 #pragma unroll
@@ -649,7 +725,8 @@ static int spmm_fwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
                          const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
                          const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
                          const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
-                         hipStream_t stream) {
+                         const void* residual, const float* ln_w, const float* ln_b,
+                         float ln_eps, int32_t epi, hipStream_t stream) {
     int st = check_common(ptr, idx, x, y, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
     if (st) return st;
@@ -661,6 +738,7 @@ static int spmm_fwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
                            level_sb, n_levels, level_desc);
     a.bias = bias; a.src = x; a.out = y;
     a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
+    a.residual = residual; a.ln_w = ln_w; a.ln_b = ln_b; a.ln_eps = ln_eps; a.epi = epi;
     if (dtype == REGNN_F32) return dispatch<float>(a, kFwd, stream);
     if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, kFwd, stream);
     return REGNN_EUNSUPPORTED;
@@ -707,7 +785,25 @@ int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    hipStream_t stream) {
     return spmm_fwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y, n_seg,
                          F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
-                         chunk_partial, level_sb, n_levels, level_desc, nullptr, 0, 1.f, stream);
+                         chunk_partial, level_sb, n_levels, level_desc, nullptr, 0, 1.f, nullptr,
+                         nullptr, nullptr, 0.f, 0, stream);
+}
+
+int regnn_spmm_fwd_fused(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                         const float* rel_table, const float* edge_w, const float* in_scale,
+                         const float* out_scale, const float* bias, const void* x, void* y,
+                         int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                         const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                         const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                         const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                         const void* residual, const float* ln_w, const float* ln_b,
+                         float ln_eps, int32_t epi, hipStream_t stream) {
+    if (epi & ~(kEpiLN | kEpiReLU)) return REGNN_EINVAL;
+    if ((epi & kEpiLN) && !(ln_eps > 0.f)) return REGNN_EINVAL;
+    return spmm_fwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y, n_seg,
+                         F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
+                         chunk_partial, level_sb, n_levels, level_desc, nullptr, 0, 1.f, residual,
+                         ln_w, ln_b, ln_eps, epi, stream);
 }
 
 int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
@@ -723,7 +819,7 @@ int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
     return spmm_fwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y, n_seg,
                          F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
                          chunk_partial, level_sb, n_levels, level_desc, drop_seed, drop_keep16,
-                         drop_scale, stream);
+                         drop_scale, nullptr, nullptr, nullptr, 0.f, 0, stream);
 }
 
 int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,

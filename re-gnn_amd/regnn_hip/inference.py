@@ -126,24 +126,59 @@ class ShardedInference:
 
     @torch.no_grad()
     def input(self, x_dict, layer=0):
-        x = self.model.group_input(x_dict, self.node_type, self.local_node_idx, self.own)
+        """group_input for the own rows (mag/regnn_ns.py:300-326). Node ids are type-contiguous
+        (the mag node numbering), so each type's Linear is one GEMM over its row range written
+        in place; otherwise the model's generic group_input."""
+        m = self.model
+        nt = self.node_type[self.r0:self.r1]
+        x = None
+        if nt.numel() and bool((nt[1:] >= nt[:-1]).all()):
+            x = torch.empty(nt.numel(), m.hidden_dim, device=nt.device)
+            types = torch.unique_consecutive(nt).tolist()
+            bounds = torch.searchsorted(nt, torch.tensor(types + [types[-1] + 1],
+                                                         device=nt.device)).tolist()
+            loc = self.local_node_idx[self.r0:self.r1]
+            for k, t in enumerate(types):
+                a, b = bounds[k], bounds[k + 1]
+                l0 = int(loc[a].item())
+                xt = x_dict[t]
+                lin = m.lins[str(t)]
+                ar = torch.arange(l0, l0 + (b - a), device=loc.device)
+                if bool((loc[a:b] == ar).all()):                  # contiguous local ids
+                    torch.addmm(lin.bias, xt[l0:l0 + (b - a)], lin.weight.t(), out=x[a:b])
+                else:
+                    torch.addmm(lin.bias, xt[loc[a:b]], lin.weight.t(), out=x[a:b])
+        if x is None:
+            x = m.group_input(x_dict, self.node_type, self.local_node_idx, self.own)
         return x, self.project(layer, x)
 
     @torch.no_grad()
     def aggregate(self, layer, xs_all, xs_loc):
+        """one HIP pass: mean aggregation with the relation table and bias, + residual,
+        LayerNorm and relu fused in the epilogue (regnn_spmm_fwd_fused)."""
         conv = self.model.convs[layer]
         tab = F.leaky_relu(conv.relation_weight * conv.scaling_factor)     # :110-111
         blk = self.block
-        out = ops.re_spmm(blk, xs_all, tab, blk.pack, post=blk.inv_in_count(), bias=conv.bias)
-        if conv.residual:
-            out = out + xs_loc                                             # x_target @ W
-        if conv.use_norm in ('bn', 'ln'):
-            out = conv.norm(out)
-        return F.relu(out)                                                 # regnn_ns.py:362
+        res = xs_loc if conv.residual else None                            # x_target @ W
+        if conv.use_norm == 'bn':
+            out = ops.re_spmm(blk, xs_all, tab, blk.pack, post=blk.inv_in_count(),
+                              bias=conv.bias)
+            out = F.relu(conv.norm(out + res if res is not None else out))
+            return out
+        ln = None
+        if conv.use_norm == 'ln':
+            ln = (conv.norm.weight, conv.norm.bias, conv.norm.eps)
+        return ops.re_spmm_fused(blk, xs_all, tab, blk.pack, post=blk.inv_in_count(),
+                                 bias=conv.bias, residual=res, ln=ln, relu=True)
 
     @torch.no_grad()
     def head(self, x_loc):
         return self.model.out_lin(x_loc)                                   # :367
+
+    @torch.no_grad()
+    def head_argmax(self, x_loc):
+        lin = self.model.out_lin
+        return ops.head_argmax(x_loc, lin.weight, lin.bias)
 
     @torch.no_grad()
     def run(self, x_dict, gather="logits", group=None):
@@ -157,10 +192,11 @@ class ShardedInference:
             del xs_all
             if layer + 1 < L:
                 xs = self.project(layer + 1, x)
+        if gather == "argmax":
+            am = self.head_argmax(x)
+            return exchange_rows(am.unsqueeze(1), self.bounds, self.rank, self.world,
+                                 group).squeeze(1)
         logits = self.head(x)
         if gather is None:
             return logits
-        if gather == "argmax":
-            am = logits.argmax(-1).to(torch.float32).unsqueeze(1)  # exact below 2^24 classes
-            return exchange_rows(am, self.bounds, self.rank, self.world, group).squeeze(1).long()
         return exchange_rows(logits, self.bounds, self.rank, self.world, group)

@@ -223,6 +223,38 @@ def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=
     return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop)
 
 
+def re_spmm_fused(rg, x, tab=None, pack=None, post=None, bias=None, residual=None, ln=None,
+                  relu=False):
+    """forward-only y = act(LN(post * (A_tab x) + bias + residual)) in one HIP pass
+    (regnn_spmm_fwd_fused; the mag REGCNConv tail at inference, mag/regnn_layers.py:129-135 +
+    mag/regnn_ns.py:362). ln = (weight, bias, eps) of a LayerNorm, or None."""
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                       for t in (x, tab, post, bias, residual)):
+        raise RuntimeError("re_spmm_fused is forward-only (use it under torch.no_grad())")
+    x = x.contiguous()
+    F = x.shape[1]
+    y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
+    t = _flat_table(tab)
+    plan_args, part = _plan_args(rg.csr_plan, F, x.device)
+    epi = (1 if ln is not None else 0) | (2 if relu else 0)
+    lw = lb = None
+    eps = 0.0
+    if ln is not None:
+        lw, lb, eps = ln
+        lw = None if lw is None else lw.detach().float().contiguous()
+        lb = None if lb is None else lb.detach().float().contiguous()
+    res = None if residual is None else residual.contiguous().to(x.dtype)
+    with timed("spmm_fwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
+                                      "spmm_fwd")):
+        L.call("regnn_spmm_fwd_fused", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+               L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
+               L.ptr(t), None, None, L.ptr(post),
+               L.ptr(None if bias is None else bias.detach().float().contiguous()),
+               L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args, L.ptr(res),
+               L.ptr(lw), L.ptr(lb), float(eps), epi, L.stream())
+    return y
+
+
 # ---------------------------------------------------------------------------------------------
 class _EdgeSpmm(torch.autograd.Function):
     """y[v] = sum_{e: u->v} ew[e] * x[u]; ew per edge in the caller's edge order."""
@@ -452,6 +484,22 @@ class _HeadCE(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = col_sum(p) * g_loss
         return gh, gW, gb, None
+
+
+def head_argmax(h, weight, bias=None):
+    """argmax_c (h W^T + b) per row without the logits tensor (regnn_head_argmax), int64."""
+    h = h.detach().contiguous().float()
+    out = torch.empty(h.shape[0], dtype=torch.int64, device=h.device)
+    C = weight.shape[0]
+    if not head_fused(h.shape[1], C):
+        return torch.addmm(bias, h, weight.t()).argmax(-1) if bias is not None else \
+            (h @ weight.t()).argmax(-1)
+    with timed("head_argmax", 4 * (h.numel() + C * h.shape[1]) + 8 * h.shape[0]):
+        L.call("regnn_head_argmax", L.ptr(h), h.shape[0], h.shape[1],
+               L.ptr(weight.detach().float().contiguous()),
+               L.ptr(None if bias is None else bias.detach().float().contiguous()), C,
+               L.ptr(out), L.stream())
+    return out
 
 
 def head_fused(K, C):

@@ -71,3 +71,35 @@ def test_sharded_inference_lockstep():
     assert ok, f"sharded inference rel err {err:.3e}"
     one = ShardedInference(model, rg, edge_type, node_type, local).run(x_dict)
     assert torch.allclose(out, one, rtol=1e-5, atol=1e-5)
+
+
+def test_inference_argmax_head():
+    """gather='argmax' runs the MFMA head without logits (regnn_head_argmax): equals the argmax
+    of the oracle logits wherever the top two classes are not within fp32 noise."""
+    from regnn_hip.inference import ShardedInference
+    gd, rg, edge_type, node_type, local, x_dict, model = _setup(scale=0.002, seed=4)
+    model.eval()
+    am = ShardedInference(model, rg, edge_type, node_type, local).run(x_dict, gather="argmax")
+    ref = _oracle_inference(gd, rg, edge_type, node_type, local, x_dict, model)
+    top2 = np.sort(ref, 1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 1e-4
+    got = am.cpu().numpy()
+    assert am.dtype == torch.int64 and got.shape == (ref.shape[0],)
+    assert np.array_equal(got[clear], ref.argmax(1)[clear])
+    assert clear.mean() > 0.9
+
+
+def test_head_argmax_ties_and_widths():
+    from regnn_hip import ops
+    g = torch.Generator().manual_seed(0)
+    for C in (5, 16, 37, 349):
+        h = torch.randn(1000, 64, generator=g).to(DEV)
+        W = torch.randn(C, 64, generator=g).to(DEV)
+        b = torch.randn(C, generator=g).to(DEV)
+        z = torch.addmm(b, h, W.t())
+        got = ops.head_argmax(h, W, b)
+        top2 = torch.topk(z, min(2, C), 1).values
+        clear = (top2[:, 0] - top2[:, -1]) > 1e-4 if C > 1 else torch.ones(1000, dtype=torch.bool)
+        assert torch.equal(got[clear], z.argmax(1)[clear])
+    W = torch.zeros(20, 64, device=DEV)                      # all classes tie -> class 0
+    assert int(ops.head_argmax(torch.randn(64, 64, device=DEV), W).max()) == 0
