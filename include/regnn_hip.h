@@ -260,6 +260,56 @@ int regnn_attn_dots_bwd(const float* ft, const float* attn_l, const float* attn_
                         float* gft, float* slab, int32_t slab_rows, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * GATv2 scores and the edge softmax over per-edge logits (re_gatv2.hip; H a power of two <= 32
+ * for the softmax entry points; D % 4 == 0 with D / 4 a power of two for the score kernels).
+ * --------------------------------------------------------------------------------------- */
+
+/* GATv2 score SDDMM (layer/REGATv2Conv.py:139-141; mag/regnn_layers.py:399-403), CSR order:
+ *   s[e,h] = sum_d att[h*D+d] * LeakyReLU(fs[idx[e], h*D+d] + fd[v, h*D+d], slope). */
+int regnn_gatv2_score_fwd(const int32_t* ptr, const int32_t* idx, const float* fs, const float* fd,
+                          const float* att, int64_t n_seg, int32_t H, int32_t D, float slope,
+                          float* s, hipStream_t stream);
+
+/* Its backward, destination side (CSR): gfd[v] = sum_{e in seg v} gs[e,h] * att * lrelu'(pre),
+ * and per-block partials of d att = sum_e gs[e,h] * LeakyReLU(pre) in att_slab
+ * [slab_rows, H*D] (every row < the launch grid written; reduce with regnn_rel_reduce over
+ * min(slab_rows, grid) rows: the grid is min(slab_rows, segments / groups per block)). */
+int regnn_gatv2_score_bwd_dst(const int32_t* ptr, const int32_t* idx, const float* fs,
+                              const float* fd, const float* att, const float* gs, int64_t n_seg,
+                              int32_t H, int32_t D, float slope, float* gfd, float* att_slab,
+                              int32_t slab_rows, hipStream_t stream);
+
+/* Its backward, source side (CSC, csc2csr maps a CSC position to the CSR edge position of gs):
+ *   gfs[u] = sum_{e: u->v} gs[e,h] * att * lrelu'(fs[u] + fd[v]). */
+int regnn_gatv2_score_bwd_src(const int32_t* csc_ptr, const int32_t* csc_idx,
+                              const int32_t* csc2csr, const float* fs, const float* fd,
+                              const float* att, const float* gs, int64_t n_src, int32_t H,
+                              int32_t D, float slope, float* gfs, hipStream_t stream);
+
+/* Edge softmax over per-edge logits z = s[e,h] + (ee_table ? ee_table[rel[e]*H + h] : 0), per
+ * destination (CSR):
+ *   gmax == NULL: a = exp(z - max_v z) / sum_v exp(z - max_v z)     (dgl edge_softmax,
+ *                 layer/REGATv2Conv.py:152)
+ *   gmax != NULL: a = exp(z - *gmax) / (sum_v exp(z - *gmax) + eps)  (mag/utils.py:45-57 with
+ *                 the global max read from device memory: far-below-max segments underflow to 0
+ *                 exactly as the reference's). */
+int regnn_edge_softmax_fwd(const int32_t* ptr, const float* s, const uint8_t* rel,
+                           const float* ee_table, const float* gmax, float eps, int64_t n_seg,
+                           int32_t H, float* a, hipStream_t stream);
+
+/* Backward (both forms; the global max's own gradient is exactly 0 up to the eps term):
+ *   gz = a * (ga - sum_v a*ga) (CSR order); slab (optional): per-block (rel, h) sums of gz. */
+int regnn_edge_softmax_bwd(const int32_t* ptr, const uint8_t* rel, const float* a,
+                           const float* ga, int64_t n_seg, int32_t H, float* gz, float* slab,
+                           int32_t n_rel, hipStream_t stream);
+
+/* GAT v1 scores written per edge (CSR): s = LeakyReLU(el[idx[e],h] + er[v,h] + ee[rel[e],h]),
+ * for the global max of the ogbn-mag softmax (mag/regnn_layers.py:297-307). */
+int regnn_gat_scores(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                     const float* ee_table, const float* el, const float* er, int64_t n_seg,
+                     int32_t H, float slope, float* s, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Neighbour sampler (replaces torch_sparse SparseTensor.sample_adj behind PyG NeighborSampler,
  * mag/regnn_ns.py:206-214). Spec (this build's, documented in DESIGN.md; torch_sparse's RNG is
  * not reproducible): for target t with in-degree d and fan-out k (k < 0: all):

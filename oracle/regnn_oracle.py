@@ -14,6 +14,7 @@ explicit hand-derived backward (VJP) of each layer on the hot path, following th
 * ``REGINConvOracle``     — layer/REGINConv.py:39-66
 * ``REGATv2ConvOracle``   — layer/REGATv2Conv.py:103-163
 * ``MagREGCNConvOracle``  — mag/regnn_layers.py:80-150 (self_loop_type 2, aggr='mean')
+* ``MagREGATConvOracle``  — mag/regnn_layers.py:153-436 (REGATConv / REGATv2Conv, global max)
 * model wiring            — model/REGCN.py:35-46, model/REGAT.py:54-66, model/REMixHop.py:87-100
 
 Pinning: every class here is checked against golden vectors produced by running the REFERENCE's own
@@ -602,6 +603,101 @@ class MagREGCNConvOracle:
             gW += x[:self.n_dst].T @ gout
             g_x[:self.n_dst] += gout @ W.T
         grads["weight"] = gW
+        return g_x, grads
+
+
+class MagREGATConvOracle:
+    """mag/regnn_layers.py:153-315 (v2=False) and :318-436 REGATv2Conv (v2=True), self_loop_type
+    2, concat heads: the edge softmax subtracts ONE global max and adds 1e-16 (mag/utils.py:45-57).
+    The backward ignores the max's own gradient (exactly 0 up to the 1e-16 term)."""
+
+    def __init__(self, n_dst, num_edge_types, scaling_factor, heads, out_channels, v2=False,
+                 residual=False, use_norm="ln", negative_slope=0.2, **_):
+        self.n_dst, self.net, self.alpha = n_dst, num_edge_types, scaling_factor
+        self.H, self.C, self.v2 = heads, out_channels, v2
+        self.residual, self.use_norm, self.slope = residual, use_norm, negative_slope
+
+    def forward(self, x, src, dst, edge_type, target_node_type, P):
+        H, C, nd = self.H, self.C, self.n_dst
+        g, et = MagREGCNConvOracle(nd, self.net, self.alpha).block(src, dst, edge_type,
+                                                                   target_node_type, x.shape[0])
+        Wl = P["lin_src.weight"]
+        xs = (x @ Wl.T).reshape(-1, H, C)                                   # :267-272
+        xd = (x[:nd] @ Wl.T).reshape(-1, H, C)
+        pre_tab = P["relation_weight"] * self.alpha                         # :294
+        tab = lrelu(pre_tab)                                                # :295
+        c = self.c = dict(g=g, et=et, x=x, xs=xs, xd=xd, pre_tab=pre_tab, P=P)
+        if self.v2:
+            pre = xs[g.src] + xd[g.dst]                                     # :399-401
+            zz = lrelu(pre, self.slope)                                     # :403
+            z = (zz * P["att"]).sum(-1) + tab[et]                           # :404-413
+            c.update(pre=pre, zz=zz)
+        else:
+            a_s = (xs * P["att_src"]).sum(-1)                               # :289
+            a_d = (xd * P["att_dst"]).sum(-1)                               # :290
+            s = tab[et] + a_s[g.src] + a_d[g.dst]                           # :298-304
+            z = lrelu(s, self.slope)                                        # :305
+            c["s"] = s
+        ex = np.exp(z - z.max())                                            # utils.py:52-53
+        S = np.zeros((nd, H))
+        np.add.at(S, g.dst, ex)
+        a = ex / (S[g.dst] + 1e-16)                                         # utils.py:57
+        out = np.zeros((nd, H, C))
+        for h in range(H):
+            out[:, h, :] = g.adj(a[:, h]) @ xs[:, h, :]                     # propagate :312
+        out = out.reshape(nd, H * C) + P["bias"]                            # :314-319
+        if self.residual:
+            out = out + xd.reshape(nd, H * C)                               # :321-322
+        ln = None
+        if self.use_norm == "ln":
+            out, ln = layer_norm(out, P["norm.weight"], P["norm.bias"])     # :324-325
+        c.update(a=a, ln=ln)
+        return out
+
+    def backward(self, gout):
+        c, P = self.c, self.c["P"]
+        g, xs, xd, a, x = c["g"], c["xs"], c["xd"], c["a"], c["x"]
+        H, C, nd = self.H, self.C, self.n_dst
+        grads = {}
+        if self.use_norm == "ln":
+            gout, grads["norm.weight"], grads["norm.bias"] = layer_norm_vjp(
+                gout, P["norm.weight"], c["ln"])
+        grads["bias"] = gout.sum(0)
+        g3 = gout.reshape(nd, H, C)
+        g_xd = g3.copy() if self.residual else np.zeros_like(xd)
+        g_xs = np.zeros_like(xs)
+        for h in range(H):
+            g_xs[:, h, :] = g.adj(a[:, h]).T @ g3[:, h, :]
+        g_a = g.edge_dot(g3, xs)                                            # (E, H)
+        t = np.zeros((nd, H))
+        np.add.at(t, g.dst, a * g_a)
+        g_z = a * (g_a - t[g.dst])                                          # softmax VJP
+        R = P["relation_weight"].shape[0]
+        if self.v2:
+            g_tab = np.stack([np.bincount(c["et"], weights=g_z[:, h], minlength=R)
+                              for h in range(H)], 1)
+            grads["att"] = (g_z[..., None] * c["zz"]).sum(0, keepdims=True)
+            g_pre = g_z[..., None] * P["att"] * lrelu_grad(c["pre"], self.slope)
+            np.add.at(g_xs, g.src, g_pre)
+            np.add.at(g_xd, g.dst, g_pre)
+        else:
+            g_s = g_z * lrelu_grad(c["s"], self.slope)
+            g_tab = np.stack([np.bincount(c["et"], weights=g_s[:, h], minlength=R)
+                              for h in range(H)], 1)
+            g_as = np.zeros((xs.shape[0], H))
+            np.add.at(g_as, g.src, g_s)
+            g_ad = np.zeros((nd, H))
+            np.add.at(g_ad, g.dst, g_s)
+            grads["att_src"] = (g_as[..., None] * xs).sum(0, keepdims=True)
+            grads["att_dst"] = (g_ad[..., None] * xd).sum(0, keepdims=True)
+            g_xs += g_as[..., None] * P["att_src"]
+            g_xd += g_ad[..., None] * P["att_dst"]
+        grads["relation_weight"] = g_tab * self.alpha * lrelu_grad(c["pre_tab"])
+        Wl = P["lin_src.weight"]
+        gs2, gd2 = g_xs.reshape(-1, H * C), g_xd.reshape(nd, H * C)
+        grads["lin_src.weight"] = gs2.T @ x + gd2.T @ x[:nd]
+        g_x = gs2 @ Wl
+        g_x[:nd] += gd2 @ Wl
         return g_x, grads
 
 

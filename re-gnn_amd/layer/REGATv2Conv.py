@@ -1,12 +1,11 @@
-"""REGATv2Conv on MI355X — drop-in for layer/REGATv2Conv.py:12-163. Not a BASELINE config: the
-GATv2 score needs the (E, H, D) LeakyReLU(el[u] + er[v]) tensor, formed with device tensor ops;
-the per-destination softmax uses the front's edge_softmax and the aggregation is the HIP per-head
-SpMM."""
+"""REGATv2Conv on MI355X — drop-in for layer/REGATv2Conv.py:12-163. The
+GATv2 score <attn, LeakyReLU(fs[u] + fd[v])> is one HIP SDDMM that never forms the (E, H, D)
+tensor (regnn_gatv2_score_*), the relation bias and per-destination softmax one HIP pass
+(regnn_edge_softmax_*), and the aggregation the HIP per-head SpMM."""
 import torch as th
 from torch import nn
 
 from dgl.base import DGLError
-from dgl.nn.pytorch.softmax import edge_softmax
 from dgl.nn.pytorch.utils import Identity
 from dgl.utils import expand_as_pair
 from regnn_hip import ops
@@ -88,18 +87,20 @@ class REGATv2Conv(nn.Module):
             h_src = h_dst = self.feat_drop(feat)
             feat_src = self.fc_src(h_src).view(-1, H, D)
             feat_dst = feat_src if self.share_weights else self.fc_dst(h_src).view(-1, H, D)
-        src, dst = graph.edges()
-        e = self.leaky_relu(feat_src[src] + feat_dst[dst])
-        e = (e * self.attn).sum(dim=-1).unsqueeze(dim=2)
+        s = ops.gatv2_scores(rg, feat_src, feat_dst, self.attn,                    # :139-141
+                             self.leaky_relu.negative_slope)
+        tab = pack = None
         if edge_feats is not None:
-            tab = relation_table(self.edge_weight, self.alpha)
-            e = e + tab[edge_feats - 1].reshape(e.size(0), H, 1)
-        a = self.attn_drop(edge_softmax(graph, e))
-        rst = ops.head_spmm(rg, a.reshape(rg.E, H)[rg.csr_eid], feat_src)
+            tab = relation_table(self.edge_weight, self.alpha)                     # :144-149
+            pack = rg.rel_pack(edge_feats, num_rel=self.num_etypes)
+        a = self.attn_drop(ops.edge_softmax_logits(rg, s, tab, pack))              # :152
+        rst = ops.head_spmm(rg, a, feat_src)                                       # :154-156
         if self.res_fc is not None:
-            rst = rst + self.res_fc(h_dst).view(h_dst.shape[0], -1, D)
+            rst = rst + self.res_fc(h_dst).view(h_dst.shape[0], -1, D)             # :158-160
         if self.activation:
             rst = self.activation(rst)
         if get_attention:
-            return rst, a
+            a_e = th.empty_like(a)
+            a_e[rg.csr_eid] = a                                                    # caller order
+            return rst, a_e.unsqueeze(-1)
         return rst

@@ -43,6 +43,13 @@ _SIG = {
     "regnn_spmm_fwd_fused": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P,
                               P, I32, P, P, I32, P, P, P, P, F32, I32, P], ctypes.c_int),
     "regnn_head_argmax": ([P, I64, I32, P, P, I32, P, P], ctypes.c_int),
+    "regnn_gatv2_score_fwd": ([P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
+    "regnn_gatv2_score_bwd_dst": ([P, P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P],
+                                  ctypes.c_int),
+    "regnn_gatv2_score_bwd_src": ([P, P, P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
+    "regnn_edge_softmax_fwd": ([P, P, P, P, P, F32, I64, I32, P, P], ctypes.c_int),
+    "regnn_edge_softmax_bwd": ([P, P, P, P, I64, I32, P, P, I32, P], ctypes.c_int),
+    "regnn_gat_scores": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_rel_reduce": ([P, I64, I32, P, I32, P], ctypes.c_int),
     "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P],

@@ -108,6 +108,8 @@ class ShardedInference:
 
     def __init__(self, model, rg, edge_type, node_type, local_node_idx, rank=0, world=1,
                  bounds=None):
+        if getattr(model, "model", "regcn") != "regcn":
+            raise NotImplementedError("sharded full-neighbour inference covers the REGCN model")
         if model.self_loop_type != 2:
             raise NotImplementedError("full-neighbour inference is built for self_loop_type=2 "
                                       "(the mag/regnn_ns.py default)")

@@ -61,6 +61,7 @@ class _Block:
         self.csr_idx = idx.to(torch.int32)
         perm = torch.sort(idx, stable=True)[1]
         self.csc_idx = dst_all[perm].to(torch.int32)
+        self.csc2csr = perm.to(torch.int32).contiguous()      # CSC position -> CSR position
         ccnt = torch.zeros(n_src, dtype=torch.int64, device=dev).index_add_(
             0, idx, torch.ones_like(idx))
         cptr = torch.zeros(n_src + 1, dtype=torch.int64, device=dev)
@@ -132,30 +133,155 @@ class REGCNConv(torch.nn.Module):
         return out
 
 
+def _block_of(x_src, x_dst, edge_index, edge_type, target_node_type, num_edge_types,
+              self_loop_type):
+    if isinstance(edge_index, tuple):           # pre-built (RelGraph, RelPack) block
+        return edge_index
+    return make_block(edge_index, edge_type, target_node_type, x_src.shape[0], x_dst.shape[0],
+                      num_edge_types, self_loop_type)
+
+
+class REGATConv(torch.nn.Module):
+    """mag/regnn_layers.py:153-315 (same constructor, parameters, state_dict and forward).
+
+    Scores LeakyReLU(rw[type] + att_src.x_src[u] + att_dst.x_dst[v]) and the ogbn-mag softmax
+    (one global max, + 1e-16, mag/utils.py:45-57) run as HIP kernels (regnn_gat_scores,
+    regnn_edge_softmax_fwd; backward regnn_gat_softmax_bwd + segment sums), the aggregation as
+    the HIP per-head SpMM."""
+
+    v2 = False
+
+    def __init__(self, in_channels, out_channels, num_node_types, num_edge_types, heads=1,
+                 scaling_factor=100., concat=True, negative_slope=0.2, dropout=0.0,
+                 residual=False, use_norm=None, self_loop_type=1, no_re=False):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.heads, self.concat = heads, concat
+        self.negative_slope, self.dropout = negative_slope, dropout
+        self.num_node_types, self.num_edge_types = num_node_types, num_edge_types
+        self.residual, self.use_norm, self.self_loop_type = residual, use_norm, self_loop_type
+        self.out_dim = heads * out_channels if concat else out_channels
+        self.lin_src = Linear(in_channels, heads * out_channels, bias=False)
+        self.lin_dst = self.lin_src                                          # :189
+        self.bias = Parameter(torch.Tensor(self.out_dim))
+        rw_dim = num_edge_types if self_loop_type in (1, 3) else num_edge_types + num_node_types
+        self.relation_weight = Parameter(torch.Tensor(rw_dim, heads), requires_grad=not no_re)
+        self.scaling_factor = scaling_factor
+        self._make_att()
+        if use_norm == 'bn':
+            self.norm = torch.nn.BatchNorm1d(self.out_dim)
+        elif use_norm == 'ln':
+            self.norm = torch.nn.LayerNorm(self.out_dim)
+        self.reset_parameters()
+
+    def _make_att(self):
+        self.att_src = Parameter(torch.Tensor(1, self.heads, self.out_channels))
+        self.att_dst = Parameter(torch.Tensor(1, self.heads, self.out_channels))
+
+    def _reset_att(self):
+        init.xavier_uniform_(self.att_src)
+        init.xavier_uniform_(self.att_dst)
+
+    def reset_parameters(self):
+        self.lin_src.reset_parameters()
+        self.lin_dst.reset_parameters()
+        self._reset_att()
+        init.zeros_(self.bias)
+        init.constant_(self.relation_weight, 1.0 / self.scaling_factor)
+        if self.use_norm in ('bn', 'ln'):
+            self.norm.reset_parameters()
+
+    def _attention(self, rg, pack, x_src, x_dst, tab):
+        a_s = (x_src * self.att_src).sum(dim=-1)                             # :289
+        a_d = (x_dst * self.att_dst).sum(dim=-1)                             # :290
+        return ops.gat_attention(rg, a_s, a_d, tab, pack, self.negative_slope,
+                                 global_max=True)                           # :298-307
+
+    def forward(self, x, edge_index, edge_type=None, target_node_type=None,
+                return_weights=False):
+        H, C = self.heads, self.out_channels
+        if isinstance(x, torch.Tensor):
+            x_src = x_dst = self.lin_src(x).view(-1, H, C)
+            n_dst = x.shape[0]
+        else:
+            xs_in, xd_in = x
+            x_src = self.lin_src(xs_in).view(-1, H, C)                       # :271-274
+            x_dst = self.lin_dst(xd_in).view(-1, H, C)
+            n_dst = xd_in.shape[0]
+        rg, pack = _block_of(x_src, x_dst, edge_index, edge_type, target_node_type,
+                             self.num_edge_types, self.self_loop_type)
+        assert rg.n_dst == n_dst
+        tab = F.leaky_relu(self.relation_weight * self.scaling_factor)       # :294-295
+        a = self._attention(rg, pack, x_src, x_dst, tab)
+        out = ops.head_spmm(rg, a, x_src)                                    # propagate :312
+        out = out.reshape(-1, H * C) if self.concat else out.mean(dim=1)     # :314-317
+        out = out + self.bias                                                # :319
+        if self.residual:
+            out = out + x_dst.reshape(-1, H * C)                             # :321-322
+        if self.use_norm in ('bn', 'ln'):
+            out = self.norm(out)                                             # :324-325
+        if return_weights:
+            ew = torch.empty_like(a)
+            if hasattr(rg, "csr_eid"):
+                ew[rg.csr_eid] = a                                           # caller edge order
+            else:
+                ew = a
+            return out, ew
+        return out
+
+
+class REGATv2Conv(REGATConv):
+    """mag/regnn_layers.py:318-436: score <att, LeakyReLU(x_src[u] + x_dst[v])> + rw[type] (HIP
+    GATv2 SDDMM, regnn_gatv2_score_*), the same global-max softmax (regnn_edge_softmax_*)."""
+
+    v2 = True
+
+    def _make_att(self):
+        self.att = Parameter(torch.Tensor(1, self.heads, self.out_channels))
+
+    def _reset_att(self):
+        init.xavier_uniform_(self.att)
+
+    def _attention(self, rg, pack, x_src, x_dst, tab):
+        s = ops.gatv2_scores(rg, x_src, x_dst, self.att, self.negative_slope)  # :399-404
+        return ops.edge_softmax_logits(rg, s, tab, pack, global_max=True)     # :407-413
+
+
 class REGNN(torch.nn.Module):
     """mag/regnn_ns.py:216-369 for model 'regcn' (feats_type != 2)."""
 
     def __init__(self, in_channels, hidden_channels, out_channels, num_layers, scaling_factor,
                  dropout, num_feature_dict, num_edge_types, residual=False, no_re=False,
-                 use_norm='ln', self_loop_type=2):
+                 use_norm='ln', self_loop_type=2, model='regcn', heads=8):
         super().__init__()
-        self.hidden_dim = hidden_channels
+        if model not in ('regcn', 'regat', 'regatv2'):
+            raise NotImplementedError(model)
+        self.model = model
+        self.hidden_dim = hidden_channels if model == 'regcn' else hidden_channels * heads
         self.num_layers, self.dropout = num_layers, dropout
         self.num_node_types = len(num_feature_dict)
         self.num_edge_types = num_edge_types
         self.self_loop_type = self_loop_type
-        self.lins = ModuleDict({str(k): Linear(d, hidden_channels)
+        self.lins = ModuleDict({str(k): Linear(d, self.hidden_dim)
                                 for k, d in num_feature_dict.items()})
-        self.convs = ModuleList([
-            REGCNConv(hidden_channels, hidden_channels, self.num_node_types, num_edge_types,
-                      scaling_factor, dropout=dropout, residual=residual, use_norm=use_norm,
-                      self_loop_type=self_loop_type, no_re=no_re)
-            for _ in range(num_layers)])
-        self.out_lin = Linear(hidden_channels, out_channels)
+        if model == 'regcn':                                                # regnn_ns.py:245-270
+            convs = [REGCNConv(hidden_channels, hidden_channels, self.num_node_types,
+                               num_edge_types, scaling_factor, dropout=dropout,
+                               residual=residual, use_norm=use_norm,
+                               self_loop_type=self_loop_type, no_re=no_re)
+                     for _ in range(num_layers)]
+        else:
+            cls = REGATConv if model == 'regat' else REGATv2Conv
+            convs = [cls(self.hidden_dim, hidden_channels, self.num_node_types, num_edge_types,
+                         heads, scaling_factor, dropout=dropout, residual=residual,
+                         use_norm=use_norm, self_loop_type=self_loop_type, no_re=no_re)
+                     for _ in range(num_layers)]
+        self.convs = ModuleList(convs)
+        self.out_lin = Linear(self.hidden_dim, out_channels)
         if use_norm == 'ln':
-            self.norm = torch.nn.LayerNorm(hidden_channels)   # declared, unused in forward
+            self.norm = torch.nn.LayerNorm(self.hidden_dim)   # declared, unused in forward
         elif use_norm == 'bn':
-            self.norm = torch.nn.BatchNorm1d(hidden_channels)
+            self.norm = torch.nn.BatchNorm1d(self.hidden_dim)
 
     def group_input(self, x_dict, node_type, local_node_idx, n_id=None):
         """mag/regnn_ns.py:300-326. When every type has the same feature width the per-type

@@ -302,15 +302,25 @@ def edge_spmm(rg, x, ew):
 # ---------------------------------------------------------------------------------------------
 class _GatAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, el, er, ee_tab, rg, pack, slope):
+    def forward(ctx, el, er, ee_tab, rg, pack, slope, global_max=False):
         el, er = el.contiguous().float(), er.contiguous().float()
         H = el.shape[1]
         a = torch.empty(rg.E, H, dtype=torch.float32, device=el.device)
         t = None if ee_tab is None else ee_tab.detach().float().contiguous()
-        with timed("gat_softmax_fwd", rg.E * (5 + 12 * H) + rg.n_dst * 8 * H):
-            L.call("regnn_gat_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
-                   L.ptr(pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
-                   L.ptr(er), rg.n_dst, H, float(slope), L.ptr(a), L.stream())
+        rel = L.ptr(pack.rel_csr if t is not None else None)
+        if global_max:
+            # mag/utils.py:45-57: ONE max over every edge and head, + 1e-16 in the denominator
+            s = torch.empty(rg.E, H, dtype=torch.float32, device=el.device)
+            L.call("regnn_gat_scores", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), rel, L.ptr(t),
+                   L.ptr(el), L.ptr(er), rg.n_dst, H, float(slope), L.ptr(s), L.stream())
+            gmax = s.amax().reshape(1) if s.numel() else torch.zeros(1, device=el.device)
+            L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), None, None,
+                   L.ptr(gmax), 1e-16, rg.n_dst, H, L.ptr(a), L.stream())
+        else:
+            with timed("gat_softmax_fwd", rg.E * (5 + 12 * H) + rg.n_dst * 8 * H):
+                L.call("regnn_gat_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), rel,
+                       L.ptr(t), L.ptr(el), L.ptr(er), rg.n_dst, H, float(slope), L.ptr(a),
+                       L.stream())
         ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
         ctx.tab_shape = None if ee_tab is None else ee_tab.shape
         ctx.save_for_backward(el, er, t, a)
@@ -334,12 +344,101 @@ class _GatAttention(torch.autograd.Function):
         L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
                L.ptr(gel), L.stream())
         g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
-        return gel, ger, g_tab, None, None, None
+        return gel, ger, g_tab, None, None, None, None
 
 
-def gat_attention(rg, el, er, ee_tab=None, pack=None, slope=0.2):
-    """a[e,h] (CSR edge order) = edge_softmax(leaky_relu(el[u]+er[v]+ee[rel_e], slope))."""
-    return _GatAttention.apply(el, er, ee_tab, rg, pack, slope)
+def gat_attention(rg, el, er, ee_tab=None, pack=None, slope=0.2, global_max=False):
+    """a[e,h] (CSR edge order) = edge_softmax(leaky_relu(el[u]+er[v]+ee[rel_e], slope)).
+
+    global_max: the ogbn-mag softmax (mag/utils.py:45-57, one max over all edges and heads,
+    + 1e-16 in the denominator). Its backward is the per-destination formula: the global max's
+    own gradient is 0 up to the 1e-16 term."""
+    return _GatAttention.apply(el, er, ee_tab, rg, pack, slope, global_max)
+
+
+# ---------------------------------------------------------------------------------------------
+class _GatV2Score(torch.autograd.Function):
+    """s[e,h] (CSR order) = <att[h], LeakyReLU(fs[u,h] + fd[v,h], slope)>."""
+
+    @staticmethod
+    def forward(ctx, fs, fd, att, rg, slope):
+        N, H, D = fs.shape
+        fs, fd = fs.contiguous().float(), fd.contiguous().float()
+        a = att.detach().reshape(H * D).contiguous().float()
+        s = torch.empty(rg.E, H, dtype=torch.float32, device=fs.device)
+        with timed("gatv2_score_fwd", rg.E * (H * D * 4 + 4 * H + 4) + rg.n_dst * H * D * 4):
+            L.call("regnn_gatv2_score_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(fs),
+                   L.ptr(fd), L.ptr(a), rg.n_dst, H, D, float(slope), L.ptr(s), L.stream())
+        ctx.rg, ctx.slope, ctx.att_shape = rg, slope, att.shape
+        ctx.save_for_backward(fs, fd, a)
+        return s
+
+    @staticmethod
+    def backward(ctx, gs):
+        fs, fd, a = ctx.saved_tensors
+        rg, slope = ctx.rg, ctx.slope
+        N, H, D = fs.shape
+        gs = gs.contiguous().float()
+        gfd = torch.empty_like(fd)
+        gfs = torch.empty_like(fs)
+        rows = L.slab_rows() // 2
+        slab = torch.zeros(rows, H * D, dtype=torch.float32, device=fs.device)
+        L.call("regnn_gatv2_score_bwd_dst", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(fs),
+               L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_dst, H, D, float(slope), L.ptr(gfd),
+               L.ptr(slab), rows, L.stream())
+        L.call("regnn_gatv2_score_bwd_src", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+               L.ptr(rg.csc2csr), L.ptr(fs), L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_src, H, D,
+               float(slope), L.ptr(gfs), L.stream())
+        g_att = _reduce(slab, H * D).view(ctx.att_shape)
+        return gfs, gfd, g_att, None, None
+
+
+def gatv2_scores(rg, fs, fd, att, slope=0.2):
+    """GATv2 attention logits per edge (CSR order): layer/REGATv2Conv.py:139-141."""
+    return _GatV2Score.apply(fs, fd, att, rg, slope)
+
+
+class _EdgeSoftmax(torch.autograd.Function):
+    """a = softmax over each destination's in-edges of z = s + ee[rel] (CSR order); per-segment
+    max (DGL) or one global max + 1e-16 (ogbn-mag, mag/utils.py:45-57)."""
+
+    @staticmethod
+    def forward(ctx, s, ee_tab, rg, pack, global_max):
+        s = s.contiguous().float()
+        H = s.shape[1]
+        t = None if ee_tab is None else ee_tab.detach().float().contiguous()
+        rel = pack.rel_csr if t is not None else None
+        a = torch.empty_like(s)
+        gmax = None
+        if global_max:
+            z = s if t is None else s + t[rel.long()]
+            gmax = z.amax().reshape(1) if z.numel() else torch.zeros(1, device=s.device)
+        L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), L.ptr(rel), L.ptr(t),
+               L.ptr(gmax), 1e-16 if global_max else 0.0, rg.n_dst, H, L.ptr(a), L.stream())
+        ctx.rg, ctx.pack = rg, pack
+        ctx.tab_shape = None if ee_tab is None else ee_tab.shape
+        ctx.save_for_backward(a)
+        return a
+
+    @staticmethod
+    def backward(ctx, ga):
+        (a,) = ctx.saved_tensors
+        rg, H = ctx.rg, a.shape[1]
+        gz = torch.empty_like(a)
+        need_tab = ctx.tab_shape is not None and ctx.needs_input_grad[1]
+        n_rel = ctx.tab_shape[0] if need_tab else 0
+        slab = _slab(n_rel * H, a.device) if need_tab else None
+        L.call("regnn_edge_softmax_bwd", L.ptr(rg.csr_ptr),
+               L.ptr(ctx.pack.rel_csr if need_tab else None), L.ptr(a),
+               L.ptr(ga.contiguous().float()), rg.n_dst, H, L.ptr(gz), L.ptr(slab), n_rel,
+               L.stream())
+        g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if need_tab else None
+        return gz, g_tab, None, None, None
+
+
+def edge_softmax_logits(rg, s, ee_tab=None, pack=None, global_max=False):
+    """edge softmax of per-edge logits s [E, H] (CSR order) plus the relation bias ee[rel]."""
+    return _EdgeSoftmax.apply(s, ee_tab, rg, pack, global_max)
 
 
 class _AttnDots(torch.autograd.Function):

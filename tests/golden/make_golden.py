@@ -381,9 +381,46 @@ def gen_layers_extra():
                lambda m, f: m(g, f, e_feat if use_ee else None))
 
 
+def gen_mag_gat():
+    """mag REGATConv / REGATv2Conv (mag/regnn_layers.py:153-436): global-max edge softmax."""
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+    rng = np.random.default_rng(40)
+    n_src, n_dst, E = 260, 90, 1400
+    num_node_types, num_edge_types = 4, 7
+    src = rng.integers(0, n_src, size=E).astype(np.int64)
+    dst = rng.integers(0, n_dst, size=E).astype(np.int64)
+    dst[np.isin(dst, [2, 11])] = 4                  # targets with only their self loop
+    edge_type = rng.integers(0, num_edge_types, size=E).astype(np.int64)
+    tnt = rng.integers(0, num_node_types, size=n_dst).astype(np.int64)
+    cases = [("regat", "REGATConv", 4, 16, False), ("regat", "REGATConv", 2, 32, True),
+             ("regatv2", "REGATv2Conv", 4, 16, False), ("regatv2", "REGATv2Conv", 2, 32, True)]
+    for tag, cls, H, C, residual in cases:
+        torch.manual_seed(9)
+        conv = getattr(regnn_layers, cls)(H * C, C, num_node_types, num_edge_types, heads=H,
+                                          scaling_factor=10.0, residual=residual,
+                                          use_norm="ln", self_loop_type=2)
+        _set_params(conv, rng, ew_alpha=10.0)
+        x = torch.from_numpy(f32(rng, n_src, H * C).astype(np.float64)).requires_grad_(True)
+        ei = torch.from_numpy(np.stack([src, dst]))
+        out = conv((x, x[:n_dst]), ei, torch.from_numpy(edge_type), torch.from_numpy(tnt))
+        gout = f32(rng, *out.shape)
+        out.backward(torch.from_numpy(gout.astype(np.float64)))
+        st = dict(src=src, dst=dst, edge_type=edge_type, target_node_type=tnt,
+                  x=x.detach().numpy().astype(np.float32), gout=gout, out=out, grad_x=x.grad)
+        _pack("p_", _params(conv), st)
+        _pack("grad_", _grads(conv), st)
+        save(f"mag_{tag}conv_h{H}_res{int(residual)}",
+             dict(layer=f"mag.{cls}", n_src=n_src, n_dst=n_dst, num_node_types=num_node_types,
+                  num_edge_types=num_edge_types, heads=H, out_channels=C, scaling_factor=10.0,
+                  residual=residual, use_norm="ln", self_loop_type=2, negative_slope=0.2), st)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float64)
-    which = sys.argv[1:] or ["layers", "models", "mag", "extra"]
+    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat"]
     if "layers" in which:
         gen_layers()
     if "models" in which:
@@ -392,3 +429,5 @@ if __name__ == "__main__":
         gen_mag()
     if "extra" in which:
         gen_layers_extra()
+    if "maggat" in which:
+        gen_mag_gat()

@@ -150,3 +150,21 @@ def test_dropout_mask_spec(keep16, ev):
     assert abs((c[1:] * c[:-1]).mean()) < 0.01 * keep
     m2 = O.dropout_mask(0xDEADBEEF12346, 4000, 16 * ev, ev, keep16)
     assert abs((m == m2).mean() - (keep ** 2 + (1 - keep) ** 2)) < 0.01
+
+
+@pytest.mark.parametrize("name", G.names("mag_regatconv_") + G.names("mag_regatv2conv_"))
+def test_mag_regatconv(name):
+    """mag REGATConv / REGATv2Conv with the global-max edge softmax."""
+    d = G.load(name)
+    m = d["meta"]
+    P = G.sub(d, "p_")
+    o = O.MagREGATConvOracle(v2="v2" in m["layer"], **m)
+    out = o.forward(d["x"].astype(np.float64), d["src"], d["dst"], d["edge_type"],
+                    d["target_node_type"], P)
+    _check("out", out, d["out"])
+    gx, gr = o.backward(d["gout"].astype(np.float64))
+    _check("grad_x", gx, d["grad_x"])
+    want = {k: v for k, v in G.sub(d, "grad_").items() if k != "x"}
+    assert set(want) == set(gr), set(want) ^ set(gr)
+    for k, v in want.items():
+        _check(k, gr[k], v)
