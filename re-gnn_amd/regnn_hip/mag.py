@@ -9,7 +9,7 @@ backward is the fused transposed SpMM + relation-bin SDDMM.
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
-from torch.nn import Linear, ModuleDict, ModuleList, Parameter, init
+from torch.nn import Linear, ModuleDict, ModuleList, Parameter, ParameterDict, init
 
 from . import ops
 from .graph import RelGraph, SegPlan
@@ -252,18 +252,29 @@ class REGNN(torch.nn.Module):
 
     def __init__(self, in_channels, hidden_channels, out_channels, num_layers, scaling_factor,
                  dropout, num_feature_dict, num_edge_types, residual=False, no_re=False,
-                 use_norm='ln', self_loop_type=2, model='regcn', heads=8):
+                 use_norm='ln', self_loop_type=2, model='regcn', heads=8, feats_type=3,
+                 num_nodes_dict=None, target_node_type=0):
         super().__init__()
         if model not in ('regcn', 'regat', 'regatv2'):
             raise NotImplementedError(model)
         self.model = model
+        self.in_channels = in_channels
         self.hidden_dim = hidden_channels if model == 'regcn' else hidden_channels * heads
         self.num_layers, self.dropout = num_layers, dropout
         self.num_node_types = len(num_feature_dict)
         self.num_edge_types = num_edge_types
         self.self_loop_type = self_loop_type
-        self.lins = ModuleDict({str(k): Linear(d, self.hidden_dim)
-                                for k, d in num_feature_dict.items()})
+        self.feats_type = feats_type
+        self._touched = {}
+        if feats_type == 2:
+            # learned per-type embeddings for every non-target type (regnn_ns.py:240-245)
+            self.emb_dict = ParameterDict({
+                str(k): Parameter(torch.Tensor(num_nodes_dict[k], in_channels))
+                for k in sorted(set(num_feature_dict) - {target_node_type})})
+            self.lin = Linear(in_channels, self.hidden_dim)
+        else:
+            self.lins = ModuleDict({str(k): Linear(d, self.hidden_dim)
+                                    for k, d in num_feature_dict.items()})
         if model == 'regcn':                                                # regnn_ns.py:245-270
             convs = [REGCNConv(hidden_channels, hidden_channels, self.num_node_types,
                                num_edge_types, scaling_factor, dropout=dropout,
@@ -282,6 +293,15 @@ class REGNN(torch.nn.Module):
             self.norm = torch.nn.LayerNorm(self.hidden_dim)   # declared, unused in forward
         elif use_norm == 'bn':
             self.norm = torch.nn.BatchNorm1d(self.hidden_dim)
+        if feats_type == 2:
+            for emb in self.emb_dict.values():                              # :289-292
+                init.xavier_uniform_(emb)
+
+    def embedding_tables(self):
+        """[(table parameter, local rows the last forward read)] of the feats_type-2 tables."""
+        if self.feats_type != 2:
+            return []
+        return [(emb, self._touched.get(k)) for k, emb in self.emb_dict.items()]
 
     def group_input(self, x_dict, node_type, local_node_idx, n_id=None):
         """mag/regnn_ns.py:300-326. When every type has the same feature width the per-type
@@ -289,6 +309,21 @@ class REGNN(torch.nn.Module):
         each node still gets exactly its own type's projection."""
         if n_id is not None:
             node_type, local_node_idx = node_type[n_id], local_node_idx[n_id]
+        if self.feats_type == 2:
+            # raw target features + learned embeddings of the other types, one shared Linear
+            # (regnn_ns.py:306-315); each table's rows read here are recorded for the
+            # sparse-row gradient all-reduce
+            t = torch.zeros(node_type.numel(), self.in_channels, device=node_type.device)
+            for key, x in x_dict.items():
+                idx = torch.nonzero(node_type == key).flatten()
+                t[idx] = x[local_node_idx[idx]].to(t.device)
+            self._touched = {}
+            for key, emb in self.emb_dict.items():
+                idx = torch.nonzero(node_type == int(key)).flatten()
+                rows = local_node_idx[idx]
+                self._touched[key] = rows
+                t = t.index_copy(0, idx, emb[rows])
+            return self.lin(t)
         keys = sorted(x_dict)
         dims = {x_dict[k].shape[1] for k in keys}
         if len(dims) == 1 and keys == list(range(len(keys))):
@@ -373,14 +408,56 @@ def flat_grad_allreduce(params, world):
         o += n
 
 
+def sparse_rows_allreduce(tables, world, group=None):
+    """SUM / world all-reduce of embedding-table gradients that are zero outside the rows each
+    rank touched (feats_type 2): every rank all-gathers the (row ids, grad
+    rows) of the others and adds them in rank order, so the traffic is the touched rows instead
+    of the whole table (~154 M parameters at the reference's defaults) and every rank ends with
+    the same dense gradient. tables: [(parameter, touched row ids)]."""
+    if world <= 1:
+        return
+    for p, rows in tables:
+        if p.grad is None:
+            continue
+        g = p.grad
+        rows = (torch.zeros(0, dtype=torch.int64, device=g.device) if rows is None
+                else rows.to(torch.int64))
+        vals = g[rows]
+        cnt = torch.tensor([rows.numel()], dtype=torch.int64, device=g.device)
+        cnts = torch.empty(world, dtype=torch.int64, device=g.device)
+        dist.all_gather_into_tensor(cnts, cnt, group=group)
+        cnts = cnts.tolist()
+        m = max(cnts)
+        if m == 0:
+            continue
+        r_pad = torch.zeros(m, dtype=torch.int64, device=g.device)
+        v_pad = torch.zeros(m, g.shape[1], dtype=g.dtype, device=g.device)
+        r_pad[:rows.numel()] = rows
+        v_pad[:rows.numel()] = vals
+        r_all = torch.empty(world * m, dtype=torch.int64, device=g.device)
+        v_all = torch.empty(world * m, g.shape[1], dtype=g.dtype, device=g.device)
+        dist.all_gather_into_tensor(r_all, r_pad, group=group)
+        dist.all_gather_into_tensor(v_all, v_pad, group=group)
+        g.index_fill_(0, rows, 0.0)
+        for r in range(world):                   # rank order: identical sums on every rank
+            rr = r_all[r * m:r * m + cnts[r]]
+            g.index_add_(0, rr, v_all[r * m:r * m + cnts[r]])
+        touched = torch.unique(torch.cat([r_all[r * m:r * m + cnts[r]] for r in range(world)]))
+        g[touched] /= world
+
+
 def train_step(model, opt, batch, x_dict, edge_type, node_type, local_node_idx, y_global, world):
-    """mag/regnn_ns.py:399-407 with the gradient all-reduce between backward and step."""
+    """mag/regnn_ns.py:399-407 with the gradient all-reduce between backward and step (dense
+    parameters in one flat bucket; feats_type-2 embedding tables by touched rows)."""
     batch_size, n_id, adjs = batch
     opt.zero_grad(set_to_none=True)
     out = model(n_id, x_dict, adjs, edge_type, node_type, local_node_idx)
     y = y_global[n_id][:batch_size].squeeze(-1)
     loss = F.nll_loss(out, y)
     loss.backward()
-    flat_grad_allreduce(list(model.parameters()), world)
+    tables = model.embedding_tables() if hasattr(model, "embedding_tables") else []
+    table_ids = {id(p) for p, _ in tables}
+    flat_grad_allreduce([p for p in model.parameters() if id(p) not in table_ids], world)
+    sparse_rows_allreduce(tables, world)
     opt.step()
     return loss

@@ -66,3 +66,32 @@ def test_dp_two_ranks():
     for r in range(world):
         for got, p in zip(out[r]["grads"], model.parameters()):
             assert torch.allclose(got, p.grad, atol=1e-6, rtol=1e-5)
+
+
+def _sparse_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from regnn_hip.mag import sparse_rows_allreduce
+    g = torch.Generator().manual_seed(10 + rank)
+    table = torch.nn.Parameter(torch.zeros(50, 6))
+    rows = torch.tensor([[1, 4, 7, 9, 30], [4, 5, 9, 49]][rank])        # overlapping rows
+    table.grad = torch.zeros(50, 6)
+    table.grad[rows] = torch.randn(rows.numel(), 6, generator=g)
+    dense = table.grad.clone()
+    dist.all_reduce(dense)
+    dense /= world
+    sparse_rows_allreduce([(table, rows)], world)
+    out[rank] = (table.grad.clone(), dense)
+    dist.destroy_process_group()
+
+
+def test_sparse_rows_allreduce_two_ranks():
+    """feats_type-2 embedding tables: the touched-rows exchange gives the
+    dense SUM / world all-reduce on every rank, identically."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sparse_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    (g0, d0), (g1, d1) = out[0], out[1]
+    assert torch.equal(g0, g1)
+    assert torch.allclose(g0, d0, atol=1e-6) and torch.allclose(g1, d1, atol=1e-6)

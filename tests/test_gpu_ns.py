@@ -113,3 +113,53 @@ def test_ns_training_step_reduces_loss():
                                                local, y, 1)))
     assert all(np.isfinite(losses))
     assert np.mean(losses[-3:]) < np.mean(losses[:3])
+
+
+def test_ns_feats_type2_embeddings():
+    """feats_type 2 (mag/regnn_ns.py:240-245,306-315): learned embeddings for the non-target
+    types + one shared Linear. group_input equals the spec's composition; the tables' gradients
+    live only on the rows the batch read (what sparse_rows_allreduce exchanges); loss falls."""
+    from regnn_hip import mag, synth
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.sampler import NeighborSampler
+    gd = synth.mag_like(0.003, seed=2, device=DEV)
+    keep = gd["rel"] <= 7
+    rg = RelGraph(gd["src"][keep], gd["dst"][keep], gd["N"], DEV)
+    edge_type = gd["rel"][keep].to(torch.int64) - 1
+    node_type = gd["ntype"]
+    offs = torch.tensor([gd["type_offsets"][t] for t in synth.NTYPES], device=DEV)
+    local = torch.arange(gd["N"], device=DEV) - offs[node_type]
+    n_paper = gd["counts"]["paper"]
+    x_dict = {0: torch.randn(n_paper, 16, device=DEV)}
+    nodes = {k: gd["counts"][t] for k, t in enumerate(synth.NTYPES)}
+    torch.manual_seed(0)
+    net = mag.REGNN(16, 32, 5, 2, 10.0, 0.0, {k: 16 for k in range(4)}, 7, use_norm="ln",
+                    self_loop_type=2, feats_type=2, num_nodes_dict=nodes,
+                    target_node_type=0).to(DEV)
+    assert set(net.emb_dict.keys()) == {"1", "2", "3"} and not hasattr(net, "lins")
+    smp = NeighborSampler(rg, torch.arange(n_paper, device=DEV), [8, 6], batch_size=128,
+                          shuffle=True, seed=1)
+    bs, n_id, adjs = next(iter(smp))
+    h = net.group_input(x_dict, node_type, local, n_id)
+    nt, loc = node_type[n_id].cpu(), local[n_id].cpu()
+    t = torch.zeros(n_id.numel(), 16, dtype=torch.float64)
+    t[nt == 0] = x_dict[0].cpu().double()[loc[nt == 0]]
+    for k in (1, 2, 3):
+        t[nt == k] = net.emb_dict[str(k)].detach().cpu().double()[loc[nt == k]]
+    ref = t @ net.lin.weight.detach().cpu().double().T + net.lin.bias.detach().cpu().double()
+    assert torch.allclose(h.detach().cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    y = torch.full((gd["N"], 1), -1, dtype=torch.int64, device=DEV)
+    y[:n_paper, 0] = (torch.arange(n_paper, device=DEV) * 3) % 5
+    opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+    net.train()
+    mag.train_step(net, opt, (bs, n_id, adjs), x_dict, edge_type, node_type, local, y, 1)
+    for p, rows in net.embedding_tables():
+        nz = torch.nonzero(p.grad.abs().sum(1)).flatten()
+        assert set(nz.tolist()) <= set(rows.tolist())
+    losses = []
+    for epoch in range(3):
+        smp.set_epoch(epoch)
+        for batch in smp:
+            losses.append(float(mag.train_step(net, opt, batch, x_dict, edge_type, node_type,
+                                               local, y, 1)))
+    assert np.mean(losses[-3:]) < np.mean(losses[:3])
