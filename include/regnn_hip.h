@@ -241,6 +241,18 @@ int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, cons
                    int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
                    float* p, float* loss_rows, hipStream_t stream);
 
+/* Backward of the fused output head from its softmax gradient p [n, C] (regnn_head_fwd), each
+ * part reading p once (fp32 MFMA):
+ *   gh (optional, [n, K], 16-byte aligned) = gscale[0] * p W   (gscale NULL: 1)
+ *   slab (optional): per-block partial rows [rows_used, Cp*K + Cp], Cp = 16 * ceil(C/16):
+ *     columns [0, Cp*K) hold (p^T h)[c][k] at c*K + k (d out_lin.weight), columns [Cp*K, +Cp)
+ *     the column sums of p (d out_lin.bias). At most slab_rows rows are written: zero the slab
+ *     first and reduce its slab_rows rows with regnn_rel_reduce (fixed order).
+ *     K must be 64, C <= 384. */
+int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
+                   const float* h, const float* gscale, float* gh, float* slab, int32_t slab_rows,
+                   hipStream_t stream);
+
 /* Inference head (mag/regnn_ns.py:367 out_lin over every node, then the caller's argmax,
  * regnn_ns.py:379): out[r] = argmax_c (h[r] W^T + b)[c] (first maximal class, as torch.argmax),
  * fp32 MFMA as regnn_head_fwd, without writing the [rows, C] logits. K must be 64, C <= 384. */

@@ -270,6 +270,176 @@ int launch_head(const float* h, int64_t rows, const float* W, const float* b, in
 #undef HEAD_V
 }
 
+// ---------------------------------------------------------------------------------------------
+// Output-head backward (run_regnn.py:146-148 through out_lin), from the scaled softmax gradient
+// p [n, C] of regnn_head_fwd, each kernel reading p once:
+//   head_gh_kernel    gh = gscale * p W          [n, 64]  (d loss / d h of the loss rows)
+//   head_wgrad_kernel gW = p^T h, gb = colsum(p)  per-block partial slab rows (fixed-order reduce)
+// fp32 MFMA v_mfma_f32_16x16x4_f32 (exact f32 products, fp32 accumulation).
+//
+// gh is computed transposed (gh^T = W^T p^T) with the same operand trick as head_fwd: k-step
+// (t, i) takes class 16 t + 4 q + i from lane quarter q, so the B operand is component i of the
+// lane's 16-byte load p[row][16 t + 4 q ..] and W^T comes from LDS; each lane ends with 4
+// consecutive k of its row per 16-k tile (16-byte stores).
+template <int NT>
+__global__ void __launch_bounds__(kHeadBlock)
+head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ W,
+               const float* __restrict__ gscale, float* __restrict__ gh) {
+    constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;
+    extern __shared__ float Wl[];
+    for (int idx = threadIdx.x; idx < CP * K; idx += blockDim.x) {
+        const int j = idx / K, k = idx - j * K;
+        Wl[k * LDW + j] = j < C ? W[(int64_t)j * K + k] : 0.f;
+    }
+    __syncthreads();
+    const float sc = gscale ? *gscale : 1.f;
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int wpb = blockDim.x >> 6;
+    const int64_t n_tiles = (n + 15) / 16;
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
+         tile += (int64_t)gridDim.x * wpb) {
+        const int64_t row = tile * 16 + c;
+        const bool valid = row < n;
+        const float* pr = p + (valid ? row : 0) * C + 4 * q;
+        f32x4 pv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (16 * t + 16 <= C) {
+                pv[t] = *reinterpret_cast<const f32x4_u*>(pr + 16 * t);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pv[t][i] = 16 * t + 4 * q + i < C ? pr[16 * t + i] : 0.f;
+            }
+            if (!valid) pv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        f32x4 acc[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        Wl[(16 * kt + c) * LDW + 16 * t + 4 * q + i], pv[t][i], acc[kt], 0, 0, 0);
+        if (valid) {
+            float* gr = gh + row * K + 4 * q;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+                *reinterpret_cast<f32x4*>(gr + 16 * kt) = acc[kt] * sc;
+        }
+    }
+}
+
+// gW^T partial of this block's row range: wave w owns class tiles w, w + 8, w + 16; per 4-row
+// k-step lane (q, c) feeds A = p[row0 + q][16 t + c] and B = h[row0 + q][16 j + c], so D[cls][k]
+// accumulates over the rows; gb rides along in VALU adds of the same A values. 8 k-steps
+// (32 rows) of loads are issued before their MFMAs.
+template <int NT>
+__global__ void __launch_bounds__(kHeadBlock)
+head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ h,
+                  int64_t rows_per_block, float* __restrict__ slab) {
+    constexpr int K = kHeadK, CP = NT * 16, MT = (NT + 7) / 8, KS = 8;
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(n, r0 + rows_per_block);
+    f32x4 acc[MT][4];
+    float gb[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        gb[m] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int64_t row0 = r0; row0 < r1; row0 += 4 * KS) {
+        float a[KS][MT], b[KS][4];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int64_t rr = row0 + 4 * s + q;
+            const bool ok = rr < r1;
+            const int64_t rc = ok ? rr : r0;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const int cls = 16 * (w + 8 * m) + c;
+                const bool in = ok && (w + 8 * m) < NT && cls < C;
+                const float v = p[rc * C + (cls < C ? cls : 0)];
+                a[s][m] = in ? v : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = h[rc * K + 16 * j + c];
+                b[s][j] = ok ? v : 0.f;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                gb[m] += a[s][m];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][m], b[s][j], acc[m][j],
+                                                                     0, 0, 0);
+            }
+    }
+    float* out = slab + (int64_t)blockIdx.x * (CP * K + CP);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int t = w + 8 * m;
+        if (t >= NT) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(16 * t + 4 * q + r) * K + 16 * j + c] = acc[m][j][r];
+        float g = gb[m];
+        g += __shfl_xor(g, 16, 64);
+        g += __shfl_xor(g, 32, 64);
+        if (q == 0) out[CP * K + 16 * t + c] = g;
+    }
+}
+
+template <int NT>
+int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const float* h,
+                    const float* gscale, float* gh, float* slab, int slab_rows,
+                    hipStream_t stream) {
+    constexpr int K = kHeadK;
+    if (gh) {
+        const size_t lds = (size_t)K * (NT * 16 + 1) * sizeof(float);
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_gh_kernel<NT>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds) != hipSuccess)
+                return REGNN_ELAUNCH;
+            attr = true;
+        }
+        const int64_t tiles = (n + 15) / 16;
+        int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
+        const int cap = resident_blocks(reinterpret_cast<const void*>(&head_gh_kernel<NT>), lds,
+                                        kHeadBlock);
+        if (grid > cap) grid = cap;
+        if (grid < 1) grid = 1;
+        hipLaunchKernelGGL((head_gh_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
+                           stream, p, n, C, W, gscale, gh);
+        REGNN_LAUNCH_CHECK();
+    }
+    if (slab) {
+        int64_t grid = slab_rows;
+        const int64_t rpb_min = 256;
+        if (grid * rpb_min > n) grid = (n + rpb_min - 1) / rpb_min;
+        if (grid < 1) grid = 1;
+        int64_t rpb = (n + grid - 1) / grid;
+        rpb = (rpb + 31) / 32 * 32;
+        grid = (n + rpb - 1) / rpb;
+        if (grid < 1) grid = 1;
+        hipLaunchKernelGGL((head_wgrad_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
+                           stream, p, n, C, h, rpb, slab);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -334,6 +504,25 @@ int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, c
         AMAX_CASE(13) AMAX_CASE(14) AMAX_CASE(15) AMAX_CASE(16) AMAX_CASE(17) AMAX_CASE(18)
         AMAX_CASE(19) AMAX_CASE(20) AMAX_CASE(21) AMAX_CASE(22) AMAX_CASE(23) AMAX_CASE(24)
 #undef AMAX_CASE
+        default: return REGNN_EINVAL;
+    }
+}
+
+int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
+                   const float* h, const float* gscale, float* gh, float* slab, int32_t slab_rows,
+                   hipStream_t stream) {
+    if (!p || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || (gh && !W) ||
+        (slab && (!h || slab_rows <= 0)) || (gh && (reinterpret_cast<uintptr_t>(gh) & 15)))
+        return REGNN_EINVAL;
+    if (n == 0) return REGNN_OK;
+    switch ((C + 15) / 16) {
+#define HB_CASE(nt) \
+        case nt: return launch_head_bwd<nt>(p, n, C, W, h, gscale, gh, slab, slab_rows, stream);
+        HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
+        HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
+        HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)
+        HB_CASE(19) HB_CASE(20) HB_CASE(21) HB_CASE(22) HB_CASE(23) HB_CASE(24)
+#undef HB_CASE
         default: return REGNN_EINVAL;
     }
 }

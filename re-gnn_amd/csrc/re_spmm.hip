@@ -628,6 +628,26 @@ rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
     }
 }
 
+// wide slabs (per-block partials of a whole weight matrix): one thread per column walks the
+// rows in order, so a warp reads consecutive columns of one row (coalesced), fixed order
+__global__ void __launch_bounds__(kBlock)
+rel_reduce_wide_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
+                       float* __restrict__ out, int32_t accumulate) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= width) return;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = 0;
+    for (; r + 4 <= n_rows; r += 4) {
+        s0 += slab[r * width + k];
+        s1 += slab[(r + 1) * width + k];
+        s2 += slab[(r + 2) * width + k];
+        s3 += slab[(r + 3) * width + k];
+    }
+    for (; r < n_rows; ++r) s0 += slab[r * width + k];
+    const float t = (s0 + s1) + (s2 + s3);
+    out[k] = accumulate ? out[k] + t : t;
+}
+
 int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
 int64_t g_tune_head = 0;
@@ -895,8 +915,12 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
 int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
                      int32_t accumulate, hipStream_t stream) {
     if (!slab || !out || width <= 0 || n_rows < 0) return REGNN_EINVAL;
-    hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(kBlock), 0, stream, slab, n_rows, width,
-                       out, accumulate);
+    if (width >= 4096)
+        hipLaunchKernelGGL(rel_reduce_wide_kernel, dim3((width + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, stream, slab, n_rows, width, out, accumulate);
+    else
+        hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(kBlock), 0, stream, slab, n_rows,
+                           width, out, accumulate);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

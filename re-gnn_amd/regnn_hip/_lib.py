@@ -42,6 +42,7 @@ _SIG = {
                                ctypes.c_int),
     "regnn_spmm_fwd_fused": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P,
                               P, I32, P, P, I32, P, P, P, P, F32, I32, P], ctypes.c_int),
+    "regnn_head_bwd": ([P, I64, I32, I32, P, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_head_argmax": ([P, I64, I32, P, P, I32, P, P], ctypes.c_int),
     "regnn_gatv2_score_fwd": ([P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
     "regnn_gatv2_score_bwd_dst": ([P, P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P],

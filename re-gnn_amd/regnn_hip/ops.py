@@ -570,17 +570,45 @@ class _HeadCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _g_logits, g_loss):
         h, W, p = ctx.saved_tensors
-        n = p.shape[0]
+        n, C = p.shape
+        K = h.shape[1]
         gh = gW = gb = None
         if g_loss is None:
             return None, None, None, None
-        if ctx.needs_input_grad[0]:
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if head_fused(K, C) and h.dtype == torch.float32:
+            # regnn_head_bwd: gh = g_loss * p W and the (p^T h | colsum p) slab, p read once each
+            # gh = g_loss * p W on hipBLASLt (it ran this GEMM faster than regnn_head_bwd's gh:
+            # 3.6 vs 5.0 ms at mag-10x, tools/ab_head_bwd.py); d weight and d bias come from
+            # regnn_head_bwd's one pass over p (the chunked bmm + col_sum read p twice)
+            Cp = 16 * ((C + 15) // 16)
+            rows = 2048
+            slab = (torch.zeros(rows, Cp * K + Cp, dtype=torch.float32, device=p.device)
+                    if (need_w or need_b) else None)
+            if need_h:
+                gh = torch.empty_like(h)
+                gh[n:].zero_()
+                torch.mm(p, W * g_loss, out=gh[:n])
+            hc = h.contiguous()
+            if slab is not None:
+                with timed("head_bwd", 4 * (p.numel() + n * K)):
+                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, None, L.ptr(hc), None, None,
+                           L.ptr(slab), rows, L.stream())
+            if slab is not None:
+                tot = _reduce(slab, Cp * K + Cp)
+                if need_w:
+                    gW = tot[:Cp * K].view(Cp, K)[:C] * g_loss
+                if need_b:
+                    gb = tot[Cp * K:Cp * K + C] * g_loss
+            return gh, gW, gb, None
+        if need_h:
             gh = torch.empty_like(h)
             gh[n:].zero_()
             torch.mm(p, W * g_loss, out=gh[:n])      # g_loss folded into the C x K weight
-        if ctx.needs_input_grad[1]:
+        if need_w:
             gW = batched_wgrad(p, h[:n]) * g_loss
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if need_b:
             gb = col_sum(p) * g_loss
         return gh, gW, gb, None
 

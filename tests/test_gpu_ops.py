@@ -114,7 +114,8 @@ def test_col_sum(rows, cols):
                                      (1001, 64, 3, 1001),       # 1 col tile, every row a loss row
                                      (77, 64, 384, 5),          # 12 col tiles, ragged tile tails
                                      (300, 64, 33, 31),     # C just past one tile
-                                     (640, 32, 349, 100)])      # K != 64: GEMM + softmax_xent
+                                     (640, 32, 349, 100),       # K != 64: GEMM + softmax_xent
+                                     (200_000, 64, 349, 150_000)])  # many rows per wgrad block
 def test_head_ce_matches_autograd(bias, N, D, C, n):
     """ops.head_ce == out_lin over all rows + cross_entropy(logits[:n], y) (run_regnn.py:146-148)."""
     from regnn_hip import ops
