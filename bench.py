@@ -73,6 +73,10 @@ def build_workload(args, dev):
         g, rg, e_feat = _full_graph(gd, dev)
         net = nets.REGCN(g, gd["R"], 100.0, 64, 64, n_classes, 2, F.elu, args.dropout,
                          [f.shape[1] for f in feats]).to(dev)
+        if args.dtype == "bf16":
+            # BASELINE configs[1]: bf16 feature storage (input features, hidden rows), fp32 master
+            # weights, fp32 accumulation in every kernel
+            feats = [f.to(torch.bfloat16) for f in feats]
         convs, kern = 2, ("spmm_fwd", "spmm_bwd")
     elif wl == "acm":
         gd = synth.acm_like(seed=0, device=dev)
@@ -104,7 +108,7 @@ def build_workload(args, dev):
         # run_regnn.py:146-150: logits = net(...) over all nodes, CE on the train rows, backward,
         # Adam. ops.head_ce computes the same logits / loss / gradients without the all-rows
         # zero-filled logits gradient (tests/test_gpu_ops.py::test_head_ce checks it vs autograd)
-        _, loss = ops.head_ce(net.embed(feats, e_feat), W, b, labels)
+        _, loss = ops.head_ce(net.embed(feats, e_feat).float(), W, b, labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
@@ -248,6 +252,9 @@ def main():
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="capture the whole train step in a HIP graph and replay it "
                          "(auto: on for the launch-bound small graphs dblp/acm/imdb)")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="feature storage type of the REGCN workloads (mag, dblp); fp32 is the "
+                         "reference's arithmetic and the default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -356,7 +363,7 @@ def main():
         "higher_is_better": True,
         "scaling": w.get("scaling", "weak"),
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": args.dtype if args.workload in ("mag", "dblp") else "fp32",
         "data": "synthetic (seeded multi-relation graph of the BASELINE shape, random features/labels)",
         "config": {
             "workload": desc, "nodes": w["N"], "edges": w["E"], "relations": w["R"],

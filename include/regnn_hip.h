@@ -129,7 +129,7 @@ int regnn_spmm_fwd_fused(const int32_t* ptr, const int32_t* idx, const uint8_t* 
  * multiple of 256 (p = 0.5, 0.25, ...), 8-bit draws: f = v*EV + 4k + b keeps iff byte b of h_k
  * is < drop_keep16 / 256 (same keep probability, half the hashing). Kept values are scaled by
  * drop_scale.
- * Rows must be 16 vectors (F = 64 fp32 / 128 bf16), else REGNN_EUNSUPPORTED. */
+ * Rows must be 16 or 8 vectors (F = 64 fp32; 64 or 128 bf16), else REGNN_EUNSUPPORTED. */
 int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            const float* rel_table, const float* edge_w,
                            const float* in_scale, const float* out_scale, const float* bias,

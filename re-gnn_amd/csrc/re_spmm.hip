@@ -517,8 +517,12 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
     constexpr int EV = Vec<T>::N;
     if (a.F <= 0 || a.F % EV) return REGNN_EUNSUPPORTED;
     const int nvec = a.F / EV;
-    if (a.drop_seed && nvec != 16) return REGNN_EUNSUPPORTED;   // fused dropout: 256-byte rows
+    if (a.drop_seed && nvec != 16 && nvec != 8) return REGNN_EUNSUPPORTED;   // fused dropout
     if (nvec <= 4) return launch_mode<T, 4, 1>(a, mode, stream);
+    if (nvec == 8 && a.drop_seed) {          // F = 64 bf16: fused dropout on 128-byte rows
+        if ((a.drop_thresh & 0xFFu) == 0) return launch_mode<T, 8, 1, 0, true, 8>(a, mode, stream);
+        return launch_mode<T, 8, 1, 0, true, 16>(a, mode, stream);
+    }
     if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
     if (nvec == 16) return launch_f16v<T>(a, mode, stream);
     if (nvec <= 16) return launch_mode<T, 16, 1>(a, mode, stream);

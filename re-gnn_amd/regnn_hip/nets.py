@@ -47,7 +47,9 @@ class _TypeProjFn(torch.autograd.Function):
         out = torch.empty(sum(rows), Ws[0].shape[0], dtype=xs[0].dtype, device=xs[0].device)
         o = 0
         for x, W, b, r in zip(xs, Ws, bs, rows):
-            torch.addmm(b, x, W.t(), out=out[o:o + r])
+            # reduced-precision feature storage (bench --dtype bf16): the fp32 master weights are
+            # cast for the GEMM (fp32 accumulation), gradients return in the weights' dtype
+            torch.addmm(b.to(x.dtype), x, W.t().to(x.dtype), out=out[o:o + r])
             o += r
         ctx.n, ctx.rows = n, rows
         ctx.save_for_backward(*xs, *Ws)
@@ -65,11 +67,11 @@ class _TypeProjFn(torch.autograd.Function):
             gt = g[o:o + r]
             o += r
             if ctx.needs_input_grad[1 + t]:
-                gx[t] = gt @ Ws[t]
+                gx[t] = gt @ Ws[t].to(gt.dtype)
             if ctx.needs_input_grad[1 + n + t]:
-                gW[t] = ops.batched_wgrad(gt, xs[t])
+                gW[t] = ops.batched_wgrad(gt, xs[t]).to(Ws[t].dtype)
             if ctx.needs_input_grad[1 + 2 * n + t]:
-                gb[t] = ops.col_sum(gt) if gt.is_cuda else gt.sum(0)
+                gb[t] = ops.col_sum(gt) if gt.is_cuda else gt.sum(0).to(Ws[t].dtype)
         return (None, *gx, *gW, *gb)
 
 

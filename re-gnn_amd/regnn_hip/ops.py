@@ -111,8 +111,10 @@ _DROP_CTR = {}
 
 
 def dropout_fusable(x):
-    """the fused-dropout SpMM kernels take 256-byte rows (F = 64 fp32 / 128 bf16)."""
-    return x.is_cuda and x.dim() == 2 and x.shape[1] * x.element_size() == 256
+    """the fused-dropout SpMM kernels take rows of 8 or 16 16-byte vectors (F = 64 fp32 / 64 or
+    128 bf16)."""
+    return x.is_cuda and x.dim() == 2 and x.shape[1] * x.element_size() in (128, 256) and \
+        x.dtype in (torch.float32, torch.bfloat16)
 
 
 def drop_request(p, device, seed=None):

@@ -21,7 +21,8 @@ def _graph(n=700, m=9000, R=6, hub=600, seed=0):
     return src, dst, rel, n, R
 
 
-@pytest.mark.parametrize("dtype,F", [(torch.float32, 64), (torch.bfloat16, 128)])
+@pytest.mark.parametrize("dtype,F", [(torch.float32, 64), (torch.bfloat16, 128),
+                                     (torch.bfloat16, 64), (torch.float32, 32)])
 @pytest.mark.parametrize("p", [0.5, 0.3, 0.75])
 def test_fused_dropout_matches_masked_composition(dtype, F, p):
     from regnn_hip import ops
@@ -95,3 +96,35 @@ def test_regcn_training_uses_fused_dropout():
     net.eval()
     e1, e2 = net.embed(feats, e_feat), net.embed(feats, e_feat)
     assert torch.equal(e1, e2)
+
+
+def test_regcn_bf16_storage_matches_fp32():
+    """bench --dtype bf16 (BASELINE configs[1]): bf16 feature storage, fp32 master weights and
+    accumulation; logits and weight gradients within bf16 tolerance of the fp32 model."""
+    import torch.nn.functional as F
+    import dgl
+    from regnn_hip import nets, ops
+    src, dst, rel, n, R = _graph(seed=5)
+    loops = np.arange(n)
+    g = dgl.DGLGraph((np.concatenate([src, loops]), np.concatenate([dst, loops])),
+                     num_nodes=n).to(DEV)
+    e_feat = torch.from_numpy(np.concatenate([rel, np.full(n, R)])).to(DEV)
+    torch.manual_seed(0)
+    net = nets.REGCN(g, R, 100.0, 64, 64, 3, 2, F.elu, 0.0, [16]).to(DEV).eval()
+    feats = [torch.randn(n, 16, device=DEV)]
+    labels = torch.randint(0, 3, (n // 2,), device=DEV)
+    W, b = net.head()
+    out = {}
+    for dt in (torch.float32, torch.bfloat16):
+        net.zero_grad()
+        h = net.embed([f.to(dt) for f in feats], e_feat)
+        assert h.dtype == dt
+        _, loss = ops.head_ce(h.float(), W, b, labels)
+        loss.backward()
+        out[dt] = (h.float().detach(), {k: p.grad.clone() for k, p in net.named_parameters()})
+    h32, g32 = out[torch.float32]
+    h16, g16 = out[torch.bfloat16]
+    rel_err = lambda a, b: float((a - b).abs().max()) / max(1e-6, float(b.abs().max()))
+    assert rel_err(h16, h32) < 2e-2
+    for k in g32:
+        assert rel_err(g16[k], g32[k]) < 5e-2, k
