@@ -333,11 +333,12 @@ def main():
     # FETCH_SIZE and WRITE_SIZE in separate runs, calibrated on a 4 GiB copy), valid only for the
     # exact graph it was measured on
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.dtype}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if rec.get("graph") == {"N": rg.n_dst, "E": rg.E} and dom in rec:
+        if rec.get("graph") == {"N": rg.n_dst, "E": rg.E} and rec.get("dtype") == args.dtype \
+                and dom in rec:
             traffic = rec[dom]["bytes_per_launch"]
 
     desc = {

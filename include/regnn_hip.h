@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 4). */
+/* ABI version (bumped on any signature change or addition; currently 5). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -139,6 +139,19 @@ int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                            float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                            const int64_t* level_desc, const uint64_t* drop_seed,
                            uint32_t drop_keep16, float drop_scale, hipStream_t stream);
+
+/* out[u][:] = (scale ? scale[u] : 1) * drop(x[u][:]) for n_rows rows of F features (dtype as
+ * x; out may not alias x). drop is the regnn_spmm_fwd_dropout mask (same seed / threshold / scale,
+ * same (row, vector) counter), or none when drop_seed is NULL. With z and dot (both or neither):
+ * dot[u] = <x[u], z[u]> / scale[u] (fp32 accumulation).
+ * Forward: the input pre-scale of layer/REGraphConv.py:73-76 (feat * norm) with the feat_dropout
+ * of :56 in front of it, applied once per node so the aggregation gathers finished rows (no
+ * per-edge mask hashing, no per-edge norm lookup); regnn_spmm_bwd_dropout with the same seed is
+ * its backward. Backward: g * norm (post-scale side) with dot = <g, y> / norm, the output-side
+ * term of d loss / d norm (layer/REGraphConv.py:97-98). */
+int regnn_row_scale(const void* x, const float* scale, void* out, int64_t n_rows, int32_t F,
+                    int32_t dtype, const uint64_t* drop_seed, uint32_t drop_keep16,
+                    float drop_scale, const void* z, float* dot, hipStream_t stream);
 
 /* Relation-embedding SpMM, fused backward over the transposed graph (CSC: segment = source u).
  * Replaces DGL GSpMM.backward (gspmm on the reverse graph + gsddmm 'dot' for the edge weight)

@@ -652,6 +652,88 @@ rel_reduce_wide_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t w
     out[k] = accumulate ? out[k] + t : t;
 }
 
+// out[u] = scale[u] * drop(x[u]) and optionally dot[u] = <x[u], z[u]> / scale[u]; LPR lanes per
+// row, 16 bytes per lane per step (streaming, coalesced). The aggregation then gathers finished
+// rows: the dropout mask is hashed N*F times instead of E*F (once per gathered edge) and the
+// per-edge scale lookup leaves the gather's dependent load chain. The mask is the
+// regnn_spmm_fwd_dropout spec (row, vector index of the row), so regnn_spmm_bwd_dropout with the
+// same seed differentiates it. The dot is the output-side norm gradient <g, y_raw> = <g, y>/post
+// of the backward, formed here while g streams by.
+template <typename T, int LPR, int DROP>
+__global__ void __launch_bounds__(kBlock)
+row_scale_kernel(const T* __restrict__ x, const float* __restrict__ scale, T* __restrict__ out,
+                 int64_t n_rows, int32_t nvec, const uint64_t* __restrict__ drop_seed,
+                 uint32_t drop_thresh, float drop_scale, const T* __restrict__ z,
+                 float* __restrict__ dot) {
+    constexpr int EV = Vec<T>::N;
+    constexpr int GPB = kBlock / LPR;
+    const int lane = threadIdx.x & (LPR - 1);
+    uint32_t key = 0;
+    if constexpr (DROP) key = drop_key(drop_seed);
+    for (int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; row < n_rows;
+         row += (int64_t)gridDim.x * GPB) {
+        const float s = scale ? scale[row] : 1.f;
+        float d = 0.f;
+        for (int vec = lane; vec < nvec; vec += LPR) {
+            const int64_t o = (row * nvec + vec) * EV;
+            float v[EV];
+            Vec<T>::load(x + o, v);
+            if (dot) {
+                float w[EV];
+                Vec<T>::load(z + o, w);
+#pragma unroll
+                for (int t = 0; t < EV; ++t) d = fmaf(v[t], w[t], d);
+            }
+#pragma unroll
+            for (int t = 0; t < EV; ++t) v[t] *= s;
+            if constexpr (DROP) drop_apply<EV, DROP>(key, drop_thresh, drop_scale, row, nvec, vec, v);
+            Vec<T>::store(out + o, v);
+        }
+        if (dot) {
+            d = group_sum<LPR>(d);
+            if (lane == 0) dot[row] = d / s;
+        }
+    }
+}
+
+template <typename T, int LPR>
+int launch_row_scale_lpr(const T* x, const float* scale, T* out, int64_t n_rows, int nvec,
+                         const uint64_t* seed, uint32_t keep16, float dscale, const T* z,
+                         float* dot, hipStream_t stream) {
+    constexpr int GPB = kBlock / LPR;
+#define REGNN_ROW_SCALE(D)                                                                       \
+    hipLaunchKernelGGL((row_scale_kernel<T, LPR, D>),                                            \
+                       dim3(grid_resident(row_scale_kernel<T, LPR, D>, n_rows, GPB, 0)),         \
+                       dim3(kBlock), 0, stream, x, scale, out, n_rows, nvec, seed, keep16, dscale, \
+                       z, dot)
+    if (!seed) REGNN_ROW_SCALE(0);
+    else if ((keep16 & 0xFFu) == 0) REGNN_ROW_SCALE(8);
+    else REGNN_ROW_SCALE(16);
+#undef REGNN_ROW_SCALE
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+template <typename T>
+int launch_row_scale(const void* x, const float* scale, void* out, int64_t n_rows, int32_t F,
+                     const uint64_t* seed, uint32_t keep16, float dscale, const void* z,
+                     float* dot, hipStream_t stream) {
+    constexpr int EV = Vec<T>::N;
+    if (F % EV) return REGNN_EUNSUPPORTED;
+    const int nvec = F / EV;
+    const T* xs = static_cast<const T*>(x);
+    const T* zs = static_cast<const T*>(z);
+    T* o = static_cast<T*>(out);
+    if (nvec <= 4)
+        return launch_row_scale_lpr<T, 4>(xs, scale, o, n_rows, nvec, seed, keep16, dscale, zs, dot,
+                                          stream);
+    if (nvec <= 8)
+        return launch_row_scale_lpr<T, 8>(xs, scale, o, n_rows, nvec, seed, keep16, dscale, zs, dot,
+                                          stream);
+    return launch_row_scale_lpr<T, 16>(xs, scale, o, n_rows, nvec, seed, keep16, dscale, zs, dot,
+                                       stream);
+}
+
 int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
 int64_t g_tune_head = 0;
@@ -687,7 +769,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 4; }
+int regnn_abi_version(void) { return 5; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -876,6 +958,22 @@ int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                          n_rel, edge_grad, node_grad, n_seg, F, dtype, split, chunk, long_ids,
                          n_long, chunk_long, chunk_off, n_chunk, chunk_partial, level_sb,
                          n_levels, level_desc, drop_seed, drop_keep16, drop_scale, stream);
+}
+
+int regnn_row_scale(const void* x, const float* scale, void* out, int64_t n_rows, int32_t F,
+                    int32_t dtype, const uint64_t* drop_seed, uint32_t drop_keep16,
+                    float drop_scale, const void* z, float* dot, hipStream_t stream) {
+    if (n_rows < 0 || F <= 0 || (n_rows > 0 && (!x || !out))) return REGNN_EINVAL;
+    if (drop_seed && drop_keep16 > 65536u) return REGNN_EINVAL;
+    if ((dot != nullptr) != (z != nullptr)) return REGNN_EINVAL;
+    if (n_rows == 0) return REGNN_OK;
+    if (dtype == REGNN_F32)
+        return launch_row_scale<float>(x, scale, out, n_rows, F, drop_seed, drop_keep16,
+                                       drop_scale, z, dot, stream);
+    if (dtype == REGNN_BF16)
+        return launch_row_scale<bf16_t>(x, scale, out, n_rows, F, drop_seed, drop_keep16,
+                                        drop_scale, z, dot, stream);
+    return REGNN_EUNSUPPORTED;
 }
 
 int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table, int64_t n_seg,

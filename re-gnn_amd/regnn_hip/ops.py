@@ -134,6 +134,30 @@ def drop_request(p, device, seed=None):
     return seed, int(round(keep * 65536)), 1.0 / keep
 
 
+# Forward pre-scale policy of _ReSpmm: "auto" | "on" | "off" (tools/ab_spmm.py flips it).
+# "on": pre * drop(x) is formed once per source row by regnn_row_scale and the aggregation
+# gathers the finished rows; "off": the gather scales and masks every edge's row itself.
+PRESCALE = {"mode": "auto", "bwd": "auto"}
+
+
+def _use_prescale(x, scale, drop, backward=False):
+    """forward: scale = pre (source rows), drop = the fused dropout; backward: scale = post
+    (the gradient rows the transposed aggregation gathers)."""
+    mode = PRESCALE["bwd" if backward else "mode"]
+    if mode == "off" or (scale is None and drop is None):
+        return False
+    # on / auto: one streaming pass over the rows (2*N*F*s bytes) takes the E*F mask hashes and
+    # the E dependent scale lookups out of the gather; measured faster for fp32 and bf16 at
+    # F = 64 on mag-10x (tools/ab_spmm.py, DESIGN.md section 4)
+    return True
+
+
+def _drop_args(drop):
+    if drop is None:
+        return None, 0, 1.0
+    return L.ptr(drop[0]), drop[1], drop[2]
+
+
 class _ReSpmm(torch.autograd.Function):
     """y = post * (A_tab (pre * drop(x))) + bias, A_tab[v,u] = sum over edges u->v of tab[rel_e];
     drop = the optional fused dropout of the gathered rows (regnn_spmm_fwd_dropout)."""
@@ -145,18 +169,26 @@ class _ReSpmm(torch.autograd.Function):
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
         t = _flat_table(tab)
         plan_args, part = _plan_args(rg.csr_plan, F, x.device)
-        args = (L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
-                L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
-                L.ptr(t), None, L.ptr(pre), L.ptr(post),
-                L.ptr(None if bias is None else bias.detach().float().contiguous()),
-                L.ptr(x), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args)
+        prescale = _use_prescale(x, pre, drop)
+        src, in_scale = x, pre
         with timed("spmm_fwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_fwd")):
-            if drop is None:
+            if prescale:
+                # pre * drop(x) once per source row (regnn_row_scale), then a plain gather
+                src, in_scale = torch.empty_like(x), None
+                L.call("regnn_row_scale", L.ptr(x), L.ptr(pre), L.ptr(src), x.shape[0], F,
+                       L.dtype_code(x), *(_drop_args(drop)), None, None, L.stream())
+            args = (L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                    L.ptr(pack.rel_csr if (pack is not None and t is not None) else None),
+                    L.ptr(t), None, L.ptr(in_scale), L.ptr(post),
+                    L.ptr(None if bias is None else bias.detach().float().contiguous()),
+                    L.ptr(src), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args)
+            if drop is None or prescale:
                 L.call("regnn_spmm_fwd", *args, L.stream())
             else:
                 L.call("regnn_spmm_fwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
                        L.stream())
+        del src
         ctx.drop = drop
         ctx.rg, ctx.pack, ctx.tab_shape = rg, pack, None if tab is None else tab.shape
         ctx.same_scale = pre is not None and pre is post and rg.n_src == rg.n_dst
@@ -179,19 +211,36 @@ class _ReSpmm(torch.autograd.Function):
         elif need_pre:
             node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
         plan_args, part = _plan_args(rg.csc_plan, F, x.device)
-        args = (L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
-                L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
-                L.ptr(t), None, L.ptr(post), L.ptr(pre), L.ptr(gy), L.ptr(x),
-                L.ptr(y if ctx.same_scale and node is not None else None), L.ptr(gx),
-                L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F, L.dtype_code(x), *plan_args)
+        # output-side norm gradient <g, y> / post: same-scale node term or d loss / d post
+        want_dot = (ctx.same_scale and node is not None) or (not ctx.same_scale and need_post)
+        prescale = post is not None and _use_prescale(x, post, None, backward=True)
+        src, in_scale, dot = gy, post, None
         drop = ctx.drop
         with timed("spmm_bwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_bwd")):
+            if prescale:
+                # post * g once per destination row (regnn_row_scale), with <g, y> / post formed
+                # in the same pass; the transposed gather then reads finished rows
+                src, in_scale = torch.empty_like(gy), None
+                dot = torch.empty(rg.n_dst, dtype=torch.float32, device=x.device) if want_dot \
+                    else None
+                L.call("regnn_row_scale", L.ptr(gy), L.ptr(post), L.ptr(src), rg.n_dst, F,
+                       L.dtype_code(x), None, 0, 1.0, L.ptr(y if want_dot else None), L.ptr(dot),
+                       L.stream())
+            args = (L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                    L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
+                    L.ptr(t), None, L.ptr(in_scale), L.ptr(pre), L.ptr(src), L.ptr(x),
+                    L.ptr(y if ctx.same_scale and node is not None and not prescale else None),
+                    L.ptr(gx), L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F,
+                    L.dtype_code(x), *plan_args)
             if drop is None:
                 L.call("regnn_spmm_bwd", *args, L.stream())
             else:
                 L.call("regnn_spmm_bwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
                        L.stream())
+            if prescale and ctx.same_scale and node is not None:
+                node.add_(dot)
+        del src
         g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
         g_pre = g_post = None
         if ctx.same_scale:
@@ -200,8 +249,11 @@ class _ReSpmm(torch.autograd.Function):
             if need_pre:
                 g_pre = node
             if need_post:
-                yf, gf = y.float(), gy.float()
-                g_post = (gf * yf).sum(1) / post
+                if dot is not None:
+                    g_post = dot
+                else:
+                    yf, gf = y.float(), gy.float()
+                    g_post = (gf * yf).sum(1) / post
         g_bias = gy.float().sum(0) if need_bias else None
         return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None
 

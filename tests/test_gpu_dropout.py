@@ -23,8 +23,21 @@ def _graph(n=700, m=9000, R=6, hub=600, seed=0):
 
 @pytest.mark.parametrize("dtype,F", [(torch.float32, 64), (torch.bfloat16, 128),
                                      (torch.bfloat16, 64), (torch.float32, 32)])
-@pytest.mark.parametrize("p", [0.5, 0.3, 0.75])
-def test_fused_dropout_matches_masked_composition(dtype, F, p):
+@pytest.mark.parametrize("p", [0.5, 0.3, 0.75, 0.0])
+@pytest.mark.parametrize("prescale", ["on", "off"])
+def test_fused_dropout_matches_masked_composition(dtype, F, p, prescale):
+    """prescale "on": regnn_row_scale forms norm * drop(x) per row and the gather reads it;
+    "off": the gather masks and scales every edge's row (regnn_spmm_fwd_dropout)."""
+    from regnn_hip import ops
+    old = dict(ops.PRESCALE)
+    ops.PRESCALE.update(mode=prescale, bwd=prescale)
+    try:
+        _check_dropout_composition(dtype, F, p)
+    finally:
+        ops.PRESCALE.update(old)
+
+
+def _check_dropout_composition(dtype, F, p):
     from regnn_hip import ops
     from regnn_hip.graph import RelGraph
     src, dst, rel, n, R = _graph()

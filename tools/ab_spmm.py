@@ -2,7 +2,8 @@
 
     python tools/ab_spmm.py [--scale 10] [--rounds 5] [--F 64] [--dtype fp32]
 
-Variants: grid cap (regnn_tune key 1) x long-segment split/chunk. Reports per variant the median
+Variants cap:split:chunk[:un[:prescale]]: grid cap (regnn_tune key 1) x long-segment
+split/chunk x rows in flight (key 2) x ops.PRESCALE mode (on/off/auto). Reports per variant the median
 ms of spmm_fwd / spmm_bwd (HIP events on the launch stream) and GB/s on SURVEY §8d bytes.
 """
 import argparse
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--F", type=int, default=64)
     ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--dropout", type=float, default=0.0, help="fused dropout of the gathered rows")
     ap.add_argument("--variants", default="res:256:256,cap2048:256:256,res:1024:256,res:256:512")
     args = ap.parse_args()
     from regnn_hip import _lib as L, ops, profile, synth
@@ -40,17 +42,19 @@ def main():
         parts = v.split(":")
         cap, split, chunk = parts[:3]
         un = int(parts[3]) if len(parts) > 3 else 0
+        pre = parts[4] if len(parts) > 4 else "auto"       # ops.PRESCALE mode
         key = (int(split), int(chunk))
         if key not in graphs:
             graphs[key] = RelGraph(gd["src"], gd["dst"], gd["N"], dev, split=key[0], chunk=key[1])
-        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key], un))
+        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key], un, pre))
     E, N = graphs[next(iter(graphs))].E, gd["N"]
     F = args.F
     fwd_b = E * (F * s + 9) + N * (F * s + 8)
     bwd_b = E * (F * s + 9) + N * (3 * F * s + 12)
     res = {v[0]: {"fwd": [], "bwd": []} for v in variants}
     for r in range(args.rounds + 1):
-        for name, cap, rg, un in variants:
+        for name, cap, rg, un, pre in variants:
+            ops.PRESCALE["mode"] = ops.PRESCALE["bwd"] = pre
             L._so.regnn_tune(1, cap)
             L._so.regnn_tune(2, un)
             pack = rg.rel_pack(e_feat, 11)
@@ -58,7 +62,7 @@ def main():
             x = x0.clone().requires_grad_(True)
             profile.enable(True)
             norm = ops.degree_norm(rg, pack, tab)
-            y = ops.re_spmm(rg, x, tab, pack, pre=norm, post=norm)
+            y = ops.re_spmm(rg, x, tab, pack, pre=norm, post=norm, dropout=args.dropout)
             y.backward(gy)
             torch.cuda.synchronize()
             st = profile.summary()
@@ -75,7 +79,7 @@ def main():
         out[name] = {"fwd_ms": round(f, 3), "bwd_ms": round(b, 3),
                      "fwd_TBs": round(fwd_b / f / 1e9, 3), "bwd_TBs": round(bwd_b / b / 1e9, 3),
                      "fwd_min": round(min(d["fwd"]), 3), "bwd_min": round(min(d["bwd"]), 3)}
-    print(json.dumps({"scale": args.scale, "F": F, "dtype": args.dtype, "E": E, "N": N,
+    print(json.dumps({"scale": args.scale, "F": F, "dtype": args.dtype, "dropout": args.dropout, "E": E, "N": N,
                       "variants": out}, indent=1))
 
 
