@@ -6,9 +6,14 @@ One step = per-type input Linear -> REGraphConv x2 (HIP degree + SpMM) -> out_li
 backward (HIP fused transposed SpMM + SDDMM + relation/degree grads) -> Adam. Inputs resident in
 HBM before timing. value = n_gpus * L * E / t_step (aggregated edges/s, whole job).
 
-Multi-GPU: the full-batch path does not shard -> every rank trains an
-independent replica on its own copy of the graph ("replicas only", weak scaling, no collective
-in the timed region). Launch: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Multi-GPU (full-batch workloads): graph-shard data parallelism, weak scaling. Every rank holds
+its own graph shard of the configured size (the same generator, seeded by rank: rank 0's shard is
+the N=1 graph) and the same replicated parameters; after backward one flat-bucket RCCL
+all-reduce averages the gradients (mag.flat_grad_allreduce, the DP exchange of
+mag/regnn_ns.py:406-407) and every rank applies the same Adam step, so the ranks train one model.
+The shards have no cross-shard edges (a whole graph fits one GPU: SURVEY.md §8e), so there is no
+halo exchange. The neighbour-sampled path (--workload ns) is the reference's own DP path.
+Launch: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mag|dblp] [--scale 10]
 """
@@ -36,11 +41,13 @@ def log(*a):
 
 def setup_dist(n):
     if n > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        dist.init_process_group("nccl")
+        # RCCL ("nccl"); REGNN_DIST_BACKEND=gloo rehearses several ranks on one device
+        dist.init_process_group(os.environ.get("REGNN_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
         local = int(os.environ.get("LOCAL_RANK", rank))
     else:
         rank, world, local = 0, 1, 0
+    local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     return rank, world, torch.device("cuda", local)
 
@@ -53,21 +60,24 @@ def _full_graph(gd, dev):
 
 def build_workload(args, dev):
     """-> dict(step=callable, edges_per_step=int|callable, rg=RelGraph, kernels=[...], ...)."""
-    from regnn_hip import nets, ops, synth
+    from regnn_hip import mag, nets, ops, synth
     t0 = time.time()
     wl = args.workload
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
     gen = torch.Generator(device=dev)
-    gen.manual_seed(2)
-    torch.manual_seed(3)
+    gen.manual_seed(2 + 1000 * rank)
+    torch.manual_seed(3)              # identical parameter init on every rank
+    gs, fs = rank, 1 + 1000 * rank    # graph / feature seeds of this rank's shard
     if wl in ("mag", "dblp"):
         if wl == "mag":
-            gd = synth.mag_like(args.scale, seed=0, device=dev)
-            feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1,
+            gd = synth.mag_like(args.scale, seed=gs, device=dev)
+            feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=fs,
                                         device=dev, kind="mag")
             n_classes, train_nodes = 349, gd["counts"]["paper"]
         else:
-            gd = synth.dblp_like(seed=0, device=dev)
-            feats = synth.type_features(gd["counts"], synth.DBLP_DIMS, seed=1, device=dev,
+            gd = synth.dblp_like(seed=gs, device=dev)
+            feats = synth.type_features(gd["counts"], synth.DBLP_DIMS, seed=fs, device=dev,
                                         kind="dblp")
             n_classes, train_nodes = 4, gd["counts"]["A"]
         g, rg, e_feat = _full_graph(gd, dev)
@@ -79,16 +89,16 @@ def build_workload(args, dev):
             feats = [f.to(torch.bfloat16) for f in feats]
         convs, kern = 2, ("spmm_fwd", "spmm_bwd")
     elif wl == "acm":
-        gd = synth.acm_like(seed=0, device=dev)
-        feats = synth.type_features(gd["counts"], synth.ACM_DIMS, seed=1, device=dev, kind="target")
+        gd = synth.acm_like(seed=gs, device=dev)
+        feats = synth.type_features(gd["counts"], synth.ACM_DIMS, seed=fs, device=dev, kind="target")
         n_classes, train_nodes = 3, gd["counts"]["P"]
         g, rg, e_feat = _full_graph(gd, dev)
         net = nets.REGAT(g, gd["R"], 100.0, 2, 64, 64, n_classes, [8, 8, 1], F.elu, args.dropout,
                          args.dropout, 0.01, False, [f.shape[1] for f in feats]).to(dev)
         convs, kern = 3, ("spmm_heads_fwd", "spmm_heads_bwd", "gat_softmax_fwd", "gat_softmax_bwd")
     elif wl == "imdb":
-        gd = synth.imdb_like(seed=0, device=dev)
-        feats = synth.type_features(gd["counts"], synth.IMDB_DIMS, seed=1, device=dev, kind="target")
+        gd = synth.imdb_like(seed=gs, device=dev)
+        feats = synth.type_features(gd["counts"], synth.IMDB_DIMS, seed=fs, device=dev, kind="target")
         n_classes, train_nodes = 3, gd["counts"]["M"]
         g, rg, e_feat = _full_graph(gd, dev)
         net = nets.REMixHop(g, gd["R"], 100.0, 64, 64, n_classes, 2, [f.shape[1] for f in feats],
@@ -103,6 +113,7 @@ def build_workload(args, dev):
     opt = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=1e-3, capturable=True)
 
     W, b = net.head()
+    params = list(net.parameters())
 
     def step():
         # run_regnn.py:146-150: logits = net(...) over all nodes, CE on the train rows, backward,
@@ -111,6 +122,8 @@ def build_workload(args, dev):
         _, loss = ops.head_ce(net.embed(feats, e_feat).float(), W, b, labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
+        if world > 1:
+            mag.flat_grad_allreduce(params, world)      # DP exchange (RCCL over xGMI)
         opt.step()
 
     torch.cuda.synchronize()
@@ -263,7 +276,10 @@ def main():
 
     w = build_workload(args, dev)
     rg = w["rg"]
-    use_graph = args.graph == "on" or (args.graph == "auto" and args.workload in ("dblp", "acm", "imdb"))
+    # (auto: capture the launch-bound single-GPU small graphs; with ranks > 1 the step holds an
+    # RCCL all-reduce and runs eagerly)
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and
+                                       args.workload in ("dblp", "acm", "imdb"))
     if use_graph and w.get("ns"):
         raise SystemExit("--graph: the sampled path has data-dependent shapes (not capturable)")
     for _ in range(args.warmup):
@@ -371,7 +387,9 @@ def main():
             "conv_applications_per_step": w["convs"], "hidden": 64,
             "parallelism": (f"data-parallel x{world} (RCCL grad all-reduce)" if w.get("ns")
                             else f"row-sharded x{world} (RCCL all-gather per layer)"
-                            if w.get("scaling") == "strong" else f"replicas x{world}"),
+                            if w.get("scaling") == "strong" else
+                            f"data-parallel x{world} over per-rank graph shards "
+                            f"(RCCL grad all-reduce)"),
             "hip_graph": use_graph,
         },
         "roofline": {

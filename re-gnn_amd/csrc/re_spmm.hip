@@ -537,10 +537,34 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
 // ---------------------------------------------------------------------------------------------
 // degree / norm
 // ---------------------------------------------------------------------------------------------
+// Weighted degree, one thread per row (consecutive rows per wave, so a wave's relation-id reads
+// walk one contiguous stretch of the CSR). The relation ids are read as aligned 32-bit words
+// (4 edges per load, bytes outside [b, e) masked) and the table lives in LDS, so a row costs
+// ~deg/4 independent loads instead of deg dependent (id -> table) global load pairs.
+__device__ __forceinline__ void rel_words(int b, int e, int& w0, int& w1) {
+    w0 = b >> 2;
+    w1 = (e + 3) >> 2;
+}
+
+__device__ __forceinline__ uint32_t word_mask(int w, int b, int e) {
+    // bit k of the result set iff byte k of word w is an edge of [b, e)
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int pos = 4 * w + k;
+        m |= (pos >= b && pos < e) ? (1u << k) : 0u;
+    }
+    return m;
+}
+
 __global__ void __launch_bounds__(kBlock)
 degree_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ rel,
-              const float* __restrict__ tab, int64_t n_seg, float power, int32_t split,
-              float* __restrict__ deg, float* __restrict__ norm) {
+              const float* __restrict__ tab, int32_t n_rel, int64_t n_seg, float power,
+              int32_t split, float* __restrict__ deg, float* __restrict__ norm) {
+    __shared__ float stab[256];
+    for (int r = threadIdx.x; r < 256; r += kBlock) stab[r] = (tab && r < n_rel) ? tab[r] : 0.f;
+    __syncthreads();
+    const uint32_t* __restrict__ rel32 = reinterpret_cast<const uint32_t*>(rel);
     for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n_seg;
          v += (int64_t)gridDim.x * kBlock) {
         const int b = ptr[v], e = ptr[v + 1];
@@ -548,7 +572,15 @@ degree_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ rel,
         float d;
         if (tab) {
             d = 0.f;
-            for (int k = b; k < e; ++k) d += tab[rel[k]];
+            int w0, w1;
+            rel_words(b, e, w0, w1);
+            for (int w = w0; w < w1; ++w) {
+                const uint32_t x = rel32[w];
+                const uint32_t m = word_mask(w, b, e);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (m & (1u << k)) d += stab[(x >> (8 * k)) & 0xFFu];
+            }
         } else {
             d = float(e - b);
         }
@@ -586,15 +618,26 @@ degree_bwd_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ r
                   const float* __restrict__ deg, const float* __restrict__ g_norm, int64_t n_seg,
                   float power, int32_t n_rel, int32_t split, const int32_t* __restrict__ long_ids,
                   int32_t n_long, const int32_t* __restrict__ long_cnt, float* __restrict__ slab) {
+    // one thread per row, relation ids read as 32-bit words (as degree_kernel); the row's degree
+    // gradient goes into the thread's own LDS relation bins (no atomics, fixed order)
     extern __shared__ float bins[];
     const int tid = threadIdx.x;
     bins_zero(bins, n_rel, tid);
+    const uint32_t* __restrict__ rel32 = reinterpret_cast<const uint32_t*>(rel);
     for (int64_t v = (int64_t)blockIdx.x * kBlock + tid; v < n_seg;
          v += (int64_t)gridDim.x * kBlock) {
         const int b = ptr[v], e = ptr[v + 1];
         if (split > 0 && e - b > split) continue;
         const float gd = dnorm_ddeg(deg[v], g_norm[v], power);
-        for (int k = b; k < e; ++k) bins[rel[k] * kBlock + tid] += gd;
+        int w0, w1;
+        rel_words(b, e, w0, w1);
+        for (int w = w0; w < w1; ++w) {
+            const uint32_t x = rel32[w];
+            const uint32_t m = word_mask(w, b, e);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (m & (1u << k)) bins[((x >> (8 * k)) & 0xFFu) * kBlock + tid] += gd;
+        }
     }
     for (int l = blockIdx.x * kBlock + tid; l < n_long; l += gridDim.x * kBlock) {
         const int64_t v = long_ids[l];
@@ -984,9 +1027,10 @@ int regnn_degree(const int32_t* ptr, const uint8_t* rel, const float* rel_table,
     if (split > 0 && n_long > 0 && (!long_ids || (rel_table && !long_cnt))) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (n_long == 0) split = 0;
+    if (rel_table && (n_rel <= 0 || n_rel > 256)) return REGNN_EINVAL;
     hipLaunchKernelGGL(degree_kernel, dim3(grid_resident(degree_kernel, n_seg, kBlock, 0)),
-                       dim3(kBlock), 0, stream, ptr,
-                       rel, rel_table, n_seg, power, split, deg, norm);
+                       dim3(kBlock), 0, stream, ptr, rel, rel_table, n_rel, n_seg, power, split,
+                       deg, norm);
     REGNN_LAUNCH_CHECK();
     if (split > 0) {
         hipLaunchKernelGGL(degree_long_kernel, dim3(grid_for(n_long, kBlock)), dim3(kBlock), 0,
@@ -1006,7 +1050,8 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
     if (n_seg == 0) return REGNN_OK;
     if (n_long == 0) split = 0;
     const size_t lds = size_t(n_rel) * kBlock * sizeof(float);
-    hipLaunchKernelGGL(degree_bwd_kernel, dim3(grid_resident(degree_bwd_kernel, n_seg, kBlock, lds)),
+    hipLaunchKernelGGL(degree_bwd_kernel,
+                       dim3(grid_resident(degree_bwd_kernel, n_seg, kBlock, lds)),
                        dim3(kBlock), lds, stream,
                        ptr, rel, deg, g_norm, n_seg, power, n_rel, split, long_ids,
                        split > 0 ? n_long : 0, long_cnt, slab);

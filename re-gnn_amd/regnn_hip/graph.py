@@ -82,6 +82,14 @@ class SegPlan:
         return torch.empty(self.partial_rows, F, dtype=torch.float32, device=device)
 
 
+def _word_padded(r):
+    """uint8 [E] view of a buffer padded to whole 32-bit words (+1 word): the degree kernels read
+    relation ids four at a time (aligned words, bytes past the row masked)."""
+    buf = torch.zeros(((r.numel() + 3) // 4 + 1) * 4, dtype=torch.uint8, device=r.device)
+    buf[:r.numel()] = r
+    return buf[:r.numel()]
+
+
 class RelPack:
     """Relation ids of one e_feat tensor laid out for both orientations (+ long-row counts)."""
 
@@ -96,8 +104,8 @@ class RelPack:
                 raise ValueError(f"relation ids must lie in [1, {num_rel or 256}], got [{lo}, {hi}]")
         self.max_rel = int(e.max().item()) if e.numel() else 0
         r = (e - 1).to(torch.uint8)
-        self.rel_csr = r[rg.csr_eid].contiguous()
-        self.rel_csc = r[rg.csc_eid].contiguous()
+        self.rel_csr = _word_padded(r[rg.csr_eid])
+        self.rel_csc = _word_padded(r[rg.csc_eid])
         self._cnt = {}
         self.rg = rg
 

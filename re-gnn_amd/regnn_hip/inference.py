@@ -23,7 +23,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import ops
-from .graph import SegPlan
+from .graph import SegPlan, _word_padded
 
 
 def shard_bounds(csr_ptr, world):
@@ -74,7 +74,7 @@ class RowBlock:
         self.csr_idx = idx
         self.csr_plan = SegPlan(self.csr_ptr)
         self.pack = type("RowPack", (), {})()
-        self.pack.rel_csr = rel
+        self.pack.rel_csr = _word_padded(rel)
         self._inv = (1.0 / (cnt + 1).to(torch.float32)).contiguous()   # mean over edges + loop
 
     def inv_in_count(self):

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 from torch.nn import Linear, ModuleDict, ModuleList, Parameter, ParameterDict, init
 
 from . import ops
-from .graph import RelGraph, SegPlan
+from .graph import RelGraph, SegPlan, _word_padded
 
 
 def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_types,
@@ -70,8 +70,8 @@ class _Block:
         self.csr_plan = SegPlan.none()                       # rows <= fan-out + 1
         self.csc_plan = SegPlan(self.csc_ptr)
         self.pack = type("BlockPack", (), {})()
-        self.pack.rel_csr = rel
-        self.pack.rel_csc = rel[perm].contiguous()
+        self.pack.rel_csr = _word_padded(rel)
+        self.pack.rel_csc = _word_padded(rel[perm])
         self._inv = (1.0 / cnt.to(torch.float32)).contiguous()
 
     def inv_in_count(self):

@@ -1,0 +1,5 @@
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out &&
+tools/gpu_step.sh 600 gpurun_out/pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider &&
+tail -2 gpurun_out/pytest_gpu.log &&
+tools/gpu_step.sh 600 gpurun_out/bench.log python bench.py --no-cpu-baseline &&
+tail -n 2 gpurun_out/bench.log | grep -o '"ms_per_step": [0-9.]*\|"kernels_ms.*'
