@@ -42,6 +42,12 @@ def test_invalid_arguments_rejected_without_gpu():
     rc = _lib._so.regnn_degree_bwd(None, None, None, None, 5, -0.5, 100, 0, None, 0, None, None,
                                    None)
     assert rc == 1
+    # regnn_row_scale: NULL rows, z without dot, keep threshold > 2^16 -> EINVAL; 0 rows -> OK
+    rs = _lib._so.regnn_row_scale
+    assert rs(None, None, None, 4, 64, 0, None, 0, 1.0, None, None, None) == 1
+    assert rs(1 << 20, None, 1 << 21, 4, 64, 0, None, 0, 1.0, 1 << 22, None, None) == 1
+    assert rs(1 << 20, None, 1 << 21, 4, 64, 0, 1 << 23, 65537, 2.0, None, None, None) == 1
+    assert rs(None, None, None, 0, 64, 0, None, 0, 1.0, None, None, None) == 0
 
 
 def test_cpu_tensor_refused():
