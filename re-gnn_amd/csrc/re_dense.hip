@@ -193,27 +193,36 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
                 if (16 * t + 16 <= C || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
         m = fmaxf(m, __shfl_xor(m, 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
-        float se = 0.f;
+        // the logits are stored: acc becomes exp(z - m) in place (one exp per class, reused for
+        // the gradient), the label's logit is picked on the way
+        const int y = node < n_loss ? (int)labels[node] : -1;
+        float se = 0.f, zy = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (16 * t + 16 <= C || 16 * t + 4 * q + i < C) se += __expf(acc[t][i] - m);
+            for (int i = 0; i < 4; ++i) {
+                const int cls = 16 * t + 4 * q + i;
+                zy = cls == y ? acc[t][i] : zy;
+                const float e = (16 * t + 16 <= C || cls < C) ? __expf(acc[t][i] - m) : 0.f;
+                acc[t][i] = e;
+                se += e;
+            }
         se += __shfl_xor(se, 16, 64);
         se += __shfl_xor(se, 32, 64);
         const float lse = m + __logf(se);
         if (node < n_loss) {
-            const int y = (int)labels[node];
             float* pr = p + node * C + 4 * q;
+            const float r = scale / se;
+            const int yq = y - 4 * q;              // the label's slot in this lane's tiles
+            if (yq >= 0 && (yq & 15) < 4) loss_rows[node] = lse - zy;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 f32x4 v;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int cls = 16 * t + 4 * q + i;
-                    const float e = __expf(acc[t][i] - lse) * scale;
+                    const float e = acc[t][i] * r;
                     v[i] = cls == y ? e - scale : e;
-                    if (cls == y) loss_rows[node] = lse - acc[t][i];
                 }
                 if (16 * t + 16 <= C) {
                     *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
