@@ -81,8 +81,8 @@ constexpr int kHeadMaxC = 24 * 16;
 // 2 = no logits stores, 4 = no loss-row epilogue. Shipped variant: FL = 0.
 // AMAX: inference variant (mag/regnn_ns.py:367 out_lin + the caller's argmax): no logits
 // stores and no loss rows; amax[node] = first class of maximal logit (torch.argmax ties).
-template <int NT, int FL, bool AMAX = false>
-__global__ void __launch_bounds__(kHeadBlock)
+template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
+__global__ void __launch_bounds__(BLK)
 head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
                 const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
                 int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
@@ -174,7 +174,7 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
             float* lr = logits + node * C + 4 * q;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                if (16 * t + 16 <= C) {
+                if ((t + 1 < NT || 16 * t + 16 <= C)) {
                     *reinterpret_cast<f32x4_u*>(lr + 16 * t) = acc[t];
                 } else {
 #pragma unroll
@@ -190,20 +190,27 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                if (16 * t + 16 <= C || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
+                if ((t + 1 < NT || 16 * t + 16 <= C) || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
         m = fmaxf(m, __shfl_xor(m, 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
-        // the logits are stored: acc becomes exp(z - m) in place (one exp per class, reused for
-        // the gradient), the label's logit is picked on the way
-        const int y = node < n_loss ? (int)labels[node] : -1;
-        float se = 0.f, zy = 0.f;
+        // The label's logit z_y comes from its own 64-term dot (the lane's 16 k of h against
+        // column y of W^T in LDS + 2 shuffles), not from a per-class compare: 88 compares per lane
+        // would hold 88 VCC masks and spill the SGPR file. acc becomes exp(z - m) in place (one
+        // exp per class, reused for the gradient); the label's entry of p is fixed up afterwards.
+        const int y = node < n_loss ? (int)labels[node] : 0;
+        float zy = 0.f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) zy = fmaf(a[s], Wl[(16 * q + s) * LDW + y], zy);
+        zy += __shfl_xor(zy, 16, 64);
+        zy += __shfl_xor(zy, 32, 64);
+        zy += Wl[K * LDW + y];                      // bias[y]
+        float se = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int cls = 16 * t + 4 * q + i;
-                zy = cls == y ? acc[t][i] : zy;
-                const float e = (16 * t + 16 <= C || cls < C) ? __expf(acc[t][i] - m) : 0.f;
+                const float e = ((t + 1 < NT || 16 * t + 16 <= C) || cls < C) ? __expf(acc[t][i] - m) : 0.f;
                 acc[t][i] = e;
                 se += e;
             }
@@ -213,18 +220,10 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
         if (node < n_loss) {
             float* pr = p + node * C + 4 * q;
             const float r = scale / se;
-            const int yq = y - 4 * q;              // the label's slot in this lane's tiles
-            if (yq >= 0 && (yq & 15) < 4) loss_rows[node] = lse - zy;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                f32x4 v;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int cls = 16 * t + 4 * q + i;
-                    const float e = acc[t][i] * r;
-                    v[i] = cls == y ? e - scale : e;
-                }
-                if (16 * t + 16 <= C) {
+                const f32x4 v = acc[t] * r;
+                if ((t + 1 < NT || 16 * t + 16 <= C)) {
                     *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
                 } else {
 #pragma unroll
@@ -232,30 +231,35 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
                         if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
                 }
             }
+            const int yq = y - 4 * q;              // the label's slot in this lane's tiles
+            if (yq >= 0 && (yq & 15) < 4) {        // same lane, same address: ordered after
+                loss_rows[node] = lse - zy;
+                p[node * C + y] = __expf(zy - m) * r - scale;
+            }
         }
     }
 }
 
-template <int NT, int FL, bool AMAX = false>
+template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
 int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, int C,
                 const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                 float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
     const size_t lds = ((size_t)kHeadK * (NT * 16 + 1) + NT * 16) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX, BLK>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return REGNN_ELAUNCH;
         attr = true;
     }
     const int64_t tiles = (rows + 15) / 16;
-    int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
-    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX>),
-                                    lds, kHeadBlock);
+    int64_t grid = (tiles + BLK / 64 - 1) / (BLK / 64);
+    const int cap = resident_blocks(
+        reinterpret_cast<const void*>(&head_fwd_kernel<NT, FL, AMAX, BLK>), lds, BLK);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
-    auto kern = &head_fwd_kernel<NT, FL, AMAX>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kHeadBlock), lds, stream, h, rows, W, b,
+    auto kern = &head_fwd_kernel<NT, FL, AMAX, BLK>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BLK), lds, stream, h, rows, W, b,
                        C, labels, n_loss, scale, logits, p, loss_rows, amax);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
@@ -313,7 +317,7 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
         f32x4 pv[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            if (16 * t + 16 <= C) {
+            if ((t + 1 < NT || 16 * t + 16 <= C)) {
                 pv[t] = *reinterpret_cast<const f32x4_u*>(pr + 16 * t);
             } else {
 #pragma unroll
