@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 5). */
+/* ABI version (bumped on any signature change or addition; currently 6). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -43,6 +43,7 @@ int regnn_abi_version(void);
  * API, the default; > 0 = fixed block count, at most 2048). key 2: rows gathered per lane per
  * step for 16-vector rows (F=64 fp32 / F=128 bf16): 0 = default (8), 4 or 16. key 3: fused
  * head variant (0 = next tile / next k-step operands prefetched, the default; 1 = plain).
+ * key 4: rows in flight per lane group of regnn_row_scale (0 = default 1, 2 or 4).
  * Returns the previous value, -1 for an unknown key. */
 int64_t regnn_tune(int32_t key, int64_t value);
 
@@ -256,15 +257,16 @@ int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, cons
 
 /* Backward of the fused output head from its softmax gradient p [n, C] (regnn_head_fwd), each
  * part reading p once (fp32 MFMA):
- *   gh (optional, [n, K], 16-byte aligned) = gscale[0] * p W   (gscale NULL: 1)
+ *   gh (optional, [n_out, K], n_out >= n, 16-byte aligned) = gscale[0] * p W on rows < n
+ *      (gscale NULL: 1) and 0 on rows [n, n_out) (nodes without a loss term)
  *   slab (optional): per-block partial rows [rows_used, Cp*K + Cp], Cp = 16 * ceil(C/16):
  *     columns [0, Cp*K) hold (p^T h)[c][k] at c*K + k (d out_lin.weight), columns [Cp*K, +Cp)
  *     the column sums of p (d out_lin.bias). At most slab_rows rows are written: zero the slab
  *     first and reduce its slab_rows rows with regnn_rel_reduce (fixed order).
  *     K must be 64, C <= 384. */
 int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
-                   const float* h, const float* gscale, float* gh, float* slab, int32_t slab_rows,
-                   hipStream_t stream);
+                   const float* h, const float* gscale, float* gh, int64_t n_out, float* slab,
+                   int32_t slab_rows, hipStream_t stream);
 
 /* Inference head (mag/regnn_ns.py:367 out_lin over every node, then the caller's argmax,
  * regnn_ns.py:379): out[r] = argmax_c (h[r] W^T + b)[c] (first maximal class, as torch.argmax),

@@ -293,11 +293,17 @@ int launch_head(const float* h, int64_t rows, const float* W, const float* b, in
 // gh is computed transposed (gh^T = W^T p^T) with the same operand trick as head_fwd: k-step
 // (t, i) takes class 16 t + 4 q + i from lane quarter q, so the B operand is component i of the
 // lane's 16-byte load p[row][16 t + 4 q ..] and W^T comes from LDS; each lane ends with 4
-// consecutive k of its row per 16-k tile (16-byte stores).
+// consecutive k of its row per 16-k tile (16-byte stores). 16 waves per block share one W^T copy
+// (4 per SIMD); a wave streams its rows' p in batches of kGhBatch class tiles (16 accumulator
+// registers, no register-resident p row), so the kernel runs near the p read rate. Rows
+// [n, n_out) of gh (nodes without a loss term) are written as zeros in the same launch.
+constexpr int kGhBlock = 1024;
+constexpr int kGhBatch = 4;
+
 template <int NT>
-__global__ void __launch_bounds__(kHeadBlock)
+__global__ void __launch_bounds__(kGhBlock)
 head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ W,
-               const float* __restrict__ gscale, float* __restrict__ gh) {
+               const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out) {
     constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;
     extern __shared__ float Wl[];
     for (int idx = threadIdx.x; idx < CP * K; idx += blockDim.x) {
@@ -313,29 +319,36 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
          tile += (int64_t)gridDim.x * wpb) {
         const int64_t row = tile * 16 + c;
         const bool valid = row < n;
-        const float* pr = p + (valid ? row : 0) * C + 4 * q;
-        f32x4 pv[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            if ((t + 1 < NT || 16 * t + 16 <= C)) {
-                pv[t] = *reinterpret_cast<const f32x4_u*>(pr + 16 * t);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) pv[t][i] = 16 * t + 4 * q + i < C ? pr[16 * t + i] : 0.f;
-            }
-            if (!valid) pv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        const float* pr = p + (valid ? row : n - 1) * C + 4 * q;
         f32x4 acc[4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int t0 = 0; t0 < NT; t0 += kGhBatch) {
+            f32x4 pv[kGhBatch];
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+            for (int j = 0; j < kGhBatch; ++j) {
+                const int t = t0 + j;
+                if (t + 1 < NT || (t < NT && 16 * t + 16 <= C)) {
+                    pv[j] = *reinterpret_cast<const f32x4_u*>(pr + 16 * t);
+                } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                    for (int i = 0; i < 4; ++i)
+                        pv[j][i] = (t < NT && 16 * t + 4 * q + i < C) ? pr[16 * t + i] : 0.f;
+                }
+            }
 #pragma unroll
-                for (int kt = 0; kt < 4; ++kt)
-                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        Wl[(16 * kt + c) * LDW + 16 * t + 4 * q + i], pv[t][i], acc[kt], 0, 0, 0);
+            for (int j = 0; j < kGhBatch; ++j) {
+                if (t0 + j >= NT) break;             // wave-uniform; LDS past CP is not W^T
+                const float* wr = Wl + c * LDW + 16 * (t0 + j) + 4 * q;   // + (16 kt) LDW + i
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int kt = 0; kt < 4; ++kt)
+                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[16 * kt * LDW + i],
+                                                                       pv[j][i], acc[kt], 0, 0, 0);
+            }
+        }
         if (valid) {
             float* gr = gh + row * K + 4 * q;
 #pragma unroll
@@ -343,6 +356,11 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
                 *reinterpret_cast<f32x4*>(gr + 16 * kt) = acc[kt] * sc;
         }
     }
+    // rows without a loss term: d loss / d h = 0
+    const int64_t z0 = n * K / 4, z1 = n_out * K / 4;
+    for (int64_t v = z0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < z1;
+         v += (int64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<f32x4*>(gh)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 // gW^T partial of this block's row range: wave w owns class tiles w, w + 8, w + 16; per 4-row
@@ -414,7 +432,7 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
 
 template <int NT>
 int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const float* h,
-                    const float* gscale, float* gh, float* slab, int slab_rows,
+                    const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
                     hipStream_t stream) {
     constexpr int K = kHeadK;
     if (gh) {
@@ -428,13 +446,13 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
             attr = true;
         }
         const int64_t tiles = (n + 15) / 16;
-        int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
+        int64_t grid = (tiles + kGhBlock / 64 - 1) / (kGhBlock / 64);
         const int cap = resident_blocks(reinterpret_cast<const void*>(&head_gh_kernel<NT>), lds,
-                                        kHeadBlock);
+                                        kGhBlock);
         if (grid > cap) grid = cap;
         if (grid < 1) grid = 1;
-        hipLaunchKernelGGL((head_gh_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
-                           stream, p, n, C, W, gscale, gh);
+        hipLaunchKernelGGL((head_gh_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
+                           stream, p, n, C, W, gscale, gh, n_out);
         REGNN_LAUNCH_CHECK();
     }
     if (slab) {
@@ -522,15 +540,17 @@ int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, c
 }
 
 int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
-                   const float* h, const float* gscale, float* gh, float* slab, int32_t slab_rows,
-                   hipStream_t stream) {
+                   const float* h, const float* gscale, float* gh, int64_t n_out, float* slab,
+                   int32_t slab_rows, hipStream_t stream) {
     if (!p || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || (gh && !W) ||
-        (slab && (!h || slab_rows <= 0)) || (gh && (reinterpret_cast<uintptr_t>(gh) & 15)))
+        (gh && n_out < n) || (slab && (!h || slab_rows <= 0)) ||
+        (gh && (reinterpret_cast<uintptr_t>(gh) & 15)))
         return REGNN_EINVAL;
-    if (n == 0) return REGNN_OK;
+    if (n == 0 && !(gh && n_out > 0)) return REGNN_OK;
     switch ((C + 15) / 16) {
 #define HB_CASE(nt) \
-        case nt: return launch_head_bwd<nt>(p, n, C, W, h, gscale, gh, slab, slab_rows, stream);
+        case nt: return launch_head_bwd<nt>(p, n, C, W, h, gscale, gh, n_out, slab, slab_rows, \
+                                            stream);
         HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
         HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
         HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)

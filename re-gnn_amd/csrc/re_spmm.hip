@@ -702,7 +702,7 @@ rel_reduce_wide_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t w
 // regnn_spmm_fwd_dropout spec (row, vector index of the row), so regnn_spmm_bwd_dropout with the
 // same seed differentiates it. The dot is the output-side norm gradient <g, y_raw> = <g, y>/post
 // of the backward, formed here while g streams by.
-template <typename T, int LPR, int DROP>
+template <typename T, int LPR, int DROP, int U>
 __global__ void __launch_bounds__(kBlock)
 row_scale_kernel(const T* __restrict__ x, const float* __restrict__ scale, T* __restrict__ out,
                  int64_t n_rows, int32_t nvec, const uint64_t* __restrict__ drop_seed,
@@ -711,30 +711,48 @@ row_scale_kernel(const T* __restrict__ x, const float* __restrict__ scale, T* __
     constexpr int EV = Vec<T>::N;
     constexpr int GPB = kBlock / LPR;
     const int lane = threadIdx.x & (LPR - 1);
+    // U rows per group per step (U x 16 B loads in flight per lane; regnn_tune key 4)
     uint32_t key = 0;
     if constexpr (DROP) key = drop_key(drop_seed);
-    for (int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; row < n_rows;
-         row += (int64_t)gridDim.x * GPB) {
-        const float s = scale ? scale[row] : 1.f;
-        float d = 0.f;
-        for (int vec = lane; vec < nvec; vec += LPR) {
-            const int64_t o = (row * nvec + vec) * EV;
-            float v[EV];
-            Vec<T>::load(x + o, v);
-            if (dot) {
-                float w[EV];
-                Vec<T>::load(z + o, w);
+    const int64_t G = (int64_t)gridDim.x * GPB;
+    for (int64_t r0 = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; r0 < n_rows; r0 += G * U) {
+        int64_t rr[U];
+        bool ok[U];
+        float s[U], d[U];
 #pragma unroll
-                for (int t = 0; t < EV; ++t) d = fmaf(v[t], w[t], d);
+        for (int u = 0; u < U; ++u) {
+            ok[u] = r0 + u * G < n_rows;             // group-uniform
+            rr[u] = ok[u] ? r0 + u * G : r0;
+            s[u] = scale ? scale[rr[u]] : 1.f;
+            d[u] = 0.f;
+        }
+        for (int vec = lane; vec < nvec; vec += LPR) {
+            float v[U][EV], w[U][EV];
+#pragma unroll
+            for (int u = 0; u < U; ++u) Vec<T>::load(x + (rr[u] * nvec + vec) * EV, v[u]);
+            if (dot) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) Vec<T>::load(z + (rr[u] * nvec + vec) * EV, w[u]);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) d[u] = fmaf(v[u][t], w[u][t], d[u]);
             }
 #pragma unroll
-            for (int t = 0; t < EV; ++t) v[t] *= s;
-            if constexpr (DROP) drop_apply<EV, DROP>(key, drop_thresh, drop_scale, row, nvec, vec, v);
-            Vec<T>::store(out + o, v);
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int t = 0; t < EV; ++t) v[u][t] *= s[u];
+                if constexpr (DROP)
+                    drop_apply<EV, DROP>(key, drop_thresh, drop_scale, rr[u], nvec, vec, v[u]);
+                if (ok[u]) Vec<T>::store(out + (rr[u] * nvec + vec) * EV, v[u]);
+            }
         }
         if (dot) {
-            d = group_sum<LPR>(d);
-            if (lane == 0) dot[row] = d / s;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float t = group_sum<LPR>(d[u]);
+                if (lane == 0 && ok[u]) dot[rr[u]] = t / s[u];
+            }
         }
     }
 }
@@ -744,14 +762,24 @@ int launch_row_scale_lpr(const T* x, const float* scale, T* out, int64_t n_rows,
                          const uint64_t* seed, uint32_t keep16, float dscale, const T* z,
                          float* dot, hipStream_t stream) {
     constexpr int GPB = kBlock / LPR;
-#define REGNN_ROW_SCALE(D)                                                                       \
-    hipLaunchKernelGGL((row_scale_kernel<T, LPR, D>),                                            \
-                       dim3(grid_resident(row_scale_kernel<T, LPR, D>, n_rows, GPB, 0)),         \
+#define REGNN_ROW_SCALE(D, U)                                                                    \
+    hipLaunchKernelGGL((row_scale_kernel<T, LPR, D, U>),                                         \
+                       dim3(grid_resident(row_scale_kernel<T, LPR, D, U>, n_rows, GPB, 0)),      \
                        dim3(kBlock), 0, stream, x, scale, out, n_rows, nvec, seed, keep16, dscale, \
                        z, dot)
-    if (!seed) REGNN_ROW_SCALE(0);
-    else if ((keep16 & 0xFFu) == 0) REGNN_ROW_SCALE(8);
-    else REGNN_ROW_SCALE(16);
+    if (g_tune_rowscale == 0 || g_tune_rowscale == 1) {
+        if (!seed) REGNN_ROW_SCALE(0, 1);
+        else if ((keep16 & 0xFFu) == 0) REGNN_ROW_SCALE(8, 1);
+        else REGNN_ROW_SCALE(16, 1);
+    } else if (g_tune_rowscale == 2) {
+        if (!seed) REGNN_ROW_SCALE(0, 2);
+        else if ((keep16 & 0xFFu) == 0) REGNN_ROW_SCALE(8, 2);
+        else REGNN_ROW_SCALE(16, 2);
+    } else {
+        if (!seed) REGNN_ROW_SCALE(0, 4);
+        else if ((keep16 & 0xFFu) == 0) REGNN_ROW_SCALE(8, 4);
+        else REGNN_ROW_SCALE(16, 4);
+    }
 #undef REGNN_ROW_SCALE
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
@@ -780,6 +808,7 @@ int launch_row_scale(const void* x, const float* scale, void* out, int64_t n_row
 int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
 int64_t g_tune_head = 0;
+int64_t g_tune_rowscale = 0;
 
 int resident_blocks(const void* kernel, size_t lds, int block) {
     struct Entry { const void* k; size_t lds; int block; int blocks; };
@@ -812,7 +841,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 5; }
+int regnn_abi_version(void) { return 6; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -828,6 +857,11 @@ int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 3) {
         const int64_t old = g_tune_head;
         g_tune_head = value;
+        return old;
+    }
+    if (key == 4) {
+        const int64_t old = g_tune_rowscale;
+        g_tune_rowscale = value;
         return old;
     }
     return -1;

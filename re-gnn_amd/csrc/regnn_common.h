@@ -138,6 +138,7 @@ inline int grid_for(int64_t units, int per_block) {
 extern int64_t g_tune_grid_cap;
 extern int64_t g_tune_un;        // rows in flight per lane for F = 16 vectors (0 = 8)
 extern int64_t g_tune_head;      // fused head variant: 0 = pipelined, 1 = plain
+extern int64_t g_tune_rowscale;  // rows in flight per lane group of regnn_row_scale (0 = 1)
 
 int resident_blocks(const void* kernel, size_t lds, int block = kBlock);  // per CU x CUs, cached
 

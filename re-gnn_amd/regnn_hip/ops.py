@@ -632,22 +632,22 @@ class _HeadCE(torch.autograd.Function):
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         if head_fused(K, C) and h.dtype == torch.float32:
-            # regnn_head_bwd: gh = g_loss * p W and the (p^T h | colsum p) slab, p read once each
-            # gh = g_loss * p W on hipBLASLt (it ran this GEMM faster than regnn_head_bwd's gh:
-            # 3.6 vs 5.0 ms at mag-10x, tools/ab_head_bwd.py); d weight and d bias come from
-            # regnn_head_bwd's one pass over p (the chunked bmm + col_sum read p twice)
+            # regnn_head_bwd: gh = g_loss * p W (rows >= n zero-filled in the same launch) and
+            # the (p^T h | colsum p) slab, each kernel reading p once (fp32 MFMA)
             Cp = 16 * ((C + 15) // 16)
             rows = 2048
             slab = (torch.zeros(rows, Cp * K + Cp, dtype=torch.float32, device=p.device)
                     if (need_w or need_b) else None)
+            hc = h.contiguous()
             if need_h:
                 gh = torch.empty_like(h)
-                gh[n:].zero_()
-                torch.mm(p, W * g_loss, out=gh[:n])
-            hc = h.contiguous()
+                gl = g_loss.detach().reshape(1).float().contiguous()
+                with timed("head_gh", 4 * (p.numel() + h.numel())):
+                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W.detach().contiguous()),
+                           None, L.ptr(gl), L.ptr(gh), h.shape[0], None, 0, L.stream())
             if slab is not None:
                 with timed("head_bwd", 4 * (p.numel() + n * K)):
-                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, None, L.ptr(hc), None, None,
+                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, None, L.ptr(hc), None, None, 0,
                            L.ptr(slab), rows, L.stream())
             if slab is not None:
                 tot = _reduce(slab, Cp * K + Cp)

@@ -17,12 +17,12 @@ slab = torch.zeros(rows, Cp * K + Cp, device="cuda")
 
 
 def gh_k():
-    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, L.ptr(gh), None, rows,
-           L.stream())
+    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, L.ptr(gh), n, None,
+           rows, L.stream())
 
 
 def wg_k():
-    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, None, L.ptr(slab),
+    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, None, 0, L.ptr(slab),
            rows, L.stream())
 
 
@@ -42,5 +42,14 @@ def t(fn, it=5):
     return s.elapsed_time(e) / it
 
 
-res = {"gh": t(gh_k), "wgrad": t(wg_k), "old_total": t(old)}
-print({k: f"{v:.2f}ms" for k, v in res.items()}, f"slab_rows={rows}", flush=True)
+def gh_blas():
+    torch.mm(p, W, out=gh)
+
+
+res = {"gh": t(gh_k), "gh_hipblaslt": t(gh_blas), "wgrad": t(wg_k), "old_total": t(old)}
+ref = p @ W
+gh_k()
+torch.cuda.synchronize()
+res_err = float((gh - ref).abs().max() / ref.abs().max())
+print({k: f"{v:.2f}ms" for k, v in res.items()}, f"slab_rows={rows}", f"gh rel err {res_err:.2e}",
+      flush=True)
