@@ -12,7 +12,7 @@ h = torch.randn(n, K, device="cuda")
 W = torch.randn(C, K, device="cuda") * 0.1
 p = torch.randn(n, C, device="cuda") * 1e-3
 gh = torch.empty(n, K, device="cuda")
-rows = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 slab = torch.zeros(rows, Cp * K + Cp, device="cuda")
 
 
