@@ -76,11 +76,114 @@ typedef float f32x4_u __attribute__((ext_vector_type(4), aligned(4)));   // dwor
 constexpr int kHeadK = 64;
 constexpr int kHeadBlock = 512;
 constexpr int kHeadMaxC = 24 * 16;
+constexpr int kX6MaxNT = 23;      // bf16x6 head: three bf16 copies of W^T fit the 160 KiB LDS
 
 // FL: diagnostic variant bits for A/B timing only (regnn_tune key 3): 1 = no prefetch,
 // 2 = no logits stores, 4 = no loss-row epilogue. Shipped variant: FL = 0.
 // AMAX: inference variant (mag/regnn_ns.py:367 out_lin + the caller's argmax): no logits
 // stores and no loss rows; amax[node] = first class of maximal logit (torch.argmax ties).
+// Tail of the fused head for one 16-node tile, shared by the fp32-MFMA and the bf16x6 kernels:
+// argmax (AMAX), logits stores, and for loss rows log-sum-exp, CE term and the scaled softmax
+// gradient. zy_part(y) returns this lane's share of the label logit z_y (its k-slice of h against
+// W[y], plus the bias in one quarter); the four quarters are summed with 2 shuffles.
+template <int NT, int FL, bool AMAX, typename ZY>
+__device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_t tile, int q,
+                                          int C, int64_t rows, int64_t n_loss, float scale,
+                                          const int64_t* __restrict__ labels,
+                                          float* __restrict__ logits, float* __restrict__ p,
+                                          float* __restrict__ loss_rows,
+                                          int64_t* __restrict__ amax, ZY zy_part) {
+    const bool valid = node < rows;
+    if constexpr (AMAX) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int cls = 16 * t + 4 * q + i;
+                if (cls < C && (acc[t][i] > bv || (acc[t][i] == bv && cls < bi))) {
+                    bv = acc[t][i];
+                    bi = cls;
+                }
+            }
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (valid && q == 0) amax[node] = bi;
+        return;
+    }
+    // ---- logits of every valid node: one 16-byte store per class tile (plain stores: the L2
+    // merges the half-line pieces; non-temporal stores bypass that and ran 2x slower) ----
+    if (!(FL & 2) && valid) {
+        float* lr = logits + node * C + 4 * q;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if ((t + 1 < NT || 16 * t + 16 <= C)) {
+                *reinterpret_cast<f32x4_u*>(lr + 16 * t) = acc[t];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (16 * t + 4 * q + i < C) lr[16 * t + i] = acc[t][i];
+            }
+        }
+    }
+    if ((FL & 4) || tile * 16 >= n_loss) return;        // wave-uniform
+    // ---- loss rows: log-sum-exp, CE term, scaled softmax gradient ----
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((t + 1 < NT || 16 * t + 16 <= C) || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    // The label's logit z_y comes from its own 64-term dot (zy_part + 2 shuffles), not from
+    // a per-class compare: 88 compares per lane would hold 88 VCC masks and spill the SGPR
+    // file. acc becomes exp(z - m) in place (one exp per class, reused for the gradient); the
+    // label's entry of p is fixed up afterwards.
+    const int y = node < n_loss ? (int)labels[node] : 0;
+    float zy = zy_part(y);
+    zy += __shfl_xor(zy, 16, 64);
+    zy += __shfl_xor(zy, 32, 64);
+    float se = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int cls = 16 * t + 4 * q + i;
+            const float e = ((t + 1 < NT || 16 * t + 16 <= C) || cls < C) ? __expf(acc[t][i] - m) : 0.f;
+            acc[t][i] = e;
+            se += e;
+        }
+    se += __shfl_xor(se, 16, 64);
+    se += __shfl_xor(se, 32, 64);
+    const float lse = m + __logf(se);
+    if (node < n_loss) {
+        float* pr = p + node * C + 4 * q;
+        const float r = scale / se;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f32x4 v = acc[t] * r;
+            if ((t + 1 < NT || 16 * t + 16 <= C)) {
+                *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
+            }
+        }
+        const int yq = y - 4 * q;              // the label's slot in this lane's tiles
+        if (yq >= 0 && (yq & 15) < 4) {        // same lane, same address: ordered after
+            loss_rows[node] = lse - zy;
+            p[node * C + y] = __expf(zy - m) * r - scale;
+        }
+    }
+}
+
 template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
 __global__ void __launch_bounds__(BLK)
 head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
@@ -146,98 +249,160 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
                 for (int t = 0; t < NT; ++t) bw[t] = bn[t];
             }
         }
-        const bool valid = node < rows;
-        if constexpr (AMAX) {
-            float bv = -INFINITY;
-            int bi = 0x7fffffff;
+        head_tail<NT, FL, AMAX>(acc, node, tile, q, C, rows, n_loss, scale, labels, logits, p,
+                                loss_rows, amax, [&](int y) {
+            float z = 0.f;
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int cls = 16 * t + 4 * q + i;
-                    if (cls < C && (acc[t][i] > bv || (acc[t][i] == bv && cls < bi))) {
-                        bv = acc[t][i];
-                        bi = cls;
-                    }
-                }
-#pragma unroll
-            for (int o = 16; o <= 32; o <<= 1) {
-                const float ov = __shfl_xor(bv, o, 64);
-                const int oi = __shfl_xor(bi, o, 64);
-                if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-            }
-            if (valid && q == 0) amax[node] = bi;
-            continue;
-        }
-        // ---- logits of every valid node: one 16-byte store per class tile ----
-        if (!(FL & 2) && valid) {
-            float* lr = logits + node * C + 4 * q;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                if ((t + 1 < NT || 16 * t + 16 <= C)) {
-                    *reinterpret_cast<f32x4_u*>(lr + 16 * t) = acc[t];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (16 * t + 4 * q + i < C) lr[16 * t + i] = acc[t][i];
-                }
-            }
-        }
-        if ((FL & 4) || tile * 16 >= n_loss) continue;      // wave-uniform
-        // ---- loss rows: log-sum-exp, CE term, scaled softmax gradient ----
-        float m = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if ((t + 1 < NT || 16 * t + 16 <= C) || 16 * t + 4 * q + i < C) m = fmaxf(m, acc[t][i]);
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-        // The label's logit z_y comes from its own 64-term dot (the lane's 16 k of h against
-        // column y of W^T in LDS + 2 shuffles), not from a per-class compare: 88 compares per lane
-        // would hold 88 VCC masks and spill the SGPR file. acc becomes exp(z - m) in place (one
-        // exp per class, reused for the gradient); the label's entry of p is fixed up afterwards.
-        const int y = node < n_loss ? (int)labels[node] : 0;
-        float zy = 0.f;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) zy = fmaf(a[s], Wl[(16 * q + s) * LDW + y], zy);
-        zy += __shfl_xor(zy, 16, 64);
-        zy += __shfl_xor(zy, 32, 64);
-        zy += Wl[K * LDW + y];                      // bias[y]
-        float se = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int cls = 16 * t + 4 * q + i;
-                const float e = ((t + 1 < NT || 16 * t + 16 <= C) || cls < C) ? __expf(acc[t][i] - m) : 0.f;
-                acc[t][i] = e;
-                se += e;
-            }
-        se += __shfl_xor(se, 16, 64);
-        se += __shfl_xor(se, 32, 64);
-        const float lse = m + __logf(se);
-        if (node < n_loss) {
-            float* pr = p + node * C + 4 * q;
-            const float r = scale / se;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const f32x4 v = acc[t] * r;
-                if ((t + 1 < NT || 16 * t + 16 <= C)) {
-                    *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
-                }
-            }
-            const int yq = y - 4 * q;              // the label's slot in this lane's tiles
-            if (yq >= 0 && (yq & 15) < 4) {        // same lane, same address: ordered after
-                loss_rows[node] = lse - zy;
-                p[node * C + y] = __expf(zy - m) * r - scale;
-            }
-        }
+            for (int s = 0; s < 16; ++s) z = fmaf(a[s], Wl[(16 * q + s) * LDW + y], z);
+            return z + (q == 0 ? Wl[K * LDW + y] : 0.f);       // + bias[y] once over the quarters
+        });
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same head on bf16 MFMA with fp32 accuracy ("bf16x6"): every fp32 operand x is split into
+// three bf16 parts x = x0 + x1 + x2 (round-to-nearest each, |x - x0 - x1 - x2| <= 2^-24 |x|), and
+// the six products x_i y_j with i + j <= 2 are accumulated in fp32 by v_mfma_f32_16x16x32_bf16
+// (exact bf16 x bf16 products): the dropped terms are below fp32 resolution. Six 16-cycle MFMAs
+// per 16x16x32 step replace eight 32-cycle fp32 16x16x4 MFMAs: 2.7x the MFMA rate.
+//
+// Same transposed tile as head_fwd_kernel (A = W rows, class on lane & 15; B = h^T, node on
+// lane & 15; C/D: lane (q, c) holds node c, classes 16 t + 4 q + 0..3), so the tail is shared.
+// For 16x16x32 lane (q, c) supplies A[c][k = 8q + j] / B[k = 8q + j][c] (j = 0..7) of each
+// 32-wide k chunk: features 32 kc + 8q .. +7 of its node. The three splits of W live in LDS as
+// bf16 rows of 72 (64 + 8 pad: 144-byte rows put the 16 class rows of a b128 read on disjoint
+// banks), bias after them: 3 * CP * 144 + 4 * CP bytes (<= 153.5 KiB for NT <= 23).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int kX6Row = 72;
+
+__device__ __forceinline__ void split3(float x, uint16_t& a, uint16_t& b, uint16_t& c) {
+    a = f2bf(x);
+    const float r = x - bf2f(a);
+    b = f2bf(r);
+    c = f2bf(r - bf2f(b));
+}
+
+__device__ __forceinline__ bf16x8_t pack8(const uint16_t (&v)[8]) {
+    uint4 u;
+    u.x = uint32_t(v[0]) | (uint32_t(v[1]) << 16);
+    u.y = uint32_t(v[2]) | (uint32_t(v[3]) << 16);
+    u.z = uint32_t(v[4]) | (uint32_t(v[5]) << 16);
+    u.w = uint32_t(v[6]) | (uint32_t(v[7]) << 16);
+    return __builtin_bit_cast(bf16x8_t, u);
+}
+
+template <int NT, bool AMAX>
+__global__ void __launch_bounds__(kHeadBlock)
+head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
+                   const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
+                   int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
+                   float* __restrict__ loss_rows, int64_t* __restrict__ amax) {
+    constexpr int K = kHeadK, CP = NT * 16, LDB = kX6Row;
+    extern __shared__ uint16_t Wb[];                       // [3][CP][LDB] bf16, then fp32 bias
+    for (int idx = threadIdx.x; idx < CP * K; idx += blockDim.x) {
+        const int j = idx / K, k = idx - j * K;
+        uint16_t s0, s1, s2;
+        split3(j < C ? W[(int64_t)j * K + k] : 0.f, s0, s1, s2);
+        Wb[j * LDB + k] = s0;
+        Wb[(CP + j) * LDB + k] = s1;
+        Wb[(2 * CP + j) * LDB + k] = s2;
+    }
+    float* bl = reinterpret_cast<float*>(Wb + 3 * CP * LDB);    // 16-byte aligned (LDB % 8 == 0)
+    for (int j = threadIdx.x; j < CP; j += blockDim.x) bl[j] = (bias && j < C) ? bias[j] : 0.f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int wpb = blockDim.x >> 6;
+    const int64_t n_tiles = (rows + 15) / 16;
+    const f32x4* bl4 = reinterpret_cast<const f32x4*>(bl) + q;  // bias[16 t + 4 q]
+    // lane's A rows: class 16 t + c of split s, k offset 32 kc + 8 q
+    const uint16_t* wa = Wb + c * LDB + 8 * q;
+    const int64_t tstride = (int64_t)gridDim.x * wpb;
+    // features 32 kc + 8 q + j of the lane's node; the next tile's rows are loaded one tile ahead
+    auto load_a = [&](int64_t tile, float (&a)[2][8]) {
+        const int64_t arow = min(tile * 16 + c, rows - 1);
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            const float4* hp = reinterpret_cast<const float4*>(h + arow * K + 32 * kc + 8 * q);
+            const float4 x0 = hp[0], x1 = hp[1];
+            a[kc][0] = x0.x; a[kc][1] = x0.y; a[kc][2] = x0.z; a[kc][3] = x0.w;
+            a[kc][4] = x1.x; a[kc][5] = x1.y; a[kc][6] = x1.z; a[kc][7] = x1.w;
+        }
+    };
+    int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+    float a[2][8], an[2][8];
+    if (tile < n_tiles) load_a(tile, an);
+    for (; tile < n_tiles; tile += tstride) {
+        const int64_t node = tile * 16 + c;
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[kc][j] = an[kc][j];
+        if (tile + tstride < n_tiles) load_a(tile + tstride, an);
+        bf16x8_t hb[2][3];
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(a[kc][j], s0[j], s1[j], s2[j]);
+            hb[kc][0] = pack8(s0);
+            hb[kc][1] = pack8(s1);
+            hb[kc][2] = pack8(s2);
+        }
+        f32x4 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            acc[t] = bl4[4 * t];
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                const uint16_t* w = wa + (16 * t) * LDB + 32 * kc;
+                const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(w);
+                const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(w + CP * LDB);
+                const bf16x8_t w2 = *reinterpret_cast<const bf16x8_t*>(w + 2 * CP * LDB);
+                // small products first
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, hb[kc][0], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, hb[kc][1], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, hb[kc][2], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, hb[kc][0], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, hb[kc][1], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, hb[kc][0], acc[t], 0, 0, 0);
+            }
+        }
+        head_tail<NT, 0, AMAX>(acc, node, tile, q, C, rows, n_loss, scale, labels, logits, p,
+                               loss_rows, amax, [&](int y) {
+            const float* wy = W + (int64_t)y * K + 8 * q;         // fp32 W row (L2-resident)
+            float z = 0.f;
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) z = fmaf(a[kc][j], wy[32 * kc + j], z);
+            return z + (q == 0 ? bl[y] : 0.f);
+        });
+    }
+}
+
+template <int NT, bool AMAX>
+int launch_head_x6(const float* h, int64_t rows, const float* W, const float* b, int C,
+                   const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
+                   float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
+    const size_t lds = (size_t)3 * NT * 16 * kX6Row * sizeof(uint16_t) + NT * 16 * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return REGNN_ELAUNCH;
+        attr = true;
+    }
+    const int64_t tiles = (rows + 15) / 16;
+    int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX>),
+                                    lds, kHeadBlock);
+    if (grid > cap) grid = cap;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((head_fwd_x6_kernel<NT, AMAX>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
+                       stream, h, rows, W, b, C, labels, n_loss, scale, logits, p, loss_rows,
+                       amax);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
@@ -276,9 +441,13 @@ int launch_head(const float* h, int64_t rows, const float* W, const float* b, in
             case 1: return HEAD_V(1);
             case 2: return HEAD_V(2);
             case 4: return HEAD_V(4);
+            case 16: return HEAD_V(0);                     // the fp32-MFMA kernel
             default: break;
         }
     }
+    if constexpr (NT <= kX6MaxNT)
+        return launch_head_x6<NT, false>(h, rows, W, b, C, labels, n_loss, scale, logits, p,
+                                         loss_rows, stream);
     return HEAD_V(0);
 #undef HEAD_V
 }

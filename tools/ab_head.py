@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "re-gnn_amd"))
 import torch
 from regnn_hip import _lib as L
 
-N, n, K, C = int(sys.argv[1]) if len(sys.argv) > 1 else 19_397_430, 7_363_890, 64, 349
+N, n, K = int(sys.argv[1]) if len(sys.argv) > 1 else 19_397_430, 7_363_890, 64
+C = int(os.environ.get("HEAD_C", "349"))
 h = torch.randn(N, K, device="cuda")
 W = torch.randn(C, K, device="cuda") * 0.1
 b = torch.randn(C, device="cuda") * 0.1
