@@ -532,6 +532,88 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
         reinterpret_cast<f32x4*>(gh)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// gh with fp32 accuracy on bf16 MFMA (the bf16x6 split of head_fwd_x6_kernel): gh^T = W^T p^T
+// over 32-class chunks, A = W^T rows (feature 16 kt + c; three bf16 splits in LDS, rows of
+// CP32 + 8 bf16: 16-byte aligned, the 16 feature rows of a b128 read on disjoint banks), B = the
+// lane's p row (classes 32 ch + 8 q .. +7, split on the fly). 4 waves per SIMD (~70 VGPRs).
+template <int NT>
+__global__ void __launch_bounds__(kGhBlock)
+head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ W,
+                  const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out) {
+    constexpr int K = kHeadK, NCH = (NT + 1) / 2, CP32 = 32 * NCH, LDR = CP32 + 8;
+    extern __shared__ uint16_t Wt[];                       // [3][K][LDR] bf16
+    for (int idx = threadIdx.x; idx < CP32 * K; idx += blockDim.x) {
+        const int j = idx / K, k = idx - j * K;             // class j, feature k (W read rowwise)
+        uint16_t s0, s1, s2;
+        split3(j < C ? W[(int64_t)j * K + k] : 0.f, s0, s1, s2);
+        Wt[k * LDR + j] = s0;
+        Wt[(K + k) * LDR + j] = s1;
+        Wt[(2 * K + k) * LDR + j] = s2;
+    }
+    __syncthreads();
+    const float sc = gscale ? *gscale : 1.f;
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int wpb = blockDim.x >> 6;
+    const int64_t n_tiles = (n + 15) / 16;
+    const uint16_t* wa = Wt + c * LDR + 8 * q;             // + (s K + 16 kt) LDR + 32 ch
+    auto load_p = [&](const float* pr, int ch, float (&v)[8]) {
+        const int cls0 = 32 * ch + 8 * q;
+        if (cls0 + 8 <= C) {
+            const f32x4 x0 = *reinterpret_cast<const f32x4_u*>(pr + cls0);
+            const f32x4 x1 = *reinterpret_cast<const f32x4_u*>(pr + cls0 + 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = cls0 + i < C ? pr[cls0 + i] : 0.f;
+        }
+    };
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
+         tile += (int64_t)gridDim.x * wpb) {
+        const int64_t row = tile * 16 + c;
+        const bool valid = row < n;
+        const float* pr = p + (valid ? row : n - 1) * C;
+        f32x4 acc[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float v[8], vn[8];
+        load_p(pr, 0, vn);
+#pragma unroll 1
+        for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = vn[i];
+            if (ch + 1 < NCH) load_p(pr, ch + 1, vn);        // next chunk in flight
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) split3(v[i], s0[i], s1[i], s2[i]);
+            const bf16x8_t b0 = pack8(s0), b1 = pack8(s1), b2 = pack8(s2);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                const uint16_t* w = wa + (16 * kt) * LDR + 32 * ch;
+                const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(w);
+                const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(w + K * LDR);
+                const bf16x8_t w2 = *reinterpret_cast<const bf16x8_t*>(w + 2 * K * LDR);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, b0, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b1, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b2, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b0, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b1, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b0, acc[kt], 0, 0, 0);
+            }
+        }
+        if (valid) {
+            float* gr = gh + row * K + 4 * q;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+                *reinterpret_cast<f32x4*>(gr + 16 * kt) = acc[kt] * sc;
+        }
+    }
+    const int64_t z0 = n * K / 4, z1 = n_out * K / 4;      // rows without a loss term: zero
+    for (int64_t v = z0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < z1;
+         v += (int64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<f32x4*>(gh)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 // gW^T partial of this block's row range: wave w owns class tiles w, w + 8, w + 16; per 4-row
 // k-step lane (q, c) feeds A = p[row0 + q][16 t + c] and B = h[row0 + q][16 j + c], so D[cls][k]
 // accumulates over the rows; gb rides along in VALU adds of the same A values. 8 k-steps
@@ -604,7 +686,26 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
                     hipStream_t stream) {
     constexpr int K = kHeadK;
-    if (gh) {
+    if (gh && g_tune_head != 16) {            // bf16x6 gh (default)
+        constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
+        static bool attr6 = false;
+        if (!attr6) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_gh_x6_kernel<NT>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds) != hipSuccess)
+                return REGNN_ELAUNCH;
+            attr6 = true;
+        }
+        const int64_t tiles = (n + 15) / 16;
+        int64_t grid = (tiles + kGhBlock / 64 - 1) / (kGhBlock / 64);
+        const int cap = resident_blocks(reinterpret_cast<const void*>(&head_gh_x6_kernel<NT>),
+                                        lds, kGhBlock);
+        if (grid > cap) grid = cap;
+        if (grid < 1) grid = 1;
+        hipLaunchKernelGGL((head_gh_x6_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
+                           stream, p, n, C, W, gscale, gh, n_out);
+        REGNN_LAUNCH_CHECK();
+    } else if (gh) {
         const size_t lds = (size_t)K * (NT * 16 + 1) * sizeof(float);
         static bool attr = false;
         if (!attr) {
