@@ -681,6 +681,92 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
     }
 }
 
+// gW^T / gb partial with fp32 accuracy on bf16 MFMA (bf16x6 split, as head_fwd_x6_kernel): the
+// same tiling as head_wgrad_kernel (wave w owns class tiles w, w + 8, w + 16; D[cls][feature]),
+// but one 16x16x32 k-step covers 32 rows: lane (q, c) supplies rows r0 + 8 q + j (j = 0..7) of
+// A = p[., 16 t + c] and B = h[., 16 kt + c], loaded 4 bytes per lane (16 lanes read 64
+// contiguous bytes of a row) and split into three bf16 fragments in registers.
+template <int NT>
+__global__ void __launch_bounds__(kHeadBlock)
+head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ h,
+                     int64_t rows_per_block, float* __restrict__ slab) {
+    constexpr int K = kHeadK, CP = NT * 16, MT = (NT + 7) / 8;
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(n, r0 + rows_per_block);
+    f32x4 acc[MT][4];
+    float gb[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        gb[m] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int64_t row0 = r0; row0 < r1; row0 += 32) {
+        float a[MT][8], b[4][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t rr = row0 + 8 * q + j;
+            const bool ok = rr < r1;
+            const int64_t rc = ok ? rr : r0;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const int cls = 16 * (w + 8 * m) + c;
+                const bool in = ok && (w + 8 * m) < NT && cls < C;
+                const float v = p[rc * C + (cls < C ? cls : 0)];
+                a[m][j] = in ? v : 0.f;
+            }
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                const float v = h[rc * K + 16 * kt + c];
+                b[kt][j] = ok ? v : 0.f;
+            }
+        }
+        bf16x8_t bf[4][3];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(b[kt][j], s0[j], s1[j], s2[j]);
+            bf[kt][0] = pack8(s0); bf[kt][1] = pack8(s1); bf[kt][2] = pack8(s2);
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            if (w + 8 * m >= NT) continue;                 // wave-uniform
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                gb[m] += a[m][j];
+                split3(a[m][j], s0[j], s1[j], s2[j]);
+            }
+            const bf16x8_t a0 = pack8(s0), a1 = pack8(s1), a2 = pack8(s2);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
+                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][0], acc[m][kt], 0, 0, 0);
+            }
+        }
+    }
+    float* out = slab + (int64_t)blockIdx.x * (CP * K + CP);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int t = w + 8 * m;
+        if (t >= NT) continue;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(16 * t + 4 * q + r) * K + 16 * kt + c] = acc[m][kt][r];
+        float g = gb[m];
+        g += __shfl_xor(g, 16, 64);
+        g += __shfl_xor(g, 32, 64);
+        if (q == 0) out[CP * K + 16 * t + c] = g;
+    }
+}
+
 template <int NT>
 int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const float* h,
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
@@ -734,8 +820,12 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
         rpb = (rpb + 31) / 32 * 32;
         grid = (n + rpb - 1) / rpb;
         if (grid < 1) grid = 1;
-        hipLaunchKernelGGL((head_wgrad_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
-                           stream, p, n, C, h, rpb, slab);
+        if (g_tune_head != 16)
+            hipLaunchKernelGGL((head_wgrad_x6_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock),
+                               0, stream, p, n, C, h, rpb, slab);
+        else
+            hipLaunchKernelGGL((head_wgrad_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
+                               stream, p, n, C, h, rpb, slab);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
