@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 6). */
+/* ABI version (bumped on any signature change or addition; currently 7). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -249,14 +249,17 @@ int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t 
 
 /* Fused output head (run_regnn.py:146-148: out_lin over all nodes, log_softmax + nll over the
  * train rows): logits[rows, C] = h[rows, K] W[C, K]^T + b  (b may be NULL), and for the first
- * n_loss rows loss_rows / p exactly as regnn_softmax_xent. fp32 MFMA; K must be 64 and
- * C <= 384 (else REGNN_EINVAL: use a GEMM + regnn_softmax_xent); h 16-byte aligned. */
+ * n_loss rows loss_rows / p exactly as regnn_softmax_xent. logits and p have row stride ld >= C
+ * (ld = 16 * ceil(C / 16) puts every row on 64-byte boundaries: the L2 then merges each row's
+ * stores into whole lines). fp32-accurate MFMA (bf16x6 split for C <= 368, f32 MFMA above);
+ * K must be 64 and C <= 384 (else REGNN_EINVAL: use a GEMM + regnn_softmax_xent); h 16-byte
+ * aligned. */
 int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
-                   int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
-                   float* p, float* loss_rows, hipStream_t stream);
+                   int32_t C, int64_t ld, const int64_t* labels, int64_t n_loss, float scale,
+                   float* logits, float* p, float* loss_rows, hipStream_t stream);
 
-/* Backward of the fused output head from its softmax gradient p [n, C] (regnn_head_fwd), each
- * part reading p once (fp32 MFMA):
+/* Backward of the fused output head from its softmax gradient p [n, C] with row stride ld
+ * (regnn_head_fwd), each part reading p once (fp32-accurate bf16x6 MFMA):
  *   gh (optional, [n_out, K], n_out >= n, 16-byte aligned) = gscale[0] * p W on rows < n
  *      (gscale NULL: 1) and 0 on rows [n, n_out) (nodes without a loss term)
  *   slab (optional): per-block partial rows [rows_used, Cp*K + Cp], Cp = 16 * ceil(C/16):
@@ -264,7 +267,7 @@ int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, cons
  *     the column sums of p (d out_lin.bias). At most slab_rows rows are written: zero the slab
  *     first and reduce its slab_rows rows with regnn_rel_reduce (fixed order).
  *     K must be 64, C <= 384. */
-int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
+int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, const float* W,
                    const float* h, const float* gscale, float* gh, int64_t n_out, float* slab,
                    int32_t slab_rows, hipStream_t stream);
 

@@ -88,7 +88,8 @@ constexpr int kX6MaxNT = 23;      // bf16x6 head: three bf16 copies of W^T fit t
 // W[y], plus the bias in one quarter); the four quarters are summed with 2 shuffles.
 template <int NT, int FL, bool AMAX, typename ZY>
 __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_t tile, int q,
-                                          int C, int64_t rows, int64_t n_loss, float scale,
+                                          int C, int64_t ld, int64_t rows, int64_t n_loss,
+                                          float scale,
                                           const int64_t* __restrict__ labels,
                                           float* __restrict__ logits, float* __restrict__ p,
                                           float* __restrict__ loss_rows,
@@ -117,12 +118,14 @@ __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_
         return;
     }
     // ---- logits of every valid node: one 16-byte store per class tile (plain stores: the L2
-    // merges the half-line pieces; non-temporal stores bypass that and ran 2x slower) ----
+    // merges the half-line pieces; non-temporal stores bypass that and ran 2x slower). With rows
+    // padded to 16 classes the last tile is stored whole too (its pad classes hold 0) ----
+    const bool padded = ld >= 16 * NT;
     if (!(FL & 2) && valid) {
-        float* lr = logits + node * C + 4 * q;
+        float* lr = logits + node * ld + 4 * q;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            if ((t + 1 < NT || 16 * t + 16 <= C)) {
+            if ((t + 1 < NT || padded || 16 * t + 16 <= C)) {
                 *reinterpret_cast<f32x4_u*>(lr + 16 * t) = acc[t];
             } else {
 #pragma unroll
@@ -163,12 +166,12 @@ __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_
     se += __shfl_xor(se, 32, 64);
     const float lse = m + __logf(se);
     if (node < n_loss) {
-        float* pr = p + node * C + 4 * q;
+        float* pr = p + node * ld + 4 * q;
         const float r = scale / se;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const f32x4 v = acc[t] * r;
-            if ((t + 1 < NT || 16 * t + 16 <= C)) {
+            if ((t + 1 < NT || padded || 16 * t + 16 <= C)) {
                 *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
             } else {
 #pragma unroll
@@ -179,7 +182,7 @@ __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_
         const int yq = y - 4 * q;              // the label's slot in this lane's tiles
         if (yq >= 0 && (yq & 15) < 4) {        // same lane, same address: ordered after
             loss_rows[node] = lse - zy;
-            p[node * C + y] = __expf(zy - m) * r - scale;
+            p[node * ld + y] = __expf(zy - m) * r - scale;
         }
     }
 }
@@ -187,7 +190,7 @@ __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_
 template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
 __global__ void __launch_bounds__(BLK)
 head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
-                const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
+                const float* __restrict__ bias, int C, int64_t ld, const int64_t* __restrict__ labels,
                 int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
                 float* __restrict__ loss_rows, int64_t* __restrict__ amax) {
     constexpr bool PIPE = !(FL & 1);
@@ -249,7 +252,7 @@ head_fwd_kernel(const float* __restrict__ h, int64_t rows, const float* __restri
                 for (int t = 0; t < NT; ++t) bw[t] = bn[t];
             }
         }
-        head_tail<NT, FL, AMAX>(acc, node, tile, q, C, rows, n_loss, scale, labels, logits, p,
+        head_tail<NT, FL, AMAX>(acc, node, tile, q, C, ld, rows, n_loss, scale, labels, logits, p,
                                 loss_rows, amax, [&](int y) {
             float z = 0.f;
 #pragma unroll
@@ -294,7 +297,8 @@ __device__ __forceinline__ bf16x8_t pack8(const uint16_t (&v)[8]) {
 template <int NT, bool AMAX>
 __global__ void __launch_bounds__(kHeadBlock)
 head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
-                   const float* __restrict__ bias, int C, const int64_t* __restrict__ labels,
+                   const float* __restrict__ bias, int C, int64_t ld,
+                   const int64_t* __restrict__ labels,
                    int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
                    float* __restrict__ loss_rows, int64_t* __restrict__ amax) {
     constexpr int K = kHeadK, CP = NT * 16, LDB = kX6Row;
@@ -367,7 +371,7 @@ head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __res
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, hb[kc][0], acc[t], 0, 0, 0);
             }
         }
-        head_tail<NT, 0, AMAX>(acc, node, tile, q, C, rows, n_loss, scale, labels, logits, p,
+        head_tail<NT, 0, AMAX>(acc, node, tile, q, C, ld, rows, n_loss, scale, labels, logits, p,
                                loss_rows, amax, [&](int y) {
             const float* wy = W + (int64_t)y * K + 8 * q;         // fp32 W row (L2-resident)
             float z = 0.f;
@@ -381,7 +385,7 @@ head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __res
 }
 
 template <int NT, bool AMAX>
-int launch_head_x6(const float* h, int64_t rows, const float* W, const float* b, int C,
+int launch_head_x6(const float* h, int64_t rows, const float* W, const float* b, int C, int64_t ld,
                    const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                    float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
     const size_t lds = (size_t)3 * NT * 16 * kX6Row * sizeof(uint16_t) + NT * 16 * sizeof(float);
@@ -399,14 +403,14 @@ int launch_head_x6(const float* h, int64_t rows, const float* W, const float* b,
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((head_fwd_x6_kernel<NT, AMAX>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
-                       stream, h, rows, W, b, C, labels, n_loss, scale, logits, p, loss_rows,
+                       stream, h, rows, W, b, C, ld, labels, n_loss, scale, logits, p, loss_rows,
                        amax);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
 
 template <int NT, int FL, bool AMAX = false, int BLK = kHeadBlock>
-int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, int C,
+int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, int C, int64_t ld,
                 const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                 float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
     const size_t lds = ((size_t)kHeadK * (NT * 16 + 1) + NT * 16) * sizeof(float);
@@ -425,17 +429,17 @@ int launch_head_v(const float* h, int64_t rows, const float* W, const float* b, 
     if (grid < 1) grid = 1;
     auto kern = &head_fwd_kernel<NT, FL, AMAX, BLK>;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BLK), lds, stream, h, rows, W, b,
-                       C, labels, n_loss, scale, logits, p, loss_rows, amax);
+                       C, ld, labels, n_loss, scale, logits, p, loss_rows, amax);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
 
 template <int NT>
-int launch_head(const float* h, int64_t rows, const float* W, const float* b, int C,
+int launch_head(const float* h, int64_t rows, const float* W, const float* b, int C, int64_t ld,
                 const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                 float* loss_rows, hipStream_t stream) {
-#define HEAD_V(fl) launch_head_v<NT, fl>(h, rows, W, b, C, labels, n_loss, scale, logits, p, \
-                                            loss_rows, stream)
+#define HEAD_V(fl) launch_head_v<NT, fl>(h, rows, W, b, C, ld, labels, n_loss, scale, logits, \
+                                            p, loss_rows, stream)
     if (NT == 22 && g_tune_head != 0) {
         switch (g_tune_head) {
             case 1: return HEAD_V(1);
@@ -446,7 +450,7 @@ int launch_head(const float* h, int64_t rows, const float* W, const float* b, in
         }
     }
     if constexpr (NT <= kX6MaxNT)
-        return launch_head_x6<NT, false>(h, rows, W, b, C, labels, n_loss, scale, logits, p,
+        return launch_head_x6<NT, false>(h, rows, W, b, C, ld, labels, n_loss, scale, logits, p,
                                          loss_rows, stream);
     return HEAD_V(0);
 #undef HEAD_V
@@ -471,7 +475,7 @@ constexpr int kGhBatch = 4;
 
 template <int NT>
 __global__ void __launch_bounds__(kGhBlock)
-head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ W,
+head_gh_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, const float* __restrict__ W,
                const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out) {
     constexpr int K = kHeadK, CP = NT * 16, LDW = CP + 1;
     extern __shared__ float Wl[];
@@ -488,7 +492,7 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
          tile += (int64_t)gridDim.x * wpb) {
         const int64_t row = tile * 16 + c;
         const bool valid = row < n;
-        const float* pr = p + (valid ? row : n - 1) * C + 4 * q;
+        const float* pr = p + (valid ? row : n - 1) * ld + 4 * q;
         f32x4 acc[4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -538,7 +542,8 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, const float* __res
 // lane's p row (classes 32 ch + 8 q .. +7, split on the fly). 4 waves per SIMD (~70 VGPRs).
 template <int NT>
 __global__ void __launch_bounds__(kGhBlock)
-head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ W,
+head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
+                  const float* __restrict__ W,
                   const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out) {
     constexpr int K = kHeadK, NCH = (NT + 1) / 2, CP32 = 32 * NCH, LDR = CP32 + 8;
     extern __shared__ uint16_t Wt[];                       // [3][K][LDR] bf16
@@ -572,7 +577,7 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
          tile += (int64_t)gridDim.x * wpb) {
         const int64_t row = tile * 16 + c;
         const bool valid = row < n;
-        const float* pr = p + (valid ? row : n - 1) * C;
+        const float* pr = p + (valid ? row : n - 1) * ld;
         f32x4 acc[4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -620,7 +625,7 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
 // (32 rows) of loads are issued before their MFMAs.
 template <int NT>
 __global__ void __launch_bounds__(kHeadBlock)
-head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ h,
+head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, const float* __restrict__ h,
                   int64_t rows_per_block, float* __restrict__ slab) {
     constexpr int K = kHeadK, CP = NT * 16, MT = (NT + 7) / 8, KS = 8;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
@@ -645,7 +650,7 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
             for (int m = 0; m < MT; ++m) {
                 const int cls = 16 * (w + 8 * m) + c;
                 const bool in = ok && (w + 8 * m) < NT && cls < C;
-                const float v = p[rc * C + (cls < C ? cls : 0)];
+                const float v = p[rc * ld + (cls < C ? cls : 0)];
                 a[s][m] = in ? v : 0.f;
             }
 #pragma unroll
@@ -688,7 +693,8 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, const float* __
 // contiguous bytes of a row) and split into three bf16 fragments in registers.
 template <int NT>
 __global__ void __launch_bounds__(kHeadBlock)
-head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float* __restrict__ h,
+head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
+                     const float* __restrict__ h,
                      int64_t rows_per_block, float* __restrict__ slab) {
     constexpr int K = kHeadK, CP = NT * 16, MT = (NT + 7) / 8;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
@@ -713,7 +719,7 @@ head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float*
             for (int m = 0; m < MT; ++m) {
                 const int cls = 16 * (w + 8 * m) + c;
                 const bool in = ok && (w + 8 * m) < NT && cls < C;
-                const float v = p[rc * C + (cls < C ? cls : 0)];
+                const float v = p[rc * ld + (cls < C ? cls : 0)];
                 a[m][j] = in ? v : 0.f;
             }
 #pragma unroll
@@ -768,7 +774,7 @@ head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, const float*
 }
 
 template <int NT>
-int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const float* h,
+int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W, const float* h,
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
                     hipStream_t stream) {
     constexpr int K = kHeadK;
@@ -789,7 +795,7 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
         if (grid > cap) grid = cap;
         if (grid < 1) grid = 1;
         hipLaunchKernelGGL((head_gh_x6_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
-                           stream, p, n, C, W, gscale, gh, n_out);
+                           stream, p, n, C, ld, W, gscale, gh, n_out);
         REGNN_LAUNCH_CHECK();
     } else if (gh) {
         const size_t lds = (size_t)K * (NT * 16 + 1) * sizeof(float);
@@ -808,7 +814,7 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
         if (grid > cap) grid = cap;
         if (grid < 1) grid = 1;
         hipLaunchKernelGGL((head_gh_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
-                           stream, p, n, C, W, gscale, gh, n_out);
+                           stream, p, n, C, ld, W, gscale, gh, n_out);
         REGNN_LAUNCH_CHECK();
     }
     if (slab) {
@@ -822,10 +828,10 @@ int launch_head_bwd(const float* p, int64_t n, int C, const float* W, const floa
         if (grid < 1) grid = 1;
         if (g_tune_head != 16)
             hipLaunchKernelGGL((head_wgrad_x6_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock),
-                               0, stream, p, n, C, h, rpb, slab);
+                               0, stream, p, n, C, ld, h, rpb, slab);
         else
             hipLaunchKernelGGL((head_wgrad_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
-                               stream, p, n, C, h, rpb, slab);
+                               stream, p, n, C, ld, h, rpb, slab);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;
@@ -860,16 +866,16 @@ int regnn_softmax_xent(const float* logits, int64_t rows, int32_t cols, int64_t 
 }
 
 int regnn_head_fwd(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
-                   int32_t C, const int64_t* labels, int64_t n_loss, float scale, float* logits,
-                   float* p, float* loss_rows, hipStream_t stream) {
-    if (!h || !W || !logits || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC ||
+                   int32_t C, int64_t ld, const int64_t* labels, int64_t n_loss, float scale,
+                   float* logits, float* p, float* loss_rows, hipStream_t stream) {
+    if (!h || !W || !logits || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C ||
         n_loss < 0 || n_loss > rows || (n_loss > 0 && (!labels || !p || !loss_rows)) ||
         (reinterpret_cast<uintptr_t>(h) & 15))
         return REGNN_EINVAL;
     if (rows == 0) return REGNN_OK;
     switch ((C + 15) / 16) {
 #define HEAD_CASE(nt) \
-        case nt: return launch_head<nt>(h, rows, W, b, C, labels, n_loss, scale, logits, p, \
+        case nt: return launch_head<nt>(h, rows, W, b, C, ld, labels, n_loss, scale, logits, p, \
                                         loss_rows, stream);
         HEAD_CASE(1) HEAD_CASE(2) HEAD_CASE(3) HEAD_CASE(4) HEAD_CASE(5) HEAD_CASE(6)
         HEAD_CASE(7) HEAD_CASE(8) HEAD_CASE(9) HEAD_CASE(10) HEAD_CASE(11) HEAD_CASE(12)
@@ -888,8 +894,8 @@ int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, c
     if (rows == 0) return REGNN_OK;
     switch ((C + 15) / 16) {
 #define AMAX_CASE(nt) \
-        case nt: return launch_head_v<nt, 0, true>(h, rows, W, b, C, nullptr, 0, 1.f, nullptr, \
-                                                   nullptr, nullptr, stream, out);
+        case nt: return launch_head_v<nt, 0, true>(h, rows, W, b, C, C, nullptr, 0, 1.f,      \
+                                                   nullptr, nullptr, nullptr, stream, out);
         AMAX_CASE(1) AMAX_CASE(2) AMAX_CASE(3) AMAX_CASE(4) AMAX_CASE(5) AMAX_CASE(6)
         AMAX_CASE(7) AMAX_CASE(8) AMAX_CASE(9) AMAX_CASE(10) AMAX_CASE(11) AMAX_CASE(12)
         AMAX_CASE(13) AMAX_CASE(14) AMAX_CASE(15) AMAX_CASE(16) AMAX_CASE(17) AMAX_CASE(18)
@@ -899,18 +905,18 @@ int regnn_head_argmax(const float* h, int64_t rows, int32_t K, const float* W, c
     }
 }
 
-int regnn_head_bwd(const float* p, int64_t n, int32_t C, int32_t K, const float* W,
+int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, const float* W,
                    const float* h, const float* gscale, float* gh, int64_t n_out, float* slab,
                    int32_t slab_rows, hipStream_t stream) {
-    if (!p || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || (gh && !W) ||
+    if (!p || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C || (gh && !W) ||
         (gh && n_out < n) || (slab && (!h || slab_rows <= 0)) ||
         (gh && (reinterpret_cast<uintptr_t>(gh) & 15)))
         return REGNN_EINVAL;
     if (n == 0 && !(gh && n_out > 0)) return REGNN_OK;
     switch ((C + 15) / 16) {
 #define HB_CASE(nt) \
-        case nt: return launch_head_bwd<nt>(p, n, C, W, h, gscale, gh, n_out, slab, slab_rows, \
-                                            stream);
+        case nt: return launch_head_bwd<nt>(p, n, C, ld, W, h, gscale, gh, n_out, slab,       \
+                                            slab_rows, stream);
         HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
         HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
         HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)

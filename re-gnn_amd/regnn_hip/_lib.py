@@ -42,7 +42,7 @@ _SIG = {
                                ctypes.c_int),
     "regnn_spmm_fwd_fused": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P,
                               P, I32, P, P, I32, P, P, P, P, F32, I32, P], ctypes.c_int),
-    "regnn_head_bwd": ([P, I64, I32, I32, P, P, P, P, I64, P, I32, P], ctypes.c_int),
+    "regnn_head_bwd": ([P, I64, I32, I64, I32, P, P, P, P, I64, P, I32, P], ctypes.c_int),
     "regnn_head_argmax": ([P, I64, I32, P, P, I32, P, P], ctypes.c_int),
     "regnn_gatv2_score_fwd": ([P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
     "regnn_gatv2_score_bwd_dst": ([P, P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P],
@@ -63,7 +63,7 @@ _SIG = {
     "regnn_softmax_xent": ([P, I64, I32, I64, P, F32, P, P, P], ctypes.c_int),
     "regnn_attn_dots_fwd": ([P, P, P, I64, I32, I32, P, P, P], ctypes.c_int),
     "regnn_attn_dots_bwd": ([P, P, P, P, P, I64, I32, I32, P, P, I32, P], ctypes.c_int),
-    "regnn_head_fwd": ([P, I64, I32, P, P, I32, P, I64, F32, P, P, P, P], ctypes.c_int),
+    "regnn_head_fwd": ([P, I64, I32, P, P, I32, I64, P, I64, F32, P, P, P, P], ctypes.c_int),
     "regnn_sample_count": ([P, P, I64, I32, P, P], ctypes.c_int),
     "regnn_sample_fill": ([P, P, P, I64, I32, U64, P, P, P, P], ctypes.c_int),
 }
@@ -74,7 +74,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 6
+ABI_VERSION = 7
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

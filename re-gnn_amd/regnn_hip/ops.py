@@ -598,19 +598,23 @@ class _HeadCE(torch.autograd.Function):
         ctx.set_materialize_grads(False)          # no all-rows zero gradient for `logits`
         n, C = labels.numel(), W.shape[0]
         dev = h.device
-        p = torch.empty(n, C, dtype=torch.float32, device=dev)
         loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
         lab = labels.to(torch.int64).contiguous()
         if head_fused(h.shape[1], C) and h.dtype == torch.float32:
             h = h.contiguous()
             Wc = W.detach().contiguous()
-            logits = torch.empty(h.shape[0], C, dtype=torch.float32, device=dev)
-            nbytes = 4 * (h.numel() + logits.numel() + p.numel() + n) + 8 * n
+            # rows padded to 16 classes (64-byte aligned): logits is a [rows, C] view of it
+            ld = 16 * ((C + 15) // 16)
+            logits = torch.empty(h.shape[0], ld, dtype=torch.float32, device=dev)[:, :C]
+            p = torch.empty(n, ld, dtype=torch.float32, device=dev)[:, :C]
+            nbytes = 4 * (h.numel() + h.shape[0] * C + n * C + n) + 8 * n
             with timed("head_fwd", nbytes):
                 L.call("regnn_head_fwd", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc),
-                       L.ptr(b.detach().contiguous()) if b is not None else None, C, L.ptr(lab),
-                       n, 1.0 / n, L.ptr(logits), L.ptr(p), L.ptr(loss_rows), L.stream())
+                       L.ptr(b.detach().contiguous()) if b is not None else None, C, ld,
+                       L.ptr(lab), n, 1.0 / n, L.ptr(logits), L.ptr(p), L.ptr(loss_rows),
+                       L.stream())
         else:
+            p = torch.empty(n, C, dtype=torch.float32, device=dev)
             logits = torch.addmm(b, h, W.t()) if b is not None else h @ W.t()
             with timed("softmax_xent", n * C * 8):
                 L.call("regnn_softmax_xent", L.ptr(logits), n, C, logits.stride(0), L.ptr(lab),
@@ -643,12 +647,13 @@ class _HeadCE(torch.autograd.Function):
                 gh = torch.empty_like(h)
                 gl = g_loss.detach().reshape(1).float().contiguous()
                 with timed("head_gh", 4 * (p.numel() + h.numel())):
-                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W.detach().contiguous()),
-                           None, L.ptr(gl), L.ptr(gh), h.shape[0], None, 0, L.stream())
+                    L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K,
+                           L.ptr(W.detach().contiguous()), None, L.ptr(gl), L.ptr(gh),
+                           h.shape[0], None, 0, L.stream())
             if slab is not None:
                 with timed("head_bwd", 4 * (p.numel() + n * K)):
-                    L.call("regnn_head_bwd", L.ptr(p), n, C, K, None, L.ptr(hc), None, None, 0,
-                           L.ptr(slab), rows, L.stream())
+                    L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K, None, L.ptr(hc),
+                           None, None, 0, L.ptr(slab), rows, L.stream())
             if slab is not None:
                 tot = _reduce(slab, Cp * K + Cp)
                 if need_w:

@@ -12,19 +12,20 @@ h = torch.randn(N, K, device="cuda")
 W = torch.randn(C, K, device="cuda") * 0.1
 b = torch.randn(C, device="cuda") * 0.1
 y = torch.randint(0, C, (n,), device="cuda")
-logits = torch.empty(N, C, device="cuda")
-p = torch.empty(n, C, device="cuda")
+LD = int(os.environ.get("HEAD_LD", str(16 * ((C + 15) // 16))))   # row stride of logits / p
+logits = torch.empty(N, LD, device="cuda")
+p = torch.empty(n, LD, device="cuda")
 lr = torch.empty(n, device="cuda")
 
 
 def fused():
-    L.call("regnn_head_fwd", L.ptr(h), N, K, L.ptr(W), L.ptr(b), C, L.ptr(y), n, 1.0 / n,
+    L.call("regnn_head_fwd", L.ptr(h), N, K, L.ptr(W), L.ptr(b), C, LD, L.ptr(y), n, 1.0 / n,
            L.ptr(logits), L.ptr(p), L.ptr(lr), L.stream())
 
 
 def unfused():
     z = torch.addmm(b, h, W.t())
-    L.call("regnn_softmax_xent", L.ptr(z), n, C, C, L.ptr(y), 1.0 / n, L.ptr(p), L.ptr(lr),
+    L.call("regnn_softmax_xent", L.ptr(z), n, C, C, L.ptr(y), 1.0 / n, L.ptr(p[:, :C].contiguous()), L.ptr(lr),
            L.stream())
 
 

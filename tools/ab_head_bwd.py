@@ -17,12 +17,12 @@ slab = torch.zeros(rows, Cp * K + Cp, device="cuda")
 
 
 def gh_k():
-    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, L.ptr(gh), n, None,
+    L.call("regnn_head_bwd", L.ptr(p), n, C, C, K, L.ptr(W), L.ptr(h), None, L.ptr(gh), n, None,
            rows, L.stream())
 
 
 def wg_k():
-    L.call("regnn_head_bwd", L.ptr(p), n, C, K, L.ptr(W), L.ptr(h), None, None, 0, L.ptr(slab),
+    L.call("regnn_head_bwd", L.ptr(p), n, C, C, K, L.ptr(W), L.ptr(h), None, None, 0, L.ptr(slab),
            rows, L.stream())
 
 
