@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 7). */
+/* ABI version (bumped on any signature change or addition; currently 8). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -239,6 +239,18 @@ int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals
  * Replaces torch's grad.sum(0) for the bias gradient of nn.Linear heads over all nodes
  * (model/REGCN.py:32,45 out_lin), which ran far below HBM rate for N ~ 1e7 rows. */
 int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipStream_t stream);
+
+/* Per-type input projection fused with the first aggregation's pre-scale (model/REGCN.py:31-35
+ * fc_list, then layer/REGraphConv.py:56,73-76 feat_dropout and feat * norm): for the rows of one
+ * node type, x [rows, K] (dtype), W [F, K] fp32, b [F] fp32 (16-byte aligned):
+ *   h [row0 + r]  = x[r] W^T + b                          (rows of the concatenated layer input)
+ *   xs[row0 + r] = scale[row0 + r] * drop(h[row0 + r])     (as regnn_row_scale(h), same mask)
+ * h / xs: dtype, [*, F] row-major. fp32-accurate (bf16x6 MFMA). F must be 64; K <= 256
+ * (REGNN_EUNSUPPORTED above: use a GEMM + regnn_row_scale). scale may be NULL (1). */
+int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_t dtype,
+                       const float* W, const float* b, const float* scale,
+                       const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                       int64_t row0, void* h, void* xs, hipStream_t stream);
 
 /* Row-wise softmax cross-entropy of the output head over `rows` logit rows (stride ld):
  * loss_rows[r] = logsumexp(z_r) - z_r[labels[r]];  p[r, c] = scale * (softmax(z_r)_c - [c == y_r])

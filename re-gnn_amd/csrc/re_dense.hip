@@ -837,11 +837,211 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
     return REGNN_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Per-type input projection fused with the first aggregation's pre-scale (model/REGCN.py:31-35
+// fc_list + layer/REGraphConv.py:56,73-76): for rows r of one node type
+//   h[row0 + r]  = x[r] W^T + b                        (the layer input, kept for the backward)
+//   xs[row0 + r] = scale[row0 + r] * drop(h[row0 + r])  (what the aggregation gathers)
+// with drop the regnn_spmm_fwd_dropout mask of (global row, 16-byte vector), applied to h as
+// stored (rounded to the storage type), so xs equals regnn_row_scale(h). This removes the
+// separate row pass over h (2 N F s bytes) and replaces the hipBLASLt GEMM.
+// fp32-accurate bf16 MFMA (bf16x6 split as head_fwd_x6_kernel; bf16 inputs are exact in their
+// first split, so 3 products suffice), transposed tile: A = W rows (feature 16 kt + c), B = x^T
+// (node on lane & 15), lane (q, c) ends with features 16 kt + 4 q .. +3 of node c.
+constexpr int kProjF = 64;
+
+template <typename T> struct XLoad;
+template <> struct XLoad<float> {
+    // 8 consecutive features k0 .. k0+7 (zero past K)
+    __device__ __forceinline__ static void load(const float* row, int k0, int K, float (&v)[8]) {
+        if (k0 + 8 <= K && (K & 3) == 0) {
+            const float4 a = *reinterpret_cast<const float4*>(row + k0);
+            const float4 b = *reinterpret_cast<const float4*>(row + k0 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = k0 + j < K ? row[k0 + j] : 0.f;
+        }
+    }
+};
+template <> struct XLoad<bf16_t> {
+    __device__ __forceinline__ static void load(const bf16_t* row, int k0, int K, float (&v)[8]) {
+        if (k0 + 8 <= K && (K & 7) == 0) {
+            Vec<bf16_t>::load(row + k0, v);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = k0 + j < K ? bf2f(row[k0 + j]) : 0.f;
+        }
+    }
+};
+
+__device__ __forceinline__ float to_storage(float v, float*) { return v; }
+__device__ __forceinline__ float to_storage(float v, bf16_t*) { return bf2f(f2bf(v)); }
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(kHeadBlock)
+type_project_kernel(const T* __restrict__ x, int64_t rows, int K, const float* __restrict__ W,
+                    const float* __restrict__ bias, const float* __restrict__ scale,
+                    const uint64_t* __restrict__ drop_seed, uint32_t drop_thresh,
+                    float drop_scale, int64_t row0, T* __restrict__ h, T* __restrict__ xs) {
+    constexpr int F = kProjF, KP = 32 * NCH, LDR = KP + 8, EV = Vec<T>::N;
+    constexpr bool EXACT_X = sizeof(T) == 2;            // bf16 x: its first split is exact
+    extern __shared__ uint16_t Wp[];                   // [3][F][LDR] bf16 splits of W
+    for (int idx = threadIdx.x; idx < F * KP; idx += blockDim.x) {
+        const int f = idx / KP, k = idx - f * KP;
+        uint16_t s0, s1, s2;
+        split3(k < K ? W[(int64_t)f * K + k] : 0.f, s0, s1, s2);
+        Wp[f * LDR + k] = s0;
+        Wp[(F + f) * LDR + k] = s1;
+        Wp[(2 * F + f) * LDR + k] = s2;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int wpb = blockDim.x >> 6;
+    const int64_t n_tiles = (rows + 15) / 16;
+    const uint16_t* wa = Wp + c * LDR + 8 * q;
+    uint32_t key = 0;
+    if (drop_seed) key = drop_key(drop_seed);
+    for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
+         tile += (int64_t)gridDim.x * wpb) {
+        const int64_t r = tile * 16 + c;
+        const bool valid = r < rows;
+        const T* xr = x + (valid ? r : rows - 1) * K;
+        f32x4 acc[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[kt] = *reinterpret_cast<const f32x4*>(bias + 16 * kt + 4 * q);
+#pragma unroll 1
+        for (int ch = 0; ch < NCH; ++ch) {
+            float v[8];
+            XLoad<T>::load(xr, 32 * ch + 8 * q, K, v);
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(v[j], s0[j], s1[j], s2[j]);
+            const bf16x8_t b0 = pack8(s0), b1 = pack8(s1), b2 = pack8(s2);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                const uint16_t* w = wa + (16 * kt) * LDR + 32 * ch;
+                const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(w);
+                const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(w + F * LDR);
+                const bf16x8_t w2 = *reinterpret_cast<const bf16x8_t*>(w + 2 * F * LDR);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, b0, acc[kt], 0, 0, 0);
+                if constexpr (!EXACT_X) {
+                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b1, acc[kt], 0, 0, 0);
+                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b2, acc[kt], 0, 0, 0);
+                }
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b0, acc[kt], 0, 0, 0);
+                if constexpr (!EXACT_X)
+                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b1, acc[kt], 0, 0, 0);
+                acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b0, acc[kt], 0, 0, 0);
+            }
+        }
+        if (!valid) continue;
+        const int64_t g = row0 + r;                     // global row: scale index, mask counter
+        const float sc = scale ? scale[g] : 1.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            const int f0 = 16 * kt + 4 * q;              // this lane's 4 features
+            float hv[4], xv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                hv[i] = to_storage(acc[kt][i], static_cast<T*>(nullptr));
+                xv[i] = hv[i] * sc;
+            }
+            if (drop_seed) {
+                // the mask of the 16-byte vector holding f0 (fp32: exactly these 4 features;
+                // bf16: 8 features, this lane's half)
+                float m[EV];
+#pragma unroll
+                for (int i = 0; i < EV; ++i) m[i] = 1.f;
+                const int vec = f0 / EV, off = f0 - vec * EV;
+                if ((drop_thresh & 0xFFu) == 0)
+                    drop_apply<EV, 8>(key, drop_thresh, drop_scale, g, F / EV, vec, m);
+                else
+                    drop_apply<EV, 16>(key, drop_thresh, drop_scale, g, F / EV, vec, m);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xv[i] = m[off + i] != 0.f ? xv[i] * drop_scale : 0.f;
+            }
+            if constexpr (sizeof(T) == 4) {
+                *reinterpret_cast<float4*>(h + g * F + f0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+                *reinterpret_cast<float4*>(xs + g * F + f0) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+            } else {
+                uint2 hb, xb;
+                hb.x = uint32_t(f2bf(hv[0])) | (uint32_t(f2bf(hv[1])) << 16);
+                hb.y = uint32_t(f2bf(hv[2])) | (uint32_t(f2bf(hv[3])) << 16);
+                xb.x = uint32_t(f2bf(xv[0])) | (uint32_t(f2bf(xv[1])) << 16);
+                xb.y = uint32_t(f2bf(xv[2])) | (uint32_t(f2bf(xv[3])) << 16);
+                *reinterpret_cast<uint2*>(h + g * F + f0) = hb;
+                *reinterpret_cast<uint2*>(xs + g * F + f0) = xb;
+            }
+        }
+    }
+}
+
+template <typename T, int NCH>
+int launch_type_project(const void* x, int64_t rows, int K, const float* W, const float* b,
+                        const float* scale, const uint64_t* seed, uint32_t keep16, float dscale,
+                        int64_t row0, void* h, void* xs, hipStream_t stream) {
+    constexpr size_t lds = (size_t)3 * kProjF * (32 * NCH + 8) * sizeof(uint16_t);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&type_project_kernel<T, NCH>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return REGNN_ELAUNCH;
+        attr = true;
+    }
+    const int64_t tiles = (rows + 15) / 16;
+    int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&type_project_kernel<T, NCH>),
+                                    lds, kHeadBlock);
+    if (grid > cap) grid = cap;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((type_project_kernel<T, NCH>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
+                       stream, static_cast<const T*>(x), rows, K, W, b, scale, seed, keep16, dscale,
+                       row0, static_cast<T*>(h), static_cast<T*>(xs));
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+template <typename T>
+int dispatch_type_project(const void* x, int64_t rows, int K, const float* W, const float* b,
+                          const float* scale, const uint64_t* seed, uint32_t keep16, float dscale,
+                          int64_t row0, void* h, void* xs, hipStream_t stream) {
+    switch ((K + 31) / 32) {
+#define TP_CASE(nch) \
+        case nch: return launch_type_project<T, nch>(x, rows, K, W, b, scale, seed, keep16, \
+                                                     dscale, row0, h, xs, stream);
+        TP_CASE(1) TP_CASE(2) TP_CASE(3) TP_CASE(4) TP_CASE(5) TP_CASE(6) TP_CASE(7) TP_CASE(8)
+#undef TP_CASE
+        default: return REGNN_EUNSUPPORTED;
+    }
+}
+
 }  // namespace regnn
 
 using namespace regnn;
 
 extern "C" {
+
+int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_t dtype,
+                       const float* W, const float* b, const float* scale,
+                       const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                       int64_t row0, void* h, void* xs, hipStream_t stream) {
+    if (rows < 0 || K <= 0 || F != kProjF || !W || !b || row0 < 0 ||
+        (rows > 0 && (!x || !h || !xs)) || (drop_seed && drop_keep16 > 65536u) ||
+        (reinterpret_cast<uintptr_t>(b) & 15) || (reinterpret_cast<uintptr_t>(h) & 7) ||
+        (reinterpret_cast<uintptr_t>(xs) & 7))
+        return REGNN_EINVAL;
+    if (K > 256) return REGNN_EUNSUPPORTED;
+    if (rows == 0) return REGNN_OK;
+    if (dtype == REGNN_F32)
+        return dispatch_type_project<float>(x, rows, K, W, b, scale, drop_seed, drop_keep16,
+                                            drop_scale, row0, h, xs, stream);
+    if (dtype == REGNN_BF16)
+        return dispatch_type_project<bf16_t>(x, rows, K, W, b, scale, drop_seed, drop_keep16,
+                                             drop_scale, row0, h, xs, stream);
+    return REGNN_EUNSUPPORTED;
+}
 
 int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipStream_t stream) {
     if (!x || !slab || rows < 0 || cols <= 0) return REGNN_EINVAL;

@@ -40,10 +40,18 @@ class REGraphConv(nn.Module):
             init.zeros_(self.bias)
         init.constant_(self.edge_weight, 1.0 / self.alpha)
 
-    def forward(self, graph, feat, e_feat, return_embedding=False, pre_dropout=0.0):
+    def forward(self, graph, feat, e_feat, return_embedding=False, pre_dropout=0.0,
+                project=None):
         """``pre_dropout`` (not in the reference signature, default off): the probability of a
         caller's nn.Dropout applied to ``feat`` just before this layer (model/REGCN.py:43), so
-        both dropouts fuse into the aggregation's gather when it reads ``feat`` directly."""
+        both dropouts fuse into the aggregation's gather when it reads ``feat`` directly.
+
+        ``project`` (not in the reference signature): instead of ``feat``, a callable
+        ``project(norm, drop) -> (feat, norm * drop(feat))`` for a weightless normalised layer:
+        the caller's producer of ``feat`` forms the pre-scaled rows the aggregation gathers
+        (nets.REGCN with ops.type_project_prescale); results are the same."""
+        if project is not None:
+            return self._forward_projected(graph, e_feat, project)
         rg = relgraph(graph, feat.device)
         pack = rg.rel_pack(e_feat, num_rel=self.edge_weight.shape[0])
         keep = 1.0
@@ -73,6 +81,24 @@ class REGraphConv(nn.Module):
                                         dropout=p_drop), self.weight)
             if self.bias is not None:
                 rst = rst + self.bias
+        if self.activation is not None:
+            rst = self.activation(rst)                                   # :103-104
+        return rst
+
+    def _forward_projected(self, graph, e_feat, project):
+        if self.weight is not None or not self.norm:
+            raise ValueError("project= needs a weightless, normalised layer")
+        dev = self.edge_weight.device
+        rg = relgraph(graph, dev)
+        pack = rg.rel_pack(e_feat, num_rel=self.edge_weight.shape[0])
+        p_drop = self.feat_dropout.p if self.training else 0.0           # :56
+        tab = relation_table(self.edge_weight, self.alpha)               # :58-61
+        norm = ops.degree_norm(rg, pack, tab)                            # :66-75
+        drop = ops.drop_request(p_drop, dev) if 0.0 < p_drop < 1.0 else None
+        feat, xs = project(norm.detach(), drop)                          # :56,73-76 fused
+        rst = ops.re_spmm(rg, feat, tab, pack, pre=norm, post=norm, bias=self.bias,
+                          dropout=p_drop if drop is not None else 0.0,
+                          drop_seed=None if drop is None else drop[0], prescaled=xs)
         if self.activation is not None:
             rst = self.activation(rst)                                   # :103-104
         return rst

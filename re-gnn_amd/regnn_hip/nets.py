@@ -97,6 +97,11 @@ def _input_proj(feats_dim_list, width):
     return fcs
 
 
+# REGCN: fuse the input projection with the first layer's pre-scale (ops.type_project_prescale)
+# where the shapes allow; False runs the unfused composition (A/B, tests)
+FUSE_PROJECTION = True
+
+
 class REGCN(nn.Module):
     """model/REGCN.py:6-46: per-type Linear -> L x REGraphConv (first/last weightless) -> out_lin."""
 
@@ -119,8 +124,15 @@ class REGCN(nn.Module):
 
     def embed(self, features_list, e_feat):
         """everything before out_lin: the node embeddings the reference returns as `h`."""
-        h = type_project(self.fc_list, features_list)
-        h = self.layers[0](self.g, h, e_feat)
+        l0 = self.layers[0]
+        if FUSE_PROJECTION and l0.weight is None and l0.norm and \
+                ops.type_project_fusable(self.fc_list, features_list):
+            # per-type Linear + the first layer's feat_dropout and norm pre-scale in one pass
+            h = l0(self.g, None, e_feat, project=lambda norm, drop: ops.type_project_prescale(
+                self.fc_list, features_list, norm, drop))
+        else:
+            h = type_project(self.fc_list, features_list)
+            h = l0(self.g, h, e_feat)
         p = self.dropout.p if self.training else 0.0
         for layer in self.layers[1:]:
             # model dropout (model/REGCN.py:43) handed to the layer: fused with its own

@@ -163,14 +163,15 @@ class _ReSpmm(torch.autograd.Function):
     drop = the optional fused dropout of the gathered rows (regnn_spmm_fwd_dropout)."""
 
     @staticmethod
-    def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None):
+    def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None, prescaled=None):
         x = x.contiguous()
         F = x.shape[1]
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
         t = _flat_table(tab)
         plan_args, part = _plan_args(rg.csr_plan, F, x.device)
-        prescale = _use_prescale(x, pre, drop)
-        src, in_scale = x, pre
+        # prescaled: pre * drop(x) already formed by the producer of x (regnn_type_project)
+        prescale = prescaled is None and _use_prescale(x, pre, drop)
+        src, in_scale = (x, pre) if prescaled is None else (prescaled, None)
         with timed("spmm_fwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_fwd")):
             if prescale:
@@ -183,7 +184,7 @@ class _ReSpmm(torch.autograd.Function):
                     L.ptr(t), None, L.ptr(in_scale), L.ptr(post),
                     L.ptr(None if bias is None else bias.detach().float().contiguous()),
                     L.ptr(src), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args)
-            if drop is None or prescale:
+            if drop is None or prescale or prescaled is not None:
                 L.call("regnn_spmm_fwd", *args, L.stream())
             else:
                 L.call("regnn_spmm_fwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
@@ -255,26 +256,99 @@ class _ReSpmm(torch.autograd.Function):
                     yf, gf = y.float(), gy.float()
                     g_post = (gf * yf).sum(1) / post
         g_bias = gy.float().sum(0) if need_bias else None
-        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None
+        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None, None
 
 
 def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=0.0,
-            drop_seed=None):
+            drop_seed=None, prescaled=None):
     """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * drop(x)[u] + bias  (HIP).
 
     dropout: probability of an nn.Dropout applied to x in front of the aggregation; fused into
     the gather for 256-byte rows (no dropped copy, no mask tensor), a torch dropout otherwise.
     The bias is fused into the kernel epilogue unless the backward needs the pre-bias output
-    (differentiable post-scale: the node-norm gradient reads <g, y> / post)."""
+    (differentiable post-scale: the node-norm gradient reads <g, y> / post).
+
+    prescaled: pre * drop(x) formed by x's producer (type_project_prescale, same pre and
+    drop_seed); the forward gathers it directly, the backward is unchanged."""
     drop = None
     if dropout:
         if dropout < 1.0 and dropout_fusable(x):
             drop = drop_request(dropout, x.device, drop_seed)
         else:
+            if prescaled is not None:
+                raise ValueError("prescaled input with an unfusable dropout")
             x = torch.nn.functional.dropout(x, dropout, training=True)
     if bias is not None and post is not None and post.requires_grad:
-        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop) + bias
-    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop)
+        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop, prescaled) + bias
+    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop, prescaled)
+
+
+class _TypeProjPre(torch.autograd.Function):
+    """h = cat_t(x_t W_t^T + b_t) and xs = scale * drop(h) in one HIP pass per node type
+    (regnn_type_project); xs is a non-differentiable side output for the aggregation's gather,
+    d h flows to W_t / b_t as in nets._TypeProjFn."""
+
+    @staticmethod
+    def forward(ctx, n, scale, drop, *args):
+        xs_in, Ws, bs = args[:n], args[n:2 * n], args[2 * n:]
+        rows = [x.shape[0] for x in xs_in]
+        dev, dt = xs_in[0].device, xs_in[0].dtype
+        F = Ws[0].shape[0]
+        h = torch.empty(sum(rows), F, dtype=dt, device=dev)
+        xs = torch.empty_like(h)
+        seed, keep16, dscale = (None, 0, 1.0) if drop is None else (L.ptr(drop[0]), drop[1],
+                                                                    drop[2])
+        sc = None if scale is None else scale.detach().float().contiguous()
+        o = 0
+        with timed("type_project", sum(x.numel() * x.element_size() for x in xs_in)
+                   + 2 * h.numel() * h.element_size()):
+            for x, W, b, r in zip(xs_in, Ws, bs, rows):
+                x = x.contiguous()
+                L.call("regnn_type_project", L.ptr(x), r, x.shape[1], F, L.dtype_code(x),
+                       L.ptr(W.detach().float().contiguous()),
+                       L.ptr(b.detach().float().contiguous()), L.ptr(sc), seed, keep16, dscale,
+                       o, L.ptr(h), L.ptr(xs), L.stream())
+                o += r
+        ctx.n, ctx.rows = n, rows
+        ctx.save_for_backward(*xs_in, *Ws)
+        ctx.mark_non_differentiable(xs)
+        return h, xs
+
+    @staticmethod
+    def backward(ctx, g, _gxs):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        xs_in, Ws = saved[:n], saved[n:]
+        g = g.contiguous()
+        gx, gW, gb = [None] * n, [None] * n, [None] * n
+        o = 0
+        for t, r in enumerate(ctx.rows):
+            gt = g[o:o + r]
+            o += r
+            if ctx.needs_input_grad[3 + t]:
+                gx[t] = gt @ Ws[t].to(gt.dtype)
+            if ctx.needs_input_grad[3 + n + t]:
+                gW[t] = batched_wgrad(gt, xs_in[t]).to(Ws[t].dtype)
+            if ctx.needs_input_grad[3 + 2 * n + t]:
+                gb[t] = col_sum(gt).to(Ws[t].dtype)
+        return (None, None, None, *gx, *gW, *gb)
+
+
+def type_project_fusable(fcs, feats, width=64):
+    """regnn_type_project's shapes: every type a biased Linear to `width` = 64 from <= 256
+    features, one storage dtype (fp32 / bf16) on the device."""
+    return (width == 64 and len(fcs) == len(feats) > 0
+            and all(fc.bias is not None and fc.weight.shape[0] == 64 and fc.weight.shape[1] <= 256
+                    for fc in fcs)
+            and all(f.is_cuda and f.dim() == 2 and f.dtype == feats[0].dtype for f in feats)
+            and feats[0].dtype in (torch.float32, torch.bfloat16))
+
+
+def type_project_prescale(fcs, feats, scale, drop):
+    """(h, xs): the concatenated per-type projections and scale * drop(h) (model/REGCN.py:31-35
+    + the first layer's pre-scale, layer/REGraphConv.py:56,73-76) from one HIP pass per type."""
+    return _TypeProjPre.apply(len(fcs), scale, drop, *feats, *[fc.weight for fc in fcs],
+                              *[fc.bias for fc in fcs])
 
 
 def re_spmm_fused(rg, x, tab=None, pack=None, post=None, bias=None, residual=None, ln=None,
