@@ -24,7 +24,7 @@ def load(d):
 def kind(name):
     if "regnn::" not in name:
         return None
-    if "head_fwd_kernel" in name:
+    if "head_fwd_kernel" in name or "head_fwd_x6_kernel" in name:
         return "head_fwd"
     if "spmm_main" in name:
         targs = name[name.index("<") + 1:name.index(">")].split(",")
