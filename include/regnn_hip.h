@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 8). */
+/* ABI version (bumped on any signature change or addition; currently 9). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -251,6 +251,17 @@ int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_
                        const float* W, const float* b, const float* scale,
                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
                        int64_t row0, void* h, void* xs, hipStream_t stream);
+
+/* Weight and bias gradient of a Linear(K -> C) layer over n rows (model/REGCN.py:31-35 fc_list
+ * backward): per-block partial slab rows [64*K + 64] (fp32): columns [0, 64*K) hold
+ * (g^T x)[c][k] at c*K + k (d weight, rows c >= C zero), columns [64*K, +64) the column sums of g
+ * (d bias). g [n, C] with row stride ldg (bf16: rows 8-byte aligned), x [n, K] row-major
+ * 16-byte aligned, both dtype; fp32-accurate bf16x6 MFMA, one pass over g and x per 64-feature block.
+ * C <= 64, K in {64, 128, 256} (else REGNN_EUNSUPPORTED). At most slab_rows (>= 8) rows are
+ * written: zero the slab first, reduce with regnn_rel_reduce. */
+int regnn_linear_wgrad(const void* g, int64_t n, int32_t C, int64_t ldg, const void* x,
+                       int32_t K, int32_t dtype, float* slab, int32_t slab_rows,
+                       hipStream_t stream);
 
 /* Row-wise softmax cross-entropy of the output head over `rows` logit rows (stride ld):
  * loss_rows[r] = logsumexp(z_r) - z_r[labels[r]];  p[r, c] = scale * (softmax(z_r)_c - [c == y_r])

@@ -686,59 +686,72 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, con
     }
 }
 
-// gW^T / gb partial with fp32 accuracy on bf16 MFMA (bf16x6 split, as head_fwd_x6_kernel): the
-// same tiling as head_wgrad_kernel (wave w owns class tiles w, w + 8, w + 16; D[cls][feature]),
-// but one 16x16x32 k-step covers 32 rows: lane (q, c) supplies rows r0 + 8 q + j (j = 0..7) of
-// A = p[., 16 t + c] and B = h[., 16 kt + c], loaded 4 bytes per lane (16 lanes read 64
-// contiguous bytes of a row) and split into three bf16 fragments in registers.
-template <int NT>
+// gW = p^T h / gb = colsum(p) partials with fp32 accuracy on bf16 MFMA (bf16x6 split, as
+// head_fwd_x6_kernel): D[cls][feature] tiles over this block's row range, one 16x16x32 k-step per
+// 32 rows: lane (q, c) supplies rows r0 + 8 q + j (j = 0..7) of A = p[., 16 t + c] and
+// B = h[., 64 fb + 16 kt + c], loaded 4 (fp32) / 2 (bf16) bytes per lane (16 lanes read one
+// contiguous row segment) and split into three bf16 fragments in registers. Work units
+// (class tile t, 64-feature block fb) go to waves round-robin (u = w + 8 m): the output head
+// (C = 349, K = 64) gives a wave class tiles w, w + 8, w + 16; an input projection's d weight
+// (C = 64 outputs, K = 128 inputs) one (tile, block) pair per wave.
+template <typename TP, typename TH, int NT, int KH>
 __global__ void __launch_bounds__(kHeadBlock)
-head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
-                     const float* __restrict__ h,
-                     int64_t rows_per_block, float* __restrict__ slab) {
-    constexpr int K = kHeadK, CP = NT * 16, MT = (NT + 7) / 8;
+wgrad_x6_kernel(const TP* __restrict__ p, int64_t n, int C, int64_t ld,
+                const TH* __restrict__ h, int64_t rows_per_block, float* __restrict__ slab) {
+    constexpr int KB = KH / 64, NU = NT * KB, MU = (NU + 7) / 8, CP = NT * 16;
+    constexpr bool EXACT = sizeof(TP) == 2 && sizeof(TH) == 2;   // bf16 x bf16: one product
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(n, r0 + rows_per_block);
-    f32x4 acc[MT][4];
-    float gb[MT];
+    auto ld_p = [&](int64_t i) -> float {
+        if constexpr (sizeof(TP) == 4) return p[i]; else return bf2f(p[i]);
+    };
+    auto ld_h = [&](int64_t i) -> float {
+        if constexpr (sizeof(TH) == 4) return h[i]; else return bf2f(h[i]);
+    };
+    f32x4 acc[MU][4];
+    float gb[MU];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
+    for (int m = 0; m < MU; ++m) {
         gb[m] = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     for (int64_t row0 = r0; row0 < r1; row0 += 32) {
-        float a[MT][8], b[4][8];
+        float a[MU][8], b[MU][4][8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int64_t rr = row0 + 8 * q + j;
             const bool ok = rr < r1;
             const int64_t rc = ok ? rr : r0;
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int cls = 16 * (w + 8 * m) + c;
-                const bool in = ok && (w + 8 * m) < NT && cls < C;
-                const float v = p[rc * ld + (cls < C ? cls : 0)];
+            for (int m = 0; m < MU; ++m) {
+                const int u = w + 8 * m, t = u % NT, fb = u / NT;
+                const int cls = 16 * t + c;
+                const bool in = ok && u < NU && cls < C;
+                const float v = ld_p(rc * ld + (cls < C ? cls : 0));
                 a[m][j] = in ? v : 0.f;
+                if (KB > 1 || m == 0) {
+#pragma unroll
+                    for (int kt = 0; kt < 4; ++kt) {
+                        const float hv = ld_h(rc * KH + 64 * (KB > 1 ? fb : 0) + 16 * kt + c);
+                        b[m][kt][j] = ok ? hv : 0.f;
+                    }
+                }
             }
+        }
+#pragma unroll
+        for (int m = 0; m < MU; ++m) {
+            if (w + 8 * m >= NU) continue;                   // wave-uniform
+            const int mb = KB > 1 ? m : 0;                   // KB == 1: units share h
+            bf16x8_t bf[4][3];
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
-                const float v = h[rc * K + 16 * kt + c];
-                b[kt][j] = ok ? v : 0.f;
+                uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) split3(b[mb][kt][j], s0[j], s1[j], s2[j]);
+                bf[kt][0] = pack8(s0); bf[kt][1] = pack8(s1); bf[kt][2] = pack8(s2);
             }
-        }
-        bf16x8_t bf[4][3];
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-            uint16_t s0[8], s1[8], s2[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) split3(b[kt][j], s0[j], s1[j], s2[j]);
-            bf[kt][0] = pack8(s0); bf[kt][1] = pack8(s1); bf[kt][2] = pack8(s2);
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-            if (w + 8 * m >= NT) continue;                 // wave-uniform
             uint16_t s0[8], s1[8], s2[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -748,29 +761,50 @@ head_wgrad_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
             const bf16x8_t a0 = pack8(s0), a1 = pack8(s1), a2 = pack8(s2);
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
+                if constexpr (!EXACT) {
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
+                }
                 acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][0], acc[m][kt], 0, 0, 0);
             }
         }
     }
-    float* out = slab + (int64_t)blockIdx.x * (CP * K + CP);
+    float* out = slab + (int64_t)blockIdx.x * (CP * KH + CP);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-        const int t = w + 8 * m;
-        if (t >= NT) continue;
+    for (int m = 0; m < MU; ++m) {
+        const int u = w + 8 * m, t = u % NT, fb = u / NT;
+        if (u >= NU) continue;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[(16 * t + 4 * q + r) * K + 16 * kt + c] = acc[m][kt][r];
+            for (int r = 0; r < 4; ++r)
+                out[(16 * t + 4 * q + r) * KH + 64 * fb + 16 * kt + c] = acc[m][kt][r];
         float g = gb[m];
         g += __shfl_xor(g, 16, 64);
         g += __shfl_xor(g, 32, 64);
-        if (q == 0) out[CP * K + 16 * t + c] = g;
+        if (fb == 0 && q == 0) out[CP * KH + 16 * t + c] = g;
     }
+}
+
+// slab rows for n rows of p: grid blocks of >= 256 rows, one slab row each (<= slab_rows)
+template <typename TP, typename TH, int NT, int KH>
+int launch_wgrad_x6(const TP* p, int64_t n, int C, int64_t ld, const TH* h, float* slab,
+                    int slab_rows, hipStream_t stream) {
+    int64_t grid = slab_rows;
+    const int64_t rpb_min = 256;
+    if (grid * rpb_min > n) grid = (n + rpb_min - 1) / rpb_min;
+    if (grid < 1) grid = 1;
+    int64_t rpb = (n + grid - 1) / grid;
+    rpb = (rpb + 31) / 32 * 32;
+    grid = (n + rpb - 1) / rpb;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((wgrad_x6_kernel<TP, TH, NT, KH>), dim3((unsigned)grid), dim3(kHeadBlock),
+                       0, stream, p, n, C, ld, h, rpb, slab);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 template <int NT>
@@ -827,8 +861,8 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
         grid = (n + rpb - 1) / rpb;
         if (grid < 1) grid = 1;
         if (g_tune_head != 16)
-            hipLaunchKernelGGL((head_wgrad_x6_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock),
-                               0, stream, p, n, C, ld, h, rpb, slab);
+            return launch_wgrad_x6<float, float, NT, kHeadK>(p, n, C, ld, h, slab, slab_rows,
+                                                            stream);
         else
             hipLaunchKernelGGL((head_wgrad_kernel<NT>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
                                stream, p, n, C, ld, h, rpb, slab);
@@ -1017,6 +1051,133 @@ int dispatch_type_project(const void* x, int64_t rows, int K, const float* W, co
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Linear(K -> C <= 64) weight / bias gradient for tall inputs (model/REGCN.py:31-35 fc_list
+// backward): gW = g^T x, gb = colsum(g), fp32-accurate on bf16 MFMA (bf16x6). Each wave streams
+// rows, 32 per 16x16x32 k-step, and keeps every output tile of its 64-feature block: lane (q, c)
+// loads 16 bytes of each of its 8 rows 8 q + j from g (classes 4c .. 4c+3) and from x (features
+// 64 fb + 4c .. +3), and component i of those loads feeds the MFMA pair (class 4m + ip, feature
+// 64 fb + 4n + ix) -- 16 tiles, 64 accumulator registers, every byte of g and x read once per
+// feature block. KB = K / 64 waves share a row stream (one per feature block); 8 / KB streams per
+// block, each writing its own slab row.
+template <typename T>
+__device__ __forceinline__ f32x4 load4f(const T* p) {
+    if constexpr (sizeof(T) == 4) {
+        return *reinterpret_cast<const f32x4_u*>(p);
+    } else {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        return f32x4{bf2f(u.x & 0xffffu), bf2f(u.x >> 16), bf2f(u.y & 0xffffu), bf2f(u.y >> 16)};
+    }
+}
+
+template <typename T, int KB>
+__global__ void __launch_bounds__(kHeadBlock)
+linear_wgrad_kernel(const T* __restrict__ g, int64_t n, int C, int64_t ldg,
+                    const T* __restrict__ x, int64_t rows_per_block, float* __restrict__ slab) {
+    constexpr int K = 64 * KB, NS = 8 / KB;
+    constexpr bool EXACT = sizeof(T) == 2;             // bf16 operands: one product
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
+    const int fb = w % KB, st = w / KB;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(n, r0 + rows_per_block);
+    const bool cfull = 4 * c + 4 <= C;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 gb = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t row0 = r0 + 32 * st; row0 < r1; row0 += 32 * NS) {
+        f32x4 P[8], X[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t rr = row0 + 8 * q + j;
+            const bool ok = rr < r1;
+            const int64_t rc = ok ? rr : r0;
+            f32x4 pv;
+            if (cfull) {
+                pv = load4f(g + rc * ldg + 4 * c);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float v = sizeof(T) == 4 ? float(g[rc * ldg + min(4 * c + i, C - 1)])
+                                                   : bf2f(uint32_t(g[rc * ldg + min(4 * c + i, C - 1)]));
+                    pv[i] = 4 * c + i < C ? v : 0.f;
+                }
+            }
+            const f32x4 xv = load4f(x + rc * K + 64 * fb + 4 * c);
+            P[j] = ok ? pv : f32x4{0.f, 0.f, 0.f, 0.f};
+            X[j] = ok ? xv : f32x4{0.f, 0.f, 0.f, 0.f};
+            gb += P[j];
+        }
+        bf16x8_t A[4][3];
+#pragma unroll
+        for (int ip = 0; ip < 4; ++ip) {
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(P[j][ip], s0[j], s1[j], s2[j]);
+            A[ip][0] = pack8(s0); A[ip][1] = pack8(s1); A[ip][2] = pack8(s2);
+        }
+#pragma unroll
+        for (int ix = 0; ix < 4; ++ix) {
+            uint16_t s0[8], s1[8], s2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(X[j][ix], s0[j], s1[j], s2[j]);
+            const bf16x8_t b0 = pack8(s0), b1 = pack8(s1), b2 = pack8(s2);
+#pragma unroll
+            for (int ip = 0; ip < 4; ++ip) {
+                f32x4& d = acc[ip][ix];
+                if constexpr (!EXACT) {
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][2], b0, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][1], b1, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][0], b2, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][1], b0, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][0], b1, d, 0, 0, 0);
+                }
+                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ip][0], b0, d, 0, 0, 0);
+            }
+        }
+    }
+    // D[m][n] of tile (ip, ix) in lane (q, c = n), register r: m = 4 q + r -> class 4 m + ip,
+    // feature 64 fb + 4 n + ix; slab row (block, stream): [64 * K + 64], class-major
+    float* out = slab + ((int64_t)blockIdx.x * NS + st) * (64 * K + 64);
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip)
+#pragma unroll
+        for (int ix = 0; ix < 4; ++ix)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(4 * (4 * q + r) + ip) * K + 64 * fb + 4 * c + ix] = acc[ip][ix][r];
+    if (fb == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float v = gb[i];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (q == 0) out[64 * K + 4 * c + i] = v;
+        }
+    }
+}
+
+template <typename T, int KB>
+int launch_linear_wgrad(const T* g, int64_t n, int C, int64_t ldg, const T* x, float* slab,
+                        int slab_rows, hipStream_t stream) {
+    constexpr int NS = 8 / KB;
+    int64_t grid = slab_rows / NS;
+    const int64_t rpb_min = 32 * NS * 4;
+    if (grid * rpb_min > n) grid = (n + rpb_min - 1) / rpb_min;
+    if (grid < 1) grid = 1;
+    int64_t rpb = (n + grid - 1) / grid;
+    rpb = (rpb + 32 * NS - 1) / (32 * NS) * (32 * NS);
+    grid = (n + rpb - 1) / rpb;
+    if (grid < 1) grid = 1;
+    if (grid * NS > slab_rows) return REGNN_EINVAL;
+    hipLaunchKernelGGL((linear_wgrad_kernel<T, KB>), dim3((unsigned)grid), dim3(kHeadBlock), 0,
+                       stream, g, n, C, ldg, x, rpb, slab);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -1040,6 +1201,27 @@ int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_
     if (dtype == REGNN_BF16)
         return dispatch_type_project<bf16_t>(x, rows, K, W, b, scale, drop_seed, drop_keep16,
                                              drop_scale, row0, h, xs, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_linear_wgrad(const void* g, int64_t n, int32_t C, int64_t ldg, const void* x,
+                       int32_t K, int32_t dtype, float* slab, int32_t slab_rows,
+                       hipStream_t stream) {
+    if (!g || !x || !slab || n < 0 || C <= 0 || C > 64 || ldg < C || slab_rows <= 0)
+        return REGNN_EINVAL;
+    if (K != 64 && K != 128 && K != 256) return REGNN_EUNSUPPORTED;
+    if (n == 0) return REGNN_OK;
+    // 16-byte x rows; bf16 g rows are read 8 bytes at a time (fp32: 4-byte aligned loads)
+    if (slab_rows < 8 || (reinterpret_cast<uintptr_t>(x) & 15) ||
+        (dtype == REGNN_BF16 && ((reinterpret_cast<uintptr_t>(g) & 7) || (ldg & 3))))
+        return REGNN_EINVAL;
+#define LW_CASE(T, KB)                                                                          \
+    if (K == 64 * KB)                                                                           \
+        return launch_linear_wgrad<T, KB>(static_cast<const T*>(g), n, C, ldg,                  \
+                                          static_cast<const T*>(x), slab, slab_rows, stream);
+    if (dtype == REGNN_F32) { LW_CASE(float, 1) LW_CASE(float, 2) LW_CASE(float, 4) }
+    if (dtype == REGNN_BF16) { LW_CASE(bf16_t, 1) LW_CASE(bf16_t, 2) LW_CASE(bf16_t, 4) }
+#undef LW_CASE
     return REGNN_EUNSUPPORTED;
 }
 

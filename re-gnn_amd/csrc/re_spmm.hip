@@ -841,7 +841,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 8; }
+int regnn_abi_version(void) { return 9; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {

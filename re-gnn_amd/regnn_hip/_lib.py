@@ -61,6 +61,7 @@ _SIG = {
     "regnn_col_sum": ([P, I64, I32, P, P], ctypes.c_int),
     "regnn_type_project": ([P, I64, I32, I32, I32, P, P, P, P, ctypes.c_uint32, F32, I64, P, P, P],
                            ctypes.c_int),
+    "regnn_linear_wgrad": ([P, I64, I32, I64, P, I32, I32, P, I32, P], ctypes.c_int),
     "regnn_row_scale": ([P, P, P, I64, I32, I32, P, ctypes.c_uint32, F32, P, P, P], ctypes.c_int),
     "regnn_softmax_xent": ([P, I64, I32, I64, P, F32, P, P, P], ctypes.c_int),
     "regnn_attn_dots_fwd": ([P, P, P, I64, I32, I32, P, P, P], ctypes.c_int),
@@ -76,7 +77,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 8
+ABI_VERSION = 9
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -68,10 +68,15 @@ class _TypeProjFn(torch.autograd.Function):
             o += r
             if ctx.needs_input_grad[1 + t]:
                 gx[t] = gt @ Ws[t].to(gt.dtype)
-            if ctx.needs_input_grad[1 + n + t]:
-                gW[t] = ops.batched_wgrad(gt, xs[t]).to(Ws[t].dtype)
-            if ctx.needs_input_grad[1 + 2 * n + t]:
-                gb[t] = ops.col_sum(gt) if gt.is_cuda else gt.sum(0).to(Ws[t].dtype)
+            if not gt.is_cuda:
+                if ctx.needs_input_grad[1 + n + t]:
+                    gW[t] = (gt.t() @ xs[t]).to(Ws[t].dtype)
+                if ctx.needs_input_grad[1 + 2 * n + t]:
+                    gb[t] = gt.sum(0).to(Ws[t].dtype)
+            elif ctx.needs_input_grad[1 + n + t] or ctx.needs_input_grad[1 + 2 * n + t]:
+                w_, b_ = ops.linear_wgrad(gt, xs[t])
+                gW[t] = w_.to(Ws[t].dtype)
+                gb[t] = b_.to(Ws[t].dtype)
         return (None, *gx, *gW, *gb)
 
 

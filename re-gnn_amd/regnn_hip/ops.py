@@ -327,10 +327,10 @@ class _TypeProjPre(torch.autograd.Function):
             o += r
             if ctx.needs_input_grad[3 + t]:
                 gx[t] = gt @ Ws[t].to(gt.dtype)
-            if ctx.needs_input_grad[3 + n + t]:
-                gW[t] = batched_wgrad(gt, xs_in[t]).to(Ws[t].dtype)
-            if ctx.needs_input_grad[3 + 2 * n + t]:
-                gb[t] = col_sum(gt).to(Ws[t].dtype)
+            if ctx.needs_input_grad[3 + n + t] or ctx.needs_input_grad[3 + 2 * n + t]:
+                w_, b_ = linear_wgrad(gt, xs_in[t])
+                gW[t] = w_.to(Ws[t].dtype)
+                gb[t] = b_.to(Ws[t].dtype)
         return (None, None, None, *gx, *gW, *gb)
 
 
@@ -654,6 +654,27 @@ def col_sum(x):
     slab = torch.zeros(L.slab_rows() // 2, cols, dtype=torch.float32, device=x.device)
     L.call("regnn_col_sum", L.ptr(x), rows, cols, L.ptr(slab), L.stream())
     return _reduce(slab, cols)
+
+
+def linear_wgrad(g, x):
+    """(g^T x, g.sum(0)) of a Linear's backward over tall row-major g [n, C], x [n, K]:
+    regnn_linear_wgrad (one fp32-accurate MFMA pass, fixed-order slab reduce) for C <= 64 and
+    K in {64, 128, 256}, else a chunked GEMM + col_sum. fp32 results."""
+    n, C = g.shape
+    K = x.shape[1]
+    aligned = g.dtype == torch.float32 or (g.stride(0) % 4 == 0 and g.data_ptr() % 8 == 0)
+    if (g.is_cuda and C <= 64 and K in (64, 128, 256) and g.dtype == x.dtype
+            and g.dtype in (torch.float32, torch.bfloat16) and g.stride(1) == 1 and aligned):
+        x = x.contiguous()
+        width = 64 * K + 64
+        rows = L.slab_rows() // 2
+        slab = torch.zeros(rows, width, dtype=torch.float32, device=g.device)
+        with timed("linear_wgrad", (n * (C + K)) * g.element_size()):
+            L.call("regnn_linear_wgrad", L.ptr(g), n, C, g.stride(0), L.ptr(x), K,
+                   L.dtype_code(g), L.ptr(slab), rows, L.stream())
+            tot = _reduce(slab, width)
+        return tot[:64 * K].view(64, K)[:C], tot[64 * K:64 * K + C]
+    return batched_wgrad(g.float(), x.float()), col_sum(g)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -46,6 +46,26 @@ def test_type_project_kernel(dtype, p):
         assert torch.equal(xs == 0, ~kept | (h == 0))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,C,K", [(20000, 64, 128), (777, 33, 64), (5000, 64, 256), (31, 64, 128),
+                                   (1000, 64, 192)])
+def test_linear_wgrad(dtype, n, C, K):
+    """regnn_linear_wgrad: (g^T x, colsum g) of a Linear's backward vs fp64, deterministic."""
+    from regnn_hip import ops
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(n)
+    g = torch.randn(n, C, generator=gen, device=DEV).to(dtype)
+    x = torch.randn(n, K, generator=gen, device=DEV).to(dtype)
+    gw, gb = ops.linear_wgrad(g, x)
+    want_w = g.double().t() @ x.double()
+    want_b = g.double().sum(0)
+    rel = lambda a, b: float((a.double() - b).abs().max()) / max(1.0, float(b.abs().max()))
+    assert gw.shape == (C, K) and gb.shape == (C,)
+    assert rel(gw, want_w) <= 1e-5 and rel(gb, want_b) <= 1e-5
+    gw2, gb2 = ops.linear_wgrad(g, x)
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
+
+
 @pytest.mark.parametrize("train", [False, True])
 def test_regcn_fused_projection_matches_unfused(train):
     import torch.nn.functional as F
