@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 9). */
+/* ABI version (bumped on any signature change or addition; currently 10). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -190,6 +190,24 @@ int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                            float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                            const int64_t* level_desc, const uint64_t* drop_seed,
                            uint32_t drop_keep16, float drop_scale, hipStream_t stream);
+
+/* regnn_spmm_bwd(_dropout when drop_seed != NULL) with the producer's pre-scale folded into the
+ * epilogue: when this op's input x is itself the output y' of an aggregation with post-scale
+ * nx_scale (y' = nx_scale * A' x'), its backward needs nx_scale * g' and <g', y'> / nx_scale for
+ * g' = gx (regnn_row_scale's backward pass). This call writes, besides gx,
+ *   nx_out[u] = nx_scale[u] * gx[u]  (dtype),  nx_dot[u] = <gx[u], x[u]> / nx_scale[u]
+ * (x undropped), so the producer's backward gathers nx_out directly: no separate row pass over
+ * gx and x (REGCN layer 1 -> layer 0, layer/REGraphConv.py:73-76,97-98). */
+int regnn_spmm_bwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* rel_table, const float* edge_w, const float* in_scale,
+                        const float* out_scale, const void* g, const void* x, const void* y,
+                        void* gx, float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                        int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                        const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                        const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                        const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                        const float* nx_scale, void* nx_out, float* nx_dot, hipStream_t stream);
 
 /* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order. */
 int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,

@@ -56,6 +56,9 @@ struct SpmmArgs {
     const float* ln_b;
     float ln_eps;
     int32_t epi;           // kEpiLN | kEpiReLU
+    const float* nx_scale; // backward: the producer's post-scale of this op's input x (see
+    void* nx_out;          //   regnn_spmm_bwd_next): nx_out = nx_scale * gx,
+    float* nx_dot;         //   nx_dot = <gx, x> / nx_scale
 };
 
 enum { kEpiLN = 1, kEpiReLU = 2 };
@@ -107,10 +110,14 @@ struct Seg {
         for (int q = 0; q < NV; ++q) unpack<T>(r[q], v[q]);
     }
 
-    // the forward input row of the segment's own node (backward); with DROP the dropped row
+    // the forward input row of the segment's own node (backward): raw = x[seg], v = drop(x[seg])
     __device__ __forceinline__ static void load_self(const SpmmArgs& a, int64_t seg, int lane,
-                                                     float (&v)[NV][EV]) {
-        load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, v);
+                                                     float (&v)[NV][EV], float (&raw)[NV][EV]) {
+        load_row(static_cast<const T*>(a.self) + seg * a.F, a.F, lane, raw);
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+            for (int t = 0; t < EV; ++t) v[q][t] = raw[q][t];
         if constexpr (DROP) {
             const uint32_t key = drop_key(a.drop_seed);
 #pragma unroll
@@ -274,7 +281,8 @@ struct Seg {
     // y = os * acc + bias; backward node grad = <self, acc> + <g_i, y_i> / in_scale[i].
     __device__ __forceinline__ static void epilogue(const SpmmArgs& a, int64_t seg, int lane,
                                                     float os, const float (&sx)[NV][EV],
-                                                    float (&acc)[NV][EV]) {
+                                                    float (&acc)[NV][EV],
+                                                    const float (&sraw)[NV][EV]) {
         const int F = a.F;
         if constexpr (BWD) {
             if (a.node_grad) {
@@ -299,6 +307,11 @@ struct Seg {
         }
         uint32_t dkey = 0;
         if constexpr (DROP && BWD) dkey = drop_key(a.drop_seed);
+        // backward with the producer's pre-scale folded in (regnn_spmm_bwd_next): gx also leaves
+        // as nx_scale * gx, and <gx, x> / nx_scale, for the producing aggregation's backward
+        const bool nx = BWD && a.nx_scale;                       // wave-uniform
+        const float ns = nx ? a.nx_scale[seg] : 1.f;
+        float nd = 0.f;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int o = off(q, lane);
@@ -313,6 +326,23 @@ struct Seg {
                 if constexpr (DROP && BWD)
                     drop_apply<EV, DROP>(dkey, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane, r);
                 Vec<T>::store(out + o, r);
+                if constexpr (BWD) {
+                    if (nx) {
+                        float rs[EV];
+#pragma unroll
+                        for (int t = 0; t < EV; ++t) {
+                            nd = fmaf(r[t], sraw[q][t], nd);
+                            rs[t] = r[t] * ns;
+                        }
+                        Vec<T>::store(static_cast<T*>(a.nx_out) + seg * F + o, rs);
+                    }
+                }
+            }
+        }
+        if constexpr (BWD) {
+            if (nx) {
+                nd = group_sum<LPR>(nd);
+                if (lane == 0) a.nx_dot[seg] = nd / ns;
             }
         }
     }
@@ -339,17 +369,17 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
-    const bool need_self = S::SLAB || S::EDGE || (S::BWD && a.node_grad);
+    const bool need_self = S::SLAB || S::EDGE || (S::BWD && (a.node_grad || a.nx_scale));
     for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < a.n_seg;
          seg += (int64_t)gridDim.x * GPB) {
         const int beg = a.ptr[seg], end = a.ptr[seg + 1];
         if (a.split > 0 && end - beg > a.split) continue;   // long-segment path
         float acc[NV][S::EV] = {};
-        float sx[NV][S::EV] = {};
-        if (need_self) S::load_self(a, seg, lane, sx);
+        float sx[NV][S::EV] = {}, sraw[NV][S::EV] = {};
+        if (need_self) S::load_self(a, seg, lane, sx, sraw);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
         if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
-        S::epilogue(a, seg, lane, os, sx, acc);
+        S::epilogue(a, seg, lane, os, sx, acc, sraw);
     }
     if constexpr (S::SLAB) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
 }
@@ -371,8 +401,8 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
         const int beg = s0 + k * a.chunk;
         const int end = min(s1, beg + a.chunk);
         float acc[NV][S::EV] = {};
-        float sx[NV][S::EV] = {};
-        if constexpr (S::SLAB || S::EDGE) S::load_self(a, seg, lane, sx);
+        float sx[NV][S::EV] = {}, sraw[NV][S::EV] = {};
+        if constexpr (S::SLAB || S::EDGE) S::load_self(a, seg, lane, sx, sraw);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
         if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
         float* part = a.chunk_partial + c * a.F;
@@ -429,13 +459,13 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
     using S = Seg<T, LPR, NV, MODE, UNT, FULL, DROP>;
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
-    const bool need_self = S::BWD && a.node_grad;
+    const bool need_self = S::BWD && (a.node_grad || a.nx_scale);
     for (int64_t l = (int64_t)blockIdx.x * GPB + tid / LPR; l < a.n_long;
          l += (int64_t)gridDim.x * GPB) {
         const int64_t seg = a.long_ids[l];
         float acc[NV][S::EV] = {};
-        float sx[NV][S::EV] = {};
-        if (need_self) S::load_self(a, seg, lane, sx);
+        float sx[NV][S::EV] = {}, sraw[NV][S::EV] = {};
+        if (need_self) S::load_self(a, seg, lane, sx, sraw);
         const int64_t row = final_base >= 0 ? final_base + l : a.chunk_off[l];
         const float* part = a.chunk_partial + row * a.F;
 #pragma unroll
@@ -447,7 +477,7 @@ __global__ void __launch_bounds__(kBlock) spmm_fixup(SpmmArgs a, int64_t final_b
             }
         }
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        S::epilogue(a, seg, lane, os, sx, acc);
+        S::epilogue(a, seg, lane, os, sx, acc, sraw);
     }
 }
 
@@ -841,7 +871,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 9; }
+int regnn_abi_version(void) { return 10; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -936,11 +966,14 @@ static int spmm_bwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
                          const int32_t* chunk_long, const int32_t* chunk_off, int32_t n_chunk,
                          float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                          const int64_t* level_desc, const uint64_t* drop_seed,
-                         uint32_t drop_keep16, float drop_scale, hipStream_t stream) {
+                         uint32_t drop_keep16, float drop_scale, hipStream_t stream,
+                         const float* nx_scale = nullptr, void* nx_out = nullptr,
+                         float* nx_dot = nullptr) {
     int st = check_common(ptr, idx, g, gx, n_seg, split, chunk, long_ids, n_long, chunk_long,
                           chunk_off, n_chunk, chunk_partial, rel, rel_table);
     if (st) return st;
     if (slab && (!rel || n_rel <= 0 || n_rel > 64)) return REGNN_EINVAL;
+    if (nx_scale && (!nx_out || !nx_dot || !x)) return REGNN_EINVAL;
     if ((slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (n_levels < 0 || (n_levels > 0 && (!level_sb || !level_desc))) return REGNN_EINVAL;
@@ -951,6 +984,7 @@ static int spmm_bwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
     a.src = g; a.out = gx; a.self = x; a.ng_a = y ? g : nullptr; a.ng_b = y;
     a.slab = slab; a.n_rel = n_rel; a.edge_grad = edge_grad; a.node_grad = node_grad;
     a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
+    a.nx_scale = nx_scale; a.nx_out = nx_out; a.nx_dot = nx_dot;
     if (drop_seed && (slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
     const int mode = slab ? (edge_grad ? kBwdBoth : kBwdSlab) : (edge_grad ? kBwdEdge : kBwd);
     if (dtype == REGNN_F32) return dispatch<float>(a, mode, stream);
@@ -1035,6 +1069,24 @@ int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                          n_rel, edge_grad, node_grad, n_seg, F, dtype, split, chunk, long_ids,
                          n_long, chunk_long, chunk_off, n_chunk, chunk_partial, level_sb,
                          n_levels, level_desc, drop_seed, drop_keep16, drop_scale, stream);
+}
+
+int regnn_spmm_bwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* rel_table, const float* edge_w, const float* in_scale,
+                        const float* out_scale, const void* g, const void* x, const void* y,
+                        void* gx, float* slab, int32_t n_rel, float* edge_grad, float* node_grad,
+                        int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                        const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                        const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                        const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                        const float* nx_scale, void* nx_out, float* nx_dot, hipStream_t stream) {
+    if (!nx_scale || (drop_seed && drop_keep16 > 65536u)) return REGNN_EINVAL;
+    return spmm_bwd_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, g, x, y, gx, slab,
+                         n_rel, edge_grad, node_grad, n_seg, F, dtype, split, chunk, long_ids,
+                         n_long, chunk_long, chunk_off, n_chunk, chunk_partial, level_sb,
+                         n_levels, level_desc, drop_seed, drop_keep16, drop_scale, stream,
+                         nx_scale, nx_out, nx_dot);
 }
 
 int regnn_row_scale(const void* x, const float* scale, void* out, int64_t n_rows, int32_t F,

@@ -137,7 +137,7 @@ def drop_request(p, device, seed=None):
 # Forward pre-scale policy of _ReSpmm: "auto" | "on" | "off" (tools/ab_spmm.py flips it).
 # "on": pre * drop(x) is formed once per source row by regnn_row_scale and the aggregation
 # gathers the finished rows; "off": the gather scales and masks every edge's row itself.
-PRESCALE = {"mode": "auto", "bwd": "auto"}
+PRESCALE = {"mode": "auto", "bwd": "auto", "next": "auto"}
 
 
 def _use_prescale(x, scale, drop, backward=False):
@@ -152,6 +152,31 @@ def _use_prescale(x, scale, drop, backward=False):
     return True
 
 
+class _NextLink:
+    """Backward hand-off between two chained aggregations y' = post' * (A' x') and y = A(..y'..).
+
+    When the consumer reads y' as its input x unchanged (no op in between and no other consumer),
+    the producer's backward needs post' * g' and <g', y'> / post' for g' = d loss / d y' = the
+    consumer's gx. The consumer's backward forms both in its epilogue (regnn_spmm_bwd_next) and
+    parks them here; the producer's backward takes them only if its incoming gradient IS that gx
+    tensor, unmodified (autograd summed nothing into it), and runs its own row pass otherwise."""
+
+    __slots__ = ("post", "handoff")
+
+    def __init__(self, post):
+        self.post = post
+        self.handoff = None
+
+    def take(self, gy):
+        h, self.handoff = self.handoff, None
+        if h is None:
+            return None
+        gx, version, nx_out, nx_dot = h
+        if gy is not gx or gy._version != version:
+            return None
+        return nx_out, nx_dot
+
+
 def _drop_args(drop):
     if drop is None:
         return None, 0, 1.0
@@ -163,7 +188,8 @@ class _ReSpmm(torch.autograd.Function):
     drop = the optional fused dropout of the gathered rows (regnn_spmm_fwd_dropout)."""
 
     @staticmethod
-    def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None, prescaled=None):
+    def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None, prescaled=None, link=None,
+                link_in=None):
         x = x.contiguous()
         F = x.shape[1]
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
@@ -191,6 +217,7 @@ class _ReSpmm(torch.autograd.Function):
                        L.stream())
         del src
         ctx.drop = drop
+        ctx.link, ctx.link_in = link, link_in
         ctx.rg, ctx.pack, ctx.tab_shape = rg, pack, None if tab is None else tab.shape
         ctx.same_scale = pre is not None and pre is post and rg.n_src == rg.n_dst
         ctx.save_for_backward(x, y, t, pre, post)
@@ -217,9 +244,17 @@ class _ReSpmm(torch.autograd.Function):
         prescale = post is not None and _use_prescale(x, post, None, backward=True)
         src, in_scale, dot = gy, post, None
         drop = ctx.drop
+        handed = ctx.link.take(gy) if (prescale and ctx.link is not None) else None
+        # the consumer of x (the next aggregation) forms its producer's pre-scaled gradient rows
+        nx = ctx.link_in if (need_x and ctx.link_in is not None and
+                             ctx.link_in.post.numel() == rg.n_src) else None
         with timed("spmm_bwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_bwd")):
-            if prescale:
+            if handed is not None:
+                # post * g and <g, y> / post came from the consumer's backward epilogue
+                src, in_scale = handed[0], None
+                dot = handed[1] if want_dot else None
+            elif prescale:
                 # post * g once per destination row (regnn_row_scale), with <g, y> / post formed
                 # in the same pass; the transposed gather then reads finished rows
                 src, in_scale = torch.empty_like(gy), None
@@ -234,7 +269,13 @@ class _ReSpmm(torch.autograd.Function):
                     L.ptr(y if ctx.same_scale and node is not None and not prescale else None),
                     L.ptr(gx), L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F,
                     L.dtype_code(x), *plan_args)
-            if drop is None:
+            if nx is not None:
+                nx_out = torch.empty_like(gx)
+                nx_dot = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
+                L.call("regnn_spmm_bwd_next", *args, *(_drop_args(drop)),
+                       L.ptr(nx.post), L.ptr(nx_out), L.ptr(nx_dot), L.stream())
+                nx.handoff = (gx, gx._version, nx_out, nx_dot)
+            elif drop is None:
                 L.call("regnn_spmm_bwd", *args, L.stream())
             else:
                 L.call("regnn_spmm_bwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
@@ -256,7 +297,8 @@ class _ReSpmm(torch.autograd.Function):
                     yf, gf = y.float(), gy.float()
                     g_post = (gf * yf).sum(1) / post
         g_bias = gy.float().sum(0) if need_bias else None
-        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None, None
+        return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None, None, \
+            None, None
 
 
 def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=0.0,
@@ -278,9 +320,22 @@ def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=
             if prescaled is not None:
                 raise ValueError("prescaled input with an unfusable dropout")
             x = torch.nn.functional.dropout(x, dropout, training=True)
+    # x produced by another aggregation, read as is: this op's backward hands the producer its
+    # pre-scaled gradient rows (_NextLink, regnn_spmm_bwd_next)
+    link_in = getattr(x, "_regnn_link", None)
+    if link_in is not None and (not x.is_cuda or not dropout_fusable(x)):
+        link_in = None
     if bias is not None and post is not None and post.requires_grad:
-        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop, prescaled) + bias
-    return _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop, prescaled)
+        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop, prescaled, None,
+                             link_in) + bias
+    link = None
+    if post is not None and x.is_cuda and PRESCALE["next"] != "off" and \
+            PRESCALE["bwd"] != "off":
+        link = _NextLink(post.detach())
+    y = _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop, prescaled, link, link_in)
+    if link is not None:
+        y._regnn_link = link
+    return y
 
 
 class _TypeProjPre(torch.autograd.Function):
