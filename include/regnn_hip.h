@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 10). */
+/* ABI version (bumped on any signature change or addition; currently 11). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -190,6 +190,23 @@ int regnn_spmm_bwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                            float* chunk_partial, const int32_t* level_sb, int32_t n_levels,
                            const int64_t* level_desc, const uint64_t* drop_seed,
                            uint32_t drop_keep16, float drop_scale, hipStream_t stream);
+
+/* regnn_spmm_fwd(_dropout when drop_seed != NULL) with the consumer's pre-scale folded into the
+ * epilogue: when y is read by a next aggregation whose source rows are nx_scale * drop'(y)
+ * (drop' = nx_seed / nx_keep16 / nx_dscale, the regnn_row_scale spec; nx_seed NULL = none),
+ * this call writes them too, nx_out[v] = drop'(nx_scale[v] * y[v]) (dtype, from the stored y),
+ * so the next aggregation gathers nx_out with no row pass (REGCN layer 0 -> layer 1,
+ * layer/REGraphConv.py:56,73-76). */
+int regnn_spmm_fwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* rel_table, const float* edge_w, const float* in_scale,
+                        const float* out_scale, const float* bias, const void* x, void* y,
+                        int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                        const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                        const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                        const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                        const float* nx_scale, const uint64_t* nx_seed, uint32_t nx_keep16,
+                        float nx_dscale, void* nx_out, hipStream_t stream);
 
 /* regnn_spmm_bwd(_dropout when drop_seed != NULL) with the producer's pre-scale folded into the
  * epilogue: when this op's input x is itself the output y' of an aggregation with post-scale

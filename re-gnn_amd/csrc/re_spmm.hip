@@ -59,6 +59,11 @@ struct SpmmArgs {
     const float* nx_scale; // backward: the producer's post-scale of this op's input x (see
     void* nx_out;          //   regnn_spmm_bwd_next): nx_out = nx_scale * gx,
     float* nx_dot;         //   nx_dot = <gx, x> / nx_scale
+                           // forward (regnn_spmm_fwd_next): the consumer's pre-scale of y,
+                           //   nx_out = drop'(nx_scale * y) with drop' = (nx_seed, nx_thresh,
+    const uint64_t* nx_seed;  //   nx_dscale), the row_scale_kernel spec
+    uint32_t nx_thresh;
+    float nx_dscale;
 };
 
 enum { kEpiLN = 1, kEpiReLU = 2 };
@@ -308,10 +313,13 @@ struct Seg {
         uint32_t dkey = 0;
         if constexpr (DROP && BWD) dkey = drop_key(a.drop_seed);
         // backward with the producer's pre-scale folded in (regnn_spmm_bwd_next): gx also leaves
-        // as nx_scale * gx, and <gx, x> / nx_scale, for the producing aggregation's backward
-        const bool nx = BWD && a.nx_scale;                       // wave-uniform
+        // as nx_scale * gx, and <gx, x> / nx_scale, for the producing aggregation's backward;
+        // forward (regnn_spmm_fwd_next): y also leaves as the consumer's drop'(nx_scale * y)
+        const bool nx = a.nx_scale != nullptr;                   // wave-uniform
         const float ns = nx ? a.nx_scale[seg] : 1.f;
         float nd = 0.f;
+        uint32_t nkey = 0;
+        if (!BWD && nx && a.nx_seed) nkey = drop_key(a.nx_seed);
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int o = off(q, lane);
@@ -326,16 +334,24 @@ struct Seg {
                 if constexpr (DROP && BWD)
                     drop_apply<EV, DROP>(dkey, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane, r);
                 Vec<T>::store(out + o, r);
-                if constexpr (BWD) {
-                    if (nx) {
-                        float rs[EV];
+                if (nx) {
+                    // from the stored (dtype-rounded) values, as a row pass over `out` would see
+                    float rs[EV];
 #pragma unroll
-                        for (int t = 0; t < EV; ++t) {
-                            nd = fmaf(r[t], sraw[q][t], nd);
-                            rs[t] = r[t] * ns;
-                        }
-                        Vec<T>::store(static_cast<T*>(a.nx_out) + seg * F + o, rs);
+                    for (int t = 0; t < EV; ++t) {
+                        const float rv = round_to<T>(r[t]);
+                        if constexpr (BWD) nd = fmaf(rv, sraw[q][t], nd);
+                        rs[t] = rv * ns;
                     }
+                    if constexpr (!BWD) {
+                        if (a.nx_seed) {
+                            if ((a.nx_thresh & 0xFFu) == 0)
+                                drop_apply<EV, 8>(nkey, a.nx_thresh, a.nx_dscale, seg, NVEC, q * LPR + lane, rs);
+                            else
+                                drop_apply<EV, 16>(nkey, a.nx_thresh, a.nx_dscale, seg, NVEC, q * LPR + lane, rs);
+                        }
+                    }
+                    Vec<T>::store(static_cast<T*>(a.nx_out) + seg * F + o, rs);
                 }
             }
         }
@@ -871,7 +887,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 10; }
+int regnn_abi_version(void) { return 11; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -957,6 +973,37 @@ static int spmm_fwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
     return REGNN_EUNSUPPORTED;
 }
 
+static int spmm_fwd_next_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                              const float* rel_table, const float* edge_w, const float* in_scale,
+                              const float* out_scale, const float* bias, const void* x, void* y,
+                              int64_t n_seg, int32_t F, int32_t dtype, int32_t split,
+                              int32_t chunk, const int32_t* long_ids, int32_t n_long,
+                              const int32_t* chunk_long, const int32_t* chunk_off,
+                              int32_t n_chunk, float* chunk_partial, const int32_t* level_sb,
+                              int32_t n_levels, const int64_t* level_desc,
+                              const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                              const float* nx_scale, const uint64_t* nx_seed, uint32_t nx_keep16,
+                              float nx_dscale, void* nx_out, hipStream_t stream) {
+    int st = check_common(ptr, idx, x, y, n_seg, split, chunk, long_ids, n_long, chunk_long,
+                          chunk_off, n_chunk, chunk_partial, rel, rel_table);
+    if (st) return st;
+    if (!nx_scale || !nx_out || (nx_seed && nx_keep16 > 65536u)) return REGNN_EINVAL;
+    if (drop_seed && drop_keep16 > 65536u) return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    if (n_levels < 0 || (n_levels > 0 && (!level_sb || !level_desc))) return REGNN_EINVAL;
+    if (n_long == 0) { split = 0; n_chunk = 0; n_levels = 0; }
+    SpmmArgs a = make_args(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, n_seg, F, split,
+                           chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk, chunk_partial,
+                           level_sb, n_levels, level_desc);
+    a.bias = bias; a.src = x; a.out = y;
+    a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
+    a.nx_scale = nx_scale; a.nx_out = nx_out;
+    a.nx_seed = nx_seed; a.nx_thresh = nx_keep16; a.nx_dscale = nx_dscale;
+    if (dtype == REGNN_F32) return dispatch<float>(a, kFwd, stream);
+    if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, kFwd, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
 static int spmm_bwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                          const float* rel_table, const float* edge_w, const float* in_scale,
                          const float* out_scale, const void* g, const void* x, const void* y,
@@ -1037,6 +1084,23 @@ int regnn_spmm_fwd_dropout(const int32_t* ptr, const int32_t* idx, const uint8_t
                          F, dtype, split, chunk, long_ids, n_long, chunk_long, chunk_off, n_chunk,
                          chunk_partial, level_sb, n_levels, level_desc, drop_seed, drop_keep16,
                          drop_scale, nullptr, nullptr, nullptr, 0.f, 0, stream);
+}
+
+int regnn_spmm_fwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* rel_table, const float* edge_w, const float* in_scale,
+                        const float* out_scale, const float* bias, const void* x, void* y,
+                        int64_t n_seg, int32_t F, int32_t dtype, int32_t split, int32_t chunk,
+                        const int32_t* long_ids, int32_t n_long, const int32_t* chunk_long,
+                        const int32_t* chunk_off, int32_t n_chunk, float* chunk_partial,
+                        const int32_t* level_sb, int32_t n_levels, const int64_t* level_desc,
+                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
+                        const float* nx_scale, const uint64_t* nx_seed, uint32_t nx_keep16,
+                        float nx_dscale, void* nx_out, hipStream_t stream) {
+    return spmm_fwd_next_impl(ptr, idx, rel, rel_table, edge_w, in_scale, out_scale, bias, x, y,
+                              n_seg, F, dtype, split, chunk, long_ids, n_long, chunk_long,
+                              chunk_off, n_chunk, chunk_partial, level_sb, n_levels, level_desc,
+                              drop_seed, drop_keep16, drop_scale, nx_scale, nx_seed, nx_keep16,
+                              nx_dscale, nx_out, stream);
 }
 
 int regnn_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,

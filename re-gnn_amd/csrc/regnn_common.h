@@ -54,6 +54,13 @@ template <> struct Vec<bf16_t> {
     }
 };
 
+// a value as it reads back after a store in T (fp32: itself; bf16: round to nearest even)
+template <typename T>
+__device__ __forceinline__ float round_to(float v) {
+    if constexpr (sizeof(T) == 2) return __uint_as_float(uint32_t(f2bf(v)) << 16);
+    else return v;
+}
+
 // raw 16-byte vector load (kept packed in 4 VGPRs until use) and its widening to fp32
 __device__ __forceinline__ uint4 load16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 

@@ -40,6 +40,9 @@ _SIG = {
     "regnn_spmm_bwd_dropout": ([P, P, P, P, P, P, P, P, P, P, P, P, I32, P, P, I64, I32, I32, I32,
                                 I32, P, I32, P, P, I32, P, P, I32, P, P, ctypes.c_uint32, F32, P],
                                ctypes.c_int),
+    "regnn_spmm_fwd_next": ([P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, P, I32, P, P,
+                             I32, P, P, I32, P, P, ctypes.c_uint32, F32, P, P, ctypes.c_uint32,
+                             F32, P, P], ctypes.c_int),
     "regnn_spmm_bwd_next": ([P, P, P, P, P, P, P, P, P, P, P, P, I32, P, P, I64, I32, I32, I32,
                              I32, P, I32, P, P, I32, P, P, I32, P, P, ctypes.c_uint32, F32, P, P,
                              P, P], ctypes.c_int),
@@ -80,7 +83,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 10
+ABI_VERSION = 11
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -105,6 +105,9 @@ def _input_proj(feats_dim_list, width):
 # REGCN: fuse the input projection with the first layer's pre-scale (ops.type_project_prescale)
 # where the shapes allow; False runs the unfused composition (A/B, tests)
 FUSE_PROJECTION = True
+# a weightless layer reading a weightless, activation-free layer's output: its pre-scaled,
+# dropped-out source rows leave the previous aggregation's epilogue (regnn_spmm_fwd_next)
+FUSE_NEXT = True
 
 
 class REGCN(nn.Module):
@@ -129,21 +132,41 @@ class REGCN(nn.Module):
 
     def embed(self, features_list, e_feat):
         """everything before out_lin: the node embeddings the reference returns as `h`."""
-        l0 = self.layers[0]
-        if FUSE_PROJECTION and l0.weight is None and l0.norm and \
-                ops.type_project_fusable(self.fc_list, features_list):
-            # per-type Linear + the first layer's feat_dropout and norm pre-scale in one pass
-            h = l0(self.g, None, e_feat, project=lambda norm, drop: ops.type_project_prescale(
-                self.fc_list, features_list, norm, drop))
-        else:
-            h = type_project(self.fc_list, features_list)
-            h = l0(self.g, h, e_feat)
         p = self.dropout.p if self.training else 0.0
-        for layer in self.layers[1:]:
+        # dropout seeds drawn in layer order, whatever order the chained calls below run in
+        seeds = [None] * self.num_layers
+        if self.training:
+            dev = self.layers[0].edge_weight.device
+            for i, layer in enumerate(self.layers):
+                pi = 1.0 - (1.0 - layer.feat_dropout.p) * (1.0 - (p if i else 0.0))
+                if 0.0 < pi < 1.0 and dev.type == "cuda":
+                    seeds[i] = ops.drop_request(pi, dev)[0]
+
+        def run(i, emit=None):
+            """layer i's output (with emit: (output, the next layer's pre-scaled rows))."""
+            layer = self.layers[i]
+            if i == 0:
+                if FUSE_PROJECTION and layer.weight is None and layer.norm and \
+                        ops.type_project_fusable(self.fc_list, features_list):
+                    # per-type Linear + the first layer's feat_dropout and norm pre-scale in
+                    # one pass
+                    return layer(self.g, None, e_feat, emit=emit, drop_seed=seeds[0],
+                                 project=lambda norm, drop: ops.type_project_prescale(
+                                     self.fc_list, features_list, norm, drop))
+                h = type_project(self.fc_list, features_list)
+                return layer(self.g, h, e_feat, emit=emit, drop_seed=seeds[0])
+            prev = self.layers[i - 1]
             # model dropout (model/REGCN.py:43) handed to the layer: fused with its own
             # feat_dropout into the aggregation's gather when the layer reads h directly
-            h = layer(self.g, h, e_feat, pre_dropout=p)
-        return h
+            if FUSE_NEXT and layer.weight is None and layer.norm and prev.weight is None and \
+                    prev.activation is None:
+                # the previous aggregation's epilogue forms this layer's norm * drop(h)
+                return layer(self.g, None, e_feat, pre_dropout=p, emit=emit, drop_seed=seeds[i],
+                             project=lambda norm, drop: run(i - 1, (norm, drop)))
+            return layer(self.g, run(i - 1), e_feat, pre_dropout=p, emit=emit,
+                         drop_seed=seeds[i])
+
+        return run(self.num_layers - 1)
 
     def forward(self, features_list, e_feat):
         h = self.embed(features_list, e_feat)

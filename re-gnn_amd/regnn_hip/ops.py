@@ -189,7 +189,7 @@ class _ReSpmm(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, tab, pre, post, bias, rg, pack, drop=None, prescaled=None, link=None,
-                link_in=None):
+                link_in=None, emit=None):
         x = x.contiguous()
         F = x.shape[1]
         y = torch.empty(rg.n_dst, F, dtype=x.dtype, device=x.device)
@@ -210,7 +210,15 @@ class _ReSpmm(torch.autograd.Function):
                     L.ptr(t), None, L.ptr(in_scale), L.ptr(post),
                     L.ptr(None if bias is None else bias.detach().float().contiguous()),
                     L.ptr(src), L.ptr(y), rg.n_dst, F, L.dtype_code(x), *plan_args)
-            if drop is None or prescale or prescaled is not None:
+            if emit is not None:
+                # the consumer's pre-scaled rows drop'(scale * y) leave from the same epilogue
+                nscale, ndrop = emit[0], emit[1]
+                xs = torch.empty_like(y)
+                gdrop = drop if (drop is not None and not prescale and prescaled is None) else None
+                L.call("regnn_spmm_fwd_next", *args, *(_drop_args(gdrop)), L.ptr(nscale),
+                       *(_drop_args(ndrop)), L.ptr(xs), L.stream())
+                emit[2] = xs
+            elif drop is None or prescale or prescaled is not None:
                 L.call("regnn_spmm_fwd", *args, L.stream())
             else:
                 L.call("regnn_spmm_fwd_dropout", *args, L.ptr(drop[0]), drop[1], drop[2],
@@ -298,11 +306,11 @@ class _ReSpmm(torch.autograd.Function):
                     g_post = (gf * yf).sum(1) / post
         g_bias = gy.float().sum(0) if need_bias else None
         return (gx if need_x else None), g_tab, g_pre, g_post, g_bias, None, None, None, None, \
-            None, None
+            None, None, None
 
 
 def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=0.0,
-            drop_seed=None, prescaled=None):
+            drop_seed=None, prescaled=None, emit=None):
     """y[v] = post[v] * sum_{e: u->v} tab[rel_e] * pre[u] * drop(x)[u] + bias  (HIP).
 
     dropout: probability of an nn.Dropout applied to x in front of the aggregation; fused into
@@ -311,7 +319,12 @@ def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=
     (differentiable post-scale: the node-norm gradient reads <g, y> / post).
 
     prescaled: pre * drop(x) formed by x's producer (type_project_prescale, same pre and
-    drop_seed); the forward gathers it directly, the backward is unchanged."""
+    drop_seed); the forward gathers it directly, the backward is unchanged.
+
+    emit: (scale, drop) of a consumer aggregation that reads y as its input (drop a
+    drop_request or None): returns (y, xs) with xs = drop(scale * y) from the same epilogue
+    (regnn_spmm_fwd_next), the consumer's `prescaled`; xs is None where the epilogue cannot form
+    it (bias added outside the op), and the consumer then runs its own row pass."""
     drop = None
     if dropout:
         if dropout < 1.0 and dropout_fusable(x):
@@ -326,16 +339,23 @@ def re_spmm(rg, x, tab=None, pack=None, pre=None, post=None, bias=None, dropout=
     if link_in is not None and (not x.is_cuda or not dropout_fusable(x)):
         link_in = None
     if bias is not None and post is not None and post.requires_grad:
-        return _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop, prescaled, None,
-                             link_in) + bias
+        y = _ReSpmm.apply(x, tab, pre, post, None, rg, pack, drop, prescaled, None,
+                          link_in) + bias
+        return y if emit is None else (y, None)
     link = None
     if post is not None and x.is_cuda and PRESCALE["next"] != "off" and \
             PRESCALE["bwd"] != "off":
         link = _NextLink(post.detach())
-    y = _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop, prescaled, link, link_in)
+    holder = None
+    if emit is not None and PRESCALE["next"] != "off" and x.is_cuda and \
+            (emit[1] is None or dropout_fusable(x)):
+        holder = [emit[0].detach().float().contiguous(), emit[1], None]
+    y = _ReSpmm.apply(x, tab, pre, post, bias, rg, pack, drop, prescaled, link, link_in, holder)
     if link is not None:
         y._regnn_link = link
-    return y
+    if emit is None:
+        return y
+    return y, (None if holder is None else holder[2])
 
 
 class _TypeProjPre(torch.autograd.Function):

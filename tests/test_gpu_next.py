@@ -122,3 +122,82 @@ def test_next_handoff_equals_row_pass():
     for a, b in zip(grads["auto"], grads["off"]):
         err = float((a - b).abs().max()) / max(1.0, float(b.abs().max()))
         assert err <= 1e-6
+
+
+@pytest.mark.parametrize("dtype,F", [(torch.float32, 64), (torch.bfloat16, 64),
+                                     (torch.bfloat16, 128)])
+@pytest.mark.parametrize("p", [0.0, 0.5, 0.75, 0.3])
+def test_fwd_emit_equals_row_pass(dtype, F, p):
+    """regnn_spmm_fwd_next: the consumer's rows drop(scale * y) from the epilogue are
+    bit-identical to regnn_row_scale over the stored y with the same scale and seed."""
+    from regnn_hip import ops
+    from regnn_hip import _lib as L
+    from regnn_hip.graph import RelGraph
+    src, dst, rel, n, R = _graph(seed=4)
+    rg = RelGraph(src, dst, n, DEV)
+    pack = rg.rel_pack(torch.from_numpy(rel).to(DEV), num_rel=R)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(n, F, generator=g).to(dtype).to(DEV)
+    tab = (torch.rand(R, 1, generator=g) + 0.2).to(DEV)
+    m0 = (torch.rand(n, generator=g) + 0.5).to(DEV)
+    s1 = (torch.rand(n, generator=g) + 0.5).to(DEV)
+    bias = torch.randn(F, generator=g).to(DEV)
+    drop = ops.drop_request(p, DEV, torch.tensor([991], dtype=torch.int64, device=DEV)) \
+        if p else None
+    with torch.no_grad():
+        y, xs = ops.re_spmm(rg, x, tab, pack, pre=m0, post=m0, bias=bias, emit=(s1, drop))
+        y_ref = ops.re_spmm(rg, x, tab, pack, pre=m0, post=m0, bias=bias)
+        ref = torch.empty_like(y)
+        L.call("regnn_row_scale", L.ptr(y), L.ptr(s1), L.ptr(ref), n, F, L.dtype_code(y),
+               *(ops._drop_args(drop)), None, None, L.stream())
+    assert xs is not None
+    assert torch.equal(y, y_ref)
+    assert torch.equal(xs, ref)
+
+
+@pytest.mark.parametrize("train", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_regcn_chained_matches_unchained(train, dtype):
+    """nets.FUSE_NEXT: REGCN with layer 1's pre-scaled rows from layer 0's epilogue (and the
+    backward hand-off) equals the unchained composition: h, loss and every gradient."""
+    import torch.nn.functional as F
+    from regnn_hip import nets, ops, synth
+    import dgl
+    gd = synth.mag_like(0.002, seed=3, device=DEV)
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    e_feat = gd["rel"].to(torch.int64)
+    feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1, device=DEV,
+                                kind="mag")
+    feats = [f.to(dtype) for f in feats]
+    torch.manual_seed(0)
+    net = nets.REGCN(g, gd["R"], 100.0, 64, 64, 349, 2, F.elu, 0.5,
+                     [f.shape[1] for f in feats]).to(DEV)
+    net.train(train)
+    labels = torch.randint(0, 349, (gd["counts"]["paper"],), device=DEV)
+    W, b = net.head()
+    out = {}
+    old = (nets.FUSE_NEXT, dict(ops.PRESCALE))
+    try:
+        for fused in (False, True):
+            nets.FUSE_NEXT = fused
+            ops.PRESCALE["next"] = "auto" if fused else "off"
+            ops._DROP_CTR.clear()
+            torch.manual_seed(5)                         # same dropout seeds in both runs
+            net.zero_grad()
+            h = net.embed(feats, e_feat)
+            _, loss = ops.head_ce(h.float(), W, b, labels)
+            loss.backward()
+            out[fused] = (h.detach().float().clone(), float(loss),
+                          {k: p.grad.clone() for k, p in net.named_parameters()
+                           if p.grad is not None})
+    finally:
+        nets.FUSE_NEXT = old[0]
+        ops.PRESCALE.update(old[1])
+    (h0, l0, g0), (h1, l1, g1) = out[False], out[True]
+    rel = lambda a, b: float((a - b).abs().max()) / max(1.0, float(b.abs().max()))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(h1, h0) <= tol
+    assert abs(l1 - l0) <= tol * max(1.0, abs(l0))
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert rel(g1[k], g0[k]) <= (1e-4 if dtype == torch.float32 else 2e-2), k
