@@ -544,7 +544,9 @@ template <int NT>
 __global__ void __launch_bounds__(kGhBlock)
 head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
                   const float* __restrict__ W,
-                  const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out) {
+                  const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out,
+                  const float* __restrict__ nx_scale, const float* __restrict__ hx,
+                  float* __restrict__ nx_out, float* __restrict__ nx_dot) {
     constexpr int K = kHeadK, NCH = (NT + 1) / 2, CP32 = 32 * NCH, LDR = CP32 + 8;
     extern __shared__ uint16_t Wt[];                       // [3][K][LDR] bf16
     for (int idx = threadIdx.x; idx < CP32 * K; idx += blockDim.x) {
@@ -606,17 +608,45 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
                 acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b0, acc[kt], 0, 0, 0);
             }
         }
+        float d = 0.f, ns = 1.f;
         if (valid) {
             float* gr = gh + row * K + 4 * q;
+            f32x4 g[4];
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-                *reinterpret_cast<f32x4*>(gr + 16 * kt) = acc[kt] * sc;
+            for (int kt = 0; kt < 4; ++kt) {
+                g[kt] = acc[kt] * sc;
+                *reinterpret_cast<f32x4*>(gr + 16 * kt) = g[kt];
+            }
+            if (nx_scale) {                                  // kernel-uniform
+                // the consumer-side row pass of h's producer (regnn_head_gh_next)
+                ns = nx_scale[row];
+                const float* hr = hx + row * K + 4 * q;
+                float* orow = nx_out + row * K + 4 * q;
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    const f32x4 hv = *reinterpret_cast<const f32x4*>(hr + 16 * kt);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) d = fmaf(g[kt][i], hv[i], d);
+                    *reinterpret_cast<f32x4*>(orow + 16 * kt) = g[kt] * ns;
+                }
+            }
+        }
+        if (nx_scale) {                                      // a row's 64 features: lanes c + 16 q
+            d += __shfl_xor(d, 16);
+            d += __shfl_xor(d, 32);
+            if (valid && q == 0) nx_dot[row] = d / ns;
         }
     }
     const int64_t z0 = n * K / 4, z1 = n_out * K / 4;      // rows without a loss term: zero
     for (int64_t v = z0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < z1;
-         v += (int64_t)gridDim.x * blockDim.x)
+         v += (int64_t)gridDim.x * blockDim.x) {
         reinterpret_cast<f32x4*>(gh)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (nx_scale) reinterpret_cast<f32x4*>(nx_out)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (nx_scale)
+        for (int64_t r = n + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_out;
+             r += (int64_t)gridDim.x * blockDim.x)
+            nx_dot[r] = 0.f;
 }
 
 // gW^T partial of this block's row range: wave w owns class tiles w, w + 8, w + 16; per 4-row
@@ -810,9 +840,12 @@ int launch_wgrad_x6(const TP* p, int64_t n, int C, int64_t ld, const TH* h, floa
 template <int NT>
 int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W, const float* h,
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
-                    hipStream_t stream) {
+                    hipStream_t stream, const float* nx_scale = nullptr,
+                    const float* hx = nullptr, float* nx_out = nullptr,
+                    float* nx_dot = nullptr) {
     constexpr int K = kHeadK;
-    if (gh && g_tune_head != 16) {            // bf16x6 gh (default)
+    if (nx_scale && !gh) return REGNN_EINVAL;
+    if (gh && (g_tune_head != 16 || nx_scale)) {   // bf16x6 gh (default)
         constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
         static bool attr6 = false;
         if (!attr6) {
@@ -829,7 +862,8 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
         if (grid > cap) grid = cap;
         if (grid < 1) grid = 1;
         hipLaunchKernelGGL((head_gh_x6_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
-                           stream, p, n, C, ld, W, gscale, gh, n_out);
+                           stream, p, n, C, ld, W, gscale, gh, n_out, nx_scale, hx, nx_out,
+                           nx_dot);
         REGNN_LAUNCH_CHECK();
     } else if (gh) {
         const size_t lds = (size_t)K * (NT * 16 + 1) * sizeof(float);
@@ -1299,6 +1333,29 @@ int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, 
 #define HB_CASE(nt) \
         case nt: return launch_head_bwd<nt>(p, n, C, ld, W, h, gscale, gh, n_out, slab,       \
                                             slab_rows, stream);
+        HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
+        HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
+        HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)
+        HB_CASE(19) HB_CASE(20) HB_CASE(21) HB_CASE(22) HB_CASE(23) HB_CASE(24)
+#undef HB_CASE
+        default: return REGNN_EINVAL;
+    }
+}
+
+int regnn_head_gh_next(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K,
+                       const float* W, const float* gscale, float* gh, int64_t n_out,
+                       const float* nx_scale, const float* h, float* nx_out, float* nx_dot,
+                       hipStream_t stream) {
+    if (!p || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C || !W || !gh ||
+        n_out < n || !nx_scale || !h || !nx_out || !nx_dot ||
+        ((reinterpret_cast<uintptr_t>(gh) | reinterpret_cast<uintptr_t>(h) |
+          reinterpret_cast<uintptr_t>(nx_out)) & 15))
+        return REGNN_EINVAL;
+    if (n_out == 0) return REGNN_OK;
+    switch ((C + 15) / 16) {
+#define HB_CASE(nt) \
+        case nt: return launch_head_bwd<nt>(p, n, C, ld, W, nullptr, gscale, gh, n_out, nullptr, \
+                                            0, stream, nx_scale, h, nx_out, nx_dot);
         HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
         HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
         HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)

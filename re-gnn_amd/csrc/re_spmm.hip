@@ -887,7 +887,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 11; }
+int regnn_abi_version(void) { return 12; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {

@@ -792,6 +792,8 @@ class _HeadCE(torch.autograd.Function):
         loss = loss_rows.sum() / n
         ctx.save_for_backward(h, W, p)
         ctx.has_bias = b is not None
+        # h straight from an aggregation (re_spmm): its backward row pass rides on gh's kernel
+        ctx.link = getattr(h, "_regnn_link", None) if h.dtype == torch.float32 else None
         ctx.mark_non_differentiable(logits)
         return logits, loss
 
@@ -816,10 +818,23 @@ class _HeadCE(torch.autograd.Function):
             if need_h:
                 gh = torch.empty_like(h)
                 gl = g_loss.detach().reshape(1).float().contiguous()
-                with timed("head_gh", 4 * (p.numel() + h.numel())):
-                    L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K,
-                           L.ptr(W.detach().contiguous()), None, L.ptr(gl), L.ptr(gh),
-                           h.shape[0], None, 0, L.stream())
+                nx = ctx.link
+                if nx is not None and nx.post.numel() == h.shape[0] and \
+                        PRESCALE["next"] != "off":
+                    # also nx.post * gh and <gh, h> / nx.post for h's producer (_NextLink)
+                    nx_out = torch.empty_like(h)
+                    nx_dot = torch.empty(h.shape[0], dtype=torch.float32, device=h.device)
+                    with timed("head_gh", 4 * (p.numel() + h.numel())):
+                        L.call("regnn_head_gh_next", L.ptr(p), n, C, p.stride(0), K,
+                               L.ptr(W.detach().contiguous()), L.ptr(gl), L.ptr(gh),
+                               h.shape[0], L.ptr(nx.post), L.ptr(hc), L.ptr(nx_out),
+                               L.ptr(nx_dot), L.stream())
+                    nx.handoff = (gh, gh._version, nx_out, nx_dot)
+                else:
+                    with timed("head_gh", 4 * (p.numel() + h.numel())):
+                        L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K,
+                               L.ptr(W.detach().contiguous()), None, L.ptr(gl), L.ptr(gh),
+                               h.shape[0], None, 0, L.stream())
             if slab is not None:
                 with timed("head_bwd", 4 * (p.numel() + n * K)):
                     L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K, None, L.ptr(hc),

@@ -201,3 +201,47 @@ def test_regcn_chained_matches_unchained(train, dtype):
     assert g0.keys() == g1.keys()
     for k in g0:
         assert rel(g1[k], g0[k]) <= (1e-4 if dtype == torch.float32 else 2e-2), k
+
+
+@pytest.mark.parametrize("n_loss", [333, 900])
+def test_head_gh_handoff(n_loss, monkeypatch):
+    """regnn_head_gh_next: the output head's gh kernel forms the last aggregation's pre-scaled
+    gradient rows (zero rows without a loss term); gradients equal the row-pass path."""
+    from regnn_hip import ops
+    from regnn_hip.graph import RelGraph
+    taken = []
+    orig = ops._NextLink.take
+
+    def spy(self, gy):
+        offered = self.handoff is not None
+        r = orig(self, gy)
+        if offered:
+            taken.append(r is not None)
+        return r
+    monkeypatch.setattr(ops._NextLink, "take", spy)
+    src, dst, rel, n, R = _graph(seed=6)
+    rg = RelGraph(src, dst, n, DEV)
+    pack = rg.rel_pack(torch.from_numpy(rel).to(DEV), num_rel=R)
+    g = torch.Generator().manual_seed(4)
+    C = 37
+    base = [torch.randn(n, 64, generator=g), torch.rand(R, 1, generator=g) + 0.2,
+            torch.rand(n, generator=g) + 0.5, torch.randn(C, 64, generator=g) * 0.1,
+            torch.randn(C, generator=g)]
+    labels = torch.randint(0, C, (n_loss,), generator=g).to(DEV)
+    grads = {}
+    old = dict(ops.PRESCALE)
+    try:
+        for mode in ("auto", "off"):
+            ops.PRESCALE["next"] = mode
+            taken.clear()
+            xd, t0, m0, W, b = [t.to(DEV).requires_grad_(True) for t in base]
+            y = ops.re_spmm(rg, xd, t0, pack, pre=m0, post=m0)
+            _, loss = ops.head_ce(y, W, b, labels)
+            loss.backward()
+            assert taken == ([True] if mode == "auto" else [])
+            grads[mode] = [t.grad.clone() for t in (xd, t0, m0, W, b)]
+    finally:
+        ops.PRESCALE.update(old)
+    for a, b in zip(grads["auto"], grads["off"]):
+        err = float((a - b).abs().max()) / max(1.0, float(b.abs().max()))
+        assert err <= 1e-6
