@@ -226,8 +226,10 @@ int regnn_spmm_bwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* r
                         const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
                         const float* nx_scale, void* nx_out, float* nx_dot, hipStream_t stream);
 
-/* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order. */
-int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
+/* out[k] = (accumulate ? out[k] : 0) + sum_{row < n_rows} slab[row][k], k < width, fixed order.
+ * The slab is scratch: a wide one (width >= 4096, n_rows >= 256) is reduced in place in two
+ * fixed-order stages (row splits, then the split sums), and its contents are clobbered. */
+int regnn_rel_reduce(float* slab, int64_t n_rows, int32_t width, float* out,
                      int32_t accumulate, hipStream_t stream);
 
 /* GAT attention, forward. Replaces apply_edges(fn.u_add_v('el','er','e')) + ee add +

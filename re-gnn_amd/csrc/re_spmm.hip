@@ -723,22 +723,44 @@ rel_reduce_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
 
 // wide slabs (per-block partials of a whole weight matrix): one thread per column walks the
 // rows in order, so a warp reads consecutive columns of one row (coalesced), fixed order
+// (rows r * stride, r < n_rows; the second stage of the split reduce below reads stride rps)
 __global__ void __launch_bounds__(kBlock)
 rel_reduce_wide_kernel(const float* __restrict__ slab, int64_t n_rows, int32_t width,
-                       float* __restrict__ out, int32_t accumulate) {
+                       float* __restrict__ out, int32_t accumulate, int64_t stride = 1) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= width) return;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    const int64_t ws = stride * width;
     int64_t r = 0;
     for (; r + 4 <= n_rows; r += 4) {
+        s0 += slab[r * ws + k];
+        s1 += slab[(r + 1) * ws + k];
+        s2 += slab[(r + 2) * ws + k];
+        s3 += slab[(r + 3) * ws + k];
+    }
+    for (; r < n_rows; ++r) s0 += slab[r * ws + k];
+    const float t = (s0 + s1) + (s2 + s3);
+    out[k] = accumulate ? out[k] + t : t;
+}
+
+// first stage of a tall wide slab's reduce: (column k, split s) sums rows [s rps, (s+1) rps) in
+// order and leaves the sum in row s rps, which no other thread reads (in place, no scratch);
+// blockIdx.y = s fills the chip where one thread per column gives only width / 256 blocks
+__global__ void __launch_bounds__(kBlock)
+rel_reduce_split_kernel(float* __restrict__ slab, int64_t n_rows, int32_t width, int64_t rps) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= width) return;
+    const int64_t r0 = (int64_t)blockIdx.y * rps, r1 = min(n_rows, r0 + rps);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0;
+    for (; r + 4 <= r1; r += 4) {
         s0 += slab[r * width + k];
         s1 += slab[(r + 1) * width + k];
         s2 += slab[(r + 2) * width + k];
         s3 += slab[(r + 3) * width + k];
     }
-    for (; r < n_rows; ++r) s0 += slab[r * width + k];
-    const float t = (s0 + s1) + (s2 + s3);
-    out[k] = accumulate ? out[k] + t : t;
+    for (; r < r1; ++r) s0 += slab[r * width + k];
+    slab[r0 * width + k] = (s0 + s1) + (s2 + s3);
 }
 
 // out[u] = scale[u] * drop(x[u]) and optionally dot[u] = <x[u], z[u]> / scale[u]; LPR lanes per
@@ -1209,12 +1231,24 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
     return REGNN_OK;
 }
 
-int regnn_rel_reduce(const float* slab, int64_t n_rows, int32_t width, float* out,
+int regnn_rel_reduce(float* slab, int64_t n_rows, int32_t width, float* out,
                      int32_t accumulate, hipStream_t stream) {
     if (!slab || !out || width <= 0 || n_rows < 0) return REGNN_EINVAL;
-    if (width >= 4096)
-        hipLaunchKernelGGL(rel_reduce_wide_kernel, dim3((width + kBlock - 1) / kBlock),
-                           dim3(kBlock), 0, stream, slab, n_rows, width, out, accumulate);
+    const int64_t cols = (width + kBlock - 1) / kBlock;
+    if (width >= 4096 && n_rows >= 256) {
+        // split rows so that ~2048 blocks run, >= 32 rows per split
+        int64_t splits = (2048 + cols - 1) / cols;
+        if (splits > n_rows / 32) splits = n_rows / 32;
+        const int64_t rps = (n_rows + splits - 1) / splits;
+        splits = (n_rows + rps - 1) / rps;
+        hipLaunchKernelGGL(rel_reduce_split_kernel, dim3((unsigned)cols, (unsigned)splits),
+                           dim3(kBlock), 0, stream, slab, n_rows, width, rps);
+        REGNN_LAUNCH_CHECK();
+        hipLaunchKernelGGL(rel_reduce_wide_kernel, dim3((unsigned)cols), dim3(kBlock), 0, stream,
+                           slab, splits, width, out, accumulate, rps);
+    } else if (width >= 4096)
+        hipLaunchKernelGGL(rel_reduce_wide_kernel, dim3((unsigned)cols), dim3(kBlock), 0, stream,
+                           slab, n_rows, width, out, accumulate, (int64_t)1);
     else
         hipLaunchKernelGGL(rel_reduce_kernel, dim3(width), dim3(kBlock), 0, stream, slab, n_rows,
                            width, out, accumulate);

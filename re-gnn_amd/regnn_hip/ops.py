@@ -387,11 +387,14 @@ class _TypeProjPre(torch.autograd.Function):
         ctx.n, ctx.rows = n, rows
         ctx.save_for_backward(*xs_in, *Ws)
         ctx.mark_non_differentiable(xs)
+        ctx.set_materialize_grads(False)      # no N x F zero gradient for the side output xs
         return h, xs
 
     @staticmethod
     def backward(ctx, g, _gxs):
         n = ctx.n
+        if g is None:
+            return (None,) * (3 + 3 * n)
         saved = ctx.saved_tensors
         xs_in, Ws = saved[:n], saved[n:]
         g = g.contiguous()

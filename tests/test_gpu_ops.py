@@ -109,6 +109,27 @@ def test_col_sum(rows, cols):
     assert torch.equal(got, ops.col_sum(x))      # deterministic
 
 
+@pytest.mark.parametrize("rows,width", [(2048, 22880), (300, 8256), (255, 5000), (2048, 4096),
+                                        (1000, 4095), (33, 9000)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_rel_reduce_wide(rows, width, accumulate):
+    """regnn_rel_reduce on wide slabs (the in-place two-stage split for tall ones): fixed-order
+    column sums, deterministic."""
+    from regnn_hip import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(rows + width)
+    slab = torch.randn(rows, width, device=DEV, generator=g)
+    base = torch.randn(width, device=DEV, generator=g)
+    want = slab.double().sum(0) + (base.double() if accumulate else 0)
+    outs = []
+    for _ in range(2):
+        s = slab.clone()
+        out = base.clone()
+        L.call("regnn_rel_reduce", L.ptr(s), rows, width, L.ptr(out), int(accumulate), L.stream())
+        outs.append(out)
+    assert _rel(outs[0], want) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("bias", [True, False])
 @pytest.mark.parametrize("N,D,C,n", [(5000, 64, 349, 1800),     # fused MFMA head, 11 col tiles
                                      (1001, 64, 3, 1001),       # 1 col tile, every row a loss row
