@@ -89,7 +89,12 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
  * p < desc[k][1]) into row desc[k][2] + p; the last level leaves row desc[n-1][2] + l for long
  * segment l (n_levels == 0: row chunk_off[l]). level_desc is a HOST array [n_levels][3]
  * (int64: sb offset, n_out, output row base); chunk_partial is fp32 scratch
- * [n_chunk + sum n_out, F]. Deterministic for any chunk count (hub rows of 10^7 edges). */
+ * [n_chunk + sum n_out, F]. Deterministic for any chunk count (hub rows of 10^7 edges).
+ * Scheduled form (split < 0, |split| is the threshold): chunk_long holds 2 * n_chunk entries and
+ * chunk_long[n_chunk + i] is the chunk handled in processing slot i (a permutation; partial rows
+ * and the tree are unchanged). The build orders slots by each chunk's first gathered row, so with
+ * rows sorted by gathered id the chunks in flight share gathered rows in L2 / Infinity Cache.
+ * Every entry point below that takes a plan accepts either form. */
 int regnn_spmm_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                    const float* rel_table, const float* edge_w,
                    const float* in_scale, const float* out_scale, const float* bias,

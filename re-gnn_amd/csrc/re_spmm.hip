@@ -37,6 +37,7 @@ struct SpmmArgs {
     int64_t n_seg;
     int32_t F;
     int32_t split;
+    const int32_t* chunk_sched;  // processing slot -> chunk (NULL: identity); see make_args
     int32_t chunk;
     const int32_t* long_ids;
     int32_t n_long;
@@ -408,8 +409,9 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     if constexpr (S::SLAB) bins_zero(bins, a.n_rel, tid);
-    for (int64_t c = (int64_t)blockIdx.x * GPB + tid / LPR; c < a.n_chunk;
-         c += (int64_t)gridDim.x * GPB) {
+    for (int64_t i = (int64_t)blockIdx.x * GPB + tid / LPR; i < a.n_chunk;
+         i += (int64_t)gridDim.x * GPB) {
+        const int64_t c = a.chunk_sched ? a.chunk_sched[i] : i;     // group-uniform
         const int l = a.chunk_long[c];
         const int64_t seg = a.long_ids[l];
         const int k = int(c) - a.chunk_off[l];
@@ -947,7 +949,11 @@ static SpmmArgs make_args(const int32_t* ptr, const int32_t* idx, const uint8_t*
     SpmmArgs a{};
     a.ptr = ptr; a.idx = idx; a.rel = rel; a.tab = tab; a.edge_w = edge_w;
     a.in_scale = in_scale; a.out_scale = out_scale; a.n_seg = n_seg; a.F = F;
-    a.split = split; a.chunk = chunk; a.long_ids = long_ids; a.n_long = n_long;
+    // split < 0: the scheduled plan form, chunk_long[n_chunk, 2 n_chunk) = the chunk handled
+    // in processing slot i (regnn_hip.h, long-segment plans)
+    a.split = split < 0 ? -split : split;
+    a.chunk_sched = split < 0 ? chunk_long + n_chunk : nullptr;
+    a.chunk = chunk; a.long_ids = long_ids; a.n_long = n_long;
     a.chunk_long = chunk_long; a.chunk_off = chunk_off; a.n_chunk = n_chunk;
     a.chunk_partial = chunk_partial;
     a.level_sb = level_sb; a.n_levels = n_levels; a.level_desc = level_desc;
@@ -961,8 +967,7 @@ static int check_common(const int32_t* ptr, const int32_t* idx, const void* src,
                         const float* tab) {
     if (n_seg < 0 || !ptr || (n_seg > 0 && (!idx || !src || !out))) return REGNN_EINVAL;
     if (tab && !rel) return REGNN_EINVAL;
-    if (split < 0) return REGNN_EINVAL;
-    if (split > 0 && n_long > 0 &&
+    if (split != 0 && n_long > 0 &&
         (chunk <= 0 || !long_ids || !chunk_long || !chunk_off || !chunk_partial || n_chunk <= 0))
         return REGNN_EINVAL;
     return REGNN_OK;

@@ -7,6 +7,12 @@ import torch
 from .base import DGLError
 
 
+
+# row order of the device layout (regnn_hip.graph): "source" sorts each row by the gathered id and
+# schedules hub-row chunks by source range (shared rows hit in L2 / Infinity Cache); "edge" keeps
+# DGL's edge-id summation order
+RELGRAPH_ORDER = "source"
+
 class _Frame(dict):
     pass
 
@@ -123,7 +129,7 @@ class DGLGraph:
         key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
         rg = self._rg_cache.get(key)
         if rg is None:
-            rg = RelGraph(self._src, self._dst, self._n, dev)
+            rg = RelGraph(self._src, self._dst, self._n, dev, order=RELGRAPH_ORDER)
             self._rg_cache[key] = rg
         return rg
 

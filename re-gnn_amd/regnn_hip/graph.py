@@ -7,8 +7,13 @@ HBM layout (built once per graph per device, int32 indices, uint8 relation ids):
   long-segment plans   segments with > split edges are cut into `chunk`-edge pieces
                        (hub rows of power-law graphs would otherwise serialise one wave)
 
-Edge ids are the caller's (DGL) edge order; within a CSR row edges stay in edge-id order
-(stable sort), which is the summation order of DGL's own CSR gspmm.
+Edge ids are the caller's (DGL) edge order. Within a row, edges are ordered either
+  order="edge"    by edge id (stable sort): the summation order of DGL's own CSR gspmm; or
+  order="source"  by the other end's id (ties by edge id): a chunk of a hub row then covers a
+                  narrow range of gathered rows, and the plan's chunk schedule (chunks sorted by
+                  their first gathered row) makes the chunks in flight at any moment gather
+                  overlapping rows, so a row shared by several hubs is fetched from HBM once and
+                  hit in L2 / Infinity Cache by the others. Sums change only by rounding order.
 """
 import ctypes
 
@@ -32,7 +37,10 @@ class SegPlan:
         plan.level_sb, plan.level_desc = None, None
         return plan
 
-    def __init__(self, ptr, split=SPLIT, chunk=CHUNK):
+    def __init__(self, ptr, split=SPLIT, chunk=CHUNK, idx=None):
+        """idx given (rows sorted by gathered id): chunks are scheduled by their first gathered
+        row (chunk_sched); kernels take the schedule as chunk_long's second half, split < 0."""
+        self.chunk_sched = None
         deg = (ptr[1:] - ptr[:-1]).to(torch.int64)
         long_ids = torch.nonzero(deg > split).flatten()
         self.split, self.chunk = split, chunk
@@ -51,6 +59,12 @@ class SegPlan:
             torch.arange(self.n_long, device=ptr.device, dtype=torch.int32), nch)
         self.n_chunk = int(off[-1].item())
         self._tree(nch, off)
+        if idx is not None:
+            l = self.chunk_long.to(torch.int64)
+            k = torch.arange(self.n_chunk, device=ptr.device) - off[l]
+            first = ptr.to(torch.int64)[long_ids[l]] + k * chunk
+            order = torch.sort(idx[first].to(torch.int64), stable=True)[1]
+            self.chunk_sched = torch.cat([self.chunk_long, order.to(torch.int32)]).contiguous()
 
     def _tree(self, counts, in_off, fanin=FANIN):
         """fixed-order reduction tree over each long segment's chunk partials (<= fanin inputs
@@ -132,7 +146,8 @@ class RelPack:
 class RelGraph:
     """CSR (by destination) + CSC (by source) of a directed multigraph on one device."""
 
-    def __init__(self, src, dst, num_nodes, device, num_dst=None, split=SPLIT, chunk=CHUNK):
+    def __init__(self, src, dst, num_nodes, device, num_dst=None, split=SPLIT, chunk=CHUNK,
+                 order="edge"):
         src = torch.as_tensor(src).to(device=device, dtype=torch.int64).reshape(-1)
         dst = torch.as_tensor(dst).to(device=device, dtype=torch.int64).reshape(-1)
         self.device = torch.device(device)
@@ -141,8 +156,15 @@ class RelGraph:
         self.E = int(src.numel())
         if self.E >= 2 ** 31 or max(self.n_src, self.n_dst) >= 2 ** 31:
             raise ValueError("graphs with >= 2^31 edges or nodes need 64-bit offsets (not built)")
-        _, csr_eid = torch.sort(dst, stable=True)
-        _, csc_eid = torch.sort(src, stable=True)
+        if order not in ("edge", "source"):
+            raise ValueError(f"order must be 'edge' or 'source', got {order!r}")
+        self.order = order
+        if order == "edge":
+            _, csr_eid = torch.sort(dst, stable=True)
+            _, csc_eid = torch.sort(src, stable=True)
+        else:
+            _, csr_eid = torch.sort(dst * self.n_src + src, stable=True)
+            _, csc_eid = torch.sort(src * self.n_dst + dst, stable=True)
         self.csr_eid = csr_eid
         self.csc_eid = csc_eid
         self.csr_idx = src[csr_eid].to(torch.int32).contiguous()
@@ -152,8 +174,9 @@ class RelGraph:
         inv = torch.empty_like(csr_eid)
         inv[csr_eid] = torch.arange(self.E, device=self.device)
         self.csc2csr = inv[csc_eid].to(torch.int32).contiguous()
-        self.csr_plan = SegPlan(self.csr_ptr, split, chunk)
-        self.csc_plan = SegPlan(self.csc_ptr, split, chunk)
+        srt = order == "source"
+        self.csr_plan = SegPlan(self.csr_ptr, split, chunk, self.csr_idx if srt else None)
+        self.csc_plan = SegPlan(self.csc_ptr, split, chunk, self.csc_idx if srt else None)
         self._packs = {}
         self._inv_cnt = None
 

@@ -35,6 +35,12 @@ def _plan_args(plan, F, device):
     if plan.n_chunk == 0:
         return (0, 0, None, 0, None, None, 0, None, None, 0, None), None
     part = plan.partial(F, device)
+    if plan.chunk_sched is not None:
+        # scheduled form (regnn_hip.h): chunk_long + the processing order, split negated
+        return (-plan.split, plan.chunk, L.ptr(plan.long_ids), plan.n_long,
+                L.ptr(plan.chunk_sched), L.ptr(plan.chunk_off), plan.n_chunk, L.ptr(part),
+                L.ptr(plan.level_sb), plan.n_levels,
+                ctypes.cast(plan.level_desc, ctypes.c_void_p)), part
     return (plan.split, plan.chunk, L.ptr(plan.long_ids), plan.n_long, L.ptr(plan.chunk_long),
             L.ptr(plan.chunk_off), plan.n_chunk, L.ptr(part), L.ptr(plan.level_sb),
             plan.n_levels, ctypes.cast(plan.level_desc, ctypes.c_void_p)), part

@@ -37,12 +37,15 @@ def _oracle_layer(src, dst, rel, N, R, feat, ew, gout, norm=True):
 
 @pytest.mark.parametrize("split,chunk", [(256, 256), (32, 16), (8, 4), (64, 64)])
 @pytest.mark.parametrize("F", [64, 32])
-def test_regraphconv_long_rows(split, chunk, F):
+@pytest.mark.parametrize("order", ["edge", "source"])
+def test_regraphconv_long_rows(split, chunk, F, order):
+    """order="source": rows sorted by gathered id and chunks run in the scheduled order."""
     from layer import REGraphConv
     from regnn_hip.graph import RelGraph
     src, dst, rel, N, R = power_graph()
-    rg = RelGraph(src, dst, N, DEV, split=split, chunk=chunk)
+    rg = RelGraph(src, dst, N, DEV, split=split, chunk=chunk, order=order)
     assert rg.csr_plan.n_long > 0 and rg.csc_plan.n_long > 0
+    assert (rg.csr_plan.chunk_sched is not None) == (order == "source")
     rng = np.random.default_rng(1)
     feat = rng.standard_normal((N, F)).astype(np.float32)
     ew = (rng.uniform(-0.5, 1.5, (R, 1)) / 100.0).astype(np.float32)
@@ -60,11 +63,12 @@ def test_regraphconv_long_rows(split, chunk, F):
         assert ok, f"{tag} (split={split}, chunk={chunk}, levels={rg.csr_plan.n_levels}): {err:.3e}"
 
 
-def test_tree_levels_and_determinism():
+@pytest.mark.parametrize("order", ["edge", "source"])
+def test_tree_levels_and_determinism(order):
     from layer import REGraphConv
     from regnn_hip.graph import RelGraph
     src, dst, rel, N, R = power_graph(hub_edges=70000)
-    rg = RelGraph(src, dst, N, DEV, split=8, chunk=4)
+    rg = RelGraph(src, dst, N, DEV, split=8, chunk=4, order=order)
     assert rg.csr_plan.n_levels >= 3, rg.csr_plan.n_levels
     rng = np.random.default_rng(2)
     x0 = torch.from_numpy(rng.standard_normal((N, 64)).astype(np.float32)).to(DEV)
