@@ -168,21 +168,24 @@ __device__ __forceinline__ void head_tail(f32x4 (&acc)[NT], int64_t node, int64_
     if (node < n_loss) {
         float* pr = p + node * ld + 4 * q;
         const float r = scale / se;
+        if (p) {                               // kernel-uniform (null: regnn_head_fwd_lse)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f32x4 v = acc[t] * r;
-            if ((t + 1 < NT || padded || 16 * t + 16 <= C)) {
-                *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
-            } else {
+            for (int t = 0; t < NT; ++t) {
+                const f32x4 v = acc[t] * r;
+                if ((t + 1 < NT || padded || 16 * t + 16 <= C)) {
+                    *reinterpret_cast<f32x4_u*>(pr + 16 * t) = v;
+                } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
+                    for (int i = 0; i < 4; ++i)
+                        if (16 * t + 4 * q + i < C) pr[16 * t + i] = v[i];
+                }
             }
         }
         const int yq = y - 4 * q;              // the label's slot in this lane's tiles
         if (yq >= 0 && (yq & 15) < 4) {        // same lane, same address: ordered after
             loss_rows[node] = lse - zy;
-            p[node * ld + y] = __expf(zy - m) * r - scale;
+            if (p) p[node * ld + y] = __expf(zy - m) * r - scale;
+            else loss_rows[n_loss + node] = lse;   // regnn_head_fwd_lse: [2, n] loss | lse
         }
     }
 }
@@ -540,13 +543,30 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, const 
 // over 32-class chunks, A = W^T rows (feature 16 kt + c; three bf16 splits in LDS, rows of
 // CP32 + 8 bf16: 16-byte aligned, the 16 feature rows of a b128 read on disjoint banks), B = the
 // lane's p row (classes 32 ch + 8 q .. +7, split on the fly). 4 waves per SIMD (~70 VGPRs).
-template <int NT>
+// ZP ("p from z", regnn_head_bwd_z): the operand pointer holds the logits rows z instead of p,
+// and p = scale (exp(z - lse) - [class == label]) is formed on the fly from the per-row lse of
+// regnn_head_fwd_lse, so the forward never writes p (the n x C fp32 rows it would store and these
+// kernels read back are the logits rows the caller gets anyway).
+struct PSrc {
+    const float* lse;
+    const int64_t* labels;
+    float scale;
+};
+constexpr float kLog2e = 1.4426950408889634f;
+
+// p = scale (exp(z - lse) - [label]) with zl2 = lse log2(e): one FMA into v_exp_f32, one FMA out
+__device__ __forceinline__ float zp_val(float z, float zl2, bool is_label, float scale) {
+    const float e = __builtin_amdgcn_exp2f(fmaf(z, kLog2e, -zl2));
+    return fmaf(e, scale, is_label ? -scale : 0.f);
+}
+
+template <int NT, bool ZP = false>
 __global__ void __launch_bounds__(kGhBlock)
 head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
                   const float* __restrict__ W,
                   const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out,
                   const float* __restrict__ nx_scale, const float* __restrict__ hx,
-                  float* __restrict__ nx_out, float* __restrict__ nx_dot) {
+                  float* __restrict__ nx_out, float* __restrict__ nx_dot, PSrc ps) {
     constexpr int K = kHeadK, NCH = (NT + 1) / 2, CP32 = 32 * NCH, LDR = CP32 + 8;
     extern __shared__ uint16_t Wt[];                       // [3][K][LDR] bf16
     for (int idx = threadIdx.x; idx < CP32 * K; idx += blockDim.x) {
@@ -563,6 +583,8 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
     const int wpb = blockDim.x >> 6;
     const int64_t n_tiles = (n + 15) / 16;
     const uint16_t* wa = Wt + c * LDR + 8 * q;             // + (s K + 16 kt) LDR + 32 ch
+    float zl = 0.f;                                        // ZP: the lane row's lse, label
+    int zy = -1;
     auto load_p = [&](const float* pr, int ch, float (&v)[8]) {
         const int cls0 = 32 * ch + 8 * q;
         if (cls0 + 8 <= C) {
@@ -570,9 +592,17 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
             const f32x4 x1 = *reinterpret_cast<const f32x4_u*>(pr + cls0 + 4);
 #pragma unroll
             for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
+            if constexpr (ZP) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = zp_val(v[i], zl, cls0 + i == zy, ps.scale);
+            }
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = cls0 + i < C ? pr[cls0 + i] : 0.f;
+            for (int i = 0; i < 8; ++i) {
+                float x = cls0 + i < C ? pr[cls0 + i] : 0.f;
+                if constexpr (ZP) x = cls0 + i < C ? zp_val(x, zl, cls0 + i == zy, ps.scale) : 0.f;
+                v[i] = x;
+            }
         }
     };
     for (int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); tile < n_tiles;
@@ -580,6 +610,10 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
         const int64_t row = tile * 16 + c;
         const bool valid = row < n;
         const float* pr = p + (valid ? row : n - 1) * ld;
+        if constexpr (ZP) {
+            zl = ps.lse[valid ? row : n - 1] * kLog2e;
+            zy = (int)ps.labels[valid ? row : n - 1];
+        }
         f32x4 acc[4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -724,10 +758,11 @@ head_wgrad_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, con
 // (class tile t, 64-feature block fb) go to waves round-robin (u = w + 8 m): the output head
 // (C = 349, K = 64) gives a wave class tiles w, w + 8, w + 16; an input projection's d weight
 // (C = 64 outputs, K = 128 inputs) one (tile, block) pair per wave.
-template <typename TP, typename TH, int NT, int KH>
+template <typename TP, typename TH, int NT, int KH, bool ZP = false>
 __global__ void __launch_bounds__(kHeadBlock)
 wgrad_x6_kernel(const TP* __restrict__ p, int64_t n, int C, int64_t ld,
-                const TH* __restrict__ h, int64_t rows_per_block, float* __restrict__ slab) {
+                const TH* __restrict__ h, int64_t rows_per_block, float* __restrict__ slab,
+                PSrc ps) {
     constexpr int KB = KH / 64, NU = NT * KB, MU = (NU + 7) / 8, CP = NT * 16;
     constexpr bool EXACT = sizeof(TP) == 2 && sizeof(TH) == 2;   // bf16 x bf16: one product
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
@@ -754,12 +789,19 @@ wgrad_x6_kernel(const TP* __restrict__ p, int64_t n, int C, int64_t ld,
             const int64_t rr = row0 + 8 * q + j;
             const bool ok = rr < r1;
             const int64_t rc = ok ? rr : r0;
+            float zl = 0.f;
+            int zy = -1;
+            if constexpr (ZP) {
+                zl = ps.lse[rc] * kLog2e;
+                zy = (int)ps.labels[rc];
+            }
 #pragma unroll
             for (int m = 0; m < MU; ++m) {
                 const int u = w + 8 * m, t = u % NT, fb = u / NT;
                 const int cls = 16 * t + c;
                 const bool in = ok && u < NU && cls < C;
-                const float v = ld_p(rc * ld + (cls < C ? cls : 0));
+                float v = ld_p(rc * ld + (cls < C ? cls : 0));
+                if constexpr (ZP) v = zp_val(v, zl, cls == zy, ps.scale);
                 a[m][j] = in ? v : 0.f;
                 if (KB > 1 || m == 0) {
 #pragma unroll
@@ -820,9 +862,9 @@ wgrad_x6_kernel(const TP* __restrict__ p, int64_t n, int C, int64_t ld,
 }
 
 // slab rows for n rows of p: grid blocks of >= 256 rows, one slab row each (<= slab_rows)
-template <typename TP, typename TH, int NT, int KH>
+template <typename TP, typename TH, int NT, int KH, bool ZP = false>
 int launch_wgrad_x6(const TP* p, int64_t n, int C, int64_t ld, const TH* h, float* slab,
-                    int slab_rows, hipStream_t stream) {
+                    int slab_rows, hipStream_t stream, PSrc ps = PSrc{nullptr, nullptr, 0.f}) {
     int64_t grid = slab_rows;
     const int64_t rpb_min = 256;
     if (grid * rpb_min > n) grid = (n + rpb_min - 1) / rpb_min;
@@ -831,8 +873,8 @@ int launch_wgrad_x6(const TP* p, int64_t n, int C, int64_t ld, const TH* h, floa
     rpb = (rpb + 31) / 32 * 32;
     grid = (n + rpb - 1) / rpb;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((wgrad_x6_kernel<TP, TH, NT, KH>), dim3((unsigned)grid), dim3(kHeadBlock),
-                       0, stream, p, n, C, ld, h, rpb, slab);
+    hipLaunchKernelGGL((wgrad_x6_kernel<TP, TH, NT, KH, ZP>), dim3((unsigned)grid),
+                       dim3(kHeadBlock), 0, stream, p, n, C, ld, h, rpb, slab, ps);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
@@ -842,9 +884,36 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
                     hipStream_t stream, const float* nx_scale = nullptr,
                     const float* hx = nullptr, float* nx_out = nullptr,
-                    float* nx_dot = nullptr) {
+                    float* nx_dot = nullptr, PSrc ps = PSrc{nullptr, nullptr, 0.f}) {
     constexpr int K = kHeadK;
     if (nx_scale && !gh) return REGNN_EINVAL;
+    if (ps.lse) {                                  // p from the logits rows: bf16x6 kernels only
+        if (gh) {
+            constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
+            static bool attrz = false;
+            if (!attrz) {
+                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_gh_x6_kernel<NT, true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds) != hipSuccess)
+                    return REGNN_ELAUNCH;
+                attrz = true;
+            }
+            const int64_t tiles = (n + 15) / 16;
+            int64_t grid = (tiles + kGhBlock / 64 - 1) / (kGhBlock / 64);
+            const int cap = resident_blocks(
+                reinterpret_cast<const void*>(&head_gh_x6_kernel<NT, true>), lds, kGhBlock);
+            if (grid > cap) grid = cap;
+            if (grid < 1) grid = 1;
+            hipLaunchKernelGGL((head_gh_x6_kernel<NT, true>), dim3((unsigned)grid),
+                               dim3(kGhBlock), lds, stream, p, n, C, ld, W, gscale, gh, n_out,
+                               nx_scale, hx, nx_out, nx_dot, ps);
+            REGNN_LAUNCH_CHECK();
+        }
+        if (slab)
+            return launch_wgrad_x6<float, float, NT, kHeadK, true>(p, n, C, ld, h, slab,
+                                                                  slab_rows, stream, ps);
+        return REGNN_OK;
+    }
     if (gh && (g_tune_head != 16 || nx_scale)) {   // bf16x6 gh (default)
         constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
         static bool attr6 = false;
@@ -863,7 +932,7 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
         if (grid < 1) grid = 1;
         hipLaunchKernelGGL((head_gh_x6_kernel<NT>), dim3((unsigned)grid), dim3(kGhBlock), lds,
                            stream, p, n, C, ld, W, gscale, gh, n_out, nx_scale, hx, nx_out,
-                           nx_dot);
+                           nx_dot, ps);
         REGNN_LAUNCH_CHECK();
     } else if (gh) {
         const size_t lds = (size_t)K * (NT * 16 + 1) * sizeof(float);
@@ -1342,6 +1411,52 @@ int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, 
     }
 }
 
+int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+                       int32_t C, int64_t ld, const int64_t* labels, int64_t n_loss,
+                       float* logits, float* loss_lse, hipStream_t stream) {
+    if (!h || !W || !logits || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C ||
+        n_loss < 0 || n_loss > rows || (n_loss > 0 && (!labels || !loss_lse)) ||
+        (reinterpret_cast<uintptr_t>(h) & 15))
+        return REGNN_EINVAL;
+    if (rows == 0) return REGNN_OK;
+    switch ((C + 15) / 16) {
+#define HEAD_CASE(nt) \
+        case nt: return launch_head<nt>(h, rows, W, b, C, ld, labels, n_loss, 1.f, logits,      \
+                                        nullptr, loss_lse, stream);
+        HEAD_CASE(1) HEAD_CASE(2) HEAD_CASE(3) HEAD_CASE(4) HEAD_CASE(5) HEAD_CASE(6)
+        HEAD_CASE(7) HEAD_CASE(8) HEAD_CASE(9) HEAD_CASE(10) HEAD_CASE(11) HEAD_CASE(12)
+        HEAD_CASE(13) HEAD_CASE(14) HEAD_CASE(15) HEAD_CASE(16) HEAD_CASE(17) HEAD_CASE(18)
+        HEAD_CASE(19) HEAD_CASE(20) HEAD_CASE(21) HEAD_CASE(22) HEAD_CASE(23) HEAD_CASE(24)
+#undef HEAD_CASE
+        default: return REGNN_EINVAL;
+    }
+}
+int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K,
+                     const float* W, const float* h, const float* gscale, float* gh,
+                     int64_t n_out, float* slab, int32_t slab_rows, const float* lse,
+                     const int64_t* labels, float scale, const float* nx_scale, float* nx_out,
+                     float* nx_dot, hipStream_t stream) {
+    if (!z || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C || (gh && !W) ||
+        (gh && n_out < n) || (slab && (!h || slab_rows <= 0)) || (n > 0 && (!lse || !labels)) ||
+        (nx_scale && (!gh || !h || !nx_out || !nx_dot)) ||
+        ((reinterpret_cast<uintptr_t>(gh) | reinterpret_cast<uintptr_t>(nx_out) |
+          (nx_scale ? reinterpret_cast<uintptr_t>(h) : 0)) & 15))
+        return REGNN_EINVAL;
+    if (n == 0 && !(gh && n_out > 0)) return REGNN_OK;
+    const PSrc ps{lse, labels, scale};
+    switch ((C + 15) / 16) {
+#define HB_CASE(nt) \
+        case nt: return launch_head_bwd<nt>(z, n, C, ld, W, h, gscale, gh, n_out, slab,      \
+                                            slab_rows, stream, nx_scale,                      \
+                                            nx_scale ? h : nullptr, nx_out, nx_dot, ps);
+        HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
+        HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
+        HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)
+        HB_CASE(19) HB_CASE(20) HB_CASE(21) HB_CASE(22) HB_CASE(23) HB_CASE(24)
+#undef HB_CASE
+        default: return REGNN_EINVAL;
+    }
+}
 int regnn_head_gh_next(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K,
                        const float* W, const float* gscale, float* gh, int64_t n_out,
                        const float* nx_scale, const float* h, float* nx_out, float* nx_dot,

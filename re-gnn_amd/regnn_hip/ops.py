@@ -10,6 +10,7 @@ math (LeakyReLU of the relation embedding) and dense projections.
 * head_spmm(rg, a, ft)                         layer/REGATConv.py:90-91
 """
 import ctypes
+import os
 
 import torch
 
@@ -785,13 +786,23 @@ class _HeadCE(torch.autograd.Function):
             # rows padded to 16 classes (64-byte aligned): logits is a [rows, C] view of it
             ld = 16 * ((C + 15) // 16)
             logits = torch.empty(h.shape[0], ld, dtype=torch.float32, device=dev)[:, :C]
-            p = torch.empty(n, ld, dtype=torch.float32, device=dev)[:, :C]
-            nbytes = 4 * (h.numel() + h.shape[0] * C + n * C + n) + 8 * n
-            with timed("head_fwd", nbytes):
-                L.call("regnn_head_fwd", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc),
-                       L.ptr(b.detach().contiguous()) if b is not None else None, C, ld,
-                       L.ptr(lab), n, 1.0 / n, L.ptr(logits), L.ptr(p), L.ptr(loss_rows),
-                       L.stream())
+            bp = L.ptr(b.detach().contiguous()) if b is not None else None
+            if HEAD["p"] == "z":
+                # no p rows: the backward re-forms them from these logits rows and the lse
+                buf = torch.empty(2, n, dtype=torch.float32, device=dev)
+                loss_rows = buf[0]
+                p = None
+                with timed("head_fwd", 4 * (h.numel() + h.shape[0] * C + 2 * n) + 8 * n):
+                    L.call("regnn_head_fwd_lse", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc),
+                           bp, C, ld, L.ptr(lab), n, L.ptr(logits), L.ptr(buf), L.stream())
+                ctx.zsrc = (logits, logits._version, buf[1], lab)
+            else:
+                p = torch.empty(n, ld, dtype=torch.float32, device=dev)[:, :C]
+                nbytes = 4 * (h.numel() + h.shape[0] * C + n * C + n) + 8 * n
+                with timed("head_fwd", nbytes):
+                    L.call("regnn_head_fwd", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc), bp,
+                           C, ld, L.ptr(lab), n, 1.0 / n, L.ptr(logits), L.ptr(p),
+                           L.ptr(loss_rows), L.stream())
         else:
             p = torch.empty(n, C, dtype=torch.float32, device=dev)
             logits = torch.addmm(b, h, W.t()) if b is not None else h @ W.t()
@@ -800,6 +811,8 @@ class _HeadCE(torch.autograd.Function):
                        1.0 / n, L.ptr(p), L.ptr(loss_rows), L.stream())
         loss = loss_rows.sum() / n
         ctx.save_for_backward(h, W, p)
+        ctx.n, ctx.C = n, C
+        ctx.bias = b.detach() if b is not None else None
         ctx.has_bias = b is not None
         # h straight from an aggregation (re_spmm): its backward row pass rides on gh's kernel
         ctx.link = getattr(h, "_regnn_link", None) if h.dtype == torch.float32 else None
@@ -809,13 +822,26 @@ class _HeadCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _g_logits, g_loss):
         h, W, p = ctx.saved_tensors
-        n, C = p.shape
+        n, C = ctx.n, ctx.C
         K = h.shape[1]
         gh = gW = gb = None
         if g_loss is None:
             return None, None, None, None
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        zsrc = getattr(ctx, "zsrc", None)
+        if zsrc is not None:
+            z, ver, lse, lab = zsrc
+            ctx.zsrc = None
+            if z._version == ver:
+                return _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b)
+            # the caller modified the logits in place: re-form p from h (the stored-p path)
+            zf = torch.addmm(ctx.bias, h[:n], W.detach().t()) if ctx.bias is not None else \
+                h[:n] @ W.detach().t()
+            p = torch.empty(n, C, dtype=torch.float32, device=h.device)
+            lr = torch.empty(n, dtype=torch.float32, device=h.device)
+            L.call("regnn_softmax_xent", L.ptr(zf), n, C, zf.stride(0), L.ptr(lab), 1.0 / n,
+                   L.ptr(p), L.ptr(lr), L.stream())
         if head_fused(K, C) and h.dtype == torch.float32:
             # regnn_head_bwd: gh = g_loss * p W (rows >= n zero-filled in the same launch) and
             # the (p^T h | colsum p) slab, each kernel reading p once (fp32 MFMA)
@@ -864,6 +890,49 @@ class _HeadCE(torch.autograd.Function):
         if need_b:
             gb = col_sum(p) * g_loss
         return gh, gW, gb, None
+
+
+# "z": regnn_head_fwd_lse stores no p rows, the backward kernels re-form p from the logits rows
+# (regnn_head_bwd_z); "p": p stored by the forward and read back (regnn_head_fwd / _bwd)
+HEAD = {"p": os.environ.get("REGNN_HEAD_P", "z")}
+
+
+def _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b):
+    """_HeadCE.backward from the logits rows z [n, C] (stride ld) and their lse."""
+    n, C = ctx.n, ctx.C
+    K = h.shape[1]
+    gh = gW = gb = None
+    Cp = 16 * ((C + 15) // 16)
+    rows = 2048
+    hc = h.contiguous()
+    zp, ld = L.ptr(z), z.stride(0)
+    if need_h:
+        gh = torch.empty_like(h)
+        gl = g_loss.detach().reshape(1).float().contiguous()
+        nx = ctx.link
+        nx_args = (None, None, None)
+        if nx is not None and nx.post.numel() == h.shape[0] and PRESCALE["next"] != "off":
+            nx_out = torch.empty_like(h)
+            nx_dot = torch.empty(h.shape[0], dtype=torch.float32, device=h.device)
+            nx_args = (L.ptr(nx.post), L.ptr(nx_out), L.ptr(nx_dot))
+        with timed("head_gh", 4 * (n * C + h.numel())):
+            L.call("regnn_head_bwd_z", zp, n, C, ld, K, L.ptr(W.detach().contiguous()),
+                   L.ptr(hc), L.ptr(gl), L.ptr(gh), h.shape[0], None, 0, L.ptr(lse),
+                   L.ptr(lab), 1.0 / n, *nx_args, L.stream())
+        if nx_args[0] is not None:
+            nx.handoff = (gh, gh._version, nx_out, nx_dot)
+    if need_w or need_b:
+        slab = torch.zeros(rows, Cp * K + Cp, dtype=torch.float32, device=h.device)
+        with timed("head_bwd", 4 * (n * C + n * K)):
+            L.call("regnn_head_bwd_z", zp, n, C, ld, K, None, L.ptr(hc), None, None, 0,
+                   L.ptr(slab), rows, L.ptr(lse), L.ptr(lab), 1.0 / n, None, None, None,
+                   L.stream())
+        tot = _reduce(slab, Cp * K + Cp)
+        if need_w:
+            gW = tot[:Cp * K].view(Cp, K)[:C] * g_loss
+        if need_b:
+            gb = tot[Cp * K:Cp * K + C] * g_loss
+    return gh, gW, gb, None
 
 
 def head_argmax(h, weight, bias=None):

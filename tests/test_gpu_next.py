@@ -203,11 +203,14 @@ def test_regcn_chained_matches_unchained(train, dtype):
         assert rel(g1[k], g0[k]) <= (1e-4 if dtype == torch.float32 else 2e-2), k
 
 
+@pytest.mark.parametrize("mode", ["z", "p"])
 @pytest.mark.parametrize("n_loss", [333, 900])
-def test_head_gh_handoff(n_loss, monkeypatch):
-    """regnn_head_gh_next: the output head's gh kernel forms the last aggregation's pre-scaled
-    gradient rows (zero rows without a loss term); gradients equal the row-pass path."""
+def test_head_gh_handoff(n_loss, mode, monkeypatch):
+    """regnn_head_gh_next / regnn_head_bwd_z: the output head's gh kernel forms the last
+    aggregation's pre-scaled gradient rows (zero rows without a loss term); gradients equal the
+    row-pass path, with p stored (p) or re-formed from the logits rows (z)."""
     from regnn_hip import ops
+    monkeypatch.setitem(ops.HEAD, "p", mode)
     from regnn_hip.graph import RelGraph
     taken = []
     orig = ops._NextLink.take

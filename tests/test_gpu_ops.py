@@ -137,9 +137,12 @@ def test_rel_reduce_wide(rows, width, accumulate):
                                      (300, 64, 33, 31),     # C just past one tile
                                      (640, 32, 349, 100),       # K != 64: GEMM + softmax_xent
                                      (200_000, 64, 349, 150_000)])  # many rows per wgrad block
-def test_head_ce_matches_autograd(bias, N, D, C, n):
-    """ops.head_ce == out_lin over all rows + cross_entropy(logits[:n], y) (run_regnn.py:146-148)."""
+@pytest.mark.parametrize("mode", ["z", "p"])
+def test_head_ce_matches_autograd(bias, N, D, C, n, mode, monkeypatch):
+    """ops.head_ce == out_lin over all rows + cross_entropy(logits[:n], y) (run_regnn.py:146-148),
+    with p re-formed from the logits rows in the backward (z, the default) or stored (p)."""
     from regnn_hip import ops
+    monkeypatch.setitem(ops.HEAD, "p", mode)
     torch.manual_seed(0)
     h0 = torch.randn(N, D, device=DEV)
     W0 = torch.randn(C, D, device=DEV) * 0.1
@@ -158,6 +161,32 @@ def test_head_ce_matches_autograd(bias, N, D, C, n):
     assert _rel(h.grad, hr.grad) < 1e-5 and _rel(W.grad, Wr.grad) < 1e-5
     if bias:
         assert _rel(b.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C,n", [(349, 1500), (40, 7)])
+def test_head_ce_logits_modified_in_place(C, n):
+    """z mode re-forms p from the logits rows it returned: a caller that overwrites them before
+    backward must still get the gradients of the loss it was given (the op recomputes p from h)."""
+    from regnn_hip import ops
+    assert ops.HEAD["p"] == "z"
+    torch.manual_seed(3)
+    N = 3000
+    h0, W0, b0 = torch.randn(N, 64, device=DEV), torch.randn(C, 64, device=DEV) * 0.1, \
+        torch.randn(C, device=DEV) * 0.1
+    y = torch.randint(0, C, (n,), device=DEV)
+    grads = []
+    for clobber in (False, True):
+        h, W, b = (t.clone().requires_grad_(True) for t in (h0, W0, b0))
+        logits, loss = ops.head_ce(h, W, b, y)
+        if clobber:
+            logits.mul_(0.0).add_(7.0)
+        loss.backward()
+        grads.append((h.grad, W.grad, b.grad))
+    hr, Wr, br = (t.double().requires_grad_(True) for t in (h0, W0, b0))
+    torch.nn.functional.cross_entropy((hr @ Wr.t() + br)[:n], y).backward()
+    for got in grads:
+        assert _rel(got[0], hr.grad) < 1e-5 and _rel(got[1], Wr.grad) < 1e-5
+        assert _rel(got[2], br.grad) < 1e-5
 
 
 @pytest.mark.parametrize("N,H,D", [(1000, 8, 64), (77, 1, 3), (300, 4, 20)])
