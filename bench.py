@@ -391,6 +391,10 @@ def main():
                             f"data-parallel x{world} over per-rank graph shards "
                             f"(RCCL grad all-reduce)"),
             "hip_graph": use_graph,
+            # the last aggregation's backward gathers only the CSC edges into loss rows (the
+            # output head's gradient is exactly zero elsewhere; ops.PRESCALE["prefix"])
+            "last_layer_bwd_edges": (min(p.E for p in rg._prefix.values())
+                                     if getattr(rg, "_prefix", None) else None),
         },
         "roofline": {
             "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -104,6 +104,25 @@ def _word_padded(r):
     return buf[:r.numel()]
 
 
+class CscPrefix:
+    """The CSC restricted to edges whose destination is < n (rows kept in their order): the
+    backward of an aggregation whose incoming gradient is zero on destination rows >= n (the
+    last REGCN layer under the output head, whose loss covers the first n rows) gathers only
+    these edges. Every skipped edge would add tab * pre * 0 to its source's sum."""
+
+    def __init__(self, rg, n):
+        keep = rg.csc_idx < n
+        ck = torch.cat([keep.new_zeros(1, dtype=torch.int64), torch.cumsum(keep, 0)])
+        self.n = int(n)
+        self.keep = keep
+        self.csc_ptr = ck[rg.csc_ptr.to(torch.int64)].to(torch.int32).contiguous()
+        self.csc_idx = rg.csc_idx[keep].contiguous()
+        self.E = int(self.csc_idx.numel())
+        srt = rg.order == "source"
+        split, chunk = rg._split
+        self.csc_plan = SegPlan(self.csc_ptr, split, chunk, self.csc_idx if srt else None)
+
+
 class RelPack:
     """Relation ids of one e_feat tensor laid out for both orientations (+ long-row counts)."""
 
@@ -121,7 +140,15 @@ class RelPack:
         self.rel_csr = _word_padded(r[rg.csr_eid])
         self.rel_csc = _word_padded(r[rg.csc_eid])
         self._cnt = {}
+        self._csc_prefix = {}
         self.rg = rg
+
+    def rel_csc_prefix(self, pre):
+        """rel_csc restricted to a CscPrefix's edges (cached per prefix)."""
+        r = self._csc_prefix.get(pre.n)
+        if r is None:
+            r = self._csc_prefix[pre.n] = _word_padded(self.rel_csc[pre.keep])
+        return r
 
     def long_cnt(self, n_rel):
         """[n_long, n_rel] int32 relation histogram of every long CSR row."""
@@ -179,6 +206,20 @@ class RelGraph:
         self.csc_plan = SegPlan(self.csc_ptr, split, chunk, self.csc_idx if srt else None)
         self._packs = {}
         self._inv_cnt = None
+        self._split = (split, chunk)
+        self._prefix = {}
+
+    def csc_prefix(self, n):
+        """CscPrefix of the destinations [0, n) (cached; None when it would keep every edge)."""
+        n = int(n)
+        if n >= self.n_dst:
+            return None
+        pre = self._prefix.get(n)
+        if pre is None:
+            if len(self._prefix) > 2:
+                self._prefix.clear()
+            pre = self._prefix[n] = CscPrefix(self, n)
+        return pre
 
     def _ptr(self, keys, n):
         cnt = torch.bincount(keys, minlength=n)

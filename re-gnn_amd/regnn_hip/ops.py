@@ -144,7 +144,9 @@ def drop_request(p, device, seed=None):
 # Forward pre-scale policy of _ReSpmm: "auto" | "on" | "off" (tools/ab_spmm.py flips it).
 # "on": pre * drop(x) is formed once per source row by regnn_row_scale and the aggregation
 # gathers the finished rows; "off": the gather scales and masks every edge's row itself.
-PRESCALE = {"mode": "auto", "bwd": "auto", "next": "auto"}
+# "prefix": an aggregation backward whose gradient is known zero past row n (the output head's
+# hand-off) gathers only the CSC edges into rows < n ("off": the whole CSC)
+PRESCALE = {"mode": "auto", "bwd": "auto", "next": "auto", "prefix": "auto"}
 
 
 def _use_prescale(x, scale, drop, backward=False):
@@ -166,7 +168,10 @@ class _NextLink:
     the producer's backward needs post' * g' and <g', y'> / post' for g' = d loss / d y' = the
     consumer's gx. The consumer's backward forms both in its epilogue (regnn_spmm_bwd_next) and
     parks them here; the producer's backward takes them only if its incoming gradient IS that gx
-    tensor, unmodified (autograd summed nothing into it), and runs its own row pass otherwise."""
+    tensor, unmodified (autograd summed nothing into it), and runs its own row pass otherwise.
+    The hand-off's last field, when not None, is a row count n such that the gradient is zero on
+    rows >= n (the output head's loss rows): the producer's transposed gather then runs over the
+    CSC prefix of edges into rows < n (RelGraph.csc_prefix)."""
 
     __slots__ = ("post", "handoff")
 
@@ -178,10 +183,10 @@ class _NextLink:
         h, self.handoff = self.handoff, None
         if h is None:
             return None
-        gx, version, nx_out, nx_dot = h
+        gx, version, nx_out, nx_dot, nz = h
         if gy is not gx or gy._version != version:
             return None
-        return nx_out, nx_dot
+        return nx_out, nx_dot, nz
 
 
 def _drop_args(drop):
@@ -253,7 +258,6 @@ class _ReSpmm(torch.autograd.Function):
             node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
         elif need_pre:
             node = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
-        plan_args, part = _plan_args(rg.csc_plan, F, x.device)
         # output-side norm gradient <g, y> / post: same-scale node term or d loss / d post
         want_dot = (ctx.same_scale and node is not None) or (not ctx.same_scale and need_post)
         prescale = post is not None and _use_prescale(x, post, None, backward=True)
@@ -263,7 +267,17 @@ class _ReSpmm(torch.autograd.Function):
         # the consumer of x (the next aggregation) forms its producer's pre-scaled gradient rows
         nx = ctx.link_in if (need_x and ctx.link_in is not None and
                              ctx.link_in.post.numel() == rg.n_src) else None
-        with timed("spmm_bwd", spmm_bytes(rg.E, rg.n_dst, rg.n_src, F, x.element_size(),
+        # gradient rows >= nz known zero (hand-off from the output head): gather only the CSC
+        # edges into rows < nz; the skipped edges' terms are exact zeros
+        pre_g = rg.csc_prefix(handed[2]) if (handed is not None and handed[2] is not None and
+                                             PRESCALE["prefix"] != "off") else None
+        csc_ptr, csc_idx, csc_plan, E_b = (rg.csc_ptr, rg.csc_idx, rg.csc_plan, rg.E) \
+            if pre_g is None else (pre_g.csc_ptr, pre_g.csc_idx, pre_g.csc_plan, pre_g.E)
+        rel_csc = None
+        if pack is not None and t is not None:
+            rel_csc = pack.rel_csc if pre_g is None else pack.rel_csc_prefix(pre_g)
+        plan_args, part = _plan_args(csc_plan, F, x.device)
+        with timed("spmm_bwd", spmm_bytes(E_b, rg.n_dst, rg.n_src, F, x.element_size(),
                                           "spmm_bwd")):
             if handed is not None:
                 # post * g and <g, y> / post came from the consumer's backward epilogue
@@ -278,8 +292,7 @@ class _ReSpmm(torch.autograd.Function):
                 L.call("regnn_row_scale", L.ptr(gy), L.ptr(post), L.ptr(src), rg.n_dst, F,
                        L.dtype_code(x), None, 0, 1.0, L.ptr(y if want_dot else None), L.ptr(dot),
                        L.stream())
-            args = (L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
-                    L.ptr(pack.rel_csc if (pack is not None and t is not None) else None),
+            args = (L.ptr(csc_ptr), L.ptr(csc_idx), L.ptr(rel_csc),
                     L.ptr(t), None, L.ptr(in_scale), L.ptr(pre), L.ptr(src), L.ptr(x),
                     L.ptr(y if ctx.same_scale and node is not None and not prescale else None),
                     L.ptr(gx), L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F,
@@ -289,7 +302,7 @@ class _ReSpmm(torch.autograd.Function):
                 nx_dot = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
                 L.call("regnn_spmm_bwd_next", *args, *(_drop_args(drop)),
                        L.ptr(nx.post), L.ptr(nx_out), L.ptr(nx_dot), L.stream())
-                nx.handoff = (gx, gx._version, nx_out, nx_dot)
+                nx.handoff = (gx, gx._version, nx_out, nx_dot, None)
             elif drop is None:
                 L.call("regnn_spmm_bwd", *args, L.stream())
             else:
@@ -864,7 +877,7 @@ class _HeadCE(torch.autograd.Function):
                                L.ptr(W.detach().contiguous()), L.ptr(gl), L.ptr(gh),
                                h.shape[0], L.ptr(nx.post), L.ptr(hc), L.ptr(nx_out),
                                L.ptr(nx_dot), L.stream())
-                    nx.handoff = (gh, gh._version, nx_out, nx_dot)
+                    nx.handoff = (gh, gh._version, nx_out, nx_dot, n)
                 else:
                     with timed("head_gh", 4 * (p.numel() + h.numel())):
                         L.call("regnn_head_bwd", L.ptr(p), n, C, p.stride(0), K,
@@ -920,7 +933,7 @@ def _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b):
                    L.ptr(hc), L.ptr(gl), L.ptr(gh), h.shape[0], None, 0, L.ptr(lse),
                    L.ptr(lab), 1.0 / n, *nx_args, L.stream())
         if nx_args[0] is not None:
-            nx.handoff = (gh, gh._version, nx_out, nx_dot)
+            nx.handoff = (gh, gh._version, nx_out, nx_dot, n)
     if need_w or need_b:
         slab = torch.zeros(rows, Cp * K + Cp, dtype=torch.float32, device=h.device)
         with timed("head_bwd", 4 * (n * C + n * K)):

@@ -48,3 +48,33 @@ def test_source_order_layout_and_chunk_schedule():
     fs = rg.csr_idx[first]
     assert bool((fs[1:] >= fs[:-1]).all())
     assert RelGraph(src, dst, N, "cpu", split=16, chunk=8).csr_plan.chunk_sched is None
+
+
+def test_csc_prefix_keeps_edges_into_leading_rows():
+    """RelGraph.csc_prefix(n): per source, exactly the CSC edges with destination < n, in their
+    CSC order, with the relation ids of those edges and a split plan of the shortened rows (the
+    backward under the output head's zero gradient rows >= n, ops._ReSpmm)."""
+    import numpy as np
+    import torch
+    from regnn_hip.graph import RelGraph
+    rng = np.random.default_rng(1)
+    N, E, n = 300, 6000, 120
+    src = np.where(rng.random(E) < 0.4, 5, rng.integers(0, N, E))        # one long CSC row
+    dst = rng.integers(0, N, E)
+    rel = rng.integers(1, 8, E)
+    for order in ("edge", "source"):
+        rg = RelGraph(src, dst, N, "cpu", split=16, chunk=8, order=order)
+        pack = rg.rel_pack(torch.from_numpy(rel), num_rel=7)
+        pre = rg.csc_prefix(n)
+        assert rg.csc_prefix(N) is None and rg.csc_prefix(n) is pre
+        rc = pack.rel_csc_prefix(pre)
+        assert pre.E == int((dst < n).sum()) == rc.numel()
+        for u in range(N):
+            a, b = int(rg.csc_ptr[u]), int(rg.csc_ptr[u + 1])
+            m = rg.csc_idx[a:b] < n
+            a2, b2 = int(pre.csc_ptr[u]), int(pre.csc_ptr[u + 1])
+            assert torch.equal(pre.csc_idx[a2:b2], rg.csc_idx[a:b][m])
+            assert torch.equal(rc[a2:b2], pack.rel_csc[a:b][m])
+        deg = pre.csc_ptr.diff()
+        assert torch.equal(pre.csc_plan.long_ids.to(torch.int64), torch.nonzero(deg > 16).flatten())
+        assert (pre.csc_plan.chunk_sched is not None) == (order == "source")
