@@ -119,7 +119,7 @@ def build_workload(args, dev):
         # run_regnn.py:146-150: logits = net(...) over all nodes, CE on the train rows, backward,
         # Adam. ops.head_ce computes the same logits / loss / gradients without the all-rows
         # zero-filled logits gradient (tests/test_gpu_ops.py::test_head_ce checks it vs autograd)
-        _, loss = ops.head_ce(net.embed(feats, e_feat).float(), W, b, labels)
+        _, loss = ops.head_ce(net.embed(feats, e_feat), W, b, labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if world > 1:

@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 13). */
+/* ABI version (bumped on any signature change or addition; currently 14). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -347,13 +347,16 @@ int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, 
 /* regnn_head_bwd / regnn_head_gh_next from the logits rows z [n, C] (row stride ld) of
  * regnn_head_fwd_lse instead of a stored p: p[r, c] = scale * (exp(z[r, c] - lse[r]) - [c ==
  * labels[r]]) is formed on the fly inside the gh and slab kernels (bf16x6 MFMA). gh, slab and
- * (nx_scale, nx_out, nx_dot) have the meaning of those calls; h feeds both the slab (p^T h) and
- * the nx dot. Either part may be NULL. */
+ * (nx_scale, nx_out, nx_dot) have the meaning of those calls; h (fp32 [n, K]) feeds the slab
+ * (p^T h), hx (the head input as the aggregation stored it, dtype) the nx dot. gh, hx and nx_out
+ * are stored in dtype (REGNN_F32: 16-byte aligned rows; REGNN_BF16: 8-byte aligned, gh rounded
+ * first and nx_out = round(nx_scale * gh) from the rounded gh, as a stored bf16 gradient would
+ * be). Either part (gh / slab) may be NULL. */
 int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K,
-                     const float* W, const float* h, const float* gscale, float* gh,
+                     const float* W, const float* h, const float* gscale, void* gh,
                      int64_t n_out, float* slab, int32_t slab_rows, const float* lse,
-                     const int64_t* labels, float scale, const float* nx_scale, float* nx_out,
-                     float* nx_dot, hipStream_t stream);
+                     const int64_t* labels, float scale, const void* hx, const float* nx_scale,
+                     void* nx_out, float* nx_dot, int32_t dtype, hipStream_t stream);
 
 /* regnn_head_bwd's gh (gscale * p W, rows [n, n_out) zero) with the consumer-side row pass of
  * h's producer folded in: when h is the output of an aggregation with post-scale nx_scale, its

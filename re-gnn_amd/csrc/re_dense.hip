@@ -547,6 +547,18 @@ head_gh_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld, const 
 // and p = scale (exp(z - lse) - [class == label]) is formed on the fly from the per-row lse of
 // regnn_head_fwd_lse, so the forward never writes p (the n x C fp32 rows it would store and these
 // kernels read back are the logits rows the caller gets anyway).
+// four consecutive features of a row in fp32 / bf16 storage (16 / 8 bytes)
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                                              uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16));
+}
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4(const bf16_t* p) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return f32x4{bf2f(u.x & 0xffffu), bf2f(u.x >> 16), bf2f(u.y & 0xffffu), bf2f(u.y >> 16)};
+}
+
 struct PSrc {
     const float* lse;
     const int64_t* labels;
@@ -560,13 +572,15 @@ __device__ __forceinline__ float zp_val(float z, float zl2, bool is_label, float
     return fmaf(e, scale, is_label ? -scale : 0.f);
 }
 
-template <int NT, bool ZP = false>
+// TO: storage type of gh, hx and nx_out (float, or bf16_t for a bf16 feature pipeline: gh and
+// nx_out are rounded as the stored-gradient path would round them, g first, then post * g)
+template <int NT, bool ZP = false, typename TO = float>
 __global__ void __launch_bounds__(kGhBlock)
 head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
                   const float* __restrict__ W,
-                  const float* __restrict__ gscale, float* __restrict__ gh, int64_t n_out,
-                  const float* __restrict__ nx_scale, const float* __restrict__ hx,
-                  float* __restrict__ nx_out, float* __restrict__ nx_dot, PSrc ps) {
+                  const float* __restrict__ gscale, TO* __restrict__ gh, int64_t n_out,
+                  const float* __restrict__ nx_scale, const TO* __restrict__ hx,
+                  TO* __restrict__ nx_out, float* __restrict__ nx_dot, PSrc ps) {
     constexpr int K = kHeadK, NCH = (NT + 1) / 2, CP32 = 32 * NCH, LDR = CP32 + 8;
     extern __shared__ uint16_t Wt[];                       // [3][K][LDR] bf16
     for (int idx = threadIdx.x; idx < CP32 * K; idx += blockDim.x) {
@@ -644,24 +658,27 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
         }
         float d = 0.f, ns = 1.f;
         if (valid) {
-            float* gr = gh + row * K + 4 * q;
+            TO* gr = gh + row * K + 4 * q;
             f32x4 g[4];
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
                 g[kt] = acc[kt] * sc;
-                *reinterpret_cast<f32x4*>(gr + 16 * kt) = g[kt];
+                st4(gr + 16 * kt, g[kt]);
+                if constexpr (sizeof(TO) == 2)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) g[kt][i] = round_to<TO>(g[kt][i]);
             }
             if (nx_scale) {                                  // kernel-uniform
                 // the consumer-side row pass of h's producer (regnn_head_gh_next)
                 ns = nx_scale[row];
-                const float* hr = hx + row * K + 4 * q;
-                float* orow = nx_out + row * K + 4 * q;
+                const TO* hr = hx + row * K + 4 * q;
+                TO* orow = nx_out + row * K + 4 * q;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
-                    const f32x4 hv = *reinterpret_cast<const f32x4*>(hr + 16 * kt);
+                    const f32x4 hv = ld4(hr + 16 * kt);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) d = fmaf(g[kt][i], hv[i], d);
-                    *reinterpret_cast<f32x4*>(orow + 16 * kt) = g[kt] * ns;
+                    st4(orow + 16 * kt, g[kt] * ns);
                 }
             }
         }
@@ -674,8 +691,8 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
     const int64_t z0 = n * K / 4, z1 = n_out * K / 4;      // rows without a loss term: zero
     for (int64_t v = z0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < z1;
          v += (int64_t)gridDim.x * blockDim.x) {
-        reinterpret_cast<f32x4*>(gh)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (nx_scale) reinterpret_cast<f32x4*>(nx_out)[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st4(gh + 4 * v, f32x4{0.f, 0.f, 0.f, 0.f});
+        if (nx_scale) st4(nx_out + 4 * v, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     if (nx_scale)
         for (int64_t r = n + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_out;
@@ -879,35 +896,50 @@ int launch_wgrad_x6(const TP* p, int64_t n, int C, int64_t ld, const TH* h, floa
     return REGNN_OK;
 }
 
+// gh of regnn_head_bwd_z (p re-formed from the logits rows), storage type TO for gh / hx / nx_out
+template <int NT, typename TO>
+int launch_gh_z(const float* z, int64_t n, int C, int64_t ld, const float* W,
+                const float* gscale, void* gh, int64_t n_out, const float* nx_scale,
+                const void* hx, void* nx_out, float* nx_dot, PSrc ps, hipStream_t stream) {
+    constexpr int K = kHeadK;
+    constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
+    auto kern = &head_gh_x6_kernel<NT, true, TO>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return REGNN_ELAUNCH;
+        attr = true;
+    }
+    const int64_t tiles = (n + 15) / 16;
+    int64_t grid = (tiles + kGhBlock / 64 - 1) / (kGhBlock / 64);
+    const int cap = resident_blocks(reinterpret_cast<const void*>(kern), lds, kGhBlock);
+    if (grid > cap) grid = cap;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kGhBlock), lds, stream, z, n, C, ld, W,
+                       gscale, static_cast<TO*>(gh), n_out, nx_scale,
+                       static_cast<const TO*>(hx), static_cast<TO*>(nx_out), nx_dot, ps);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
 template <int NT>
 int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W, const float* h,
                     const float* gscale, float* gh, int64_t n_out, float* slab, int slab_rows,
                     hipStream_t stream, const float* nx_scale = nullptr,
                     const float* hx = nullptr, float* nx_out = nullptr,
-                    float* nx_dot = nullptr, PSrc ps = PSrc{nullptr, nullptr, 0.f}) {
+                    float* nx_dot = nullptr, PSrc ps = PSrc{nullptr, nullptr, 0.f},
+                    int dtype = 0) {
     constexpr int K = kHeadK;
     if (nx_scale && !gh) return REGNN_EINVAL;
     if (ps.lse) {                                  // p from the logits rows: bf16x6 kernels only
         if (gh) {
-            constexpr size_t lds = (size_t)3 * K * (32 * ((NT + 1) / 2) + 8) * sizeof(uint16_t);
-            static bool attrz = false;
-            if (!attrz) {
-                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_gh_x6_kernel<NT, true>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds) != hipSuccess)
-                    return REGNN_ELAUNCH;
-                attrz = true;
-            }
-            const int64_t tiles = (n + 15) / 16;
-            int64_t grid = (tiles + kGhBlock / 64 - 1) / (kGhBlock / 64);
-            const int cap = resident_blocks(
-                reinterpret_cast<const void*>(&head_gh_x6_kernel<NT, true>), lds, kGhBlock);
-            if (grid > cap) grid = cap;
-            if (grid < 1) grid = 1;
-            hipLaunchKernelGGL((head_gh_x6_kernel<NT, true>), dim3((unsigned)grid),
-                               dim3(kGhBlock), lds, stream, p, n, C, ld, W, gscale, gh, n_out,
-                               nx_scale, hx, nx_out, nx_dot, ps);
-            REGNN_LAUNCH_CHECK();
+            const int rc = dtype == 1
+                ? launch_gh_z<NT, bf16_t>(p, n, C, ld, W, gscale, gh, n_out, nx_scale, hx, nx_out,
+                                          nx_dot, ps, stream)
+                : launch_gh_z<NT, float>(p, n, C, ld, W, gscale, gh, n_out, nx_scale, hx, nx_out,
+                                         nx_dot, ps, stream);
+            if (rc != REGNN_OK) return rc;
         }
         if (slab)
             return launch_wgrad_x6<float, float, NT, kHeadK, true>(p, n, C, ld, h, slab,
@@ -1432,23 +1464,25 @@ int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, 
     }
 }
 int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K,
-                     const float* W, const float* h, const float* gscale, float* gh,
+                     const float* W, const float* h, const float* gscale, void* gh,
                      int64_t n_out, float* slab, int32_t slab_rows, const float* lse,
-                     const int64_t* labels, float scale, const float* nx_scale, float* nx_out,
-                     float* nx_dot, hipStream_t stream) {
+                     const int64_t* labels, float scale, const void* hx, const float* nx_scale,
+                     void* nx_out, float* nx_dot, int32_t dtype, hipStream_t stream) {
     if (!z || n < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C || (gh && !W) ||
+        (dtype != 0 && dtype != 1) || (nx_scale && !hx) ||
         (gh && n_out < n) || (slab && (!h || slab_rows <= 0)) || (n > 0 && (!lse || !labels)) ||
-        (nx_scale && (!gh || !h || !nx_out || !nx_dot)) ||
+        (nx_scale && (!gh || !nx_out || !nx_dot)) ||
         ((reinterpret_cast<uintptr_t>(gh) | reinterpret_cast<uintptr_t>(nx_out) |
-          (nx_scale ? reinterpret_cast<uintptr_t>(h) : 0)) & 15))
+          (nx_scale ? reinterpret_cast<uintptr_t>(hx) : 0)) & (dtype == 1 ? 7 : 15)))
         return REGNN_EINVAL;
     if (n == 0 && !(gh && n_out > 0)) return REGNN_OK;
     const PSrc ps{lse, labels, scale};
     switch ((C + 15) / 16) {
 #define HB_CASE(nt) \
-        case nt: return launch_head_bwd<nt>(z, n, C, ld, W, h, gscale, gh, n_out, slab,      \
-                                            slab_rows, stream, nx_scale,                      \
-                                            nx_scale ? h : nullptr, nx_out, nx_dot, ps);
+        case nt: return launch_head_bwd<nt>(z, n, C, ld, W, h, gscale,                        \
+                                            static_cast<float*>(gh), n_out, slab, slab_rows,  \
+                                            stream, nx_scale, static_cast<const float*>(hx),  \
+                                            static_cast<float*>(nx_out), nx_dot, ps, dtype);
         HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6)
         HB_CASE(7) HB_CASE(8) HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12)
         HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16) HB_CASE(17) HB_CASE(18)

@@ -793,8 +793,13 @@ class _HeadCE(torch.autograd.Function):
         dev = h.device
         loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
         lab = labels.to(torch.int64).contiguous()
-        if head_fused(h.shape[1], C) and h.dtype == torch.float32:
-            h = h.contiguous()
+        hin = h
+        ctx.in_dtype = h.dtype
+        if head_fused(h.shape[1], C) and (h.dtype == torch.float32 or (
+                h.dtype == torch.bfloat16 and HEAD["p"] == "z")):
+            # bf16 rows (a bf16 feature pipeline): the head computes on their fp32 widening and
+            # hands back a bf16 gradient (regnn_head_bwd_z dtype)
+            h = h.contiguous().float()
             Wc = W.detach().contiguous()
             # rows padded to 16 classes (64-byte aligned): logits is a [rows, C] view of it
             ld = 16 * ((C + 15) // 16)
@@ -828,7 +833,9 @@ class _HeadCE(torch.autograd.Function):
         ctx.bias = b.detach() if b is not None else None
         ctx.has_bias = b is not None
         # h straight from an aggregation (re_spmm): its backward row pass rides on gh's kernel
-        ctx.link = getattr(h, "_regnn_link", None) if h.dtype == torch.float32 else None
+        ctx.link = getattr(hin, "_regnn_link", None) if (
+            hin.dtype == torch.float32 or getattr(ctx, "zsrc", None) is not None) else None
+        ctx.hx = hin if hin.dtype != torch.float32 else None
         ctx.mark_non_differentiable(logits)
         return logits, loss
 
@@ -849,6 +856,8 @@ class _HeadCE(torch.autograd.Function):
             if z._version == ver:
                 return _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b)
             # the caller modified the logits in place: re-form p from h (the stored-p path)
+            if ctx.in_dtype != torch.float32:
+                ctx.link = None                    # the fp32 hand-off kernels do not apply
             zf = torch.addmm(ctx.bias, h[:n], W.detach().t()) if ctx.bias is not None else \
                 h[:n] @ W.detach().t()
             p = torch.empty(n, C, dtype=torch.float32, device=h.device)
@@ -893,6 +902,8 @@ class _HeadCE(torch.autograd.Function):
                     gW = tot[:Cp * K].view(Cp, K)[:C] * g_loss
                 if need_b:
                     gb = tot[Cp * K:Cp * K + C] * g_loss
+            if gh is not None and gh.dtype != ctx.in_dtype:
+                gh = gh.to(ctx.in_dtype)
             return gh, gW, gb, None
         if need_h:
             gh = torch.empty_like(h)
@@ -918,28 +929,30 @@ def _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b):
     Cp = 16 * ((C + 15) // 16)
     rows = 2048
     hc = h.contiguous()
+    hx = ctx.hx if ctx.hx is not None else hc        # rows in the caller's storage dtype
     zp, ld = L.ptr(z), z.stride(0)
     if need_h:
-        gh = torch.empty_like(h)
+        gh = torch.empty_like(hx)
         gl = g_loss.detach().reshape(1).float().contiguous()
         nx = ctx.link
         nx_args = (None, None, None)
         if nx is not None and nx.post.numel() == h.shape[0] and PRESCALE["next"] != "off":
-            nx_out = torch.empty_like(h)
+            nx_out = torch.empty_like(hx)
             nx_dot = torch.empty(h.shape[0], dtype=torch.float32, device=h.device)
             nx_args = (L.ptr(nx.post), L.ptr(nx_out), L.ptr(nx_dot))
-        with timed("head_gh", 4 * (n * C + h.numel())):
+        with timed("head_gh", 4 * n * C + (2 if nx_args[0] is not None else 1) * gh.numel() *
+                   gh.element_size()):
             L.call("regnn_head_bwd_z", zp, n, C, ld, K, L.ptr(W.detach().contiguous()),
                    L.ptr(hc), L.ptr(gl), L.ptr(gh), h.shape[0], None, 0, L.ptr(lse),
-                   L.ptr(lab), 1.0 / n, *nx_args, L.stream())
+                   L.ptr(lab), 1.0 / n, L.ptr(hx), *nx_args, L.dtype_code(hx), L.stream())
         if nx_args[0] is not None:
             nx.handoff = (gh, gh._version, nx_out, nx_dot, n)
     if need_w or need_b:
         slab = torch.zeros(rows, Cp * K + Cp, dtype=torch.float32, device=h.device)
         with timed("head_bwd", 4 * (n * C + n * K)):
             L.call("regnn_head_bwd_z", zp, n, C, ld, K, None, L.ptr(hc), None, None, 0,
-                   L.ptr(slab), rows, L.ptr(lse), L.ptr(lab), 1.0 / n, None, None, None,
-                   L.stream())
+                   L.ptr(slab), rows, L.ptr(lse), L.ptr(lab), 1.0 / n, None, None, None, None,
+                   0, L.stream())
         tot = _reduce(slab, Cp * K + Cp)
         if need_w:
             gW = tot[:Cp * K].view(Cp, K)[:C] * g_loss
@@ -985,5 +998,9 @@ def batched_wgrad(g, x, chunk=1 << 15):
 
 
 def head_ce(h, weight, bias, labels):
-    """fused output head + cross-entropy over rows [0, len(labels)) -> (logits, loss)."""
+    """fused output head + cross-entropy over rows [0, len(labels)) -> (logits, loss).
+    bf16 rows go in as they are (z mode: widened inside, bf16 gradient out), else as fp32."""
+    if h.dtype != torch.float32 and not (h.dtype == torch.bfloat16 and HEAD["p"] == "z" and
+                                         head_fused(h.shape[-1], weight.shape[0])):
+        h = h.float()
     return _HeadCE.apply(h, weight, bias, labels)

@@ -251,3 +251,54 @@ def test_head_gh_handoff(n_loss, mode, monkeypatch):
         for a, b in zip(grads[m], grads["off"]):
             err = float((a - b).abs().max()) / max(1.0, float(b.abs().max()))
             assert err <= 1e-6
+
+
+@pytest.mark.parametrize("n_loss", [20, 333])
+def test_head_gh_handoff_bf16(n_loss, monkeypatch):
+    """bf16 feature pipeline: head_ce takes the aggregation's bf16 rows, its z-mode gh kernel
+    stores the bf16 gradient and the producer's bf16 pre-scaled rows (regnn_head_bwd_z dtype 1);
+    gradients match the unlinked path (bf16 gradient from the head, row pass in the producer)."""
+    from regnn_hip import ops
+    from regnn_hip.graph import RelGraph
+    monkeypatch.setitem(ops.HEAD, "p", "z")
+    taken = []
+    orig = ops._NextLink.take
+
+    def spy(self, gy):
+        offered = self.handoff is not None
+        r = orig(self, gy)
+        if offered:
+            taken.append(r is not None)
+        return r
+    monkeypatch.setattr(ops._NextLink, "take", spy)
+    src, dst, rel, n, R = _graph(seed=8)
+    rg = RelGraph(src, dst, n, DEV)
+    pack = rg.rel_pack(torch.from_numpy(rel).to(DEV), num_rel=R)
+    g = torch.Generator().manual_seed(5)
+    C = 349
+    base = [torch.randn(n, 64, generator=g), torch.rand(R, 1, generator=g) + 0.2,
+            torch.rand(n, generator=g) + 0.5, torch.randn(C, 64, generator=g) * 0.1,
+            torch.randn(C, generator=g)]
+    labels = torch.randint(0, C, (n_loss,), generator=g).to(DEV)
+    grads, losses = {}, {}
+    old = dict(ops.PRESCALE)
+    try:
+        for mode in ("auto", "noprefix", "off"):
+            ops.PRESCALE["next"] = "off" if mode == "off" else "auto"
+            ops.PRESCALE["prefix"] = "off" if mode == "noprefix" else "auto"
+            taken.clear()
+            xd, t0, m0, W, b = [t.to(DEV).requires_grad_(True) for t in base]
+            y = ops.re_spmm(rg, xd.bfloat16(), t0, pack, pre=m0, post=m0)
+            assert y.dtype == torch.bfloat16
+            _, loss = ops.head_ce(y, W, b, labels)
+            loss.backward()
+            assert taken == ([True] if mode != "off" else [])
+            grads[mode] = [t.grad.clone() for t in (xd, t0, m0, W, b)]
+            losses[mode] = loss.item()
+    finally:
+        ops.PRESCALE.update(old)
+    assert losses["auto"] == losses["off"]
+    for m in ("auto", "noprefix"):
+        for a, b in zip(grads[m], grads["off"]):
+            err = float((a - b).abs().max()) / max(1e-3, float(b.abs().max()))
+            assert err <= 1e-2
