@@ -799,65 +799,140 @@ wgrad_x6_kernel(const TP* __restrict__ p, int64_t n, int C, int64_t ld,
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int64_t row0 = r0; row0 < r1; row0 += 32) {
-        float a[MU][8], b[MU][4][8];
+    if constexpr (KB == 1) {
+        // The h operand is the same for every wave of the block: per 32-row k-step, lanes
+        // 0..255 of the block split one (kt, q, c) column piece each (8 rows) and publish its
+        // three bf16 fragments in LDS (double-buffered, one barrier per step); every wave then
+        // reads its B fragments with ds_read_b128 instead of splitting 32 values per lane.
+        __shared__ bf16x8_t hs[2][3][4][4][16];             // [buf][split][kt][q][c]: 24 KiB
+        const int gid = threadIdx.x;
+        const int wkt = (gid >> 6) & 3, wq = (gid >> 4) & 3, wc = gid & 15;
+        int buf = 0;
+        for (int64_t row0 = r0; row0 < r1; row0 += 32, buf ^= 1) {
+            if (gid < 256) {
+                uint16_t s0[8], s1[8], s2[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t rr = row0 + 8 * q + j;
-            const bool ok = rr < r1;
-            const int64_t rc = ok ? rr : r0;
-            float zl = 0.f;
-            int zy = -1;
-            if constexpr (ZP) {
-                zl = ps.lse[rc] * kLog2e;
-                zy = (int)ps.labels[rc];
+                for (int j = 0; j < 8; ++j) {
+                    const int64_t rr = row0 + 8 * wq + j;
+                    const float hv = ld_h((rr < r1 ? rr : r0) * KH + 16 * wkt + wc);
+                    split3(rr < r1 ? hv : 0.f, s0[j], s1[j], s2[j]);
+                }
+                hs[buf][0][wkt][wq][wc] = pack8(s0);
+                hs[buf][1][wkt][wq][wc] = pack8(s1);
+                hs[buf][2][wkt][wq][wc] = pack8(s2);
             }
+            float a[MU][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t rr = row0 + 8 * q + j;
+                const bool ok = rr < r1;
+                const int64_t rc = ok ? rr : r0;
+                float zl = 0.f;
+                int zy = -1;
+                if constexpr (ZP) {
+                    zl = ps.lse[rc] * kLog2e;
+                    zy = (int)ps.labels[rc];
+                }
+#pragma unroll
+                for (int m = 0; m < MU; ++m) {
+                    const int u = w + 8 * m, t = u % NT;
+                    const int cls = 16 * t + c;
+                    const bool in = ok && u < NU && cls < C;
+                    float v = ld_p(rc * ld + (cls < C ? cls : 0));
+                    if constexpr (ZP) v = zp_val(v, zl, cls == zy, ps.scale);
+                    a[m][j] = in ? v : 0.f;
+                }
+            }
+            __syncthreads();                                 // block-uniform: r0, r1, row0
+            bf16x8_t bf[4][3];
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int sp = 0; sp < 3; ++sp) bf[kt][sp] = hs[buf][sp][kt][q][c];
 #pragma unroll
             for (int m = 0; m < MU; ++m) {
-                const int u = w + 8 * m, t = u % NT, fb = u / NT;
-                const int cls = 16 * t + c;
-                const bool in = ok && u < NU && cls < C;
-                float v = ld_p(rc * ld + (cls < C ? cls : 0));
-                if constexpr (ZP) v = zp_val(v, zl, cls == zy, ps.scale);
-                a[m][j] = in ? v : 0.f;
-                if (KB > 1 || m == 0) {
+                if (w + 8 * m >= NU) continue;               // wave-uniform
+                uint16_t s0[8], s1[8], s2[8];
 #pragma unroll
-                    for (int kt = 0; kt < 4; ++kt) {
-                        const float hv = ld_h(rc * KH + 64 * (KB > 1 ? fb : 0) + 16 * kt + c);
-                        b[m][kt][j] = ok ? hv : 0.f;
+                for (int j = 0; j < 8; ++j) {
+                    gb[m] += a[m][j];
+                    split3(a[m][j], s0[j], s1[j], s2[j]);
+                }
+                const bf16x8_t a0 = pack8(s0), a1 = pack8(s1), a2 = pack8(s2);
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    if constexpr (!EXACT) {
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
                     }
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][0], acc[m][kt], 0, 0, 0);
                 }
             }
         }
-#pragma unroll
-        for (int m = 0; m < MU; ++m) {
-            if (w + 8 * m >= NU) continue;                   // wave-uniform
-            const int mb = KB > 1 ? m : 0;                   // KB == 1: units share h
-            bf16x8_t bf[4][3];
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                uint16_t s0[8], s1[8], s2[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) split3(b[mb][kt][j], s0[j], s1[j], s2[j]);
-                bf[kt][0] = pack8(s0); bf[kt][1] = pack8(s1); bf[kt][2] = pack8(s2);
-            }
-            uint16_t s0[8], s1[8], s2[8];
-#pragma unroll
+    } else {
+        for (int64_t row0 = r0; row0 < r1; row0 += 32) {
+            float a[MU][8], b[MU][4][8];
+    #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                gb[m] += a[m][j];
-                split3(a[m][j], s0[j], s1[j], s2[j]);
-            }
-            const bf16x8_t a0 = pack8(s0), a1 = pack8(s1), a2 = pack8(s2);
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                if constexpr (!EXACT) {
-                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
-                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
-                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
-                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
-                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
+                const int64_t rr = row0 + 8 * q + j;
+                const bool ok = rr < r1;
+                const int64_t rc = ok ? rr : r0;
+                float zl = 0.f;
+                int zy = -1;
+                if constexpr (ZP) {
+                    zl = ps.lse[rc] * kLog2e;
+                    zy = (int)ps.labels[rc];
                 }
-                acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][0], acc[m][kt], 0, 0, 0);
+    #pragma unroll
+                for (int m = 0; m < MU; ++m) {
+                    const int u = w + 8 * m, t = u % NT, fb = u / NT;
+                    const int cls = 16 * t + c;
+                    const bool in = ok && u < NU && cls < C;
+                    float v = ld_p(rc * ld + (cls < C ? cls : 0));
+                    if constexpr (ZP) v = zp_val(v, zl, cls == zy, ps.scale);
+                    a[m][j] = in ? v : 0.f;
+                    if (KB > 1 || m == 0) {
+    #pragma unroll
+                        for (int kt = 0; kt < 4; ++kt) {
+                            const float hv = ld_h(rc * KH + 64 * (KB > 1 ? fb : 0) + 16 * kt + c);
+                            b[m][kt][j] = ok ? hv : 0.f;
+                        }
+                    }
+                }
+            }
+    #pragma unroll
+            for (int m = 0; m < MU; ++m) {
+                if (w + 8 * m >= NU) continue;                   // wave-uniform
+                const int mb = KB > 1 ? m : 0;                   // KB == 1: units share h
+                bf16x8_t bf[4][3];
+    #pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    uint16_t s0[8], s1[8], s2[8];
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) split3(b[mb][kt][j], s0[j], s1[j], s2[j]);
+                    bf[kt][0] = pack8(s0); bf[kt][1] = pack8(s1); bf[kt][2] = pack8(s2);
+                }
+                uint16_t s0[8], s1[8], s2[8];
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    gb[m] += a[m][j];
+                    split3(a[m][j], s0[j], s1[j], s2[j]);
+                }
+                const bf16x8_t a0 = pack8(s0), a1 = pack8(s1), a2 = pack8(s2);
+    #pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    if constexpr (!EXACT) {
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[kt][0], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][1], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][2], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[kt][0], acc[m][kt], 0, 0, 0);
+                        acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][1], acc[m][kt], 0, 0, 0);
+                    }
+                    acc[m][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[kt][0], acc[m][kt], 0, 0, 0);
+                }
             }
         }
     }
