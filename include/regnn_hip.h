@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 14). */
+/* ABI version (bumped on any signature change or addition; currently 15). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -362,7 +362,8 @@ int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K
  * h's producer folded in: when h is the output of an aggregation with post-scale nx_scale, its
  * backward needs nx_scale * gh and <gh, h> / nx_scale; this call writes, besides gh,
  *   nx_out[u] = nx_scale[u] * gh[u],  nx_dot[u] = <gh[u], h[u]> / nx_scale[u]
- * (zero for the rows without a loss term, whose h is not read). K = 64, fp32, 16-byte aligned
+ * (nx_dot zero for the rows without a loss term, whose h is not read; nx_out rows [n, n_out) are
+ * NOT written: the gradient there is zero, and the consumer gathers only edges into rows < n). K = 64, fp32, 16-byte aligned
  * gh / h / nx_out (REGCN's last layer -> out_lin, run_regnn.py:146-148). */
 int regnn_head_gh_next(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K,
                        const float* W, const float* gscale, float* gh, int64_t n_out,

@@ -691,8 +691,7 @@ head_gh_x6_kernel(const float* __restrict__ p, int64_t n, int C, int64_t ld,
     const int64_t z0 = n * K / 4, z1 = n_out * K / 4;      // rows without a loss term: zero
     for (int64_t v = z0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < z1;
          v += (int64_t)gridDim.x * blockDim.x) {
-        st4(gh + 4 * v, f32x4{0.f, 0.f, 0.f, 0.f});
-        if (nx_scale) st4(nx_out + 4 * v, f32x4{0.f, 0.f, 0.f, 0.f});
+        st4(gh + 4 * v, f32x4{0.f, 0.f, 0.f, 0.f});     // nx_out rows >= n: not written
     }
     if (nx_scale)
         for (int64_t r = n + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_out;

@@ -170,8 +170,9 @@ class _NextLink:
     parks them here; the producer's backward takes them only if its incoming gradient IS that gx
     tensor, unmodified (autograd summed nothing into it), and runs its own row pass otherwise.
     The hand-off's last field, when not None, is a row count n such that the gradient is zero on
-    rows >= n (the output head's loss rows): the producer's transposed gather then runs over the
-    CSC prefix of edges into rows < n (RelGraph.csc_prefix)."""
+    rows >= n (the output head's loss rows) and the handed rows >= n are not written: the
+    producer's transposed gather must then run over the CSC prefix of edges into rows < n
+    (RelGraph.csc_prefix), or not take the hand-off."""
 
     __slots__ = ("post", "handoff")
 
@@ -264,6 +265,9 @@ class _ReSpmm(torch.autograd.Function):
         src, in_scale, dot = gy, post, None
         drop = ctx.drop
         handed = ctx.link.take(gy) if (prescale and ctx.link is not None) else None
+        if handed is not None and handed[2] is not None and handed[2] < rg.n_dst and \
+                PRESCALE["prefix"] == "off":
+            handed = None          # its rows >= nz are not written: only the prefix may use it
         # the consumer of x (the next aggregation) forms its producer's pre-scaled gradient rows
         nx = ctx.link_in if (need_x and ctx.link_in is not None and
                              ctx.link_in.post.numel() == rg.n_src) else None

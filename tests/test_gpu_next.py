@@ -242,6 +242,7 @@ def test_head_gh_handoff(n_loss, mode, monkeypatch):
             y = ops.re_spmm(rg, xd, t0, pack, pre=m0, post=m0)
             _, loss = ops.head_ce(y, W, b, labels)
             loss.backward()
+            # (without the prefix, the producer declines a truncating hand-off after taking it)
             assert taken == ([True] if mode != "off" else [])
             grads[mode] = [t.grad.clone() for t in (xd, t0, m0, W, b)]
     finally:
@@ -292,6 +293,7 @@ def test_head_gh_handoff_bf16(n_loss, monkeypatch):
             assert y.dtype == torch.bfloat16
             _, loss = ops.head_ce(y, W, b, labels)
             loss.backward()
+            # (without the prefix, the producer declines a truncating hand-off after taking it)
             assert taken == ([True] if mode != "off" else [])
             grads[mode] = [t.grad.clone() for t in (xd, t0, m0, W, b)]
             losses[mode] = loss.item()
