@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 15). */
+/* ABI version (bumped on any signature change or addition; currently 16). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -339,21 +339,23 @@ int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, 
 /* regnn_head_fwd without the p output: the same logits, and loss_lse [2, n_loss] holds the loss
  * rows (row 0) and each loss row's log-sum-exp (row 1), from which regnn_head_bwd_z re-forms
  * p = scale * (exp(z - lse) - [c == y]) out of the logits rows it already has. The forward then
- * stores n_loss x ld fp32 fewer (10.4 GB at mag-10x). Same shape limits as regnn_head_fwd. */
-int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+ * stores n_loss x ld fp32 fewer (10.4 GB at mag-10x). Same shape limits as regnn_head_fwd. h rows
+ * in dtype: REGNN_F32, or REGNN_BF16 (a bf16 feature pipeline's rows, read as they are: exact in
+ * the first bf16x6 split; C <= 368, else REGNN_EUNSUPPORTED). */
+int regnn_head_fwd_lse(const void* h, int64_t rows, int32_t K, const float* W, const float* b,
                        int32_t C, int64_t ld, const int64_t* labels, int64_t n_loss,
-                       float* logits, float* loss_lse, hipStream_t stream);
+                       float* logits, float* loss_lse, int32_t dtype, hipStream_t stream);
 
 /* regnn_head_bwd / regnn_head_gh_next from the logits rows z [n, C] (row stride ld) of
  * regnn_head_fwd_lse instead of a stored p: p[r, c] = scale * (exp(z[r, c] - lse[r]) - [c ==
  * labels[r]]) is formed on the fly inside the gh and slab kernels (bf16x6 MFMA). gh, slab and
- * (nx_scale, nx_out, nx_dot) have the meaning of those calls; h (fp32 [n, K]) feeds the slab
- * (p^T h), hx (the head input as the aggregation stored it, dtype) the nx dot. gh, hx and nx_out
+ * (nx_scale, nx_out, nx_dot) have the meaning of those calls; h ([n, K] in dtype) feeds the
+ * slab (p^T h), hx (the head input as the aggregation stored it, dtype) the nx dot. gh, hx and nx_out
  * are stored in dtype (REGNN_F32: 16-byte aligned rows; REGNN_BF16: 8-byte aligned, gh rounded
  * first and nx_out = round(nx_scale * gh) from the rounded gh, as a stored bf16 gradient would
  * be). Either part (gh / slab) may be NULL. */
 int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K,
-                     const float* W, const float* h, const float* gscale, void* gh,
+                     const float* W, const void* h, const float* gscale, void* gh,
                      int64_t n_out, float* slab, int32_t slab_rows, const float* lse,
                      const int64_t* labels, float scale, const void* hx, const float* nx_scale,
                      void* nx_out, float* nx_dot, int32_t dtype, hipStream_t stream);

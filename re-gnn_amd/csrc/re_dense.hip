@@ -297,9 +297,9 @@ __device__ __forceinline__ bf16x8_t pack8(const uint16_t (&v)[8]) {
     return __builtin_bit_cast(bf16x8_t, u);
 }
 
-template <int NT, bool AMAX>
+template <int NT, bool AMAX, typename TH = float>
 __global__ void __launch_bounds__(kHeadBlock)
-head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __restrict__ W,
+head_fwd_x6_kernel(const TH* __restrict__ h, int64_t rows, const float* __restrict__ W,
                    const float* __restrict__ bias, int C, int64_t ld,
                    const int64_t* __restrict__ labels,
                    int64_t n_loss, float scale, float* __restrict__ logits, float* __restrict__ p,
@@ -329,10 +329,14 @@ head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __res
         const int64_t arow = min(tile * 16 + c, rows - 1);
 #pragma unroll
         for (int kc = 0; kc < 2; ++kc) {
-            const float4* hp = reinterpret_cast<const float4*>(h + arow * K + 32 * kc + 8 * q);
-            const float4 x0 = hp[0], x1 = hp[1];
-            a[kc][0] = x0.x; a[kc][1] = x0.y; a[kc][2] = x0.z; a[kc][3] = x0.w;
-            a[kc][4] = x1.x; a[kc][5] = x1.y; a[kc][6] = x1.z; a[kc][7] = x1.w;
+            if constexpr (sizeof(TH) == 2) {                 // bf16 rows: one 16-byte load
+                Vec<bf16_t>::load(h + arow * K + 32 * kc + 8 * q, a[kc]);
+            } else {
+                const float4* hp = reinterpret_cast<const float4*>(h + arow * K + 32 * kc + 8 * q);
+                const float4 x0 = hp[0], x1 = hp[1];
+                a[kc][0] = x0.x; a[kc][1] = x0.y; a[kc][2] = x0.z; a[kc][3] = x0.w;
+                a[kc][4] = x1.x; a[kc][5] = x1.y; a[kc][6] = x1.z; a[kc][7] = x1.w;
+            }
         }
     };
     int64_t tile = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
@@ -387,25 +391,25 @@ head_fwd_x6_kernel(const float* __restrict__ h, int64_t rows, const float* __res
     }
 }
 
-template <int NT, bool AMAX>
-int launch_head_x6(const float* h, int64_t rows, const float* W, const float* b, int C, int64_t ld,
+template <int NT, bool AMAX, typename TH = float>
+int launch_head_x6(const TH* h, int64_t rows, const float* W, const float* b, int C, int64_t ld,
                    const int64_t* labels, int64_t n_loss, float scale, float* logits, float* p,
                    float* loss_rows, hipStream_t stream, int64_t* amax = nullptr) {
     const size_t lds = (size_t)3 * NT * 16 * kX6Row * sizeof(uint16_t) + NT * 16 * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX, TH>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return REGNN_ELAUNCH;
         attr = true;
     }
     const int64_t tiles = (rows + 15) / 16;
     int64_t grid = (tiles + kHeadBlock / 64 - 1) / (kHeadBlock / 64);
-    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX>),
+    const int cap = resident_blocks(reinterpret_cast<const void*>(&head_fwd_x6_kernel<NT, AMAX, TH>),
                                     lds, kHeadBlock);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((head_fwd_x6_kernel<NT, AMAX>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
+    hipLaunchKernelGGL((head_fwd_x6_kernel<NT, AMAX, TH>), dim3((unsigned)grid), dim3(kHeadBlock), lds,
                        stream, h, rows, W, b, C, ld, labels, n_loss, scale, logits, p, loss_rows,
                        amax);
     REGNN_LAUNCH_CHECK();
@@ -1015,6 +1019,9 @@ int launch_head_bwd(const float* p, int64_t n, int C, int64_t ld, const float* W
                                          nx_dot, ps, stream);
             if (rc != REGNN_OK) return rc;
         }
+        if (slab && dtype == 1)                    // h rows in bf16 (exact in their first split)
+            return launch_wgrad_x6<float, bf16_t, NT, kHeadK, true>(
+                p, n, C, ld, reinterpret_cast<const bf16_t*>(h), slab, slab_rows, stream, ps);
         if (slab)
             return launch_wgrad_x6<float, float, NT, kHeadK, true>(p, n, C, ld, h, slab,
                                                                   slab_rows, stream, ps);
@@ -1517,18 +1524,36 @@ int regnn_head_bwd(const float* p, int64_t n, int32_t C, int64_t ld, int32_t K, 
     }
 }
 
-int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, const float* b,
+}  // extern "C"
+
+template <int NT>
+int head_fwd_lse_nt(const void* h, int64_t rows, const float* W, const float* b, int C,
+                    int64_t ld, const int64_t* labels, int64_t n_loss, float* logits,
+                    float* loss_lse, int dtype, hipStream_t stream) {
+    if (dtype == 0)
+        return launch_head<NT>(static_cast<const float*>(h), rows, W, b, C, ld, labels, n_loss,
+                               1.f, logits, nullptr, loss_lse, stream);
+    if constexpr (NT <= kX6MaxNT)
+        return launch_head_x6<NT, false, bf16_t>(static_cast<const bf16_t*>(h), rows, W, b, C,
+                                                 ld, labels, n_loss, 1.f, logits, nullptr,
+                                                 loss_lse, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+extern "C" {
+
+int regnn_head_fwd_lse(const void* h, int64_t rows, int32_t K, const float* W, const float* b,
                        int32_t C, int64_t ld, const int64_t* labels, int64_t n_loss,
-                       float* logits, float* loss_lse, hipStream_t stream) {
+                       float* logits, float* loss_lse, int32_t dtype, hipStream_t stream) {
     if (!h || !W || !logits || rows < 0 || K != kHeadK || C <= 0 || C > kHeadMaxC || ld < C ||
         n_loss < 0 || n_loss > rows || (n_loss > 0 && (!labels || !loss_lse)) ||
-        (reinterpret_cast<uintptr_t>(h) & 15))
+        (dtype != 0 && dtype != 1) || (reinterpret_cast<uintptr_t>(h) & 15))
         return REGNN_EINVAL;
     if (rows == 0) return REGNN_OK;
     switch ((C + 15) / 16) {
 #define HEAD_CASE(nt) \
-        case nt: return launch_head<nt>(h, rows, W, b, C, ld, labels, n_loss, 1.f, logits,      \
-                                        nullptr, loss_lse, stream);
+        case nt: return head_fwd_lse_nt<nt>(h, rows, W, b, C, ld, labels, n_loss, logits,       \
+                                            loss_lse, dtype, stream);
         HEAD_CASE(1) HEAD_CASE(2) HEAD_CASE(3) HEAD_CASE(4) HEAD_CASE(5) HEAD_CASE(6)
         HEAD_CASE(7) HEAD_CASE(8) HEAD_CASE(9) HEAD_CASE(10) HEAD_CASE(11) HEAD_CASE(12)
         HEAD_CASE(13) HEAD_CASE(14) HEAD_CASE(15) HEAD_CASE(16) HEAD_CASE(17) HEAD_CASE(18)
@@ -1538,7 +1563,7 @@ int regnn_head_fwd_lse(const float* h, int64_t rows, int32_t K, const float* W, 
     }
 }
 int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K,
-                     const float* W, const float* h, const float* gscale, void* gh,
+                     const float* W, const void* h, const float* gscale, void* gh,
                      int64_t n_out, float* slab, int32_t slab_rows, const float* lse,
                      const int64_t* labels, float scale, const void* hx, const float* nx_scale,
                      void* nx_out, float* nx_dot, int32_t dtype, hipStream_t stream) {
@@ -1553,7 +1578,8 @@ int regnn_head_bwd_z(const float* z, int64_t n, int32_t C, int64_t ld, int32_t K
     const PSrc ps{lse, labels, scale};
     switch ((C + 15) / 16) {
 #define HB_CASE(nt) \
-        case nt: return launch_head_bwd<nt>(z, n, C, ld, W, h, gscale,                        \
+        case nt: return launch_head_bwd<nt>(z, n, C, ld, W, static_cast<const float*>(h),      \
+                                            gscale,                                           \
                                             static_cast<float*>(gh), n_out, slab, slab_rows,  \
                                             stream, nx_scale, static_cast<const float*>(hx),  \
                                             static_cast<float*>(nx_out), nx_dot, ps, dtype);

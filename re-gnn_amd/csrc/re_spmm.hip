@@ -911,7 +911,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 15; }
+int regnn_abi_version(void) { return 16; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {

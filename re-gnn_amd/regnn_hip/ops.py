@@ -801,9 +801,9 @@ class _HeadCE(torch.autograd.Function):
         ctx.in_dtype = h.dtype
         if head_fused(h.shape[1], C) and (h.dtype == torch.float32 or (
                 h.dtype == torch.bfloat16 and HEAD["p"] == "z")):
-            # bf16 rows (a bf16 feature pipeline): the head computes on their fp32 widening and
-            # hands back a bf16 gradient (regnn_head_bwd_z dtype)
-            h = h.contiguous().float()
+            # bf16 rows (a bf16 feature pipeline, z mode only) are read as they are and get a
+            # bf16 gradient back (regnn_head_fwd_lse / regnn_head_bwd_z dtype)
+            h = h.contiguous()
             Wc = W.detach().contiguous()
             # rows padded to 16 classes (64-byte aligned): logits is a [rows, C] view of it
             ld = 16 * ((C + 15) // 16)
@@ -814,9 +814,11 @@ class _HeadCE(torch.autograd.Function):
                 buf = torch.empty(2, n, dtype=torch.float32, device=dev)
                 loss_rows = buf[0]
                 p = None
-                with timed("head_fwd", 4 * (h.numel() + h.shape[0] * C + 2 * n) + 8 * n):
+                with timed("head_fwd", h.numel() * h.element_size() +
+                           4 * (h.shape[0] * C + 2 * n) + 8 * n):
                     L.call("regnn_head_fwd_lse", L.ptr(h), h.shape[0], h.shape[1], L.ptr(Wc),
-                           bp, C, ld, L.ptr(lab), n, L.ptr(logits), L.ptr(buf), L.stream())
+                           bp, C, ld, L.ptr(lab), n, L.ptr(logits), L.ptr(buf),
+                           L.dtype_code(h), L.stream())
                 ctx.zsrc = (logits, logits._version, buf[1], lab)
             else:
                 p = torch.empty(n, ld, dtype=torch.float32, device=dev)[:, :C]
@@ -839,7 +841,7 @@ class _HeadCE(torch.autograd.Function):
         # h straight from an aggregation (re_spmm): its backward row pass rides on gh's kernel
         ctx.link = getattr(hin, "_regnn_link", None) if (
             hin.dtype == torch.float32 or getattr(ctx, "zsrc", None) is not None) else None
-        ctx.hx = hin if hin.dtype != torch.float32 else None
+        ctx.hx = None
         ctx.mark_non_differentiable(logits)
         return logits, loss
 
@@ -862,6 +864,7 @@ class _HeadCE(torch.autograd.Function):
             # the caller modified the logits in place: re-form p from h (the stored-p path)
             if ctx.in_dtype != torch.float32:
                 ctx.link = None                    # the fp32 hand-off kernels do not apply
+                h = h.float()
             zf = torch.addmm(ctx.bias, h[:n], W.detach().t()) if ctx.bias is not None else \
                 h[:n] @ W.detach().t()
             p = torch.empty(n, C, dtype=torch.float32, device=h.device)
@@ -913,6 +916,8 @@ class _HeadCE(torch.autograd.Function):
             gh = torch.empty_like(h)
             gh[n:].zero_()
             torch.mm(p, W * g_loss, out=gh[:n])      # g_loss folded into the C x K weight
+            if gh.dtype != ctx.in_dtype:
+                gh = gh.to(ctx.in_dtype)
         if need_w:
             gW = batched_wgrad(p, h[:n]) * g_loss
         if need_b:
@@ -956,7 +961,7 @@ def _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b):
         with timed("head_bwd", 4 * (n * C + n * K)):
             L.call("regnn_head_bwd_z", zp, n, C, ld, K, None, L.ptr(hc), None, None, 0,
                    L.ptr(slab), rows, L.ptr(lse), L.ptr(lab), 1.0 / n, None, None, None, None,
-                   0, L.stream())
+                   L.dtype_code(hc), L.stream())
         tot = _reduce(slab, Cp * K + Cp)
         if need_w:
             gW = tot[:Cp * K].view(Cp, K)[:C] * g_loss

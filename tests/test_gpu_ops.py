@@ -207,3 +207,32 @@ def test_attn_dots_matches_autograd(N, H, D):
     assert _rel(el, elr) < 1e-5 and _rel(er, err) < 1e-5
     assert _rel(ft.grad, ftr.grad) < 1e-5
     assert _rel(al.grad, alr.grad) < 1e-5 and _rel(ar.grad, arr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("clobber", [False, True])
+def test_head_ce_bf16_rows_match_widened(clobber):
+    """head_ce on bf16 rows (read as they are, regnn_head_fwd_lse / _bwd_z dtype 1) equals head_ce
+    on their fp32 widening: logits and loss bit-identical (bf16 values are exact in the first
+    bf16x6 split), gradients equal up to the final bf16 rounding of d h; also when the logits
+    are overwritten before backward (p recomputed from the rows)."""
+    from regnn_hip import ops
+    torch.manual_seed(4)
+    N, n, C = 5000, 1800, 349
+    hb = torch.randn(N, 64, device=DEV).bfloat16()
+    W0, b0 = torch.randn(C, 64, device=DEV) * 0.1, torch.randn(C, device=DEV) * 0.1
+    y = torch.randint(0, C, (n,), device=DEV)
+    out = {}
+    for dt in (torch.bfloat16, torch.float32):
+        h = hb.to(dt).clone().requires_grad_(True)
+        W, b = W0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        logits, loss = ops.head_ce(h, W, b, y)
+        lg = logits.clone()
+        if clobber:
+            logits.fill_(3.0)
+        loss.backward()
+        assert h.grad.dtype == dt
+        out[dt] = (lg, loss.detach(), h.grad.float(), W.grad, b.grad)
+    a, r = out[torch.bfloat16], out[torch.float32]
+    assert torch.equal(a[0], r[0]) and torch.equal(a[1], r[1])
+    assert torch.equal(a[2], r[2].bfloat16().float())
+    assert _rel(a[3], r[3]) < 1e-6 and _rel(a[4], r[4]) < 1e-6
