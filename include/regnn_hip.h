@@ -35,7 +35,7 @@ typedef struct ihipStream_t* hipStream_t;
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
 
-/* ABI version (bumped on any signature change or addition; currently 16). */
+/* ABI version (bumped on any signature change or addition; currently 17). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -73,6 +73,21 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
                      int64_t n_seg, float power, int32_t n_rel, int32_t split,
                      const int32_t* long_ids, int32_t n_long, const int32_t* long_cnt,
                      float* slab, hipStream_t stream);
+
+/* regnn_degree / regnn_degree_bwd from the graph's per-row relation histogram instead of its
+ * relation ids: cnt [n_seg, n_rel] uint16 row-major, cnt[v, r] = number of in-edges of v with
+ * relation r for the rows of at most `split` edges and 0 for the long rows (static per graph and
+ * e_feat; RelPack.row_cnt builds it once). deg[v] = sum_r rel_table[r] cnt[v, r] (long rows from
+ * long_cnt, as regnn_degree; ptr is read only for them), norm as regnn_degree. The backward
+ * writes one slab row of n_rel partials per block (zero the slab, reduce with
+ * regnn_rel_reduce). n_rel <= 16 (else REGNN_EINVAL: use the id-walking calls). */
+int regnn_degree_cnt(const uint16_t* cnt, const float* rel_table, int32_t n_rel, int64_t n_seg,
+                     float power, const int32_t* ptr, const int32_t* long_ids, int32_t n_long,
+                     const int32_t* long_cnt, float* deg, float* norm, hipStream_t stream);
+int regnn_degree_cnt_bwd(const uint16_t* cnt, const float* deg, const float* g_norm,
+                         int64_t n_seg, float power, int32_t n_rel, const int32_t* long_ids,
+                         int32_t n_long, const int32_t* long_cnt, float* slab,
+                         hipStream_t stream);
 
 /* Relation-embedding SpMM, forward direction.
  * Replaces DGL gspmm for graph.update_all(fn.u_mul_e('h','ew','m'), fn.sum('m','h'))

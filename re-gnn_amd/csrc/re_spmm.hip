@@ -656,6 +656,8 @@ degree_long_kernel(const int32_t* __restrict__ ptr, const float* __restrict__ ta
     }
 }
 
+constexpr int kDegCntMaxRel = 16;   // regnn_degree_cnt / _bwd: relation tables up to 16 entries
+
 __device__ __forceinline__ float dnorm_ddeg(float d, float g, float power) {
     // d/d deg of max(deg,1)^power with torch clamp semantics (gradient passes where deg >= 1)
     return d >= 1.f ? g * power * powf(d, power - 1.f) : 0.f;
@@ -694,6 +696,66 @@ degree_bwd_kernel(const int32_t* __restrict__ ptr, const uint8_t* __restrict__ r
             bins[r * kBlock + tid] += gd * float(long_cnt[(int64_t)l * n_rel + r]);
     }
     bins_flush(bins, n_rel, tid, slab, blockIdx.x);
+}
+
+// Weighted degree and its backward from the graph's per-row relation histogram cnt [n_seg, n_rel]
+// (uint16, RelPack.row_cnt: static per graph and relation-id tensor, long rows zero): a row
+// costs n_rel coalesced 2-byte reads instead of a walk over its relation ids, and the backward
+// is a reduction of gd[v] * cnt[v, r] over rows in registers (no LDS bins). The long rows are
+// then overwritten by degree_long_kernel (forward) / added from long_cnt (backward).
+__global__ void __launch_bounds__(kBlock)
+degree_cnt_kernel(const uint16_t* __restrict__ cnt, const float* __restrict__ tab,
+                  int32_t n_rel, int64_t n_seg, float power, float* __restrict__ deg,
+                  float* __restrict__ norm) {
+    __shared__ float stab[kDegCntMaxRel];
+    for (int r = threadIdx.x; r < kDegCntMaxRel; r += kBlock) stab[r] = r < n_rel ? tab[r] : 0.f;
+    __syncthreads();
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n_seg;
+         v += (int64_t)gridDim.x * kBlock) {
+        const uint16_t* c = cnt + v * n_rel;
+        float d = 0.f;
+        for (int r = 0; r < n_rel; ++r) d = fmaf(stab[r], float(c[r]), d);
+        deg[v] = d;
+        if (norm) norm[v] = powf(fmaxf(d, 1.f), power);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+degree_cnt_bwd_kernel(const uint16_t* __restrict__ cnt, const float* __restrict__ deg,
+                      const float* __restrict__ g_norm, int64_t n_seg, float power, int32_t n_rel,
+                      const int32_t* __restrict__ long_ids, int32_t n_long,
+                      const int32_t* __restrict__ long_cnt, float* __restrict__ slab) {
+    float acc[kDegCntMaxRel];
+#pragma unroll
+    for (int r = 0; r < kDegCntMaxRel; ++r) acc[r] = 0.f;
+    const int tid = threadIdx.x;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + tid; v < n_seg;
+         v += (int64_t)gridDim.x * kBlock) {
+        const float gd = dnorm_ddeg(deg[v], g_norm[v], power);
+        const uint16_t* c = cnt + v * n_rel;
+#pragma unroll
+        for (int r = 0; r < kDegCntMaxRel; ++r)
+            if (r < n_rel) acc[r] = fmaf(gd, float(c[r]), acc[r]);
+    }
+    for (int l = blockIdx.x * kBlock + tid; l < n_long; l += gridDim.x * kBlock) {
+        const int64_t v = long_ids[l];
+        const float gd = dnorm_ddeg(deg[v], g_norm[v], power);
+#pragma unroll
+        for (int r = 0; r < kDegCntMaxRel; ++r)
+            if (r < n_rel) acc[r] = fmaf(gd, float(long_cnt[(int64_t)l * n_rel + r]), acc[r]);
+    }
+    __shared__ float red[kBlock / 64][kDegCntMaxRel];
+#pragma unroll
+    for (int r = 0; r < kDegCntMaxRel; ++r) {
+        const float t = group_sum<64>(acc[r]);
+        if ((tid & 63) == 0) red[tid >> 6][r] = t;
+    }
+    __syncthreads();
+    if (tid < n_rel) {
+        float t = 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w][tid];       // fixed order
+        slab[(int64_t)blockIdx.x * n_rel + tid] = t;
+    }
 }
 
 // one block per output column k: fixed-order sum over slab rows
@@ -911,7 +973,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 16; }
+int regnn_abi_version(void) { return 17; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -1232,6 +1294,41 @@ int regnn_degree_bwd(const int32_t* ptr, const uint8_t* rel, const float* deg, c
                        dim3(kBlock), lds, stream,
                        ptr, rel, deg, g_norm, n_seg, power, n_rel, split, long_ids,
                        split > 0 ? n_long : 0, long_cnt, slab);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_degree_cnt(const uint16_t* cnt, const float* rel_table, int32_t n_rel, int64_t n_seg,
+                     float power, const int32_t* ptr, const int32_t* long_ids, int32_t n_long,
+                     const int32_t* long_cnt, float* deg, float* norm, hipStream_t stream) {
+    if (!cnt || !rel_table || !deg || n_seg < 0 || n_rel <= 0 || n_rel > kDegCntMaxRel ||
+        (n_long > 0 && (!ptr || !long_ids || !long_cnt)))
+        return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    hipLaunchKernelGGL(degree_cnt_kernel, dim3(grid_resident(degree_cnt_kernel, n_seg, kBlock, 0)),
+                       dim3(kBlock), 0, stream, cnt, rel_table, n_rel, n_seg, power, deg, norm);
+    REGNN_LAUNCH_CHECK();
+    if (n_long > 0) {
+        hipLaunchKernelGGL(degree_long_kernel, dim3(grid_for(n_long, kBlock)), dim3(kBlock), 0,
+                           stream, ptr, rel_table, long_ids, n_long, long_cnt, n_rel, power, deg,
+                           norm);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
+int regnn_degree_cnt_bwd(const uint16_t* cnt, const float* deg, const float* g_norm,
+                         int64_t n_seg, float power, int32_t n_rel, const int32_t* long_ids,
+                         int32_t n_long, const int32_t* long_cnt, float* slab,
+                         hipStream_t stream) {
+    if (!cnt || !deg || !g_norm || !slab || n_seg < 0 || n_rel <= 0 || n_rel > kDegCntMaxRel ||
+        (n_long > 0 && (!long_ids || !long_cnt)))
+        return REGNN_EINVAL;
+    if (n_seg == 0 && n_long == 0) return REGNN_OK;
+    hipLaunchKernelGGL(degree_cnt_bwd_kernel,
+                       dim3(grid_resident(degree_cnt_bwd_kernel, n_seg, kBlock, 0)),
+                       dim3(kBlock), 0, stream, cnt, deg, g_norm, n_seg, power, n_rel, long_ids,
+                       n_long, long_cnt, slab);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

@@ -50,6 +50,8 @@ _SIG = {
                               P, I32, P, P, I32, P, P, P, P, F32, I32, P], ctypes.c_int),
     "regnn_head_gh_next": ([P, I64, I32, I64, I32, P, P, P, I64, P, P, P, P, P], ctypes.c_int),
     "regnn_head_bwd": ([P, I64, I32, I64, I32, P, P, P, P, I64, P, I32, P], ctypes.c_int),
+    "regnn_degree_cnt": ([P, P, I32, I64, F32, P, P, I32, P, P, P, P], ctypes.c_int),
+    "regnn_degree_cnt_bwd": ([P, P, P, I64, F32, I32, P, I32, P, P, P], ctypes.c_int),
     "regnn_head_fwd_lse": ([P, I64, I32, P, P, I32, I64, P, I64, P, P, I32, P], ctypes.c_int),
     "regnn_head_bwd_z": ([P, I64, I32, I64, I32, P, P, P, P, I64, P, I32, P, P, F32, P, P, P, P,
                           I32, P], ctypes.c_int),
@@ -87,7 +89,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 16
+ABI_VERSION = 17
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

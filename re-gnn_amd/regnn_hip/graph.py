@@ -150,6 +150,25 @@ class RelPack:
             r = self._csc_prefix[pre.n] = _word_padded(self.rel_csc[pre.keep])
         return r
 
+    def row_cnt(self, n_rel):
+        """[n_dst, n_rel] int16 (read as uint16) relation histogram of every CSR row of at most
+        `split` edges, long rows zero (regnn_degree_cnt): static per graph and e_feat, so the
+        degree kernels read 2 n_rel bytes per row instead of walking the relation ids."""
+        key = ("rows", n_rel)
+        if key not in self._cnt:
+            rg = self.rg
+            deg = (rg.csr_ptr[1:] - rg.csr_ptr[:-1]).to(torch.int64)
+            row = torch.repeat_interleave(torch.arange(rg.n_dst, device=rg.device), deg)
+            k = row * n_rel + self.rel_csr.to(torch.int64)
+            del row
+            cnt = torch.bincount(k, minlength=rg.n_dst * n_rel).view(rg.n_dst, n_rel)
+            del k
+            plan = rg.csr_plan
+            if plan.n_long:
+                cnt[plan.long_ids.to(torch.int64)] = 0
+            self._cnt[key] = cnt.to(torch.int16).contiguous()
+        return self._cnt[key]
+
     def long_cnt(self, n_rel):
         """[n_long, n_rel] int32 relation histogram of every long CSR row."""
         plan = self.rg.csr_plan

@@ -73,11 +73,19 @@ class _DegreeNorm(torch.autograd.Function):
         n_rel = t.numel() if t is not None else 0
         plan = rg.csr_plan
         cnt = pack.long_cnt(n_rel) if (t is not None and plan.n_long) else None
-        with timed("degree", rg.E + rg.n_dst * 16):
-            L.call("regnn_degree", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr if pack else None),
-                   L.ptr(t), rg.n_dst, float(power), plan.split,
-                   L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), n_rel, L.ptr(deg), L.ptr(norm),
-                   L.stream())
+        ctx.hist = _use_row_cnt(pack, t, n_rel)
+        if ctx.hist:
+            with timed("degree", rg.n_dst * (2 * n_rel + 8)):
+                L.call("regnn_degree_cnt", L.ptr(pack.row_cnt(n_rel)), L.ptr(t), n_rel,
+                       rg.n_dst, float(power), L.ptr(rg.csr_ptr), L.ptr(plan.long_ids),
+                       plan.n_long if plan.split > 0 else 0, L.ptr(cnt), L.ptr(deg),
+                       L.ptr(norm), L.stream())
+        else:
+            with timed("degree", rg.E + rg.n_dst * 16):
+                L.call("regnn_degree", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr if pack else None),
+                       L.ptr(t), rg.n_dst, float(power), plan.split,
+                       L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), n_rel, L.ptr(deg),
+                       L.ptr(norm), L.stream())
         ctx.rg, ctx.pack, ctx.power, ctx.n_rel, ctx.shape = rg, pack, power, n_rel, tab.shape
         ctx.save_for_backward(deg)
         ctx.mark_non_differentiable(deg)
@@ -92,13 +100,30 @@ class _DegreeNorm(torch.autograd.Function):
         plan = rg.csr_plan
         slab = _slab(n_rel, rg.device)
         cnt = pack.long_cnt(n_rel) if plan.n_long else None
-        with timed("degree_bwd", rg.E + rg.n_dst * 16):
-            L.call("regnn_degree_bwd", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr), L.ptr(deg),
-                   L.ptr(g_norm.contiguous().float()), rg.n_dst, float(ctx.power), n_rel,
-                   plan.split, L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), L.ptr(slab),
-                   L.stream())
+        if ctx.hist:
+            with timed("degree_bwd", rg.n_dst * (2 * n_rel + 8)):
+                L.call("regnn_degree_cnt_bwd", L.ptr(pack.row_cnt(n_rel)), L.ptr(deg),
+                       L.ptr(g_norm.contiguous().float()), rg.n_dst, float(ctx.power), n_rel,
+                       L.ptr(plan.long_ids), plan.n_long if plan.split > 0 else 0, L.ptr(cnt),
+                       L.ptr(slab), L.stream())
+        else:
+            with timed("degree_bwd", rg.E + rg.n_dst * 16):
+                L.call("regnn_degree_bwd", L.ptr(rg.csr_ptr), L.ptr(pack.rel_csr), L.ptr(deg),
+                       L.ptr(g_norm.contiguous().float()), rg.n_dst, float(ctx.power), n_rel,
+                       plan.split, L.ptr(plan.long_ids), plan.n_long, L.ptr(cnt), L.ptr(slab),
+                       L.stream())
         g = _reduce(slab, n_rel)
         return g.view(ctx.shape), None, None, None
+
+
+# "hist": weighted degrees from the per-row relation histogram (RelPack.row_cnt,
+# regnn_degree_cnt), built once per graph; "off": walk the relation ids every call
+DEGREE = {"mode": os.environ.get("REGNN_DEGREE", "hist")}
+
+
+def _use_row_cnt(pack, t, n_rel):
+    return (DEGREE["mode"] == "hist" and pack is not None and t is not None and
+            0 < n_rel <= 16 and pack.max_rel <= n_rel and pack.rg.device.type == "cuda")
 
 
 def degree_norm(rg, pack, tab, power=-0.5):

@@ -78,3 +78,24 @@ def test_csc_prefix_keeps_edges_into_leading_rows():
         deg = pre.csc_ptr.diff()
         assert torch.equal(pre.csc_plan.long_ids.to(torch.int64), torch.nonzero(deg > 16).flatten())
         assert (pre.csc_plan.chunk_sched is not None) == (order == "source")
+
+
+def test_row_cnt_histogram():
+    """RelPack.row_cnt: per CSR row the count of each relation among its in-edges, long rows
+    (more than `split` edges) zero (regnn_degree_cnt's table)."""
+    import numpy as np
+    import torch
+    from regnn_hip.graph import RelGraph
+    rng = np.random.default_rng(2)
+    N, E, R = 200, 5000, 6
+    src = rng.integers(0, N, E)
+    dst = np.where(rng.random(E) < 0.3, 9, rng.integers(0, N, E))        # row 9 is long
+    rel = rng.integers(1, R + 1, E)
+    rg = RelGraph(src, dst, N, "cpu", split=16, chunk=8)
+    pack = rg.rel_pack(torch.from_numpy(rel), num_rel=R)
+    cnt = pack.row_cnt(R)
+    assert cnt.shape == (N, R) and cnt.dtype == torch.int16
+    want = np.zeros((N, R), np.int64)
+    np.add.at(want, (dst, rel - 1), 1)
+    want[np.bincount(dst, minlength=N) > 16] = 0
+    assert np.array_equal(cnt.numpy().astype(np.int64), want)

@@ -236,3 +236,35 @@ def test_head_ce_bf16_rows_match_widened(clobber):
     assert torch.equal(a[0], r[0]) and torch.equal(a[1], r[1])
     assert torch.equal(a[2], r[2].bfloat16().float())
     assert _rel(a[3], r[3]) < 1e-6 and _rel(a[4], r[4]) < 1e-6
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_degree_histogram_matches_walk(seed):
+    """regnn_degree_cnt / _bwd (per-row relation histogram) == regnn_degree / _bwd (relation-id
+    walk): weighted degrees, norms and the relation-table gradient, on a graph with long rows."""
+    import numpy as np
+    from regnn_hip import ops
+    from regnn_hip.graph import RelGraph
+    rng = np.random.default_rng(seed)
+    N, E, R = 3000, 60000, 11
+    src = rng.integers(0, N, E)
+    dst = np.where(rng.random(E) < 0.2, rng.integers(0, 3, E), rng.integers(0, N, E))
+    rel = rng.integers(1, R + 1, E)
+    rg = RelGraph(src, dst, N, DEV)
+    pack = rg.rel_pack(torch.from_numpy(rel).to(DEV), num_rel=R)
+    assert rg.csr_plan.n_long > 0
+    tab0 = torch.rand(R, 1, device=DEV) * 2 - 0.5
+    gn = torch.randn(N, device=DEV)
+    out = {}
+    old = ops.DEGREE["mode"]
+    try:
+        for mode in ("hist", "off"):
+            ops.DEGREE["mode"] = mode
+            tab = tab0.clone().requires_grad_(True)
+            norm = ops.degree_norm(rg, pack, tab)
+            (norm * gn).sum().backward()
+            out[mode] = (norm.detach(), tab.grad)
+    finally:
+        ops.DEGREE["mode"] = old
+    assert _rel(out["hist"][0], out["off"][0]) < 1e-6
+    assert _rel(out["hist"][1], out["off"][1]) < 1e-5
