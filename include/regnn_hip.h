@@ -34,8 +34,13 @@ typedef struct ihipStream_t* hipStream_t;
 
 enum { REGNN_OK = 0, REGNN_EINVAL = 1, REGNN_EUNSUPPORTED = 2, REGNN_ELAUNCH = 3 };
 enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
+/* Flag or-ed into the dtype of the regnn_spmm_bwd* calls: the x rows passed are the rows the
+ * forward gathered, out_scale * drop(x) (a producer that formed them, e.g. regnn_type_project),
+ * not x itself; the per-edge relation dots then take them as they are and the node gradient is
+ * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
+enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 17). */
+/* ABI version (bumped on any signature change or addition; currently 18). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -303,7 +308,8 @@ int regnn_col_sum(const float* x, int64_t rows, int32_t cols, float* slab, hipSt
  *   h [row0 + r]  = x[r] W^T + b                          (rows of the concatenated layer input)
  *   xs[row0 + r] = scale[row0 + r] * drop(h[row0 + r])     (as regnn_row_scale(h), same mask)
  * h / xs: dtype, [*, F] row-major. fp32-accurate (bf16x6 MFMA). F must be 64; K <= 256
- * (REGNN_EUNSUPPORTED above: use a GEMM + regnn_row_scale). scale may be NULL (1). */
+ * (REGNN_EUNSUPPORTED above: use a GEMM + regnn_row_scale). scale may be NULL (1). h may be
+ * NULL: only xs is written (its consumer's backward then takes xs, REGNN_SELF_PRESCALED). */
 int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_t dtype,
                        const float* W, const float* b, const float* scale,
                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,

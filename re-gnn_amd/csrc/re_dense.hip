@@ -1213,7 +1213,8 @@ type_project_kernel(const T* __restrict__ x, int64_t rows, int K, const float* _
                 for (int i = 0; i < 4; ++i) xv[i] = m[off + i] != 0.f ? xv[i] * drop_scale : 0.f;
             }
             if constexpr (sizeof(T) == 4) {
-                *reinterpret_cast<float4*>(h + g * F + f0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+                if (h)                                   // kernel-uniform (NULL: xs only)
+                    *reinterpret_cast<float4*>(h + g * F + f0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
                 *reinterpret_cast<float4*>(xs + g * F + f0) = make_float4(xv[0], xv[1], xv[2], xv[3]);
             } else {
                 uint2 hb, xb;
@@ -1221,7 +1222,7 @@ type_project_kernel(const T* __restrict__ x, int64_t rows, int K, const float* _
                 hb.y = uint32_t(f2bf(hv[2])) | (uint32_t(f2bf(hv[3])) << 16);
                 xb.x = uint32_t(f2bf(xv[0])) | (uint32_t(f2bf(xv[1])) << 16);
                 xb.y = uint32_t(f2bf(xv[2])) | (uint32_t(f2bf(xv[3])) << 16);
-                *reinterpret_cast<uint2*>(h + g * F + f0) = hb;
+                if (h) *reinterpret_cast<uint2*>(h + g * F + f0) = hb;
                 *reinterpret_cast<uint2*>(xs + g * F + f0) = xb;
             }
         }
@@ -1405,7 +1406,7 @@ int regnn_type_project(const void* x, int64_t rows, int32_t K, int32_t F, int32_
                        const uint64_t* drop_seed, uint32_t drop_keep16, float drop_scale,
                        int64_t row0, void* h, void* xs, hipStream_t stream) {
     if (rows < 0 || K <= 0 || F != kProjF || !W || !b || row0 < 0 ||
-        (rows > 0 && (!x || !h || !xs)) || (drop_seed && drop_keep16 > 65536u) ||
+        (rows > 0 && (!x || !xs)) || (drop_seed && drop_keep16 > 65536u) ||
         (reinterpret_cast<uintptr_t>(b) & 15) || (reinterpret_cast<uintptr_t>(h) & 7) ||
         (reinterpret_cast<uintptr_t>(xs) & 7))
         return REGNN_EINVAL;

@@ -65,6 +65,9 @@ struct SpmmArgs {
     const uint64_t* nx_seed;  //   nx_dscale), the row_scale_kernel spec
     uint32_t nx_thresh;
     float nx_dscale;
+    int32_t self_pre;      // backward: `self` holds out_scale * drop(x) (the gathered rows of the
+                           //   forward), not x: no mask on load, per-edge dots without out_scale,
+                           //   node grad divided by out_scale (REGNN_SELF_PRESCALED)
 };
 
 enum { kEpiLN = 1, kEpiReLU = 2 };
@@ -125,10 +128,13 @@ struct Seg {
 #pragma unroll
             for (int t = 0; t < EV; ++t) v[q][t] = raw[q][t];
         if constexpr (DROP) {
-            const uint32_t key = drop_key(a.drop_seed);
+            if (!a.self_pre) {                                     // kernel-uniform
+                const uint32_t key = drop_key(a.drop_seed);
 #pragma unroll
-            for (int q = 0; q < NV; ++q)
-                drop_apply<EV, DROP>(key, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane, v[q]);
+                for (int q = 0; q < NV; ++q)
+                    drop_apply<EV, DROP>(key, a.drop_thresh, a.drop_scale, seg, NVEC, q * LPR + lane,
+                                         v[q]);
+            }
         }
     }
 
@@ -293,6 +299,7 @@ struct Seg {
         if constexpr (BWD) {
             if (a.node_grad) {
                 float ng = dot(sx, acc);
+                if (a.self_pre) ng /= os;                          // <drop(x), acc> = <self, acc>/os
                 if (a.ng_a && a.ng_b) {
                     float ga[NV][EV], yb[NV][EV];
                     load_row(static_cast<const T*>(a.ng_a) + seg * F, F, lane, ga);
@@ -395,7 +402,7 @@ __global__ void __launch_bounds__(kBlock) spmm_main(SpmmArgs a) {
         float sx[NV][S::EV] = {}, sraw[NV][S::EV] = {};
         if (need_self) S::load_self(a, seg, lane, sx, sraw);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
+        if (beg < end) S::accumulate(a, beg, end, lane, a.self_pre ? 1.f : os, sx, acc, bins, tid);
         S::epilogue(a, seg, lane, os, sx, acc, sraw);
     }
     if constexpr (S::SLAB) bins_flush(bins, a.n_rel, tid, a.slab, a.slab_row0 + blockIdx.x);
@@ -422,7 +429,7 @@ __global__ void __launch_bounds__(kBlock) spmm_chunks(SpmmArgs a) {
         float sx[NV][S::EV] = {}, sraw[NV][S::EV] = {};
         if constexpr (S::SLAB || S::EDGE) S::load_self(a, seg, lane, sx, sraw);
         const float os = a.out_scale ? a.out_scale[seg] : 1.f;
-        if (beg < end) S::accumulate(a, beg, end, lane, os, sx, acc, bins, tid);
+        if (beg < end) S::accumulate(a, beg, end, lane, a.self_pre ? 1.f : os, sx, acc, bins, tid);
         float* part = a.chunk_partial + c * a.F;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -973,7 +980,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 17; }
+int regnn_abi_version(void) { return 18; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
@@ -1122,6 +1129,9 @@ static int spmm_bwd_impl(const int32_t* ptr, const int32_t* idx, const uint8_t* 
     a.drop_seed = drop_seed; a.drop_thresh = drop_keep16; a.drop_scale = drop_scale;
     a.nx_scale = nx_scale; a.nx_out = nx_out; a.nx_dot = nx_dot;
     if (drop_seed && (slab || edge_grad || node_grad) && !x) return REGNN_EINVAL;
+    a.self_pre = (dtype & REGNN_SELF_PRESCALED) ? 1 : 0;
+    dtype &= ~REGNN_SELF_PRESCALED;
+    if (a.self_pre && (nx_scale || edge_grad)) return REGNN_EINVAL;
     const int mode = slab ? (edge_grad ? kBwdBoth : kBwdSlab) : (edge_grad ? kBwdEdge : kBwd);
     if (dtype == REGNN_F32) return dispatch<float>(a, mode, stream);
     if (dtype == REGNN_BF16) return dispatch<bf16_t>(a, mode, stream);

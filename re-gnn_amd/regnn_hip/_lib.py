@@ -89,12 +89,13 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 17
+ABI_VERSION = 18
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")
 
 F32_CODE, BF16_CODE = 0, 1
+SELF_PRESCALED = 0x100        # or-ed into the dtype of regnn_spmm_bwd* (regnn_hip.h)
 _ERR = {1: "invalid argument", 2: "unsupported shape/dtype", 3: "kernel launch failed"}
 
 

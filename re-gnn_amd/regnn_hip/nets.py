@@ -152,7 +152,7 @@ class REGCN(nn.Module):
                     # one pass
                     return layer(self.g, None, e_feat, emit=emit, drop_seed=seeds[0],
                                  project=lambda norm, drop: ops.type_project_prescale(
-                                     self.fc_list, features_list, norm, drop))
+                                     self.fc_list, features_list, norm, drop, keep_h=False))
                 h = type_project(self.fc_list, features_list)
                 return layer(self.g, h, e_feat, emit=emit, drop_seed=seeds[0])
             prev = self.layers[i - 1]

@@ -171,7 +171,9 @@ def drop_request(p, device, seed=None):
 # gathers the finished rows; "off": the gather scales and masks every edge's row itself.
 # "prefix": an aggregation backward whose gradient is known zero past row n (the output head's
 # hand-off) gathers only the CSC edges into rows < n ("off": the whole CSC)
-PRESCALE = {"mode": "auto", "bwd": "auto", "next": "auto", "prefix": "auto"}
+# "self": the input projection skips h when the first aggregation's backward can read its
+# pre-scaled rows instead (type_project_prescale keep_h=False; "off": h always written)
+PRESCALE = {"mode": "auto", "bwd": "auto", "next": "auto", "prefix": "auto", "self": "auto"}
 
 
 def _use_prescale(x, scale, drop, backward=False):
@@ -266,6 +268,13 @@ class _ReSpmm(torch.autograd.Function):
         ctx.link, ctx.link_in = link, link_in
         ctx.rg, ctx.pack, ctx.tab_shape = rg, pack, None if tab is None else tab.shape
         ctx.same_scale = pre is not None and pre is post and rg.n_src == rg.n_dst
+        # x never written (type_project_prescale keep_h=False): the backward reads the gathered
+        # rows pre * drop(x) instead (REGNN_SELF_PRESCALED; pre is a positive degree norm)
+        ctx.self_pre = getattr(x, "_regnn_unwritten", False)
+        if ctx.self_pre:
+            if prescaled is None or pre is None or link_in is not None:
+                raise RuntimeError("re_spmm: an unwritten input needs its pre-scaled rows")
+            x = prescaled
         ctx.save_for_backward(x, y, t, pre, post)
         return y
 
@@ -325,7 +334,7 @@ class _ReSpmm(torch.autograd.Function):
                     L.ptr(t), None, L.ptr(in_scale), L.ptr(pre), L.ptr(src), L.ptr(x),
                     L.ptr(y if ctx.same_scale and node is not None and not prescale else None),
                     L.ptr(gx), L.ptr(slab), n_rel, None, L.ptr(node), rg.n_src, F,
-                    L.dtype_code(x), *plan_args)
+                    L.dtype_code(x) | (L.SELF_PRESCALED if ctx.self_pre else 0), *plan_args)
             if nx is not None:
                 nx_out = torch.empty_like(gx)
                 nx_dot = torch.empty(rg.n_src, dtype=torch.float32, device=x.device)
@@ -413,7 +422,7 @@ class _TypeProjPre(torch.autograd.Function):
     d h flows to W_t / b_t as in nets._TypeProjFn."""
 
     @staticmethod
-    def forward(ctx, n, scale, drop, *args):
+    def forward(ctx, n, scale, drop, keep_h, *args):
         xs_in, Ws, bs = args[:n], args[n:2 * n], args[2 * n:]
         rows = [x.shape[0] for x in xs_in]
         dev, dt = xs_in[0].device, xs_in[0].dtype
@@ -425,13 +434,13 @@ class _TypeProjPre(torch.autograd.Function):
         sc = None if scale is None else scale.detach().float().contiguous()
         o = 0
         with timed("type_project", sum(x.numel() * x.element_size() for x in xs_in)
-                   + 2 * h.numel() * h.element_size()):
+                   + (2 if keep_h else 1) * h.numel() * h.element_size()):
             for x, W, b, r in zip(xs_in, Ws, bs, rows):
                 x = x.contiguous()
                 L.call("regnn_type_project", L.ptr(x), r, x.shape[1], F, L.dtype_code(x),
                        L.ptr(W.detach().float().contiguous()),
                        L.ptr(b.detach().float().contiguous()), L.ptr(sc), seed, keep16, dscale,
-                       o, L.ptr(h), L.ptr(xs), L.stream())
+                       o, L.ptr(h) if keep_h else None, L.ptr(xs), L.stream())
                 o += r
         ctx.n, ctx.rows = n, rows
         ctx.save_for_backward(*xs_in, *Ws)
@@ -443,7 +452,7 @@ class _TypeProjPre(torch.autograd.Function):
     def backward(ctx, g, _gxs):
         n = ctx.n
         if g is None:
-            return (None,) * (3 + 3 * n)
+            return (None,) * (4 + 3 * n)
         saved = ctx.saved_tensors
         xs_in, Ws = saved[:n], saved[n:]
         g = g.contiguous()
@@ -452,13 +461,13 @@ class _TypeProjPre(torch.autograd.Function):
         for t, r in enumerate(ctx.rows):
             gt = g[o:o + r]
             o += r
-            if ctx.needs_input_grad[3 + t]:
+            if ctx.needs_input_grad[4 + t]:
                 gx[t] = gt @ Ws[t].to(gt.dtype)
-            if ctx.needs_input_grad[3 + n + t] or ctx.needs_input_grad[3 + 2 * n + t]:
+            if ctx.needs_input_grad[4 + n + t] or ctx.needs_input_grad[4 + 2 * n + t]:
                 w_, b_ = linear_wgrad(gt, xs_in[t])
                 gW[t] = w_.to(Ws[t].dtype)
                 gb[t] = b_.to(Ws[t].dtype)
-        return (None, None, None, *gx, *gW, *gb)
+        return (None, None, None, None, *gx, *gW, *gb)
 
 
 def type_project_fusable(fcs, feats, width=64):
@@ -471,11 +480,19 @@ def type_project_fusable(fcs, feats, width=64):
             and feats[0].dtype in (torch.float32, torch.bfloat16))
 
 
-def type_project_prescale(fcs, feats, scale, drop):
+def type_project_prescale(fcs, feats, scale, drop, keep_h=True):
     """(h, xs): the concatenated per-type projections and scale * drop(h) (model/REGCN.py:31-35
-    + the first layer's pre-scale, layer/REGraphConv.py:56,73-76) from one HIP pass per type."""
-    return _TypeProjPre.apply(len(fcs), scale, drop, *feats, *[fc.weight for fc in fcs],
-                              *[fc.bias for fc in fcs])
+    + the first layer's pre-scale, layer/REGraphConv.py:56,73-76) from one HIP pass per type.
+
+    keep_h=False: h is not written (an allocated, unwritten tensor marked `_regnn_unwritten`);
+    only an aggregation that gathers xs (re_spmm prescaled=xs) may take it, and its backward
+    then reads xs for the terms that need h (REGNN_SELF_PRESCALED)."""
+    keep_h = keep_h or PRESCALE["self"] == "off"
+    h, xs = _TypeProjPre.apply(len(fcs), scale, drop, keep_h, *feats,
+                               *[fc.weight for fc in fcs], *[fc.bias for fc in fcs])
+    if not keep_h:
+        h._regnn_unwritten = True
+    return h, xs
 
 
 def re_spmm_fused(rg, x, tab=None, pack=None, post=None, bias=None, residual=None, ln=None,

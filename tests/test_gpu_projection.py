@@ -105,3 +105,50 @@ def test_regcn_fused_projection_matches_unfused(train):
     assert g0.keys() == g1.keys()
     for k in g0:
         assert rel(g1[k], g0[k]) <= 1e-4, k
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("train", [False, True])
+def test_regcn_projection_without_h_matches(dtype, train):
+    """type_project_prescale(keep_h=False): the projection writes only the gathered rows xs and
+    layer 0's backward reads xs for its node-norm and relation terms (REGNN_SELF_PRESCALED);
+    loss and every gradient equal the run that stores h."""
+    import torch.nn.functional as F
+    from regnn_hip import nets, ops, synth
+    import dgl
+    gd = synth.mag_like(0.002, seed=4, device=DEV)
+    g = dgl.DGLGraph((gd["src"], gd["dst"]), num_nodes=gd["N"])
+    e_feat = gd["rel"].to(torch.int64)
+    feats = [f.to(dtype) for f in synth.type_features(
+        gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1, device=DEV, kind="mag")]
+    torch.manual_seed(0)
+    net = nets.REGCN(g, gd["R"], 100.0, 64, 64, 349, 2, F.elu, 0.5,
+                     [f.shape[1] for f in feats]).to(DEV)
+    with torch.no_grad():                                # relation weights of both signs
+        for layer in net.layers:
+            layer.edge_weight.uniform_(-0.005, 0.015)
+    net.train(train)
+    labels = torch.randint(0, 349, (gd["counts"]["paper"],), device=DEV)
+    W, b = net.head()
+    out = {}
+    old = dict(ops.PRESCALE)
+    try:
+        for mode in ("off", "auto"):
+            ops.PRESCALE["self"] = mode
+            ops._DROP_CTR.clear()
+            torch.manual_seed(5)
+            net.zero_grad()
+            h = net.embed(feats, e_feat)
+            _, loss = ops.head_ce(h, W, b, labels)
+            loss.backward()
+            out[mode] = (float(loss), {k: p.grad.clone() for k, p in net.named_parameters()
+                                       if p.grad is not None})
+    finally:
+        ops.PRESCALE.update(old)
+    (l0, g0), (l1, g1) = out["off"], out["auto"]
+    assert l0 == l1
+    rel = lambda a, b: float((a - b).abs().max()) / max(1e-3, float(b.abs().max()))
+    assert g0.keys() == g1.keys()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for k in g0:
+        assert rel(g1[k], g0[k]) <= tol, k
