@@ -20,7 +20,8 @@
  *  - Segments with more than `split` edges are processed by the long-segment plan
  *    (long_ids/chunk_long/chunk_off, see regnn_spmm_fwd) so hubs do not serialise one wave;
  *    split == 0 disables splitting. Results are bitwise reproducible run to run: no float
- *    atomics anywhere; cross-block reductions go through fixed-order slabs.
+ *    atomics (except regnn_ns_spmm_bwd, the sampled-block backward); cross-block reductions go
+ *    through fixed-order slabs.
  */
 #ifndef REGNN_HIP_H
 #define REGNN_HIP_H
@@ -40,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 18). */
+/* ABI version (bumped on any signature change or addition; currently 19). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -480,6 +481,64 @@ int regnn_sample_count(const int32_t* ptr, const int32_t* targets, int64_t n_tar
 int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* targets,
                       int64_t n_targets, int32_t k, uint64_t seed, const int32_t* offs,
                       int32_t* out_src, int32_t* out_eid, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Device-resident neighbour-sampled step (re_ns.hip). The same sampler spec as above, with no
+ * host sizes anywhere, so a whole mag/regnn_ns.py training step (sample, fwd, bwd, Adam) runs
+ * without a host synchronisation and can be captured in a HIP graph.
+ *
+ *  state  int64 [8] (device): [0] base seed, [1] epoch, [2] step within the epoch (this rank),
+ *         [3] global batch of the current step (the hop seeds use it), [4] step stamp (dedup
+ *         tables), [5] running count of aggregated edges (every hop's block incl. self loops).
+ *         Zero it once (then set [0], [1]); regnn_ns_batch advances [2]-[4] per step.
+ *  sizes  int32 [16] (device): [h] = |n_id| after h hops ([0] = batch size), [8 + h] = edges of
+ *         hop h's block (sampled + one self loop per target).
+ *  n_id   int32 [cap_src]: hop h's targets n_id[0, sizes[h]), it appends its new sources in
+ *         first-seen order (the sampler_oracle / PyG n_id contract).
+ *  g2l, first  uint64 [num_nodes] dedup tables: g2l zero-filled, first all-ones, once.
+ *  Per-hop scratch (cap_dst = capacity of the hop's targets, k = fan-out, cap_e = cap_dst*(k+1)):
+ *  samp, spos [cap_dst*k] int32; scnt [cap_dst] int32; gsrc [cap_e] int32; flag [cap_e] uint8;
+ *  tiles [ceil(cap_e/1024) + 1] int32, zero-filled once.
+ *  Block output (mag/regnn_layers.py:90-99 with self_loop_type 2): blk_ptr [cap_dst+1],
+ *  blk_idx [cap_e] (local source ids; row i's self loop last), blk_rel [cap_e] uint8 (edge type
+ *  etype[csr position], or num_edge_types + ntype[target] for the loop), blk_pos [cap_e] (CSR
+ *  position of the sampled edge in the global graph, -1 for the loop), inv [cap_dst] =
+ *  1 / (sampled + 1) (torch_scatter 'mean', mag/regnn_layers.py:37). Rows >= sizes[hop] empty.
+ * --------------------------------------------------------------------------------------- */
+
+/* Step prologue: rank r of `world` takes global batch g = (r + state[2] * world) mod nb of the
+ * epoch permutation perm [n_perm] (nb = ceil(n_perm / batch); every rank runs the same number of
+ * steps, a rank past the end wraps), writes its targets to n_id[0, cnt) and sizes[0] = cnt,
+ * state[3] = g, and advances state[2] and state[4]. */
+int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
+                   int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,
+                   hipStream_t stream);
+
+/* One sampling hop (replaces torch_sparse sample_adj for one layer of PyG NeighborSampler,
+ * mag/regnn_ns.py:206-214): targets n_id[0, sizes[hop]) of the global CSR (ptr, idx; etype =
+ * 0-based edge type per CSR position, ntype = node type per node), fan-out k in [1, 64], seed
+ * hop_seed(state[0], state[1], state[3], hop). Writes the block (above), appends the new nodes,
+ * sets sizes[hop + 1] and sizes[8 + hop], adds the block's edges to state[5]. */
+int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
+                 const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
+                 int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
+                 uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
+                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, int32_t* blk_ptr,
+                 int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos, float* inv,
+                 hipStream_t stream);
+
+/* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
+ * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
+ *   gx[idx_e] += rel_table[rel_e] * out_scale[v] * g[v]   (gx zero-filled by the caller; hardware
+ *                                                          float atomics: a block has no CSC)
+ *   slab[b][r] (optional) = block b's partial of sum_{e: rel_e = r} out_scale[v] <g[v], x[idx_e]>
+ *   (reduce with regnn_rel_reduce over min(n_rows, 2048) rows; zero it first).
+ * fp32 rows, F % 4 == 0. The atomics make the summation order run-dependent (the reference's
+ * torch_scatter CUDA backward is the same); every other entry point stays deterministic. */
+int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                      const float* rel_table, const float* out_scale, const float* g,
+                      const float* x, float* gx, float* slab, int32_t n_rel, int64_t n_rows,
+                      int32_t F, hipStream_t stream);
 
 #ifdef __cplusplus
 }

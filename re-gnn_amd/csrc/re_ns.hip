@@ -1,0 +1,464 @@
+// Device-resident neighbour-sampled (NS) pipeline for the ogbn-mag path (mag/regnn_ns.py):
+// the per-batch sampler that replaces torch_sparse sample_adj behind PyG NeighborSampler
+// (mag/regnn_ns.py:206-214, consumed at :399-401), built so that a whole NS training step runs
+// with no host synchronisation and can be captured in a HIP graph:
+//
+//  * every buffer is sized by its capacity (batch B, fan-outs k_h): targets of hop h fill
+//    n_id[0, n_h), the hop appends its new nodes at n_id[n_h, n_{h+1}); the counts live in a
+//    device int32 array `sizes` ([h] = n_h, [8 + h] = edges of hop h's block incl. self loops);
+//  * the sampled block of a hop is written straight in the layout its aggregation reads: CSR by
+//    target (local ids), the target's self loop last in its row (mag/regnn_layers.py:90-96),
+//    0-based relation ids (edge type, or num_edge_types + node type for the loop), 1/in-count;
+//  * first-seen de-duplication without sorting: a direct-mapped table over the global node ids
+//    (g2l: stamp << 32 | local id; first: (~stamp) << 32 | block position, 64-bit atomicMin).
+//    Entries carry the hop's stamp, so nothing is reset between hops or steps;
+//  * the flag scan runs tile-parallel with the tile offsets scanned by the last tile to finish.
+//
+// Sampler spec (bit-identical to oracle/sampler_oracle.py and to regnn_sample_fill): Floyd
+// sampling of k distinct in-edge positions per target with hash(seed, t, j), ascending order;
+// n_id = targets, then new sources in first-seen order over the target-major edge list.
+#include "regnn_common.h"
+
+namespace regnn {
+
+constexpr int kNsTile = 1024;        // block positions per flag tile (256 threads x 4)
+constexpr int kNsRowsBlock = 1024;   // the single-block row scan
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+// per-(epoch, global batch, hop) seed: sampler_oracle.hop_seed
+__device__ __forceinline__ uint64_t ns_hop_seed(const int64_t* state, int hop) {
+    const uint64_t base = uint64_t(state[0]), epoch = uint64_t(state[1]),
+                   batch = uint64_t(state[3]);
+    return mix64(base ^ mix64((epoch << 40) ^ (batch << 8) ^ uint64_t(hop)));
+}
+
+__device__ __forceinline__ uint32_t ns_stamp(const int64_t* state, int hop) {
+    return uint32_t(uint64_t(state[4]) * 8u + uint64_t(hop) + 1u);
+}
+
+__device__ __forceinline__ uint32_t ns_hash(uint64_t seed, uint64_t t, uint64_t j) {
+    return uint32_t(mix64(seed + 0x9E3779B97F4A7C15ull * (t + 1) + 0xD1B54A32D192ED03ull * (j + 1))
+                    >> 32);
+}
+
+// exclusive block scan of one int per thread; *total = block sum. lds: NT / 64 + 1 ints.
+template <int NT>
+__device__ __forceinline__ int block_exscan(int v, int* lds, int* total) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        const int s = lane < NW ? lds[lane] : 0;
+        int t = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(t, o, 64);
+            if (lane >= o) t += y;
+        }
+        if (lane < NW) lds[lane] = t - s;
+        if (lane == NW - 1) lds[NW] = t;
+    }
+    __syncthreads();
+    const int r = x - v + lds[w];
+    *total = lds[NW];
+    __syncthreads();
+    return r;
+}
+
+// step prologue: the targets of this rank's next batch (rank r of W takes global batches r,
+// r+W, ... of the epoch permutation; a rank past the last batch wraps, so every rank runs the
+// same number of steps), the batch id the hop seeds use, a new dedup stamp.
+__global__ void __launch_bounds__(kBlock)
+ns_batch_kernel(const int64_t* __restrict__ perm, int64_t n_perm, int B, int rank, int world,
+                int64_t* __restrict__ state, int32_t* __restrict__ n_id,
+                int32_t* __restrict__ sizes) {
+    __shared__ int64_t s_start, s_cnt;
+    if (threadIdx.x == 0) {
+        const int64_t nb = (n_perm + B - 1) / B;
+        const int64_t j = state[2];
+        int64_t g = int64_t(rank) + j * int64_t(world);
+        if (nb > 0) g %= nb;
+        const int64_t start = g * B;
+        int64_t cnt = n_perm - start;
+        if (cnt > B) cnt = B;
+        if (cnt < 0) cnt = 0;
+        s_start = start;
+        s_cnt = cnt;
+        state[3] = g;
+        state[2] = j + 1;
+        state[4] = state[4] + 1;
+        sizes[0] = int32_t(cnt);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < s_cnt; i += blockDim.x) n_id[i] = int32_t(perm[s_start + i]);
+}
+
+// one wave per target: Floyd sampling (regnn_sample_fill's spec) into fixed-stride slots
+__global__ void __launch_bounds__(kBlock)
+ns_sample_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                 const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
+                 int cap, int k, const int64_t* __restrict__ state, uint64_t* __restrict__ g2l,
+                 int32_t* __restrict__ samp, int32_t* __restrict__ spos,
+                 int32_t* __restrict__ scnt) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (i >= cap) return;
+    const int n = sizes[hop];
+    if (i >= n) {
+        if (lane == 0) scnt[i] = 0;
+        return;
+    }
+    const uint32_t stamp = ns_stamp(state, hop);
+    const uint64_t seed = ns_hop_seed(state, hop);
+    const int t = n_id[i];
+    if (lane == 0) g2l[t] = (uint64_t(stamp) << 32) | uint32_t(i);
+    const int b = ptr[t], d = ptr[t + 1] - b;
+    const int64_t o = int64_t(i) * k;
+    if (d <= k) {
+        for (int q = lane; q < d; q += 64) {
+            samp[o + q] = idx[b + q];
+            spos[o + q] = b + q;
+        }
+        if (lane == 0) scnt[i] = d;
+        return;
+    }
+    int slot = -1;
+    int filled = 0;
+    for (int j = d - k; j < d; ++j) {
+        const uint32_t r = ns_hash(seed, uint64_t(t), uint64_t(j));
+        const int pos = int((uint64_t(r) * uint64_t(j + 1)) >> 32);
+        const bool seen = __any(slot == pos);
+        const int pick = seen ? j : pos;
+        if (lane == filled) slot = pick;
+        ++filled;
+    }
+    int rank = 0;
+    for (int m = 0; m < k; ++m) {
+        const int other = __shfl(slot, m, 64);
+        rank += (lane < k && other < slot) ? 1 : 0;
+    }
+    if (lane < k) {
+        samp[o + rank] = idx[b + slot];
+        spos[o + rank] = b + slot;
+    }
+    if (lane == 0) scnt[i] = k;
+}
+
+// single block: row offsets (sampled count + the self loop), 1/in-count, the self-loop entries
+template <int IT>
+__global__ void __launch_bounds__(kNsRowsBlock)
+ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_id,
+               const int32_t* __restrict__ ntype, int num_edge_types, int32_t* __restrict__ sizes,
+               int hop, int cap, int64_t* __restrict__ state, int32_t* __restrict__ blk_ptr,
+               int32_t* __restrict__ blk_idx, uint8_t* __restrict__ blk_rel,
+               int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv) {
+    __shared__ int lds[kNsRowsBlock / 64 + 1];
+    const int n = sizes[hop];
+    int carry = 0;
+    for (int base = 0; base < cap; base += kNsRowsBlock * IT) {
+        const int i0 = base + threadIdx.x * IT;
+        int vals[IT];
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const int i = i0 + j;
+            vals[j] = (i < cap && i < n) ? scnt[i] + 1 : 0;
+            s += vals[j];
+        }
+        int total;
+        int off = carry + block_exscan<kNsRowsBlock>(s, lds, &total);
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const int i = i0 + j;
+            if (i < cap) {
+                blk_ptr[i] = off;
+                if (i < n) {
+                    const int lp = off + vals[j] - 1;      // the self loop closes the row
+                    blk_idx[lp] = i;
+                    blk_rel[lp] = uint8_t(ntype[n_id[i]] + num_edge_types);
+                    blk_pos[lp] = -1;
+                    gsrc[lp] = -1;
+                    inv[i] = 1.f / float(vals[j]);
+                } else {
+                    inv[i] = 1.f;
+                }
+            }
+            off += vals[j];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) {
+        blk_ptr[cap] = carry;
+        sizes[8 + hop] = carry;
+        state[5] += carry;
+    }
+}
+
+__device__ __forceinline__ uint64_t first_key(uint32_t stamp, int bp) {
+    return (uint64_t(~stamp) << 32) | uint32_t(bp);
+}
+
+// sampled slots -> block positions; candidate first occurrences of non-target sources
+__global__ void __launch_bounds__(kBlock)
+ns_place_kernel(const int32_t* __restrict__ samp, const int32_t* __restrict__ spos,
+                const int32_t* __restrict__ scnt, const int32_t* __restrict__ sizes, int hop,
+                int cap, int k, const int64_t* __restrict__ state, const uint8_t* __restrict__ etype,
+                const uint64_t* __restrict__ g2l, uint64_t* __restrict__ first,
+                const int32_t* __restrict__ blk_ptr, uint8_t* __restrict__ blk_rel,
+                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc) {
+    const int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (s >= int64_t(cap) * k) return;
+    const int i = int(s / k), r = int(s - int64_t(i) * k);
+    if (i >= sizes[hop] || r >= scnt[i]) return;
+    const uint32_t stamp = ns_stamp(state, hop);
+    const int bp = blk_ptr[i] + r;
+    const int u = samp[s], p = spos[s];
+    gsrc[bp] = u;
+    blk_rel[bp] = etype[p];
+    blk_pos[bp] = p;
+    if (uint32_t(g2l[u] >> 32) != stamp)
+        atomicMin(reinterpret_cast<unsigned long long*>(first + u),
+                  (unsigned long long)first_key(stamp, bp));
+}
+
+// first-occurrence flags per tile, tile counts; the last tile scans the tile counts and writes
+// n_{h+1}
+__global__ void __launch_bounds__(kBlock)
+ns_flags_kernel(const int32_t* __restrict__ gsrc, int32_t* __restrict__ sizes, int hop,
+                const int64_t* __restrict__ state, const uint64_t* __restrict__ g2l,
+                const uint64_t* __restrict__ first, uint8_t* __restrict__ flag,
+                int32_t* __restrict__ tiles, int n_tiles) {
+    __shared__ int lds[kBlock / 64 + 1];
+    __shared__ bool last;
+    const int E = sizes[8 + hop];
+    const uint32_t stamp = ns_stamp(state, hop);
+    const int base = blockIdx.x * kNsTile + threadIdx.x * 4;
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int bp = base + j;
+        if (bp < E) {
+            const int u = gsrc[bp];
+            const bool f = u >= 0 && uint32_t(g2l[u] >> 32) != stamp &&
+                           first[u] == first_key(stamp, bp);
+            flag[bp] = f ? 1 : 0;
+            c += f ? 1 : 0;
+        }
+    }
+    int total;
+    block_exscan<kBlock>(c, lds, &total);
+    if (threadIdx.x == 0) {
+        tiles[blockIdx.x] = total;
+        __threadfence();
+        const int ticket = atomicAdd(tiles + n_tiles, 1);
+        last = ticket == int(gridDim.x) - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    int carry = 0;
+    for (int b0 = 0; b0 < int(gridDim.x); b0 += kBlock) {
+        const int b = b0 + threadIdx.x;
+        const int v = b < int(gridDim.x) ? reinterpret_cast<volatile int32_t*>(tiles)[b] : 0;
+        int tot;
+        const int ex = block_exscan<kBlock>(v, lds, &tot);
+        if (b < int(gridDim.x)) tiles[b] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        sizes[hop + 1] = sizes[hop] + carry;
+        tiles[n_tiles] = 0;
+    }
+}
+
+// new nodes: n_id append and their local id in g2l
+__global__ void __launch_bounds__(kBlock)
+ns_finish_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes, int hop,
+                 const int64_t* __restrict__ state, const uint8_t* __restrict__ flag,
+                 const int32_t* __restrict__ tiles, uint64_t* __restrict__ g2l,
+                 int32_t* __restrict__ n_id) {
+    __shared__ int lds[kBlock / 64 + 1];
+    const int E = sizes[8 + hop];
+    const int n = sizes[hop];
+    const uint32_t stamp = ns_stamp(state, hop);
+    const int base = blockIdx.x * kNsTile + threadIdx.x * 4;
+    int f[4], c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        f[j] = base + j < E ? flag[base + j] : 0;
+        c += f[j];
+    }
+    int total;
+    int off = tiles[blockIdx.x] + block_exscan<kBlock>(c, lds, &total);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (f[j]) {
+            const int u = gsrc[base + j];
+            const int loc = n + off;
+            n_id[loc] = u;
+            g2l[u] = (uint64_t(stamp) << 32) | uint32_t(loc);
+            ++off;
+        }
+    }
+}
+
+// every sampled edge's local source id
+__global__ void __launch_bounds__(kBlock)
+ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes, int hop,
+                  const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx, int cap_e) {
+    const int bp = blockIdx.x * kBlock + threadIdx.x;
+    if (bp >= cap_e || bp >= sizes[8 + hop]) return;
+    const int u = gsrc[bp];
+    if (u >= 0) blk_idx[bp] = int32_t(uint32_t(g2l[u]));
+}
+
+// Backward of the sampled block's mean aggregation y[v] = s[v] sum_e tab[rel_e] x[idx_e] + b
+// (mag/regnn_layers.py:129,142-148 through torch_scatter's mean): per target row v the scaled
+// gradient s[v] g[v] is scattered to the gathered rows with hardware float atomics (the block's
+// sources have no CSC: a sampled hub is gathered by many targets of this batch), and the
+// relation dots <s[v] g[v], x[u]> go into per-block LDS bins -> one slab row per block.
+template <int LPR>
+__global__ void __launch_bounds__(kBlock)
+ns_spmm_bwd_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                   const uint8_t* __restrict__ rel, const float* __restrict__ tab,
+                   const float* __restrict__ out_scale, const float* __restrict__ g,
+                   const float* __restrict__ x, float* __restrict__ gx, float* __restrict__ slab,
+                   int n_rel, int64_t n_rows, int F) {
+    __shared__ float bins[256];
+    for (int r = threadIdx.x; r < n_rel; r += blockDim.x) bins[r] = 0.f;
+    __syncthreads();
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63, l = lane % LPR, sub = lane / LPR;
+    const int64_t rows_per_block = int64_t(kBlock / 64) * RPW;
+    for (int64_t v0 = int64_t(blockIdx.x) * rows_per_block; v0 < n_rows;
+         v0 += int64_t(gridDim.x) * rows_per_block) {
+        const int64_t v = v0 + (threadIdx.x >> 6) * RPW + sub;
+        if (v >= n_rows) continue;
+        const int e0 = ptr[v], e1 = ptr[v + 1];
+        if (e0 == e1) continue;
+        const float sc = out_scale ? out_scale[v] : 1.f;
+        for (int f0 = 4 * l; f0 < F; f0 += 4 * LPR) {
+            const float4 gv4 = *reinterpret_cast<const float4*>(g + v * F + f0);
+            const float gv[4] = {gv4.x * sc, gv4.y * sc, gv4.z * sc, gv4.w * sc};
+            for (int e = e0; e < e1; ++e) {
+                const int u = idx[e];
+                const int r = rel ? rel[e] : 0;
+                const float w = tab ? tab[r] : 1.f;
+                float* dst = gx + int64_t(u) * F + f0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) unsafeAtomicAdd(dst + i, w * gv[i]);
+                if (slab) {
+                    const float4 xv = *reinterpret_cast<const float4*>(x + int64_t(u) * F + f0);
+                    float d = gv[0] * xv.x + gv[1] * xv.y + gv[2] * xv.z + gv[3] * xv.w;
+                    d = group_sum<LPR>(d);
+                    if (l == 0) atomicAdd(bins + r, d);
+                }
+            }
+        }
+    }
+    if (!slab) return;
+    __syncthreads();
+    for (int r = threadIdx.x; r < n_rel; r += blockDim.x) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
+}
+
+}  // namespace regnn
+
+using namespace regnn;
+
+extern "C" {
+
+int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
+                   int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,
+                   hipStream_t stream) {
+    if (!perm || !state || !n_id || !sizes || n_perm < 0 || batch <= 0 || world <= 0 ||
+        rank < 0 || rank >= world)
+        return REGNN_EINVAL;
+    hipLaunchKernelGGL(ns_batch_kernel, dim3(1), dim3(kBlock), 0, stream, perm, n_perm, batch,
+                       rank, world, state, n_id, sizes);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
+                 const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
+                 int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
+                 uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
+                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, int32_t* blk_ptr,
+                 int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos, float* inv,
+                 hipStream_t stream) {
+    if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
+        !samp || !spos || !scnt || !gsrc || !flag || !tiles || !blk_ptr || !blk_idx ||
+        !blk_rel || !blk_pos || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
+        return REGNN_EINVAL;
+    if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
+    const int64_t cap_e = int64_t(cap_dst) * (k + 1);
+    if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
+    const int n_tiles = int((cap_e + kNsTile - 1) / kNsTile);
+    hipLaunchKernelGGL(ns_sample_kernel, dim3((cap_dst + 3) / 4), dim3(kBlock), 0, stream, ptr,
+                       idx, n_id, sizes, hop, cap_dst, k, state, g2l, samp, spos, scnt);
+    REGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL((ns_rows_kernel<16>), dim3(1), dim3(kNsRowsBlock), 0, stream, scnt, n_id,
+                       ntype, num_edge_types, sizes, hop, cap_dst, state, blk_ptr, blk_idx,
+                       blk_rel, blk_pos, gsrc, inv);
+    REGNN_LAUNCH_CHECK();
+    const int64_t slots = int64_t(cap_dst) * k;
+    hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, stream, samp, spos, scnt, sizes, hop, cap_dst, k, state,
+                       etype, g2l, first, blk_ptr, blk_rel, blk_pos, gsrc);
+    REGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ns_flags_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes, hop,
+                       state, g2l, first, flag, tiles, n_tiles);
+    REGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ns_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes, hop,
+                       state, flag, tiles, g2l, n_id);
+    REGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, int(cap_e));
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                      const float* rel_table, const float* out_scale, const float* g,
+                      const float* x, float* gx, float* slab, int32_t n_rel, int64_t n_rows,
+                      int32_t F, hipStream_t stream) {
+    if (!ptr || !idx || !g || !gx || n_rows < 0 || F <= 0 || (F & 3) || n_rel < 0 ||
+        n_rel > 256 || (slab && (!x || !rel || !rel_table || n_rel == 0)))
+        return REGNN_EINVAL;
+    if (n_rows == 0) return REGNN_OK;
+    const int nvec = F / 4;
+    int lpr = 16;                      // lanes per row: the largest power of two <= 16 dividing F/4
+    while (nvec % lpr) lpr >>= 1;
+    const int64_t rpb = int64_t(kBlock / 64) * (64 / lpr);
+    int64_t grid = (n_rows + rpb - 1) / rpb;
+    if (grid > kMaxGrid) grid = kMaxGrid;
+    if (grid < 1) grid = 1;
+#define NSB_CASE(L)                                                                            \
+    if (lpr == L) {                                                                            \
+        hipLaunchKernelGGL((ns_spmm_bwd_kernel<L>), dim3((unsigned)grid), dim3(kBlock), 0,     \
+                           stream, ptr, idx, rel, rel_table, out_scale, g, x, gx, slab, n_rel, \
+                           n_rows, F);                                                         \
+        REGNN_LAUNCH_CHECK();                                                                  \
+        return REGNN_OK;                                                                       \
+    }
+    NSB_CASE(16) NSB_CASE(8) NSB_CASE(4) NSB_CASE(2) NSB_CASE(1)
+#undef NSB_CASE
+    return REGNN_EUNSUPPORTED;
+}
+
+}  // extern "C"

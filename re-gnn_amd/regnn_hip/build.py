@@ -3,11 +3,16 @@
     python -m regnn_hip.build          (from re-gnn_amd/)   or   __graft_entry__.build()
 
 Compiles every csrc/*.hip to an object (in parallel), links one shared library next to this file.
-Rebuilds only when a source or header is newer than the library.
+Freshness is decided by content, not mtime: the library is rebuilt unless its sidecar
+``libregnn_hip.so.hash`` holds the SHA-256 of every source, header and build flag AND the library
+reports the ABI version include/regnn_hip.h declares.
 """
 import concurrent.futures as cf
+import ctypes
 import glob
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -16,6 +21,7 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 LIB = os.path.join(HERE, "libregnn_hip.so")
+HASH = LIB + ".hash"
 OBJDIR = os.path.join(PKG, "build")
 ARCH = os.environ.get("REGNN_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -28,14 +34,42 @@ def _sources():
 
 
 def _deps():
-    return _sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return sorted(_sources() + glob.glob(os.path.join(CSRC, "*.h")) +
+                  glob.glob(os.path.join(INCLUDE, "*.h")))
+
+
+def source_hash():
+    """SHA-256 over the kernel sources, headers and compiler flags (also keys the committed
+    rocprofv3 counter summaries in profiles/ to the code they were measured on)."""
+    h = hashlib.sha256()
+    for p in _deps():
+        h.update(os.path.relpath(p, os.path.dirname(PKG)).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()
+
+
+def header_abi():
+    with open(os.path.join(INCLUDE, "regnn_hip.h")) as f:
+        m = re.search(r"ABI version \(.*?currently (\d+)\)", f.read(), re.S)
+    return int(m.group(1)) if m else None
+
+
+def _lib_abi():
+    try:
+        return int(ctypes.CDLL(LIB).regnn_abi_version())
+    except OSError:
+        return None
 
 
 def up_to_date():
-    if not os.path.exists(LIB):
+    if not (os.path.exists(LIB) and os.path.exists(HASH)):
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(p) <= t for p in _deps() + [__file__])
+    with open(HASH) as f:
+        if f.read().strip() != source_hash():
+            return False
+    return _lib_abi() == header_abi()
 
 
 def _compile(src):
@@ -50,6 +84,7 @@ def _compile(src):
 def build(force=False, verbose=True):
     if not force and up_to_date():
         return LIB
+    digest = source_hash()
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
@@ -60,6 +95,11 @@ def build(force=False, verbose=True):
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(HASH, "w") as f:
+        f.write(digest + "\n")
+    if _lib_abi() != header_abi():
+        raise RuntimeError(f"built library reports ABI {_lib_abi()}, header declares "
+                           f"{header_abi()}")
     if verbose:
         print(f"[regnn_hip] built {LIB} ({len(srcs)} sources, {ARCH})", file=sys.stderr)
     return LIB

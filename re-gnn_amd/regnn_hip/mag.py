@@ -12,7 +12,7 @@ import torch.nn.functional as F
 from torch.nn import Linear, ModuleDict, ModuleList, Parameter, ParameterDict, init
 
 from . import ops
-from .graph import RelGraph, SegPlan, _word_padded
+from .graph import RelGraph
 
 
 def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_types,
@@ -29,53 +29,6 @@ def make_block(edge_index, edge_type, target_node_type, n_src, n_dst, num_edge_t
     rg = RelGraph(src, dst, n_src, src.device, num_dst=n_dst)
     pack = rg.rel_pack(et + 1)
     return rg, pack
-
-
-class _Block:
-    """CSR/CSC of one sampled block built from the sampler's dst-major output without sorting the
-    CSR side and with host syncs only for the CSC long-segment plan (RelGraph-compatible for
-    ops.re_spmm). Self loops are placed last in every target row (mag/regnn_layers.py:90-96)."""
-
-    def __init__(self, adj, edge_type, target_node_type, num_edge_types):
-        (ei, _, (n_src, n_dst)) = adj.edge_index, adj.e_id, adj.size
-        src_l, dst_l = ei[0], ei[1]
-        dev = src_l.device
-        M = src_l.numel()
-        self.device, self.n_src, self.n_dst, self.E = dev, n_src, n_dst, M + n_dst
-        cnt = adj.counts.to(torch.int64) + 1
-        ptr = torch.zeros(n_dst + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(cnt, 0, out=ptr[1:])
-        posn = torch.arange(M, device=dev) + dst_l          # rows keep the sampled order
-        loop_pos = ptr[1:] - 1
-        ar = torch.arange(n_dst, device=dev)
-        idx = torch.empty(self.E, dtype=torch.int64, device=dev)
-        idx[posn] = src_l
-        idx[loop_pos] = ar
-        dst_all = torch.empty_like(idx)
-        dst_all[posn] = dst_l
-        dst_all[loop_pos] = ar
-        rel = torch.empty(self.E, dtype=torch.uint8, device=dev)
-        rel[posn] = edge_type.to(torch.uint8)
-        rel[loop_pos] = (target_node_type + num_edge_types).to(torch.uint8)
-        self.csr_ptr = ptr.to(torch.int32)
-        self.csr_idx = idx.to(torch.int32)
-        perm = torch.sort(idx, stable=True)[1]
-        self.csc_idx = dst_all[perm].to(torch.int32)
-        self.csc2csr = perm.to(torch.int32).contiguous()      # CSC position -> CSR position
-        ccnt = torch.zeros(n_src, dtype=torch.int64, device=dev).index_add_(
-            0, idx, torch.ones_like(idx))
-        cptr = torch.zeros(n_src + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(ccnt, 0, out=cptr[1:])
-        self.csc_ptr = cptr.to(torch.int32)
-        self.csr_plan = SegPlan.none()                       # rows <= fan-out + 1
-        self.csc_plan = SegPlan(self.csc_ptr)
-        self.pack = type("BlockPack", (), {})()
-        self.pack.rel_csr = _word_padded(rel)
-        self.pack.rel_csc = _word_padded(rel[perm])
-        self._inv = (1.0 / cnt.to(torch.float32)).contiguous()
-
-    def inv_in_count(self):
-        return self._inv
 
 
 class REGCNConv(torch.nn.Module):
@@ -112,25 +65,78 @@ class REGCNConv(torch.nn.Module):
 
     def forward(self, x, edge_index, edge_type=None, target_node_type=None,
                 return_weights=False):
-        if self.use_softmax:
-            raise NotImplementedError("use_softmax=True (global-max softmax) is not on the HIP path")
         x_src, x_target = x
-        if isinstance(edge_index, tuple):           # pre-built (RelGraph, RelPack) block
-            rg, pack = edge_index
-        else:
-            rg, pack = make_block(edge_index, edge_type, target_node_type, x_src.shape[0],
-                                  x_target.shape[0], self.num_edge_types, self.self_loop_type)
         xs = torch.matmul(x_src, self.weight)                                    # :102
         tab = F.leaky_relu(self.relation_weight * self.scaling_factor)           # :110-111
-        # mean of ew * x_j over in-edges incl. self loops, + bias (:113,129,142-148)
-        out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
+        # mean of ew * x_j over in-edges incl. self loops, + bias (:113,129,142-148); the
+        # use_softmax / degree-normalised ew of :116-126 is computed there but propagate() gets
+        # the raw edge_weight, so neither changes the output (only return_weights shows ew)
+        if getattr(edge_index, "is_ns_block", False):             # device-sampled block
+            blk = edge_index
+            out = ops.ns_spmm(blk, xs, tab, bias=self.bias)
+        else:
+            if isinstance(edge_index, tuple):       # pre-built (RelGraph, RelPack) block
+                rg, pack = edge_index
+            else:
+                rg, pack = make_block(edge_index, edge_type, target_node_type, x_src.shape[0],
+                                      x_target.shape[0], self.num_edge_types,
+                                      self.self_loop_type)
+            out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
         if self.residual:
             out = out + torch.matmul(x_target, self.weight)                      # :104,131-132
         if self.use_norm in ('bn', 'ln'):
             out = self.norm(out)                                                 # :134-135
         if return_weights:
-            return out, None, tab
+            return out, self._edge_weights(edge_index, edge_type, target_node_type, tab,
+                                           x_target.shape[0]), tab
         return out
+
+    def _edge_weights(self, edge_index, edge_type, target_node_type, tab, n_dst):
+        """ew of mag/regnn_layers.py:110-126 per edge in the reference's order (sampled edges,
+        then the appended self loops): softmax of tab[type] over each target's in-edges with the
+        global max subtracted and + 1e-16 (mag/utils.py:45-57) when use_softmax, else
+        tab[type] / weighted in-degree (weighted_degree, mag/utils.py:15-21)."""
+        if not isinstance(edge_index, torch.Tensor):
+            raise ValueError("return_weights needs the edge_index / edge_type tensors")
+        col = edge_index[1].to(torch.int64)
+        et = edge_type.to(torch.int64)
+        if self.self_loop_type == 2:
+            loop = torch.arange(n_dst, device=col.device)
+            col = torch.cat([col, loop])
+            et = torch.cat([et, target_node_type.to(torch.int64) + self.num_edge_types])
+        with torch.no_grad():
+            w = tab.detach()[et]
+            if self.use_softmax:
+                e = (w - w.max()).exp()
+                den = torch.zeros(n_dst, dtype=e.dtype, device=e.device).index_add_(0, col, e)
+                return e / (den[col] + 1e-16)
+            deg = torch.zeros(n_dst, dtype=w.dtype, device=w.device).index_add_(0, col, w)
+            return w * deg.pow(-1.0)[col]
+
+
+def _typed_block(adj, edge_type, ntype_dst, n_id, size, num_edge_types):
+    """NSBlock of a sampled Adj (dst-major edge_index, per-target counts) with its relation ids
+    from the caller's edge_type (mag/regnn_layers.py:90-99): sampled edges in order, the target's
+    self loop last in its row. Device ops only, sizes from the Adj."""
+    from .ns import NSBlock
+    ei, e_id = adj.edge_index, adj.e_id
+    n_src, n_dst = size
+    dev = ei.device
+    M = ei.shape[1]
+    cnt = adj.counts.to(torch.int64) + 1
+    ptr = torch.zeros(n_dst + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, out=ptr[1:])
+    posn = torch.arange(M, device=dev) + ei[1]
+    loop_pos = ptr[1:] - 1
+    E = M + n_dst
+    idx = torch.empty(E, dtype=torch.int32, device=dev)
+    idx[posn] = ei[0].to(torch.int32)
+    idx[loop_pos] = torch.arange(n_dst, device=dev, dtype=torch.int32)
+    rel = torch.empty(E, dtype=torch.uint8, device=dev)
+    rel[posn] = edge_type[e_id].to(torch.uint8)
+    rel[loop_pos] = (ntype_dst + num_edge_types).to(torch.uint8)
+    inv = (1.0 / cnt.to(torch.float32)).contiguous()
+    return NSBlock(ptr.to(torch.int32), idx, rel, None, inv, n_dst, n_src, E, dev)
 
 
 def _block_of(x_src, x_dst, edge_index, edge_type, target_node_type, num_edge_types,
@@ -356,9 +362,14 @@ class REGNN(torch.nn.Module):
             edge_index, e_id, size = adj
             x_target = x[:size[1]]
             ntype = ntype[:size[1]]
-            if getattr(adj, "counts", None) is not None and self.self_loop_type == 2:
-                blk = _Block(adj, edge_type[e_id], ntype, self.num_edge_types)
-                x = self.convs[i]((x, x_target), (blk, blk.pack))
+            blk = edge_index if getattr(edge_index, "is_ns_block", False) else \
+                getattr(adj, "block", None)
+            if blk is not None and self.model == 'regcn' and self.self_loop_type == 2:
+                x = self.convs[i]((x, x_target), blk)          # relation ids formed on device
+            elif (self.model == 'regcn' and self.self_loop_type == 2 and
+                  getattr(adj, "counts", None) is not None):
+                x = self.convs[i]((x, x_target), _typed_block(adj, edge_type, ntype, n_id, size,
+                                                              self.num_edge_types))
             else:
                 x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
             x = F.relu(x)

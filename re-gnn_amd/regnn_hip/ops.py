@@ -528,6 +528,57 @@ def re_spmm_fused(rg, x, tab=None, pack=None, post=None, bias=None, residual=Non
 
 
 # ---------------------------------------------------------------------------------------------
+_NO_PLAN = (0, 0, None, 0, None, None, 0, None, None, 0, None)
+
+
+class _NsSpmm(torch.autograd.Function):
+    """y[v] = inv[v] * sum_{e in row v} tab[rel_e] * x[idx_e] + bias over a sampled block
+    (regnn_hip.ns.NSBlock: rows <= fan-out + 1, no long-row plan, no host sizes)."""
+
+    @staticmethod
+    def forward(ctx, x, tab, bias, blk):
+        x = x.contiguous()
+        if x.dtype != torch.float32:
+            raise TypeError("ns_spmm: the sampled-block aggregation runs on fp32 rows")
+        F = x.shape[1]
+        y = torch.empty(blk.n_dst, F, dtype=x.dtype, device=x.device)
+        t = _flat_table(tab)
+        with timed("ns_spmm_fwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_fwd")):
+            L.call("regnn_spmm_fwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
+                   L.ptr(blk.rel if t is not None else None), L.ptr(t), None, None,
+                   L.ptr(blk.inv), L.ptr(None if bias is None else bias.detach().float().contiguous()),
+                   L.ptr(x), L.ptr(y), blk.n_dst, F, L.F32_CODE, *_NO_PLAN, L.stream())
+        ctx.blk, ctx.tab_shape = blk, None if tab is None else tab.shape
+        ctx.save_for_backward(x, t)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, t = ctx.saved_tensors
+        blk = ctx.blk
+        need_x, need_tab, _, = ctx.needs_input_grad[:3]
+        gy = gy.contiguous().float()
+        F = x.shape[1]
+        gx = torch.zeros_like(x)
+        n_rel = t.numel() if t is not None else 0
+        slab = _slab(n_rel, x.device) if (need_tab and t is not None) else None
+        with timed("ns_spmm_bwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_bwd")):
+            L.call("regnn_ns_spmm_bwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
+                   L.ptr(blk.rel if t is not None else None), L.ptr(t), L.ptr(blk.inv), L.ptr(gy),
+                   L.ptr(x), L.ptr(gx), L.ptr(slab), n_rel, blk.n_dst, F, L.stream())
+        g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
+        g_bias = gy.sum(0) if ctx.needs_input_grad[2] else None
+        return (gx if need_x else None), g_tab, g_bias, None
+
+
+def ns_spmm(blk, x, tab=None, bias=None):
+    """mean aggregation of a sampled block with the relation table and the bias fused
+    (mag/regnn_layers.py:110-148: ew = LeakyReLU(rw)[type], propagate aggr='mean', update +bias).
+    x holds the block's source rows (>= blk.n_src rows; rows past the sampled ones unread)."""
+    return _NsSpmm.apply(x, tab, bias, blk)
+
+
+# ---------------------------------------------------------------------------------------------
 class _EdgeSpmm(torch.autograd.Function):
     """y[v] = sum_{e: u->v} ew[e] * x[u]; ew per edge in the caller's edge order."""
 

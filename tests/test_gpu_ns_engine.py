@@ -1,0 +1,261 @@
+"""GPU checks of the device-resident NS step (regnn_hip.ns: regnn_ns_batch / regnn_ns_hop /
+regnn_ns_spmm_bwd, mag/regnn_ns.py:206-214,392-420):
+
+* the capacity-sized sampler is bit-exact against oracle/sampler_oracle.py (n_id, edge lists,
+  e_id, block layout) including a partial last batch;
+* one NSTrainer step (no host sizes) gives the same loss and parameter gradients as the
+  PyG-style path (NeighborSampler + mag.train_step) on the same batch;
+* the HIP-graph replay of the step tracks the eager step;
+* data parallelism: the gradient of the union batch equals the mean of its two halves'
+  gradients (the DP all-reduce's contract);
+* one step at the BASELINE config-5 scale (mag_like(10), batch 512, fan-out [25, 20]): sampled
+  rows against the oracle spec, sampler properties, and block aggregation rows against fp64.
+"""
+import numpy as np
+import pytest
+import torch
+
+import _golden as G
+from oracle import sampler_oracle as SO
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _mag(scale, seed=0, F=16, hidden=32, classes=5, dropout=0.0):
+    from regnn_hip import mag, synth
+    from regnn_hip.graph import RelGraph
+    gd = synth.mag_like(scale, seed=seed, device=DEV)
+    keep = gd["rel"] <= 7
+    rg = RelGraph(gd["src"][keep], gd["dst"][keep], gd["N"], DEV)
+    edge_type = gd["rel"][keep].to(torch.int64) - 1
+    del keep
+    node_type = gd["ntype"]
+    offs = torch.tensor([gd["type_offsets"][t] for t in synth.NTYPES], device=DEV)
+    local = torch.arange(gd["N"], device=DEV) - offs[node_type]
+    feats = synth.type_features(gd["counts"], {t: F for t in synth.NTYPES}, seed=1, device=DEV)
+    x_dict = {k: f for k, f in enumerate(feats)}
+    n_paper = gd["counts"]["paper"]
+    y = torch.full((gd["N"], 1), -1, dtype=torch.int64, device=DEV)
+    y[:n_paper, 0] = (torch.arange(n_paper, device=DEV) * 7) % classes
+
+    def model(seed=0):
+        torch.manual_seed(seed)
+        m = mag.REGNN(F, hidden, classes, 2, 10.0, dropout, {k: F for k in x_dict}, 7,
+                      use_norm="ln", self_loop_type=2).to(DEV)
+        with torch.no_grad():
+            for conv in m.convs:
+                conv.relation_weight.copy_(torch.linspace(0.02, 0.12, 11, device=DEV))
+                conv.bias.normal_(0, 0.1)
+        return m
+
+    return dict(gd=gd, rg=rg, edge_type=edge_type, node_type=node_type, local=local,
+                x_dict=x_dict, y=y, n_paper=n_paper, model=model)
+
+
+def _oracle_csr(rg):
+    return rg.csr_ptr.cpu().numpy(), rg.csr_idx.cpu().numpy(), rg.csr_eid.cpu().numpy()
+
+
+def test_device_sampler_bit_exact_partial_batch():
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.ns import DeviceSampler
+    rng = np.random.default_rng(3)
+    N, E = 4000, 60000
+    dst = np.minimum((rng.pareto(1.1, E) * 4).astype(np.int64), N - 1)
+    src = rng.integers(0, N, E)
+    et = rng.integers(0, 7, E)
+    nt = rng.integers(0, 4, N)
+    rg = RelGraph(src, dst, N, DEV)
+    ptr, idx, eid = _oracle_csr(rg)
+    ds = DeviceSampler(rg, [9, 5], 100, etype=torch.from_numpy(et), ntype=torch.from_numpy(nt),
+                       num_edge_types=7)
+    for bi, batch in enumerate([np.arange(0, 100), rng.permutation(N)[:37], np.array([11])]):
+        ds.set_seed(99, 2, bi)
+        ds.set_targets(torch.from_numpy(batch).to(DEV))
+        ds.run_hops()
+        n_total, hops = ds.exact_adjs()
+        _, rn_id, radjs = SO.neighbor_sample(ptr, idx, batch.tolist(), [9, 5], 99, epoch=2,
+                                             batch_idx=bi)
+        assert ds.n_id[:n_total].cpu().tolist() == rn_id
+        for (ei, e_id, size, blk, cnt), (s, d, e, rsize) in zip(hops, radjs[::-1]):
+            assert tuple(size) == tuple(rsize)
+            assert ei[0].cpu().tolist() == s and ei[1].cpu().tolist() == d
+            assert e_id.cpu().tolist() == [int(eid[p]) for p in e]
+            # block layout: row v = its sampled edges in order, then its self loop
+            p_ = blk.csr_ptr.cpu().numpy()
+            ix, rl, ps = blk.csr_idx.cpu().numpy(), blk.rel.cpu().numpy(), blk.pos.cpu().numpy()
+            n_dst = size[1]
+            tgt = np.asarray(rn_id[:n_dst])
+            assert p_[0] == 0 and np.all(np.diff(p_) == cnt.cpu().numpy() + 1)
+            assert np.all(ix[p_[1:] - 1] == np.arange(n_dst))
+            assert np.all(rl[p_[1:] - 1] == 7 + nt[tgt])
+            keep = ps >= 0
+            assert np.all(rl[keep] == et[eid[ps[keep]]])
+            inv = blk.inv.cpu().numpy()
+            assert np.allclose(inv, 1.0 / np.diff(p_))
+
+
+def _setup_trainer(d, model, batch=64, sizes=(6, 4), seed=3, lr=1e-2):
+    from regnn_hip.ns import NSTrainer
+    opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True)
+    return NSTrainer(model, opt, d["rg"], list(sizes), batch,
+                     torch.arange(d["n_paper"], device=DEV), d["x_dict"], d["edge_type"],
+                     d["node_type"], d["local"], d["y"], 7, seed=seed), opt
+
+
+def test_trainer_step_matches_pyg_path():
+    """one device-engine step == NeighborSampler + mag.train_step on the same batch (loss and
+    every parameter gradient at 1e-5)."""
+    from regnn_hip import mag
+    from regnn_hip.sampler import NeighborSampler
+    d = _mag(0.003, seed=1)
+    m_api, m_eng = d["model"](), d["model"]()
+    m_api.train(); m_eng.train()
+    smp = NeighborSampler(d["rg"], torch.arange(d["n_paper"], device=DEV), [6, 4], batch_size=64,
+                          shuffle=True, seed=3)
+    batch = next(iter(smp))
+    opt_api = torch.optim.SGD(m_api.parameters(), lr=0.0)
+    loss_api = mag.train_step(m_api, opt_api, batch, d["x_dict"], d["edge_type"], d["node_type"],
+                              d["local"], d["y"], 1)
+    tr, _ = _setup_trainer(d, m_eng)
+    tr._forward_backward()
+    torch.cuda.synchronize()
+    assert abs(float(tr.loss) - float(loss_api)) <= 1e-5 * max(1.0, abs(float(loss_api)))
+    assert int(tr.sampler.sizes[0]) == 64
+    gp = dict(m_api.named_parameters())
+    for n, p in m_eng.named_parameters():
+        ok, err = G.close(p.grad.cpu().numpy(), gp[n].grad.cpu().numpy().astype(np.float64), 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+
+
+def test_trainer_graph_replay_tracks_eager():
+    d = _mag(0.003, seed=2)
+    tr_e, _ = _setup_trainer(d, d["model"](7), batch=128, sizes=(10, 5))
+    tr_g, _ = _setup_trainer(d, d["model"](7), batch=128, sizes=(10, 5))
+    # capture's warm-up runs optimizer steps: give the eager twin the same steps
+    tr_g.capture(warmup=2)
+    for _ in range(2):
+        tr_e.step()
+    tr_e.sampler.state[2:3].zero_()
+    le, lg = [], []
+    for _ in range(6):
+        tr_e.step()
+        le.append(float(tr_e.loss))
+        tr_g.replay()
+        lg.append(float(tr_g.loss))
+    assert np.all(np.isfinite(lg))
+    assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
+    assert tr_g.edges_total() > 0
+
+
+def test_trainer_epoch_wraps_and_counts():
+    """steps_per_epoch = ceil(ceil(n/B) / W); the last batch of an epoch is partial."""
+    d = _mag(0.002, seed=4)
+    tr, _ = _setup_trainer(d, d["model"](), batch=100, sizes=(4, 3))
+    n = d["n_paper"]
+    steps = tr.steps_per_epoch()
+    assert steps == -(-n // 100)
+    seen = []
+    for _ in range(steps):
+        tr.step()
+        seen.append(tr.sampler.n_id[:int(tr.sampler.sizes[0])].cpu())
+    allt = torch.cat(seen)
+    assert sorted(allt.tolist()) == list(range(n))       # one epoch covers every target once
+    assert int(tr.sampler.sizes[0]) == n - 100 * (steps - 1)
+
+
+def test_dp_union_gradient_equals_mean_of_halves():
+    """per-target samples are keyed on (hop seed, node): two half-batches sampled with the batch
+    index of their union see the same neighbourhoods, so mean(grad(half_a), grad(half_b)) equals
+    grad(union) -- what the flat-bucket all-reduce computes across two ranks."""
+    from regnn_hip import mag
+    from regnn_hip.sampler import NeighborSampler
+    d = _mag(0.003, seed=5)
+    smp = NeighborSampler(d["rg"], torch.arange(d["n_paper"], device=DEV), [8, 5], batch_size=128,
+                          shuffle=False, seed=11)
+    union = torch.randperm(d["n_paper"], generator=torch.Generator().manual_seed(0))[:128].to(DEV)
+    grads = []
+    for part in (union, union[:64], union[64:]):
+        m = d["model"]()
+        m.train()
+        opt = torch.optim.SGD(m.parameters(), lr=0.0)
+        mag.train_step(m, opt, smp.sample(part, 4), d["x_dict"], d["edge_type"], d["node_type"],
+                       d["local"], d["y"], 1)
+        grads.append({n: p.grad.double().cpu() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        mean = 0.5 * (grads[1][n] + grads[2][n])
+        err = (mean - grads[0][n]).abs().max().item()
+        scale = max(1e-3, grads[0][n].abs().max().item())
+        assert err <= 2e-6 * scale, f"{n}: {err:.3e} (scale {scale:.3e})"
+
+
+def test_ns_step_mag10_scale():
+    """BASELINE config 5 at its own size: mag_like(10) (19.4 M nodes, 422 M raw edges), batch 512,
+    fan-out [25, 20]: one device-engine step; sampled targets against the oracle spec (sampled
+    rows re-derived with sampler_oracle.sample_row from the CSR rows), count = min(deg, k),
+    unique n_id, and block aggregation rows against fp64 sums."""
+    from regnn_hip import ops
+    d = _mag(10.0, seed=0, F=128, hidden=64, classes=349)
+    rg = d["rg"]
+    model = d["model"]()
+    model.train()
+    tr, _ = _setup_trainer(d, model, batch=512, sizes=(25, 20), seed=123)
+    tr.step()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(tr.loss))
+    s = tr.sampler
+    sz = s.sizes.cpu().tolist()
+    n_id = s.n_id[:sz[2]].cpu().numpy()
+    assert np.unique(n_id).size == n_id.size
+    ptr_d = rg.csr_ptr
+    st = s.state.cpu().numpy()
+    from regnn_hip.sampler import hop_seed
+    rng = np.random.default_rng(0)
+    for h, k in enumerate((25, 20)):
+        blk = s.blocks[h]
+        n_dst, E = sz[h], sz[8 + h]
+        bp = blk.csr_ptr[:n_dst + 1].cpu().numpy()
+        tgt = n_id[:n_dst]
+        deg = (ptr_d[1:] - ptr_d[:-1]).cpu().numpy()[tgt]
+        assert np.all(np.diff(bp) == np.minimum(deg, k) + 1)
+        assert E == bp[-1]
+        pos = blk.pos[:E].cpu().numpy()
+        idx_l = blk.csr_idx[:E].cpu().numpy()
+        seed = hop_seed(int(st[0]) & ((1 << 64) - 1), int(st[1]), int(st[3]), h)
+        for v in rng.choice(n_dst, size=24, replace=False):
+            t = int(tgt[v])
+            a, b = int(ptr_d[t]), int(ptr_d[t + 1])
+            row_idx = rg.csr_idx[a:b].cpu().numpy()
+            # the oracle's row sampler (keyed on the global target id) on this CSR row
+            want_src, want_pos = _sample_row_global(row_idx, t, k, seed, a)
+            got_pos = pos[bp[v]:bp[v + 1] - 1]
+            assert got_pos.tolist() == want_pos
+            assert n_id[idx_l[bp[v]:bp[v + 1] - 1]].tolist() == want_src
+    # layer-0 block aggregation rows (the outermost hop) against fp64 sums
+    blk = s.blocks[1]
+    n_dst = sz[1]
+    x = torch.randn(s.caps[2], 64, device=DEV)
+    tab = torch.linspace(-0.3, 1.2, 11, device=DEV)
+    bias = torch.randn(64, device=DEV)
+    y = ops.ns_spmm(blk, x, tab, bias).cpu().double().numpy()
+    xd = x.cpu().double().numpy()
+    bp = blk.csr_ptr.cpu().numpy()
+    ix, rl = blk.csr_idx.cpu().numpy(), blk.rel.cpu().numpy()
+    tb = tab.cpu().double().numpy()
+    for v in rng.choice(n_dst, size=200, replace=False):
+        e = np.arange(bp[v], bp[v + 1])
+        want = (tb[rl[e]][:, None] * xd[ix[e]]).sum(0) / e.size + bias.cpu().double().numpy()
+        assert np.allclose(y[v], want, rtol=1e-5, atol=1e-5)
+
+
+def _sample_row_global(row_idx, t, k, seed, base):
+    d = row_idx.size
+    if d <= k:
+        return row_idx.tolist(), [base + q for q in range(d)]
+    chosen = []
+    for j in range(d - k, d):
+        pos = (SO.sample_hash(seed, t, j) * (j + 1)) >> 32
+        chosen.append(j if pos in chosen else pos)
+    chosen.sort()
+    return [int(row_idx[p]) for p in chosen], [base + p for p in chosen]
