@@ -582,6 +582,20 @@ class MagREGCNConvOracle:
         self.c = dict(g=g, et=et, x=x, xs=xs, ew=ew, cnt=cnt, pre_tab=pre_tab, ln=ln, P=P)
         return out
 
+    def edge_weights(self, use_softmax):
+        """return_weights' ew of the last forward (mag/regnn_layers.py:116-126,137): softmax of
+        the relation weights over each target's in-edges with ONE global max subtracted and
+        + 1e-16 in the denominator (mag/utils.py:45-57), else weight / weighted in-degree
+        (mag/utils.py:15-21). Edge order: sampled edges, then the appended self loops."""
+        c = self.c
+        w, col = c["ew"], c["g"].dst
+        if use_softmax:
+            e = np.exp(w - w.max())
+            den = np.bincount(col, weights=e, minlength=self.n_dst)
+            return e / (den[col] + 1e-16)
+        deg = np.bincount(col, weights=w, minlength=self.n_dst)
+        return w / deg[col]
+
     def backward(self, gout):
         c, P = self.c, self.c["P"]
         g, W = c["g"], P["weight"]

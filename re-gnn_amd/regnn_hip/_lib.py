@@ -6,6 +6,7 @@ the stream is torch's current HIP stream, so kernels order with surrounding torc
 """
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -111,21 +112,48 @@ def dtype_code(t):
     raise TypeError(f"regnn_hip: unsupported feature dtype {t.dtype} (float32 / bfloat16)")
 
 
+# Device of the pointers formed for the call being assembled: ``call(name, ptr(a), ...,
+# stream())`` evaluates ptr() first, so stream() picks the current stream of the TENSORS'
+# device (not of torch's current device) and call() runs the launch under that device.
+_tls = threading.local()
+
+
+def _reset():
+    _tls.dev, _tls.mixed = None, False
+
+
 def ptr(t):
     """device pointer of a tensor (None -> NULL); refuses CPU tensors: no CPU fallback."""
     if t is None:
         return None
     if not t.is_cuda:
+        _reset()
         raise RuntimeError("regnn_hip kernels need ROCm device tensors (there is no CPU path)")
+    d = t.device.index
+    cur = getattr(_tls, "dev", None)
+    if cur is None:
+        _tls.dev = d
+    elif cur != d:
+        _tls.mixed = True
     return t.data_ptr()
 
 
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """current HIP stream of the device the call's tensors live on (torch's current device
+    when no tensor pointer was formed yet)."""
+    return torch.cuda.current_stream(getattr(_tls, "dev", None)).cuda_stream
 
 
 def call(name, *args):
-    rc = getattr(_so, name)(*args)
+    dev, mixed = getattr(_tls, "dev", None), getattr(_tls, "mixed", False)
+    _reset()
+    if mixed:
+        raise RuntimeError(f"regnn_hip.{name}: tensors on different devices")
+    if dev is not None and dev != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            rc = getattr(_so, name)(*args)
+    else:
+        rc = getattr(_so, name)(*args)
     if rc != 0:
         raise RuntimeError(f"regnn_hip.{name} failed: {_ERR.get(rc, rc)}")
 

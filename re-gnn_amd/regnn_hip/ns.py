@@ -257,7 +257,11 @@ class NSTrainer:
                 self.step()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
-        self.sampler.state.copy_(st0)                 # warm-up steps do not advance the epoch
+        # warm-up steps do not advance the epoch (batch counter, edge counter); the dedup stamp
+        # (state[4]) stays monotone: the tables still hold the warm-up steps' stamps
+        st = self.sampler.state
+        st[2:4].copy_(st0[2:4])
+        st[5:6].copy_(st0[5:6])
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self._forward_backward()

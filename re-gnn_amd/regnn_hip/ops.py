@@ -950,8 +950,8 @@ class _HeadCE(torch.autograd.Function):
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         zsrc = getattr(ctx, "zsrc", None)
         if zsrc is not None:
+            # kept until the graph is freed: a retain_graph backward re-forms p from z again
             z, ver, lse, lab = zsrc
-            ctx.zsrc = None
             if z._version == ver:
                 return _head_bwd_z(ctx, h, W, z, lse, lab, g_loss, need_h, need_w, need_b)
             # the caller modified the logits in place: re-form p from h (the stored-p path)

@@ -291,24 +291,31 @@ def gen_mag():
     dst[np.isin(dst, [3, 17, 42])] = 5
     edge_type = rng.integers(0, num_edge_types, size=E).astype(np.int64)
     tnt = rng.integers(0, num_node_types, size=n_dst).astype(np.int64)
-    for residual in (False, True):
+    # (residual, use_softmax): the softmax case also records return_weights' ew (:119-121,137)
+    for residual, use_softmax in ((False, False), (True, False), (False, True)):
         torch.manual_seed(8)
         conv = regnn_layers.REGCNConv(64, 64, num_node_types, num_edge_types, 10.0,
-                                      residual=residual, use_norm="ln", self_loop_type=2)
+                                      use_softmax=use_softmax, residual=residual,
+                                      use_norm="ln", self_loop_type=2)
         _set_params(conv, rng, ew_alpha=10.0)
         x = torch.from_numpy(f32(rng, n_src, 64).astype(np.float64)).requires_grad_(True)
         ei = torch.from_numpy(np.stack([src, dst]))
-        out = conv((x, x[:n_dst]), ei, torch.from_numpy(edge_type), torch.from_numpy(tnt))
+        res = conv((x, x[:n_dst]), ei, torch.from_numpy(edge_type), torch.from_numpy(tnt),
+                   return_weights=use_softmax)
+        out = res[0] if use_softmax else res
         gout = f32(rng, *out.shape)
         out.backward(torch.from_numpy(gout.astype(np.float64)))
         st = dict(src=src, dst=dst, edge_type=edge_type, target_node_type=tnt,
                   x=x.detach().numpy().astype(np.float32), gout=gout, out=out, grad_x=x.grad)
+        if use_softmax:
+            st["ew"] = res[1].detach()
         _pack("p_", _params(conv), st)
         _pack("grad_", _grads(conv), st)
-        save(f"mag_regcnconv_res{int(residual)}",
-             dict(layer="mag.REGCNConv", n_src=n_src, n_dst=n_dst, num_node_types=num_node_types,
-                  num_edge_types=num_edge_types, scaling_factor=10.0, residual=residual,
-                  use_norm="ln", self_loop_type=2), st)
+        name = "mag_regcnconv_softmax" if use_softmax else f"mag_regcnconv_res{int(residual)}"
+        save(name, dict(layer="mag.REGCNConv", n_src=n_src, n_dst=n_dst,
+                        num_node_types=num_node_types, num_edge_types=num_edge_types,
+                        scaling_factor=10.0, residual=residual, use_softmax=use_softmax,
+                        use_norm="ln", self_loop_type=2), st)
 
 
 # ------------------------------------------------------------------------------------------

@@ -95,3 +95,32 @@ def test_sparse_rows_allreduce_two_ranks():
     (g0, d0), (g1, d1) = out[0], out[1]
     assert torch.equal(g0, g1)
     assert torch.allclose(g0, d0, atol=1e-6) and torch.allclose(g1, d1, atol=1e-6)
+
+
+def _uneven_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from regnn_hip.mag import flat_grad_allreduce
+    from regnn_hip.sampler import NeighborSampler
+    # 1000 targets / batch 200 = 5 global batches over 2 ranks: rank 1 wraps to batch 0, so both
+    # ranks run 3 steps and every per-step all-reduce has its partner (no hang at epoch end)
+    smp = NeighborSampler(_StubGraph(1000), torch.arange(1000), [25, 20], batch_size=200,
+                          shuffle=True, seed=9, rank=rank, world_size=world)
+    model = torch.nn.Linear(4, 2)
+    steps = []
+    for b, t in smp.batches():
+        model.zero_grad()
+        model(t.float().reshape(-1, 1).repeat(1, 4)[:8] / 1000).sum().backward()
+        flat_grad_allreduce(list(model.parameters()), world)
+        steps.append(b)
+    out[rank] = steps
+    dist.destroy_process_group()
+
+
+def test_dp_uneven_batch_count_same_steps_per_rank():
+    """nb % world != 0 must not leave one rank alone in the gradient all-reduce."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_uneven_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[0] == [0, 2, 4] and out[1] == [1, 3, 0]

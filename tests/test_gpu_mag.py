@@ -23,8 +23,10 @@ def test_mag_regcnconv(name):
     from regnn_hip.mag import REGCNConv
     d = G.load(name)
     m = d["meta"]
+    sm = bool(m.get("use_softmax", False))
     conv = REGCNConv(64, 64, m["num_node_types"], m["num_edge_types"], m["scaling_factor"],
-                     residual=m["residual"], use_norm=m["use_norm"], self_loop_type=2)
+                     use_softmax=sm, residual=m["residual"], use_norm=m["use_norm"],
+                     self_loop_type=2)
     P = G.sub(d, "p_", np.float32)
     assert {n for n, _ in conv.named_parameters()} == set(P)
     with torch.no_grad():
@@ -33,10 +35,13 @@ def test_mag_regcnconv(name):
     conv = conv.to(DEV)
     x = torch.from_numpy(d["x"]).to(DEV).requires_grad_(True)
     ei = torch.from_numpy(np.stack([d["src"], d["dst"]])).to(DEV)
-    out = conv((x, x[:m["n_dst"]]), ei, torch.from_numpy(d["edge_type"]).to(DEV),
-               torch.from_numpy(d["target_node_type"]).to(DEV))
+    res = conv((x, x[:m["n_dst"]]), ei, torch.from_numpy(d["edge_type"]).to(DEV),
+               torch.from_numpy(d["target_node_type"]).to(DEV), return_weights=sm)
+    out = res[0] if sm else res
     out.backward(torch.from_numpy(d["gout"]).to(DEV))
     _check("out", out, d["out"])
+    if sm:           # the reference computes the softmax ew but propagates the raw weights
+        _check("ew", res[1], d["ew"])
     _check("grad_x", x.grad, d["grad_x"])
     for k, v in G.sub(d, "grad_").items():
         if k != "x":

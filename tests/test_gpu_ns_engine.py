@@ -121,10 +121,13 @@ def test_trainer_step_matches_pyg_path():
     tr, _ = _setup_trainer(d, m_eng)
     tr._forward_backward()
     torch.cuda.synchronize()
-    assert abs(float(tr.loss) - float(loss_api)) <= 1e-5 * max(1.0, abs(float(loss_api)))
+    assert abs(float(tr.loss) - float(loss_api.detach())) <= 1e-5 * max(1.0, abs(float(loss_api.detach())))
     assert int(tr.sampler.sizes[0]) == 64
     gp = dict(m_api.named_parameters())
     for n, p in m_eng.named_parameters():
+        if gp[n].grad is None:                 # declared, unused in forward (REGNN.norm)
+            assert not p.grad.any(), n
+            continue
         ok, err = G.close(p.grad.cpu().numpy(), gp[n].grad.cpu().numpy().astype(np.float64), 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
 

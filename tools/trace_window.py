@@ -1,0 +1,34 @@
+"""Per-step kernel time of the last K steps in a rocprofv3 kernel trace.
+
+usage: trace_window.py TRACE_CSV MARKER K
+The timed window starts at the K-th last dispatch whose name contains MARKER (the first kernel of
+a step, e.g. ns_batch_kernel) and ends with the last dispatch. Prints per-kernel device time per
+step, the summed busy time per step and the window's wall time per step (gaps included)."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def main():
+    path, marker, k = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    if len(starts) < k:
+        raise SystemExit(f"only {len(starts)} '{marker}' dispatches")
+    win = rows[starts[-k]:]
+    tot, cnt = defaultdict(float), defaultdict(int)
+    for r in win:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        name = r["Kernel_Name"]
+        tot[name] += d
+        cnt[name] += 1
+    busy = sum(tot.values()) / k
+    wall = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e3 / k
+    print(f"window: {k} steps, {len(win)} dispatches ({len(win) / k:.1f}/step), "
+          f"busy {busy:.1f} us/step, wall {wall:.1f} us/step")
+    for name, t in sorted(tot.items(), key=lambda x: -x[1]):
+        print(f"{t / k:9.1f} us  x{cnt[name] / k:5.2f}  {name[:140]}")
+
+
+if __name__ == "__main__":
+    main()
