@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 19). */
+/* ABI version (bumped on any signature change or addition; currently 20). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -539,6 +539,93 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
                       const float* rel_table, const float* out_scale, const float* g,
                       const float* x, float* gx, float* slab, int32_t n_rel, int64_t n_rows,
                       int32_t F, hipStream_t stream);
+
+
+/* ---------------------------------------------------------------------------------------
+ * Fused NS model step: the REGNN of mag/regnn_ns.py:216-346 (model 'regcn', self_loop_type 2,
+ * use_norm 'ln', residual off, feats_type != 2, hidden 64) forward + nll_loss + backward over the
+ * blocks regnn_ns_hop wrote, with no host sizes (every kernel reads the counts in `sizes`).
+ * Replaces, per step (mag/regnn_ns.py:399-406): group_input's per-type Linear (:300-326), each
+ * REGCNConv (x @ W, relation-table mean aggregation + bias, LayerNorm; mag/regnn_layers.py:
+ * 80-150), relu + dropout (:341-343), out_lin + log_softmax (:345-346), F.nll_loss (:404) and
+ * loss.backward() (:405), writing every parameter gradient into caller-provided buffers.
+ *
+ * Arithmetic (fp32 throughout): the group_input Linear and the first conv's weight are applied
+ * as one composed map x @ (W_t^T W_0) + b_t W_0 (associativity; the gradients of W_t, b_t and W_0
+ * follow by the chain rule). Dropout masks are this build's hash (regnn_spmm_fwd_dropout's spec)
+ * keyed on s = mix64(state[0] ^ mix64((state[4] << 4) + layer + 0x51ED27)), row = target row of
+ * the layer's block, 4 features per 16-byte vector. The sampled blocks' transposed aggregation
+ * uses float atomics (as regnn_ns_spmm_bwd); every other reduction is fixed-order.
+ * --------------------------------------------------------------------------------------- */
+#define REGNN_NSM_MAX_TYPES 8
+#define REGNN_NSM_MAX_LAYERS 4
+
+typedef struct regnn_nsm_params {
+    int32_t n_types;          /* node types T (x_dict keys 0..T-1), <= 8 */
+    int32_t k_in;             /* input feature width: 64 or 128, T * (k_in + 1) <= 600 */
+    int32_t n_layers;         /* L in [1, 4]; layer l reads hop L-1-l's block */
+    int32_t n_classes;        /* C <= 512 */
+    float alpha;              /* scaling_factor (mag/regnn_layers.py:110) */
+    float p_drop;             /* dropout after each conv's relu (training), in [0, 1) */
+    int32_t n_rel[REGNN_NSM_MAX_LAYERS];  /* len(relation_weight) per layer, <= 64 */
+    const float* x_tab[REGNN_NSM_MAX_TYPES];  /* x_dict[t] [n_t, k_in], rows = local_node_idx */
+    const float* lin_w[REGNN_NSM_MAX_TYPES];  /* lins[t].weight [64, k_in] */
+    const float* lin_b[REGNN_NSM_MAX_TYPES];  /* lins[t].bias [64] */
+    const float* conv_w[REGNN_NSM_MAX_LAYERS];  /* convs[l].weight [64, 64] (x @ W) */
+    const float* conv_b[REGNN_NSM_MAX_LAYERS];
+    const float* conv_rw[REGNN_NSM_MAX_LAYERS]; /* convs[l].relation_weight [n_rel] */
+    const float* ln_w[REGNN_NSM_MAX_LAYERS];
+    const float* ln_b[REGNN_NSM_MAX_LAYERS];
+    const float* out_w;       /* out_lin.weight [C, 64] */
+    const float* out_b;       /* out_lin.bias [C] */
+    float* g_lin_w[REGNN_NSM_MAX_TYPES];
+    float* g_lin_b[REGNN_NSM_MAX_TYPES];
+    float* g_conv_w[REGNN_NSM_MAX_LAYERS];
+    float* g_conv_b[REGNN_NSM_MAX_LAYERS];
+    float* g_conv_rw[REGNN_NSM_MAX_LAYERS];
+    float* g_ln_w[REGNN_NSM_MAX_LAYERS];
+    float* g_ln_b[REGNN_NSM_MAX_LAYERS];
+    float* g_out_w;
+    float* g_out_b;
+    float* loss;              /* [1]: mean nll over the batch targets with a label >= 0 */
+} regnn_nsm_params;
+
+typedef struct regnn_nsm_work {
+    const int64_t* state;     /* regnn_ns_batch / regnn_ns_hop state (reads [0] and [4]) */
+    const int32_t* sizes;     /* regnn_ns_hop sizes */
+    const int32_t* n_id;      /* [cap[L]] int32 */
+    int32_t cap[REGNN_NSM_MAX_LAYERS + 1];    /* capacity of n_id after h hops */
+    const int32_t* blk_ptr[REGNN_NSM_MAX_LAYERS];   /* hop h's block (regnn_ns_hop output) */
+    const int32_t* blk_idx[REGNN_NSM_MAX_LAYERS];
+    const uint8_t* blk_rel[REGNN_NSM_MAX_LAYERS];
+    const float* blk_inv[REGNN_NSM_MAX_LAYERS];
+    const int32_t* ntype;     /* node type per global node */
+    const int64_t* local;     /* local_node_idx per global node */
+    const int64_t* labels;    /* label per global node (< 0: none) */
+    /* scratch, caller-allocated (sizes in rows of 64 floats unless noted) */
+    float* wc;                /* T * (k_in + 1) * 64 floats: the composed first map */
+    float* gwc;               /* same size: its gradient */
+    float* tabs;              /* L * 64 floats */
+    float* xs[REGNN_NSM_MAX_LAYERS];    /* layer l's source rows: cap[L-l] rows */
+    float* gxs[REGNN_NSM_MAX_LAYERS];   /* their gradient: cap[L-l] rows */
+    float* a[REGNN_NSM_MAX_LAYERS];     /* layer l's pre-LayerNorm rows: cap[L-1-l] rows */
+    float* stats[REGNN_NSM_MAX_LAYERS]; /* (mean, rstd) per row: 2 * cap[L-1-l] floats */
+    float* ga[REGNN_NSM_MAX_LAYERS];    /* d loss / d pre-LN rows: cap[L-1-l] rows */
+    float* gy[REGNN_NSM_MAX_LAYERS];    /* d loss / d LN output: cap[L-1-l] rows */
+    float* gyx[REGNN_NSM_MAX_LAYERS];   /* gy * normalised rows: cap[L-1-l] rows */
+    float* h_last;            /* the last layer's output rows: cap[0] rows */
+    float* glogits;           /* d loss / d logits: cap[0] * C floats */
+    float* loss_rows;         /* cap[0] + 1 floats ([cap[0]] = labelled-target count) */
+    float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
+} regnn_nsm_work;
+
+/* Floats of the per-block partial slab regnn_nsm_step needs for these parameters. */
+int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p);
+
+/* One forward + loss + backward of the model over the current batch (after regnn_ns_batch and
+ * the L regnn_ns_hop calls of the step): writes every g_* buffer (overwritten, not accumulated)
+ * and *loss. 10 kernel launches for L = 2, none of them sized from the host. */
+int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,957 @@
+// Fused neighbour-sampled (NS) model step of the ogbn-mag path (regnn_nsm_step, regnn_hip.h):
+// the REGNN of mag/regnn_ns.py:216-346 ('regcn', self_loop_type 2, LayerNorm, hidden 64) with
+// its loss and backward over the blocks regnn_ns_hop wrote, as ten launches for two layers.
+// Every kernel reads the batch's counts from `sizes` (device) and leaves rows past them alone,
+// so the whole step is one HIP-graph replay with no host synchronisation.
+//
+//   prep        W_c[t] = lins[t].weight^T convs[0].weight, b_c[t] = lins[t].bias convs[0].weight,
+//               relation tables LeakyReLU(alpha * rw_l)                (mag/regnn_layers.py:110)
+//   project     xs_0[i] = x_t[local(i)] W_c[t] + b_c[t] for the outermost hop's sources
+//               (group_input + the first x @ W: mag/regnn_ns.py:300-326, regnn_layers.py:102)
+//   agg         layer l < L-1: mean aggregation with the relation table + bias, LayerNorm, relu,
+//               dropout, then x @ W_{l+1} of the next layer                (regnn_layers.py:
+//               129-148, regnn_ns.py:341-343)
+//   head        layer L-1 as above, then out_lin, log_softmax, nll_loss (mean) and their
+//               backward down to the pre-LayerNorm rows                   (regnn_ns.py:345, 404)
+//   agg_bwd     transposed block aggregation (float atomics: a sampled block has no CSC) and
+//               the relation-table dots
+//   post_bwd    x @ W_{l+1} backward (its weight gradient per block), dropout / relu / LayerNorm
+//               backward of layer l
+//   project_bwd per-type x^T g of the composed first map
+//   finalize    fixed-order reductions of every per-row / per-block partial into the gradients;
+//               chain rule of the composed map onto lins[t] and convs[0].weight
+#include "regnn_common.h"
+
+namespace regnn {
+namespace nsm {
+
+constexpr int F = 64;                  // hidden width
+constexpr int MT = REGNN_NSM_MAX_TYPES;
+constexpr int ML = REGNN_NSM_MAX_LAYERS;
+constexpr int kAggBlocks = 512;        // persistent grids: fixed, so the slab layout is static
+constexpr int kPostBlocks = 256;
+constexpr int kProjBlocks = 128;       // per node type
+constexpr int kProjTile = 64;          // rows per project_bwd tile
+constexpr int kWPad = 65;              // padded row stride of 64-wide matrices in LDS
+constexpr float kLnEps = 1e-5f;
+
+struct Ptrs {                          // per-type / per-layer pointer tables passed by value
+    const float* p[MT];
+};
+
+struct Ints {
+    int v[ML];
+};
+
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&a)[N], int i) {
+    T r = a[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+        if (i == k) r = a[k];
+    return r;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+// dropout key of layer `layer` for the current step (spec in regnn_hip.h)
+__device__ __forceinline__ uint32_t layer_key(const int64_t* state, int layer) {
+    const uint64_t s =
+        mix64(uint64_t(state[0]) ^ mix64((uint64_t(state[4]) << 4) + uint64_t(layer) + 0x51ED27ull));
+    return fmix32(uint32_t(s) ^ fmix32(uint32_t(s >> 32) ^ 0x5BD1E995u));
+}
+
+struct Drop {
+    uint32_t thresh;    // keep16
+    float scale;        // 1 / keep
+    bool on, b8;        // b8: 8-bit draws (keep16 a multiple of 256), as the host picks for the
+                        // other fused-dropout kernels
+};
+
+// keep factors (0 or scale) of the 4 features of 16-byte vector `vec` of row `row`
+__device__ __forceinline__ void drop_factors(uint32_t key, const Drop& d, int64_t row, int vec,
+                                             float (&m)[4]) {
+    m[0] = m[1] = m[2] = m[3] = 1.f;
+    if (!d.on) return;
+    if (d.b8) drop_apply<4, 8>(key, d.thresh, d.scale, row, F / 4, vec, m);
+    else drop_apply<4, 16>(key, d.thresh, d.scale, row, F / 4, vec, m);
+}
+
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// prep: composed first map and the relation tables (deterministic fixed-order dots)
+__global__ void __launch_bounds__(64)
+prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, Ptrs rw,
+            int L, Ints n_rel, float alpha, float* __restrict__ wc,
+            float* __restrict__ tabs) {
+    const int j = threadIdx.x;
+    const int b = blockIdx.x;
+    if (b < T * (K + 1)) {
+        const int t = b / (K + 1), k = b - t * (K + 1);
+        float s = 0.f;
+        if (k < K) {
+            const float* W = pick(lin_w.p, t);
+            for (int o = 0; o < F; ++o) s = fmaf(W[int64_t(o) * K + k], w0[o * F + j], s);
+        } else {
+            const float* bb = pick(lin_b.p, t);
+            for (int o = 0; o < F; ++o) s = fmaf(bb[o], w0[o * F + j], s);
+        }
+        wc[int64_t(b) * F + j] = s;
+        return;
+    }
+    const int l = b - T * (K + 1);
+    if (l >= L) return;
+    const int nr = pick(n_rel.v, l);
+    float v = 0.f;
+    if (j < nr) {
+        const float x = pick(rw.p, l)[j] * alpha;
+        v = x > 0.f ? x : 0.01f * x;                      // F.leaky_relu default slope
+    }
+    tabs[l * F + j] = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// project: xs0[i] = x_t[local(n_id[i])] . W_c[t] + b_c[t]; 4 lanes per row, 16 outputs per lane;
+// every type's W_c in LDS (types staggered by 4 banks). Zeroes gxs0's rows for the scatter.
+__global__ void __launch_bounds__(1024)
+project_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
+               const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, int T, int K,
+               Ptrs xt, const float* __restrict__ wc, float* __restrict__ xs,
+               float* __restrict__ gxs) {
+    extern __shared__ float lw[];
+    const int str = (K + 1) * F + 4;
+    for (int i = threadIdx.x; i < T * (K + 1) * (F / 4); i += blockDim.x) {
+        const int t = i / ((K + 1) * (F / 4)), r = i - t * (K + 1) * (F / 4);
+        reinterpret_cast<float4*>(lw + t * str)[r] =
+            reinterpret_cast<const float4*>(wc + int64_t(t) * (K + 1) * F)[r];
+    }
+    __syncthreads();
+    const int n = sizes[hop];
+    const int q = threadIdx.x & 3;
+    const int rpb = blockDim.x / 4;
+    for (int i = blockIdx.x * rpb + (threadIdx.x >> 2); i < n; i += gridDim.x * rpb) {
+        const int g = n_id[i];
+        const int t = ntype[g];
+        const float* xr = pick(xt.p, t) + local[g] * int64_t(K);
+        const float* wt = lw + t * str + q * 16;
+        float acc[16];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 b = *reinterpret_cast<const float4*>(wt + K * F + 4 * m);
+            acc[4 * m] = b.x; acc[4 * m + 1] = b.y; acc[4 * m + 2] = b.z; acc[4 * m + 3] = b.w;
+        }
+        for (int k0 = 0; k0 < K; k0 += 4) {
+            const float4 xv = *reinterpret_cast<const float4*>(xr + k0);
+            const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const float* wr = wt + (k0 + kk) * F;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float4 w = *reinterpret_cast<const float4*>(wr + 4 * m);
+                    acc[4 * m] = fmaf(xk[kk], w.x, acc[4 * m]);
+                    acc[4 * m + 1] = fmaf(xk[kk], w.y, acc[4 * m + 1]);
+                    acc[4 * m + 2] = fmaf(xk[kk], w.z, acc[4 * m + 2]);
+                    acc[4 * m + 3] = fmaf(xk[kk], w.w, acc[4 * m + 3]);
+                }
+            }
+        }
+        float* o = xs + int64_t(i) * F + q * 16;
+        float* z = gxs + int64_t(i) * F + q * 16;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            *reinterpret_cast<float4*>(o + 4 * m) =
+                make_float4(acc[4 * m], acc[4 * m + 1], acc[4 * m + 2], acc[4 * m + 3]);
+            *reinterpret_cast<float4*>(z + 4 * m) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// agg (layer l < L-1): 16 lanes per row (4 features each), 16 rows per block. a = inv * sum_e
+// tab[rel] xs[idx] + bias; LayerNorm; relu; dropout -> h; xs_next = h W_next (W_next in LDS).
+struct AggArgs {
+    const int32_t* sizes; int hop;
+    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const float* tab; const float* xs; const float* bias; const float* ln_w; const float* ln_b;
+    const int64_t* state; int layer; Drop drop;
+    const float* w_next;
+    float* a; float* stats; float* xs_next; float* gxs_next;
+};
+
+__global__ void __launch_bounds__(kBlock) agg_kernel(AggArgs A) {
+    __shared__ float Wn[F * F];            // [k][j], read as float4 along j (broadcast per k)
+    __shared__ float hrow[16][F];
+    __shared__ float tab[F];
+    for (int i = threadIdx.x; i < F * F / 4; i += kBlock)
+        reinterpret_cast<float4*>(Wn)[i] = reinterpret_cast<const float4*>(A.w_next)[i];
+    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4;
+    const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
+    const float4 bias = reinterpret_cast<const float4*>(A.bias)[l];
+    const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
+    for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
+        const int v = base + sub;
+        const bool act = v < n;
+        if (act) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            for (int e = e0; e < e1; ++e) {
+                const float w = tab[A.rel[e]];
+                const float4 x = *reinterpret_cast<const float4*>(A.xs + int64_t(A.idx[e]) * F + 4 * l);
+                s0 = fmaf(w, x.x, s0); s1 = fmaf(w, x.y, s1);
+                s2 = fmaf(w, x.z, s2); s3 = fmaf(w, x.w, s3);
+            }
+            const float iv = A.inv[v];
+            const float a[4] = {fmaf(iv, s0, bias.x), fmaf(iv, s1, bias.y), fmaf(iv, s2, bias.z),
+                                fmaf(iv, s3, bias.w)};
+            *reinterpret_cast<float4*>(A.a + int64_t(v) * F + 4 * l) = make_float4(a[0], a[1], a[2], a[3]);
+            const float mean = group_sum<16>(a[0] + a[1] + a[2] + a[3]) * (1.f / F);
+            const float d[4] = {a[0] - mean, a[1] - mean, a[2] - mean, a[3] - mean};
+            const float var = group_sum<16>(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) * (1.f / F);
+            const float rstd = rsqrtf(var + kLnEps);
+            if (l == 0) reinterpret_cast<float2*>(A.stats)[v] = make_float2(mean, rstd);
+            const float gws[4] = {gw.x, gw.y, gw.z, gw.w}, gbs[4] = {gb.x, gb.y, gb.z, gb.w};
+            float m[4];
+            drop_factors(key, A.drop, v, l, m);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float y = fmaf(d[c] * rstd, gws[c], gbs[c]);
+                hrow[sub][4 * l + c] = fmaxf(y, 0.f) * m[c];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < F; ++k) {
+                const float hk = hrow[sub][k];
+                const float4 w = *reinterpret_cast<const float4*>(Wn + k * F + 4 * l);
+                o0 = fmaf(hk, w.x, o0); o1 = fmaf(hk, w.y, o1);
+                o2 = fmaf(hk, w.z, o2); o3 = fmaf(hk, w.w, o3);
+            }
+            *reinterpret_cast<float4*>(A.xs_next + int64_t(v) * F + 4 * l) = make_float4(o0, o1, o2, o3);
+            *reinterpret_cast<float4*>(A.gxs_next + int64_t(v) * F + 4 * l) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm / relu / dropout backward of one row held one feature per lane (wave per row):
+// g = d loss / d (dropped relu output); writes ga (d / d pre-LN row), gy, gy * xhat.
+__device__ __forceinline__ void ln_relu_drop_bwd(float g, float xhat, float rstd, float gw,
+                                                 float gb, float mfac, float* ga, float* gy,
+                                                 float* gyx) {
+    const float y = fmaf(xhat, gw, gb);
+    const float g_y = y > 0.f ? g * mfac : 0.f;
+    const float gx = g_y * gw;
+    const float m1 = wave_sum(gx) * (1.f / F);
+    const float m2 = wave_sum(gx * xhat) * (1.f / F);
+    *ga = rstd * (gx - m1 - xhat * m2);
+    *gy = g_y;
+    *gyx = g_y * xhat;
+}
+
+// keep factor of feature f (lane) of row `row`
+__device__ __forceinline__ float lane_drop(uint32_t key, const Drop& d, int64_t row, int f) {
+    float m[4];
+    drop_factors(key, d, row, f >> 2, m);
+    return (f & 3) == 0 ? m[0] : (f & 3) == 1 ? m[1] : (f & 3) == 2 ? m[2] : m[3];
+}
+
+// ---------------------------------------------------------------------------------------------
+// head: the last layer (wave per target row, lane = feature) + out_lin + log_softmax + nll +
+// backward down to the pre-LN rows. out_lin.weight in LDS with rows padded to 65 floats.
+struct HeadArgs {
+    const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
+    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const float* tab; const float* xs; const float* bias; const float* ln_w; const float* ln_b;
+    const int64_t* state; int layer; Drop drop;
+    const float* w_out; const float* b_out; int C;
+    float* h_last; float* glogits; float* loss_rows; float* ga; float* gy; float* gyx;
+    int cap0;
+};
+
+constexpr int kHeadRows = 4;           // waves (= rows) per block
+
+__global__ void __launch_bounds__(kHeadRows * 64) head_kernel(HeadArgs A) {
+    extern __shared__ float hl[];      // [C][65] W_out, then [kHeadRows][F] h, [kHeadRows][C] g
+    float* Wl = hl;
+    float* hs = Wl + A.C * kWPad;
+    float* gs = hs + kHeadRows * F;
+    __shared__ float tab[F];
+    __shared__ int s_valid;
+    const int C = A.C;
+    for (int i = threadIdx.x; i < C * F; i += blockDim.x) {
+        const int c = i / F, k = i - c * F;
+        Wl[c * kWPad + k] = A.w_out[i];
+    }
+    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
+    const int n = A.sizes[0];
+    if (threadIdx.x == 0) s_valid = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+    atomicAdd(&s_valid, cnt);              // integer count: order-independent
+    __syncthreads();
+    const int n_valid = s_valid;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.loss_rows[A.cap0] = float(n_valid);
+    const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
+    const int v = blockIdx.x * kHeadRows + w;
+    if (v >= n) return;                    // no block-wide barrier below this point
+    float s = 0.f;
+    const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+    for (int e = e0; e < e1; ++e) s = fmaf(tab[A.rel[e]], A.xs[int64_t(A.idx[e]) * F + f], s);
+    const float a = fmaf(A.inv[v], s, A.bias[f]);
+    const float mean = wave_sum(a) * (1.f / F);
+    const float dlt = a - mean;
+    const float rstd = rsqrtf(wave_sum(dlt * dlt) * (1.f / F) + kLnEps);
+    const float xhat = dlt * rstd;
+    const float gw = A.ln_w[f], gb = A.ln_b[f];
+    const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
+    const float mfac = lane_drop(key, A.drop, v, f);
+    const float h = fmaxf(fmaf(xhat, gw, gb), 0.f) * mfac;
+    A.h_last[int64_t(v) * F + f] = h;
+    float* hw = hs + w * F;
+    float* gw_ = gs + w * C;
+    hw[f] = h;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);    // lgkmcnt(0): the wave's LDS writes are visible
+    constexpr int MC = 8;                  // up to 512 classes: 8 per lane
+    float z[MC];
+#pragma unroll
+    for (int m = 0; m < MC; ++m) {
+        const int c = f + 64 * m;
+        z[m] = c < C ? A.b_out[c] : -INFINITY;
+    }
+    for (int k = 0; k < F; ++k) {
+        const float hk = hw[k];
+#pragma unroll
+        for (int m = 0; m < MC; ++m) {
+            const int c = f + 64 * m;
+            if (c < C) z[m] = fmaf(hk, Wl[c * kWPad + k], z[m]);
+        }
+    }
+    float zmax = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < MC; ++m) zmax = fmaxf(zmax, z[m]);
+    zmax = wave_max(zmax);
+    float se = 0.f;
+#pragma unroll
+    for (int m = 0; m < MC; ++m)
+        if (f + 64 * m < C) se += expf(z[m] - zmax);
+    const float lse = zmax + logf(wave_sum(se));
+    const int64_t y = A.labels[A.n_id[v]];
+    float zy = 0.f;
+#pragma unroll
+    for (int m = 0; m < MC; ++m)
+        if (int64_t(f + 64 * m) == y) zy = z[m];
+    zy = wave_sum(zy);                     // exactly one lane holds it (or none: y < 0)
+    if (f == 0) A.loss_rows[v] = y >= 0 ? lse - zy : 0.f;
+    const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
+#pragma unroll
+    for (int m = 0; m < MC; ++m) {
+        const int c = f + 64 * m;
+        if (c < C) {
+            const float g = (expf(z[m] - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n;
+            gw_[c] = g;
+            A.glogits[int64_t(v) * C + c] = g;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    float gh = 0.f;
+    for (int c = 0; c < C; ++c) gh = fmaf(gw_[c], Wl[c * kWPad + f], gh);
+    float ga, gyv, gyx;
+    ln_relu_drop_bwd(gh, xhat, rstd, gw, gb, mfac, &ga, &gyv, &gyx);
+    A.ga[int64_t(v) * F + f] = ga;
+    A.gy[int64_t(v) * F + f] = gyv;
+    A.gyx[int64_t(v) * F + f] = gyx;
+}
+
+// ---------------------------------------------------------------------------------------------
+// agg_bwd: gxs[idx_e] += tab[rel_e] inv[v] ga[v] (atomics) and per-relation dots
+// inv[v] <ga[v], xs[idx_e]> in lane-private LDS bins -> slab[block][64].
+struct AggBwdArgs {
+    const int32_t* sizes; int hop;
+    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const float* tab; const float* xs; const float* ga; float* gxs; float* slab; int n_rel;
+};
+
+__global__ void __launch_bounds__(kBlock) agg_bwd_kernel(AggBwdArgs A) {
+    extern __shared__ float bins[];        // [n_rel][kBlock]: a thread owns its column
+    __shared__ float tab[F];
+    for (int i = threadIdx.x; i < A.n_rel * kBlock; i += kBlock) bins[i] = 0.f;
+    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int f = threadIdx.x & 63;
+    for (int v = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); v < n;
+         v += gridDim.x * (kBlock / 64)) {
+        const float g = A.inv[v] * A.ga[int64_t(v) * F + f];
+        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        for (int e = e0; e < e1; ++e) {
+            const int u = A.idx[e];
+            const int r = A.rel[e];
+            unsafeAtomicAdd(A.gxs + int64_t(u) * F + f, tab[r] * g);
+            bins[r * kBlock + threadIdx.x] += g * A.xs[int64_t(u) * F + f];
+        }
+    }
+    __syncthreads();
+    // block sum per relation: 4 waves x 64 lanes, fixed order
+    for (int r = threadIdx.x >> 6; r < A.n_rel; r += kBlock / 64) {
+        float s = bins[r * kBlock + f] + bins[r * kBlock + 64 + f] + bins[r * kBlock + 128 + f] +
+                  bins[r * kBlock + 192 + f];
+        s = wave_sum(s);
+        if (f == 0) A.slab[int64_t(blockIdx.x) * F + r] = s;
+    }
+    for (int r = A.n_rel + threadIdx.x; r < F; r += kBlock) A.slab[int64_t(blockIdx.x) * F + r] = 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// post_bwd (layer l < L-1): gs = gxs_{l+1}[v]; gh = gs W_{l+1}^T; slab += h^T gs (this block's
+// rows); dropout / relu / LayerNorm backward -> ga, gy, gyx of layer l. Wave per row.
+struct PostArgs {
+    const int32_t* sizes; int hop;
+    const float* a; const float* stats; const float* ln_w; const float* ln_b;
+    const int64_t* state; int layer; Drop drop;
+    const float* w_next; const float* gxs_next;
+    float* ga; float* gy; float* gyx; float* slab;
+};
+
+__global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
+    __shared__ float Wt[F * kWPad];        // W[k][j] at k*65 + j
+    __shared__ float hs[4][F], gsr[4][F];
+    for (int i = threadIdx.x; i < F * F; i += kBlock) Wt[(i / F) * kWPad + (i % F)] = A.w_next[i];
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
+    const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
+    const float gwf = A.ln_w[f], gbf = A.ln_b[f];
+    // this thread's 16 entries of the block's W_{l+1} gradient partial: k = tid / 4,
+    // j = (tid % 4) * 16 .. +15
+    const int kk = threadIdx.x >> 2, j0 = (threadIdx.x & 3) * 16;
+    float acc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    for (int base = blockIdx.x * 4; base < n; base += gridDim.x * 4) {
+        const int v = base + w;
+        const bool act = v < n;
+        float xhat = 0.f, rstd = 0.f, mfac = 0.f, gsv = 0.f;
+        if (act) {
+            const float2 st = reinterpret_cast<const float2*>(A.stats)[v];
+            rstd = st.y;
+            xhat = (A.a[int64_t(v) * F + f] - st.x) * rstd;
+            mfac = lane_drop(key, A.drop, v, f);
+            gsv = A.gxs_next[int64_t(v) * F + f];
+        }
+        hs[w][f] = act ? fmaxf(fmaf(xhat, gwf, gbf), 0.f) * mfac : 0.f;
+        gsr[w][f] = gsv;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float hk = hs[r][kk];
+#pragma unroll
+            for (int c = 0; c < 16; c += 4) {
+                const float4 g4 = *reinterpret_cast<const float4*>(&gsr[r][j0 + c]);
+                acc[c] = fmaf(hk, g4.x, acc[c]);
+                acc[c + 1] = fmaf(hk, g4.y, acc[c + 1]);
+                acc[c + 2] = fmaf(hk, g4.z, acc[c + 2]);
+                acc[c + 3] = fmaf(hk, g4.w, acc[c + 3]);
+            }
+        }
+        if (act) {
+            float gh = 0.f;                // d loss / d h[f] = sum_j gs[j] W[f][j]
+#pragma unroll 8
+            for (int j = 0; j < F; ++j) gh = fmaf(gsr[w][j], Wt[f * kWPad + j], gh);
+            float ga, gyv, gyx;
+            ln_relu_drop_bwd(gh, xhat, rstd, gwf, gbf, mfac, &ga, &gyv, &gyx);
+            A.ga[int64_t(v) * F + f] = ga;
+            A.gy[int64_t(v) * F + f] = gyv;
+            A.gyx[int64_t(v) * F + f] = gyx;
+        }
+        __syncthreads();
+    }
+    float* o = A.slab + int64_t(blockIdx.x) * F * F + kk * F + j0;
+#pragma unroll
+    for (int c = 0; c < 16; c += 4)
+        *reinterpret_cast<float4*>(o + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// project_bwd: block (b, t) accumulates sum over rows i of type t of x_i^T g_i (K x 64) and
+// sum g_i (64) over its grid-stride share of 64-row tiles. Thread: k = kq*KPT .. +KPT-1 (16 k
+// groups), j = 4*j4 .. +3 (16 j groups).
+template <int KPT>
+__global__ void __launch_bounds__(kBlock)
+project_bwd_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
+                   const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, Ptrs xt,
+                   const float* __restrict__ gxs, float* __restrict__ slab) {
+    constexpr int K = KPT * 16;
+    constexpr int XS = K + 4, GS = F + 4;
+    __shared__ float xsh[kProjTile * XS];
+    __shared__ float gsh[kProjTile * GS];
+    __shared__ int rows[kProjTile];
+    __shared__ int s_cnt;
+    const int t = blockIdx.y;
+    const float* X = pick(xt.p, t);
+    const int n = sizes[hop];
+    const int kq = threadIdx.x >> 4, j4 = threadIdx.x & 15;
+    float acc[KPT][4];
+    float accb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < KPT; ++a) acc[a][0] = acc[a][1] = acc[a][2] = acc[a][3] = 0.f;
+    for (int base = blockIdx.x * kProjTile; base < n; base += gridDim.x * kProjTile) {
+        if (threadIdx.x < 64) {            // wave 0 compacts the tile's rows of type t
+            const int i = base + threadIdx.x;
+            const bool mine = i < n && ntype[n_id[i]] == t;
+            const uint64_t bal = __ballot(mine);
+            const int pos = __popcll(bal & ((1ull << threadIdx.x) - 1ull));
+            if (mine) rows[pos] = i;
+            if (threadIdx.x == 0) s_cnt = __popcll(bal);
+        }
+        __syncthreads();
+        const int cnt = s_cnt;
+        for (int q = threadIdx.x; q < cnt * (K / 4); q += kBlock) {
+            const int r = q / (K / 4), c = q - r * (K / 4);
+            const int i = rows[r];
+            *reinterpret_cast<float4*>(xsh + r * XS + 4 * c) =
+                *reinterpret_cast<const float4*>(X + local[n_id[i]] * int64_t(K) + 4 * c);
+        }
+        for (int q = threadIdx.x; q < cnt * (F / 4); q += kBlock) {
+            const int r = q / (F / 4), c = q - r * (F / 4);
+            *reinterpret_cast<float4*>(gsh + r * GS + 4 * c) =
+                *reinterpret_cast<const float4*>(gxs + int64_t(rows[r]) * F + 4 * c);
+        }
+        __syncthreads();
+        for (int r = 0; r < cnt; ++r) {
+            const float4 g = *reinterpret_cast<const float4*>(gsh + r * GS + 4 * j4);
+            if (kq == 0) {
+                accb[0] += g.x; accb[1] += g.y; accb[2] += g.z; accb[3] += g.w;
+            }
+#pragma unroll
+            for (int a = 0; a < KPT; a += 4) {
+                const float4 x = *reinterpret_cast<const float4*>(xsh + r * XS + kq * KPT + a);
+                const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc[a + u][0] = fmaf(xv[u], g.x, acc[a + u][0]);
+                    acc[a + u][1] = fmaf(xv[u], g.y, acc[a + u][1]);
+                    acc[a + u][2] = fmaf(xv[u], g.z, acc[a + u][2]);
+                    acc[a + u][3] = fmaf(xv[u], g.w, acc[a + u][3]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    float* o = slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
+#pragma unroll
+    for (int a = 0; a < KPT; ++a)
+        *reinterpret_cast<float4*>(o + (kq * KPT + a) * F + 4 * j4) =
+            make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
+    if (kq == 0)
+        *reinterpret_cast<float4*>(o + K * F + 4 * j4) = make_float4(accb[0], accb[1], accb[2], accb[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// finalize: one launch, a job per block range (fixed-order sums everywhere).
+struct FinArgs {
+    const int32_t* sizes; int L; int C; int T; int K; float alpha;
+    // out_lin
+    const float* glogits; const float* h_last; float* g_out_w; float* g_out_b;
+    // per layer (index l): row buffers over sizes[L-1-l] rows
+    const float* ga[ML]; const float* gy[ML]; const float* gyx[ML];
+    float* g_conv_b[ML]; float* g_ln_b[ML]; float* g_ln_w[ML];
+    // relation tables
+    const float* rel_slab[ML]; const float* rw[ML]; int n_rel[ML]; float* g_rw[ML];
+    // conv weights l >= 1 from the post_bwd slabs of layer l-1
+    const float* w_slab[ML]; float* g_conv_w[ML];
+    // composed first map
+    const float* proj_slab; float* gwc;
+    // loss
+    const float* loss_rows; int cap0; float* loss;
+    // job boundaries (block indices)
+    int j_out, j_rows, j_rel, j_w, j_wc, j_loss;
+};
+
+__global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
+    __shared__ float sh[4][F + 1];
+    __shared__ float gsh[64][17];
+    __shared__ float hsh[64][F + 1];
+    int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (b < A.j_out) {                    // out_lin: 16 classes per block
+        const int c0 = b * 16;
+        const int n0 = A.sizes[0];
+        const int cl = tid >> 4, kq = tid & 15;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        float accb = 0.f;
+        for (int r0 = 0; r0 < n0; r0 += 64) {
+            const int nr = min(64, n0 - r0);
+            for (int q = tid; q < nr * 16; q += kBlock) {
+                const int r = q >> 4, c = q & 15;
+                gsh[r][c] = c0 + c < A.C ? A.glogits[int64_t(r0 + r) * A.C + c0 + c] : 0.f;
+            }
+            for (int q = tid; q < nr * F; q += kBlock) {
+                const int r = q / F, k = q % F;
+                hsh[r][k] = A.h_last[int64_t(r0 + r) * F + k];
+            }
+            __syncthreads();
+            for (int r = 0; r < nr; ++r) {
+                const float g = gsh[r][cl];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] = fmaf(g, hsh[r][4 * kq + u], acc[u]);
+                accb += g;
+            }
+            __syncthreads();
+        }
+        const int c = c0 + cl;
+        if (c < A.C) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) A.g_out_w[int64_t(c) * F + 4 * kq + u] = acc[u];
+            if (kq == 0) A.g_out_b[c] = accb;
+        }
+        return;
+    }
+    b -= A.j_out;
+    if (b < A.j_rows) {                   // per layer: column sums of ga / gy / gyx
+        const int l = b / 3, which = b % 3;
+        const float* src = which == 0 ? A.ga[l] : which == 1 ? A.gy[l] : A.gyx[l];
+        float* dst = which == 0 ? A.g_conv_b[l] : which == 1 ? A.g_ln_b[l] : A.g_ln_w[l];
+        const int n = A.sizes[A.L - 1 - l];
+        const int j = tid & 63, part = tid >> 6;
+        float s = 0.f;
+        for (int v = part; v < n; v += 4) s += src[int64_t(v) * F + j];
+        sh[part][j] = s;
+        __syncthreads();
+        if (tid < F) dst[tid] = ((sh[0][tid] + sh[1][tid]) + sh[2][tid]) + sh[3][tid];
+        return;
+    }
+    b -= A.j_rows;
+    if (b < A.j_rel) {                    // relation tables: sum of per-block bins, chain rule
+        const int l = b;
+        if (tid < A.n_rel[l]) {
+            float s = 0.f;
+            for (int k = 0; k < kAggBlocks; ++k) s += A.rel_slab[l][int64_t(k) * F + tid];
+            const float x = A.rw[l][tid] * A.alpha;
+            A.g_rw[l][tid] = s * A.alpha * (x > 0.f ? 1.f : 0.01f);
+        }
+        return;
+    }
+    b -= A.j_rel;
+    if (b < A.j_w) {                      // convs[l].weight, l >= 1: 16 blocks per layer
+        const int l = 1 + b / 16;
+        const int e = (b % 16) * kBlock + tid;
+        float s = 0.f;
+        for (int k = 0; k < kPostBlocks; ++k) s += A.w_slab[l][int64_t(k) * F * F + e];
+        A.g_conv_w[l][e] = s;
+        return;
+    }
+    b -= A.j_w;
+    if (b < A.j_wc) {                     // composed map: per-type partials over project blocks
+        const int64_t e = int64_t(b) * kBlock + tid;
+        const int64_t per = int64_t(A.K + 1) * F;
+        if (e < A.T * per) {
+            const int t = int(e / per);
+            const int64_t o = e - t * per;
+            float s = 0.f;
+            for (int k = 0; k < kProjBlocks; ++k) s += A.proj_slab[(int64_t(t) * kProjBlocks + k) * per + o];
+            A.gwc[e] = s;
+        }
+        return;
+    }
+    b -= A.j_wc;
+    if (b < A.j_loss) {                   // mean nll
+        const int n0 = A.sizes[0];
+        float s = 0.f;
+        for (int v = tid; v < n0; v += kBlock) s += A.loss_rows[v];
+        s = wave_sum(s);
+        if ((tid & 63) == 0) sh[0][tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) {
+            const float nv = A.loss_rows[A.cap0];
+            const float tot = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
+            *A.loss = nv > 0.f ? tot / nv : 0.f;
+        }
+    }
+}
+
+// chain rule of the composed map W_c[t] = W_t^T W_0, b_c[t] = b_t W_0 (one thread per output):
+//   g W_t[o][k] = sum_j W_0[o][j] gW_c[t][k][j];  g b_t[o] = sum_j W_0[o][j] gb_c[t][j];
+//   g W_0[o][j] = sum_t (sum_k W_t[o][k] gW_c[t][k][j] + b_t[o] gb_c[t][j])
+struct ChainArgs {
+    int T; int K; Ptrs lin_w; Ptrs lin_b; const float* w0; const float* gwc;
+    float* g_lin_w[MT]; float* g_lin_b[MT]; float* g_w0;
+};
+
+__global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
+    const int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const int K = A.K;
+    const int64_t per = int64_t(F) * (K + 1);           // g W_t (64 x K) then g b_t (64)
+    if (e < A.T * per) {
+        const int t = int(e / per);
+        const int64_t r = e - t * per;
+        const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
+        if (r < int64_t(F) * K) {
+            const int o = int(r / K), k = int(r % K);
+            float s = 0.f;
+            for (int j = 0; j < F; ++j) s = fmaf(A.w0[o * F + j], gw[int64_t(k) * F + j], s);
+            pick(A.g_lin_w, t)[r] = s;
+        } else {
+            const int o = int(r - int64_t(F) * K);
+            float s = 0.f;
+            for (int j = 0; j < F; ++j) s = fmaf(A.w0[o * F + j], gw[int64_t(K) * F + j], s);
+            pick(A.g_lin_b, t)[o] = s;
+        }
+        return;
+    }
+    const int64_t q = e - A.T * per;
+    if (q >= F * F) return;
+    const int o = int(q / F), j = int(q % F);
+    float s = 0.f;
+    for (int t = 0; t < A.T; ++t) {
+        const float* W = pick(A.lin_w.p, t);
+        const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
+        for (int k = 0; k < K; ++k) s = fmaf(W[int64_t(o) * K + k], gw[int64_t(k) * F + j], s);
+        s = fmaf(pick(A.lin_b.p, t)[o], gw[int64_t(K) * F + j], s);
+    }
+    A.g_w0[q] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+struct SlabLayout {
+    int64_t rel[ML], w[ML], proj, total;
+};
+
+inline SlabLayout slab_layout(const regnn_nsm_params* p) {
+    SlabLayout s{};
+    int64_t o = 0;
+    for (int l = 0; l < ML; ++l) {
+        s.rel[l] = o;
+        if (l < p->n_layers) o += int64_t(kAggBlocks) * F;
+    }
+    for (int l = 0; l < ML; ++l) {        // w[l]: partials of convs[l].weight (l >= 1)
+        s.w[l] = o;
+        if (l >= 1 && l < p->n_layers) o += int64_t(kPostBlocks) * F * F;
+    }
+    s.proj = o;
+    o += int64_t(p->n_types) * kProjBlocks * (p->k_in + 1) * F;
+    s.total = o;
+    return s;
+}
+
+inline Drop make_drop(float p) {
+    Drop d{};
+    d.on = p > 0.f;
+    const float keep = 1.f - p;
+    int k16 = int(keep * 65536.f + 0.5f);
+    if (k16 > 65536) k16 = 65536;
+    d.thresh = uint32_t(k16);
+    d.scale = d.on ? 1.f / keep : 1.f;
+    d.b8 = (k16 % 256) == 0;
+    return d;
+}
+
+bool set_lds(const void* k, size_t bytes) {
+    if (bytes <= 64 * 1024) return true;
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes)) ==
+           hipSuccess;
+}
+
+}  // namespace nsm
+}  // namespace regnn
+
+using namespace regnn;
+using namespace regnn::nsm;
+
+extern "C" {
+
+int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p) {
+    if (!p) return -1;
+    return slab_layout(p).total;
+}
+
+int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
+    if (!p || !w) return REGNN_EINVAL;
+    const int T = p->n_types, K = p->k_in, L = p->n_layers, C = p->n_classes;
+    if (T < 1 || T > MT || L < 1 || L > ML || C < 1 || C > 512 || (K != 64 && K != 128) ||
+        T * (K + 1) > 600 || !(p->p_drop >= 0.f && p->p_drop < 1.f))
+        return REGNN_EUNSUPPORTED;
+    for (int l = 0; l < L; ++l)
+        if (p->n_rel[l] < 1 || p->n_rel[l] > F) return REGNN_EUNSUPPORTED;
+    if (!w->state || !w->sizes || !w->n_id || !w->ntype || !w->local || !w->labels || !w->wc ||
+        !w->gwc || !w->tabs || !w->h_last || !w->glogits || !w->loss_rows || !w->slab || !p->loss ||
+        !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b)
+        return REGNN_EINVAL;
+    for (int t = 0; t < T; ++t)
+        if (!p->x_tab[t] || !p->lin_w[t] || !p->lin_b[t] || !p->g_lin_w[t] || !p->g_lin_b[t])
+            return REGNN_EINVAL;
+    for (int l = 0; l < L; ++l) {
+        const int h = L - 1 - l;
+        if (!p->conv_w[l] || !p->conv_b[l] || !p->conv_rw[l] || !p->ln_w[l] || !p->ln_b[l] ||
+            !p->g_conv_w[l] || !p->g_conv_b[l] || !p->g_conv_rw[l] || !p->g_ln_w[l] ||
+            !p->g_ln_b[l] || !w->xs[l] || !w->gxs[l] || !w->ga[l] || !w->gy[l] || !w->gyx[l] ||
+            !w->blk_ptr[h] || !w->blk_idx[h] || !w->blk_rel[h] || !w->blk_inv[h] ||
+            w->cap[h] <= 0 || w->cap[h + 1] <= 0)
+            return REGNN_EINVAL;
+        if (l < L - 1 && (!w->a[l] || !w->stats[l])) return REGNN_EINVAL;
+    }
+    const SlabLayout S = slab_layout(p);
+    const Drop drop = make_drop(p->p_drop);
+    Ptrs lin_w{}, lin_b{}, xt{}, rw{};
+    for (int t = 0; t < T; ++t) {
+        lin_w.p[t] = p->lin_w[t];
+        lin_b.p[t] = p->lin_b[t];
+        xt.p[t] = p->x_tab[t];
+    }
+    for (int l = 0; l < L; ++l) rw.p[l] = p->conv_rw[l];
+
+    // 1. composed first map + relation tables
+    Ints nrel{};
+    for (int l = 0; l < L; ++l) nrel.v[l] = p->n_rel[l];
+    hipLaunchKernelGGL(prep_kernel, dim3(T * (K + 1) + L), dim3(64), 0, stream, T, K, lin_w,
+                       lin_b, p->conv_w[0], rw, L, nrel, p->alpha, w->wc, w->tabs);
+    REGNN_LAUNCH_CHECK();
+    // 2. projection of the outermost hop's sources (hop L) -> layer 0's rows
+    {
+        const size_t lds = size_t(T) * ((K + 1) * F + 4) * sizeof(float);
+        static bool ok = set_lds(reinterpret_cast<const void*>(&project_kernel), 160 * 1024);
+        if (!ok || lds > 160 * 1024) return REGNN_EUNSUPPORTED;
+        const int rows = w->cap[L];
+        int grid = (rows + 255) / 256;
+        if (grid > 256) grid = 256;
+        hipLaunchKernelGGL(project_kernel, dim3(grid), dim3(1024), lds, stream, w->n_id, w->sizes,
+                           L, w->ntype, w->local, T, K, xt, w->wc, w->xs[0], w->gxs[0]);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 3. layers 0 .. L-2
+    for (int l = 0; l < L - 1; ++l) {
+        const int h = L - 1 - l;
+        AggArgs A{};
+        A.sizes = w->sizes; A.hop = h;
+        A.ptr = w->blk_ptr[h]; A.idx = w->blk_idx[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.tab = w->tabs + l * F; A.xs = w->xs[l]; A.bias = p->conv_b[l];
+        A.ln_w = p->ln_w[l]; A.ln_b = p->ln_b[l]; A.state = w->state; A.layer = l; A.drop = drop;
+        A.w_next = p->conv_w[l + 1];
+        A.a = w->a[l]; A.stats = w->stats[l]; A.xs_next = w->xs[l + 1]; A.gxs_next = w->gxs[l + 1];
+        int grid = (w->cap[h] + 15) / 16;
+        if (grid > 1024) grid = 1024;
+        hipLaunchKernelGGL(agg_kernel, dim3(grid), dim3(kBlock), 0, stream, A);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 4. last layer + head + loss + backward to its pre-LN rows
+    {
+        const int l = L - 1;
+        HeadArgs H{};
+        H.sizes = w->sizes; H.n_id = w->n_id; H.labels = w->labels;
+        H.ptr = w->blk_ptr[0]; H.idx = w->blk_idx[0]; H.rel = w->blk_rel[0]; H.inv = w->blk_inv[0];
+        H.tab = w->tabs + l * F; H.xs = w->xs[l]; H.bias = p->conv_b[l];
+        H.ln_w = p->ln_w[l]; H.ln_b = p->ln_b[l]; H.state = w->state; H.layer = l; H.drop = drop;
+        H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
+        H.h_last = w->h_last; H.glogits = w->glogits; H.loss_rows = w->loss_rows;
+        H.ga = w->ga[l]; H.gy = w->gy[l]; H.gyx = w->gyx[l]; H.cap0 = w->cap[0];
+        const size_t lds = (size_t(C) * kWPad + kHeadRows * F + size_t(kHeadRows) * C) * sizeof(float);
+        static bool ok = set_lds(reinterpret_cast<const void*>(&head_kernel), 160 * 1024);
+        if (!ok || lds > 150 * 1024) return REGNN_EUNSUPPORTED;
+        const int grid = (w->cap[0] + kHeadRows - 1) / kHeadRows;
+        hipLaunchKernelGGL(head_kernel, dim3(grid), dim3(kHeadRows * 64), lds, stream, H);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 5. backward, last layer first
+    for (int l = L - 1; l >= 0; --l) {
+        const int h = L - 1 - l;
+        AggBwdArgs B{};
+        B.sizes = w->sizes; B.hop = h;
+        B.ptr = w->blk_ptr[h]; B.idx = w->blk_idx[h]; B.rel = w->blk_rel[h]; B.inv = w->blk_inv[h];
+        B.tab = w->tabs + l * F; B.xs = w->xs[l]; B.ga = w->ga[l]; B.gxs = w->gxs[l];
+        B.slab = w->slab + S.rel[l]; B.n_rel = p->n_rel[l];
+        hipLaunchKernelGGL(agg_bwd_kernel, dim3(kAggBlocks), dim3(kBlock),
+                           size_t(p->n_rel[l]) * kBlock * sizeof(float), stream, B);
+        REGNN_LAUNCH_CHECK();
+        if (l == 0) break;
+        PostArgs Q{};
+        const int lp = l - 1, hp = L - 1 - lp;
+        Q.sizes = w->sizes; Q.hop = hp;
+        Q.a = w->a[lp]; Q.stats = w->stats[lp]; Q.ln_w = p->ln_w[lp]; Q.ln_b = p->ln_b[lp];
+        Q.state = w->state; Q.layer = lp; Q.drop = drop;
+        Q.w_next = p->conv_w[l]; Q.gxs_next = w->gxs[l];
+        Q.ga = w->ga[lp]; Q.gy = w->gy[lp]; Q.gyx = w->gyx[lp]; Q.slab = w->slab + S.w[l];
+        hipLaunchKernelGGL(post_bwd_kernel, dim3(kPostBlocks), dim3(kBlock), 0, stream, Q);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 6. composed first map: per-type x^T g partials
+    {
+        const dim3 grid(kProjBlocks, T);
+        float* sl = w->slab + S.proj;
+        switch (K / 16) {
+#define PB_CASE(KPT_)                                                                        \
+    case KPT_:                                                                               \
+        hipLaunchKernelGGL(project_bwd_kernel<KPT_>, grid, dim3(kBlock), 0, stream, w->n_id, \
+                           w->sizes, L, w->ntype, w->local, xt, w->gxs[0], sl);              \
+        break;
+            PB_CASE(4) PB_CASE(8)
+#undef PB_CASE
+            default: return REGNN_EUNSUPPORTED;
+        }
+        REGNN_LAUNCH_CHECK();
+    }
+    // 7. reductions
+    {
+        FinArgs A{};
+        A.sizes = w->sizes; A.L = L; A.C = C; A.T = T; A.K = K; A.alpha = p->alpha;
+        A.glogits = w->glogits; A.h_last = w->h_last; A.g_out_w = p->g_out_w; A.g_out_b = p->g_out_b;
+        for (int l = 0; l < L; ++l) {
+            A.ga[l] = w->ga[l]; A.gy[l] = w->gy[l]; A.gyx[l] = w->gyx[l];
+            A.g_conv_b[l] = p->g_conv_b[l]; A.g_ln_b[l] = p->g_ln_b[l]; A.g_ln_w[l] = p->g_ln_w[l];
+            A.rel_slab[l] = w->slab + S.rel[l]; A.rw[l] = p->conv_rw[l]; A.n_rel[l] = p->n_rel[l];
+            A.g_rw[l] = p->g_conv_rw[l];
+            A.w_slab[l] = w->slab + S.w[l]; A.g_conv_w[l] = p->g_conv_w[l];
+        }
+        A.proj_slab = w->slab + S.proj; A.gwc = w->gwc;
+        A.loss_rows = w->loss_rows; A.cap0 = w->cap[0]; A.loss = p->loss;
+        A.j_out = (C + 15) / 16;
+        A.j_rows = 3 * L;
+        A.j_rel = L;
+        A.j_w = 16 * (L - 1);
+        A.j_wc = int((int64_t(T) * (K + 1) * F + kBlock - 1) / kBlock);
+        A.j_loss = 1;
+        const int grid = A.j_out + A.j_rows + A.j_rel + A.j_w + A.j_wc + A.j_loss;
+        hipLaunchKernelGGL(finalize_kernel, dim3(grid), dim3(kBlock), 0, stream, A);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 8. chain rule onto lins[t] and convs[0].weight
+    {
+        ChainArgs A{};
+        A.T = T; A.K = K; A.lin_w = lin_w; A.lin_b = lin_b; A.w0 = p->conv_w[0]; A.gwc = w->gwc;
+        for (int t = 0; t < T; ++t) {
+            A.g_lin_w[t] = p->g_lin_w[t];
+            A.g_lin_b[t] = p->g_lin_b[t];
+        }
+        A.g_w0 = p->g_conv_w[0];
+        const int64_t n = int64_t(T) * F * (K + 1) + F * F;
+        hipLaunchKernelGGL(chain_kernel, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           stream, A);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
+}  // extern "C"

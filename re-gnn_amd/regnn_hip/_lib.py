@@ -86,6 +86,8 @@ _SIG = {
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P], ctypes.c_int),
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
+    "regnn_nsm_slab_floats": ([P], I64),
+    "regnn_nsm_step": ([P, P, P], ctypes.c_int),
 }
 
 for _name, (_args, _ret) in _SIG.items():
@@ -94,7 +96,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 19
+ABI_VERSION = 20
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -14,10 +14,13 @@ synchronisation, so one training step is one HIP-graph replay.
 
 The sampled indices follow the build's sampler spec (oracle/sampler_oracle.py, bit-exact).
 """
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
 from . import _lib as L
+from .profile import timed
 
 M64 = (1 << 64) - 1
 
@@ -162,6 +165,152 @@ class DeviceSampler:
         return sz[len(self.sizes_k)], out
 
 
+_P = ctypes.c_void_p
+_MT, _ML = 8, 4
+
+
+class _NsmParams(ctypes.Structure):
+    """regnn_nsm_params (include/regnn_hip.h)."""
+    _fields_ = [("n_types", ctypes.c_int32), ("k_in", ctypes.c_int32),
+                ("n_layers", ctypes.c_int32), ("n_classes", ctypes.c_int32),
+                ("alpha", ctypes.c_float), ("p_drop", ctypes.c_float),
+                ("n_rel", ctypes.c_int32 * _ML),
+                ("x_tab", _P * _MT), ("lin_w", _P * _MT), ("lin_b", _P * _MT),
+                ("conv_w", _P * _ML), ("conv_b", _P * _ML), ("conv_rw", _P * _ML),
+                ("ln_w", _P * _ML), ("ln_b", _P * _ML), ("out_w", _P), ("out_b", _P),
+                ("g_lin_w", _P * _MT), ("g_lin_b", _P * _MT), ("g_conv_w", _P * _ML),
+                ("g_conv_b", _P * _ML), ("g_conv_rw", _P * _ML), ("g_ln_w", _P * _ML),
+                ("g_ln_b", _P * _ML), ("g_out_w", _P), ("g_out_b", _P), ("loss", _P)]
+
+
+class _NsmWork(ctypes.Structure):
+    """regnn_nsm_work (include/regnn_hip.h)."""
+    _fields_ = [("state", _P), ("sizes", _P), ("n_id", _P), ("cap", ctypes.c_int32 * (_ML + 1)),
+                ("blk_ptr", _P * _ML), ("blk_idx", _P * _ML), ("blk_rel", _P * _ML),
+                ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
+                ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
+                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("gy", _P * _ML),
+                ("gyx", _P * _ML), ("h_last", _P), ("glogits", _P), ("loss_rows", _P),
+                ("slab", _P)]
+
+
+def fused_unsupported(model, x_dict):
+    """why regnn_nsm_step cannot run this model (None: it can). The fused step covers the
+    reference configuration of mag/regnn_ns.py: model 'regcn', self_loop_type 2, use_norm 'ln',
+    no residual, feats_type != 2, hidden 64, equal input widths 64 / 128, <= 8 node types,
+    <= 4 layers, <= 512 classes."""
+    if getattr(model, "model", None) != "regcn" or getattr(model, "feats_type", 3) == 2:
+        return "model is not the feats_type-3 regcn"
+    if model.self_loop_type != 2:
+        return "self_loop_type != 2"
+    convs = list(model.convs)
+    if not 1 <= len(convs) <= _ML:
+        return "1..4 layers"
+    for c in convs:
+        if c.residual or c.use_norm != "ln" or tuple(c.weight.shape) != (64, 64):
+            return "conv needs LayerNorm, no residual, hidden 64"
+        if c.relation_weight.numel() > 64 or abs(c.scaling_factor - convs[0].scaling_factor) > 0:
+            return "relation table > 64 or mixed scaling factors"
+    keys = sorted(x_dict)
+    if keys != list(range(len(keys))) or len(keys) > _MT:
+        return "x_dict keys must be 0..T-1, T <= 8"
+    dims = {int(x_dict[k].shape[1]) for k in keys}
+    if len(dims) != 1 or dims.pop() not in (64, 128):
+        return "input widths must be equal, 64 or 128"
+    if any(x_dict[k].dtype != torch.float32 or not x_dict[k].is_contiguous() for k in keys):
+        return "inputs must be contiguous fp32"
+    if model.out_lin.weight.shape[0] > 512 or model.out_lin.weight.shape[1] != 64:
+        return "out_lin must be 64 -> <= 512"
+    return None
+
+
+class FusedStep:
+    """regnn_nsm_step over a DeviceSampler's blocks: the model's forward, nll loss and backward
+    in ten launches (two layers), gradients written straight into each parameter's .grad (the
+    caller's flat bucket views), loss into `loss`. Keeps every buffer it points the library at."""
+
+    def __init__(self, model, sampler, x_dict, node_type, local_node_idx, y_flat, loss):
+        why = fused_unsupported(model, x_dict)
+        if why is not None:
+            raise ValueError(f"regnn_nsm_step does not cover this model: {why}")
+        dev = sampler.device
+        self.device = dev
+        nl = len(model.convs)
+        if len(sampler.sizes_k) != nl:
+            raise ValueError(f"{nl} layers need {nl} sampler hops, got {len(sampler.sizes_k)}")
+        keys = sorted(x_dict)
+        T, K = len(keys), int(x_dict[0].shape[1])
+        C = int(model.out_lin.weight.shape[0])
+        caps = sampler.caps
+        self.keep = []                                 # every tensor the structs point at
+
+        def ptr(t):
+            self.keep.append(t)
+            return t.data_ptr()
+
+        def grad_ptr(p):
+            if p.grad is None:                        # frozen parameter (no_re): scratch
+                p_scratch = torch.zeros_like(p)
+                return ptr(p_scratch)
+            return ptr(p.grad)
+
+        P = self.P = _NsmParams()
+        P.n_types, P.k_in, P.n_layers, P.n_classes = T, K, nl, C
+        P.alpha = float(model.convs[0].scaling_factor)
+        P.p_drop = float(model.dropout) if model.training else 0.0
+        for t, k in enumerate(keys):
+            lin = model.lins[str(k)]
+            P.x_tab[t] = ptr(x_dict[k])
+            P.lin_w[t], P.lin_b[t] = ptr(lin.weight), ptr(lin.bias)
+            P.g_lin_w[t], P.g_lin_b[t] = grad_ptr(lin.weight), grad_ptr(lin.bias)
+        for l, c in enumerate(model.convs):
+            P.n_rel[l] = c.relation_weight.numel()
+            P.conv_w[l], P.conv_b[l], P.conv_rw[l] = ptr(c.weight), ptr(c.bias), ptr(c.relation_weight)
+            P.ln_w[l], P.ln_b[l] = ptr(c.norm.weight), ptr(c.norm.bias)
+            P.g_conv_w[l], P.g_conv_b[l] = grad_ptr(c.weight), grad_ptr(c.bias)
+            P.g_conv_rw[l] = grad_ptr(c.relation_weight)
+            P.g_ln_w[l], P.g_ln_b[l] = grad_ptr(c.norm.weight), grad_ptr(c.norm.bias)
+        P.out_w, P.out_b = ptr(model.out_lin.weight), ptr(model.out_lin.bias)
+        P.g_out_w, P.g_out_b = grad_ptr(model.out_lin.weight), grad_ptr(model.out_lin.bias)
+        P.loss = ptr(loss)
+
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=dev)  # noqa: E731
+        W = self.W = _NsmWork()
+        W.state, W.sizes, W.n_id = ptr(sampler.state), ptr(sampler.sizes), ptr(sampler.n_id)
+        for h, c in enumerate(caps):
+            W.cap[h] = c
+        for h, blk in enumerate(sampler.blocks):
+            W.blk_ptr[h], W.blk_idx[h] = ptr(blk.csr_ptr), ptr(blk.csr_idx)
+            W.blk_rel[h], W.blk_inv[h] = ptr(blk.rel), ptr(blk.inv)
+        W.ntype = ptr(sampler.ntype)
+        W.local = ptr(torch.as_tensor(local_node_idx).to(dev, torch.int64).contiguous())
+        W.labels = ptr(y_flat.to(dev, torch.int64).contiguous())
+        W.wc, W.gwc, W.tabs = ptr(z(T, K + 1, 64)), ptr(z(T, K + 1, 64)), ptr(z(nl, 64))
+        for l in range(nl):
+            n_src, n_dst = caps[nl - l], caps[nl - 1 - l]
+            W.xs[l], W.gxs[l] = ptr(z(n_src, 64)), ptr(z(n_src, 64))
+            W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
+            W.ga[l], W.gy[l], W.gyx[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 64)), ptr(z(n_dst, 64))
+        W.h_last, W.glogits = ptr(z(caps[0], 64)), ptr(z(caps[0], C))
+        W.loss_rows = ptr(z(caps[0] + 1))
+        W.slab = ptr(z(_slab_floats(P)))
+        self.model = model
+
+    def step(self):
+        # train / eval decides the dropout (a captured graph keeps the value it was captured with)
+        self.P.p_drop = float(self.model.dropout) if self.model.training else 0.0
+        with torch.cuda.device(self.device), timed("nsm_step"):
+            L.call("regnn_nsm_step", ctypes.addressof(self.P), ctypes.addressof(self.W),
+                   torch.cuda.current_stream(self.device).cuda_stream)
+
+
+def _slab_floats(P):
+    n = int(L._so.regnn_nsm_slab_floats(ctypes.addressof(P)))
+    if n <= 0:
+        raise RuntimeError("regnn_nsm_slab_floats rejected the parameters")
+    return n
+
+
 class NSTrainer:
     """One rank's NS training step (mag/regnn_ns.py:392-420) on the device sampler.
 
@@ -172,7 +321,7 @@ class NSTrainer:
 
     def __init__(self, model, opt, rg, sizes, batch_size, train_idx, x_dict, edge_type,
                  node_type, local_node_idx, y_global, num_edge_types, seed=0, rank=0, world=1,
-                 shuffle=True):
+                 shuffle=True, engine="auto"):
         self.model, self.opt = model, opt
         dev = rg.device
         self.device, self.rank, self.world = dev, int(rank), int(world)
@@ -190,8 +339,16 @@ class NSTrainer:
         for p in self.params:
             p.grad = self.flat[o:o + p.numel()].view_as(p)
             o += p.numel()
-        self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in ten HIP
+        # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
+        why = fused_unsupported(model, x_dict)
+        if engine == "fused" and why is not None:
+            raise ValueError(f"fused NS step unavailable: {why}")
+        self.fused = None
+        if engine != "module" and why is None:
+            self.fused = FusedStep(model, self.sampler, x_dict, node_type, local_node_idx,
+                                   self.y_flat, self.loss)
         self.graphs = None
         self.epoch = -1
         self.set_epoch(0)
@@ -219,6 +376,13 @@ class NSTrainer:
     # -- one step --------------------------------------------------------------------------------
     def _forward_backward(self):
         s = self.sampler
+        if self.fused is not None:
+            # every gradient is overwritten by the step (parameters the forward never reads,
+            # e.g. REGNN.norm, keep the zeros of the bucket's allocation)
+            s.batch_from_perm(self.perm, self.rank, self.world)
+            s.run_hops()
+            self.fused.step()
+            return
         self.flat.zero_()
         s.batch_from_perm(self.perm, self.rank, self.world)
         s.run_hops()
@@ -233,7 +397,6 @@ class NSTrainer:
         loss.backward()
         with torch.no_grad():
             self.loss.copy_(loss.detach())
-            self.loss_sum.add_(loss.detach() * s.sizes[0].to(torch.float32))
 
     def _exchange(self):
         if self.world > 1:

@@ -263,3 +263,71 @@ def _sample_row_global(row_idx, t, k, seed, base):
         chosen.append(j if pos in chosen else pos)
     chosen.sort()
     return [int(row_idx[p]) for p in chosen], [base + p for p in chosen]
+
+
+def _nsm_seed(state0, stamp, layer):
+    """the fused step's dropout seed of `layer` (include/regnn_hip.h, regnn_nsm_step)."""
+    from regnn_hip.sampler import _mix
+    M = (1 << 64) - 1
+    return _mix((state0 & M) ^ _mix(((stamp << 4) + layer + 0x51ED27) & M))
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_fused_step_matches_module_path(monkeypatch, dropout):
+    """regnn_nsm_step (the model's forward / nll / backward in ten launches) against the
+    mag.REGNN autograd path on the same sampled batch: loss and every parameter gradient at
+    1e-5. With dropout the module path gets the fused step's hash masks (oracle.dropout_mask of
+    the documented per-layer seed) in place of torch's RNG."""
+    from oracle import regnn_oracle as O
+    d = _mag(0.003, seed=6, F=128, hidden=64, classes=37, dropout=dropout)
+    m_mod, m_fus = d["model"](1), d["model"](1)
+    m_mod.train(); m_fus.train()
+    tr_m, _ = _setup_trainer(d, m_mod, batch=96, sizes=(7, 5))
+    tr_m.fused = None                                   # the module (autograd) path
+    tr_f, _ = _setup_trainer(d, m_fus, batch=96, sizes=(7, 5))
+    assert tr_f.fused is not None
+    tr_f._forward_backward()
+    torch.cuda.synchronize()
+    st = tr_f.sampler.state.cpu().tolist()
+    calls = []
+    if dropout > 0:
+        keep16 = int(round((1 - dropout) * 65536))
+
+        def hash_dropout(x, p=0.5, training=True, inplace=False):
+            layer = len(calls)
+            calls.append(layer)
+            seed = _nsm_seed(st[0], st[4], layer)
+            mask = O.dropout_mask(seed, x.shape[0], x.shape[1], 4, keep16)
+            return x * torch.from_numpy(mask).to(x.device, x.dtype) / (keep16 / 65536)
+        monkeypatch.setattr(torch.nn.functional, "dropout", hash_dropout)
+    tr_m._forward_backward()
+    torch.cuda.synchronize()
+    if dropout > 0:
+        assert calls == [0, 1]
+    assert torch.equal(tr_m.sampler.n_id, tr_f.sampler.n_id)
+    lm, lf = float(tr_m.loss), float(tr_f.loss)
+    assert abs(lm - lf) <= 1e-5 * max(1.0, abs(lm)), (lm, lf)
+    gm = dict(m_mod.named_parameters())
+    for n, p in m_fus.named_parameters():
+        ok, err = G.close(p.grad.cpu().numpy(), gm[n].grad.cpu().numpy().astype(np.float64), 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+
+
+def test_fused_step_graph_replay_tracks_eager():
+    """the fused step captured in a HIP graph: losses equal the eager twin's step by step."""
+    d = _mag(0.003, seed=7, F=128, hidden=64, classes=11, dropout=0.3)
+    tr_e, _ = _setup_trainer(d, d["model"](4), batch=128, sizes=(10, 5))
+    tr_g, _ = _setup_trainer(d, d["model"](4), batch=128, sizes=(10, 5))
+    assert tr_e.fused is not None and tr_g.fused is not None
+    tr_g.capture(warmup=2)
+    for _ in range(2):
+        tr_e.step()
+    tr_e.sampler.state[2:3].zero_()
+    le, lg = [], []
+    for _ in range(5):
+        tr_e.step()
+        le.append(float(tr_e.loss))
+        tr_g.replay()
+        lg.append(float(tr_g.loss))
+    assert np.all(np.isfinite(lg))
+    assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
