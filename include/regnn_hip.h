@@ -608,19 +608,18 @@ typedef struct regnn_nsm_work {
     float* tabs;              /* L * 64 floats */
     float* xs[REGNN_NSM_MAX_LAYERS];    /* layer l's source rows: cap[L-l] rows */
     float* gxs[REGNN_NSM_MAX_LAYERS];   /* their gradient: cap[L-l] rows */
-    float* a[REGNN_NSM_MAX_LAYERS];     /* layer l's pre-LayerNorm rows: cap[L-1-l] rows */
-    float* stats[REGNN_NSM_MAX_LAYERS]; /* (mean, rstd) per row: 2 * cap[L-1-l] floats */
+    float* a[REGNN_NSM_MAX_LAYERS];     /* layer l < L-1: pre-LayerNorm rows, cap[L-1-l] rows */
+    float* stats[REGNN_NSM_MAX_LAYERS]; /* layer l < L-1: (mean, rstd), 2 * cap[L-1-l] floats */
     float* ga[REGNN_NSM_MAX_LAYERS];    /* d loss / d pre-LN rows: cap[L-1-l] rows */
-    float* gy[REGNN_NSM_MAX_LAYERS];    /* d loss / d LN output: cap[L-1-l] rows */
-    float* gyx[REGNN_NSM_MAX_LAYERS];   /* gy * normalised rows: cap[L-1-l] rows */
-    float* h_last;            /* the last layer's output rows: cap[0] rows */
-    float* glogits;           /* d loss / d logits: cap[0] * C floats */
-    float* loss_rows;         /* cap[0] + 1 floats ([cap[0]] = labelled-target count) */
+    int32_t* row_type;        /* cap[L] int32: node type of each outermost source row */
+    int64_t* row_off;         /* cap[L] int64: its row in x_tab[type] */
+    float* nvalid;            /* 1 float: labelled targets of the batch */
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
 } regnn_nsm_work;
 
-/* Floats of the per-block partial slab regnn_nsm_step needs for these parameters. */
-int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p);
+/* Floats of the per-block partial slab regnn_nsm_step needs for these parameters and a batch
+ * capacity cap0 (= regnn_nsm_work.cap[0]). */
+int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0);
 
 /* One forward + loss + backward of the model over the current batch (after regnn_ns_batch and
  * the L regnn_ns_hop calls of the step): writes every g_* buffer (overwritten, not accumulated)

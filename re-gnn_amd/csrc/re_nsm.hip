@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(1024)
 project_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
                const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, int T, int K,
                Ptrs xt, const float* __restrict__ wc, float* __restrict__ xs,
-               float* __restrict__ gxs) {
+               float* __restrict__ gxs, int32_t* __restrict__ row_type,
+               int64_t* __restrict__ row_off) {
     extern __shared__ float lw[];
     const int str = (K + 1) * F + 4;
     for (int i = threadIdx.x; i < T * (K + 1) * (F / 4); i += blockDim.x) {
@@ -146,7 +147,12 @@ project_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ siz
     for (int i = blockIdx.x * rpb + (threadIdx.x >> 2); i < n; i += gridDim.x * rpb) {
         const int g = n_id[i];
         const int t = ntype[g];
-        const float* xr = pick(xt.p, t) + local[g] * int64_t(K);
+        const int64_t lo = local[g];
+        if (q == 0) {                      // row descriptors for project_bwd
+            row_type[i] = t;
+            row_off[i] = lo;
+        }
+        const float* xr = pick(xt.p, t) + lo * int64_t(K);
         const float* wt = lw + t * str + q * 16;
         float acc[16];
 #pragma unroll
@@ -279,27 +285,33 @@ __device__ __forceinline__ float lane_drop(uint32_t key, const Drop& d, int64_t 
 
 // ---------------------------------------------------------------------------------------------
 // head: the last layer (wave per target row, lane = feature) + out_lin + log_softmax + nll +
-// backward down to the pre-LN rows. out_lin.weight in LDS with rows padded to 65 floats.
+// backward down to the pre-LN rows (ga). out_lin.weight in LDS with rows padded to 65 floats.
+// The block's parameter-gradient partials go to one slab row (finalize sums them):
+//   [C*64: sum_r g[r][c] h[r][k] | C: sum_r g[r][c] | 64: sum_r ga | 64: sum_r gy |
+//    64: sum_r gy*xhat | 1: sum_r loss_r]
 struct HeadArgs {
     const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
     const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
     const float* tab; const float* xs; const float* bias; const float* ln_w; const float* ln_b;
     const int64_t* state; int layer; Drop drop;
     const float* w_out; const float* b_out; int C;
-    float* h_last; float* glogits; float* loss_rows; float* ga; float* gy; float* gyx;
-    int cap0;
+    float* ga; float* nvalid; float* part; int64_t part_w;
 };
 
-constexpr int kHeadRows = 4;           // waves (= rows) per block
+constexpr int kHeadRows = 8;           // waves (= rows) per block
+
+inline int64_t head_part_width(int C) { return ((int64_t(C) * (F + 1) + 3 * F + 1) + 3) & ~3ll; }
 
 __global__ void __launch_bounds__(kHeadRows * 64) head_kernel(HeadArgs A) {
-    extern __shared__ float hl[];      // [C][65] W_out, then [kHeadRows][F] h, [kHeadRows][C] g
-    float* Wl = hl;
-    float* hs = Wl + A.C * kWPad;
-    float* gs = hs + kHeadRows * F;
-    __shared__ float tab[F];
-    __shared__ int s_valid;
+    extern __shared__ float hl[];      // [C][65] W_out | [R][F] h | [R][C] g | [3][R][F] ga,gy,gyx
     const int C = A.C;
+    float* Wl = hl;
+    float* hs = Wl + C * kWPad;
+    float* gs = hs + kHeadRows * F;
+    float* rs = gs + kHeadRows * C;
+    __shared__ float tab[F];
+    __shared__ float lrow[kHeadRows];
+    __shared__ int s_valid;
     for (int i = threadIdx.x; i < C * F; i += blockDim.x) {
         const int c = i / F, k = i - c * F;
         Wl[c * kWPad + k] = A.w_out[i];
@@ -313,78 +325,110 @@ __global__ void __launch_bounds__(kHeadRows * 64) head_kernel(HeadArgs A) {
     atomicAdd(&s_valid, cnt);              // integer count: order-independent
     __syncthreads();
     const int n_valid = s_valid;
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.loss_rows[A.cap0] = float(n_valid);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
     const int v = blockIdx.x * kHeadRows + w;
-    if (v >= n) return;                    // no block-wide barrier below this point
-    float s = 0.f;
-    const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-    for (int e = e0; e < e1; ++e) s = fmaf(tab[A.rel[e]], A.xs[int64_t(A.idx[e]) * F + f], s);
-    const float a = fmaf(A.inv[v], s, A.bias[f]);
-    const float mean = wave_sum(a) * (1.f / F);
-    const float dlt = a - mean;
-    const float rstd = rsqrtf(wave_sum(dlt * dlt) * (1.f / F) + kLnEps);
-    const float xhat = dlt * rstd;
-    const float gw = A.ln_w[f], gb = A.ln_b[f];
-    const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
-    const float mfac = lane_drop(key, A.drop, v, f);
-    const float h = fmaxf(fmaf(xhat, gw, gb), 0.f) * mfac;
-    A.h_last[int64_t(v) * F + f] = h;
     float* hw = hs + w * F;
     float* gw_ = gs + w * C;
-    hw[f] = h;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xc07f);    // lgkmcnt(0): the wave's LDS writes are visible
-    constexpr int MC = 8;                  // up to 512 classes: 8 per lane
-    float z[MC];
-#pragma unroll
-    for (int m = 0; m < MC; ++m) {
-        const int c = f + 64 * m;
-        z[m] = c < C ? A.b_out[c] : -INFINITY;
-    }
-    for (int k = 0; k < F; ++k) {
-        const float hk = hw[k];
+    if (v < n) {                           // wave-uniform
+        float s = 0.f;
+        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        for (int e = e0; e < e1; ++e) s = fmaf(tab[A.rel[e]], A.xs[int64_t(A.idx[e]) * F + f], s);
+        const float a = fmaf(A.inv[v], s, A.bias[f]);
+        const float mean = wave_sum(a) * (1.f / F);
+        const float dlt = a - mean;
+        const float rstd = rsqrtf(wave_sum(dlt * dlt) * (1.f / F) + kLnEps);
+        const float xhat = dlt * rstd;
+        const float gw = A.ln_w[f], gb = A.ln_b[f];
+        const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
+        const float mfac = lane_drop(key, A.drop, v, f);
+        const float h = fmaxf(fmaf(xhat, gw, gb), 0.f) * mfac;
+        hw[f] = h;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);    // lgkmcnt(0): the wave's LDS writes are visible
+        constexpr int MC = 8;                  // up to 512 classes: 8 per lane
+        float z[MC];
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
             const int c = f + 64 * m;
-            if (c < C) z[m] = fmaf(hk, Wl[c * kWPad + k], z[m]);
+            z[m] = c < C ? A.b_out[c] : -INFINITY;
         }
-    }
-    float zmax = -INFINITY;
+        for (int k = 0; k < F; ++k) {
+            const float hk = hw[k];
 #pragma unroll
-    for (int m = 0; m < MC; ++m) zmax = fmaxf(zmax, z[m]);
-    zmax = wave_max(zmax);
-    float se = 0.f;
-#pragma unroll
-    for (int m = 0; m < MC; ++m)
-        if (f + 64 * m < C) se += expf(z[m] - zmax);
-    const float lse = zmax + logf(wave_sum(se));
-    const int64_t y = A.labels[A.n_id[v]];
-    float zy = 0.f;
-#pragma unroll
-    for (int m = 0; m < MC; ++m)
-        if (int64_t(f + 64 * m) == y) zy = z[m];
-    zy = wave_sum(zy);                     // exactly one lane holds it (or none: y < 0)
-    if (f == 0) A.loss_rows[v] = y >= 0 ? lse - zy : 0.f;
-    const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
-#pragma unroll
-    for (int m = 0; m < MC; ++m) {
-        const int c = f + 64 * m;
-        if (c < C) {
-            const float g = (expf(z[m] - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n;
-            gw_[c] = g;
-            A.glogits[int64_t(v) * C + c] = g;
+            for (int m = 0; m < MC; ++m) {
+                const int c = f + 64 * m;
+                if (c < C) z[m] = fmaf(hk, Wl[c * kWPad + k], z[m]);
+            }
         }
+        float zmax = -INFINITY;
+#pragma unroll
+        for (int m = 0; m < MC; ++m) zmax = fmaxf(zmax, z[m]);
+        zmax = wave_max(zmax);
+        float se = 0.f;
+#pragma unroll
+        for (int m = 0; m < MC; ++m)
+            if (f + 64 * m < C) se += expf(z[m] - zmax);
+        const float lse = zmax + logf(wave_sum(se));
+        const int64_t y = A.labels[A.n_id[v]];
+        float zy = 0.f;
+#pragma unroll
+        for (int m = 0; m < MC; ++m)
+            if (int64_t(f + 64 * m) == y) zy = z[m];
+        zy = wave_sum(zy);                     // exactly one lane holds it (or none: y < 0)
+        if (f == 0) lrow[w] = y >= 0 ? lse - zy : 0.f;
+        const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
+#pragma unroll
+        for (int m = 0; m < MC; ++m) {
+            const int c = f + 64 * m;
+            if (c < C) gw_[c] = (expf(z[m] - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        float gh = 0.f;
+        for (int c = 0; c < C; ++c) gh = fmaf(gw_[c], Wl[c * kWPad + f], gh);
+        float ga, gyv, gyx;
+        ln_relu_drop_bwd(gh, xhat, rstd, gw, gb, mfac, &ga, &gyv, &gyx);
+        A.ga[int64_t(v) * F + f] = ga;
+        rs[(0 * kHeadRows + w) * F + f] = ga;
+        rs[(1 * kHeadRows + w) * F + f] = gyv;
+        rs[(2 * kHeadRows + w) * F + f] = gyx;
+    } else {                               // rows past the batch contribute zeros
+        hw[f] = 0.f;
+        for (int c = f; c < C; c += 64) gw_[c] = 0.f;
+        rs[(0 * kHeadRows + w) * F + f] = 0.f;
+        rs[(1 * kHeadRows + w) * F + f] = 0.f;
+        rs[(2 * kHeadRows + w) * F + f] = 0.f;
+        if (f == 0) lrow[w] = 0.f;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    float gh = 0.f;
-    for (int c = 0; c < C; ++c) gh = fmaf(gw_[c], Wl[c * kWPad + f], gh);
-    float ga, gyv, gyx;
-    ln_relu_drop_bwd(gh, xhat, rstd, gw, gb, mfac, &ga, &gyv, &gyx);
-    A.ga[int64_t(v) * F + f] = ga;
-    A.gy[int64_t(v) * F + f] = gyv;
-    A.gyx[int64_t(v) * F + f] = gyx;
+    __syncthreads();
+    float* o = A.part + int64_t(blockIdx.x) * A.part_w;
+    for (int e = threadIdx.x; e < C * F; e += blockDim.x) {      // out_lin.weight partial
+        const int c = e >> 6, k = e & 63;
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kHeadRows; ++r) acc = fmaf(gs[r * C + c], hs[r * F + k], acc);
+        o[e] = acc;
+    }
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {          // out_lin.bias partial
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kHeadRows; ++r) acc += gs[r * C + c];
+        o[C * F + c] = acc;
+    }
+    if (threadIdx.x < 3 * F) {                                   // conv bias, LN beta, LN gamma
+        const int which = threadIdx.x >> 6;
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kHeadRows; ++r) acc += rs[(which * kHeadRows + r) * F + f];
+        o[C * (F + 1) + threadIdx.x] = acc;
+    }
+    if (threadIdx.x == 0) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kHeadRows; ++r) acc += lrow[r];
+        o[C * (F + 1) + 3 * F] = acc;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -427,19 +471,23 @@ __global__ void __launch_bounds__(kBlock) agg_bwd_kernel(AggBwdArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// post_bwd (layer l < L-1): gs = gxs_{l+1}[v]; gh = gs W_{l+1}^T; slab += h^T gs (this block's
-// rows); dropout / relu / LayerNorm backward -> ga, gy, gyx of layer l. Wave per row.
+// post_bwd (layer l < L-1): gs = gxs_{l+1}[v]; gh = gs W_{l+1}^T; dropout / relu / LayerNorm
+// backward -> ga of layer l. Wave per row. The block's partials go to one slab row:
+//   [64*64: sum_v h[v]^T gs[v] (convs[l+1].weight) | 64: sum ga | 64: sum gy | 64: sum gy*xhat]
+constexpr int kPostW = F * F + 3 * F;
+
 struct PostArgs {
     const int32_t* sizes; int hop;
     const float* a; const float* stats; const float* ln_w; const float* ln_b;
     const int64_t* state; int layer; Drop drop;
     const float* w_next; const float* gxs_next;
-    float* ga; float* gy; float* gyx; float* slab;
+    float* ga; float* slab;
 };
 
 __global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
     __shared__ float Wt[F * kWPad];        // W[k][j] at k*65 + j
     __shared__ float hs[4][F], gsr[4][F];
+    __shared__ float cs[3][4][F];
     for (int i = threadIdx.x; i < F * F; i += kBlock) Wt[(i / F) * kWPad + (i % F)] = A.w_next[i];
     __syncthreads();
     const int n = A.sizes[A.hop];
@@ -452,6 +500,7 @@ __global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
     float acc[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    float sga = 0.f, sgy = 0.f, sgyx = 0.f;
     for (int base = blockIdx.x * 4; base < n; base += gridDim.x * 4) {
         const int v = base + w;
         const bool act = v < n;
@@ -485,31 +534,41 @@ __global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
             float ga, gyv, gyx;
             ln_relu_drop_bwd(gh, xhat, rstd, gwf, gbf, mfac, &ga, &gyv, &gyx);
             A.ga[int64_t(v) * F + f] = ga;
-            A.gy[int64_t(v) * F + f] = gyv;
-            A.gyx[int64_t(v) * F + f] = gyx;
+            sga += ga; sgy += gyv; sgyx += gyx;
         }
         __syncthreads();
     }
-    float* o = A.slab + int64_t(blockIdx.x) * F * F + kk * F + j0;
+    float* o = A.slab + int64_t(blockIdx.x) * kPostW;
 #pragma unroll
     for (int c = 0; c < 16; c += 4)
-        *reinterpret_cast<float4*>(o + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
+        *reinterpret_cast<float4*>(o + kk * F + j0 + c) =
+            make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
+    cs[0][w][f] = sga; cs[1][w][f] = sgy; cs[2][w][f] = sgyx;
+    __syncthreads();
+    if (threadIdx.x < 3 * F) {
+        const int which = threadIdx.x >> 6;
+        o[F * F + threadIdx.x] =
+            ((cs[which][0][f] + cs[which][1][f]) + cs[which][2][f]) + cs[which][3][f];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
 // project_bwd: block (b, t) accumulates sum over rows i of type t of x_i^T g_i (K x 64) and
-// sum g_i (64) over its grid-stride share of 64-row tiles. Thread: k = kq*KPT .. +KPT-1 (16 k
-// groups), j = 4*j4 .. +3 (16 j groups).
+// sum g_i (64) over its grid-stride share of 64-row tiles, reading the row descriptors the
+// forward wrote (type, row of the type's table); wave 0 compacts a tile's rows of type t and
+// already loads the next tile's descriptors. Thread: k = kq*KPT .. +KPT-1 (16 k groups),
+// j = 4*j4 .. +3 (16 j groups). Slab row: [K*64 | 64].
 template <int KPT>
 __global__ void __launch_bounds__(kBlock)
-project_bwd_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
-                   const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, Ptrs xt,
-                   const float* __restrict__ gxs, float* __restrict__ slab) {
+project_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ row_type,
+                   const int64_t* __restrict__ row_off, Ptrs xt, const float* __restrict__ gxs,
+                   float* __restrict__ slab) {
     constexpr int K = KPT * 16;
     constexpr int XS = K + 4, GS = F + 4;
     __shared__ float xsh[kProjTile * XS];
     __shared__ float gsh[kProjTile * GS];
     __shared__ int rows[kProjTile];
+    __shared__ int64_t offs[kProjTile];
     __shared__ int s_cnt;
     const int t = blockIdx.y;
     const float* X = pick(xt.p, t);
@@ -519,22 +578,33 @@ project_bwd_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__
     float accb[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < KPT; ++a) acc[a][0] = acc[a][1] = acc[a][2] = acc[a][3] = 0.f;
-    for (int base = blockIdx.x * kProjTile; base < n; base += gridDim.x * kProjTile) {
+    const int stride = gridDim.x * kProjTile;
+    int rt = -1;
+    int64_t ro = 0;
+    if (threadIdx.x < 64) {
+        const int i = blockIdx.x * kProjTile + threadIdx.x;
+        if (i < n) { rt = row_type[i]; ro = row_off[i]; }
+    }
+    for (int base = blockIdx.x * kProjTile; base < n; base += stride) {
         if (threadIdx.x < 64) {            // wave 0 compacts the tile's rows of type t
-            const int i = base + threadIdx.x;
-            const bool mine = i < n && ntype[n_id[i]] == t;
+            const bool mine = rt == t;
             const uint64_t bal = __ballot(mine);
             const int pos = __popcll(bal & ((1ull << threadIdx.x) - 1ull));
-            if (mine) rows[pos] = i;
+            if (mine) {
+                rows[pos] = base + threadIdx.x;
+                offs[pos] = ro;
+            }
             if (threadIdx.x == 0) s_cnt = __popcll(bal);
+            const int i = base + stride + threadIdx.x;          // next tile's descriptors
+            rt = -1;
+            if (i < n) { rt = row_type[i]; ro = row_off[i]; }
         }
         __syncthreads();
         const int cnt = s_cnt;
         for (int q = threadIdx.x; q < cnt * (K / 4); q += kBlock) {
             const int r = q / (K / 4), c = q - r * (K / 4);
-            const int i = rows[r];
             *reinterpret_cast<float4*>(xsh + r * XS + 4 * c) =
-                *reinterpret_cast<const float4*>(X + local[n_id[i]] * int64_t(K) + 4 * c);
+                *reinterpret_cast<const float4*>(X + offs[r] * int64_t(K) + 4 * c);
         }
         for (int q = threadIdx.x; q < cnt * (F / 4); q += kBlock) {
             const int r = q / (F / 4), c = q - r * (F / 4);
@@ -572,186 +642,134 @@ project_bwd_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// finalize: one launch, a job per block range (fixed-order sums everywhere).
+// finalize: every gradient is a fixed-order sum of per-block partials. A job sums `nparts` rows
+// (stride pstride) of a slab segment of `width` floats into dst; 32 entries per block, 8
+// thread groups over the partials, combined in a fixed order.
+enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2 };
+
+struct Job {
+    const float* src;
+    int64_t pstride;
+    int nparts, width, op, blocks;
+    float* dst;
+    const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
+};
+
+constexpr int kMaxJobs = 32;
+
 struct FinArgs {
-    const int32_t* sizes; int L; int C; int T; int K; float alpha;
-    // out_lin
-    const float* glogits; const float* h_last; float* g_out_w; float* g_out_b;
-    // per layer (index l): row buffers over sizes[L-1-l] rows
-    const float* ga[ML]; const float* gy[ML]; const float* gyx[ML];
-    float* g_conv_b[ML]; float* g_ln_b[ML]; float* g_ln_w[ML];
-    // relation tables
-    const float* rel_slab[ML]; const float* rw[ML]; int n_rel[ML]; float* g_rw[ML];
-    // conv weights l >= 1 from the post_bwd slabs of layer l-1
-    const float* w_slab[ML]; float* g_conv_w[ML];
-    // composed first map
-    const float* proj_slab; float* gwc;
-    // loss
-    const float* loss_rows; int cap0; float* loss;
-    // job boundaries (block indices)
-    int j_out, j_rows, j_rel, j_w, j_wc, j_loss;
+    Job job[kMaxJobs];
+    int n_jobs;
+    float alpha;
 };
 
 __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
-    __shared__ float sh[4][F + 1];
-    __shared__ float gsh[64][17];
-    __shared__ float hsh[64][F + 1];
-    int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    if (b < A.j_out) {                    // out_lin: 16 classes per block
-        const int c0 = b * 16;
-        const int n0 = A.sizes[0];
-        const int cl = tid >> 4, kq = tid & 15;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        float accb = 0.f;
-        for (int r0 = 0; r0 < n0; r0 += 64) {
-            const int nr = min(64, n0 - r0);
-            for (int q = tid; q < nr * 16; q += kBlock) {
-                const int r = q >> 4, c = q & 15;
-                gsh[r][c] = c0 + c < A.C ? A.glogits[int64_t(r0 + r) * A.C + c0 + c] : 0.f;
-            }
-            for (int q = tid; q < nr * F; q += kBlock) {
-                const int r = q / F, k = q % F;
-                hsh[r][k] = A.h_last[int64_t(r0 + r) * F + k];
-            }
-            __syncthreads();
-            for (int r = 0; r < nr; ++r) {
-                const float g = gsh[r][cl];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) acc[u] = fmaf(g, hsh[r][4 * kq + u], acc[u]);
-                accb += g;
-            }
-            __syncthreads();
-        }
-        const int c = c0 + cl;
-        if (c < A.C) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) A.g_out_w[int64_t(c) * F + 4 * kq + u] = acc[u];
-            if (kq == 0) A.g_out_b[c] = accb;
-        }
-        return;
+    __shared__ float red[8][33];
+    int b = blockIdx.x, ji = 0;
+    while (ji < A.n_jobs - 1 && b >= A.job[ji].blocks) {
+        b -= A.job[ji].blocks;
+        ++ji;
     }
-    b -= A.j_out;
-    if (b < A.j_rows) {                   // per layer: column sums of ga / gy / gyx
-        const int l = b / 3, which = b % 3;
-        const float* src = which == 0 ? A.ga[l] : which == 1 ? A.gy[l] : A.gyx[l];
-        float* dst = which == 0 ? A.g_conv_b[l] : which == 1 ? A.g_ln_b[l] : A.g_ln_w[l];
-        const int n = A.sizes[A.L - 1 - l];
-        const int j = tid & 63, part = tid >> 6;
-        float s = 0.f;
-        for (int v = part; v < n; v += 4) s += src[int64_t(v) * F + j];
-        sh[part][j] = s;
-        __syncthreads();
-        if (tid < F) dst[tid] = ((sh[0][tid] + sh[1][tid]) + sh[2][tid]) + sh[3][tid];
-        return;
-    }
-    b -= A.j_rows;
-    if (b < A.j_rel) {                    // relation tables: sum of per-block bins, chain rule
-        const int l = b;
-        if (tid < A.n_rel[l]) {
-            float s = 0.f;
-            for (int k = 0; k < kAggBlocks; ++k) s += A.rel_slab[l][int64_t(k) * F + tid];
-            const float x = A.rw[l][tid] * A.alpha;
-            A.g_rw[l][tid] = s * A.alpha * (x > 0.f ? 1.f : 0.01f);
+    const Job J = A.job[ji];
+    const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    const int e = b * 32 + el;
+    float s = 0.f;
+    if (e < J.width) {
+        const float* src = J.src + e;
+        int p = grp;
+        for (; p + 24 < J.nparts; p += 32) {
+            const float v0 = src[int64_t(p) * J.pstride], v1 = src[int64_t(p + 8) * J.pstride];
+            const float v2 = src[int64_t(p + 16) * J.pstride], v3 = src[int64_t(p + 24) * J.pstride];
+            s += v0; s += v1; s += v2; s += v3;
         }
-        return;
+        for (; p < J.nparts; p += 8) s += src[int64_t(p) * J.pstride];
     }
-    b -= A.j_rel;
-    if (b < A.j_w) {                      // convs[l].weight, l >= 1: 16 blocks per layer
-        const int l = 1 + b / 16;
-        const int e = (b % 16) * kBlock + tid;
-        float s = 0.f;
-        for (int k = 0; k < kPostBlocks; ++k) s += A.w_slab[l][int64_t(k) * F * F + e];
-        A.g_conv_w[l][e] = s;
-        return;
-    }
-    b -= A.j_w;
-    if (b < A.j_wc) {                     // composed map: per-type partials over project blocks
-        const int64_t e = int64_t(b) * kBlock + tid;
-        const int64_t per = int64_t(A.K + 1) * F;
-        if (e < A.T * per) {
-            const int t = int(e / per);
-            const int64_t o = e - t * per;
-            float s = 0.f;
-            for (int k = 0; k < kProjBlocks; ++k) s += A.proj_slab[(int64_t(t) * kProjBlocks + k) * per + o];
-            A.gwc[e] = s;
+    red[grp][el] = s;
+    __syncthreads();
+    if (threadIdx.x < 32 && e < J.width) {
+        const float tot = ((red[0][el] + red[1][el]) + (red[2][el] + red[3][el])) +
+                          ((red[4][el] + red[5][el]) + (red[6][el] + red[7][el]));
+        float out = tot;
+        if (J.op == kOpRel) {
+            const float x = J.aux[e] * A.alpha;                // d tab / d rw (LeakyReLU)
+            out = tot * A.alpha * (x > 0.f ? 1.f : 0.01f);
+        } else if (J.op == kOpLoss) {
+            const float nv = *J.aux;
+            out = nv > 0.f ? tot / nv : 0.f;
         }
-        return;
-    }
-    b -= A.j_wc;
-    if (b < A.j_loss) {                   // mean nll
-        const int n0 = A.sizes[0];
-        float s = 0.f;
-        for (int v = tid; v < n0; v += kBlock) s += A.loss_rows[v];
-        s = wave_sum(s);
-        if ((tid & 63) == 0) sh[0][tid >> 6] = s;
-        __syncthreads();
-        if (tid == 0) {
-            const float nv = A.loss_rows[A.cap0];
-            const float tot = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
-            *A.loss = nv > 0.f ? tot / nv : 0.f;
-        }
+        J.dst[e] = out;
     }
 }
 
-// chain rule of the composed map W_c[t] = W_t^T W_0, b_c[t] = b_t W_0 (one thread per output):
-//   g W_t[o][k] = sum_j W_0[o][j] gW_c[t][k][j];  g b_t[o] = sum_j W_0[o][j] gb_c[t][j];
-//   g W_0[o][j] = sum_t (sum_k W_t[o][k] gW_c[t][k][j] + b_t[o] gb_c[t][j])
+// chain rule of the composed map W_c[t] = W_t^T W_0, b_c[t] = b_t W_0:
+//   blocks [0, 64): g W_0[o][:] = sum_t (sum_k W_t[o][k] gW_c[t][k][:] + b_t[o] gb_c[t][:]),
+//     4 thread groups over (t, k), combined in a fixed order;
+//   blocks [64, 64 + 64 T): g W_t[o][k] = sum_j W_0[o][j] gW_c[t][k][j] (thread k), and
+//     g b_t[o] (thread K)
 struct ChainArgs {
     int T; int K; Ptrs lin_w; Ptrs lin_b; const float* w0; const float* gwc;
     float* g_lin_w[MT]; float* g_lin_b[MT]; float* g_w0;
 };
 
 __global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
-    const int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    __shared__ float red[4][F];
+    __shared__ float w0r[F];
     const int K = A.K;
-    const int64_t per = int64_t(F) * (K + 1);           // g W_t (64 x K) then g b_t (64)
-    if (e < A.T * per) {
-        const int t = int(e / per);
-        const int64_t r = e - t * per;
-        const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
-        if (r < int64_t(F) * K) {
-            const int o = int(r / K), k = int(r % K);
-            float s = 0.f;
-            for (int j = 0; j < F; ++j) s = fmaf(A.w0[o * F + j], gw[int64_t(k) * F + j], s);
-            pick(A.g_lin_w, t)[r] = s;
-        } else {
-            const int o = int(r - int64_t(F) * K);
-            float s = 0.f;
-            for (int j = 0; j < F; ++j) s = fmaf(A.w0[o * F + j], gw[int64_t(K) * F + j], s);
-            pick(A.g_lin_b, t)[o] = s;
+    if (blockIdx.x < F) {
+        const int o = blockIdx.x, j = threadIdx.x & 63, g = threadIdx.x >> 6;
+        float s = 0.f;
+        for (int t = 0; t < A.T; ++t) {
+            const float* W = pick(A.lin_w.p, t) + int64_t(o) * K;
+            const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
+            for (int k = g; k < K; k += 4) s = fmaf(W[k], gw[int64_t(k) * F + j], s);
+            if (g == 0) s = fmaf(pick(A.lin_b.p, t)[o], gw[int64_t(K) * F + j], s);
         }
+        red[g][j] = s;
+        __syncthreads();
+        if (threadIdx.x < F)
+            A.g_w0[o * F + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
         return;
     }
-    const int64_t q = e - A.T * per;
-    if (q >= F * F) return;
-    const int o = int(q / F), j = int(q % F);
+    const int b = blockIdx.x - F;
+    const int t = b / F, o = b - t * F;
+    if (threadIdx.x < F) w0r[threadIdx.x] = A.w0[o * F + threadIdx.x];
+    __syncthreads();
+    const int k = threadIdx.x;
+    if (k > K) return;
+    const float* gw = A.gwc + (int64_t(t) * (K + 1) + k) * F;
     float s = 0.f;
-    for (int t = 0; t < A.T; ++t) {
-        const float* W = pick(A.lin_w.p, t);
-        const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
-        for (int k = 0; k < K; ++k) s = fmaf(W[int64_t(o) * K + k], gw[int64_t(k) * F + j], s);
-        s = fmaf(pick(A.lin_b.p, t)[o], gw[int64_t(K) * F + j], s);
+#pragma unroll 4
+    for (int j = 0; j < F; j += 4) {
+        const float4 g4 = *reinterpret_cast<const float4*>(gw + j);
+        s = fmaf(w0r[j], g4.x, s);
+        s = fmaf(w0r[j + 1], g4.y, s);
+        s = fmaf(w0r[j + 2], g4.z, s);
+        s = fmaf(w0r[j + 3], g4.w, s);
     }
-    A.g_w0[q] = s;
+    if (k < K) pick(A.g_lin_w, t)[int64_t(o) * K + k] = s;
+    else pick(A.g_lin_b, t)[o] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
 struct SlabLayout {
-    int64_t rel[ML], w[ML], proj, total;
+    int64_t rel[ML], post[ML], head, proj, total;
+    int head_blocks;
 };
 
-inline SlabLayout slab_layout(const regnn_nsm_params* p) {
+inline SlabLayout slab_layout(const regnn_nsm_params* p, int cap0) {
     SlabLayout s{};
     int64_t o = 0;
-    for (int l = 0; l < ML; ++l) {
+    for (int l = 0; l < ML; ++l) {        // agg_bwd: relation dots of layer l
         s.rel[l] = o;
         if (l < p->n_layers) o += int64_t(kAggBlocks) * F;
     }
-    for (int l = 0; l < ML; ++l) {        // w[l]: partials of convs[l].weight (l >= 1)
-        s.w[l] = o;
-        if (l >= 1 && l < p->n_layers) o += int64_t(kPostBlocks) * F * F;
+    for (int l = 0; l < ML; ++l) {        // post_bwd of layer l < L-1
+        s.post[l] = o;
+        if (l + 1 < p->n_layers) o += int64_t(kPostBlocks) * kPostW;
     }
+    s.head_blocks = (cap0 + kHeadRows - 1) / kHeadRows;
+    s.head = o;
+    o += int64_t(s.head_blocks) * head_part_width(p->n_classes);
     s.proj = o;
     o += int64_t(p->n_types) * kProjBlocks * (p->k_in + 1) * F;
     s.total = o;
@@ -770,11 +788,27 @@ inline Drop make_drop(float p) {
     return d;
 }
 
-bool set_lds(const void* k, size_t bytes) {
-    if (bytes <= 64 * 1024) return true;
-    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes)) ==
-           hipSuccess;
+// raise a kernel's dynamic-LDS limit to `bytes` once (the largest size asked so far is kept)
+bool set_lds(const void* k, size_t bytes, size_t* done) {
+    if (bytes <= 64 * 1024 || bytes <= *done) return true;
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes)) !=
+        hipSuccess)
+        return false;
+    *done = bytes;
+    return true;
 }
+
+struct JobList {
+    FinArgs A{};
+    int blocks = 0;
+    void add(const float* src, int64_t pstride, int nparts, int width, float* dst, int op = kOpCopy,
+             const float* aux = nullptr) {
+        Job& j = A.job[A.n_jobs++];
+        j.src = src; j.pstride = pstride; j.nparts = nparts; j.width = width; j.dst = dst;
+        j.op = op; j.aux = aux; j.blocks = (width + 31) / 32;
+        blocks += j.blocks;
+    }
+};
 
 }  // namespace nsm
 }  // namespace regnn
@@ -784,9 +818,9 @@ using namespace regnn::nsm;
 
 extern "C" {
 
-int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p) {
-    if (!p) return -1;
-    return slab_layout(p).total;
+int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
+    if (!p || cap0 <= 0) return -1;
+    return slab_layout(p, cap0).total;
 }
 
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
@@ -798,8 +832,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     for (int l = 0; l < L; ++l)
         if (p->n_rel[l] < 1 || p->n_rel[l] > F) return REGNN_EUNSUPPORTED;
     if (!w->state || !w->sizes || !w->n_id || !w->ntype || !w->local || !w->labels || !w->wc ||
-        !w->gwc || !w->tabs || !w->h_last || !w->glogits || !w->loss_rows || !w->slab || !p->loss ||
-        !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b)
+        !w->gwc || !w->tabs || !w->nvalid || !w->row_type || !w->row_off || !w->slab ||
+        !p->loss || !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b || w->cap[0] <= 0)
         return REGNN_EINVAL;
     for (int t = 0; t < T; ++t)
         if (!p->x_tab[t] || !p->lin_w[t] || !p->lin_b[t] || !p->g_lin_w[t] || !p->g_lin_b[t])
@@ -808,13 +842,13 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         const int h = L - 1 - l;
         if (!p->conv_w[l] || !p->conv_b[l] || !p->conv_rw[l] || !p->ln_w[l] || !p->ln_b[l] ||
             !p->g_conv_w[l] || !p->g_conv_b[l] || !p->g_conv_rw[l] || !p->g_ln_w[l] ||
-            !p->g_ln_b[l] || !w->xs[l] || !w->gxs[l] || !w->ga[l] || !w->gy[l] || !w->gyx[l] ||
-            !w->blk_ptr[h] || !w->blk_idx[h] || !w->blk_rel[h] || !w->blk_inv[h] ||
-            w->cap[h] <= 0 || w->cap[h + 1] <= 0)
+            !p->g_ln_b[l] || !w->xs[l] || !w->gxs[l] || !w->ga[l] || !w->blk_ptr[h] ||
+            !w->blk_idx[h] || !w->blk_rel[h] || !w->blk_inv[h] || w->cap[h] <= 0 ||
+            w->cap[h + 1] <= 0)
             return REGNN_EINVAL;
         if (l < L - 1 && (!w->a[l] || !w->stats[l])) return REGNN_EINVAL;
     }
-    const SlabLayout S = slab_layout(p);
+    const SlabLayout S = slab_layout(p, w->cap[0]);
     const Drop drop = make_drop(p->p_drop);
     Ptrs lin_w{}, lin_b{}, xt{}, rw{};
     for (int t = 0; t < T; ++t) {
@@ -833,13 +867,16 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     // 2. projection of the outermost hop's sources (hop L) -> layer 0's rows
     {
         const size_t lds = size_t(T) * ((K + 1) * F + 4) * sizeof(float);
-        static bool ok = set_lds(reinterpret_cast<const void*>(&project_kernel), 160 * 1024);
-        if (!ok || lds > 160 * 1024) return REGNN_EUNSUPPORTED;
+        static size_t done = 0;
+        if (lds > 160 * 1024 ||
+            !set_lds(reinterpret_cast<const void*>(&project_kernel), lds, &done))
+            return REGNN_EUNSUPPORTED;
         const int rows = w->cap[L];
         int grid = (rows + 255) / 256;
         if (grid > 256) grid = 256;
         hipLaunchKernelGGL(project_kernel, dim3(grid), dim3(1024), lds, stream, w->n_id, w->sizes,
-                           L, w->ntype, w->local, T, K, xt, w->wc, w->xs[0], w->gxs[0]);
+                           L, w->ntype, w->local, T, K, xt, w->wc, w->xs[0], w->gxs[0],
+                           w->row_type, w->row_off);
         REGNN_LAUNCH_CHECK();
     }
     // 3. layers 0 .. L-2
@@ -858,6 +895,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         REGNN_LAUNCH_CHECK();
     }
     // 4. last layer + head + loss + backward to its pre-LN rows
+    const int64_t hw = head_part_width(C);
     {
         const int l = L - 1;
         HeadArgs H{};
@@ -866,13 +904,13 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         H.tab = w->tabs + l * F; H.xs = w->xs[l]; H.bias = p->conv_b[l];
         H.ln_w = p->ln_w[l]; H.ln_b = p->ln_b[l]; H.state = w->state; H.layer = l; H.drop = drop;
         H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
-        H.h_last = w->h_last; H.glogits = w->glogits; H.loss_rows = w->loss_rows;
-        H.ga = w->ga[l]; H.gy = w->gy[l]; H.gyx = w->gyx[l]; H.cap0 = w->cap[0];
-        const size_t lds = (size_t(C) * kWPad + kHeadRows * F + size_t(kHeadRows) * C) * sizeof(float);
-        static bool ok = set_lds(reinterpret_cast<const void*>(&head_kernel), 160 * 1024);
-        if (!ok || lds > 150 * 1024) return REGNN_EUNSUPPORTED;
-        const int grid = (w->cap[0] + kHeadRows - 1) / kHeadRows;
-        hipLaunchKernelGGL(head_kernel, dim3(grid), dim3(kHeadRows * 64), lds, stream, H);
+        H.ga = w->ga[l]; H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
+        const size_t lds = (size_t(C) * kWPad + kHeadRows * F + size_t(kHeadRows) * C +
+                            3 * kHeadRows * F) * sizeof(float);
+        static size_t done = 0;
+        if (lds > 150 * 1024 || !set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
+            return REGNN_EUNSUPPORTED;
+        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kHeadRows * 64), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
     // 5. backward, last layer first
@@ -893,7 +931,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         Q.a = w->a[lp]; Q.stats = w->stats[lp]; Q.ln_w = p->ln_w[lp]; Q.ln_b = p->ln_b[lp];
         Q.state = w->state; Q.layer = lp; Q.drop = drop;
         Q.w_next = p->conv_w[l]; Q.gxs_next = w->gxs[l];
-        Q.ga = w->ga[lp]; Q.gy = w->gy[lp]; Q.gyx = w->gyx[lp]; Q.slab = w->slab + S.w[l];
+        Q.ga = w->ga[lp]; Q.slab = w->slab + S.post[lp];
         hipLaunchKernelGGL(post_bwd_kernel, dim3(kPostBlocks), dim3(kBlock), 0, stream, Q);
         REGNN_LAUNCH_CHECK();
     }
@@ -904,8 +942,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         switch (K / 16) {
 #define PB_CASE(KPT_)                                                                        \
     case KPT_:                                                                               \
-        hipLaunchKernelGGL(project_bwd_kernel<KPT_>, grid, dim3(kBlock), 0, stream, w->n_id, \
-                           w->sizes, L, w->ntype, w->local, xt, w->gxs[0], sl);              \
+        hipLaunchKernelGGL(project_bwd_kernel<KPT_>, grid, dim3(kBlock), 0, stream, w->sizes, \
+                           L, w->row_type, w->row_off, xt, w->gxs[0], sl);                   \
         break;
             PB_CASE(4) PB_CASE(8)
 #undef PB_CASE
@@ -913,28 +951,33 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         }
         REGNN_LAUNCH_CHECK();
     }
-    // 7. reductions
+    // 7. reductions of every partial into the gradients (and the composed map's gradient)
     {
-        FinArgs A{};
-        A.sizes = w->sizes; A.L = L; A.C = C; A.T = T; A.K = K; A.alpha = p->alpha;
-        A.glogits = w->glogits; A.h_last = w->h_last; A.g_out_w = p->g_out_w; A.g_out_b = p->g_out_b;
-        for (int l = 0; l < L; ++l) {
-            A.ga[l] = w->ga[l]; A.gy[l] = w->gy[l]; A.gyx[l] = w->gyx[l];
-            A.g_conv_b[l] = p->g_conv_b[l]; A.g_ln_b[l] = p->g_ln_b[l]; A.g_ln_w[l] = p->g_ln_w[l];
-            A.rel_slab[l] = w->slab + S.rel[l]; A.rw[l] = p->conv_rw[l]; A.n_rel[l] = p->n_rel[l];
-            A.g_rw[l] = p->g_conv_rw[l];
-            A.w_slab[l] = w->slab + S.w[l]; A.g_conv_w[l] = p->g_conv_w[l];
+        JobList J;
+        J.A.alpha = p->alpha;
+        const float* hp = w->slab + S.head;
+        const int nh = S.head_blocks;
+        J.add(hp, hw, nh, C * F, p->g_out_w);
+        J.add(hp + int64_t(C) * F, hw, nh, C, p->g_out_b);
+        J.add(hp + int64_t(C) * (F + 1), hw, nh, F, p->g_conv_b[L - 1]);
+        J.add(hp + int64_t(C) * (F + 1) + F, hw, nh, F, p->g_ln_b[L - 1]);
+        J.add(hp + int64_t(C) * (F + 1) + 2 * F, hw, nh, F, p->g_ln_w[L - 1]);
+        J.add(hp + int64_t(C) * (F + 1) + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
+        for (int l = 0; l < L; ++l)
+            J.add(w->slab + S.rel[l], F, kAggBlocks, p->n_rel[l], p->g_conv_rw[l], kOpRel,
+                  p->conv_rw[l]);
+        for (int l = 0; l + 1 < L; ++l) {
+            const float* pp = w->slab + S.post[l];
+            J.add(pp, kPostW, kPostBlocks, F * F, p->g_conv_w[l + 1]);
+            J.add(pp + F * F, kPostW, kPostBlocks, F, p->g_conv_b[l]);
+            J.add(pp + F * F + F, kPostW, kPostBlocks, F, p->g_ln_b[l]);
+            J.add(pp + F * F + 2 * F, kPostW, kPostBlocks, F, p->g_ln_w[l]);
         }
-        A.proj_slab = w->slab + S.proj; A.gwc = w->gwc;
-        A.loss_rows = w->loss_rows; A.cap0 = w->cap[0]; A.loss = p->loss;
-        A.j_out = (C + 15) / 16;
-        A.j_rows = 3 * L;
-        A.j_rel = L;
-        A.j_w = 16 * (L - 1);
-        A.j_wc = int((int64_t(T) * (K + 1) * F + kBlock - 1) / kBlock);
-        A.j_loss = 1;
-        const int grid = A.j_out + A.j_rows + A.j_rel + A.j_w + A.j_wc + A.j_loss;
-        hipLaunchKernelGGL(finalize_kernel, dim3(grid), dim3(kBlock), 0, stream, A);
+        const int64_t pw = int64_t(K + 1) * F;
+        for (int t = 0; t < T; ++t)
+            J.add(w->slab + S.proj + int64_t(t) * kProjBlocks * pw, pw, kProjBlocks, int(pw),
+                  w->gwc + t * pw);
+        hipLaunchKernelGGL(finalize_kernel, dim3(J.blocks), dim3(kBlock), 0, stream, J.A);
         REGNN_LAUNCH_CHECK();
     }
     // 8. chain rule onto lins[t] and convs[0].weight
@@ -946,9 +989,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
             A.g_lin_b[t] = p->g_lin_b[t];
         }
         A.g_w0 = p->g_conv_w[0];
-        const int64_t n = int64_t(T) * F * (K + 1) + F * F;
-        hipLaunchKernelGGL(chain_kernel, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           stream, A);
+        hipLaunchKernelGGL(chain_kernel, dim3(F + T * F), dim3(kBlock), 0, stream, A);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

@@ -189,9 +189,8 @@ class _NsmWork(ctypes.Structure):
                 ("blk_ptr", _P * _ML), ("blk_idx", _P * _ML), ("blk_rel", _P * _ML),
                 ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
-                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("gy", _P * _ML),
-                ("gyx", _P * _ML), ("h_last", _P), ("glogits", _P), ("loss_rows", _P),
-                ("slab", _P)]
+                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("row_type", _P),
+                ("row_off", _P), ("nvalid", _P), ("slab", _P)]
 
 
 def fused_unsupported(model, x_dict):
@@ -289,11 +288,13 @@ class FusedStep:
         for l in range(nl):
             n_src, n_dst = caps[nl - l], caps[nl - 1 - l]
             W.xs[l], W.gxs[l] = ptr(z(n_src, 64)), ptr(z(n_src, 64))
-            W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
-            W.ga[l], W.gy[l], W.gyx[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 64)), ptr(z(n_dst, 64))
-        W.h_last, W.glogits = ptr(z(caps[0], 64)), ptr(z(caps[0], C))
-        W.loss_rows = ptr(z(caps[0] + 1))
-        W.slab = ptr(z(_slab_floats(P)))
+            if l < nl - 1:
+                W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
+            W.ga[l] = ptr(z(n_dst, 64))
+        W.row_type = ptr(torch.zeros(caps[nl], dtype=torch.int32, device=dev))
+        W.row_off = ptr(torch.zeros(caps[nl], dtype=torch.int64, device=dev))
+        W.nvalid = ptr(z(1))
+        W.slab = ptr(z(_slab_floats(P, caps[0])))
         self.model = model
 
     def step(self):
@@ -304,8 +305,8 @@ class FusedStep:
                    torch.cuda.current_stream(self.device).cuda_stream)
 
 
-def _slab_floats(P):
-    n = int(L._so.regnn_nsm_slab_floats(ctypes.addressof(P)))
+def _slab_floats(P, cap0):
+    n = int(L._so.regnn_nsm_slab_floats(ctypes.addressof(P), int(cap0)))
     if n <= 0:
         raise RuntimeError("regnn_nsm_slab_floats rejected the parameters")
     return n
