@@ -94,18 +94,15 @@ def build_ns(args, dev, hidden=64):
     torch.manual_seed(3)
     model = mag.REGNN(128, hidden, 349, 2, 10.0, args.dropout, {k: 128 for k in x_dict}, 7,
                       use_norm="ln", self_loop_type=2).to(dev)
-    try:        # one multi-tensor launch per step (capturable: the step counters stay on device)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True, fused=True)
-    except (RuntimeError, ValueError):
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
     n_paper = gd["counts"]["paper"]
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
     y_global = torch.full((gd["N"], 1), -1, dtype=torch.int64, device=dev)
     y_global[:n_paper, 0] = torch.randint(0, 349, (n_paper,), generator=gen, device=dev)
-    tr = NSTrainer(model, opt, rg, [25, 20], args.batch, torch.arange(n_paper, device=dev),
+    # Adam (mag/regnn_ns.py:495, lr 1e-3) as one flat-bucket launch (regnn_hip.ns.FlatAdam)
+    tr = NSTrainer(model, None, rg, [25, 20], args.batch, torch.arange(n_paper, device=dev),
                    x_dict, edge_type, node_type, local_node_idx, y_global, 7, seed=123,
-                   rank=rank, world=world)
+                   rank=rank, world=world, adam=dict(lr=1e-3))
     torch.cuda.synchronize()
     log(f"[bench] ns: N={gd['N']:,} E={rg.E:,} built in {time.time() - t0:.1f}s; "
         f"{tr.steps_per_epoch()} steps/epoch/rank, capacities {tr.sampler.caps}")

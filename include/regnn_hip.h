@@ -626,6 +626,16 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0);
  * and *loss. 10 kernel launches for L = 2, none of them sized from the host. */
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
 
+/* Adam step over flat buffers (replaces torch.optim.Adam.step, mag/regnn_ns.py:407, for
+ * parameters laid out in one flat bucket): with weight decay wd the gradient is g + wd * p
+ * (torch's L2 form), t = *step + 1, m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
+ * p -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps). *step (int64) and *ticket
+ * (uint32, zero-filled once) live on the device; the launch advances *step itself, so a
+ * captured graph needs no host update. */
+int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    float lr, float beta1, float beta2, float eps, float weight_decay,
+                    int64_t* step, uint32_t* ticket, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -172,14 +172,20 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
     int carry = 0;
     for (int base = 0; base < cap; base += kNsRowsBlock * IT) {
         const int i0 = base + threadIdx.x * IT;
-        int vals[IT];
+        int vals[IT], rels[IT];
         int s = 0;
+        // every global load of the tile first (the n_id -> ntype chain is two round trips for
+        // all IT rows at once, not per row between the stores below)
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             const int i = i0 + j;
-            vals[j] = (i < cap && i < n) ? scnt[i] + 1 : 0;
+            const bool live = i < cap && i < n;
+            vals[j] = live ? scnt[i] + 1 : 0;
+            rels[j] = live ? n_id[i] : 0;
             s += vals[j];
         }
+#pragma unroll
+        for (int j = 0; j < IT; ++j) rels[j] = vals[j] ? ntype[rels[j]] + num_edge_types : 0;
         int total;
         int off = carry + block_exscan<kNsRowsBlock>(s, lds, &total);
 #pragma unroll
@@ -190,7 +196,7 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                 if (i < n) {
                     const int lp = off + vals[j] - 1;      // the self loop closes the row
                     blk_idx[lp] = i;
-                    blk_rel[lp] = uint8_t(ntype[n_id[i]] + num_edge_types);
+                    blk_rel[lp] = uint8_t(rels[j]);
                     blk_pos[lp] = -1;
                     gsrc[lp] = -1;
                     inv[i] = 1.f / float(vals[j]);

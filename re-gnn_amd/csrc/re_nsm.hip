@@ -219,11 +219,30 @@ __global__ void __launch_bounds__(kBlock) agg_kernel(AggArgs A) {
         if (act) {
             float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
             const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-            for (int e = e0; e < e1; ++e) {
-                const float w = tab[A.rel[e]];
-                const float4 x = *reinterpret_cast<const float4*>(A.xs + int64_t(A.idx[e]) * F + 4 * l);
-                s0 = fmaf(w, x.x, s0); s1 = fmaf(w, x.y, s1);
-                s2 = fmaf(w, x.z, s2); s3 = fmaf(w, x.w, s3);
+            const int gl = threadIdx.x & 48;          // first lane of this row's 16-lane group
+            for (int c0 = e0; c0 < e1; c0 += 16) {   // the group loads 16 edges' ids at once
+                const int m = min(16, e1 - c0);
+                const int my_u = l < m ? A.idx[c0 + l] : 0;
+                const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
+                int j = 0;
+                for (; j + 2 <= m; j += 2) {
+                    const int u0 = __shfl(my_u, gl + j, 64), u1 = __shfl(my_u, gl + j + 1, 64);
+                    const float w0 = tab[__shfl(my_r, gl + j, 64)];
+                    const float w1 = tab[__shfl(my_r, gl + j + 1, 64)];
+                    const float4 x0 = *reinterpret_cast<const float4*>(A.xs + int64_t(u0) * F + 4 * l);
+                    const float4 x1 = *reinterpret_cast<const float4*>(A.xs + int64_t(u1) * F + 4 * l);
+                    s0 = fmaf(w0, x0.x, s0); s1 = fmaf(w0, x0.y, s1);
+                    s2 = fmaf(w0, x0.z, s2); s3 = fmaf(w0, x0.w, s3);
+                    s0 = fmaf(w1, x1.x, s0); s1 = fmaf(w1, x1.y, s1);
+                    s2 = fmaf(w1, x1.z, s2); s3 = fmaf(w1, x1.w, s3);
+                }
+                if (j < m) {
+                    const int u0 = __shfl(my_u, gl + j, 64);
+                    const float w0 = tab[__shfl(my_r, gl + j, 64)];
+                    const float4 x0 = *reinterpret_cast<const float4*>(A.xs + int64_t(u0) * F + 4 * l);
+                    s0 = fmaf(w0, x0.x, s0); s1 = fmaf(w0, x0.y, s1);
+                    s2 = fmaf(w0, x0.z, s2); s3 = fmaf(w0, x0.w, s3);
+                }
             }
             const float iv = A.inv[v];
             const float a[4] = {fmaf(iv, s0, bias.x), fmaf(iv, s1, bias.y), fmaf(iv, s2, bias.z),
@@ -333,7 +352,25 @@ __global__ void __launch_bounds__(kHeadRows * 64) head_kernel(HeadArgs A) {
     if (v < n) {                           // wave-uniform
         float s = 0.f;
         const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-        for (int e = e0; e < e1; ++e) s = fmaf(tab[A.rel[e]], A.xs[int64_t(A.idx[e]) * F + f], s);
+        for (int c0 = e0; c0 < e1; c0 += 64) {       // edge ids loaded by the wave at once
+            const int m = min(64, e1 - c0);
+            const int my_u = f < m ? A.idx[c0 + f] : 0;
+            const int my_r = f < m ? int(A.rel[c0 + f]) : 0;
+            int j = 0;
+            for (; j + 4 <= m; j += 4) {
+                float x[4], wt[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    x[q] = A.xs[int64_t(__builtin_amdgcn_readlane(my_u, j + q)) * F + f];
+                    wt[q] = tab[__builtin_amdgcn_readlane(my_r, j + q)];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) s = fmaf(wt[q], x[q], s);
+            }
+            for (; j < m; ++j)
+                s = fmaf(tab[__builtin_amdgcn_readlane(my_r, j)],
+                         A.xs[int64_t(__builtin_amdgcn_readlane(my_u, j)) * F + f], s);
+        }
         const float a = fmaf(A.inv[v], s, A.bias[f]);
         const float mean = wave_sum(a) * (1.f / F);
         const float dlt = a - mean;
@@ -452,11 +489,35 @@ __global__ void __launch_bounds__(kBlock) agg_bwd_kernel(AggBwdArgs A) {
          v += gridDim.x * (kBlock / 64)) {
         const float g = A.inv[v] * A.ga[int64_t(v) * F + f];
         const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-        for (int e = e0; e < e1; ++e) {
-            const int u = A.idx[e];
-            const int r = A.rel[e];
-            unsafeAtomicAdd(A.gxs + int64_t(u) * F + f, tab[r] * g);
-            bins[r * kBlock + threadIdx.x] += g * A.xs[int64_t(u) * F + f];
+        for (int c0 = e0; c0 < e1; c0 += 64) {
+            // the wave loads up to 64 edges' (source, relation) at once; lane-uniform reads
+            // below, so the per-edge row loads do not wait on an index load each
+            const int m = min(64, e1 - c0);
+            const int my_u = f < m ? A.idx[c0 + f] : 0;
+            const int my_r = f < m ? int(A.rel[c0 + f]) : 0;
+            int j = 0;
+            for (; j + 4 <= m; j += 4) {
+                int u[4], r[4];
+                float x[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    u[q] = __builtin_amdgcn_readlane(my_u, j + q);
+                    r[q] = __builtin_amdgcn_readlane(my_r, j + q);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x[q] = A.xs[int64_t(u[q]) * F + f];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    unsafeAtomicAdd(A.gxs + int64_t(u[q]) * F + f, tab[r[q]] * g);
+                    bins[r[q] * kBlock + threadIdx.x] += g * x[q];
+                }
+            }
+            for (; j < m; ++j) {
+                const int u = __builtin_amdgcn_readlane(my_u, j);
+                const int r = __builtin_amdgcn_readlane(my_r, j);
+                unsafeAtomicAdd(A.gxs + int64_t(u) * F + f, tab[r] * g);
+                bins[r * kBlock + threadIdx.x] += g * A.xs[int64_t(u) * F + f];
+            }
         }
     }
     __syncthreads();
@@ -751,6 +812,46 @@ __global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Adam over flat parameter / gradient / moment buffers (torch.optim.Adam's arithmetic, L2 weight
+// decay added to the gradient). The step count lives on the device: every block uses
+// t = step[0] + 1 and the last block to finish stores it (ticket), so a captured graph advances
+// it on every replay.
+__global__ void __launch_bounds__(kBlock)
+adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                 float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                 float wd, int64_t* __restrict__ step, unsigned* __restrict__ ticket) {
+    __shared__ bool last;
+    const int64_t t = step[0] + 1;
+    const double bc1 = 1.0 - pow(double(b1), double(t));
+    const double bc2 = 1.0 - pow(double(b2), double(t));
+    const float step_size = float(double(lr) / bc1);
+    const float bc2_sqrt = float(sqrt(bc2));
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * kBlock) {
+        float gi = g[i];
+        const float pi = p[i];
+        if (wd != 0.f) gi = gi + wd * pi;
+        const float mi = m[i], vi = v[i];
+        const float mn = mi + (1.f - b1) * (gi - mi);                 // exp_avg.lerp_(grad, 1-b1)
+        const float vn = vi * b2 + (1.f - b2) * gi * gi;               // mul_(b2).addcmul_
+        m[i] = mn;
+        v[i] = vn;
+        const float denom = sqrtf(vn) / bc2_sqrt + eps;
+        p[i] = pi - step_size * (mn / denom);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        step[0] = t;
+        ticket[0] = 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 struct SlabLayout {
     int64_t rel[ML], post[ML], head, proj, total;
     int head_blocks;
@@ -992,6 +1093,19 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         hipLaunchKernelGGL(chain_kernel, dim3(F + T * F), dim3(kBlock), 0, stream, A);
         REGNN_LAUNCH_CHECK();
     }
+    return REGNN_OK;
+}
+
+int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    float lr, float beta1, float beta2, float eps, float weight_decay,
+                    int64_t* step, uint32_t* ticket, hipStream_t stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !ticket || n < 0) return REGNN_EINVAL;
+    if (n == 0) return REGNN_OK;
+    int64_t grid = (n + kBlock - 1) / kBlock;
+    if (grid > 1024) grid = 1024;
+    hipLaunchKernelGGL(adam_flat_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, stream, param, grad,
+                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step, ticket);
+    REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
 

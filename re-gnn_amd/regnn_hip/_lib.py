@@ -88,6 +88,7 @@ _SIG = {
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
+    "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
 }
 
 for _name, (_args, _ret) in _SIG.items():

@@ -312,17 +312,40 @@ def _slab_floats(P, cap0):
     return n
 
 
+class FlatAdam:
+    """torch.optim.Adam (mag/regnn_ns.py:495: lr, weight_decay) over one flat parameter bucket
+    and its flat gradient bucket, one launch per step (regnn_adam_flat); the step count stays on
+    the device, so the step can be captured in a HIP graph."""
+
+    def __init__(self, params_flat, grads_flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0):
+        self.p, self.g = params_flat, grads_flat
+        self.m = torch.zeros_like(params_flat)
+        self.v = torch.zeros_like(params_flat)
+        dev = params_flat.device
+        self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), \
+            float(weight_decay)
+
+    def step(self):
+        L.call("regnn_adam_flat", L.ptr(self.p), L.ptr(self.g), L.ptr(self.m), L.ptr(self.v),
+               self.p.numel(), self.lr, float(self.betas[0]), float(self.betas[1]), self.eps,
+               self.weight_decay, L.ptr(self.step_count), L.ptr(self.ticket), L.stream())
+
+
 class NSTrainer:
     """One rank's NS training step (mag/regnn_ns.py:392-420) on the device sampler.
 
     model: mag.REGNN; opt: an optimizer over model.parameters() (Adam(capturable=True) for
-    graph capture); train_idx: target nodes (the paper train split); y_global [N, 1] labels.
+    graph capture), or None for FlatAdam over a flat parameter bucket (`adam`: lr, betas, eps,
+    weight_decay); train_idx: target nodes (the paper train split); y_global [N, 1] labels.
     The gradients live in one flat fp32 bucket (p.grad are views of it): one RCCL all-reduce
     per step for world > 1 (mag.flat_grad_allreduce's exchange), outside the captured graph."""
 
     def __init__(self, model, opt, rg, sizes, batch_size, train_idx, x_dict, edge_type,
                  node_type, local_node_idx, y_global, num_edge_types, seed=0, rank=0, world=1,
-                 shuffle=True, engine="auto"):
+                 shuffle=True, engine="auto", adam=None):
         self.model, self.opt = model, opt
         dev = rg.device
         self.device, self.rank, self.world = dev, int(rank), int(world)
@@ -340,6 +363,15 @@ class NSTrainer:
         for p in self.params:
             p.grad = self.flat[o:o + p.numel()].view_as(p)
             o += p.numel()
+        if opt is None:
+            # the parameters become views of one flat bucket too, and one launch updates them
+            # all (FlatAdam; `adam` = torch.optim.Adam's keyword arguments)
+            self.pflat = torch.cat([p.detach().reshape(-1) for p in self.params]).contiguous()
+            o = 0
+            for p in self.params:
+                p.data = self.pflat[o:o + p.numel()].view_as(p)
+                o += p.numel()
+            self.opt = opt = FlatAdam(self.pflat, self.flat, **(adam or {}))
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in ten HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies

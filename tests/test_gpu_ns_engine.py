@@ -313,11 +313,20 @@ def test_fused_step_matches_module_path(monkeypatch, dropout):
         assert ok, f"{n}: rel err {err:.3e}"
 
 
-def test_fused_step_graph_replay_tracks_eager():
-    """the fused step captured in a HIP graph: losses equal the eager twin's step by step."""
+@pytest.mark.parametrize("flat_adam", [False, True])
+def test_fused_step_graph_replay_tracks_eager(flat_adam):
+    """the fused step captured in a HIP graph: losses equal the eager twin's step by step
+    (torch Adam(capturable) or the one-launch FlatAdam)."""
+    from regnn_hip.ns import NSTrainer
     d = _mag(0.003, seed=7, F=128, hidden=64, classes=11, dropout=0.3)
-    tr_e, _ = _setup_trainer(d, d["model"](4), batch=128, sizes=(10, 5))
-    tr_g, _ = _setup_trainer(d, d["model"](4), batch=128, sizes=(10, 5))
+
+    def make():
+        if not flat_adam:
+            return _setup_trainer(d, d["model"](4), batch=128, sizes=(10, 5))[0]
+        return NSTrainer(d["model"](4), None, d["rg"], [10, 5], 128,
+                         torch.arange(d["n_paper"], device=DEV), d["x_dict"], d["edge_type"],
+                         d["node_type"], d["local"], d["y"], 7, seed=3, adam=dict(lr=1e-2))
+    tr_e, tr_g = make(), make()
     assert tr_e.fused is not None and tr_g.fused is not None
     tr_g.capture(warmup=2)
     for _ in range(2):
@@ -331,3 +340,28 @@ def test_fused_step_graph_replay_tracks_eager():
         lg.append(float(tr_g.loss))
     assert np.all(np.isfinite(lg))
     assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
+
+
+@pytest.mark.parametrize("wd", [0.0, 1e-3])
+def test_flat_adam_matches_torch_adam(wd):
+    """regnn_adam_flat (the NS trainer's one-launch optimizer) against torch.optim.Adam over
+    the same gradients for 4 steps, with and without weight decay."""
+    from regnn_hip.ns import FlatAdam
+    g = torch.Generator(device=DEV).manual_seed(5)
+    shapes = [(64, 128), (64,), (11,), (349, 64)]
+    ref = [torch.randn(s, generator=g, device=DEV).requires_grad_(True) for s in shapes]
+    opt = torch.optim.Adam(ref, lr=1e-2, weight_decay=wd)
+    pflat = torch.cat([p.detach().reshape(-1) for p in ref]).clone()
+    gflat = torch.zeros_like(pflat)
+    fa = FlatAdam(pflat, gflat, lr=1e-2, weight_decay=wd)
+    for _ in range(4):
+        grads = [torch.randn(s, generator=g, device=DEV) for s in shapes]
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        gflat.copy_(torch.cat([gr.reshape(-1) for gr in grads]))
+        opt.step()
+        fa.step()
+    torch.cuda.synchronize()
+    want = torch.cat([p.detach().reshape(-1) for p in ref])
+    assert int(fa.step_count) == 4
+    assert torch.allclose(pflat, want, rtol=1e-6, atol=1e-7), (pflat - want).abs().max()
