@@ -498,7 +498,8 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
  *  g2l, first  uint64 [num_nodes] dedup tables: g2l zero-filled, first all-ones, once.
  *  Per-hop scratch (cap_dst = capacity of the hop's targets, k = fan-out, cap_e = cap_dst*(k+1)):
  *  samp, spos [cap_dst*k] int32; scnt [cap_dst] int32; gsrc [cap_e] int32; flag [cap_e] uint8;
- *  tiles [ceil(cap_e/1024) + 1] int32, zero-filled once.
+ *  tiles [ceil(cap_e/1024) + 1] int32, zero-filled once; status [ceil(cap_dst/1024)] uint64
+ *  (row-offset look-back, zero-filled once).
  *  Block output (mag/regnn_layers.py:90-99 with self_loop_type 2): blk_ptr [cap_dst+1],
  *  blk_idx [cap_e] (local source ids; row i's self loop last), blk_rel [cap_e] uint8 (edge type
  *  etype[csr position], or num_edge_types + ntype[target] for the loop), blk_pos [cap_e] (CSR
@@ -523,9 +524,9 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
-                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, int32_t* blk_ptr,
-                 int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos, float* inv,
-                 hipStream_t stream);
+                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
+                 int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
+                 float* inv, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):

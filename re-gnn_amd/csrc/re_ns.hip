@@ -22,7 +22,6 @@
 namespace regnn {
 
 constexpr int kNsTile = 1024;        // block positions per flag tile (256 threads x 4)
-constexpr int kNsRowsBlock = 1024;   // the single-block row scan
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 30;
@@ -159,59 +158,91 @@ ns_sample_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
     if (lane == 0) scnt[i] = k;
 }
 
-// single block: row offsets (sampled count + the self loop), 1/in-count, the self-loop entries
-template <int IT>
-__global__ void __launch_bounds__(kNsRowsBlock)
+// row offsets (sampled count + the self loop), 1/in-count and the self-loop entries: one tile of
+// kNsRowsTile rows per block, the tiles' exclusive prefix by decoupled look-back (integer sums:
+// exact in any order). status[tile] = stamp << 32 | kind << 30 | value, kind 1 = the tile's own
+// count, 2 = inclusive prefix; entries of another stamp are stale (nothing is reset between
+// steps). A block only waits on lower tiles, which were dispatched before it.
+constexpr int kNsRowsIT = 4;
+constexpr int kNsRowsTile = kBlock * kNsRowsIT;
+
+__device__ __forceinline__ uint64_t lb_pack(uint32_t stamp, uint32_t kind, uint32_t v) {
+    return (uint64_t(stamp) << 32) | (uint64_t(kind) << 30) | uint64_t(v);
+}
+
+__global__ void __launch_bounds__(kBlock)
 ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_id,
                const int32_t* __restrict__ ntype, int num_edge_types, int32_t* __restrict__ sizes,
                int hop, int cap, int64_t* __restrict__ state, int32_t* __restrict__ blk_ptr,
                int32_t* __restrict__ blk_idx, uint8_t* __restrict__ blk_rel,
-               int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv) {
-    __shared__ int lds[kNsRowsBlock / 64 + 1];
+               int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv,
+               uint64_t* __restrict__ status) {
+    __shared__ int lds[kBlock / 64 + 1];
+    __shared__ int s_prefix;
     const int n = sizes[hop];
-    int carry = 0;
-    for (int base = 0; base < cap; base += kNsRowsBlock * IT) {
-        const int i0 = base + threadIdx.x * IT;
-        int vals[IT], rels[IT];
-        int s = 0;
-        // every global load of the tile first (the n_id -> ntype chain is two round trips for
-        // all IT rows at once, not per row between the stores below)
+    const uint32_t stamp = ns_stamp(state, hop);
+    const int tile = blockIdx.x;
+    const int i0 = tile * kNsRowsTile + threadIdx.x * kNsRowsIT;
+    int vals[kNsRowsIT], rels[kNsRowsIT];
+    int s = 0;
 #pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const int i = i0 + j;
-            const bool live = i < cap && i < n;
-            vals[j] = live ? scnt[i] + 1 : 0;
-            rels[j] = live ? n_id[i] : 0;
-            s += vals[j];
-        }
-#pragma unroll
-        for (int j = 0; j < IT; ++j) rels[j] = vals[j] ? ntype[rels[j]] + num_edge_types : 0;
-        int total;
-        int off = carry + block_exscan<kNsRowsBlock>(s, lds, &total);
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const int i = i0 + j;
-            if (i < cap) {
-                blk_ptr[i] = off;
-                if (i < n) {
-                    const int lp = off + vals[j] - 1;      // the self loop closes the row
-                    blk_idx[lp] = i;
-                    blk_rel[lp] = uint8_t(rels[j]);
-                    blk_pos[lp] = -1;
-                    gsrc[lp] = -1;
-                    inv[i] = 1.f / float(vals[j]);
-                } else {
-                    inv[i] = 1.f;
-                }
-            }
-            off += vals[j];
-        }
-        carry += total;
+    for (int j = 0; j < kNsRowsIT; ++j) {
+        const int i = i0 + j;
+        const bool live = i < cap && i < n;
+        vals[j] = live ? scnt[i] + 1 : 0;
+        rels[j] = live ? n_id[i] : 0;
+        s += vals[j];
     }
+#pragma unroll
+    for (int j = 0; j < kNsRowsIT; ++j) rels[j] = vals[j] ? ntype[rels[j]] + num_edge_types : 0;
+    int total;
+    const int ex = block_exscan<kBlock>(s, lds, &total);
     if (threadIdx.x == 0) {
-        blk_ptr[cap] = carry;
-        sizes[8 + hop] = carry;
-        state[5] += carry;
+        int prefix = 0;
+        if (tile == 0) {
+            __hip_atomic_store(status, lb_pack(stamp, 2u, uint32_t(total)), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(status + tile, lb_pack(stamp, 1u, uint32_t(total)),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            for (int p = tile - 1; p >= 0;) {
+                const uint64_t st =
+                    __hip_atomic_load(status + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (uint32_t(st >> 32) != stamp) continue;            // not yet published
+                prefix += int(st & 0x3FFFFFFFu);
+                if (((st >> 30) & 3u) == 2u) break;
+                --p;
+            }
+            __hip_atomic_store(status + tile, lb_pack(stamp, 2u, uint32_t(prefix + total)),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_prefix = prefix;
+    }
+    __syncthreads();
+    int off = s_prefix + ex;
+#pragma unroll
+    for (int j = 0; j < kNsRowsIT; ++j) {
+        const int i = i0 + j;
+        if (i < cap) {
+            blk_ptr[i] = off;
+            if (i < n) {
+                const int lp = off + vals[j] - 1;      // the self loop closes the row
+                blk_idx[lp] = i;
+                blk_rel[lp] = uint8_t(rels[j]);
+                blk_pos[lp] = -1;
+                gsrc[lp] = -1;
+                inv[i] = 1.f / float(vals[j]);
+            } else {
+                inv[i] = 1.f;
+            }
+        }
+        off += vals[j];
+    }
+    if (tile == int(gridDim.x) - 1 && threadIdx.x == 0) {
+        const int E = s_prefix + total;
+        blk_ptr[cap] = E;
+        sizes[8 + hop] = E;
+        state[5] += E;
     }
 }
 
@@ -404,11 +435,11 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
-                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, int32_t* blk_ptr,
-                 int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos, float* inv,
-                 hipStream_t stream) {
+                 int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
+                 int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
+                 float* inv, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
-        !samp || !spos || !scnt || !gsrc || !flag || !tiles || !blk_ptr || !blk_idx ||
+        !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
         return REGNN_EINVAL;
     if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
@@ -418,9 +449,9 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     hipLaunchKernelGGL(ns_sample_kernel, dim3((cap_dst + 3) / 4), dim3(kBlock), 0, stream, ptr,
                        idx, n_id, sizes, hop, cap_dst, k, state, g2l, samp, spos, scnt);
     REGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL((ns_rows_kernel<16>), dim3(1), dim3(kNsRowsBlock), 0, stream, scnt, n_id,
-                       ntype, num_edge_types, sizes, hop, cap_dst, state, blk_ptr, blk_idx,
-                       blk_rel, blk_pos, gsrc, inv);
+    hipLaunchKernelGGL(ns_rows_kernel, dim3((cap_dst + kNsRowsTile - 1) / kNsRowsTile),
+                       dim3(kBlock), 0, stream, scnt, n_id, ntype, num_edge_types, sizes, hop,
+                       cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, gsrc, inv, status);
     REGNN_LAUNCH_CHECK();
     const int64_t slots = int64_t(cap_dst) * k;
     hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),

@@ -101,7 +101,8 @@ class DeviceSampler:
             nt = (ce + 1023) // 1024
             z = lambda n, dt=torch.int32: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
             self.hop_bufs.append(dict(samp=z(cd * k), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
-                                      flag=z(ce, torch.uint8), tiles=z(nt + 1)))
+                                      flag=z(ce, torch.uint8), tiles=z(nt + 1),
+                                      status=z((cd + 1023) // 1024, torch.int64)))
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
                           torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev)
             self.blocks.append(blk)
@@ -120,7 +121,8 @@ class DeviceSampler:
                    L.ptr(self.ntype), self.num_edge_types, k, h, L.ptr(self.state),
                    L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h], L.ptr(self.g2l),
                    L.ptr(self.first), L.ptr(b["samp"]), L.ptr(b["spos"]), L.ptr(b["scnt"]),
-                   L.ptr(b["gsrc"]), L.ptr(b["flag"]), L.ptr(b["tiles"]), L.ptr(blk.csr_ptr),
+                   L.ptr(b["gsrc"]), L.ptr(b["flag"]), L.ptr(b["tiles"]), L.ptr(b["status"]),
+                   L.ptr(blk.csr_ptr),
                    L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos), L.ptr(blk.inv),
                    L.stream())
 
