@@ -31,7 +31,6 @@ constexpr int ML = REGNN_NSM_MAX_LAYERS;
 constexpr int kAggBlocks = 512;        // persistent grids: fixed, so the slab layout is static
 constexpr int kPostBlocks = 256;
 constexpr int kProjBlocks = 128;       // per node type
-constexpr int kProjTile = 64;          // rows per project_bwd tile
 constexpr int kWPad = 65;              // padded row stride of 64-wide matrices in LDS
 constexpr float kLnEps = 1e-5f;
 
@@ -110,7 +109,10 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
             const float* bb = pick(lin_b.p, t);
             for (int o = 0; o < F; ++o) s = fmaf(bb[o], w0[o * F + j], s);
         }
-        wc[int64_t(b) * F + j] = s;
+        // wcT[t]: W_c[t]^T row-major [64][K], then b_c[t] [64] (project_kernel's LDS image)
+        float* o = wc + int64_t(t) * (K + 1) * F;
+        if (k < K) o[int64_t(j) * K + k] = s;
+        else o[int64_t(K) * F + j] = s;
         return;
     }
     const int l = b - T * (K + 1);
@@ -125,64 +127,116 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// project: xs0[i] = x_t[local(n_id[i])] . W_c[t] + b_c[t]; 4 lanes per row, 16 outputs per lane;
-// every type's W_c in LDS (types staggered by 4 banks). Zeroes gxs0's rows for the scatter.
-__global__ void __launch_bounds__(1024)
+// project: xs0[i] = x_t[local(n_id[i])] W_c[t] + b_c[t] on fp32 MFMA (v_mfma_f32_16x16x4_f32:
+// exact fp32 products, the precision of an fmaf chain). A block takes 256-row chunks of the
+// outermost hop's sources (grid-stride), writes their descriptors (type, table row) for
+// project_bwd, and per node type compacts the chunk's rows of that type (wave 0, in order) and
+// runs them in 16-row tiles against W_c[t]^T staged in LDS (row stride K + 8: conflict-free
+// ds_read_b128). Lane (c, q) of a tile: node c, k = k0 + 4q .. +3 per 16-k step; output
+// features 16 kt + 4q .. +3 of node c. Zeroes gxs0's rows for the transposed scatter.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kPjChunk = 256;
+
+__device__ __forceinline__ int compact_rows(const int* types, int t, int* list) {
+    // wave 0: list = chunk positions whose type is t, ascending; returns the count
+    const int lane = threadIdx.x & 63;
+    int cnt = 0;
+#pragma unroll
+    for (int s0 = 0; s0 < kPjChunk; s0 += 64) {
+        const bool mine = types[s0 + lane] == t;
+        const uint64_t bal = __ballot(mine);
+        if (mine) list[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = s0 + lane;
+        cnt += __popcll(bal);
+    }
+    return cnt;
+}
+
+template <int K>
+__global__ void __launch_bounds__(kBlock)
 project_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
-               const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, int T, int K,
-               Ptrs xt, const float* __restrict__ wc, float* __restrict__ xs,
+               const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, int T,
+               Ptrs xt, const float* __restrict__ wct, float* __restrict__ xs,
                float* __restrict__ gxs, int32_t* __restrict__ row_type,
                int64_t* __restrict__ row_off) {
-    extern __shared__ float lw[];
-    const int str = (K + 1) * F + 4;
-    for (int i = threadIdx.x; i < T * (K + 1) * (F / 4); i += blockDim.x) {
-        const int t = i / ((K + 1) * (F / 4)), r = i - t * (K + 1) * (F / 4);
-        reinterpret_cast<float4*>(lw + t * str)[r] =
-            reinterpret_cast<const float4*>(wc + int64_t(t) * (K + 1) * F)[r];
-    }
-    __syncthreads();
+    constexpr int S = K + 8;
+    __shared__ float WT[F * S + F];
+    __shared__ int types[kPjChunk];
+    __shared__ int64_t offs[kPjChunk];
+    __shared__ int list[kPjChunk];
+    __shared__ int s_cnt;
     const int n = sizes[hop];
-    const int q = threadIdx.x & 3;
-    const int rpb = blockDim.x / 4;
-    for (int i = blockIdx.x * rpb + (threadIdx.x >> 2); i < n; i += gridDim.x * rpb) {
-        const int g = n_id[i];
-        const int t = ntype[g];
-        const int64_t lo = local[g];
-        if (q == 0) {                      // row descriptors for project_bwd
-            row_type[i] = t;
-            row_off[i] = lo;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    for (int c0 = blockIdx.x * kPjChunk; c0 < n; c0 += gridDim.x * kPjChunk) {
+        {
+            const int i = threadIdx.x;         // kPjChunk == kBlock: one row per thread
+            const int row = c0 + i;
+            int t = -1;
+            int64_t lo = 0;
+            if (row < n) {
+                const int g = n_id[row];
+                t = ntype[g];
+                lo = local[g];
+                row_type[row] = t;
+                row_off[row] = lo;
+            }
+            types[i] = t;
+            offs[i] = lo;
         }
-        const float* xr = pick(xt.p, t) + lo * int64_t(K);
-        const float* wt = lw + t * str + q * 16;
-        float acc[16];
+        __syncthreads();
+        for (int t = 0; t < T; ++t) {
+            if (threadIdx.x < 64) {
+                const int cnt = compact_rows(types, t, list);
+                if (threadIdx.x == 0) s_cnt = cnt;
+            }
+            const float* src = wct + int64_t(t) * (K + 1) * F;
+            for (int e = threadIdx.x; e < F * K / 4; e += kBlock) {
+                const int j = e / (K / 4), k4 = e - j * (K / 4);
+                *reinterpret_cast<float4*>(WT + j * S + 4 * k4) =
+                    reinterpret_cast<const float4*>(src)[e];
+            }
+            if (threadIdx.x < F) WT[F * S + threadIdx.x] = src[K * F + threadIdx.x];
+            __syncthreads();
+            const int cnt = s_cnt;
+            const float* X = pick(xt.p, t);
+            for (int tile = w; tile * 16 < cnt; tile += kBlock / 64) {
+                const int r = tile * 16 + c;
+                const bool valid = r < cnt;
+                const int li = valid ? list[r] : 0;
+                const float* xr = X + offs[li] * int64_t(K) + 4 * q;
+                float4 xv[K / 16];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const float4 b = *reinterpret_cast<const float4*>(wt + K * F + 4 * m);
-            acc[4 * m] = b.x; acc[4 * m + 1] = b.y; acc[4 * m + 2] = b.z; acc[4 * m + 3] = b.w;
-        }
-        for (int k0 = 0; k0 < K; k0 += 4) {
-            const float4 xv = *reinterpret_cast<const float4*>(xr + k0);
-            const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+                for (int s = 0; s < K / 16; ++s)
+                    xv[s] = valid ? *reinterpret_cast<const float4*>(xr + 16 * s)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                f32x4 acc[4];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const float* wr = wt + (k0 + kk) * F;
+                for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float4 w = *reinterpret_cast<const float4*>(wr + 4 * m);
-                    acc[4 * m] = fmaf(xk[kk], w.x, acc[4 * m]);
-                    acc[4 * m + 1] = fmaf(xk[kk], w.y, acc[4 * m + 1]);
-                    acc[4 * m + 2] = fmaf(xk[kk], w.z, acc[4 * m + 2]);
-                    acc[4 * m + 3] = fmaf(xk[kk], w.w, acc[4 * m + 3]);
+                    for (int i = 0; i < 4; ++i) acc[kt][i] = WT[F * S + 16 * kt + 4 * q + i];
+#pragma unroll
+                for (int s = 0; s < K / 16; ++s) {
+                    const float xs4[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
+#pragma unroll
+                    for (int kt = 0; kt < 4; ++kt) {
+                        const float4 a = *reinterpret_cast<const float4*>(WT + (16 * kt + c) * S + 16 * s + 4 * q);
+                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, xs4[0], acc[kt], 0, 0, 0);
+                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, xs4[1], acc[kt], 0, 0, 0);
+                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, xs4[2], acc[kt], 0, 0, 0);
+                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, xs4[3], acc[kt], 0, 0, 0);
+                    }
+                }
+                if (valid) {
+                    const int64_t row = c0 + li;
+#pragma unroll
+                    for (int kt = 0; kt < 4; ++kt) {
+                        *reinterpret_cast<float4*>(xs + row * F + 16 * kt + 4 * q) =
+                            make_float4(acc[kt][0], acc[kt][1], acc[kt][2], acc[kt][3]);
+                        *reinterpret_cast<float4*>(gxs + row * F + 16 * kt + 4 * q) =
+                            make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
             }
-        }
-        float* o = xs + int64_t(i) * F + q * 16;
-        float* z = gxs + int64_t(i) * F + q * 16;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            *reinterpret_cast<float4*>(o + 4 * m) =
-                make_float4(acc[4 * m], acc[4 * m + 1], acc[4 * m + 2], acc[4 * m + 3]);
-            *reinterpret_cast<float4*>(z + 4 * m) = make_float4(0.f, 0.f, 0.f, 0.f);
+            __syncthreads();
         }
     }
 }
@@ -614,92 +668,107 @@ __global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// project_bwd: block (b, t) accumulates sum over rows i of type t of x_i^T g_i (K x 64) and
-// sum g_i (64) over its grid-stride share of 64-row tiles, reading the row descriptors the
-// forward wrote (type, row of the type's table); wave 0 compacts a tile's rows of type t and
-// already loads the next tile's descriptors. Thread: k = kq*KPT .. +KPT-1 (16 k groups),
-// j = 4*j4 .. +3 (16 j groups). Slab row: [K*64 | 64].
-template <int KPT>
+// project_bwd: block (b, t) accumulates gW_c[t] = sum over rows i of type t of x_i^T g_i (K x 64)
+// and gb_c[t] = sum g_i over its grid-stride share of 256-row chunks, on fp32 MFMA: D[k][j] with
+// A[k][row] = x[row][k], B[row][j] = g[row][j], 4 rows per instruction. Wave w owns k blocks
+// KB*w .. +KB-1 and all 4 j blocks. 16-row tiles staged in LDS; the next tile's rows are loaded
+// into registers before the current one is computed. Slab row: [K*64 | 64].
+template <int K>
 __global__ void __launch_bounds__(kBlock)
 project_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ row_type,
                    const int64_t* __restrict__ row_off, Ptrs xt, const float* __restrict__ gxs,
                    float* __restrict__ slab) {
-    constexpr int K = KPT * 16;
-    constexpr int XS = K + 4, GS = F + 4;
-    __shared__ float xsh[kProjTile * XS];
-    __shared__ float gsh[kProjTile * GS];
-    __shared__ int rows[kProjTile];
-    __shared__ int64_t offs[kProjTile];
+    constexpr int XS = K + 16, GS = F + 16;   // ds_read_b32 rows 16 banks apart
+    constexpr int KB = K / 64;                // k blocks per wave
+    constexpr int XV = K / 4 * 16 / kBlock;   // x float4 per thread per tile (K=128: 2, 64: 1)
+    __shared__ float xsh[16 * XS];
+    __shared__ float gsh[16 * GS];
+    __shared__ int types[kPjChunk];
+    __shared__ int list[kPjChunk];
+    __shared__ int64_t offs[kPjChunk];
     __shared__ int s_cnt;
     const int t = blockIdx.y;
     const float* X = pick(xt.p, t);
     const int n = sizes[hop];
-    const int kq = threadIdx.x >> 4, j4 = threadIdx.x & 15;
-    float acc[KPT][4];
-    float accb[4] = {0.f, 0.f, 0.f, 0.f};
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    f32x4 acc[KB][4];
 #pragma unroll
-    for (int a = 0; a < KPT; ++a) acc[a][0] = acc[a][1] = acc[a][2] = acc[a][3] = 0.f;
-    const int stride = gridDim.x * kProjTile;
-    int rt = -1;
-    int64_t ro = 0;
-    if (threadIdx.x < 64) {
-        const int i = blockIdx.x * kProjTile + threadIdx.x;
-        if (i < n) { rt = row_type[i]; ro = row_off[i]; }
-    }
-    for (int base = blockIdx.x * kProjTile; base < n; base += stride) {
-        if (threadIdx.x < 64) {            // wave 0 compacts the tile's rows of type t
-            const bool mine = rt == t;
-            const uint64_t bal = __ballot(mine);
-            const int pos = __popcll(bal & ((1ull << threadIdx.x) - 1ull));
-            if (mine) {
-                rows[pos] = base + threadIdx.x;
-                offs[pos] = ro;
-            }
-            if (threadIdx.x == 0) s_cnt = __popcll(bal);
-            const int i = base + stride + threadIdx.x;          // next tile's descriptors
-            rt = -1;
-            if (i < n) { rt = row_type[i]; ro = row_off[i]; }
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    // tile loader mapping: x: float4 e = threadIdx.x + kBlock * v -> row e / (K/4), k4 e % (K/4);
+    // g: float4 threadIdx.x -> row threadIdx.x / 16, j4 threadIdx.x % 16
+    for (int c0 = blockIdx.x * kPjChunk; c0 < n; c0 += gridDim.x * kPjChunk) {
+        {
+            const int row = c0 + threadIdx.x;
+            types[threadIdx.x] = row < n ? row_type[row] : -1;
+            offs[threadIdx.x] = row < n ? row_off[row] : 0;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int cnt = compact_rows(types, t, list);
+            if (threadIdx.x == 0) s_cnt = cnt;
         }
         __syncthreads();
         const int cnt = s_cnt;
-        for (int q = threadIdx.x; q < cnt * (K / 4); q += kBlock) {
-            const int r = q / (K / 4), c = q - r * (K / 4);
-            *reinterpret_cast<float4*>(xsh + r * XS + 4 * c) =
-                *reinterpret_cast<const float4*>(X + offs[r] * int64_t(K) + 4 * c);
-        }
-        for (int q = threadIdx.x; q < cnt * (F / 4); q += kBlock) {
-            const int r = q / (F / 4), c = q - r * (F / 4);
-            *reinterpret_cast<float4*>(gsh + r * GS + 4 * c) =
-                *reinterpret_cast<const float4*>(gxs + int64_t(rows[r]) * F + 4 * c);
-        }
-        __syncthreads();
-        for (int r = 0; r < cnt; ++r) {
-            const float4 g = *reinterpret_cast<const float4*>(gsh + r * GS + 4 * j4);
-            if (kq == 0) {
-                accb[0] += g.x; accb[1] += g.y; accb[2] += g.z; accb[3] += g.w;
+        float4 xr[XV], gr;
+        auto load = [&](int tile) {
+#pragma unroll
+            for (int v = 0; v < XV; ++v) {
+                const int e = threadIdx.x + kBlock * v;
+                const int r = e / (K / 4), k4 = e - r * (K / 4);
+                const int li = tile * 16 + r;
+                xr[v] = li < cnt ? *reinterpret_cast<const float4*>(
+                                        X + offs[list[li]] * int64_t(K) + 4 * k4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            const int r = threadIdx.x >> 4, j4 = threadIdx.x & 15;
+            const int li = tile * 16 + r;
+            gr = li < cnt ? *reinterpret_cast<const float4*>(gxs + int64_t(c0 + list[li]) * F + 4 * j4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        if (cnt > 0) load(0);
+        for (int tile = 0; tile * 16 < cnt; ++tile) {
+#pragma unroll
+            for (int v = 0; v < XV; ++v) {
+                const int e = threadIdx.x + kBlock * v;
+                const int r = e / (K / 4), k4 = e - r * (K / 4);
+                *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[v];
+            }
+            *reinterpret_cast<float4*>(gsh + (threadIdx.x >> 4) * GS + 4 * (threadIdx.x & 15)) = gr;
+            __syncthreads();
+            if ((tile + 1) * 16 < cnt) load(tile + 1);
+            if (threadIdx.x < F) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) bsum += gsh[r * GS + threadIdx.x];
             }
 #pragma unroll
-            for (int a = 0; a < KPT; a += 4) {
-                const float4 x = *reinterpret_cast<const float4*>(xsh + r * XS + kq * KPT + a);
-                const float xv[4] = {x.x, x.y, x.z, x.w};
+            for (int st = 0; st < 4; ++st) {
+                const int r = 4 * st + q;
+                float bv[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc[a + u][0] = fmaf(xv[u], g.x, acc[a + u][0]);
-                    acc[a + u][1] = fmaf(xv[u], g.y, acc[a + u][1]);
-                    acc[a + u][2] = fmaf(xv[u], g.z, acc[a + u][2]);
-                    acc[a + u][3] = fmaf(xv[u], g.w, acc[a + u][3]);
+                for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+#pragma unroll
+                for (int a = 0; a < KB; ++a) {
+                    const float av = xsh[r * XS + 16 * (KB * w + a) + c];
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb)
+                        acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
     float* o = slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
 #pragma unroll
-    for (int a = 0; a < KPT; ++a)
-        *reinterpret_cast<float4*>(o + (kq * KPT + a) * F + 4 * j4) =
-            make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
-    if (kq == 0)
-        *reinterpret_cast<float4*>(o + K * F + 4 * j4) = make_float4(accb[0], accb[1], accb[2], accb[3]);
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                o[(16 * (KB * w + a) + 4 * q + i) * F + 16 * jb + c] = acc[a][jb][i];
+    if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -967,17 +1036,16 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     REGNN_LAUNCH_CHECK();
     // 2. projection of the outermost hop's sources (hop L) -> layer 0's rows
     {
-        const size_t lds = size_t(T) * ((K + 1) * F + 4) * sizeof(float);
-        static size_t done = 0;
-        if (lds > 160 * 1024 ||
-            !set_lds(reinterpret_cast<const void*>(&project_kernel), lds, &done))
-            return REGNN_EUNSUPPORTED;
-        const int rows = w->cap[L];
-        int grid = (rows + 255) / 256;
-        if (grid > 256) grid = 256;
-        hipLaunchKernelGGL(project_kernel, dim3(grid), dim3(1024), lds, stream, w->n_id, w->sizes,
-                           L, w->ntype, w->local, T, K, xt, w->wc, w->xs[0], w->gxs[0],
-                           w->row_type, w->row_off);
+        int grid = (w->cap[L] + kPjChunk - 1) / kPjChunk;
+        if (grid > 1024) grid = 1024;
+        if (K == 128)
+            hipLaunchKernelGGL(project_kernel<128>, dim3(grid), dim3(kBlock), 0, stream, w->n_id,
+                               w->sizes, L, w->ntype, w->local, T, xt, w->wc, w->xs[0],
+                               w->gxs[0], w->row_type, w->row_off);
+        else
+            hipLaunchKernelGGL(project_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, w->n_id,
+                               w->sizes, L, w->ntype, w->local, T, xt, w->wc, w->xs[0],
+                               w->gxs[0], w->row_type, w->row_off);
         REGNN_LAUNCH_CHECK();
     }
     // 3. layers 0 .. L-2
@@ -1040,16 +1108,12 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     {
         const dim3 grid(kProjBlocks, T);
         float* sl = w->slab + S.proj;
-        switch (K / 16) {
-#define PB_CASE(KPT_)                                                                        \
-    case KPT_:                                                                               \
-        hipLaunchKernelGGL(project_bwd_kernel<KPT_>, grid, dim3(kBlock), 0, stream, w->sizes, \
-                           L, w->row_type, w->row_off, xt, w->gxs[0], sl);                   \
-        break;
-            PB_CASE(4) PB_CASE(8)
-#undef PB_CASE
-            default: return REGNN_EUNSUPPORTED;
-        }
+        if (K == 128)
+            hipLaunchKernelGGL(project_bwd_kernel<128>, grid, dim3(kBlock), 0, stream, w->sizes,
+                               L, w->row_type, w->row_off, xt, w->gxs[0], sl);
+        else
+            hipLaunchKernelGGL(project_bwd_kernel<64>, grid, dim3(kBlock), 0, stream, w->sizes,
+                               L, w->row_type, w->row_off, xt, w->gxs[0], sl);
         REGNN_LAUNCH_CHECK();
     }
     // 7. reductions of every partial into the gradients (and the composed map's gradient)
