@@ -109,6 +109,29 @@ def build_ns(args, dev, hidden=64):
     return tr, dict(N=gd["N"], E=rg.E, n_train=n_paper)
 
 
+def ns_step_bytes(sz, K, C, L=2, F=64):
+    """algorithmic HBM bytes of one fused NS model step (regnn_nsm_step) at the sampled sizes
+    sz (regnn_ns_hop sizes: sz[h] = rows after h hops, sz[8 + h] = edges of hop h's block,
+    self loops included): every row / index / feature byte a kernel must read or write once.
+      project      n_L x (K*4 gathered input row + 2*F*4 xs write + gxs zero + 28 index bytes)
+      agg l < L-1  E x (F*4 gathered row + 5) + n_dst x (4*F*4 + 20: a, xs_next, gxs_next, ga)
+      head         E0 x (F*4 + 5) + n0 x (F*4 ga + 24); out_lin in
+      agg_bwd l    E x (F*4 row read + F*4 atomic add + 5) + n_dst x (F*4 + 12)
+      post_bwd l   n_dst x (3*F*4 + 8)
+      project_bwd  n_L x (K*4 + F*4 + 12)"""
+    f = 4 * F
+    b = sz[L] * (4 * K + 2 * f + 28)                                   # project
+    for l in range(L - 1):                                             # agg / agg_bwd / post
+        h = L - 1 - l
+        b += sz[8 + h] * (f + 5) + sz[h] * (4 * f + 20)
+        b += sz[8 + h] * (2 * f + 5) + sz[h] * (f + 12)
+        b += sz[h] * (3 * f + 8)
+    b += sz[8] * (f + 5) + sz[0] * (f + 24) + 4 * C * F                # head (layer L-1)
+    b += sz[8] * (2 * f + 5) + sz[0] * (f + 12)                         # its agg_bwd
+    b += sz[L] * (4 * K + f + 12)                                      # project_bwd
+    return b
+
+
 def run_ns(args, dev):
     from regnn_hip import profile
     rank, world = _world()
@@ -117,8 +140,11 @@ def run_ns(args, dev):
     for _ in range(max(1, args.warmup)):
         tr.step()
     profile.enable(True)
+    nsm_bytes = []
     for _ in range(5):
         tr.step()
+        if tr.fused is not None:
+            nsm_bytes.append(ns_step_bytes(tr.sampler.sizes.cpu().tolist(), 128, 349))
     torch.cuda.synchronize()
     kstats = profile.summary()
     profile.enable(False)
@@ -180,6 +206,16 @@ def run_ns(args, dev):
         "ns_kernels_ms": {k: round(v[1], 4) for k, v in kstats.items()},
     }
     res["config"]["engine"] = "fused regnn_nsm_step" if tr.fused is not None else "module"
+    if "nsm_step" in kstats and nsm_bytes:
+        # the fused model step (ten launches): algorithmic bytes of its reads and writes at the
+        # profiled steps' sampled sizes (ns_step_bytes) / its device time
+        launches, mean_ms, total_ms, _ = kstats["nsm_step"]
+        b = statistics.mean(nsm_bytes)
+        ach = b / (mean_ms / 1e3) / 1e9
+        res["ns_roofline"] = {"bound": "hbm", "kernel": "regnn_nsm_step (10 launches)",
+                              "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": ach / HBM_PEAK_GBS, "launch_ms": mean_ms,
+                              "algorithmic_bytes_per_launch": b}
     cand = {k: v for k, v in kstats.items() if k in ("ns_spmm_fwd", "ns_spmm_bwd")}
     if cand:
         dom = max(cand, key=lambda k: cand[k][2])
@@ -273,7 +309,7 @@ def pmc_traffic(wl, dtype, rg, op):
     """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary
     (tools/gpu_pmc2.sh: FETCH_SIZE / WRITE_SIZE in separate passes, copy-calibrated), or
     (None, reason) when it was measured on another graph, dtype or kernel code."""
-    from regnn_hip.build import source_hash
+    from regnn_hip.build import kernel_hash
     path = os.path.join(ROOT, "profiles", f"pmc_{wl}_{dtype}.json")
     if not os.path.exists(path):
         return None, "no PMC summary committed"
@@ -281,7 +317,7 @@ def pmc_traffic(wl, dtype, rg, op):
         rec = json.load(f)
     if rec.get("graph") != {"N": rg.n_dst, "E": rg.E} or rec.get("dtype") != dtype:
         return None, "PMC summary is for another graph / dtype"
-    if rec.get("code_hash") != source_hash():
+    if rec.get("code_hash") != kernel_hash():
         return None, "PMC summary is for other kernel code (stale: re-run tools/gpu_pmc2.sh)"
     if op not in rec:
         return None, f"PMC summary has no {op}"

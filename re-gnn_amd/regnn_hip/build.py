@@ -50,6 +50,22 @@ def source_hash():
     return h.hexdigest()
 
 
+# the kernels the committed rocprofv3 counter summaries measure (bench.py pmc_traffic): their
+# sources alone key the summaries, so a change elsewhere (e.g. the NS engine) keeps them valid
+PMC_SOURCES = ("re_spmm.hip", "re_dense.hip", "regnn_common.h")
+
+
+def kernel_hash(names=PMC_SOURCES):
+    """SHA-256 over the named csrc/ files and the compiler flags."""
+    h = hashlib.sha256()
+    for name in names:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode())
+            h.update(f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()
+
+
 def header_abi():
     with open(os.path.join(INCLUDE, "regnn_hip.h")) as f:
         m = re.search(r"ABI version \(.*?currently (\d+)\)", f.read(), re.S)

@@ -89,8 +89,8 @@ def main():
     res["dtype"] = dtype
     # the kernel code the counters were collected on (bench.py refuses a stale summary)
     sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/re-gnn_amd")
-    from regnn_hip.build import source_hash
-    res["code_hash"] = source_hash()
+    from regnn_hip.build import kernel_hash
+    res["code_hash"] = kernel_hash()
     json.dump(res, open(out_json, "w"), indent=1)
     print(json.dumps({k: v.get("bytes_per_launch") if isinstance(v, dict) and "fetch_scale" in v
                       else v for k, v in res.items()}, indent=1))
