@@ -29,6 +29,13 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE,
          "-Wno-unused-result"]
 
 
+def _flags_key():
+    """the compiler flags with the include path made repo-relative: a hash of them is the same
+    in every checkout (here and on the GPU box)."""
+    root = os.path.dirname(PKG)
+    return " ".join(os.path.relpath(f, root) if os.path.isabs(f) else f for f in FLAGS)
+
+
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
@@ -46,7 +53,7 @@ def source_hash():
         h.update(os.path.relpath(p, os.path.dirname(PKG)).encode())
         with open(p, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(FLAGS).encode())
+    h.update(_flags_key().encode())
     return h.hexdigest()
 
 
@@ -62,7 +69,7 @@ def kernel_hash(names=PMC_SOURCES):
         with open(os.path.join(CSRC, name), "rb") as f:
             h.update(name.encode())
             h.update(f.read())
-    h.update(" ".join(FLAGS).encode())
+    h.update(_flags_key().encode())
     return h.hexdigest()
 
 
