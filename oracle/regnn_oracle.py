@@ -16,6 +16,7 @@ explicit hand-derived backward (VJP) of each layer on the hot path, following th
 * ``MagREGCNConvOracle``  — mag/regnn_layers.py:80-150 (self_loop_type 2, aggr='mean')
 * ``MagREGATConvOracle``  — mag/regnn_layers.py:153-436 (REGATConv / REGATv2Conv, global max)
 * model wiring            — model/REGCN.py:35-46, model/REGAT.py:54-66, model/REMixHop.py:87-100
+* ``mag_regnn_model``      — mag/regnn_ns.py:216-346 + nll_loss (:404), feats_type 3 and 2
 
 Pinning: every class here is checked against golden vectors produced by running the REFERENCE's own
 layer/model source (tests/golden/make_golden.py, on a test-only DGL/PyG shim) — see
@@ -829,6 +830,76 @@ def remixhop_model(g, feats, rel, P, num_layers, hidden, alpha, gout, p=(0, 1, 2
             grads[f"layers.{l}.{k}"] = v
     _input_proj_vjp(lins, feats, gh, grads)
     return logits, h, grads
+
+
+# ------------------------------------------------------------------------------------------
+# mag REGNN (mag/regnn_ns.py:216-346) + nll_loss (:404), eval mode, on a sampled batch
+# ------------------------------------------------------------------------------------------
+def mag_regnn_model(x_dict, node_type, local, n_id, adjs, edge_type, P, y, feats_type=3,
+                    num_edge_types=7, alpha=10.0, target_node_type=0):
+    """forward + VJP of the reference REGNN for model 'regcn', self_loop_type 2, LayerNorm.
+    adjs: [(src_local, dst_local, e_id, (n_src, n_dst))] outermost hop first (PyG order).
+    Returns (log-probabilities, mean nll loss, {parameter name: gradient})."""
+    nid = np.asarray(n_id)
+    nt, loc = np.asarray(node_type)[nid], np.asarray(local)[nid]
+    grads = {}
+    if feats_type == 2:                                              # regnn_ns.py:306-315
+        t = np.zeros((nid.size, P["lin.weight"].shape[1]))
+        for key, x in x_dict.items():
+            m = nt == key
+            t[m] = x[loc[m]]
+        for key in {int(k.split(".")[1]) for k in P if k.startswith("emb_dict.")}:
+            m = nt == key
+            t[m] = P[f"emb_dict.{key}"][loc[m]]
+        lin = Linear(P["lin.weight"], P["lin.bias"])
+        h = lin.forward(t)
+    else:                                                            # regnn_ns.py:316-324
+        h = np.zeros((nid.size, P["lins.0.weight"].shape[0]))
+        lins = {}
+        for key, x in x_dict.items():
+            m = nt == key
+            lins[key] = Linear(P[f"lins.{key}.weight"], P[f"lins.{key}.bias"])
+            h[m] = lins[key].forward(x[loc[m]])
+    et = np.asarray(edge_type)
+    caches, x, ntype = [], h, nt
+    for i, (s_, d_, e_, size) in enumerate(adjs):                    # regnn_ns.py:335-343
+        ntype = ntype[:size[1]]
+        pc = {k[len(f"convs.{i}."):]: v for k, v in P.items() if k.startswith(f"convs.{i}.")}
+        o = MagREGCNConvOracle(size[1], num_edge_types, alpha, residual=False, use_norm="ln")
+        yv = o.forward(x, np.asarray(s_), np.asarray(d_), et[np.asarray(e_)], ntype, pc)
+        caches.append((o, yv))
+        x = np.maximum(yv, 0)
+    out_lin = Linear(P["out_lin.weight"], P["out_lin.bias"])
+    z = out_lin.forward(x)
+    zmax = z.max(1, keepdims=True)
+    logp = z - (zmax + np.log(np.exp(z - zmax).sum(1, keepdims=True)))
+    yb = np.asarray(y)
+    n = yb.size
+    loss = -logp[np.arange(n), yb].mean()
+    g = np.zeros_like(logp)
+    g[np.arange(n), yb] = -1.0 / n                                   # nll_loss mean
+    gz = g - np.exp(logp) * g.sum(1, keepdims=True)                  # log_softmax VJP
+    gx, gr = out_lin.backward(gz)
+    grads["out_lin.weight"], grads["out_lin.bias"] = gr["weight"], gr["bias"]
+    for i in range(len(caches) - 1, -1, -1):
+        o, yv = caches[i]
+        gx, grc = o.backward(gx * (yv > 0))
+        for k, v in grc.items():
+            grads[f"convs.{i}.{k}"] = v
+    if feats_type == 2:
+        gt, gr = lin.backward(gx)
+        grads["lin.weight"], grads["lin.bias"] = gr["weight"], gr["bias"]
+        for key in {int(k.split(".")[1]) for k in P if k.startswith("emb_dict.")}:
+            m = nt == key
+            ge = np.zeros_like(P[f"emb_dict.{key}"])
+            np.add.at(ge, loc[m], gt[m])
+            grads[f"emb_dict.{key}"] = ge
+    else:
+        for key, l_ in lins.items():
+            m = nt == key
+            _, gr = l_.backward(gx[m])
+            grads[f"lins.{key}.weight"], grads[f"lins.{key}.bias"] = gr["weight"], gr["bias"]
+    return logp, loss, grads
 
 
 # ------------------------------------------------------------------------------------------

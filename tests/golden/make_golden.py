@@ -425,9 +425,101 @@ def gen_mag_gat():
                   residual=residual, use_norm="ln", self_loop_type=2, negative_slope=0.2), st)
 
 
+# ------------------------------------------------------------------------------------------
+# the REGNN model of mag/regnn_ns.py:216-346 (group_input feats_type 3 / 2, 2 x REGCNConv, relu,
+# out_lin, log_softmax) + nll_loss (:404) on a sampled batch of a small typed graph
+# ------------------------------------------------------------------------------------------
+def _reference_regnn_class(args, num_nodes_dict, target_node_type, regnn_layers):
+    """The reference's `class REGNN` is defined in the training script, whose top level parses
+    argv and downloads ogbn-mag: compile ONLY that class definition (ast) against the globals it
+    reads (args, num_nodes_dict, target_node_type, the layers)."""
+    import ast
+    from types import SimpleNamespace  # noqa: F401
+    path = os.path.join(REF, "mag", "regnn_ns.py")
+    tree = ast.parse(open(path).read(), path)
+    cls = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "REGNN"]
+    assert len(cls) == 1
+    code = compile(ast.Module(body=cls, type_ignores=[]), path, "exec")
+    from torch.nn import Linear, ModuleDict, ModuleList, Parameter, ParameterDict
+    ns = dict(torch=torch, F=torch.nn.functional, Linear=Linear, ModuleDict=ModuleDict,
+              ModuleList=ModuleList, Parameter=Parameter, ParameterDict=ParameterDict,
+              REGCNConv=regnn_layers.REGCNConv, REGATConv=regnn_layers.REGATConv,
+              REGATv2Conv=regnn_layers.REGATv2Conv, args=args, num_nodes_dict=num_nodes_dict,
+              target_node_type=target_node_type)
+    exec(code, ns)
+    return ns["REGNN"]
+
+
+def gen_regnn():
+    from types import SimpleNamespace
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import sampler_oracle as SO
+    rng = np.random.default_rng(50)
+    counts = [40, 50, 8, 12]                       # paper (target), author, institution, field
+    N = sum(counts)
+    ntype = np.repeat(np.arange(4), counts)
+    local = np.concatenate([np.arange(c) for c in counts])
+    E = 900
+    src = rng.integers(0, N, E)
+    dst = rng.integers(0, N, E)
+    dst[:40] = rng.integers(0, 3, 40)              # a few hub targets (rows longer than the fan-out)
+    order = np.argsort(dst, kind="stable")         # edge ids = CSR positions of the dst-major CSR
+    src, dst = src[order].astype(np.int64), dst[order].astype(np.int64)
+    edge_type = rng.integers(0, 7, E).astype(np.int64)
+    ptr = np.zeros(N + 1, np.int64)
+    np.add.at(ptr, dst + 1, 1)
+    ptr = np.cumsum(ptr)
+    batch = rng.choice(counts[0], 12, replace=False).astype(np.int64)
+    sizes, seed, epoch, batch_idx = [4, 3], 7, 1, 2
+    _, n_id, adjs = SO.neighbor_sample(ptr, src, batch.tolist(), sizes, seed, epoch, batch_idx)
+    K, H, C = 64, 64, 5
+    y = rng.integers(0, C, counts[0]).astype(np.int64)
+    for feats_type in (3, 2):
+        args = SimpleNamespace(model="regcn", feats_type=feats_type, self_loop_type=2,
+                               no_re=False)
+        num_nodes_dict = {t: counts[t] for t in range(4)}
+        REGNN = _reference_regnn_class(args, num_nodes_dict, 0, regnn_layers)
+        torch.manual_seed(11)
+        nfd = {t: K for t in range(4)}
+        model = REGNN(K, H, C, 1, 2, 10.0, 0.0, nfd, 7, False, False, use_norm="ln")
+        _set_params(model, rng, ew_alpha=10.0)
+        model.eval()
+        if feats_type == 3:
+            x_dict = {t: torch.from_numpy(f32(rng, counts[t], K).astype(np.float64))
+                      for t in range(4)}
+        else:
+            x_dict = {0: torch.from_numpy(f32(rng, counts[0], K).astype(np.float64))}
+        t_adjs = [(torch.tensor([s_, d_], dtype=torch.int64), torch.tensor(e_, dtype=torch.int64),
+                   sz) for s_, d_, e_, sz in adjs]
+        out = model(torch.tensor(n_id), x_dict, t_adjs, torch.from_numpy(edge_type),
+                    torch.from_numpy(ntype), torch.from_numpy(local))
+        yb = torch.from_numpy(y[batch])
+        loss = torch.nn.functional.nll_loss(out, yb)
+        loss.backward()
+        st = dict(src=src, dst=dst, edge_type=edge_type, ntype=ntype, local=local, y=y,
+                  batch=batch, n_id=np.asarray(n_id, np.int64), logp=out, loss=loss.detach())
+        for t, x in x_dict.items():
+            st[f"x{t}"] = x.numpy().astype(np.float32)
+        for h, (s_, d_, e_, sz) in enumerate(adjs):
+            st[f"adj{h}_src"], st[f"adj{h}_dst"] = np.asarray(s_), np.asarray(d_)
+            st[f"adj{h}_eid"] = np.asarray(e_)
+            st[f"adj{h}_size"] = np.asarray(sz)
+        _pack("p_", _params(model), st)
+        _pack("grad_", _grads(model), st)
+        save(f"mag_regnn_ft{feats_type}",
+             dict(model="mag.REGNN", feats_type=feats_type, in_channels=K, hidden=H, classes=C,
+                  num_layers=2, scaling_factor=10.0, num_edge_types=7, counts=counts,
+                  sizes=sizes, seed=seed, epoch=epoch, batch_idx=batch_idx, use_norm="ln",
+                  self_loop_type=2, dropout=0.0), st)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float64)
-    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat"]
+    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat", "regnn"]
     if "layers" in which:
         gen_layers()
     if "models" in which:
@@ -438,3 +530,5 @@ if __name__ == "__main__":
         gen_layers_extra()
     if "maggat" in which:
         gen_mag_gat()
+    if "regnn" in which:
+        gen_regnn()

@@ -168,3 +168,27 @@ def test_mag_regatconv(name):
     assert set(want) == set(gr), set(want) ^ set(gr)
     for k, v in want.items():
         _check(k, gr[k], v)
+
+
+def _regnn_adjs(d):
+    return [(d[f"adj{h}_src"], d[f"adj{h}_dst"], d[f"adj{h}_eid"], tuple(int(v) for v in d[f"adj{h}_size"]))
+            for h in range(d["meta"]["num_layers"])]
+
+
+@pytest.mark.parametrize("name", G.names("mag_regnn_"))
+def test_mag_regnn_model(name):
+    """the oracle's REGNN composition (group_input, 2 x REGCNConv + relu, out_lin, log_softmax,
+    nll) against the reference's own REGNN class run on a sampled batch (make_golden.gen_regnn)."""
+    d = G.load(name)
+    m = d["meta"]
+    P = G.sub(d, "p_")
+    x_dict = {t: d[f"x{t}"].astype(np.float64) for t in range(4) if f"x{t}" in d}
+    logp, loss, gr = O.mag_regnn_model(x_dict, d["ntype"], d["local"], d["n_id"], _regnn_adjs(d),
+                                       d["edge_type"], P, d["y"][d["batch"]],
+                                       feats_type=m["feats_type"])
+    _check("logp", logp, d["logp"])
+    _check("loss", np.asarray(loss), d["loss"])
+    want = G.sub(d, "grad_")
+    assert set(want) == set(gr), set(want) ^ set(gr)
+    for k, v in want.items():
+        _check(k, gr[k], v)
