@@ -74,7 +74,7 @@ def _full_graph(gd, dev):
 # ---------------------------------------------------------------------------------------------
 # neighbour-sampled step (configs[4])
 # ---------------------------------------------------------------------------------------------
-def build_ns(args, dev, hidden=64):
+def build_ns(args, dev, hidden=None):
     """mag/regnn_ns.py training step on the device engine (regnn_hip.ns.NSTrainer)."""
     from regnn_hip import mag, synth
     from regnn_hip.graph import RelGraph
@@ -92,6 +92,7 @@ def build_ns(args, dev, hidden=64):
     feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1, device=dev)
     x_dict = {k: f for k, f in enumerate(feats)}
     torch.manual_seed(3)
+    hidden = hidden or args.hidden
     model = mag.REGNN(128, hidden, 349, 2, 10.0, args.dropout, {k: 128 for k in x_dict}, 7,
                       use_norm="ln", self_loop_type=2).to(dev)
     n_paper = gd["counts"]["paper"]
@@ -106,7 +107,48 @@ def build_ns(args, dev, hidden=64):
     torch.cuda.synchronize()
     log(f"[bench] ns: N={gd['N']:,} E={rg.E:,} built in {time.time() - t0:.1f}s; "
         f"{tr.steps_per_epoch()} steps/epoch/rank, capacities {tr.sampler.caps}")
-    return tr, dict(N=gd["N"], E=rg.E, n_train=n_paper)
+    return tr, dict(N=gd["N"], E=rg.E, n_train=n_paper, rg=rg, edge_type=edge_type,
+                    node_type=node_type, local=local_node_idx, x_dict=x_dict, model=model)
+
+
+def run_ns_epoch(args, dev):
+    """context line: one whole NS training epoch over the synthetic paper train
+    split (steps_per_epoch steps, HIP-graph replays) plus the layer-wise full-neighbour
+    inference pass the reference runs each epoch (mag/regnn_ns.py:348-369, 422-443), in seconds,
+    next to mag/README.md:226-234 (448 s/epoch for the reference on 4 CPU cores, hidden 512,
+    ogbn-mag). The fused step covers hidden 64; other widths run the autograd path."""
+    from regnn_hip.inference import ShardedInference
+    rank, world = _world()
+    tr, info = build_ns(args, dev)
+    steps = tr.steps_per_epoch()
+    tr.capture(warmup=2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.replay()
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    model = info["model"].eval()
+    si = ShardedInference(model, info["rg"], info["edge_type"], info["node_type"],
+                          info["local"], rank, world)
+    si.run(info["x_dict"], gather="argmax")          # warm-up (kernel selection)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    si.run(info["x_dict"], gather="argmax")
+    torch.cuda.synchronize()
+    t_inf = time.perf_counter() - t0
+    return {"metric": "NS training epoch + full-neighbour inference (s)",
+            "value": t_train + t_inf, "unit": "s", "n_gpus": world, "steps": steps,
+            "warmup": 2, "ms_per_step": t_train / steps * 1e3, "higher_is_better": False,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded ogbn-mag-shaped graph)",
+            "config": {"workload": f"mag_like(scale={args.scale}) NS epoch: {steps} steps of "
+                                   f"{args.batch} papers x [25, 20], hidden {args.hidden}, "
+                                   f"then layer-wise inference over every node",
+                       "engine": "fused regnn_nsm_step" if tr.fused is not None else "module",
+                       "train_s": t_train, "inference_s": t_inf,
+                       "reference_context": "mag/README.md:226-234: 448.42 s per epoch, 4 CPU "
+                                            "cores, hidden 512, real ogbn-mag"}}
 
 
 def ns_step_bytes(sz, K, C, L=2, F=64):
@@ -270,6 +312,29 @@ def build_full(args, dev, wl):
                          args.dropout, 0.01, False, [f.shape[1] for f in feats]).to(dev)
         convs, kern = 3, ("spmm_heads_fwd", "spmm_heads_bwd", "gat_softmax_fwd",
                           "gat_softmax_bwd")
+    elif wl == "gat":
+        # the fused GAT path where bandwidth is the limit: one REGATConv
+        # layer (heads 8, out 64, relation bias, LeakyReLU 0.01) forward + backward on the
+        # ogbn-mag-shaped graph mag_like(scale); ft rows are 8 x 64 fp32 = 2 KiB
+        from layer import REGATConv
+        gd = synth.mag_like(args.scale, seed=0, device=dev)
+        g, rg, e_feat = _full_graph(gd, dev)
+        conv = REGATConv(gd["R"], 100.0, 64, 64, 8, 0.0, 0.0, 0.01).to(dev).eval()
+        x = torch.randn(gd["N"], 64, generator=gen, device=dev)
+        gout = torch.randn(gd["N"], 8, 64, generator=gen, device=dev)
+        params = list(conv.parameters())
+
+        def step():
+            y = conv(g, x, e_feat)
+            y.backward(gout)
+            for p_ in params:
+                p_.grad = None
+
+        torch.cuda.synchronize()
+        log(f"[bench] gat: N={gd['N']:,} E={rg.E:,} R={gd['R']} built in {time.time() - t0:.1f}s")
+        return dict(step=step, edges_per_step=rg.E, rg=rg, R=gd["R"],
+                    kernels=("gat_fused_fwd", "spmm_heads_bwd", "gat_softmax_bwd",
+                             "gat_attn_lse"), convs=1, N=rg.n_dst, E=rg.E, train_nodes=0)
     elif wl == "imdb":
         gd = synth.imdb_like(seed=0, device=dev)
         feats = synth.type_features(gd["counts"], synth.IMDB_DIMS, seed=1, device=dev,
@@ -393,7 +458,9 @@ def run_full(args, dev, wl):
                    f"fwd+bwd, out_lin 349 classes, CE, Adam) on mag_like(scale={args.scale})",
             "dblp": "REGCN 2-layer hidden=64 full-graph train step on dblp_like (configs[1])",
             "acm": "REGAT 2-layer hidden=64 heads [8,8,1] (last layer twice) on acm_like",
-            "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 on imdb_like"}[wl],
+            "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 on imdb_like",
+            "gat": f"REGATConv heads 8 x 64, relation bias, fwd (fused scores + softmax + SpMM) "
+                   f"+ bwd on mag_like(scale={args.scale})"}[wl],
             "nodes": w["N"], "edges": w["E"], "relations": w["R"],
             "conv_applications_per_step": w["convs"], "hidden": 64, "hip_graph": use_graph,
             "label_rows": f"the first {w['train_nodes']:,} nodes (a type-contiguous prefix)",
@@ -490,8 +557,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "ns_infer"],
-                    default="ns")
+    ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "gat",
+                                           "ns_infer", "ns_epoch"], default="ns")
+    ap.add_argument("--hidden", type=int, default=64, help="ns / ns_epoch: hidden width")
     ap.add_argument("--scale", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=512, help="ns: target papers per rank")
     ap.add_argument("--dropout", type=float, default=0.5)
@@ -514,6 +582,8 @@ def main():
             result["full_batch"] = fb
     elif args.workload == "ns_infer":
         result = run_other_ns_infer(args, dev)
+    elif args.workload == "ns_epoch":
+        result = run_ns_epoch(args, dev)
     else:
         fb = run_full(args, dev, args.workload)
         result = {"metric": METRIC, "value": fb["value"], "unit": "edges/s", "n_gpus": world,

@@ -277,6 +277,23 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
                           float* gs_out, float* ger, float* slab, int32_t n_rel,
                           hipStream_t stream);
 
+/* Fused GAT forward (layer/REGATConv.py:80-92 in one pass: the u_add_v SDDMM + relation bias +
+ * LeakyReLU, DGL edge_softmax over each destination's in-edges, and the per-head weighted SpMM):
+ *   out[v,h,:] = sum_{e: u->v} softmax_v(e)[h] * x[u,h,:],  lse[v,h] = log sum_e exp(e[h])
+ * with e[h] = LeakyReLU(el[u,h] + er[v,h] + ee_table[rel[e],h], slope), computed with an online
+ * softmax (no [E, H] attention written). x / out [n, H*D] in dtype; lse [n_seg, H] fp32 (-inf for
+ * a destination without in-edges, whose out row is 0). */
+int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* ee_table, const float* el, const float* er, const void* x,
+                        void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
+                        int32_t dtype, hipStream_t stream);
+
+/* The attention a[e,h] = exp(e[h] - lse[v,h]) (CSR edge order) of regnn_gat_fused_fwd, re-formed
+ * for the backward. H a power of two <= 32. */
+int regnn_gat_attn_lse(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                       const float* ee_table, const float* el, const float* er, const float* lse,
+                       int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream);
+
 /* Per-head weighted SpMM (GAT message passing, layer/REGATConv.py:90-91,
  * update_all(fn.u_mul_e('ft','a','m'), fn.sum('m','ft'))):
  *   y[v,h,:] = sum_{e in seg v} a[eid(e)*H + h] * x[idx[e],h,:],  eid(e) = perm ? perm[e] : e.

@@ -396,6 +396,171 @@ inline int gat_log2(int H) {    // log2(H) if H is a power of two <= kGatGroup, 
     return -1;
 }
 
+// ---- fused score + edge softmax + weighted SpMM (layer/REGATConv.py:80-92) ---------------
+// One pass per destination v: for each in-edge u -> v and head h the score
+// e = LeakyReLU(el[u,h] + er[v,h] + ee[rel,h]) enters an online softmax (running max m, sum s,
+// accumulator rescaled when the max grows) while the same lanes gather x[u,h,:]:
+//   out[v,h,:] = sum_e exp(e - m) x[u,h,:] / s,   lse[v,h] = m + log s.
+// Every lane of a head carries its own copy of (m, s) (identical: the same scores), so no
+// cross-lane reduction is needed; a[e,h] is never written (the backward re-forms it from lse).
+// Lanes / vectors as spmm_heads_kernel; edge ids loaded cooperatively, UN rows in flight.
+struct GatFusedArgs {
+    const int32_t* ptr;
+    const int32_t* idx;
+    const uint8_t* rel;
+    const float* ee;
+    const float* el;
+    const float* er;
+    const void* x;
+    void* out;
+    float* lse;
+    int64_t n_seg;
+    int H, D;
+    float slope;
+};
+
+template <typename T, int LPR, int NV>
+__global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p) {
+    constexpr int EV = Vec<T>::N;
+    constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);
+    constexpr int GPB = kBlock / LPR;
+    const int tid = threadIdx.x, lane = tid & (LPR - 1);
+    const int F = p.H * p.D;
+    const T* __restrict__ src = static_cast<const T*>(p.x);
+    for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < p.n_seg;
+         seg += (int64_t)gridDim.x * GPB) {
+        const int beg = p.ptr[seg], end = p.ptr[seg + 1];
+        float acc[NV][EV] = {};
+        float m[NV], s[NV], erv[NV];
+        int head[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = (q * LPR + lane) * EV;
+            head[q] = o < F ? o / p.D : 0;
+            erv[q] = p.er[seg * p.H + head[q]];
+            m[q] = -INFINITY;
+            s[q] = 0.f;
+        }
+        for (int e0 = beg; e0 < end; e0 += LPR) {
+            const int e = e0 + lane;
+            int j = 0, r = 0;
+            if (e < end) {
+                j = p.idx[e];
+                r = p.ee ? int(p.rel[e]) : 0;
+            }
+            const int cnt = min(LPR, end - e0);
+            for (int k0 = 0; k0 < cnt; k0 += UN) {
+                float v[UN][NV][EV];
+                float sc[UN][NV];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    const int kk = min(k0 + u, cnt - 1);
+                    const int jj = __shfl(j, kk, LPR);
+                    const int rr = __shfl(r, kk, LPR);
+#pragma unroll
+                    for (int q = 0; q < NV; ++q) {
+                        const int o = (q * LPR + lane) * EV;
+                        if (o < F) {
+                            Vec<T>::load(src + (int64_t)jj * F + o, v[u][q]);
+                            float z = p.el[(int64_t)jj * p.H + head[q]] + erv[q];
+                            if (p.ee) z += p.ee[rr * p.H + head[q]];
+                            sc[u][q] = lrelu(z, p.slope);
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < EV; ++t) v[u][q][t] = 0.f;
+                            sc[u][q] = 0.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    if (k0 + u >= cnt) break;
+#pragma unroll
+                    for (int q = 0; q < NV; ++q) {
+                        const float d = sc[u][q] - m[q];
+                        const bool grow = d > 0.f;                   // new running max
+                        const float ex = __expf(grow ? -d : d);
+                        const float sa = grow ? ex : 1.f, sv = grow ? 1.f : ex;
+#pragma unroll
+                        for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(acc[q][t], sa, sv * v[u][q][t]);
+                        s[q] = fmaf(s[q], sa, sv);
+                        m[q] = grow ? sc[u][q] : m[q];
+                    }
+                }
+            }
+        }
+        T* __restrict__ out = static_cast<T*>(p.out) + seg * F;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int o = (q * LPR + lane) * EV;
+            if (o < F) {
+                const float inv = s[q] > 0.f ? 1.f / s[q] : 0.f;
+                float w[EV];
+#pragma unroll
+                for (int t = 0; t < EV; ++t) w[t] = acc[q][t] * inv;
+                Vec<T>::store(out + o, w);
+                if (o % p.D == 0)
+                    p.lse[seg * p.H + head[q]] = s[q] > 0.f ? m[q] + __logf(s[q]) : -INFINITY;
+            }
+        }
+    }
+}
+
+// a[e,h] = exp(LeakyReLU(el[u,h] + er[v,h] + ee[rel,h]) - lse[v,h]) in CSR edge order (the
+// attention the fused forward did not store; its backward needs it). Group layout of
+// gat_softmax_fwd_group: (edge, head) pairs flattened per segment, coalesced H-vectors.
+__global__ void __launch_bounds__(kBlock)
+gat_attn_lse_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                   const uint8_t* __restrict__ rel, const float* __restrict__ ee,
+                   const float* __restrict__ el, const float* __restrict__ er,
+                   const float* __restrict__ lse, int64_t n_seg, int H, int lgH, float slope,
+                   float* __restrict__ a) {
+    constexpr int G = kGatGroup, U = kGatUn;
+    const int lane = threadIdx.x & (G - 1), h = lane & (H - 1);
+    for (int64_t seg = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; seg < n_seg;
+         seg += (int64_t)gridDim.x * (kBlock / G)) {
+        const int beg = ptr[seg], np = (ptr[seg + 1] - beg) << lgH;
+        const float erv = er[seg * H + h], l = lse[seg * H + h];
+        for (int p0 = lane; p0 < np; p0 += G * U) {
+            float sc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = p0 + u * G;
+                sc[u] = q < np ? gat_score(idx, rel, ee, el, erv, beg + (q >> lgH), H, h, slope)
+                               : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = p0 + u * G;
+                if (q < np) a[(int64_t)beg * H + q] = __expf(sc[u] - l);
+            }
+        }
+    }
+}
+
+template <typename T>
+int dispatch_gat_fused(GatFusedArgs p, hipStream_t stream) {
+    constexpr int EV = Vec<T>::N;
+    const int F = p.H * p.D;
+    if (p.D <= 0 || p.D % EV || p.H <= 0) return REGNN_EUNSUPPORTED;
+    const int nvec = F / EV;
+#define REGNN_GATF(LPR, NV)                                                                   \
+    if (nvec <= (LPR) * (NV)) {                                                               \
+        hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV>),                                \
+                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p); \
+        REGNN_LAUNCH_CHECK();                                                                 \
+        return REGNN_OK;                                                                      \
+    }
+    REGNN_GATF(16, 1)
+    REGNN_GATF(16, 2)
+    REGNN_GATF(16, 4)
+    REGNN_GATF(64, 2)
+    REGNN_GATF(64, 4)
+    REGNN_GATF(64, 8)
+#undef REGNN_GATF
+    return REGNN_EUNSUPPORTED;
+}
+
 // ---- attention logits el / er (layer/REGATConv.py:68-69) ------------------------------------
 // el[n,h] = <ft[n,h,:], attn_l[h,:]>, er likewise: a group of 16 lanes per (node, head) reads the
 // D-vector coalesced and reduces with xor-shuffles; both dots share the one read of ft.
@@ -501,6 +666,33 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
         hipLaunchKernelGGL(gat_softmax_bwd_generic, dim3(grid_for(n_seg * H, kBlock)),
                            dim3(kBlock), lds, stream, ptr, idx, rel, ee_table, el, er, a, ga,
                            n_seg, H, slope, gs_out, ger, slab, n_rel);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                        const float* ee_table, const float* el, const float* er, const void* x,
+                        void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
+                        int32_t dtype, hipStream_t stream) {
+    if (!ptr || !idx || !el || !er || !x || !out || !lse || n_seg < 0 || (ee_table && !rel))
+        return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    GatFusedArgs p{ptr, idx, rel, ee_table, el, er, x, out, lse, n_seg, H, D, slope};
+    if (dtype == REGNN_F32) return dispatch_gat_fused<float>(p, stream);
+    if (dtype == REGNN_BF16) return dispatch_gat_fused<bf16_t>(p, stream);
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_gat_attn_lse(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                       const float* ee_table, const float* el, const float* er, const float* lse,
+                       int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream) {
+    if (!ptr || !idx || !el || !er || !lse || !a || H <= 0 || n_seg < 0 || (ee_table && !rel))
+        return REGNN_EINVAL;
+    if (n_seg == 0) return REGNN_OK;
+    const int lg = gat_log2(H);
+    if (lg < 0) return REGNN_EUNSUPPORTED;
+    hipLaunchKernelGGL(gat_attn_lse_group, dim3(grid_for(n_seg, kBlock / kGatGroup)), dim3(kBlock),
+                       0, stream, ptr, idx, rel, ee_table, el, er, lse, n_seg, H, lg, slope, a);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

@@ -62,9 +62,14 @@ class REGATConv(nn.Module):
         if edge_feats is not None:
             tab = relation_table(self.edge_weight, self.alpha)                     # :72-74
             pack = rg.rel_pack(edge_feats, num_rel=self.num_etypes)
-        a = ops.gat_attention(rg, el, er, tab, pack, self.leaky_relu.negative_slope)  # :80-88
-        a = self.attn_drop(a)                                                      # :88
-        rst = ops.head_spmm(rg, a, ft)                                             # :90-92
+        slope = self.leaky_relu.negative_slope
+        if self.training and self.attn_drop.p > 0:
+            a = ops.gat_attention(rg, el, er, tab, pack, slope)                    # :80-88
+            a = self.attn_drop(a)                                                  # :88
+            rst = ops.head_spmm(rg, a, ft)                                         # :90-92
+        else:
+            # no attention dropout: scores, softmax and aggregation in one pass (:80-92)
+            rst = ops.gat_fused(rg, el, er, ft, tab, pack, slope)
         if self.res_fc is not None:
             resval = self.res_fc(h).view(h.shape[0], -1, self.out_feats)           # :94-96
             rst = rst + resval

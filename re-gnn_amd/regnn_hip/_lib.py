@@ -69,6 +69,8 @@ _SIG = {
     "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P],
                               ctypes.c_int),
     "regnn_spmm_heads_fwd": ([P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
+    "regnn_gat_fused_fwd": ([P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I32, P], ctypes.c_int),
+    "regnn_gat_attn_lse": ([P, P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_spmm_heads_bwd": ([P, P, P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
     "regnn_segment_sum": ([P, P, P, I64, I32, P, P], ctypes.c_int),
     "regnn_col_sum": ([P, I64, I32, P, P], ctypes.c_int),

@@ -836,6 +836,75 @@ class _HeadSpmm(torch.autograd.Function):
         return ga, gft, None
 
 
+class _GatFused(torch.autograd.Function):
+    """out[v,h,:] = sum_{e: u->v} edge_softmax(LeakyReLU(el[u]+er[v]+ee[rel]))[e,h] * ft[u,h,:]
+    in one pass (regnn_gat_fused_fwd, online softmax; the [E, H] attention is not stored). The
+    backward re-forms the attention from the per-(destination, head) log-sum-exp
+    (regnn_gat_attn_lse) and runs the unfused backward kernels."""
+
+    @staticmethod
+    def forward(ctx, el, er, ee_tab, ft, rg, pack, slope):
+        N, H, D = ft.shape
+        el, er, ft = el.contiguous().float(), er.contiguous().float(), ft.contiguous()
+        t = None if ee_tab is None else ee_tab.detach().float().contiguous()
+        rel = pack.rel_csr if t is not None else None
+        out = torch.empty(rg.n_dst, H, D, dtype=ft.dtype, device=ft.device)
+        lse = torch.empty(rg.n_dst, H, dtype=torch.float32, device=ft.device)
+        s_ = ft.element_size()
+        with timed("gat_fused_fwd", rg.E * (H * D * s_ + 4 * H + 5) +
+                   rg.n_dst * (H * D * s_ + 8 * H + 4)):
+            L.call("regnn_gat_fused_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
+                   L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(ft), L.ptr(out), L.ptr(lse), rg.n_dst, H,
+                   D, float(slope), L.dtype_code(ft), L.stream())
+        ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
+        ctx.tab_shape = None if ee_tab is None else ee_tab.shape
+        ctx.save_for_backward(el, er, t, ft, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        el, er, t, ft, lse = ctx.saved_tensors
+        rg, pack, slope = ctx.rg, ctx.pack, ctx.slope
+        N, H, D = ft.shape
+        rel = pack.rel_csr if t is not None else None
+        a = torch.empty(rg.E, H, dtype=torch.float32, device=ft.device)
+        with timed("gat_attn_lse", rg.E * (5 + 8 * H) + rg.n_dst * 8 * H):
+            L.call("regnn_gat_attn_lse", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
+                   L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(lse), rg.n_dst, H, float(slope),
+                   L.ptr(a), L.stream())
+        gy = gy.contiguous().to(ft.dtype)
+        gft = torch.empty_like(ft)
+        ga = torch.empty_like(a)
+        s_ = ft.element_size()
+        with timed("spmm_heads_bwd",
+                   rg.E * (H * D * s_ + 8 * H + 8) + rg.n_src * (2 * H * D * s_ + 4)):
+            L.call("regnn_spmm_heads_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                   L.ptr(rg.csc2csr), L.ptr(a), L.ptr(gy), L.ptr(ft), L.ptr(gft), L.ptr(ga),
+                   rg.n_src, H, D, L.dtype_code(ft), L.stream())
+        gs = torch.empty_like(a)
+        ger = torch.empty_like(er)
+        n_rel = t.shape[0] if t is not None else 0
+        slab = _slab(n_rel * H, el.device) if (t is not None and ctx.needs_input_grad[2]) else None
+        with timed("gat_softmax_bwd", rg.E * (5 + 16 * H) + rg.n_dst * 12 * H):
+            L.call("regnn_gat_softmax_bwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
+                   L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(a), L.ptr(ga), rg.n_dst, H,
+                   float(slope), L.ptr(gs), L.ptr(ger), L.ptr(slab), n_rel, L.stream())
+        gel = torch.empty(rg.n_src, H, dtype=torch.float32, device=el.device)
+        L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
+               L.ptr(gel), L.stream())
+        g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
+        return gel, ger, g_tab, gft, None, None, None
+
+
+def gat_fused(rg, el, er, ft, ee_tab=None, pack=None, slope=0.2):
+    """layer/REGATConv.py:80-92 without attention dropout, as one fused forward pass (H a power of
+    two <= 32; otherwise the unfused gat_attention + head_spmm)."""
+    H = ft.shape[1]
+    if H & (H - 1) or H > 32:
+        return head_spmm(rg, gat_attention(rg, el, er, ee_tab, pack, slope), ft)
+    return _GatFused.apply(el, er, ee_tab, ft, rg, pack, slope)
+
+
 def head_spmm(rg, a, ft):
     """out[v,h,:] = sum_{e: u->v} a[e,h] * ft[u,h,:]   (a in CSR edge order)."""
     return _HeadSpmm.apply(a, ft, rg)
