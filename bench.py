@@ -81,7 +81,7 @@ def build_ns(args, dev, hidden=None):
     from regnn_hip.ns import NSTrainer
     t0 = time.time()
     rank, world = _world()
-    gd = synth.mag_like(args.scale, seed=0, device=dev)         # replicated on every rank
+    gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)         # replicated on every rank
     keep = gd["rel"] <= 7                                       # the 7 raw edge types, no loops
     rg = RelGraph(gd["src"][keep], gd["dst"][keep], gd["N"], dev)
     edge_type = gd["rel"][keep].to(torch.int64) - 1
@@ -285,7 +285,7 @@ def build_full(args, dev, wl):
     torch.manual_seed(3)
     if wl in ("mag", "dblp"):
         if wl == "mag":
-            gd = synth.mag_like(args.scale, seed=0, device=dev)
+            gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)
             feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1,
                                         device=dev, kind="mag")
             n_classes, train_nodes = 349, gd["counts"]["paper"]
@@ -317,7 +317,7 @@ def build_full(args, dev, wl):
         # layer (heads 8, out 64, relation bias, LeakyReLU 0.01) forward + backward on the
         # ogbn-mag-shaped graph mag_like(scale); ft rows are 8 x 64 fp32 = 2 KiB
         from layer import REGATConv
-        gd = synth.mag_like(args.scale, seed=0, device=dev)
+        gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)
         g, rg, e_feat = _full_graph(gd, dev)
         conv = REGATConv(gd["R"], 100.0, 64, 64, 8, 0.0, 0.0, 0.01).to(dev).eval()
         x = torch.randn(gd["N"], 64, generator=gen, device=dev)
@@ -460,7 +460,7 @@ def run_full(args, dev, wl):
             "acm": "REGAT 2-layer hidden=64 heads [8,8,1] (last layer twice) on acm_like",
             "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 on imdb_like",
             "gat": f"REGATConv heads 8 x 64, relation bias, fwd (fused scores + softmax + SpMM) "
-                   f"+ bwd on mag_like(scale={args.scale})"}[wl],
+                   f"+ bwd on mag_like(scale={args.scale}, zipf_s={args.zipf})"}[wl],
             "nodes": w["N"], "edges": w["E"], "relations": w["R"],
             "conv_applications_per_step": w["convs"], "hidden": 64, "hip_graph": use_graph,
             "label_rows": f"the first {w['train_nodes']:,} nodes (a type-contiguous prefix)",
@@ -486,7 +486,7 @@ def build_ns_infer(args, dev):
     from regnn_hip.graph import RelGraph
     from regnn_hip.inference import ShardedInference
     rank, world = _world()
-    gd = synth.mag_like(args.scale, seed=0, device=dev)
+    gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)
     keep = gd["rel"] <= 7
     rg = RelGraph(gd["src"][keep], gd["dst"][keep], gd["N"], dev)
     edge_type = gd["rel"][keep].to(torch.int64) - 1
@@ -560,6 +560,8 @@ def main():
     ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "gat",
                                            "ns_infer", "ns_epoch"], default="ns")
     ap.add_argument("--hidden", type=int, default=64, help="ns / ns_epoch: hidden width")
+    ap.add_argument("--zipf", type=float, default=1.1,
+                    help="mag_like destination skew (1.1: ogbn-mag-like hubs; 0: uniform)")
     ap.add_argument("--scale", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=512, help="ns: target papers per rank")
     ap.add_argument("--dropout", type=float, default=0.5)
