@@ -288,7 +288,19 @@ def build_full(args, dev, wl):
             gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)
             feats = synth.type_features(gd["counts"], {t: 128 for t in synth.NTYPES}, seed=1,
                                         device=dev, kind="mag")
-            n_classes, train_nodes = 349, gd["counts"]["paper"]
+            # a random train split at ogbn-mag's train fraction (629,571 of 736,389 papers),
+            # its rows renumbered first once (data.loss_rows_first): head_ce's loss-row prefix
+            from regnn_hip import data
+            n_paper = gd["counts"]["paper"]
+            split_gen = torch.Generator(device=dev)
+            split_gen.manual_seed(5)
+            train = torch.randperm(n_paper, generator=split_gen, device=dev)
+            train = train[:int(round(n_paper * 629_571 / 736_389))]
+            perm, inv = data.loss_rows_first(gd["N"], train, n_paper)
+            gd["src"], gd["dst"] = inv[gd["src"]], inv[gd["dst"]]
+            feats[0] = feats[0][perm[:n_paper]].contiguous()
+            del perm, inv
+            n_classes, train_nodes = 349, train.numel()
         else:
             gd = synth.dblp_like(seed=0, device=dev)
             feats = synth.type_features(gd["counts"], synth.DBLP_DIMS, seed=1, device=dev,
@@ -463,7 +475,10 @@ def run_full(args, dev, wl):
                    f"+ bwd on mag_like(scale={args.scale}, zipf_s={args.zipf})"}[wl],
             "nodes": w["N"], "edges": w["E"], "relations": w["R"],
             "conv_applications_per_step": w["convs"], "hidden": 64, "hip_graph": use_graph,
-            "label_rows": f"the first {w['train_nodes']:,} nodes (a type-contiguous prefix)",
+            "label_rows": (f"{w['train_nodes']:,} train rows: a seeded random 85.5 % of the "
+                           f"papers (ogbn-mag's train fraction), renumbered first once "
+                           f"(data.loss_rows_first)" if wl == "mag" else
+                           f"the first {w['train_nodes']:,} nodes (the target type)"),
             "last_layer_bwd_edges": (min(p.E for p in rg._prefix.values())
                                      if getattr(rg, "_prefix", None) else None)},
         "roofline": {

@@ -133,3 +133,26 @@ def build_graph(adjM, adjMM_wsl_2, device=None):
     if device is not None:
         g = g.to(device)
     return g, torch.from_numpy(e_feat).to(device if device is not None else "cpu")
+
+
+def loss_rows_first(num_nodes, train_idx, first_type_count):
+    """node renumbering that puts the loss rows (train_idx, all of the first node type, as the
+    target type of run_regnn.py / mag/regnn_ns.py is) at [0, n_train), the rest of the first
+    type after them, every other node where it was: ops.head_ce's fast path (the loss rows a
+    prefix) for any train split. Returns (perm, inv) int64: new row r holds old node perm[r],
+    old node u becomes inv[u]. Apply once to the edge list (inv[src], inv[dst]), the first type's
+    feature rows (x0[perm[:first_type_count]]) and the labels (labels[train_idx])."""
+    t = torch.as_tensor(train_idx).reshape(-1).to(torch.int64)
+    dev = t.device
+    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= first_type_count):
+        raise ValueError("loss rows must lie in the first node type's range")
+    is_train = torch.zeros(first_type_count, dtype=torch.bool, device=dev)
+    is_train[t] = True
+    if int(is_train.sum()) != t.numel():
+        raise ValueError("duplicate loss rows")
+    rest = torch.nonzero(~is_train).flatten()
+    perm = torch.cat([torch.sort(t)[0], rest,
+                      torch.arange(first_type_count, num_nodes, dtype=torch.int64, device=dev)])
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(num_nodes, dtype=torch.int64, device=dev)
+    return perm, inv

@@ -1168,10 +1168,29 @@ def batched_wgrad(g, x, chunk=1 << 15):
     return out
 
 
-def head_ce(h, weight, bias, labels):
-    """fused output head + cross-entropy over rows [0, len(labels)) -> (logits, loss).
+def head_ce(h, weight, bias, labels, rows=None):
+    """fused output head + cross-entropy -> (logits of every row, mean loss over the loss rows).
+
+    rows = None: the loss rows are [0, len(labels)) (run_regnn.py:146-148 with the train nodes
+    numbered first, e.g. by data.loss_rows_first): the fast path, whose backward hands the last
+    aggregation its gradient rows and gathers only the CSC edges into the loss rows.
+    rows = an index tensor (any train split): the loss rows h[rows] go through the same fused
+    head (labels[i] is the label of row rows[i]); the logits of every row are returned without
+    a gradient, and the gradient reaches h through the gather (no hand-off).
     bf16 rows go in as they are (z mode: widened inside, bf16 gradient out), else as fp32."""
     if h.dtype != torch.float32 and not (h.dtype == torch.bfloat16 and HEAD["p"] == "z" and
                                          head_fused(h.shape[-1], weight.shape[0])):
         h = h.float()
+    if rows is not None:
+        rows = rows.to(h.device, torch.int64).reshape(-1)
+        n = rows.numel()
+        if n != labels.numel():
+            raise ValueError(f"{n} loss rows but {labels.numel()} labels")
+        if not (n <= h.shape[0] and bool((rows == torch.arange(n, device=rows.device)).all())):
+            _, loss = _HeadCE.apply(h.index_select(0, rows), weight, bias, labels)
+            with torch.no_grad():
+                logits = h.float() @ weight.detach().t()
+                if bias is not None:
+                    logits += bias.detach()
+            return logits, loss
     return _HeadCE.apply(h, weight, bias, labels)

@@ -304,3 +304,76 @@ def test_head_gh_handoff_bf16(n_loss, monkeypatch):
         for a, b in zip(grads[m], grads["off"]):
             err = float((a - b).abs().max()) / max(1e-3, float(b.abs().max()))
             assert err <= 1e-2
+
+
+@pytest.mark.parametrize("n_loss", [20, 333])
+def test_head_ce_non_prefix_loss_rows(n_loss):
+    """head_ce with an arbitrary loss-row set (rows=): loss and every gradient equal torch's
+    cross-entropy over logits[rows] (run_regnn.py:146-148 with a random train split)."""
+    from regnn_hip import ops
+    from regnn_hip.graph import RelGraph
+    src, dst, rel, n, R = _graph(seed=9)
+    rg = RelGraph(src, dst, n, DEV)
+    pack = rg.rel_pack(torch.from_numpy(rel).to(DEV), num_rel=R)
+    g = torch.Generator().manual_seed(6)
+    C = 37
+    base = [torch.randn(n, 64, generator=g), torch.rand(R, 1, generator=g) + 0.2,
+            torch.rand(n, generator=g) + 0.5, torch.randn(C, 64, generator=g) * 0.1,
+            torch.randn(C, generator=g)]
+    rows = torch.randperm(n, generator=g)[:n_loss].to(DEV)
+    labels = torch.randint(0, C, (n_loss,), generator=g).to(DEV)
+    out = []
+    for fused in (True, False):
+        xd, t0, m0, W, b = [t.to(DEV).requires_grad_(True) for t in base]
+        y = ops.re_spmm(rg, xd, t0, pack, pre=m0, post=m0)
+        if fused:
+            logits, loss = ops.head_ce(y, W, b, labels, rows=rows)
+        else:
+            logits = y @ W.t() + b
+            loss = torch.nn.functional.cross_entropy(logits[rows], labels)
+        loss.backward()
+        out.append([loss.detach(), logits.detach()] + [t.grad for t in (xd, t0, m0, W, b)])
+    for name, a, b_ in zip(["loss", "logits", "x", "tab", "scale", "W", "b"], out[0], out[1]):
+        err = (a - b_).abs().max().item() / max(1.0, b_.abs().max().item())
+        assert err <= 1e-5, f"{name}: rel err {err:.3e}"
+
+
+def test_loss_rows_first_renumbering_preserves_the_model():
+    """data.loss_rows_first: REGCN on the renumbered graph with head_ce's prefix fast path gives
+    the loss and parameter gradients of the original numbering with the loss over a random
+    (non-prefix) train split."""
+    import torch.nn.functional as F
+    import dgl
+    from regnn_hip import data, nets, ops, synth
+    gd = synth.mag_like(0.002, seed=3, device=DEV)
+    feats = synth.type_features(gd["counts"], {t: 16 for t in synth.NTYPES}, seed=1, device=DEV)
+    n_paper = gd["counts"]["paper"]
+    gen = torch.Generator(device=DEV).manual_seed(2)
+    train = torch.randperm(n_paper, generator=gen, device=DEV)[:n_paper // 2]
+    y = torch.randint(0, 7, (n_paper,), generator=gen, device=DEV)
+    res = []
+    for renumber in (False, True):
+        src, dst, fs = gd["src"], gd["dst"], list(feats)
+        lab_rows, lab = train, y[train]
+        if renumber:
+            perm, inv = data.loss_rows_first(gd["N"], train, n_paper)
+            src, dst = inv[src], inv[dst]
+            fs[0] = fs[0][perm[:n_paper]].contiguous()
+            lab = y[perm[:train.numel()]]
+        g = dgl.DGLGraph((src, dst), num_nodes=gd["N"])
+        torch.manual_seed(0)
+        net = nets.REGCN(g, gd["R"], 100.0, 64, 64, 7, 2, F.elu, 0.0,
+                         [f.shape[1] for f in fs]).to(DEV).eval()
+        h = net.embed(fs, gd["rel"].to(torch.int64))
+        W, b = net.head()
+        if renumber:
+            _, loss = ops.head_ce(h, W, b, lab)
+        else:
+            loss = F.cross_entropy((h @ W.t() + b)[lab_rows], lab)
+        loss.backward()
+        res.append((loss.detach(), {n: p.grad.clone() for n, p in net.named_parameters()}))
+    (l0, g0), (l1, g1) = res
+    assert abs(float(l0) - float(l1)) <= 1e-5 * max(1.0, abs(float(l0)))
+    for k in g0:
+        err = (g0[k] - g1[k]).abs().max().item() / max(1.0, g0[k].abs().max().item())
+        assert err <= 1e-5, f"{k}: rel err {err:.3e}"
