@@ -87,11 +87,9 @@ struct Seg {
     static constexpr bool BWD = MODE != kFwd;
     static constexpr bool SLAB = MODE == kBwdSlab || MODE == kBwdBoth;
     static constexpr bool EDGE = MODE == kBwdEdge || MODE == kBwdBoth;
-    // rows gathered per step: 8 x 16-byte loads in flight per lane (NV vectors per row);
-    // UNT a multiple (MB >= 2) of LPR: MB batches of LPR edges per step (accumulate_mb)
-    static constexpr int MB = (UNT > LPR && UNT % LPR == 0) ? UNT / LPR : 1;
+    // rows gathered per step: 8 x 16-byte loads in flight per lane (NV vectors per row)
     static constexpr int UN0 = UNT > 0 ? UNT : (NV >= 8 ? 1 : (8 / NV));
-    static constexpr int UN = MB > 1 ? UNT : (UN0 < LPR ? UN0 : LPR);
+    static constexpr int UN = UN0 < LPR ? UN0 : LPR;
     static constexpr int NVEC = LPR * NV;    // 16-byte vectors per row (FULL rows)
 
     __device__ __forceinline__ static int off(int q, int lane) { return (q * LPR + lane) * EV; }
@@ -158,102 +156,9 @@ struct Seg {
     // unconditional: edge indices are clamped to the segment, absent optional arrays read one
     // constant (kOneF / kZeroU8), and a batch tail is processed as a full step with weight 0 and
     // the dot scale 0, so no run-time branch forces a vmcnt(0) inside the loop.
-    // accumulate() with MB batches of LPR edges per step (MB * LPR rows in flight per lane: the
-    // 128-byte rows of F=64 bf16 carry half the bytes per lane of fp32 rows). Ids and relation /
-    // edge-weight loads run one step ahead; the same edge order, so the same sums.
-    __device__ __forceinline__ static void accumulate_mb(const SpmmArgs& a, int beg, int end,
-                                                         int lane, float os,
-                                                         const float (&sx)[NV][EV],
-                                                         float (&acc)[NV][EV], float* bins, int tid) {
-        constexpr int S = MB * LPR;
-        const T* __restrict__ src = static_cast<const T*>(a.src);
-        const int F = a.F;
-        const int last = end - 1;
-        const float* tabp = a.tab ? a.tab : kOneF;
-        const float* scp = a.in_scale ? a.in_scale : kOneF;
-        const float* ewp = a.edge_w ? a.edge_w : kOneF;
-        const uint8_t* relp = a.rel ? a.rel : kZeroU8;
-        const int tm = a.tab ? 0xff : 0, sm = a.in_scale ? -1 : 0;
-        const int em = a.edge_w ? -1 : 0, rm = a.rel ? -1 : 0;
-        uint32_t dkey = 0;
-        if constexpr (DROP && !BWD) dkey = drop_key(a.drop_seed);
-        int j[MB], r[MB];
-        float ew[MB];
-#pragma unroll
-        for (int m = 0; m < MB; ++m) {
-            const int ec = min(beg + m * LPR + lane, last);
-            j[m] = a.idx[ec];
-            r[m] = relp[ec & rm];
-            ew[m] = ewp[ec & em];
-        }
-        for (int e0 = beg; e0 < end; e0 += S) {
-            float w[MB], d[MB];
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                const float sc = scp[j[m] & sm], t = tabp[r[m] & tm];
-                const bool live = e0 + m * LPR + lane < end;
-                w[m] = live ? t * ew[m] * sc : 0.f;
-                d[m] = live ? sc * os : 0.f;
-            }
-            int jn[MB], rn[MB];
-            float ewn[MB];
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {                           // next step's ids
-                const int ec = min(e0 + S + m * LPR + lane, last);
-                jn[m] = a.idx[ec];
-                rn[m] = relp[ec & rm];
-                ewn[m] = ewp[ec & em];
-            }
-            const int cnt = min(S, end - e0);
-            int jj[S];
-            float wk[S];
-            uint4 raw[S][NV];
-#pragma unroll
-            for (int u = 0; u < S; ++u) jj[u] = __shfl(j[u / LPR], u % LPR, LPR);
-#pragma unroll
-            for (int u = 0; u < S; ++u) load_raw(src + (int64_t)jj[u] * F, F, lane, raw[u]);
-#pragma unroll
-            for (int u = 0; u < S; ++u) wk[u] = __shfl(w[u / LPR], u % LPR, LPR);
-#pragma unroll
-            for (int u = 0; u < S; ++u) {
-                float v[NV][EV];
-#pragma unroll
-                for (int q = 0; q < NV; ++q) unpack<T>(raw[u][q], v[q]);
-                if constexpr (DROP && !BWD) {
-#pragma unroll
-                    for (int q = 0; q < NV; ++q)
-                        drop_apply<EV, DROP>(dkey, a.drop_thresh, a.drop_scale, jj[u], NVEC,
-                                             q * LPR + lane, v[q]);
-                }
-#pragma unroll
-                for (int q = 0; q < NV; ++q)
-#pragma unroll
-                    for (int t = 0; t < EV; ++t) acc[q][t] = fmaf(wk[u], v[q][t], acc[q][t]);
-                if constexpr (SLAB || EDGE) {
-                    const float p = dot(v, sx) * __shfl(d[u / LPR], u % LPR, LPR);
-                    if constexpr (SLAB) bins[__shfl(r[u / LPR], u % LPR, LPR) * kBlock + tid] += p;
-                    if constexpr (EDGE) {
-                        const float sum = group_sum<LPR>(p);
-                        if (lane == 0 && u < cnt) a.edge_grad[e0 + u] = sum;
-                    }
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                j[m] = jn[m];
-                r[m] = rn[m];
-                ew[m] = ewn[m];
-            }
-        }
-    }
-
     __device__ __forceinline__ static void accumulate(const SpmmArgs& a, int beg, int end, int lane,
                                                       float os, const float (&sx)[NV][EV],
                                                       float (&acc)[NV][EV], float* bins, int tid) {
-        if constexpr (MB > 1) {
-            accumulate_mb(a, beg, end, lane, os, sx, acc, bins, tid);
-            return;
-        }
         const T* __restrict__ src = static_cast<const T*>(a.src);
         const int F = a.F;
         const int last = end - 1;
@@ -677,9 +582,6 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
         if (g_tune_v8 == 1) return launch_mode<T, 8, 1, 0, true>(a, mode, stream);
         if (g_tune_v8 == 2) return launch_mode<T, 4, 2, 0, true>(a, mode, stream);
         if (g_tune_v8 == 3) return launch_mode<T, 16, 1, 0, false>(a, mode, stream);
-        if (g_tune_v8 == 4) return launch_mode<T, 8, 1, 16, true>(a, mode, stream);
-        if (g_tune_v8 == 5) return launch_mode<T, 8, 1, 24, true>(a, mode, stream);
-        if (g_tune_v8 == 6) return launch_mode<T, 4, 2, 8, true>(a, mode, stream);
     }
     if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
     if (nvec == 16) return launch_f16v<T>(a, mode, stream);

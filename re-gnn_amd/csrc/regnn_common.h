@@ -147,8 +147,7 @@ extern int64_t g_tune_un;        // rows in flight per lane for F = 16 vectors (
 extern int64_t g_tune_head;      // fused head variant: 0 = pipelined, 1 = plain
 extern int64_t g_tune_rowscale;  // rows in flight per lane group of regnn_row_scale (0 = 1)
 extern int64_t g_tune_v8;        // 8-vector rows (F=64 bf16): 0 = 8 lanes, 1 = 8 lanes unmasked,
-                                 // 2 = 4 lanes x 2 vectors, 3 = 16 lanes (half masked),
-                                 // 4 / 5 = 8 lanes with 16 / 24 rows in flight, 6 = 4x2, 8 rows
+                                 // 2 = 4 lanes x 2 vectors, 3 = 16 lanes (half masked)
 
 int resident_blocks(const void* kernel, size_t lds, int block = kBlock);  // per CU x CUs, cached
 
