@@ -50,8 +50,6 @@ int regnn_abi_version(void);
  * step for 16-vector rows (F=64 fp32 / F=128 bf16): 0 = default (8), 4 or 16. key 3: fused
  * head variant (0 = next tile / next k-step operands prefetched, the default; 1 = plain).
  * key 4: rows in flight per lane group of regnn_row_scale (0 = default 1, 2 or 4).
- * key 5: SpMM lane layout of 8-vector rows (F = 64 bf16): 0 = 8 lanes per row (default),
- * 1 = the same without lane masking, 2 = 4 lanes x 2 vectors, 3 = 16 lanes.
  * Returns the previous value, -1 for an unknown key. */
 int64_t regnn_tune(int32_t key, int64_t value);
 

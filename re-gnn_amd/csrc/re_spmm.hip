@@ -578,11 +578,6 @@ int dispatch(SpmmArgs a, int mode, hipStream_t stream) {
         if ((a.drop_thresh & 0xFFu) == 0) return launch_mode<T, 8, 1, 0, true, 8>(a, mode, stream);
         return launch_mode<T, 8, 1, 0, true, 16>(a, mode, stream);
     }
-    if (nvec == 8) {                          // F = 64 bf16 (128-byte rows), regnn_tune key 5
-        if (g_tune_v8 == 1) return launch_mode<T, 8, 1, 0, true>(a, mode, stream);
-        if (g_tune_v8 == 2) return launch_mode<T, 4, 2, 0, true>(a, mode, stream);
-        if (g_tune_v8 == 3) return launch_mode<T, 16, 1, 0, false>(a, mode, stream);
-    }
     if (nvec <= 8) return launch_mode<T, 8, 1>(a, mode, stream);
     if (nvec == 16) return launch_f16v<T>(a, mode, stream);
     if (nvec <= 16) return launch_mode<T, 16, 1>(a, mode, stream);
@@ -953,7 +948,6 @@ int64_t g_tune_grid_cap = 0;
 int64_t g_tune_un = 0;
 int64_t g_tune_head = 0;
 int64_t g_tune_rowscale = 0;
-int64_t g_tune_v8 = 0;
 
 int resident_blocks(const void* kernel, size_t lds, int block) {
     struct Entry { const void* k; size_t lds; int block; int blocks; };
@@ -1007,11 +1001,6 @@ int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 4) {
         const int64_t old = g_tune_rowscale;
         g_tune_rowscale = value;
-        return old;
-    }
-    if (key == 5) {
-        const int64_t old = g_tune_v8;
-        g_tune_v8 = value;
         return old;
     }
     return -1;

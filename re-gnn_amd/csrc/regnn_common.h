@@ -146,8 +146,6 @@ extern int64_t g_tune_grid_cap;
 extern int64_t g_tune_un;        // rows in flight per lane for F = 16 vectors (0 = 8)
 extern int64_t g_tune_head;      // fused head variant: 0 = pipelined, 1 = plain
 extern int64_t g_tune_rowscale;  // rows in flight per lane group of regnn_row_scale (0 = 1)
-extern int64_t g_tune_v8;        // 8-vector rows (F=64 bf16): 0 = 8 lanes, 1 = 8 lanes unmasked,
-                                 // 2 = 4 lanes x 2 vectors, 3 = 16 lanes (half masked)
 
 int resident_blocks(const void* kernel, size_t lds, int block = kBlock);  // per CU x CUs, cached
 

@@ -2,7 +2,7 @@
 
     python tools/ab_spmm.py [--scale 10] [--rounds 5] [--F 64] [--dtype fp32]
 
-Variants cap:split:chunk[:un[:prescale[:rs[:v8]]]]: grid cap (regnn_tune key 1) x long-segment
+Variants cap:split:chunk[:un[:prescale[:rs]]]: grid cap (regnn_tune key 1) x long-segment
 split/chunk x rows in flight (key 2) x ops.PRESCALE mode (on/off/auto). Reports per variant the median
 ms of spmm_fwd / spmm_bwd (HIP events on the launch stream) and GB/s on SURVEY §8d bytes.
 """
@@ -44,22 +44,19 @@ def main():
         un = int(parts[3]) if len(parts) > 3 else 0
         pre = parts[4] if len(parts) > 4 else "auto"       # ops.PRESCALE mode
         rs = int(parts[5]) if len(parts) > 5 else 0        # regnn_row_scale rows in flight (key 4)
-        v8 = int(parts[6]) if len(parts) > 6 else 0        # 8-vector row layout (key 5)
         key = (int(split), int(chunk))
         if key not in graphs:
-            graphs[key] = RelGraph(gd["src"], gd["dst"], gd["N"], dev, split=key[0], chunk=key[1],
-                                   order="source")
-        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key], un, pre, rs, v8))
+            graphs[key] = RelGraph(gd["src"], gd["dst"], gd["N"], dev, split=key[0], chunk=key[1])
+        variants.append((v, 0 if cap == "res" else int(cap[3:]), graphs[key], un, pre, rs))
     E, N = graphs[next(iter(graphs))].E, gd["N"]
     F = args.F
     fwd_b = E * (F * s + 9) + N * (F * s + 8)
     bwd_b = E * (F * s + 9) + N * (3 * F * s + 12)
     res = {v[0]: {"fwd": [], "bwd": []} for v in variants}
     for r in range(args.rounds + 1):
-        for name, cap, rg, un, pre, rs, v8 in variants:
+        for name, cap, rg, un, pre, rs in variants:
             ops.PRESCALE["mode"] = ops.PRESCALE["bwd"] = pre
             L._so.regnn_tune(4, rs)
-            L._so.regnn_tune(5, v8)
             L._so.regnn_tune(1, cap)
             L._so.regnn_tune(2, un)
             pack = rg.rel_pack(e_feat, 11)
@@ -79,7 +76,6 @@ def main():
     L._so.regnn_tune(1, 0)
     L._so.regnn_tune(2, 0)
     L._so.regnn_tune(4, 0)
-    L._so.regnn_tune(5, 0)
     out = {}
     for name, d in res.items():
         f, b = statistics.median(d["fwd"]), statistics.median(d["bwd"])
