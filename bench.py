@@ -41,6 +41,10 @@ import torch.distributed as dist  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+# Measured ceiling of a gather of B-byte rows at uniformly random indices out of an 8 GiB table
+# (rows + 4-byte indices; tools/gather_probe.hip, profiles/r02_gather_probe.txt): the rate the
+# SpMM's row gathers can reach on this part, below the sequential 8 TB/s.
+GATHER_CEILING_GBS = {64: 2769.0, 128: 5106.0, 256: 5938.0, 512: 6008.0}
 METRIC = "aggregated edges/sec per GPU (REGCN fwd+bwd, hidden=64); % HBM roofline"
 
 
@@ -487,12 +491,23 @@ def run_full(args, dev, wl):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "achieved_hbm": hbm, "frac_hbm": None if hbm is None else hbm / HBM_PEAK_GBS,
             "pmc": pmc_status, "launch_ms": mean_ms, "launches": launches,
-            "algorithmic_bytes_per_launch": total_bytes / launches},
+            "algorithmic_bytes_per_launch": total_bytes / launches,
+            "gather_ceiling": _gather_ceiling(wl, args.dtype, hbm)},
         "kernels_ms": {k: round(v[1], 4) for k, v in kstats.items()},
     }
     del w
     torch.cuda.empty_cache()
     return out
+
+
+def _gather_ceiling(wl, dtype, hbm):
+    """The random row-gather ceiling for the SpMM's rows (hidden 64: 256 B fp32, 128 B bf16)."""
+    if wl not in ("mag", "dblp"):
+        return None
+    row = 64 * (2 if dtype == "bf16" else 4)
+    c = GATHER_CEILING_GBS[row]
+    return {"row_bytes": row, "GB/s": c, "source": "profiles/r02_gather_probe.txt",
+            "frac_hbm_of_ceiling": None if hbm is None else hbm / c}
 
 
 def build_ns_infer(args, dev):
