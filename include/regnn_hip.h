@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 20). */
+/* ABI version (bumped on any signature change or addition; currently 21). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -570,9 +570,10 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  *
  * Arithmetic (fp32 throughout): the group_input Linear and the first conv's weight are applied
  * as one composed map x @ (W_t^T W_0) + b_t W_0 (associativity; the gradients of W_t, b_t and W_0
- * follow by the chain rule). Dropout masks are this build's hash (regnn_spmm_fwd_dropout's spec)
- * keyed on s = mix64(state[0] ^ mix64((state[4] << 4) + layer + 0x51ED27)), row = target row of
- * the layer's block, 4 features per 16-byte vector. The sampled blocks' transposed aggregation
+ * follow by the chain rule), after layer 0's aggregation (linearity: the input rows are summed
+ * per target row and source type, then projected). Dropout masks are this build's hash
+ * (regnn_spmm_fwd_dropout's spec) keyed on s = mix64(state[0] ^ mix64((state[4] << 4) + layer +
+ * 0x51ED27)), row = target row of the layer's block, 4 features per 16-byte vector. The transposed aggregation of layers >= 1
  * uses float atomics (as regnn_ns_spmm_bwd); every other reduction is fixed-order.
  * --------------------------------------------------------------------------------------- */
 #define REGNN_NSM_MAX_TYPES 8
@@ -624,13 +625,18 @@ typedef struct regnn_nsm_work {
     float* wc;                /* T * (k_in + 1) * 64 floats: the composed first map */
     float* gwc;               /* same size: its gradient */
     float* tabs;              /* L * 64 floats */
-    float* xs[REGNN_NSM_MAX_LAYERS];    /* layer l's source rows: cap[L-l] rows */
-    float* gxs[REGNN_NSM_MAX_LAYERS];   /* their gradient: cap[L-l] rows */
+    float* xs[REGNN_NSM_MAX_LAYERS];    /* layer l >= 1's source rows: cap[L-l] rows ([0] unused) */
+    float* gxs[REGNN_NSM_MAX_LAYERS];   /* their gradient: cap[L-l] rows ([0] unused) */
     float* a[REGNN_NSM_MAX_LAYERS];     /* layer l < L-1: pre-LayerNorm rows, cap[L-1-l] rows */
     float* stats[REGNN_NSM_MAX_LAYERS]; /* layer l < L-1: (mean, rstd), 2 * cap[L-1-l] floats */
     float* ga[REGNN_NSM_MAX_LAYERS];    /* d loss / d pre-LN rows: cap[L-1-l] rows */
-    int32_t* row_type;        /* cap[L] int32: node type of each outermost source row */
-    int64_t* row_off;         /* cap[L] int64: its row in x_tab[type] */
+    /* layer 0 (target rows of hop L-1's block, cap[L-1] of them; E1 = that block's edge capacity) */
+    float* s_agg;             /* cap[L-1] * T * k_in: per-type weighted input sums of each row */
+    float* s_w;               /* cap[L-1] * T: per-type sums of the relation weights */
+    float* z;                 /* cap[L-1] * T * k_in: W_c[t] (inv ga) per row and type */
+    float* beta;              /* cap[L-1] * T */
+    int32_t* edge_type;       /* E1 int32: node type of each edge's source */
+    int64_t* edge_off;        /* E1 int64: its row in x_tab[type] */
     float* nvalid;            /* 1 float: labelled targets of the batch */
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
 } regnn_nsm_work;
@@ -641,7 +647,7 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0);
 
 /* One forward + loss + backward of the model over the current batch (after regnn_ns_batch and
  * the L regnn_ns_hop calls of the step): writes every g_* buffer (overwritten, not accumulated)
- * and *loss. 10 kernel launches for L = 2, none of them sized from the host. */
+ * and *loss. 8 kernel launches for L = 2 (L in [2, 4]), none of them sized from the host. */
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
 
 /* Adam step over flat buffers (replaces torch.optim.Adam.step, mag/regnn_ns.py:407, for

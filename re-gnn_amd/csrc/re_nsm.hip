@@ -1,25 +1,27 @@
 // Fused neighbour-sampled (NS) model step of the ogbn-mag path (regnn_nsm_step, regnn_hip.h):
 // the REGNN of mag/regnn_ns.py:216-346 ('regcn', self_loop_type 2, LayerNorm, hidden 64) with
-// its loss and backward over the blocks regnn_ns_hop wrote, as ten launches for two layers.
+// its loss and backward over the blocks regnn_ns_hop wrote, as eight launches for two layers.
 // Every kernel reads the batch's counts from `sizes` (device) and leaves rows past them alone,
 // so the whole step is one HIP-graph replay with no host synchronisation.
 //
 //   prep        W_c[t] = lins[t].weight^T convs[0].weight, b_c[t] = lins[t].bias convs[0].weight,
 //               relation tables LeakyReLU(alpha * rw_l)                (mag/regnn_layers.py:110)
-//   project     xs_0[i] = x_t[local(i)] W_c[t] + b_c[t] for the outermost hop's sources
-//               (group_input + the first x @ W: mag/regnn_ns.py:300-326, regnn_layers.py:102)
-//   agg         layer l < L-1: mean aggregation with the relation table + bias, LayerNorm, relu,
-//               dropout, then x @ W_{l+1} of the next layer                (regnn_layers.py:
-//               129-148, regnn_ns.py:341-343)
+//   agg0        layer 0 = group_input's per-type Linear + the first conv (mag/regnn_ns.py:300-326,
+//               regnn_layers.py:80-150): the input rows aggregated per source type, then
+//               projected per target row and type with the composed map; LayerNorm, relu,
+//               dropout, then x @ W_1 of the next layer
+//   agg         layers 1 .. L-2: mean aggregation with the relation table + bias, LayerNorm,
+//               relu, dropout, x @ W_{l+1}                   (regnn_layers.py:129-148, :341-343)
 //   head        layer L-1 as above, then out_lin, log_softmax, nll_loss (mean) and their
 //               backward down to the pre-LayerNorm rows                   (regnn_ns.py:345, 404)
-//   agg_bwd     transposed block aggregation (float atomics: a sampled block has no CSC) and
-//               the relation-table dots
+//   agg_bwd     layer l >= 1: transposed block aggregation (float atomics: a sampled block has
+//               no CSC) and the relation-table dots
 //   post_bwd    x @ W_{l+1} backward (its weight gradient per block), dropout / relu / LayerNorm
 //               backward of layer l
-//   project_bwd per-type x^T g of the composed first map
-//   finalize    fixed-order reductions of every per-row / per-block partial into the gradients;
-//               chain rule of the composed map onto lins[t] and convs[0].weight
+//   bwd0, rel0  layer 0: the composed map's gradient per target row and type, and the
+//               relation-table dots edge by edge (no source-row gradient, no atomics)
+//   finalize    fixed-order reductions of every per-row / per-block partial into the gradients
+//   chain       chain rule of the composed map onto lins[t] and convs[0].weight
 #include "regnn_common.h"
 
 namespace regnn {
@@ -109,7 +111,7 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
             const float* bb = pick(lin_b.p, t);
             for (int o = 0; o < F; ++o) s = fmaf(bb[o], w0[o * F + j], s);
         }
-        // wcT[t]: W_c[t]^T row-major [64][K], then b_c[t] [64] (project_kernel's LDS image)
+        // wcT[t]: W_c[t]^T row-major [64][K], then b_c[t] [64]
         float* o = wc + int64_t(t) * (K + 1) * F;
         if (k < K) o[int64_t(j) * K + k] = s;
         else o[int64_t(K) * F + j] = s;
@@ -127,117 +129,192 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// project: xs0[i] = x_t[local(n_id[i])] W_c[t] + b_c[t] on fp32 MFMA (v_mfma_f32_16x16x4_f32:
-// exact fp32 products, the precision of an fmaf chain). A block takes 256-row chunks of the
-// outermost hop's sources (grid-stride), writes their descriptors (type, table row) for
-// project_bwd, and per node type compacts the chunk's rows of that type (wave 0, in order) and
-// runs them in 16-row tiles against W_c[t]^T staged in LDS (row stride K + 8: conflict-free
-// ds_read_b128). Lane (c, q) of a tile: node c, k = k0 + 4q .. +3 per 16-k step; output
-// features 16 kt + 4q .. +3 of node c. Zeroes gxs0's rows for the transposed scatter.
+// agg0 (layer 0, L >= 2): aggregate first, then project. With xs0[u] = x_u W_c[t_u] + b_c[t_u]
+// (the composed first map of node type t_u), layer 0's mean aggregation regroups by source type:
+//   a_v = inv_v (sum_t S_vt W_c[t] + w_vt b_c[t]) + bias,  S_vt = sum_{e in v, t_u = t} tab[r_e] x_u,
+//   w_vt = sum_{e in v, t_u = t} tab[r_e],
+// so the input rows are gathered once per edge (K wide) and the projection runs per target row
+// and type (fp32 MFMA) instead of per source row. 16 target rows per block:
+//   gather  16 lanes per row (K/64 float4 each): every edge's (type, table row) from n_id /
+//           ntype / local, loaded by the row's lanes together and kept per edge for the
+//           backward; the weighted row added to its type's accumulator; S, w to LDS and HBM;
+//   project wave w -> output features 16w .. +15, D[v][j] += S_vt[k] W_c[t][k][j] over t and k
+//           (lane (c, q): A = S[c][16b + 4q + i] from LDS, B = W_c^T[16w + c][16b + 4q + i] from
+//           L2, 4 instructions per float4);
+//   epilogue as agg: LayerNorm, relu, dropout, then x @ W_1 of the next layer.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kPjChunk = 256;
 
-__device__ __forceinline__ int compact_rows(const int* types, int t, int* list) {
-    // wave 0: list = chunk positions whose type is t, ascending; returns the count
-    const int lane = threadIdx.x & 63;
-    int cnt = 0;
-#pragma unroll
-    for (int s0 = 0; s0 < kPjChunk; s0 += 64) {
-        const bool mine = types[s0 + lane] == t;
-        const uint64_t bal = __ballot(mine);
-        if (mine) list[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = s0 + lane;
-        cnt += __popcll(bal);
-    }
-    return cnt;
+struct Agg0Args {
+    const int32_t* sizes; int hop;
+    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const int32_t* n_id; const int32_t* ntype; const int64_t* local; Ptrs xt; int T;
+    const float* wc;                       // prep's W_c[t]^T [64][K] | b_c[t] [64] per type
+    const float* tab; const float* bias; const float* ln_w; const float* ln_b;
+    const int64_t* state; Drop drop;
+    const float* w_next;
+    float* s_agg; float* s_w; int32_t* edge_type; int64_t* edge_off;
+    float* a; float* stats; float* xs_next; float* gxs_next;
+};
+
+inline size_t agg0_lds(int T, int K) {
+    return (size_t(16) * (T * K + 4) + 16 * MT + 2 * 16 * F + F * F + F) * sizeof(float);
 }
 
 template <int K>
-__global__ void __launch_bounds__(kBlock)
-project_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes, int hop,
-               const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, int T,
-               Ptrs xt, const float* __restrict__ wct, float* __restrict__ xs,
-               float* __restrict__ gxs, int32_t* __restrict__ row_type,
-               int64_t* __restrict__ row_off) {
-    constexpr int S = K + 8;
-    __shared__ float WT[F * S + F];
-    __shared__ int types[kPjChunk];
-    __shared__ int64_t offs[kPjChunk];
-    __shared__ int list[kPjChunk];
-    __shared__ int s_cnt;
-    const int n = sizes[hop];
+__global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
+    constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
+    extern __shared__ float sm[];
+    const int T = A.T;
+    const int SR = T * K + 4;              // S tile row stride: rows 4 banks apart
+    float* St = sm;                        // [16][SR]
+    float* sw = St + 16 * SR;              // [16][MT]
+    float* at = sw + 16 * MT;              // [16][F] pre-LN rows
+    float* hrow = at + 16 * F;             // [16][F] dropped relu rows
+    float* Wn = hrow + 16 * F;             // [F][F] next layer's weight
+    float* tab = Wn + F * F;               // [F]
+    for (int i = threadIdx.x; i < F * F / 4; i += kBlock)
+        reinterpret_cast<float4*>(Wn)[i] = reinterpret_cast<const float4*>(A.w_next)[i];
+    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-    for (int c0 = blockIdx.x * kPjChunk; c0 < n; c0 += gridDim.x * kPjChunk) {
-        {
-            const int i = threadIdx.x;         // kPjChunk == kBlock: one row per thread
-            const int row = c0 + i;
-            int t = -1;
-            int64_t lo = 0;
-            if (row < n) {
-                const int g = n_id[row];
-                t = ntype[g];
-                lo = local[g];
-                row_type[row] = t;
-                row_off[row] = lo;
+    const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
+    const float4 bias = reinterpret_cast<const float4*>(A.bias)[l];
+    const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
+    for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
+        // ---- gather: S_vt, w_vt of row base + sub
+        const int v = base + sub;
+        float4 acc[MT][VPL];
+        float wsum[MT];
+#pragma unroll
+        for (int tt = 0; tt < MT; ++tt) {
+            wsum[tt] = 0.f;
+#pragma unroll
+            for (int p = 0; p < VPL; ++p) acc[tt][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (v < n) {
+            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            for (int c0 = e0; c0 < e1; c0 += 16) {
+                const int m = min(16, e1 - c0);
+                int my_t = 0;
+                int64_t my_lo = 0;
+                float my_w = 0.f;
+                if (l < m) {
+                    const int g = A.n_id[A.idx[c0 + l]];
+                    my_t = A.ntype[g];
+                    my_lo = A.local[g];
+                    my_w = tab[A.rel[c0 + l]];
+                    A.edge_type[c0 + l] = my_t;
+                    A.edge_off[c0 + l] = my_lo;
+                }
+                const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
+                for (int j = 0; j < m; ++j) {
+                    const int t = __shfl(my_t, gl + j, 64);
+                    const float wt = __shfl(my_w, gl + j, 64);
+                    const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + j, 64))) << 32) |
+                                               uint32_t(__shfl(lo_lo, gl + j, 64)));
+                    const float* xr = pick(A.xt.p, t) + lo * K + 4 * l;
+                    float4 x[VPL];
+#pragma unroll
+                    for (int p = 0; p < VPL; ++p) x[p] = *reinterpret_cast<const float4*>(xr + 64 * p);
+#pragma unroll
+                    for (int tt = 0; tt < MT; ++tt) {
+                        if (tt == t) {
+                            wsum[tt] += wt;
+#pragma unroll
+                            for (int p = 0; p < VPL; ++p) {
+                                acc[tt][p].x = fmaf(wt, x[p].x, acc[tt][p].x);
+                                acc[tt][p].y = fmaf(wt, x[p].y, acc[tt][p].y);
+                                acc[tt][p].z = fmaf(wt, x[p].z, acc[tt][p].z);
+                                acc[tt][p].w = fmaf(wt, x[p].w, acc[tt][p].w);
+                            }
+                        }
+                    }
+                }
             }
-            types[i] = t;
-            offs[i] = lo;
+        }
+#pragma unroll
+        for (int tt = 0; tt < MT; ++tt) {
+            if (tt < T) {
+#pragma unroll
+                for (int p = 0; p < VPL; ++p) {
+                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = acc[tt][p];
+                    if (v < n)
+                        *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l + 64 * p) =
+                            acc[tt][p];
+                }
+                if (l == 0) {
+                    sw[sub * MT + tt] = wsum[tt];
+                    if (v < n) A.s_w[int64_t(v) * T + tt] = wsum[tt];
+                }
+            }
         }
         __syncthreads();
-        for (int t = 0; t < T; ++t) {
-            if (threadIdx.x < 64) {
-                const int cnt = compact_rows(types, t, list);
-                if (threadIdx.x == 0) s_cnt = cnt;
+        // ---- project: D[v][j] = sum_t S_vt W_c[t]  (v = 4q + r, j = 16w + c)
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        for (int tt = 0; tt < T; ++tt) {
+            const float* wt = A.wc + int64_t(tt) * (K + 1) * F + (16 * w + c) * K + 4 * q;
+            const float* sa = St + c * SR + tt * K + 4 * q;
+#pragma unroll 4
+            for (int b = 0; b < K / 16; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                const float4 bv = *reinterpret_cast<const float4*>(wt + 16 * b);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, d, 0, 0, 0);
             }
-            const float* src = wct + int64_t(t) * (K + 1) * F;
-            for (int e = threadIdx.x; e < F * K / 4; e += kBlock) {
-                const int j = e / (K / 4), k4 = e - j * (K / 4);
-                *reinterpret_cast<float4*>(WT + j * S + 4 * k4) =
-                    reinterpret_cast<const float4*>(src)[e];
-            }
-            if (threadIdx.x < F) WT[F * S + threadIdx.x] = src[K * F + threadIdx.x];
-            __syncthreads();
-            const int cnt = s_cnt;
-            const float* X = pick(xt.p, t);
-            for (int tile = w; tile * 16 < cnt; tile += kBlock / 64) {
-                const int r = tile * 16 + c;
-                const bool valid = r < cnt;
-                const int li = valid ? list[r] : 0;
-                const float* xr = X + offs[li] * int64_t(K) + 4 * q;
-                float4 xv[K / 16];
-#pragma unroll
-                for (int s = 0; s < K / 16; ++s)
-                    xv[s] = valid ? *reinterpret_cast<const float4*>(xr + 16 * s)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-                f32x4 acc[4];
-#pragma unroll
-                for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[kt][i] = WT[F * S + 16 * kt + 4 * q + i];
-#pragma unroll
-                for (int s = 0; s < K / 16; ++s) {
-                    const float xs4[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
-#pragma unroll
-                    for (int kt = 0; kt < 4; ++kt) {
-                        const float4 a = *reinterpret_cast<const float4*>(WT + (16 * kt + c) * S + 16 * s + 4 * q);
-                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, xs4[0], acc[kt], 0, 0, 0);
-                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, xs4[1], acc[kt], 0, 0, 0);
-                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, xs4[2], acc[kt], 0, 0, 0);
-                        acc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, xs4[3], acc[kt], 0, 0, 0);
-                    }
-                }
-                if (valid) {
-                    const int64_t row = c0 + li;
-#pragma unroll
-                    for (int kt = 0; kt < 4; ++kt) {
-                        *reinterpret_cast<float4*>(xs + row * F + 16 * kt + 4 * q) =
-                            make_float4(acc[kt][0], acc[kt][1], acc[kt][2], acc[kt][3]);
-                        *reinterpret_cast<float4*>(gxs + row * F + 16 * kt + 4 * q) =
-                            make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-            }
-            __syncthreads();
         }
+        {
+            const int j = 16 * w + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int vr = 4 * q + r;
+                float bsum = 0.f;
+                for (int tt = 0; tt < T; ++tt)
+                    bsum = fmaf(sw[vr * MT + tt], A.wc[int64_t(tt) * (K + 1) * F + K * F + j], bsum);
+                const int vv = base + vr;
+                const float iv = vv < n ? A.inv[vv] : 0.f;
+                at[vr * F + j] = fmaf(iv, d[r] + bsum, A.bias[j]);
+            }
+        }
+        __syncthreads();
+        // ---- epilogue (agg_kernel's): LayerNorm, relu, dropout, x @ W_1
+        const bool act = v < n;
+        if (act) {
+            const float4 a4 = *reinterpret_cast<const float4*>(at + sub * F + 4 * l);
+            const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+            *reinterpret_cast<float4*>(A.a + int64_t(v) * F + 4 * l) = a4;
+            const float mean = group_sum<16>(a[0] + a[1] + a[2] + a[3]) * (1.f / F);
+            const float dd[4] = {a[0] - mean, a[1] - mean, a[2] - mean, a[3] - mean};
+            const float var = group_sum<16>(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2] + dd[3] * dd[3]) * (1.f / F);
+            const float rstd = rsqrtf(var + kLnEps);
+            if (l == 0) reinterpret_cast<float2*>(A.stats)[v] = make_float2(mean, rstd);
+            const float gws[4] = {gw.x, gw.y, gw.z, gw.w}, gbs[4] = {gb.x, gb.y, gb.z, gb.w};
+            float mk[4];
+            drop_factors(key, A.drop, v, l, mk);
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const float y = fmaf(dd[cc] * rstd, gws[cc], gbs[cc]);
+                hrow[sub * F + 4 * l + cc] = fmaxf(y, 0.f) * mk[cc];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < F; ++k) {
+                const float hk = hrow[sub * F + k];
+                const float4 wv = *reinterpret_cast<const float4*>(Wn + k * F + 4 * l);
+                o0 = fmaf(hk, wv.x, o0); o1 = fmaf(hk, wv.y, o1);
+                o2 = fmaf(hk, wv.z, o2); o3 = fmaf(hk, wv.w, o3);
+            }
+            *reinterpret_cast<float4*>(A.xs_next + int64_t(v) * F + 4 * l) = make_float4(o0, o1, o2, o3);
+            *reinterpret_cast<float4*>(A.gxs_next + int64_t(v) * F + 4 * l) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
     }
 }
 
@@ -668,99 +745,134 @@ __global__ void __launch_bounds__(kBlock) post_bwd_kernel(PostArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// project_bwd: block (b, t) accumulates gW_c[t] = sum over rows i of type t of x_i^T g_i (K x 64)
-// and gb_c[t] = sum g_i over its grid-stride share of 256-row chunks, on fp32 MFMA: D[k][j] with
-// A[k][row] = x[row][k], B[row][j] = g[row][j], 4 rows per instruction. Wave w owns k blocks
-// KB*w .. +KB-1 and all 4 j blocks. 16-row tiles staged in LDS; the next tile's rows are loaded
-// into registers before the current one is computed. Slab row: [K*64 | 64].
+// bwd0 (layer 0 backward, the GEMM half): with G_v = inv_v ga_v (ga = d loss / d a_0),
+//   gW_c[t] = sum_v S_vt^T G_v,   gb_c[t] = sum_v w_vt G_v,
+//   Z_vt = W_c[t] G_v (K wide),   beta_vt = <b_c[t], G_v>
+// where Z and beta turn the relation-table gradient into a per-edge dot (rel0). Block (b, t)
+// takes 16-row tiles (grid-stride), S and G staged in LDS with the next tile prefetched into
+// registers; W_c[t] in LDS k-major (row stride 68: conflict-free ds_read_b128).
+//   gW: D[k][j] (lane (c, q): k = 16 kb + c, 4 rows q per instruction), wave w owns k blocks
+//       KB*w .. +KB-1 and all 4 j blocks, as a per-block partial [K*64 | 64] in the slab;
+//   Z:  D[v][k] = sum_j G[v][j] W_c[t][k][j] (lane (c, q): A = G[c][16b + 4q + i] from a second
+//       copy of the tile at row stride 68, B = W_c[t][16 kb + c][16b + 4q + i]).
+struct Bwd0Args {
+    const int32_t* sizes; int hop; int T;
+    const float* inv; const float* ga; const float* s_agg; const float* s_w; const float* wc;
+    float* z; float* beta; float* slab;
+};
+
 template <int K>
-__global__ void __launch_bounds__(kBlock)
-project_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ row_type,
-                   const int64_t* __restrict__ row_off, Ptrs xt, const float* __restrict__ gxs,
-                   float* __restrict__ slab) {
-    constexpr int XS = K + 16, GS = F + 16;   // ds_read_b32 rows 16 banks apart
+__global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
+    constexpr int XS = K + 16, GS = F + 16, G2 = F + 4, WS = F + 4;
     constexpr int KB = K / 64;                // k blocks per wave
-    constexpr int XV = K / 4 * 16 / kBlock;   // x float4 per thread per tile (K=128: 2, 64: 1)
+    constexpr int XV = K / 4 * 16 / kBlock;   // S float4 per thread per tile (K=128: 2, 64: 1)
+    __shared__ float Wk[K * WS];
+    __shared__ float bc[F];
     __shared__ float xsh[16 * XS];
     __shared__ float gsh[16 * GS];
-    __shared__ int types[kPjChunk];
-    __shared__ int list[kPjChunk];
-    __shared__ int64_t offs[kPjChunk];
-    __shared__ int s_cnt;
-    const int t = blockIdx.y;
-    const float* X = pick(xt.p, t);
-    const int n = sizes[hop];
+    __shared__ float gs2[16 * G2];
+    __shared__ float sws[16];
+    const int t = blockIdx.y, T = A.T;
+    const float* wct = A.wc + int64_t(t) * (K + 1) * F;
+    for (int e = threadIdx.x; e < K * F; e += kBlock) {      // wcT[j][k] -> Wk[k][j]
+        const int j = e / K, k = e - j * K;
+        Wk[k * WS + j] = wct[e];
+    }
+    if (threadIdx.x < F) bc[threadIdx.x] = wct[K * F + threadIdx.x];
+    const int n = A.sizes[A.hop];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int gr = threadIdx.x >> 4, gj = threadIdx.x & 15;
     f32x4 acc[KB][4];
 #pragma unroll
     for (int a = 0; a < KB; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int jb = 0; jb < 4; ++jb) acc[a][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bsum = 0.f;
-    // tile loader mapping: x: float4 e = threadIdx.x + kBlock * v -> row e / (K/4), k4 e % (K/4);
-    // g: float4 threadIdx.x -> row threadIdx.x / 16, j4 threadIdx.x % 16
-    for (int c0 = blockIdx.x * kPjChunk; c0 < n; c0 += gridDim.x * kPjChunk) {
-        {
-            const int row = c0 + threadIdx.x;
-            types[threadIdx.x] = row < n ? row_type[row] : -1;
-            offs[threadIdx.x] = row < n ? row_off[row] : 0;
+    float4 sr[XV], gv;
+    float swv = 0.f;
+    auto load = [&](int v0) {
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            sr[u] = v0 + r < n ? *reinterpret_cast<const float4*>(
+                                     A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int v = v0 + gr;
+        if (v < n) {
+            const float iv = A.inv[v];
+            const float4 g4 = *reinterpret_cast<const float4*>(A.ga + int64_t(v) * F + 4 * gj);
+            gv = make_float4(iv * g4.x, iv * g4.y, iv * g4.z, iv * g4.w);
+        } else {
+            gv = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (threadIdx.x < 16) swv = v0 + threadIdx.x < n ? A.s_w[int64_t(v0 + threadIdx.x) * T + t] : 0.f;
+    };
+    int tile = blockIdx.x;
+    if (tile * 16 < n) load(tile * 16);
+    for (; tile * 16 < n; tile += gridDim.x) {
+        const int v0 = tile * 16;
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = sr[u];
+        }
+        *reinterpret_cast<float4*>(gsh + gr * GS + 4 * gj) = gv;
+        *reinterpret_cast<float4*>(gs2 + gr * G2 + 4 * gj) = gv;
+        if (threadIdx.x < 16) sws[threadIdx.x] = swv;
+        __syncthreads();
+        if ((tile + gridDim.x) * 16 < n) load((tile + gridDim.x) * 16);
+        if (threadIdx.x < F) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bsum = fmaf(sws[r], gsh[r * GS + threadIdx.x], bsum);
+        }
+        // gW partial
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            float bv[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+#pragma unroll
+            for (int a = 0; a < KB; ++a) {
+                const float av = xsh[r * XS + 16 * (KB * w + a) + c];
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
+            }
+        }
+        // Z rows of this tile: wave w -> k blocks KB*w .. +KB-1
+#pragma unroll
+        for (int a = 0; a < KB; ++a) {
+            const int kb = KB * w + a;
+            f32x4 zc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < F / 16; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
+                const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw.x, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw.y, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw.z, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw.w, zc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int v = v0 + 4 * q + r;
+                if (v < n) A.z[(int64_t(v) * T + t) * K + 16 * kb + c] = zc[r];
+            }
+        }
+        {                                      // beta_vt = <b_c[t], G_v>
+            const float4 g4 = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
+            float bt = bc[4 * gj] * g4.x + bc[4 * gj + 1] * g4.y + bc[4 * gj + 2] * g4.z +
+                       bc[4 * gj + 3] * g4.w;
+            bt = group_sum<16>(bt);
+            if (gj == 0 && v0 + gr < n) A.beta[int64_t(v0 + gr) * T + t] = bt;
         }
         __syncthreads();
-        if (threadIdx.x < 64) {
-            const int cnt = compact_rows(types, t, list);
-            if (threadIdx.x == 0) s_cnt = cnt;
-        }
-        __syncthreads();
-        const int cnt = s_cnt;
-        float4 xr[XV], gr;
-        auto load = [&](int tile) {
-#pragma unroll
-            for (int v = 0; v < XV; ++v) {
-                const int e = threadIdx.x + kBlock * v;
-                const int r = e / (K / 4), k4 = e - r * (K / 4);
-                const int li = tile * 16 + r;
-                xr[v] = li < cnt ? *reinterpret_cast<const float4*>(
-                                        X + offs[list[li]] * int64_t(K) + 4 * k4)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            const int r = threadIdx.x >> 4, j4 = threadIdx.x & 15;
-            const int li = tile * 16 + r;
-            gr = li < cnt ? *reinterpret_cast<const float4*>(gxs + int64_t(c0 + list[li]) * F + 4 * j4)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-        };
-        if (cnt > 0) load(0);
-        for (int tile = 0; tile * 16 < cnt; ++tile) {
-#pragma unroll
-            for (int v = 0; v < XV; ++v) {
-                const int e = threadIdx.x + kBlock * v;
-                const int r = e / (K / 4), k4 = e - r * (K / 4);
-                *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[v];
-            }
-            *reinterpret_cast<float4*>(gsh + (threadIdx.x >> 4) * GS + 4 * (threadIdx.x & 15)) = gr;
-            __syncthreads();
-            if ((tile + 1) * 16 < cnt) load(tile + 1);
-            if (threadIdx.x < F) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) bsum += gsh[r * GS + threadIdx.x];
-            }
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const int r = 4 * st + q;
-                float bv[4];
-#pragma unroll
-                for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
-#pragma unroll
-                for (int a = 0; a < KB; ++a) {
-                    const float av = xsh[r * XS + 16 * (KB * w + a) + c];
-#pragma unroll
-                    for (int jb = 0; jb < 4; ++jb)
-                        acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
-                }
-            }
-            __syncthreads();
-        }
     }
-    float* o = slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
+    float* o = A.slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
 #pragma unroll
     for (int a = 0; a < KB; ++a)
 #pragma unroll
@@ -769,6 +881,67 @@ project_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __
             for (int i = 0; i < 4; ++i)
                 o[(16 * (KB * w + a) + 4 * q + i) * F + 16 * jb + c] = acc[a][jb][i];
     if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
+}
+
+// rel0 (layer 0 backward, the edge half): d tab[r] = sum_{e: rel_e = r} inv_v <ga_v, xs0[u_e]>
+// = sum_e (<x_u, Z_{v,t_u}> + beta_{v,t_u}), the input row gathered again (agg0's per-edge type
+// and table row). 16 lanes per target row, lane-private relation bins -> one slab row per block.
+struct Rel0Args {
+    const int32_t* sizes; int hop; int T;
+    const int32_t* ptr; const uint8_t* rel; const int32_t* edge_type; const int64_t* edge_off;
+    Ptrs xt; const float* z; const float* beta; float* slab; int n_rel;
+};
+
+template <int K>
+__global__ void __launch_bounds__(kBlock) rel0_kernel(Rel0Args A) {
+    constexpr int VPL = K / 64;
+    extern __shared__ float bins[];        // [n_rel][kBlock]: a thread owns its column
+    for (int i = threadIdx.x; i < A.n_rel * kBlock; i += kBlock) bins[i] = 0.f;
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int T = A.T;
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
+    for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
+        const int v = base + sub;
+        if (v >= n) continue;
+        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        for (int c0 = e0; c0 < e1; c0 += 16) {
+            const int m = min(16, e1 - c0);
+            int my_t = 0, my_r = 0;
+            int64_t my_lo = 0;
+            if (l < m) {
+                my_t = A.edge_type[c0 + l];
+                my_lo = A.edge_off[c0 + l];
+                my_r = int(A.rel[c0 + l]);
+            }
+            const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
+            for (int j = 0; j < m; ++j) {
+                const int t = __shfl(my_t, gl + j, 64);
+                const int r = __shfl(my_r, gl + j, 64);
+                const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + j, 64))) << 32) |
+                                           uint32_t(__shfl(lo_lo, gl + j, 64)));
+                const float* xr = pick(A.xt.p, t) + lo * K + 4 * l;
+                const float* zr = A.z + (int64_t(v) * T + t) * K + 4 * l;
+                float dsum = l == 0 ? A.beta[int64_t(v) * T + t] : 0.f;
+#pragma unroll
+                for (int p = 0; p < VPL; ++p) {
+                    const float4 x = *reinterpret_cast<const float4*>(xr + 64 * p);
+                    const float4 zz = *reinterpret_cast<const float4*>(zr + 64 * p);
+                    dsum += x.x * zz.x + x.y * zz.y + x.z * zz.z + x.w * zz.w;
+                }
+                bins[r * kBlock + threadIdx.x] += dsum;
+            }
+        }
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
+    for (int r = w; r < A.n_rel; r += kBlock / 64) {
+        float s = bins[r * kBlock + f] + bins[r * kBlock + 64 + f] + bins[r * kBlock + 128 + f] +
+                  bins[r * kBlock + 192 + f];
+        s = wave_sum(s);
+        if (f == 0) A.slab[int64_t(blockIdx.x) * F + r] = s;
+    }
+    for (int r = A.n_rel + threadIdx.x; r < F; r += kBlock) A.slab[int64_t(blockIdx.x) * F + r] = 0.f;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -929,7 +1102,7 @@ struct SlabLayout {
 inline SlabLayout slab_layout(const regnn_nsm_params* p, int cap0) {
     SlabLayout s{};
     int64_t o = 0;
-    for (int l = 0; l < ML; ++l) {        // agg_bwd: relation dots of layer l
+    for (int l = 0; l < ML; ++l) {        // relation dots of layer l: rel0 (l = 0), agg_bwd
         s.rel[l] = o;
         if (l < p->n_layers) o += int64_t(kAggBlocks) * F;
     }
@@ -996,13 +1169,14 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     if (!p || !w) return REGNN_EINVAL;
     const int T = p->n_types, K = p->k_in, L = p->n_layers, C = p->n_classes;
-    if (T < 1 || T > MT || L < 1 || L > ML || C < 1 || C > 512 || (K != 64 && K != 128) ||
+    if (T < 1 || T > MT || L < 2 || L > ML || C < 1 || C > 512 || (K != 64 && K != 128) ||
         T * (K + 1) > 600 || !(p->p_drop >= 0.f && p->p_drop < 1.f))
         return REGNN_EUNSUPPORTED;
     for (int l = 0; l < L; ++l)
         if (p->n_rel[l] < 1 || p->n_rel[l] > F) return REGNN_EUNSUPPORTED;
     if (!w->state || !w->sizes || !w->n_id || !w->ntype || !w->local || !w->labels || !w->wc ||
-        !w->gwc || !w->tabs || !w->nvalid || !w->row_type || !w->row_off || !w->slab ||
+        !w->gwc || !w->tabs || !w->nvalid || !w->s_agg || !w->s_w || !w->z || !w->beta ||
+        !w->edge_type || !w->edge_off || !w->slab ||
         !p->loss || !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b || w->cap[0] <= 0)
         return REGNN_EINVAL;
     for (int t = 0; t < T; ++t)
@@ -1012,7 +1186,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         const int h = L - 1 - l;
         if (!p->conv_w[l] || !p->conv_b[l] || !p->conv_rw[l] || !p->ln_w[l] || !p->ln_b[l] ||
             !p->g_conv_w[l] || !p->g_conv_b[l] || !p->g_conv_rw[l] || !p->g_ln_w[l] ||
-            !p->g_ln_b[l] || !w->xs[l] || !w->gxs[l] || !w->ga[l] || !w->blk_ptr[h] ||
+            !p->g_ln_b[l] || (l > 0 && (!w->xs[l] || !w->gxs[l])) || !w->ga[l] || !w->blk_ptr[h] ||
             !w->blk_idx[h] || !w->blk_rel[h] || !w->blk_inv[h] || w->cap[h] <= 0 ||
             w->cap[h + 1] <= 0)
             return REGNN_EINVAL;
@@ -1034,22 +1208,35 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     hipLaunchKernelGGL(prep_kernel, dim3(T * (K + 1) + L), dim3(64), 0, stream, T, K, lin_w,
                        lin_b, p->conv_w[0], rw, L, nrel, p->alpha, w->wc, w->tabs);
     REGNN_LAUNCH_CHECK();
-    // 2. projection of the outermost hop's sources (hop L) -> layer 0's rows
+    // 2. layer 0: gather per source type, project per target row, LayerNorm ... x @ W_1
     {
-        int grid = (w->cap[L] + kPjChunk - 1) / kPjChunk;
-        if (grid > 1024) grid = 1024;
-        if (K == 128)
-            hipLaunchKernelGGL(project_kernel<128>, dim3(grid), dim3(kBlock), 0, stream, w->n_id,
-                               w->sizes, L, w->ntype, w->local, T, xt, w->wc, w->xs[0],
-                               w->gxs[0], w->row_type, w->row_off);
-        else
-            hipLaunchKernelGGL(project_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, w->n_id,
-                               w->sizes, L, w->ntype, w->local, T, xt, w->wc, w->xs[0],
-                               w->gxs[0], w->row_type, w->row_off);
+        const int h = L - 1;
+        Agg0Args A{};
+        A.sizes = w->sizes; A.hop = h;
+        A.ptr = w->blk_ptr[h]; A.idx = w->blk_idx[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.n_id = w->n_id; A.ntype = w->ntype; A.local = w->local; A.xt = xt; A.T = T; A.wc = w->wc;
+        A.tab = w->tabs; A.bias = p->conv_b[0]; A.ln_w = p->ln_w[0]; A.ln_b = p->ln_b[0];
+        A.state = w->state; A.drop = drop; A.w_next = p->conv_w[1];
+        A.s_agg = w->s_agg; A.s_w = w->s_w; A.edge_type = w->edge_type; A.edge_off = w->edge_off;
+        A.a = w->a[0]; A.stats = w->stats[0]; A.xs_next = w->xs[1]; A.gxs_next = w->gxs[1];
+        int grid = (w->cap[h] + 15) / 16;
+        if (grid > 2048) grid = 2048;
+        const size_t lds = agg0_lds(T, K);
+        if (K == 128) {
+            static size_t done = 0;
+            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<128>), lds, &done))
+                return REGNN_EUNSUPPORTED;
+            hipLaunchKernelGGL(agg0_kernel<128>, dim3(grid), dim3(kBlock), lds, stream, A);
+        } else {
+            static size_t done = 0;
+            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<64>), lds, &done))
+                return REGNN_EUNSUPPORTED;
+            hipLaunchKernelGGL(agg0_kernel<64>, dim3(grid), dim3(kBlock), lds, stream, A);
+        }
         REGNN_LAUNCH_CHECK();
     }
-    // 3. layers 0 .. L-2
-    for (int l = 0; l < L - 1; ++l) {
+    // 3. layers 1 .. L-2
+    for (int l = 1; l < L - 1; ++l) {
         const int h = L - 1 - l;
         AggArgs A{};
         A.sizes = w->sizes; A.hop = h;
@@ -1082,8 +1269,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kHeadRows * 64), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
-    // 5. backward, last layer first
-    for (int l = L - 1; l >= 0; --l) {
+    // 5. backward, last layer first, down to layer 0's pre-LN rows
+    for (int l = L - 1; l >= 1; --l) {
         const int h = L - 1 - l;
         AggBwdArgs B{};
         B.sizes = w->sizes; B.hop = h;
@@ -1093,7 +1280,6 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         hipLaunchKernelGGL(agg_bwd_kernel, dim3(kAggBlocks), dim3(kBlock),
                            size_t(p->n_rel[l]) * kBlock * sizeof(float), stream, B);
         REGNN_LAUNCH_CHECK();
-        if (l == 0) break;
         PostArgs Q{};
         const int lp = l - 1, hp = L - 1 - lp;
         Q.sizes = w->sizes; Q.hop = hp;
@@ -1104,16 +1290,30 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         hipLaunchKernelGGL(post_bwd_kernel, dim3(kPostBlocks), dim3(kBlock), 0, stream, Q);
         REGNN_LAUNCH_CHECK();
     }
-    // 6. composed first map: per-type x^T g partials
+    // 6. layer 0: the composed map's gradient and Z / beta per target row and type, then the
+    //    relation-table dots edge by edge
     {
+        const int h = L - 1;
+        Bwd0Args B{};
+        B.sizes = w->sizes; B.hop = h; B.T = T;
+        B.inv = w->blk_inv[h]; B.ga = w->ga[0]; B.s_agg = w->s_agg; B.s_w = w->s_w; B.wc = w->wc;
+        B.z = w->z; B.beta = w->beta; B.slab = w->slab + S.proj;
         const dim3 grid(kProjBlocks, T);
-        float* sl = w->slab + S.proj;
         if (K == 128)
-            hipLaunchKernelGGL(project_bwd_kernel<128>, grid, dim3(kBlock), 0, stream, w->sizes,
-                               L, w->row_type, w->row_off, xt, w->gxs[0], sl);
+            hipLaunchKernelGGL(bwd0_kernel<128>, grid, dim3(kBlock), 0, stream, B);
         else
-            hipLaunchKernelGGL(project_bwd_kernel<64>, grid, dim3(kBlock), 0, stream, w->sizes,
-                               L, w->row_type, w->row_off, xt, w->gxs[0], sl);
+            hipLaunchKernelGGL(bwd0_kernel<64>, grid, dim3(kBlock), 0, stream, B);
+        REGNN_LAUNCH_CHECK();
+        Rel0Args R{};
+        R.sizes = w->sizes; R.hop = h; R.T = T;
+        R.ptr = w->blk_ptr[h]; R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
+        R.edge_off = w->edge_off; R.xt = xt; R.z = w->z; R.beta = w->beta;
+        R.slab = w->slab + S.rel[0]; R.n_rel = p->n_rel[0];
+        const size_t lds = size_t(p->n_rel[0]) * kBlock * sizeof(float);
+        if (K == 128)
+            hipLaunchKernelGGL(rel0_kernel<128>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
+        else
+            hipLaunchKernelGGL(rel0_kernel<64>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
         REGNN_LAUNCH_CHECK();
     }
     // 7. reductions of every partial into the gradients (and the composed map's gradient)

@@ -191,22 +191,23 @@ class _NsmWork(ctypes.Structure):
                 ("blk_ptr", _P * _ML), ("blk_idx", _P * _ML), ("blk_rel", _P * _ML),
                 ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
-                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("row_type", _P),
-                ("row_off", _P), ("nvalid", _P), ("slab", _P)]
+                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("s_agg", _P),
+                ("s_w", _P), ("z", _P), ("beta", _P), ("edge_type", _P), ("edge_off", _P),
+                ("nvalid", _P), ("slab", _P)]
 
 
 def fused_unsupported(model, x_dict):
     """why regnn_nsm_step cannot run this model (None: it can). The fused step covers the
     reference configuration of mag/regnn_ns.py: model 'regcn', self_loop_type 2, use_norm 'ln',
     no residual, feats_type != 2, hidden 64, equal input widths 64 / 128, <= 8 node types,
-    <= 4 layers, <= 512 classes."""
+    2..4 layers, <= 512 classes."""
     if getattr(model, "model", None) != "regcn" or getattr(model, "feats_type", 3) == 2:
         return "model is not the feats_type-3 regcn"
     if model.self_loop_type != 2:
         return "self_loop_type != 2"
     convs = list(model.convs)
-    if not 1 <= len(convs) <= _ML:
-        return "1..4 layers"
+    if not 2 <= len(convs) <= _ML:
+        return "2..4 layers"
     for c in convs:
         if c.residual or c.use_norm != "ln" or tuple(c.weight.shape) != (64, 64):
             return "conv needs LayerNorm, no residual, hidden 64"
@@ -227,7 +228,7 @@ def fused_unsupported(model, x_dict):
 
 class FusedStep:
     """regnn_nsm_step over a DeviceSampler's blocks: the model's forward, nll loss and backward
-    in ten launches (two layers), gradients written straight into each parameter's .grad (the
+    in eight launches (two layers), gradients written straight into each parameter's .grad (the
     caller's flat bucket views), loss into `loss`. Keeps every buffer it points the library at."""
 
     def __init__(self, model, sampler, x_dict, node_type, local_node_idx, y_flat, loss):
@@ -289,12 +290,16 @@ class FusedStep:
         W.wc, W.gwc, W.tabs = ptr(z(T, K + 1, 64)), ptr(z(T, K + 1, 64)), ptr(z(nl, 64))
         for l in range(nl):
             n_src, n_dst = caps[nl - l], caps[nl - 1 - l]
-            W.xs[l], W.gxs[l] = ptr(z(n_src, 64)), ptr(z(n_src, 64))
+            if l > 0:                                  # layer 0 reads the input tables directly
+                W.xs[l], W.gxs[l] = ptr(z(n_src, 64)), ptr(z(n_src, 64))
             if l < nl - 1:
                 W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
             W.ga[l] = ptr(z(n_dst, 64))
-        W.row_type = ptr(torch.zeros(caps[nl], dtype=torch.int32, device=dev))
-        W.row_off = ptr(torch.zeros(caps[nl], dtype=torch.int64, device=dev))
+        n0, e0 = caps[nl - 1], sampler.blocks[nl - 1].csr_idx.numel()
+        W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
+        W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
+        W.edge_type = ptr(torch.zeros(e0, dtype=torch.int32, device=dev))
+        W.edge_off = ptr(torch.zeros(e0, dtype=torch.int64, device=dev))
         W.nvalid = ptr(z(1))
         W.slab = ptr(z(_slab_floats(P, caps[0])))
         self.model = model
