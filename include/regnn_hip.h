@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 21). */
+/* ABI version (bumped on any signature change or addition; currently 22). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -582,8 +582,8 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
 typedef struct regnn_nsm_params {
     int32_t n_types;          /* node types T (x_dict keys 0..T-1), <= 8 */
     int32_t k_in;             /* input feature width: 64 or 128, T * (k_in + 1) <= 600 */
-    int32_t n_layers;         /* L in [1, 4]; layer l reads hop L-1-l's block */
-    int32_t n_classes;        /* C <= 512 */
+    int32_t n_layers;         /* L in [2, 4]; layer l reads hop L-1-l's block */
+    int32_t n_classes;        /* C <= 448 */
     float alpha;              /* scaling_factor (mag/regnn_layers.py:110) */
     float p_drop;             /* dropout after each conv's relu (training), in [0, 1) */
     int32_t n_rel[REGNN_NSM_MAX_LAYERS];  /* len(relation_weight) per layer, <= 64 */
@@ -631,6 +631,7 @@ typedef struct regnn_nsm_work {
     float* stats[REGNN_NSM_MAX_LAYERS]; /* layer l < L-1: (mean, rstd), 2 * cap[L-1-l] floats */
     float* ga[REGNN_NSM_MAX_LAYERS];    /* d loss / d pre-LN rows: cap[L-1-l] rows */
     /* layer 0 (target rows of hop L-1's block, cap[L-1] of them; E1 = that block's edge capacity) */
+    const int32_t* gsrc;      /* hop L-1's regnn_ns_hop gsrc scratch: global source per edge */
     float* s_agg;             /* cap[L-1] * T * k_in: per-type weighted input sums of each row */
     float* s_w;               /* cap[L-1] * T: per-type sums of the relation weights */
     float* z;                 /* cap[L-1] * T * k_in: W_c[t] (inv ga) per row and type */

@@ -146,7 +146,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct Agg0Args {
     const int32_t* sizes; int hop;
-    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const int32_t* ptr; const int32_t* gsrc; const uint8_t* rel; const float* inv;
     const int32_t* n_id; const int32_t* ntype; const int64_t* local; Ptrs xt; int T;
     const float* wc;                       // prep's W_c[t]^T [64][K] | b_c[t] [64] per type
     const float* tab; const float* bias; const float* ln_w; const float* ln_b;
@@ -160,8 +160,8 @@ inline size_t agg0_lds(int T, int K) {
     return (size_t(16) * (T * K + 4) + 16 * MT + 2 * 16 * F + F * F + F) * sizeof(float);
 }
 
-template <int K>
-__global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
+template <int K, int NT>                   // NT: register accumulators per lane (T <= NT <= MT)
+__global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
     constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
     extern __shared__ float sm[];
     const int T = A.T;
@@ -184,25 +184,28 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
-        // ---- gather: S_vt, w_vt of row base + sub
+        // ---- gather: S_vt (accumulated in the row's LDS slots, each lane its own 4 * VPL of
+        // every type) and w_vt of row base + sub
         const int v = base + sub;
-        float4 acc[MT][VPL];
-        float wsum[MT];
+        float wsum[NT];
 #pragma unroll
-        for (int tt = 0; tt < MT; ++tt) {
-            wsum[tt] = 0.f;
+        for (int tt = 0; tt < NT; ++tt) wsum[tt] = 0.f;
+        for (int tt = 0; tt < T; ++tt)
 #pragma unroll
-            for (int p = 0; p < VPL; ++p) acc[tt][p] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+            for (int p = 0; p < VPL; ++p)
+                *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) =
+                    make_float4(0.f, 0.f, 0.f, 0.f);
         if (v < n) {
             const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            const int g_self = A.n_id[v];      // the self loop's source (gsrc -1)
             for (int c0 = e0; c0 < e1; c0 += 16) {
                 const int m = min(16, e1 - c0);
                 int my_t = 0;
                 int64_t my_lo = 0;
                 float my_w = 0.f;
                 if (l < m) {
-                    const int g = A.n_id[A.idx[c0 + l]];
+                    int g = A.gsrc[c0 + l];    // the sampled edge's global source
+                    if (g < 0) g = g_self;
                     my_t = A.ntype[g];
                     my_lo = A.local[g];
                     my_w = tab[A.rel[c0 + l]];
@@ -210,41 +213,52 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
                     A.edge_off[c0 + l] = my_lo;
                 }
                 const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
-                for (int j = 0; j < m; ++j) {
-                    const int t = __shfl(my_t, gl + j, 64);
-                    const float wt = __shfl(my_w, gl + j, 64);
-                    const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + j, 64))) << 32) |
-                                               uint32_t(__shfl(lo_lo, gl + j, 64)));
-                    const float* xr = pick(A.xt.p, t) + lo * K + 4 * l;
-                    float4 x[VPL];
+                // UN edges' rows in flight per lane, then their accumulation in edge order
+                constexpr int UN = 4;
+                for (int j = 0; j < m; j += UN) {
+                    int t[UN];
+                    float wt[UN];
+                    float4 x[UN][VPL];
 #pragma unroll
-                    for (int p = 0; p < VPL; ++p) x[p] = *reinterpret_cast<const float4*>(xr + 64 * p);
+                    for (int u = 0; u < UN; ++u) {
+                        const int jj = min(j + u, m - 1);
+                        t[u] = __shfl(my_t, gl + jj, 64);
+                        wt[u] = __shfl(my_w, gl + jj, 64);
+                        const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + jj, 64))) << 32) |
+                                                   uint32_t(__shfl(lo_lo, gl + jj, 64)));
+                        const float* xr = pick(A.xt.p, t[u]) + lo * K + 4 * l;
 #pragma unroll
-                    for (int tt = 0; tt < MT; ++tt) {
-                        if (tt == t) {
-                            wsum[tt] += wt;
+                        for (int p = 0; p < VPL; ++p) x[u][p] = *reinterpret_cast<const float4*>(xr + 64 * p);
+                        if (j + u >= m) t[u] = -1;     // padding: loaded (a valid row), not added
+                    }
 #pragma unroll
-                            for (int p = 0; p < VPL; ++p) {
-                                acc[tt][p].x = fmaf(wt, x[p].x, acc[tt][p].x);
-                                acc[tt][p].y = fmaf(wt, x[p].y, acc[tt][p].y);
-                                acc[tt][p].z = fmaf(wt, x[p].z, acc[tt][p].z);
-                                acc[tt][p].w = fmaf(wt, x[p].w, acc[tt][p].w);
-                            }
+                    for (int u = 0; u < UN; ++u) {
+                        if (t[u] < 0) continue;
+#pragma unroll
+                        for (int tt = 0; tt < NT; ++tt)
+                            if (tt == t[u]) wsum[tt] += wt[u];
+                        float* sp = St + sub * SR + t[u] * K + 4 * l;
+#pragma unroll
+                        for (int p = 0; p < VPL; ++p) {
+                            float4 a4 = *reinterpret_cast<float4*>(sp + 64 * p);
+                            a4.x = fmaf(wt[u], x[u][p].x, a4.x);
+                            a4.y = fmaf(wt[u], x[u][p].y, a4.y);
+                            a4.z = fmaf(wt[u], x[u][p].z, a4.z);
+                            a4.w = fmaf(wt[u], x[u][p].w, a4.w);
+                            *reinterpret_cast<float4*>(sp + 64 * p) = a4;
                         }
                     }
                 }
             }
         }
 #pragma unroll
-        for (int tt = 0; tt < MT; ++tt) {
+        for (int tt = 0; tt < NT; ++tt) {
             if (tt < T) {
+                if (v < n)
 #pragma unroll
-                for (int p = 0; p < VPL; ++p) {
-                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = acc[tt][p];
-                    if (v < n)
+                    for (int p = 0; p < VPL; ++p)
                         *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l + 64 * p) =
-                            acc[tt][p];
-                }
+                            *reinterpret_cast<const float4*>(St + sub * SR + tt * K + 4 * l + 64 * p);
                 if (l == 0) {
                     sw[sub * MT + tt] = wsum[tt];
                     if (v < n) A.s_w[int64_t(v) * T + tt] = wsum[tt];
@@ -434,11 +448,20 @@ __device__ __forceinline__ float lane_drop(uint32_t key, const Drop& d, int64_t 
 }
 
 // ---------------------------------------------------------------------------------------------
-// head: the last layer (wave per target row, lane = feature) + out_lin + log_softmax + nll +
-// backward down to the pre-LN rows (ga). out_lin.weight in LDS with rows padded to 65 floats.
-// The block's parameter-gradient partials go to one slab row (finalize sums them):
-//   [C*64: sum_r g[r][c] h[r][k] | C: sum_r g[r][c] | 64: sum_r ga | 64: sum_r gy |
-//    64: sum_r gy*xhat | 1: sum_r loss_r]
+// head: the last layer + out_lin + log_softmax + nll + backward down to the pre-LN rows (ga),
+// 16 target rows per block, the three products with out_lin.weight on fp32 MFMA:
+//   1. aggregation + LayerNorm + relu + dropout: 16 lanes per row (agg's layout) -> h [16][64];
+//   2. z = h W^T + b: class tiles of 16 split over the waves, D[v][c] (A = h[c'][16b + 4q + i],
+//      B = W[16 ct + c'][16b + 4q + i]);
+//   3. log_softmax, nll, g = (softmax - onehot) / n_valid per row (16 lanes per row);
+//   4. gh = g W: wave w -> features 16w .. +15, 4 classes per instruction;
+//   5. LayerNorm / relu / dropout backward -> ga; row sums of ga, gy, gy * xhat;
+//   6. out_lin.weight partial g^T h: D[c][k], class tiles split over the waves.
+// out_lin.weight staged in LDS once per block as [CT*16][64] with the float4 index XOR-swizzled
+// by the row (conflict-free ds_read_b128 along k and ds_read_b32 along c). The block's
+// parameter-gradient partials go to one slab row (finalize sums them):
+//   [C*64: sum_v g[v][c] h[v][k] | C: sum_v g[v][c] | 64: sum_v ga | 64: sum_v gy |
+//    64: sum_v gy*xhat | 1: sum_v loss_v]
 struct HeadArgs {
     const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
     const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
@@ -448,154 +471,220 @@ struct HeadArgs {
     float* ga; float* nvalid; float* part; int64_t part_w;
 };
 
-constexpr int kHeadRows = 8;           // waves (= rows) per block
+constexpr int kHeadRows = 16;          // target rows per block (one MFMA row tile)
 
 inline int64_t head_part_width(int C) { return ((int64_t(C) * (F + 1) + 3 * F + 1) + 3) & ~3ll; }
+__host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }   // z / g row stride: 4 banks apart
+inline size_t head_lds(int C) {
+    const int CT = (C + 15) / 16;
+    const size_t wl = size_t(CT) * 16 * F;                 // also the row-sum scratch (3*16*64)
+    return ((wl > size_t(3 * 16 * F) ? wl : size_t(3 * 16 * F)) + size_t(16) * head_cp(C) + 16 * 68 + 16 * 80 +
+            16 * 68) * sizeof(float);
+}
 
-__global__ void __launch_bounds__(kHeadRows * 64) head_kernel(HeadArgs A) {
-    extern __shared__ float hl[];      // [C][65] W_out | [R][F] h | [R][C] g | [3][R][F] ga,gy,gyx
-    const int C = A.C;
-    float* Wl = hl;
-    float* hs = Wl + C * kWPad;
-    float* gs = hs + kHeadRows * F;
-    float* rs = gs + kHeadRows * C;
+__device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c & 15) << 2)); }
+
+__global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
+    extern __shared__ float hl[];
+    const int C = A.C, CT = (C + 15) / 16, CP = head_cp(C);
+    float* Wl = hl;                                        // [CT*16][64] swizzled; later red
+    float* zs = Wl + max(CT * 16 * F, 3 * 16 * F);         // [16][CP]: z, then g
+    float* hs = zs + 16 * CP;                              // [16][68]: h (row reads)
+    float* hs2 = hs + 16 * 68;                             // [16][80]: h (column reads)
+    float* ghs = hs2 + 16 * 80;                            // [16][68]: gh
     __shared__ float tab[F];
     __shared__ float lrow[kHeadRows];
     __shared__ int s_valid;
-    for (int i = threadIdx.x; i < C * F; i += blockDim.x) {
-        const int c = i / F, k = i - c * F;
-        Wl[c * kWPad + k] = A.w_out[i];
+    for (int e4 = threadIdx.x; e4 < CT * 16 * (F / 4); e4 += kBlock) {
+        const int c = e4 >> 4, k4 = (e4 & 15) * 4;
+        const float4 wv = c < C ? *reinterpret_cast<const float4*>(A.w_out + int64_t(c) * F + k4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(Wl + head_sw(c, k4)) = wv;
     }
     if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
     const int n = A.sizes[0];
     if (threadIdx.x == 0) s_valid = 0;
     __syncthreads();
     int cnt = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+    for (int i = threadIdx.x; i < n; i += kBlock) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
     atomicAdd(&s_valid, cnt);              // integer count: order-independent
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
+    const int v = blockIdx.x * kHeadRows + sub;
+    const bool act = v < n;
+    // ---- 1. aggregation, LayerNorm, relu, dropout
+    const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
+    const float gwf[4] = {gw4.x, gw4.y, gw4.z, gw4.w}, gbf[4] = {gb4.x, gb4.y, gb4.z, gb4.w};
+    float xhat[4] = {0.f, 0.f, 0.f, 0.f}, mfac[4] = {0.f, 0.f, 0.f, 0.f}, rstd = 0.f;
+    float hv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (act) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        for (int c0 = e0; c0 < e1; c0 += 16) {
+            const int m = min(16, e1 - c0);
+            const int my_u = l < m ? A.idx[c0 + l] : 0;
+            const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
+            constexpr int UN = 4;
+            for (int j = 0; j < m; j += UN) {
+                float4 x[UN];
+                float wt[UN];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    const int jj = min(j + u, m - 1);
+                    const int uu = __shfl(my_u, gl + jj, 64);
+                    wt[u] = j + u < m ? tab[__shfl(my_r, gl + jj, 64)] : 0.f;
+                    x[u] = *reinterpret_cast<const float4*>(A.xs + int64_t(uu) * F + 4 * l);
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    if (j + u >= m) break;
+                    s0 = fmaf(wt[u], x[u].x, s0); s1 = fmaf(wt[u], x[u].y, s1);
+                    s2 = fmaf(wt[u], x[u].z, s2); s3 = fmaf(wt[u], x[u].w, s3);
+                }
+            }
+        }
+        const float iv = A.inv[v];
+        const float4 b4 = reinterpret_cast<const float4*>(A.bias)[l];
+        const float a[4] = {fmaf(iv, s0, b4.x), fmaf(iv, s1, b4.y), fmaf(iv, s2, b4.z),
+                            fmaf(iv, s3, b4.w)};
+        const float mean = group_sum<16>(a[0] + a[1] + a[2] + a[3]) * (1.f / F);
+        const float d[4] = {a[0] - mean, a[1] - mean, a[2] - mean, a[3] - mean};
+        rstd = rsqrtf(group_sum<16>(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) *
+                          (1.f / F) + kLnEps);
+        const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
+        drop_factors(key, A.drop, v, l, mfac);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xhat[i] = d[i] * rstd;
+            hv[i] = fmaxf(fmaf(xhat[i], gwf[i], gbf[i]), 0.f) * mfac[i];
+        }
+    }
+    *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     __syncthreads();
     const int n_valid = s_valid;
     if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
-    const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
-    const int v = blockIdx.x * kHeadRows + w;
-    float* hw = hs + w * F;
-    float* gw_ = gs + w * C;
-    if (v < n) {                           // wave-uniform
-        float s = 0.f;
-        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-        for (int c0 = e0; c0 < e1; c0 += 64) {       // edge ids loaded by the wave at once
-            const int m = min(64, e1 - c0);
-            const int my_u = f < m ? A.idx[c0 + f] : 0;
-            const int my_r = f < m ? int(A.rel[c0 + f]) : 0;
-            int j = 0;
-            for (; j + 4 <= m; j += 4) {
-                float x[4], wt[4];
+    // ---- 2. z = h W^T + b -> zs (classes >= C: -inf)
+    for (int ct = w; ct < CT; ct += kBlock / 64) {
+        const int c = 16 * ct + cc;
+        f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    x[q] = A.xs[int64_t(__builtin_amdgcn_readlane(my_u, j + q)) * F + f];
-                    wt[q] = tab[__builtin_amdgcn_readlane(my_r, j + q)];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) s = fmaf(wt[q], x[q], s);
-            }
-            for (; j < m; ++j)
-                s = fmaf(tab[__builtin_amdgcn_readlane(my_r, j)],
-                         A.xs[int64_t(__builtin_amdgcn_readlane(my_u, j)) * F + f], s);
+        for (int b = 0; b < F / 16; ++b) {
+            const float4 av = *reinterpret_cast<const float4*>(hs + cc * 68 + 16 * b + 4 * q);
+            const float4 bv = *reinterpret_cast<const float4*>(Wl + head_sw(c, 16 * b + 4 * q));
+            dz = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, dz, 0, 0, 0);
+            dz = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, dz, 0, 0, 0);
+            dz = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, dz, 0, 0, 0);
+            dz = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, dz, 0, 0, 0);
         }
-        const float a = fmaf(A.inv[v], s, A.bias[f]);
-        const float mean = wave_sum(a) * (1.f / F);
-        const float dlt = a - mean;
-        const float rstd = rsqrtf(wave_sum(dlt * dlt) * (1.f / F) + kLnEps);
-        const float xhat = dlt * rstd;
-        const float gw = A.ln_w[f], gb = A.ln_b[f];
-        const uint32_t key = A.drop.on ? layer_key(A.state, A.layer) : 0u;
-        const float mfac = lane_drop(key, A.drop, v, f);
-        const float h = fmaxf(fmaf(xhat, gw, gb), 0.f) * mfac;
-        hw[f] = h;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0xc07f);    // lgkmcnt(0): the wave's LDS writes are visible
-        constexpr int MC = 8;                  // up to 512 classes: 8 per lane
-        float z[MC];
+        const float bo = c < C ? A.b_out[c] : 0.f;
 #pragma unroll
-        for (int m = 0; m < MC; ++m) {
-            const int c = f + 64 * m;
-            z[m] = c < C ? A.b_out[c] : -INFINITY;
-        }
-        for (int k = 0; k < F; ++k) {
-            const float hk = hw[k];
-#pragma unroll
-            for (int m = 0; m < MC; ++m) {
-                const int c = f + 64 * m;
-                if (c < C) z[m] = fmaf(hk, Wl[c * kWPad + k], z[m]);
-            }
-        }
+        for (int r = 0; r < 4; ++r) zs[(4 * q + r) * CP + c] = c < C ? dz[r] + bo : -INFINITY;
+    }
+    __syncthreads();
+    // ---- 3. log_softmax, nll, g
+    {
         float zmax = -INFINITY;
+        for (int c = l; c < CT * 16; c += 16) zmax = fmaxf(zmax, zs[sub * CP + c]);
 #pragma unroll
-        for (int m = 0; m < MC; ++m) zmax = fmaxf(zmax, z[m]);
-        zmax = wave_max(zmax);
+        for (int o = 8; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
         float se = 0.f;
-#pragma unroll
-        for (int m = 0; m < MC; ++m)
-            if (f + 64 * m < C) se += expf(z[m] - zmax);
-        const float lse = zmax + logf(wave_sum(se));
-        const int64_t y = A.labels[A.n_id[v]];
-        float zy = 0.f;
-#pragma unroll
-        for (int m = 0; m < MC; ++m)
-            if (int64_t(f + 64 * m) == y) zy = z[m];
-        zy = wave_sum(zy);                     // exactly one lane holds it (or none: y < 0)
-        if (f == 0) lrow[w] = y >= 0 ? lse - zy : 0.f;
+        for (int c = l; c < C; c += 16) se += expf(zs[sub * CP + c] - zmax);
+        const float lse = zmax + logf(group_sum<16>(se));
+        const int64_t y = act ? A.labels[A.n_id[v]] : -1;
+        const float zy = y >= 0 ? zs[sub * CP + y] : 0.f;
+        if (l == 0) lrow[sub] = y >= 0 ? lse - zy : 0.f;
         const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
-#pragma unroll
-        for (int m = 0; m < MC; ++m) {
-            const int c = f + 64 * m;
-            if (c < C) gw_[c] = (expf(z[m] - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n;
+        for (int c = l; c < CT * 16; c += 16) {
+            const float z = zs[sub * CP + c];
+            zs[sub * CP + c] = act && c < C ? (expf(z - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        float gh = 0.f;
-        for (int c = 0; c < C; ++c) gh = fmaf(gw_[c], Wl[c * kWPad + f], gh);
-        float ga, gyv, gyx;
-        ln_relu_drop_bwd(gh, xhat, rstd, gw, gb, mfac, &ga, &gyv, &gyx);
-        A.ga[int64_t(v) * F + f] = ga;
-        rs[(0 * kHeadRows + w) * F + f] = ga;
-        rs[(1 * kHeadRows + w) * F + f] = gyv;
-        rs[(2 * kHeadRows + w) * F + f] = gyx;
-    } else {                               // rows past the batch contribute zeros
-        hw[f] = 0.f;
-        for (int c = f; c < C; c += 64) gw_[c] = 0.f;
-        rs[(0 * kHeadRows + w) * F + f] = 0.f;
-        rs[(1 * kHeadRows + w) * F + f] = 0.f;
-        rs[(2 * kHeadRows + w) * F + f] = 0.f;
-        if (f == 0) lrow[w] = 0.f;
+    }
+    __syncthreads();
+    // ---- 4. gh = g W: wave w -> features 16w + cc, rows 4q + r
+    {
+        f32x4 dg = {0.f, 0.f, 0.f, 0.f};
+        const int k = 16 * w + cc;
+        for (int b = 0; b < CT; ++b) {         // classes 16b + 4q + i, i = instruction
+            const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
+            const int c0 = 16 * b + 4 * q;
+            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, Wl[head_sw(c0 + 0, k)], dg, 0, 0, 0);
+            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, Wl[head_sw(c0 + 1, k)], dg, 0, 0, 0);
+            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, Wl[head_sw(c0 + 2, k)], dg, 0, 0, 0);
+            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, Wl[head_sw(c0 + 3, k)], dg, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg[r];
+    }
+    __syncthreads();
+    // ---- 5. LayerNorm / relu / dropout backward -> ga; per-feature row terms to red
+    float* red = Wl;                       // [3][16][64]: ga, gy, gy*xhat (W no longer needed)
+    {
+        const float4 g4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
+        const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+        float gy[4], gx[4];
+        float p1 = 0.f, p2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float y = fmaf(xhat[i], gwf[i], gbf[i]);
+            gy[i] = act && y > 0.f ? g[i] * mfac[i] : 0.f;
+            gx[i] = gy[i] * gwf[i];
+            p1 += gx[i];
+            p2 += gx[i] * xhat[i];
+        }
+        const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
+        float ga[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ga[i] = act ? rstd * (gx[i] - m1 - xhat[i] * m2) : 0.f;
+        if (act)
+            *reinterpret_cast<float4*>(A.ga + int64_t(v) * F + 4 * l) = make_float4(ga[0], ga[1], ga[2], ga[3]);
+        *reinterpret_cast<float4*>(red + (0 * 16 + sub) * F + 4 * l) = make_float4(ga[0], ga[1], ga[2], ga[3]);
+        *reinterpret_cast<float4*>(red + (1 * 16 + sub) * F + 4 * l) = make_float4(gy[0], gy[1], gy[2], gy[3]);
+        *reinterpret_cast<float4*>(red + (2 * 16 + sub) * F + 4 * l) =
+            make_float4(gy[0] * xhat[0], gy[1] * xhat[1], gy[2] * xhat[2], gy[3] * xhat[3]);
     }
     __syncthreads();
     float* o = A.part + int64_t(blockIdx.x) * A.part_w;
-    for (int e = threadIdx.x; e < C * F; e += blockDim.x) {      // out_lin.weight partial
-        const int c = e >> 6, k = e & 63;
-        float acc = 0.f;
+    // ---- 6. out_lin.weight partial: D[c][k] = sum_v g[v][c] h[v][k]
+    for (int ct = w; ct < CT; ct += kBlock / 64) {
+        f32x4 dw[4];
 #pragma unroll
-        for (int r = 0; r < kHeadRows; ++r) acc = fmaf(gs[r * C + c], hs[r * F + k], acc);
-        o[e] = acc;
+        for (int kb = 0; kb < 4; ++kb) dw[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            const float av = zs[r * CP + 16 * ct + cc];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+                dw[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, hs2[r * 80 + 16 * kb + cc], dw[kb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * ct + 4 * q + r;
+                if (c < C) o[int64_t(c) * F + 16 * kb + cc] = dw[kb][r];
+            }
     }
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {          // out_lin.bias partial
+    for (int c = threadIdx.x; c < C; c += kBlock) {           // out_lin.bias partial
         float acc = 0.f;
 #pragma unroll
-        for (int r = 0; r < kHeadRows; ++r) acc += gs[r * C + c];
-        o[C * F + c] = acc;
+        for (int r = 0; r < kHeadRows; ++r) acc += zs[r * CP + c];
+        o[int64_t(C) * F + c] = acc;
     }
-    if (threadIdx.x < 3 * F) {                                   // conv bias, LN beta, LN gamma
-        const int which = threadIdx.x >> 6;
+    if (threadIdx.x < 3 * F) {                                 // conv bias, LN beta, LN gamma
+        const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
         float acc = 0.f;
 #pragma unroll
-        for (int r = 0; r < kHeadRows; ++r) acc += rs[(which * kHeadRows + r) * F + f];
-        o[C * (F + 1) + threadIdx.x] = acc;
+        for (int r = 0; r < kHeadRows; ++r) acc += red[(which * 16 + r) * F + f];
+        o[int64_t(C) * (F + 1) + threadIdx.x] = acc;
     }
     if (threadIdx.x == 0) {
         float acc = 0.f;
 #pragma unroll
         for (int r = 0; r < kHeadRows; ++r) acc += lrow[r];
-        o[C * (F + 1) + 3 * F] = acc;
+        o[int64_t(C) * (F + 1) + 3 * F] = acc;
     }
 }
 
@@ -915,21 +1004,36 @@ __global__ void __launch_bounds__(kBlock) rel0_kernel(Rel0Args A) {
                 my_r = int(A.rel[c0 + l]);
             }
             const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
-            for (int j = 0; j < m; ++j) {
-                const int t = __shfl(my_t, gl + j, 64);
-                const int r = __shfl(my_r, gl + j, 64);
-                const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + j, 64))) << 32) |
-                                           uint32_t(__shfl(lo_lo, gl + j, 64)));
-                const float* xr = pick(A.xt.p, t) + lo * K + 4 * l;
-                const float* zr = A.z + (int64_t(v) * T + t) * K + 4 * l;
-                float dsum = l == 0 ? A.beta[int64_t(v) * T + t] : 0.f;
+            constexpr int UN = 4;                  // edges in flight per lane
+            for (int j = 0; j < m; j += UN) {
+                int r[UN];
+                float dsum[UN];
+                float4 x[UN][VPL], zz[UN][VPL];
 #pragma unroll
-                for (int p = 0; p < VPL; ++p) {
-                    const float4 x = *reinterpret_cast<const float4*>(xr + 64 * p);
-                    const float4 zz = *reinterpret_cast<const float4*>(zr + 64 * p);
-                    dsum += x.x * zz.x + x.y * zz.y + x.z * zz.z + x.w * zz.w;
+                for (int u = 0; u < UN; ++u) {
+                    const int jj = min(j + u, m - 1);
+                    const int t = __shfl(my_t, gl + jj, 64);
+                    r[u] = __shfl(my_r, gl + jj, 64);
+                    const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + jj, 64))) << 32) |
+                                               uint32_t(__shfl(lo_lo, gl + jj, 64)));
+                    const float* xr = pick(A.xt.p, t) + lo * K + 4 * l;
+                    const float* zr = A.z + (int64_t(v) * T + t) * K + 4 * l;
+                    dsum[u] = l == 0 ? A.beta[int64_t(v) * T + t] : 0.f;
+#pragma unroll
+                    for (int p = 0; p < VPL; ++p) {
+                        x[u][p] = *reinterpret_cast<const float4*>(xr + 64 * p);
+                        zz[u][p] = *reinterpret_cast<const float4*>(zr + 64 * p);
+                    }
                 }
-                bins[r * kBlock + threadIdx.x] += dsum;
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    if (j + u >= m) break;
+#pragma unroll
+                    for (int p = 0; p < VPL; ++p)
+                        dsum[u] += x[u][p].x * zz[u][p].x + x[u][p].y * zz[u][p].y +
+                                   x[u][p].z * zz[u][p].z + x[u][p].w * zz[u][p].w;
+                    bins[r[u] * kBlock + threadIdx.x] += dsum[u];
+                }
             }
         }
     }
@@ -1169,13 +1273,13 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     if (!p || !w) return REGNN_EINVAL;
     const int T = p->n_types, K = p->k_in, L = p->n_layers, C = p->n_classes;
-    if (T < 1 || T > MT || L < 2 || L > ML || C < 1 || C > 512 || (K != 64 && K != 128) ||
+    if (T < 1 || T > MT || L < 2 || L > ML || C < 1 || C > 448 || (K != 64 && K != 128) ||
         T * (K + 1) > 600 || !(p->p_drop >= 0.f && p->p_drop < 1.f))
         return REGNN_EUNSUPPORTED;
     for (int l = 0; l < L; ++l)
         if (p->n_rel[l] < 1 || p->n_rel[l] > F) return REGNN_EUNSUPPORTED;
     if (!w->state || !w->sizes || !w->n_id || !w->ntype || !w->local || !w->labels || !w->wc ||
-        !w->gwc || !w->tabs || !w->nvalid || !w->s_agg || !w->s_w || !w->z || !w->beta ||
+        !w->gwc || !w->tabs || !w->nvalid || !w->gsrc || !w->s_agg || !w->s_w || !w->z || !w->beta ||
         !w->edge_type || !w->edge_off || !w->slab ||
         !p->loss || !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b || w->cap[0] <= 0)
         return REGNN_EINVAL;
@@ -1213,7 +1317,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         const int h = L - 1;
         Agg0Args A{};
         A.sizes = w->sizes; A.hop = h;
-        A.ptr = w->blk_ptr[h]; A.idx = w->blk_idx[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.ptr = w->blk_ptr[h]; A.gsrc = w->gsrc; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
         A.n_id = w->n_id; A.ntype = w->ntype; A.local = w->local; A.xt = xt; A.T = T; A.wc = w->wc;
         A.tab = w->tabs; A.bias = p->conv_b[0]; A.ln_w = p->ln_w[0]; A.ln_b = p->ln_b[0];
         A.state = w->state; A.drop = drop; A.w_next = p->conv_w[1];
@@ -1222,18 +1326,17 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         int grid = (w->cap[h] + 15) / 16;
         if (grid > 2048) grid = 2048;
         const size_t lds = agg0_lds(T, K);
-        if (K == 128) {
-            static size_t done = 0;
-            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<128>), lds, &done))
-                return REGNN_EUNSUPPORTED;
-            hipLaunchKernelGGL(agg0_kernel<128>, dim3(grid), dim3(kBlock), lds, stream, A);
-        } else {
-            static size_t done = 0;
-            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<64>), lds, &done))
-                return REGNN_EUNSUPPORTED;
-            hipLaunchKernelGGL(agg0_kernel<64>, dim3(grid), dim3(kBlock), lds, stream, A);
-        }
-        REGNN_LAUNCH_CHECK();
+#define AGG0_CASE(KK, NN)                                                                      \
+        if (K == KK && (NN == MT || T <= NN)) {                                                \
+            static size_t done = 0;                                                            \
+            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<KK, NN>), lds, &done))     \
+                return REGNN_EUNSUPPORTED;                                                     \
+            hipLaunchKernelGGL((agg0_kernel<KK, NN>), dim3(grid), dim3(kBlock), lds, stream, A); \
+            REGNN_LAUNCH_CHECK();                                                              \
+        } else
+        AGG0_CASE(128, 4) AGG0_CASE(128, MT) AGG0_CASE(64, 4) AGG0_CASE(64, MT)
+            return REGNN_EUNSUPPORTED;
+#undef AGG0_CASE
     }
     // 3. layers 1 .. L-2
     for (int l = 1; l < L - 1; ++l) {
@@ -1261,12 +1364,11 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         H.ln_w = p->ln_w[l]; H.ln_b = p->ln_b[l]; H.state = w->state; H.layer = l; H.drop = drop;
         H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
         H.ga = w->ga[l]; H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
-        const size_t lds = (size_t(C) * kWPad + kHeadRows * F + size_t(kHeadRows) * C +
-                            3 * kHeadRows * F) * sizeof(float);
+        const size_t lds = head_lds(C);
         static size_t done = 0;
-        if (lds > 150 * 1024 || !set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
+        if (lds > 156 * 1024 || !set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
             return REGNN_EUNSUPPORTED;
-        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kHeadRows * 64), lds, stream, H);
+        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kBlock), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
     // 5. backward, last layer first, down to layer 0's pre-LN rows

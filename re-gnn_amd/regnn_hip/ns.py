@@ -191,7 +191,7 @@ class _NsmWork(ctypes.Structure):
                 ("blk_ptr", _P * _ML), ("blk_idx", _P * _ML), ("blk_rel", _P * _ML),
                 ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
-                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("s_agg", _P),
+                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("gsrc", _P), ("s_agg", _P),
                 ("s_w", _P), ("z", _P), ("beta", _P), ("edge_type", _P), ("edge_off", _P),
                 ("nvalid", _P), ("slab", _P)]
 
@@ -200,7 +200,7 @@ def fused_unsupported(model, x_dict):
     """why regnn_nsm_step cannot run this model (None: it can). The fused step covers the
     reference configuration of mag/regnn_ns.py: model 'regcn', self_loop_type 2, use_norm 'ln',
     no residual, feats_type != 2, hidden 64, equal input widths 64 / 128, <= 8 node types,
-    2..4 layers, <= 512 classes."""
+    2..4 layers, <= 448 classes."""
     if getattr(model, "model", None) != "regcn" or getattr(model, "feats_type", 3) == 2:
         return "model is not the feats_type-3 regcn"
     if model.self_loop_type != 2:
@@ -221,8 +221,8 @@ def fused_unsupported(model, x_dict):
         return "input widths must be equal, 64 or 128"
     if any(x_dict[k].dtype != torch.float32 or not x_dict[k].is_contiguous() for k in keys):
         return "inputs must be contiguous fp32"
-    if model.out_lin.weight.shape[0] > 512 or model.out_lin.weight.shape[1] != 64:
-        return "out_lin must be 64 -> <= 512"
+    if model.out_lin.weight.shape[0] > 448 or model.out_lin.weight.shape[1] != 64:
+        return "out_lin must be 64 -> <= 448"
     return None
 
 
@@ -296,6 +296,7 @@ class FusedStep:
                 W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
             W.ga[l] = ptr(z(n_dst, 64))
         n0, e0 = caps[nl - 1], sampler.blocks[nl - 1].csr_idx.numel()
+        W.gsrc = ptr(sampler.hop_bufs[nl - 1]["gsrc"])
         W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
         W.edge_type = ptr(torch.zeros(e0, dtype=torch.int32, device=dev))
