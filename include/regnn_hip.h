@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 22). */
+/* ABI version (bumped on any signature change or addition; currently 24). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -527,23 +527,29 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
 /* Step prologue: rank r of `world` takes global batch g = (r + state[2] * world) mod nb of the
  * epoch permutation perm [n_perm] (nb = ceil(n_perm / batch); every rank runs the same number of
  * steps, a rank past the end wraps), writes its targets to n_id[0, cnt) and sizes[0] = cnt,
- * state[3] = g, and advances state[2] and state[4]. */
+ * state[3] = g, and advances state[2] and the dedup stamp state[4] (by one, or, with stamp_src
+ * non-null, to ++*stamp_src: one int64 counter shared by samplers that use the same dedup
+ * tables one after another, so their stamps stay increasing). */
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
                    int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,
-                   hipStream_t stream);
+                   int64_t* stamp_src, hipStream_t stream);
 
 /* One sampling hop (replaces torch_sparse sample_adj for one layer of PyG NeighborSampler,
  * mag/regnn_ns.py:206-214): targets n_id[0, sizes[hop]) of the global CSR (ptr, idx; etype =
  * 0-based edge type per CSR position, ntype = node type per node), fan-out k in [1, 64], seed
  * hop_seed(state[0], state[1], state[3], hop). Writes the block (above), appends the new nodes,
- * sets sizes[hop + 1] and sizes[8 + hop], adds the block's edges to state[5]. */
+ * sets sizes[hop + 1] and sizes[8 + hop], adds the block's edges to state[5]. Optional (all
+ * three or none): with local = the per-node row in its type's table (mag local_node_idx), also
+ * writes each block edge's source node type edge_type [cap_e] int32 and table row edge_off
+ * [cap_e] int64 (what the fused step's layer 0 gathers by). */
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
-                 float* inv, hipStream_t stream);
+                 float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
+                 hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -572,8 +578,9 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  * as one composed map x @ (W_t^T W_0) + b_t W_0 (associativity; the gradients of W_t, b_t and W_0
  * follow by the chain rule), after layer 0's aggregation (linearity: the input rows are summed
  * per target row and source type, then projected). Dropout masks are this build's hash
- * (regnn_spmm_fwd_dropout's spec) keyed on s = mix64(state[0] ^ mix64((state[4] << 4) + layer +
- * 0x51ED27)), row = target row of the layer's block, 4 features per 16-byte vector. The transposed aggregation of layers >= 1
+ * (regnn_spmm_fwd_dropout's spec) keyed on s = mix64(state[0] ^ mix64((state[1] << 40) ^
+ * (state[3] << 8) ^ (layer + 0x51ED27))) (seed, epoch, global batch), row = target row of the
+ * layer's block, 4 features per 16-byte vector. The transposed aggregation of layers >= 1
  * uses float atomics (as regnn_ns_spmm_bwd); every other reduction is fixed-order.
  * --------------------------------------------------------------------------------------- */
 #define REGNN_NSM_MAX_TYPES 8
@@ -631,13 +638,12 @@ typedef struct regnn_nsm_work {
     float* stats[REGNN_NSM_MAX_LAYERS]; /* layer l < L-1: (mean, rstd), 2 * cap[L-1-l] floats */
     float* ga[REGNN_NSM_MAX_LAYERS];    /* d loss / d pre-LN rows: cap[L-1-l] rows */
     /* layer 0 (target rows of hop L-1's block, cap[L-1] of them; E1 = that block's edge capacity) */
-    const int32_t* gsrc;      /* hop L-1's regnn_ns_hop gsrc scratch: global source per edge */
+    const int32_t* edge_type; /* E1: regnn_ns_hop's edge_type output for hop L-1 */
+    const int64_t* edge_off;  /* E1: its edge_off output */
     float* s_agg;             /* cap[L-1] * T * k_in: per-type weighted input sums of each row */
     float* s_w;               /* cap[L-1] * T: per-type sums of the relation weights */
     float* z;                 /* cap[L-1] * T * k_in: W_c[t] (inv ga) per row and type */
     float* beta;              /* cap[L-1] * T */
-    int32_t* edge_type;       /* E1 int32: node type of each edge's source */
-    int64_t* edge_off;        /* E1 int64: its row in x_tab[type] */
     float* nvalid;            /* 1 float: labelled targets of the batch */
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
 } regnn_nsm_work;

@@ -85,7 +85,7 @@ __device__ __forceinline__ int block_exscan(int v, int* lds, int* total) {
 __global__ void __launch_bounds__(kBlock)
 ns_batch_kernel(const int64_t* __restrict__ perm, int64_t n_perm, int B, int rank, int world,
                 int64_t* __restrict__ state, int32_t* __restrict__ n_id,
-                int32_t* __restrict__ sizes) {
+                int32_t* __restrict__ sizes, int64_t* __restrict__ stamp_src) {
     __shared__ int64_t s_start, s_cnt;
     if (threadIdx.x == 0) {
         const int64_t nb = (n_perm + B - 1) / B;
@@ -100,7 +100,13 @@ ns_batch_kernel(const int64_t* __restrict__ perm, int64_t n_perm, int B, int ran
         s_cnt = cnt;
         state[3] = g;
         state[2] = j + 1;
-        state[4] = state[4] + 1;
+        if (stamp_src) {                   // a counter shared by several samplers of one table
+            const int64_t st = stamp_src[0] + 1;
+            stamp_src[0] = st;
+            state[4] = st;
+        } else {
+            state[4] = state[4] + 1;
+        }
         sizes[0] = int32_t(cnt);
     }
     __syncthreads();
@@ -176,25 +182,30 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                int hop, int cap, int64_t* __restrict__ state, int32_t* __restrict__ blk_ptr,
                int32_t* __restrict__ blk_idx, uint8_t* __restrict__ blk_rel,
                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv,
-               uint64_t* __restrict__ status) {
+               uint64_t* __restrict__ status, const int64_t* __restrict__ local,
+               int32_t* __restrict__ e_type, int64_t* __restrict__ e_off) {
     __shared__ int lds[kBlock / 64 + 1];
     __shared__ int s_prefix;
     const int n = sizes[hop];
     const uint32_t stamp = ns_stamp(state, hop);
     const int tile = blockIdx.x;
     const int i0 = tile * kNsRowsTile + threadIdx.x * kNsRowsIT;
-    int vals[kNsRowsIT], rels[kNsRowsIT];
+    int vals[kNsRowsIT], rels[kNsRowsIT], gids[kNsRowsIT];
+    int64_t offs[kNsRowsIT];
     int s = 0;
 #pragma unroll
     for (int j = 0; j < kNsRowsIT; ++j) {
         const int i = i0 + j;
         const bool live = i < cap && i < n;
         vals[j] = live ? scnt[i] + 1 : 0;
-        rels[j] = live ? n_id[i] : 0;
+        gids[j] = live ? n_id[i] : 0;
         s += vals[j];
     }
 #pragma unroll
-    for (int j = 0; j < kNsRowsIT; ++j) rels[j] = vals[j] ? ntype[rels[j]] + num_edge_types : 0;
+    for (int j = 0; j < kNsRowsIT; ++j) {
+        rels[j] = vals[j] ? ntype[gids[j]] : 0;
+        offs[j] = vals[j] && local ? local[gids[j]] : 0;
+    }
     int total;
     const int ex = block_exscan<kBlock>(s, lds, &total);
     if (threadIdx.x == 0) {
@@ -228,10 +239,14 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
             if (i < n) {
                 const int lp = off + vals[j] - 1;      // the self loop closes the row
                 blk_idx[lp] = i;
-                blk_rel[lp] = uint8_t(rels[j]);
+                blk_rel[lp] = uint8_t(rels[j] + num_edge_types);
                 blk_pos[lp] = -1;
                 gsrc[lp] = -1;
                 inv[i] = 1.f / float(vals[j]);
+                if (e_type) {
+                    e_type[lp] = rels[j];
+                    e_off[lp] = offs[j];
+                }
             } else {
                 inv[i] = 1.f;
             }
@@ -354,14 +369,22 @@ ns_finish_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ s
     }
 }
 
-// every sampled edge's local source id
+// every sampled edge's local source id (and, when asked, its source's node type and row in
+// that type's table, read beside the dedup table)
 __global__ void __launch_bounds__(kBlock)
 ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes, int hop,
-                  const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx, int cap_e) {
+                  const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx, int cap_e,
+                  const int32_t* __restrict__ ntype, const int64_t* __restrict__ local,
+                  int32_t* __restrict__ e_type, int64_t* __restrict__ e_off) {
     const int bp = blockIdx.x * kBlock + threadIdx.x;
     if (bp >= cap_e || bp >= sizes[8 + hop]) return;
     const int u = gsrc[bp];
-    if (u >= 0) blk_idx[bp] = int32_t(uint32_t(g2l[u]));
+    if (u < 0) return;
+    blk_idx[bp] = int32_t(uint32_t(g2l[u]));
+    if (e_type) {
+        e_type[bp] = ntype[u];
+        e_off[bp] = local[u];
+    }
 }
 
 // Backward of the sampled block's mean aggregation y[v] = s[v] sum_e tab[rel_e] x[idx_e] + b
@@ -421,12 +444,12 @@ extern "C" {
 
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
                    int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,
-                   hipStream_t stream) {
+                   int64_t* stamp_src, hipStream_t stream) {
     if (!perm || !state || !n_id || !sizes || n_perm < 0 || batch <= 0 || world <= 0 ||
         rank < 0 || rank >= world)
         return REGNN_EINVAL;
     hipLaunchKernelGGL(ns_batch_kernel, dim3(1), dim3(kBlock), 0, stream, perm, n_perm, batch,
-                       rank, world, state, n_id, sizes);
+                       rank, world, state, n_id, sizes, stamp_src);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
@@ -437,11 +460,13 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
-                 float* inv, hipStream_t stream) {
+                 float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
+                 hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
         return REGNN_EINVAL;
+    if (!!local != !!edge_type || !!local != !!edge_off) return REGNN_EINVAL;
     if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
     const int64_t cap_e = int64_t(cap_dst) * (k + 1);
     if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
@@ -451,7 +476,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_rows_kernel, dim3((cap_dst + kNsRowsTile - 1) / kNsRowsTile),
                        dim3(kBlock), 0, stream, scnt, n_id, ntype, num_edge_types, sizes, hop,
-                       cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, gsrc, inv, status);
+                       cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, gsrc, inv, status, local,
+                       edge_type, edge_off);
     REGNN_LAUNCH_CHECK();
     const int64_t slots = int64_t(cap_dst) * k;
     hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),
@@ -465,7 +491,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                        state, flag, tiles, g2l, n_id);
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, int(cap_e));
+                       dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, int(cap_e), ntype, local,
+                       edge_type, edge_off);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

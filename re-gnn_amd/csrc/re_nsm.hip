@@ -62,10 +62,12 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     return x;
 }
 
-// dropout key of layer `layer` for the current step (spec in regnn_hip.h)
+// dropout key of layer `layer` for the current batch (spec in regnn_hip.h): the seed, the epoch
+// and the global batch, so a batch draws the same masks whichever sampler slot produced it
 __device__ __forceinline__ uint32_t layer_key(const int64_t* state, int layer) {
-    const uint64_t s =
-        mix64(uint64_t(state[0]) ^ mix64((uint64_t(state[4]) << 4) + uint64_t(layer) + 0x51ED27ull));
+    const uint64_t s = mix64(uint64_t(state[0]) ^
+                             mix64((uint64_t(state[1]) << 40) ^ (uint64_t(state[3]) << 8) ^
+                                   (uint64_t(layer) + 0x51ED27ull)));
     return fmix32(uint32_t(s) ^ fmix32(uint32_t(s >> 32) ^ 0x5BD1E995u));
 }
 
@@ -135,57 +137,72 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
 //   w_vt = sum_{e in v, t_u = t} tab[r_e],
 // so the input rows are gathered once per edge (K wide) and the projection runs per target row
 // and type (fp32 MFMA) instead of per source row. 16 target rows per block:
-//   gather  16 lanes per row (K/64 float4 each): every edge's (type, table row) from n_id /
-//           ntype / local, loaded by the row's lanes together and kept per edge for the
-//           backward; the weighted row added to its type's accumulator; S, w to LDS and HBM;
+//   gather  16 lanes per row (K/64 float4 each): every edge's (type, table row) as the sampler
+//           wrote them, loaded by the row's lanes together; the weighted row added to its
+//           type's slot of the row in LDS; S, w to HBM for the backward;
 //   project wave w -> output features 16w .. +15, D[v][j] += S_vt[k] W_c[t][k][j] over t and k
 //           (lane (c, q): A = S[c][16b + 4q + i] from LDS, B = W_c^T[16w + c][16b + 4q + i] from
-//           L2, 4 instructions per float4);
+//           L2, the next type's columns loaded during this type's products);
 //   epilogue as agg: LayerNorm, relu, dropout, then x @ W_1 of the next layer.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct Agg0Args {
     const int32_t* sizes; int hop;
-    const int32_t* ptr; const int32_t* gsrc; const uint8_t* rel; const float* inv;
-    const int32_t* n_id; const int32_t* ntype; const int64_t* local; Ptrs xt; int T;
+    const int32_t* ptr; const uint8_t* rel; const float* inv;
+    const int32_t* edge_type; const int64_t* edge_off; Ptrs xt; int T;
     const float* wc;                       // prep's W_c[t]^T [64][K] | b_c[t] [64] per type
     const float* tab; const float* bias; const float* ln_w; const float* ln_b;
     const int64_t* state; Drop drop;
     const float* w_next;
-    float* s_agg; float* s_w; int32_t* edge_type; int64_t* edge_off;
+    const int32_t* n_id; const int64_t* labels; float* nvalid;
+    float* s_agg; float* s_w;
     float* a; float* stats; float* xs_next; float* gxs_next;
 };
 
+// LDS: S tile [16][T*K + 4] (after the projection: W_1 [64][64] and the h rows [16][64]) |
+// s_w [16][MT] | pre-LN rows [16][64] | relation table [64]
 inline size_t agg0_lds(int T, int K) {
-    return (size_t(16) * (T * K + 4) + 16 * MT + 2 * 16 * F + F * F + F) * sizeof(float);
+    const size_t st = size_t(16) * (T * K + 4);
+    return ((st > size_t(F * F + 16 * F) ? st : size_t(F * F + 16 * F)) + 16 * MT + 16 * F + F) *
+           sizeof(float);
 }
 
-template <int K, int NT>                   // NT: register accumulators per lane (T <= NT <= MT)
-__global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
+template <int K, int NT>                   // NT: register slots of w_vt per lane (T <= NT <= MT)
+__global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
+    constexpr int KB = K / 16;             // float4 steps of the projection per type
     extern __shared__ float sm[];
     const int T = A.T;
     const int SR = T * K + 4;              // S tile row stride: rows 4 banks apart
     float* St = sm;                        // [16][SR]
-    float* sw = St + 16 * SR;              // [16][MT]
+    float* Wn = sm;                        // after the projection: [F][F]
+    float* hrow = sm + F * F;              //                        [16][F]
+    const int st_floats = max(16 * SR, F * F + 16 * F);
+    float* sw = sm + st_floats;            // [16][MT]
     float* at = sw + 16 * MT;              // [16][F] pre-LN rows
-    float* hrow = at + 16 * F;             // [16][F] dropped relu rows
-    float* Wn = hrow + 16 * F;             // [F][F] next layer's weight
-    float* tab = Wn + F * F;               // [F]
-    for (int i = threadIdx.x; i < F * F / 4; i += kBlock)
-        reinterpret_cast<float4*>(Wn)[i] = reinterpret_cast<const float4*>(A.w_next)[i];
+    float* tab = at + 16 * F;              // [F]
     if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
-    __syncthreads();
     const int n = A.sizes[A.hop];
+    if (blockIdx.x == 0) {                 // the labelled-target count the head divides by
+        __shared__ int s_valid;
+        if (threadIdx.x == 0) s_valid = 0;
+        __syncthreads();
+        const int n0 = A.sizes[0];
+        int cnt = 0;
+        for (int i = threadIdx.x; i < n0; i += kBlock) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+        atomicAdd(&s_valid, cnt);          // integer count: order-independent
+        __syncthreads();
+        if (threadIdx.x == 0) *A.nvalid = float(s_valid);
+    }
+    __syncthreads();
     const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
     const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
-    const float4 bias = reinterpret_cast<const float4*>(A.bias)[l];
     const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
-        // ---- gather: S_vt (accumulated in the row's LDS slots, each lane its own 4 * VPL of
-        // every type) and w_vt of row base + sub
+        // ---- gather: S_vt accumulated in the row's LDS slots (each lane its own 4 * VPL
+        // features of every type), w_vt in registers
         const int v = base + sub;
         float wsum[NT];
 #pragma unroll
@@ -197,22 +214,15 @@ __global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
                     make_float4(0.f, 0.f, 0.f, 0.f);
         if (v < n) {
             const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-            const int g_self = A.n_id[v];      // the self loop's source (gsrc -1)
             for (int c0 = e0; c0 < e1; c0 += 16) {
                 const int m = min(16, e1 - c0);
-                int my_t = 0;
-                int64_t my_lo = 0;
+                int my_t = 0, my_lo = 0;           // table rows < 2^31 (checked by the host)
                 float my_w = 0.f;
                 if (l < m) {
-                    int g = A.gsrc[c0 + l];    // the sampled edge's global source
-                    if (g < 0) g = g_self;
-                    my_t = A.ntype[g];
-                    my_lo = A.local[g];
+                    my_t = A.edge_type[c0 + l];
+                    my_lo = int(A.edge_off[c0 + l]);
                     my_w = tab[A.rel[c0 + l]];
-                    A.edge_type[c0 + l] = my_t;
-                    A.edge_off[c0 + l] = my_lo;
                 }
-                const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
                 // UN edges' rows in flight per lane, then their accumulation in edge order
                 constexpr int UN = 4;
                 for (int j = 0; j < m; j += UN) {
@@ -224,8 +234,7 @@ __global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
                         const int jj = min(j + u, m - 1);
                         t[u] = __shfl(my_t, gl + jj, 64);
                         wt[u] = __shfl(my_w, gl + jj, 64);
-                        const int64_t lo = int64_t((uint64_t(uint32_t(__shfl(lo_hi, gl + jj, 64))) << 32) |
-                                                   uint32_t(__shfl(lo_lo, gl + jj, 64)));
+                        const int64_t lo = __shfl(my_lo, gl + jj, 64);
                         const float* xr = pick(A.xt.p, t[u]) + lo * K + 4 * l;
 #pragma unroll
                         for (int p = 0; p < VPL; ++p) x[u][p] = *reinterpret_cast<const float4*>(xr + 64 * p);
@@ -266,23 +275,39 @@ __global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
             }
         }
         __syncthreads();
-        // ---- project: D[v][j] = sum_t S_vt W_c[t]  (v = 4q + r, j = 16w + c)
+        // ---- project: D[v][j] = sum_t S_vt W_c[t]  (v = 4q + r, j = 16w + c); type t + 1's
+        // W_c columns are loaded while type t's products run
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
-        for (int tt = 0; tt < T; ++tt) {
-            const float* wt = A.wc + int64_t(tt) * (K + 1) * F + (16 * w + c) * K + 4 * q;
-            const float* sa = St + c * SR + tt * K + 4 * q;
-#pragma unroll 4
-            for (int b = 0; b < K / 16; ++b) {
+        constexpr int HB = KB / 2;             // float4 steps per half type
+        float4 bcur[HB], bnext[HB];
+        auto bload = [&](int step, float4 (&dst)[HB]) {
+            const int tt = step >> 1, h0 = (step & 1) * HB;
+            const float* wt = A.wc + int64_t(tt) * (K + 1) * F + (16 * w + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+        };
+        bload(0, bcur);
+        for (int step = 0; step < 2 * T; ++step) {
+            if (step + 1 < 2 * T) bload(step + 1, bnext);
+            const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) {
                 const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
-                const float4 bv = *reinterpret_cast<const float4*>(wt + 16 * b);
-                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bcur[b].x, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bcur[b].y, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bcur[b].z, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bcur[b].w, d, 0, 0, 0);
             }
+#pragma unroll
+            for (int b = 0; b < HB; ++b) bcur[b] = bnext[b];
         }
+        float4 wn[F * F / 4 / kBlock];         // W_1, staged into the S tile once it is read
+#pragma unroll
+        for (int i = 0; i < F * F / 4 / kBlock; ++i)
+            wn[i] = reinterpret_cast<const float4*>(A.w_next)[threadIdx.x + kBlock * i];
         {
             const int j = 16 * w + c;
+            const float bj = A.bias[j];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int vr = 4 * q + r;
@@ -291,10 +316,13 @@ __global__ void __launch_bounds__(kBlock, 4) agg0_kernel(Agg0Args A) {
                     bsum = fmaf(sw[vr * MT + tt], A.wc[int64_t(tt) * (K + 1) * F + K * F + j], bsum);
                 const int vv = base + vr;
                 const float iv = vv < n ? A.inv[vv] : 0.f;
-                at[vr * F + j] = fmaf(iv, d[r] + bsum, A.bias[j]);
+                at[vr * F + j] = fmaf(iv, d[r] + bsum, bj);
             }
         }
-        __syncthreads();
+        __syncthreads();                       // S tile free: W_1 and the h rows go there
+#pragma unroll
+        for (int i = 0; i < F * F / 4 / kBlock; ++i)
+            reinterpret_cast<float4*>(Wn)[threadIdx.x + kBlock * i] = wn[i];
         // ---- epilogue (agg_kernel's): LayerNorm, relu, dropout, x @ W_1
         const bool act = v < n;
         if (act) {
@@ -472,6 +500,7 @@ struct HeadArgs {
 };
 
 constexpr int kHeadRows = 16;          // target rows per block (one MFMA row tile)
+constexpr int kMaxCT = 28;             // class tiles of 16: C <= 448
 
 inline int64_t head_part_width(int C) { return ((int64_t(C) * (F + 1) + 3 * F + 1) + 3) & ~3ll; }
 __host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }   // z / g row stride: 4 banks apart
@@ -494,24 +523,33 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     float* ghs = hs2 + 16 * 80;                            // [16][68]: gh
     __shared__ float tab[F];
     __shared__ float lrow[kHeadRows];
-    __shared__ int s_valid;
-    for (int e4 = threadIdx.x; e4 < CT * 16 * (F / 4); e4 += kBlock) {
-        const int c = e4 >> 4, k4 = (e4 & 15) * 4;
-        const float4 wv = c < C ? *reinterpret_cast<const float4*>(A.w_out + int64_t(c) * F + k4)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(Wl + head_sw(c, k4)) = wv;
-    }
-    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
-    const int n = A.sizes[0];
-    if (threadIdx.x == 0) s_valid = 0;
-    __syncthreads();
-    int cnt = 0;
-    for (int i = threadIdx.x; i < n; i += kBlock) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
-    atomicAdd(&s_valid, cnt);              // integer count: order-independent
     const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
+    const int n = A.sizes[0];
     const int v = blockIdx.x * kHeadRows + sub;
     const bool act = v < n;
+    const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
+    {                                      // out_lin.weight -> LDS: thread (row c = tid/16 + 16i,
+        constexpr int UB = 8;              // float4 tid%16), UB rows in flight
+        const int k4 = (threadIdx.x & 15) * 4;
+        for (int i0 = 0; i0 < CT; i0 += UB) {
+            float4 wv[UB];
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const int c = (threadIdx.x >> 4) + 16 * (i0 + u);
+                wv[u] = i0 + u < CT && c < C
+                            ? *reinterpret_cast<const float4*>(A.w_out + int64_t(c) * F + k4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const int c = (threadIdx.x >> 4) + 16 * (i0 + u);
+                if (i0 + u < CT) *reinterpret_cast<float4*>(Wl + head_sw(c, k4)) = wv[u];
+            }
+        }
+    }
+    if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
+    __syncthreads();
     // ---- 1. aggregation, LayerNorm, relu, dropout
     const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
@@ -563,8 +601,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     __syncthreads();
-    const int n_valid = s_valid;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
+    const int n_valid = int(*A.nvalid);    // agg0's count of labelled targets
     // ---- 2. z = h W^T + b -> zs (classes >= C: -inf)
     for (int ct = w; ct < CT; ct += kBlock / 64) {
         const int c = 16 * ct + cc;
@@ -584,38 +621,51 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     }
     __syncthreads();
     // ---- 3. log_softmax, nll, g
-    {
+    {                                      // lane l holds classes l + 16i of row sub
+        float zr[kMaxCT];
         float zmax = -INFINITY;
-        for (int c = l; c < CT * 16; c += 16) zmax = fmaxf(zmax, zs[sub * CP + c]);
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            zr[i] = i < CT ? zs[sub * CP + l + 16 * i] : -INFINITY;
+            zmax = fmaxf(zmax, zr[i]);
+        }
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
         float se = 0.f;
-        for (int c = l; c < C; c += 16) se += expf(zs[sub * CP + c] - zmax);
-        const float lse = zmax + logf(group_sum<16>(se));
-        const int64_t y = act ? A.labels[A.n_id[v]] : -1;
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            zr[i] = expf(zr[i] - zmax);        // classes >= C: exp(-inf) = 0
+            se += zr[i];
+        }
+        se = group_sum<16>(se);
+        const float lse = zmax + logf(se), rse = 1.f / se;
         const float zy = y >= 0 ? zs[sub * CP + y] : 0.f;
         if (l == 0) lrow[sub] = y >= 0 ? lse - zy : 0.f;
         const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
-        for (int c = l; c < CT * 16; c += 16) {
-            const float z = zs[sub * CP + c];
-            zs[sub * CP + c] = act && c < C ? (expf(z - lse) - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            const int c = l + 16 * i;
+            if (i < CT)
+                zs[sub * CP + c] = act && c < C ? (zr[i] * rse - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
         }
     }
     __syncthreads();
     // ---- 4. gh = g W: wave w -> features 16w + cc, rows 4q + r
     {
-        f32x4 dg = {0.f, 0.f, 0.f, 0.f};
+        f32x4 dg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         const int k = 16 * w + cc;
+#pragma unroll 2
         for (int b = 0; b < CT; ++b) {         // classes 16b + 4q + i, i = instruction
             const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
             const int c0 = 16 * b + 4 * q;
-            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, Wl[head_sw(c0 + 0, k)], dg, 0, 0, 0);
-            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, Wl[head_sw(c0 + 1, k)], dg, 0, 0, 0);
-            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, Wl[head_sw(c0 + 2, k)], dg, 0, 0, 0);
-            dg = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, Wl[head_sw(c0 + 3, k)], dg, 0, 0, 0);
+            f32x4& dd = dg[b & 1];             // two independent chains
+            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, Wl[head_sw(c0 + 0, k)], dd, 0, 0, 0);
+            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, Wl[head_sw(c0 + 1, k)], dd, 0, 0, 0);
+            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, Wl[head_sw(c0 + 2, k)], dd, 0, 0, 0);
+            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, Wl[head_sw(c0 + 3, k)], dd, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg[r];
+        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg[0][r] + dg[1][r];
     }
     __syncthreads();
     // ---- 5. LayerNorm / relu / dropout backward -> ga; per-feature row terms to red
@@ -1118,16 +1168,17 @@ struct ChainArgs {
     float* g_lin_w[MT]; float* g_lin_b[MT]; float* g_w0;
 };
 
+template <int K>
 __global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
     __shared__ float red[4][F];
     __shared__ float w0r[F];
-    const int K = A.K;
     if (blockIdx.x < F) {
         const int o = blockIdx.x, j = threadIdx.x & 63, g = threadIdx.x >> 6;
         float s = 0.f;
         for (int t = 0; t < A.T; ++t) {
             const float* W = pick(A.lin_w.p, t) + int64_t(o) * K;
             const float* gw = A.gwc + int64_t(t) * (K + 1) * F;
+#pragma unroll 8
             for (int k = g; k < K; k += 4) s = fmaf(W[k], gw[int64_t(k) * F + j], s);
             if (g == 0) s = fmaf(pick(A.lin_b.p, t)[o], gw[int64_t(K) * F + j], s);
         }
@@ -1279,8 +1330,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     for (int l = 0; l < L; ++l)
         if (p->n_rel[l] < 1 || p->n_rel[l] > F) return REGNN_EUNSUPPORTED;
     if (!w->state || !w->sizes || !w->n_id || !w->ntype || !w->local || !w->labels || !w->wc ||
-        !w->gwc || !w->tabs || !w->nvalid || !w->gsrc || !w->s_agg || !w->s_w || !w->z || !w->beta ||
-        !w->edge_type || !w->edge_off || !w->slab ||
+        !w->gwc || !w->tabs || !w->nvalid || !w->edge_type || !w->edge_off || !w->s_agg ||
+        !w->s_w || !w->z || !w->beta || !w->slab ||
         !p->loss || !p->out_w || !p->out_b || !p->g_out_w || !p->g_out_b || w->cap[0] <= 0)
         return REGNN_EINVAL;
     for (int t = 0; t < T; ++t)
@@ -1317,11 +1368,12 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         const int h = L - 1;
         Agg0Args A{};
         A.sizes = w->sizes; A.hop = h;
-        A.ptr = w->blk_ptr[h]; A.gsrc = w->gsrc; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
-        A.n_id = w->n_id; A.ntype = w->ntype; A.local = w->local; A.xt = xt; A.T = T; A.wc = w->wc;
+        A.ptr = w->blk_ptr[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.edge_type = w->edge_type; A.edge_off = w->edge_off; A.xt = xt; A.T = T; A.wc = w->wc;
+        A.n_id = w->n_id; A.labels = w->labels; A.nvalid = w->nvalid;
         A.tab = w->tabs; A.bias = p->conv_b[0]; A.ln_w = p->ln_w[0]; A.ln_b = p->ln_b[0];
         A.state = w->state; A.drop = drop; A.w_next = p->conv_w[1];
-        A.s_agg = w->s_agg; A.s_w = w->s_w; A.edge_type = w->edge_type; A.edge_off = w->edge_off;
+        A.s_agg = w->s_agg; A.s_w = w->s_w;
         A.a = w->a[0]; A.stats = w->stats[0]; A.xs_next = w->xs[1]; A.gxs_next = w->gxs[1];
         int grid = (w->cap[h] + 15) / 16;
         if (grid > 2048) grid = 2048;
@@ -1456,7 +1508,10 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
             A.g_lin_b[t] = p->g_lin_b[t];
         }
         A.g_w0 = p->g_conv_w[0];
-        hipLaunchKernelGGL(chain_kernel, dim3(F + T * F), dim3(kBlock), 0, stream, A);
+        if (K == 128)
+            hipLaunchKernelGGL(chain_kernel<128>, dim3(F + T * F), dim3(kBlock), 0, stream, A);
+        else
+            hipLaunchKernelGGL(chain_kernel<64>, dim3(F + T * F), dim3(kBlock), 0, stream, A);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

@@ -980,7 +980,7 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 22; }
+int regnn_abi_version(void) { return 24; }
 
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {

@@ -59,7 +59,11 @@ class DeviceSampler:
     etype: 0-based edge type per caller edge (mag edge_type), or None (relation 0);
     ntype: node type per global node (self-loop relation num_edge_types + ntype), or None."""
 
-    def __init__(self, rg, sizes, batch_size, etype=None, ntype=None, num_edge_types=0):
+    def __init__(self, rg, sizes, batch_size, etype=None, ntype=None, num_edge_types=0,
+                 share=None):
+        """share: another DeviceSampler over the same graph whose read-only tables (edge and
+        node types) and dedup tables are reused (a second pipeline slot: the two never sample
+        at the same time, and their dedup stamps never coincide)."""
         dev = rg.device
         self.rg, self.device = rg, dev
         self.sizes_k = [int(k) for k in sizes]
@@ -76,14 +80,18 @@ class DeviceSampler:
         self.caps = caps
         self.num_edge_types = int(num_edge_types)
         n_nodes = max(rg.n_src, rg.n_dst)
-        if etype is None:
+        if share is not None:
+            self.etype_csr, self.ntype = share.etype_csr, share.ntype
+        elif etype is None:
             self.etype_csr = torch.zeros(rg.E, dtype=torch.uint8, device=dev)
         else:
             et = torch.as_tensor(etype).to(dev).reshape(-1)
             if et.numel() != rg.E:
                 raise ValueError(f"etype has {et.numel()} entries, graph has {rg.E} edges")
             self.etype_csr = et[rg.csr_eid].to(torch.uint8).contiguous()
-        if ntype is None:
+        if share is not None:
+            pass
+        elif ntype is None:
             self.ntype = torch.zeros(n_nodes, dtype=torch.int32, device=dev)
         else:
             self.ntype = torch.as_tensor(ntype).to(dev).to(torch.int32).contiguous()
@@ -92,8 +100,16 @@ class DeviceSampler:
         self.state = torch.zeros(8, dtype=torch.int64, device=dev)
         self.sizes = torch.zeros(16, dtype=torch.int32, device=dev)
         self.n_id = torch.zeros(caps[-1], dtype=torch.int32, device=dev)
-        self.g2l = torch.zeros(n_nodes, dtype=torch.int64, device=dev)
-        self.first = torch.full((n_nodes,), -1, dtype=torch.int64, device=dev)
+        if share is not None:
+            # one stamp counter for both: the dedup tables need increasing stamps
+            self.g2l, self.first = share.g2l, share.first
+            if share.stamp_src is None:
+                share.stamp_src = share.state[4:5].clone()
+            self.stamp_src = share.stamp_src
+        else:
+            self.g2l = torch.zeros(n_nodes, dtype=torch.int64, device=dev)
+            self.first = torch.full((n_nodes,), -1, dtype=torch.int64, device=dev)
+            self.stamp_src = None
         self.hop_bufs, self.blocks = [], []
         for h, k in enumerate(self.sizes_k):
             cd = caps[h]
@@ -106,12 +122,25 @@ class DeviceSampler:
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
                           torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev)
             self.blocks.append(blk)
+        self.local, self.edge_meta = None, [None] * len(self.sizes_k)
+        self.meta_fresh = [False] * len(self.sizes_k)
+
+    def enable_edge_meta(self, local_node_idx, hop):
+        """also write hop `hop`'s per-edge source node type and table row (regnn_ns_hop's
+        optional outputs; what regnn_nsm_step's layer 0 gathers by)."""
+        self.local = torch.as_tensor(local_node_idx).to(self.device, torch.int64).contiguous()
+        ce = self.blocks[hop].csr_idx.numel()
+        self.edge_meta[hop] = (torch.zeros(ce, dtype=torch.int32, device=self.device),
+                               torch.zeros(ce, dtype=torch.int64, device=self.device))
+        self.meta_fresh[hop] = False          # written by the next run_hops
+        return self.edge_meta[hop]
 
     # -- the per-step device work ------------------------------------------------------------
     def batch_from_perm(self, perm, rank=0, world=1):
         """regnn_ns_batch: this rank's next targets from the epoch permutation (device int64)."""
         L.call("regnn_ns_batch", L.ptr(perm), perm.numel(), self.B, int(rank), int(world),
-               L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes), L.stream())
+               L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes),
+               None if self.stamp_src is None else L.ptr(self.stamp_src), L.stream())
 
     def run_hops(self):
         rg = self.rg
@@ -124,13 +153,20 @@ class DeviceSampler:
                    L.ptr(b["gsrc"]), L.ptr(b["flag"]), L.ptr(b["tiles"]), L.ptr(b["status"]),
                    L.ptr(blk.csr_ptr),
                    L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos), L.ptr(blk.inv),
+                   *((L.ptr(self.local), L.ptr(self.edge_meta[h][0]), L.ptr(self.edge_meta[h][1]))
+                     if self.edge_meta[h] is not None else (None, None, None)),
                    L.stream())
+            self.meta_fresh[h] = self.edge_meta[h] is not None
 
     def set_seed(self, base_seed, epoch, batch_idx):
         """host-driven batches (the PyG-style iterator): seed words + a fresh dedup stamp."""
         st = self.state.cpu()
         st[0], st[1], st[3] = _i64(int(base_seed)), int(epoch), int(batch_idx)
-        st[4] += 1
+        if self.stamp_src is not None:
+            self.stamp_src += 1
+            st[4] = int(self.stamp_src.item())
+        else:
+            st[4] += 1
         self.state.copy_(st)
 
     def set_targets(self, targets):
@@ -191,9 +227,8 @@ class _NsmWork(ctypes.Structure):
                 ("blk_ptr", _P * _ML), ("blk_idx", _P * _ML), ("blk_rel", _P * _ML),
                 ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
-                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("gsrc", _P), ("s_agg", _P),
-                ("s_w", _P), ("z", _P), ("beta", _P), ("edge_type", _P), ("edge_off", _P),
-                ("nvalid", _P), ("slab", _P)]
+                ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
+                ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P)]
 
 
 def fused_unsupported(model, x_dict):
@@ -295,17 +330,19 @@ class FusedStep:
             if l < nl - 1:
                 W.a[l], W.stats[l] = ptr(z(n_dst, 64)), ptr(z(n_dst, 2))
             W.ga[l] = ptr(z(n_dst, 64))
-        n0, e0 = caps[nl - 1], sampler.blocks[nl - 1].csr_idx.numel()
-        W.gsrc = ptr(sampler.hop_bufs[nl - 1]["gsrc"])
+        n0 = caps[nl - 1]
+        et, eo = sampler.enable_edge_meta(local_node_idx, nl - 1)
+        W.edge_type, W.edge_off = ptr(et), ptr(eo)
         W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
-        W.edge_type = ptr(torch.zeros(e0, dtype=torch.int32, device=dev))
-        W.edge_off = ptr(torch.zeros(e0, dtype=torch.int64, device=dev))
         W.nvalid = ptr(z(1))
         W.slab = ptr(z(_slab_floats(P, caps[0])))
-        self.model = model
+        self.model, self.sampler, self.n_layers = model, sampler, nl
 
     def step(self):
+        if not self.sampler.meta_fresh[self.n_layers - 1]:
+            raise RuntimeError("run the sampler's hops after building FusedStep: layer 0 reads the "
+                               "per-edge source type / table row they write")
         # train / eval decides the dropout (a captured graph keeps the value it was captured with)
         self.P.p_drop = float(self.model.dropout) if self.model.training else 0.0
         with torch.cuda.device(self.device), timed("nsm_step"):
@@ -349,16 +386,22 @@ class NSTrainer:
     graph capture), or None for FlatAdam over a flat parameter bucket (`adam`: lr, betas, eps,
     weight_decay); train_idx: target nodes (the paper train split); y_global [N, 1] labels.
     The gradients live in one flat fp32 bucket (p.grad are views of it): one RCCL all-reduce
-    per step for world > 1 (mag.flat_grad_allreduce's exchange), outside the captured graph."""
+    per step for world > 1 (mag.flat_grad_allreduce's exchange), outside the captured graph.
+
+    pipeline (fused engine): two sampler slots; while the model trains on one slot's batch, the
+    next batch is sampled into the other on a second stream (the reference's NeighborSampler
+    prefetches batches with DataLoader workers, mag/regnn_ns.py:206-208). Slot s deals global
+    batches as rank + s * world of 2 * world, so the batch sequence is the unpipelined one."""
 
     def __init__(self, model, opt, rg, sizes, batch_size, train_idx, x_dict, edge_type,
                  node_type, local_node_idx, y_global, num_edge_types, seed=0, rank=0, world=1,
-                 shuffle=True, engine="auto", adam=None):
+                 shuffle=True, engine="auto", adam=None, pipeline=True):
         self.model, self.opt = model, opt
         dev = rg.device
         self.device, self.rank, self.world = dev, int(rank), int(world)
-        self.sampler = DeviceSampler(rg, sizes, batch_size, etype=edge_type, ntype=node_type,
-                                     num_edge_types=num_edge_types)
+        self.slots = [DeviceSampler(rg, sizes, batch_size, etype=edge_type, ntype=node_type,
+                                    num_edge_types=num_edge_types)]
+        self.cur, self._primed, self._trained = 0, False, 0
         self.train_idx = torch.as_tensor(train_idx).to(dev, torch.int64)
         self.perm = self.train_idx.clone()
         self.shuffle, self.seed = shuffle, int(seed)
@@ -388,8 +431,16 @@ class NSTrainer:
             raise ValueError(f"fused NS step unavailable: {why}")
         self.fused = None
         if engine != "module" and why is None:
-            self.fused = FusedStep(model, self.sampler, x_dict, node_type, local_node_idx,
+            self.fused = FusedStep(model, self.slots[0], x_dict, node_type, local_node_idx,
                                    self.y_flat, self.loss)
+        self.pipelined = self.fused is not None and bool(pipeline)
+        if self.pipelined:
+            s1 = DeviceSampler(rg, sizes, batch_size, num_edge_types=num_edge_types,
+                               share=self.slots[0])
+            self.slots.append(s1)
+            self.fused_slots = [self.fused, FusedStep(model, s1, x_dict, node_type,
+                                                      local_node_idx, self.y_flat, self.loss)]
+            self._side = torch.cuda.Stream(device=dev)
         self.graphs = None
         self.epoch = -1
         self.set_epoch(0)
@@ -409,22 +460,54 @@ class NSTrainer:
             self.perm.copy_(self.train_idx[order])
         else:
             self.perm.copy_(self.train_idx)
-        st = self.sampler.state
-        st[0:1].fill_(_i64(self.seed))
-        st[1:2].fill_(self.epoch)
-        st[2:3].zero_()
+        for s in self.slots:
+            st = s.state
+            st[0:1].fill_(_i64(self.seed))
+            st[1:2].fill_(self.epoch)
+            st[2:3].zero_()
+        self.cur, self._primed, self._trained = 0, False, 0
+
+    @property
+    def sampler(self):
+        """the sampler slot of the most recently trained batch."""
+        return self.slots[self._trained]
 
     # -- one step --------------------------------------------------------------------------------
+    def _sample(self, slot):
+        n = len(self.slots)
+        s = self.slots[slot]
+        s.batch_from_perm(self.perm, self.rank + slot * self.world, n * self.world)
+        s.run_hops()
+
+    def _pipelined_body(self, cur):
+        """train slot `cur`'s batch while the next one is sampled into the other slot."""
+        cs = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cs)
+        with torch.cuda.stream(self._side):
+            self._sample(1 - cur)
+        self.fused_slots[cur].step()
+        cs.wait_stream(self._side)
+
+    def _prime(self):
+        if not self._primed:
+            self._sample(self.cur)
+            self._primed = True
+
     def _forward_backward(self):
-        s = self.sampler
         if self.fused is not None:
             # every gradient is overwritten by the step (parameters the forward never reads,
             # e.g. REGNN.norm, keep the zeros of the bucket's allocation)
-            s.batch_from_perm(self.perm, self.rank, self.world)
-            s.run_hops()
+            if self.pipelined:
+                self._prime()
+                self._pipelined_body(self.cur)
+                self._trained, self.cur = self.cur, 1 - self.cur
+                return
+            self._sample(0)
             self.fused.step()
             return
         self.flat.zero_()
+        s = self.slots[0]
+        self._trained = 0
         s.batch_from_perm(self.perm, self.rank, self.world)
         s.run_hops()
         B = s.B
@@ -455,7 +538,7 @@ class NSTrainer:
         """capture the step as HIP graphs: [fwd/bwd] (+ the eager all-reduce) + [optimizer]."""
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        st0 = self.sampler.state.clone()
+        st0 = [s.state.clone() for s in self.slots]
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self.step()
@@ -463,12 +546,23 @@ class NSTrainer:
         torch.cuda.synchronize(self.device)
         # warm-up steps do not advance the epoch (batch counter, edge counter); the dedup stamp
         # (state[4]) stays monotone: the tables still hold the warm-up steps' stamps
-        st = self.sampler.state
-        st[2:4].copy_(st0[2:4])
-        st[5:6].copy_(st0[5:6])
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            self._forward_backward()
+        for s, s0 in zip(self.slots, st0):
+            s.state[2:4].copy_(s0[2:4])
+            s.state[5:6].copy_(s0[5:6])
+        self.cur, self._primed, self._trained = 0, False, 0
+        if self.pipelined:
+            self._prime()                      # slot 0's batch, before the first replay
+            torch.cuda.synchronize(self.device)
+            g1 = []
+            for cur in (0, 1):                 # one graph per slot parity
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._pipelined_body(cur)
+                g1.append(g)
+        else:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self._forward_backward()
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
             self.opt.step()
@@ -476,10 +570,16 @@ class NSTrainer:
 
     def replay(self):
         g1, g2 = self.graphs
-        g1.replay()
+        if self.pipelined:
+            self._prime()                      # after set_epoch: the new epoch's first batch
+            g1[self.cur].replay()
+            self._trained, self.cur = self.cur, 1 - self.cur
+        else:
+            g1.replay()
         self._exchange()
         g2.replay()
 
     def edges_total(self):
-        """aggregated edges of every step so far (device counter: one host sync)."""
-        return int(self.sampler.state[5].item())
+        """aggregated edges of every batch sampled so far (device counters: one host sync;
+        pipelined, that includes the batch sampled ahead)."""
+        return int(sum(int(s.state[5].item()) for s in self.slots))

@@ -140,7 +140,7 @@ def test_trainer_graph_replay_tracks_eager():
     tr_g.capture(warmup=2)
     for _ in range(2):
         tr_e.step()
-    tr_e.sampler.state[2:3].zero_()
+    tr_e.set_epoch(0)                                  # the epoch again from its first batch
     le, lg = [], []
     for _ in range(6):
         tr_e.step()
@@ -150,6 +150,41 @@ def test_trainer_graph_replay_tracks_eager():
     assert np.all(np.isfinite(lg))
     assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
     assert tr_g.edges_total() > 0
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_pipelined_trainer_matches_unpipelined(graph):
+    """two sampler slots (the next batch sampled on a second stream while the model trains)
+    give the unpipelined batch sequence, dropout masks and losses, across an epoch change."""
+    from regnn_hip.ns import NSTrainer
+    d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.4)
+
+    def make(pipe):
+        return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 100,
+                         torch.arange(d["n_paper"], device=DEV), d["x_dict"], d["edge_type"],
+                         d["node_type"], d["local"], d["y"], 7, seed=9, adam=dict(lr=1e-2),
+                         pipeline=pipe)
+    tr_p, tr_u = make(True), make(False)
+    assert tr_p.pipelined and not tr_u.pipelined
+    if graph:
+        tr_p.capture(warmup=2)
+        for _ in range(2):
+            tr_u.step()
+        tr_u.set_epoch(0)
+    run_p = tr_p.replay if graph else tr_p.step
+    lp, lu = [], []
+    for i in range(7):
+        if i == 4:                                      # an epoch change mid-run
+            tr_p.set_epoch(1)
+            tr_u.set_epoch(1)
+        run_p()
+        tr_u.step()
+        assert torch.equal(tr_p.sampler.n_id[:int(tr_p.sampler.sizes[0])],
+                           tr_u.sampler.n_id[:int(tr_u.sampler.sizes[0])])
+        lp.append(float(tr_p.loss))
+        lu.append(float(tr_u.loss))
+    assert np.all(np.isfinite(lp))
+    assert np.allclose(lp, lu, rtol=1e-6, atol=1e-7), (lp, lu)
 
 
 def test_trainer_epoch_wraps_and_counts():
@@ -265,11 +300,12 @@ def _sample_row_global(row_idx, t, k, seed, base):
     return [int(row_idx[p]) for p in chosen], [base + p for p in chosen]
 
 
-def _nsm_seed(state0, stamp, layer):
-    """the fused step's dropout seed of `layer` (include/regnn_hip.h, regnn_nsm_step)."""
+def _nsm_seed(st, layer):
+    """the fused step's dropout seed of `layer` (include/regnn_hip.h, regnn_nsm_step): seed
+    word, epoch and global batch of the step's sampler state."""
     from regnn_hip.sampler import _mix
     M = (1 << 64) - 1
-    return _mix((state0 & M) ^ _mix(((stamp << 4) + layer + 0x51ED27) & M))
+    return _mix((st[0] & M) ^ _mix(((st[1] << 40) ^ (st[3] << 8) ^ (layer + 0x51ED27)) & M))
 
 
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
@@ -296,7 +332,7 @@ def test_fused_step_matches_module_path(monkeypatch, dropout):
         def hash_dropout(x, p=0.5, training=True, inplace=False):
             layer = len(calls)
             calls.append(layer)
-            seed = _nsm_seed(st[0], st[4], layer)
+            seed = _nsm_seed(st, layer)
             mask = O.dropout_mask(seed, x.shape[0], x.shape[1], 4, keep16)
             return x * torch.from_numpy(mask).to(x.device, x.dtype) / (keep16 / 65536)
         monkeypatch.setattr(torch.nn.functional, "dropout", hash_dropout)
@@ -331,7 +367,7 @@ def test_fused_step_graph_replay_tracks_eager(flat_adam):
     tr_g.capture(warmup=2)
     for _ in range(2):
         tr_e.step()
-    tr_e.sampler.state[2:3].zero_()
+    tr_e.set_epoch(0)                                  # the epoch again from its first batch
     le, lg = [], []
     for _ in range(5):
         tr_e.step()

@@ -76,11 +76,6 @@ def test_regnn_fused_step_vs_reference():
     rg = RelGraph(torch.from_numpy(d["src"]), torch.from_numpy(d["dst"]), N, DEV)
     ds = DeviceSampler(rg, m["sizes"], len(d["batch"]), etype=torch.from_numpy(d["edge_type"]),
                        ntype=torch.from_numpy(d["ntype"]), num_edge_types=m["num_edge_types"])
-    ds.set_seed(m["seed"], m["epoch"], m["batch_idx"])
-    ds.set_targets(torch.from_numpy(d["batch"]).to(DEV))
-    ds.run_hops()
-    n_tot = int(ds.sizes[len(m["sizes"])])
-    assert ds.n_id[:n_tot].cpu().numpy().tolist() == d["n_id"].tolist()
     model = _model(d)
     model.eval()
     for p in model.parameters():
@@ -90,6 +85,20 @@ def test_regnn_fused_step_vs_reference():
     y_flat[:m["counts"][0]] = torch.from_numpy(d["y"])
     loss = torch.zeros((), device=DEV)
     fs = FusedStep(model, ds, x_dict, nt, loc, y_flat, loss)
+    with pytest.raises(RuntimeError):                  # the hops have not run since
+        fs.step()
+    ds.set_seed(m["seed"], m["epoch"], m["batch_idx"])
+    ds.set_targets(torch.from_numpy(d["batch"]).to(DEV))
+    ds.run_hops()
+    n_tot = int(ds.sizes[len(m["sizes"])])
+    assert ds.n_id[:n_tot].cpu().numpy().tolist() == d["n_id"].tolist()
+    # the sampler's per-edge source type / table row of the last hop (layer 0's block)
+    et, eo = ds.edge_meta[len(m["sizes"]) - 1]
+    blk = ds.blocks[len(m["sizes"]) - 1]
+    E = int(ds.sizes[8 + len(m["sizes"]) - 1])
+    g = ds.n_id.long()[blk.csr_idx[:E].long()]
+    assert torch.equal(et[:E].long(), nt.to(DEV).long()[g])
+    assert torch.equal(eo[:E], loc.to(DEV).long()[g])
     fs.step()
     torch.cuda.synchronize()
     _check("loss", loss, d["loss"])
