@@ -155,26 +155,31 @@ def run_ns_epoch(args, dev):
                                             "cores, hidden 512, real ogbn-mag"}}
 
 
-def ns_step_bytes(sz, K, C, L=2, F=64):
+def ns_step_bytes(sz, K, C, L=2, F=64, T=4):
     """algorithmic HBM bytes of one fused NS model step (regnn_nsm_step) at the sampled sizes
     sz (regnn_ns_hop sizes: sz[h] = rows after h hops, sz[8 + h] = edges of hop h's block,
     self loops included): every row / index / feature byte a kernel must read or write once.
-      project      n_L x (K*4 gathered input row + 2*F*4 xs write + gxs zero + 28 index bytes)
-      agg l < L-1  E x (F*4 gathered row + 5) + n_dst x (4*F*4 + 20: a, xs_next, gxs_next, ga)
-      head         E0 x (F*4 + 5) + n0 x (F*4 ga + 24); out_lin in
-      agg_bwd l    E x (F*4 row read + F*4 atomic add + 5) + n_dst x (F*4 + 12)
-      post_bwd l   n_dst x (3*F*4 + 8)
-      project_bwd  n_L x (K*4 + F*4 + 12)"""
+    Layer 0 (block L-1: n rows, E edges, T node types):
+      agg0   E x (K*4 gathered input row + 13 type / row / relation) + n x (T*K*4 S + T*4 w
+             + 3*F*4 a, xs_next, gxs_next + 16 stats / ptr / inv)
+      bwd0   n x (T*K*4 S + F*4 ga + T*K*4 Z + T*8 w / beta + 4)
+      rel0   E x (K*4 input row again + 13) + n x (T*K*4 Z + T*4 beta)
+    Layers 1 .. L-2: agg E x (F*4 + 5) + n x (4*F*4 + 20); agg_bwd E x (2*F*4 + 5) + n x (F*4 + 12).
+    post_bwd of layers 0 .. L-2: n x (3*F*4 + 8). Head (layer L-1): E0 x (F*4 + 5) + n0 x (F*4 +
+    24) + out_lin; its agg_bwd E0 x (2*F*4 + 5) + n0 x (F*4 + 12)."""
     f = 4 * F
-    b = sz[L] * (4 * K + 2 * f + 28)                                   # project
-    for l in range(L - 1):                                             # agg / agg_bwd / post
+    n, E = sz[L - 1], sz[8 + L - 1]
+    b = E * (4 * K + 13) + n * (T * 4 * K + 4 * T + 3 * f + 16)       # agg0
+    b += n * (2 * T * 4 * K + f + 8 * T + 4)                            # bwd0
+    b += E * (4 * K + 13) + n * (T * 4 * K + 4 * T)                     # rel0
+    for l in range(1, L - 1):                                           # agg / agg_bwd
         h = L - 1 - l
         b += sz[8 + h] * (f + 5) + sz[h] * (4 * f + 20)
         b += sz[8 + h] * (2 * f + 5) + sz[h] * (f + 12)
-        b += sz[h] * (3 * f + 8)
+    for l in range(L - 1):                                              # post_bwd
+        b += sz[L - 1 - l] * (3 * f + 8)
     b += sz[8] * (f + 5) + sz[0] * (f + 24) + 4 * C * F                # head (layer L-1)
     b += sz[8] * (2 * f + 5) + sz[0] * (f + 12)                         # its agg_bwd
-    b += sz[L] * (4 * K + f + 12)                                      # project_bwd
     return b
 
 
@@ -253,12 +258,12 @@ def run_ns(args, dev):
     }
     res["config"]["engine"] = "fused regnn_nsm_step" if tr.fused is not None else "module"
     if "nsm_step" in kstats and nsm_bytes:
-        # the fused model step (ten launches): algorithmic bytes of its reads and writes at the
+        # the fused model step (eight launches): algorithmic bytes of its reads and writes at the
         # profiled steps' sampled sizes (ns_step_bytes) / its device time
         launches, mean_ms, total_ms, _ = kstats["nsm_step"]
         b = statistics.mean(nsm_bytes)
         ach = b / (mean_ms / 1e3) / 1e9
-        res["ns_roofline"] = {"bound": "hbm", "kernel": "regnn_nsm_step (10 launches)",
+        res["ns_roofline"] = {"bound": "hbm", "kernel": "regnn_nsm_step (8 launches)",
                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": ach / HBM_PEAK_GBS, "launch_ms": mean_ms,
                               "algorithmic_bytes_per_launch": b}

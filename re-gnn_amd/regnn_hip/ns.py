@@ -424,7 +424,7 @@ class NSTrainer:
                 o += p.numel()
             self.opt = opt = FlatAdam(self.pflat, self.flat, **(adam or {}))
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
-        # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in ten HIP
+        # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in eight HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
         why = fused_unsupported(model, x_dict)
         if engine == "fused" and why is not None:

@@ -310,7 +310,7 @@ def _nsm_seed(st, layer):
 
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
 def test_fused_step_matches_module_path(monkeypatch, dropout):
-    """regnn_nsm_step (the model's forward / nll / backward in ten launches) against the
+    """regnn_nsm_step (the model's forward / nll / backward in eight launches) against the
     mag.REGNN autograd path on the same sampled batch: loss and every parameter gradient at
     1e-5. With dropout the module path gets the fused step's hash masks (oracle.dropout_mask of
     the documented per-layer seed) in place of torch's RNG."""
