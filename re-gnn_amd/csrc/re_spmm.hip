@@ -980,8 +980,6 @@ using namespace regnn;
 
 extern "C" {
 
-int regnn_abi_version(void) { return 24; }
-
 int64_t regnn_tune(int32_t key, int64_t value) {
     if (key == 1) {
         const int64_t old = g_tune_grid_cap;
