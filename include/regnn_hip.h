@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 24). */
+/* ABI version (bumped on any signature change or addition; currently 25). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -258,6 +258,24 @@ int regnn_spmm_bwd_next(const int32_t* ptr, const int32_t* idx, const uint8_t* r
 int regnn_rel_reduce(float* slab, int64_t n_rows, int32_t width, float* out,
                      int32_t accumulate, hipStream_t stream);
 
+/* Long-segment plan of the GAT / per-head kernels below (the regnn_spmm_fwd split, as a struct):
+ * segments with more than `split` edges (long_ids, n_long of them) are cut into chunks of `chunk`
+ * edges (chunk c belongs to long segment chunk_long[c], the chunks of segment l are
+ * [chunk_off[l], chunk_off[l+1])), processed by their own workgroups into fp32 partial rows
+ * 0 .. n_chunk-1 of `partial` and combined per segment by the fixed-order tree of level_sb /
+ * level_desc (HOST, [n_levels][3]: sb offset, n_out, row base; as regnn_spmm_fwd). partial holds
+ * partial_rows rows of the width the entry point names; partial_floats is its capacity. A NULL
+ * plan (or n_long = 0) runs every segment whole. The kernels skip long segments only when H is a
+ * power of two <= 32 (their group forms); the generic forms run every segment whole. */
+typedef struct regnn_seg_plan {
+    int32_t split, chunk;
+    const int32_t* long_ids; int32_t n_long;
+    const int32_t* chunk_long; const int32_t* chunk_off; int32_t n_chunk;
+    const int32_t* level_sb; int32_t n_levels; const int64_t* level_desc;
+    int64_t partial_rows;
+    float* partial; int64_t partial_floats;
+} regnn_seg_plan;
+
 /* GAT attention, forward. Replaces apply_edges(fn.u_add_v('el','er','e')) + ee add +
  * LeakyReLU + dgl edge_softmax (layer/REGATConv.py:80-88):
  *   s(e,h) = el[idx[e],h] + er[v,h] + (ee_table ? ee_table[rel[e]*H + h] : 0)
@@ -265,7 +283,8 @@ int regnn_rel_reduce(float* slab, int64_t n_rows, int32_t width, float* out,
  * over the in-edges of each destination v (CSR). a is written in CSR edge order [nnz, H]. */
 int regnn_gat_softmax_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                           const float* ee_table, const float* el, const float* er,
-                          int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream);
+                          int64_t n_seg, int32_t H, float slope, float* a,
+                          const regnn_seg_plan* plan, hipStream_t stream);  /* partial width 2H */
 
 /* GAT attention, backward (edge_softmax VJP + LeakyReLU + u_add_v), per destination v (CSR):
  *   gz = a * (ga - sum_v a*ga);  gs = gz * (s > 0 ? 1 : slope)
@@ -275,7 +294,7 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
                           const float* ee_table, const float* el, const float* er,
                           const float* a, const float* ga, int64_t n_seg, int32_t H, float slope,
                           float* gs_out, float* ger, float* slab, int32_t n_rel,
-                          hipStream_t stream);
+                          const regnn_seg_plan* plan, hipStream_t stream);  /* partial width H */
 
 /* Fused GAT forward (layer/REGATConv.py:80-92 in one pass: the u_add_v SDDMM + relation bias +
  * LeakyReLU, DGL edge_softmax over each destination's in-edges, and the per-head weighted SpMM):
@@ -286,13 +305,15 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
 int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                         const float* ee_table, const float* el, const float* er, const void* x,
                         void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
-                        int32_t dtype, hipStream_t stream);
+                        int32_t dtype, const regnn_seg_plan* plan,
+                        hipStream_t stream);  /* partial width H*D + 2H */
 
 /* The attention a[e,h] = exp(e[h] - lse[v,h]) (CSR edge order) of regnn_gat_fused_fwd, re-formed
  * for the backward. H a power of two <= 32. */
 int regnn_gat_attn_lse(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                        const float* ee_table, const float* el, const float* er, const float* lse,
-                       int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream);
+                       int64_t n_seg, int32_t H, float slope, float* a,
+                       const regnn_seg_plan* plan, hipStream_t stream);  /* no partials */
 
 /* Per-head weighted SpMM (GAT message passing, layer/REGATConv.py:90-91,
  * update_all(fn.u_mul_e('ft','a','m'), fn.sum('m','ft'))):
@@ -300,18 +321,21 @@ int regnn_gat_attn_lse(const int32_t* ptr, const int32_t* idx, const uint8_t* re
  * Rows are H*D wide, D % 4 == 0 (fp32). */
 int regnn_spmm_heads_fwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
                          const float* a, const void* x, void* y, int64_t n_seg, int32_t H,
-                         int32_t D, int32_t dtype, hipStream_t stream);
+                         int32_t D, int32_t dtype, const regnn_seg_plan* plan,
+                         hipStream_t stream);  /* partial width H*D */
 
 /* Fused backward of regnn_spmm_heads_fwd over the CSC (segment = source u, perm = CSC->CSR edge):
  *   gx[u,h,:] = sum_{e: u->v} a[perm[e],h] * g[v,h,:];   ga[perm[e],h] = <g[v,h,:], x[u,h,:]> */
 int regnn_spmm_heads_bwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
                          const float* a, const void* g, const void* x, void* gx, float* ga,
-                         int64_t n_seg, int32_t H, int32_t D, int32_t dtype, hipStream_t stream);
+                         int64_t n_seg, int32_t H, int32_t D, int32_t dtype,
+                         const regnn_seg_plan* plan, hipStream_t stream);  /* partial width H*D */
 
 /* out[s,h] = sum_{e in seg s} vals[(perm ? perm[e] : e)*H + h]  (segment sum of edge values,
  * e.g. d loss / d el over the CSC). */
 int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals, int64_t n_seg,
-                      int32_t H, float* out, hipStream_t stream);
+                      int32_t H, float* out, const regnn_seg_plan* plan,
+                      hipStream_t stream);  /* partial width H */
 
 /* Column sum of a row-major fp32 [rows, cols] matrix into per-block partial rows:
  * slab[b][c] = sum of column c over block b's row range (at most regnn_slab_rows()/2 blocks;

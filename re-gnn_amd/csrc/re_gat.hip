@@ -11,6 +11,178 @@ namespace regnn {
 
 __device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
 
+template <typename T>
+__device__ __forceinline__ T from_f32(float v) {
+    if constexpr (sizeof(T) == 2) return f2bf(v);
+    else return v;
+}
+
+// ---- long segments (regnn_seg_plan) ---------------------------------------------------------
+// A segment with more than `split` edges is skipped by the per-segment kernels and cut into
+// `chunk`-edge chunks, each run by its own group into an fp32 partial row; a fixed-order tree
+// (SegPlan's levels) combines a segment's partials and an emit kernel writes the result.
+struct LongPlan {
+    int split, chunk;                      // split = INT_MAX: every segment whole
+    const int32_t* long_ids; const int32_t* chunk_long; const int32_t* chunk_off;
+    int n_long, n_chunk;
+    float* part;
+};
+
+inline LongPlan long_plan(const regnn_seg_plan* pl) {
+    LongPlan P{};
+    P.split = 0x7fffffff;
+    if (pl && pl->n_long > 0 && pl->n_chunk > 0) {
+        P.split = pl->split; P.chunk = pl->chunk;
+        P.long_ids = pl->long_ids; P.chunk_long = pl->chunk_long; P.chunk_off = pl->chunk_off;
+        P.n_long = pl->n_long; P.n_chunk = pl->n_chunk; P.part = pl->partial;
+    }
+    return P;
+}
+
+inline int check_plan(const regnn_seg_plan* pl, int64_t width) {
+    if (!pl || pl->n_long <= 0 || pl->n_chunk <= 0) return REGNN_OK;
+    if (pl->split < 1 || pl->chunk < 1 || !pl->long_ids || !pl->chunk_long || !pl->chunk_off ||
+        pl->n_levels < 0 || (pl->n_levels > 0 && (!pl->level_sb || !pl->level_desc)))
+        return REGNN_EINVAL;
+    if (width > 0 && (!pl->partial || pl->partial_floats < pl->partial_rows * width ||
+                      pl->partial_rows < pl->n_chunk))
+        return REGNN_EINVAL;
+    return REGNN_OK;
+}
+
+// chunk c -> (segment, edge range[, its long-segment index])
+__device__ __forceinline__ void chunk_range(const LongPlan& P, const int32_t* __restrict__ ptr,
+                                            int64_t c, int64_t& seg, int& beg, int& end, int& l) {
+    l = P.chunk_long[c];
+    seg = P.long_ids[l];
+    const int rb = ptr[seg], re = ptr[seg + 1];
+    beg = rb + int(c - P.chunk_off[l]) * P.chunk;
+    end = min(beg + P.chunk, re);
+}
+
+__device__ __forceinline__ void chunk_range(const LongPlan& P, const int32_t* __restrict__ ptr,
+                                            int64_t c, int64_t& seg, int& beg, int& end) {
+    int l;
+    chunk_range(P, ptr, c, seg, beg, end, l);
+}
+
+// the unit loop of the group kernels: unit -> (segment, first edge, edge count); false for a
+// long segment in the per-segment pass
+template <bool CH>
+__device__ __forceinline__ bool group_unit(const LongPlan& P, const int32_t* __restrict__ ptr,
+                                           int64_t unit, int64_t& seg, int& beg, int& n, int& l) {
+    if (CH) {
+        int end;
+        chunk_range(P, ptr, unit, seg, beg, end, l);
+        n = end - beg;
+        return true;
+    }
+    seg = unit;
+    l = -1;
+    beg = ptr[seg];
+    n = ptr[seg + 1] - beg;
+    return n <= P.split;
+}
+
+// one tree level: partial row base_out + p = combine(rows base_in + [sb[p], sb[p+1])) in order
+// (sb is relative to the level's inputs: the chunk rows, then the previous level's outputs).
+// MODE 0: plain sums of W floats. MODE 1: online-softmax rows [acc F | max H | sum H] (head of
+// acc column f: f / D), rescaled to the larger max.
+template <int MODE>
+__global__ void __launch_bounds__(kBlock)
+seg_tree_level(float* __restrict__ part, const int32_t* __restrict__ sb, int64_t n_out, int W,
+               int F, int H, int D, int64_t base_in, int64_t base_out) {
+    for (int64_t p = blockIdx.x; p < n_out; p += gridDim.x) {
+        const int64_t r0 = base_in + sb[p], r1 = base_in + sb[p + 1];
+        float* __restrict__ o = part + (base_out + p) * W;
+        for (int w = threadIdx.x; w < W; w += kBlock) {
+            if (MODE == 0) {
+                float acc = 0.f;
+                for (int64_t r = r0; r < r1; ++r) acc += part[r * W + w];
+                o[w] = acc;
+            } else {
+                const int h = w < F ? w / D : (w < F + H ? w - F : w - F - H);
+                float M = -INFINITY, S = 0.f, A = 0.f;
+                for (int64_t r = r0; r < r1; ++r) {
+                    const float* pr = part + r * W;
+                    const float m = pr[F + h], sv = pr[F + H + h], a = w < F ? pr[w] : 0.f;
+                    const float mn = fmaxf(M, m);
+                    if (mn == -INFINITY) continue;
+                    const float f0 = M == -INFINITY ? 0.f : __expf(M - mn);
+                    const float f1 = m == -INFINITY ? 0.f : __expf(m - mn);
+                    A = A * f0 + a * f1;
+                    S = S * f0 + sv * f1;
+                    M = mn;
+                }
+                o[w] = w < F ? A : (w < F + H ? M : S);
+            }
+        }
+    }
+}
+
+// row of the combined partial of long segment l
+__device__ __forceinline__ int64_t final_row(const int32_t* __restrict__ chunk_off, int64_t base,
+                                             int n_levels, int l) {
+    return n_levels > 0 ? base + l : int64_t(chunk_off[l]);
+}
+
+// dst[long_ids[l]][w] = combined partial (plain sums), l < n_long
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+seg_emit_sum(const float* __restrict__ part, const int32_t* __restrict__ chunk_off, int64_t base,
+             int n_levels, const int32_t* __restrict__ long_ids, int n_long, int W,
+             T* __restrict__ dst) {
+    for (int l = blockIdx.x; l < n_long; l += gridDim.x) {
+        const float* __restrict__ pr = part + final_row(chunk_off, base, n_levels, l) * W;
+        const int64_t row = long_ids[l];
+        for (int w = threadIdx.x; w < W; w += kBlock) dst[row * W + w] = from_f32<T>(pr[w]);
+    }
+}
+
+// out[row] = acc / sum, lse[row] = max + log sum from a combined online-softmax row
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+seg_emit_softmax(const float* __restrict__ part, const int32_t* __restrict__ chunk_off,
+                 int64_t base, int n_levels, const int32_t* __restrict__ long_ids, int n_long,
+                 int F, int H, int D, T* __restrict__ out, float* __restrict__ lse) {
+    const int W = F + 2 * H;
+    for (int l = blockIdx.x; l < n_long; l += gridDim.x) {
+        const float* __restrict__ pr = part + final_row(chunk_off, base, n_levels, l) * W;
+        const int64_t row = long_ids[l];
+        for (int f = threadIdx.x; f < F; f += kBlock) {
+            const float sv = pr[F + H + f / D];
+            out[row * F + f] = from_f32<T>(sv > 0.f ? pr[f] / sv : 0.f);
+        }
+        for (int h = threadIdx.x; h < H; h += kBlock) {
+            const float sv = pr[F + H + h];
+            lse[row * H + h] = sv > 0.f ? pr[F + h] + __logf(sv) : -INFINITY;
+        }
+    }
+}
+
+// launch the tree levels of a plan; returns the row base of the last level
+inline int64_t run_tree(const regnn_seg_plan* pl, int mode, int W, int F, int H, int D,
+                        hipStream_t stream) {
+    int64_t base = 0, base_in = 0;
+    for (int k = 0; k < pl->n_levels; ++k) {
+        const int64_t sb_off = pl->level_desc[3 * k], n_out = pl->level_desc[3 * k + 1];
+        base = pl->level_desc[3 * k + 2];
+        const int grid = int(n_out < kMaxGrid ? n_out : kMaxGrid);
+        if (mode == 0)
+            hipLaunchKernelGGL(seg_tree_level<0>, dim3(grid), dim3(kBlock), 0, stream,
+                               pl->partial, pl->level_sb + sb_off, n_out, W, F, H, D, base_in,
+                               base);
+        else
+            hipLaunchKernelGGL(seg_tree_level<1>, dim3(grid), dim3(kBlock), 0, stream,
+                               pl->partial, pl->level_sb + sb_off, n_out, W, F, H, D, base_in,
+                               base);
+        base_in = base;
+    }
+    return base;
+}
+
+inline int long_grid(int n) { return n < kMaxGrid ? (n > 0 ? n : 1) : kMaxGrid; }
+
 __global__ void __launch_bounds__(kBlock)
 gat_softmax_fwd_generic(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                        const uint8_t* __restrict__ rel, const float* __restrict__ ee,
@@ -102,8 +274,10 @@ struct HeadArgs {
     int H, D;
 };
 
-template <typename T, int LPR, int NV, bool BWD>
-__global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p) {
+// CH: the units are the chunks of long segments (fp32 partial rows of the sums); otherwise the
+// segments, long ones skipped. The per-edge ga of the backward is written either way.
+template <typename T, int LPR, int NV, bool BWD, bool CH>
+__global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p, LongPlan P) {
     constexpr int EV = Vec<T>::N;
     constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);   // edge rows in flight per step
     constexpr int GPB = kBlock / LPR;
@@ -111,9 +285,19 @@ __global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p) {
     const int F = p.H * p.D;
     const int vph = p.D / EV;   // vectors per head (power of two, <= LPR)
     const T* __restrict__ src = static_cast<const T*>(p.src);
-    for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < p.n_seg;
-         seg += (int64_t)gridDim.x * GPB) {
-        const int beg = p.ptr[seg], end = p.ptr[seg + 1];
+    const int64_t n_units = CH ? P.n_chunk : p.n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * GPB + tid / LPR; unit < n_units;
+         unit += (int64_t)gridDim.x * GPB) {
+        int64_t seg;
+        int beg, end;
+        if (CH) {
+            chunk_range(P, p.ptr, unit, seg, beg, end);
+        } else {
+            seg = unit;
+            beg = p.ptr[seg];
+            end = p.ptr[seg + 1];
+            if (end - beg > P.split) continue;
+        }
         float acc[NV][EV] = {};
         float sx[NV][EV] = {};
         int head[NV];
@@ -173,6 +357,17 @@ __global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p) {
                 }
             }
         }
+        if (CH) {
+            float* __restrict__ pr = P.part + unit * F;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int o = (q * LPR + lane) * EV;
+                if (o < F)
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) pr[o + t] = acc[q][t];
+            }
+            continue;
+        }
         T* __restrict__ out = static_cast<T*>(p.out) + seg * F;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -183,18 +378,29 @@ __global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p) {
 }
 
 template <typename T, bool BWD>
-int dispatch_heads(HeadArgs p, hipStream_t stream) {
+int dispatch_heads(HeadArgs p, const regnn_seg_plan* pl, hipStream_t stream) {
     constexpr int EV = Vec<T>::N;
     const int F = p.H * p.D;
     if (p.D <= 0 || p.D % EV || p.H <= 0) return REGNN_EUNSUPPORTED;
     const int vph = p.D / EV;
     if (vph & (vph - 1)) return REGNN_EUNSUPPORTED;
     const int nvec = F / EV;
+    const LongPlan P = long_plan(pl);
 #define REGNN_HEADS(LPR, NV)                                                                    \
     if (nvec <= (LPR) * (NV) && vph <= (LPR)) {                                                 \
-        hipLaunchKernelGGL((spmm_heads_kernel<T, LPR, NV, BWD>),                                \
-                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p); \
+        hipLaunchKernelGGL((spmm_heads_kernel<T, LPR, NV, BWD, false>),                         \
+                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p, P); \
         REGNN_LAUNCH_CHECK();                                                                   \
+        if (P.n_chunk > 0) {                                                                    \
+            hipLaunchKernelGGL((spmm_heads_kernel<T, LPR, NV, BWD, true>),                      \
+                               dim3(grid_for(P.n_chunk, kBlock / (LPR))), dim3(kBlock), 0, stream, \
+                               p, P);                                                           \
+            const int64_t base = run_tree(pl, 0, F, F, p.H, p.D, stream);                       \
+            hipLaunchKernelGGL(seg_emit_sum<T>, dim3(long_grid(P.n_long)), dim3(kBlock), 0,     \
+                               stream, P.part, P.chunk_off, base, pl->n_levels, P.long_ids,     \
+                               P.n_long, F, static_cast<T*>(p.out));                            \
+            REGNN_LAUNCH_CHECK();                                                               \
+        }                                                                                       \
         return REGNN_OK;                                                                        \
     }
     REGNN_HEADS(16, 1)
@@ -249,31 +455,52 @@ __device__ __forceinline__ float gat_score(const int32_t* __restrict__ idx,
     return lrelu(s, slope);
 }
 
+// MODE 0: segments (long ones skipped); MODE 1: chunks -> partial rows [max H | sum H];
+// MODE 2: chunks, attention from the combined (max, sum) of their segment (rows fin + 2H l)
+template <int MODE>
 __global__ void __launch_bounds__(kBlock)
 gat_softmax_fwd_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                       const uint8_t* __restrict__ rel, const float* __restrict__ ee,
                       const float* __restrict__ el, const float* __restrict__ er, int64_t n_seg,
-                      int H, int lgH, float slope, float* __restrict__ a) {
+                      int H, int lgH, float slope, float* __restrict__ a, LongPlan P,
+                      const float* __restrict__ fin) {
     constexpr int G = kGatGroup, U = kGatUn;
+    constexpr bool CH = MODE > 0;
     const int lane = threadIdx.x & (G - 1), h = lane & (H - 1);
-    for (int64_t seg = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; seg < n_seg;
-         seg += (int64_t)gridDim.x * (kBlock / G)) {
-        const int beg = ptr[seg], np = (ptr[seg + 1] - beg) << lgH;
+    const int64_t n_units = CH ? P.n_chunk : n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; unit < n_units;
+         unit += (int64_t)gridDim.x * (kBlock / G)) {
+        int64_t seg;
+        int beg, ne, l;
+        if (!group_unit<CH>(P, ptr, unit, seg, beg, ne, l)) continue;
+        const int np = ne << lgH;
         const float erv = er[seg * H + h];
         float m = -INFINITY, sum = 0.f;
-        for (int p0 = lane; p0 < np; p0 += G * U) {
-            float sc[U];
+        if (MODE != 2) {
+            for (int p0 = lane; p0 < np; p0 += G * U) {
+                float sc[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int p = p0 + u * G;
-                sc[u] = p < np ? gat_score(idx, rel, ee, el, erv, beg + (p >> lgH), H, h, slope)
-                               : -INFINITY;
+                for (int u = 0; u < U; ++u) {
+                    const int p = p0 + u * G;
+                    sc[u] = p < np ? gat_score(idx, rel, ee, el, erv, beg + (p >> lgH), H, h, slope)
+                                   : -INFINITY;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) softmax_merge(m, sum, sc[u], 1.f);
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) softmax_merge(m, sum, sc[u], 1.f);
+            for (int o = H; o < G; o <<= 1)
+                softmax_merge(m, sum, __shfl_xor(m, o, G), __shfl_xor(sum, o, G));
+            if (MODE == 1) {
+                if (lane < H) {
+                    P.part[unit * 2 * H + h] = m;
+                    P.part[unit * 2 * H + H + h] = sum;
+                }
+                continue;
+            }
+        } else {
+            m = fin[int64_t(l) * 2 * H + h];
+            sum = fin[int64_t(l) * 2 * H + H + h];
         }
-        for (int o = H; o < G; o <<= 1)
-            softmax_merge(m, sum, __shfl_xor(m, o, G), __shfl_xor(sum, o, G));
         const float inv = 1.f / sum;
         for (int p0 = lane; p0 < np; p0 += G * U) {
             float sc[U];
@@ -292,34 +519,52 @@ gat_softmax_fwd_group(const int32_t* __restrict__ ptr, const int32_t* __restrict
     }
 }
 
+// MODE 0: segments (long ones skipped); MODE 1: chunks -> partial dots sum a*ga [H];
+// MODE 2: chunks with their segment's combined dot (rows fin + H l) -> gs, partial gsum [H]
+template <int MODE>
 __global__ void __launch_bounds__(kBlock)
 gat_softmax_bwd_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                       const uint8_t* __restrict__ rel, const float* __restrict__ ee,
                       const float* __restrict__ el, const float* __restrict__ er,
                       const float* __restrict__ a, const float* __restrict__ ga, int64_t n_seg,
                       int H, int lgH, float slope, float* __restrict__ gs_out,
-                      float* __restrict__ ger, float* __restrict__ slab, int n_rel) {
+                      float* __restrict__ ger, float* __restrict__ slab, int n_rel, LongPlan P,
+                      const float* __restrict__ fin) {
     constexpr int G = kGatGroup, U = kGatUn;
+    constexpr bool CH = MODE > 0;
     extern __shared__ float bins[];   // [n_rel][kBlock]; a thread only touches its own column
     const int tid = threadIdx.x, lane = tid & (G - 1), h = lane & (H - 1);
-    if (slab) for (int r = 0; r < n_rel; ++r) bins[r * kBlock + tid] = 0.f;
-    for (int64_t seg = (int64_t)blockIdx.x * (kBlock / G) + tid / G; seg < n_seg;
-         seg += (int64_t)gridDim.x * (kBlock / G)) {
-        const int beg = ptr[seg], np = (ptr[seg + 1] - beg) << lgH;
+    const bool do_bins = slab && MODE != 1;
+    if (do_bins) for (int r = 0; r < n_rel; ++r) bins[r * kBlock + tid] = 0.f;
+    const int64_t n_units = CH ? P.n_chunk : n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * (kBlock / G) + tid / G; unit < n_units;
+         unit += (int64_t)gridDim.x * (kBlock / G)) {
+        int64_t seg;
+        int beg, ne, l;
+        if (!group_unit<CH>(P, ptr, unit, seg, beg, ne, l)) continue;
+        const int np = ne << lgH;
         const float* __restrict__ as = a + (int64_t)beg * H;
         const float* __restrict__ gas = ga + (int64_t)beg * H;
         float dot = 0.f;
-        for (int p0 = lane; p0 < np; p0 += G * U) {
-            float d[U];
+        if (MODE != 2) {
+            for (int p0 = lane; p0 < np; p0 += G * U) {
+                float d[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int p = p0 + u * G;
-                d[u] = p < np ? as[p] * gas[p] : 0.f;
+                for (int u = 0; u < U; ++u) {
+                    const int p = p0 + u * G;
+                    d[u] = p < np ? as[p] * gas[p] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) dot += d[u];
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) dot += d[u];
+            for (int o = H; o < G; o <<= 1) dot += __shfl_xor(dot, o, G);
+            if (MODE == 1) {
+                if (lane < H) P.part[unit * H + h] = dot;
+                continue;
+            }
+        } else {
+            dot = fin[int64_t(l) * H + h];
         }
-        for (int o = H; o < G; o <<= 1) dot += __shfl_xor(dot, o, G);
         const float erv = er[seg * H + h];
         float gsum = 0.f;
         for (int p0 = lane; p0 < np; p0 += G * U) {
@@ -345,14 +590,17 @@ gat_softmax_bwd_group(const int32_t* __restrict__ ptr, const int32_t* __restrict
                     const float gs = sc[u] > 0.f ? gz : gz * slope;
                     gs_out[(int64_t)beg * H + p] = gs;
                     gsum += gs;
-                    if (slab) bins[r[u] * kBlock + tid] += gs;
+                    if (do_bins) bins[r[u] * kBlock + tid] += gs;
                 }
             }
         }
         for (int o = H; o < G; o <<= 1) gsum += __shfl_xor(gsum, o, G);
-        if (lane < H) ger[seg * H + h] = gsum;
+        if (lane < H) {
+            if (CH) P.part[unit * H + h] = gsum;
+            else ger[seg * H + h] = gsum;
+        }
     }
-    if (slab) {
+    if (do_bins) {
         // G % H == 0 and kBlock % G == 0, so thread tid always works on head tid % H
         __syncthreads();
         for (int c = tid; c < n_rel * H; c += kBlock) {
@@ -364,15 +612,20 @@ gat_softmax_bwd_group(const int32_t* __restrict__ ptr, const int32_t* __restrict
     }
 }
 
+template <bool CH>
 __global__ void __launch_bounds__(kBlock)
 segment_sum_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ perm,
                   const float* __restrict__ vals, int64_t n_seg, int H, int lgH,
-                  float* __restrict__ out) {
+                  float* __restrict__ out, LongPlan P) {
     constexpr int G = kGatGroup, U = kGatUn;
     const int lane = threadIdx.x & (G - 1), h = lane & (H - 1);
-    for (int64_t seg = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; seg < n_seg;
-         seg += (int64_t)gridDim.x * (kBlock / G)) {
-        const int beg = ptr[seg], np = (ptr[seg + 1] - beg) << lgH;
+    const int64_t n_units = CH ? P.n_chunk : n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; unit < n_units;
+         unit += (int64_t)gridDim.x * (kBlock / G)) {
+        int64_t seg;
+        int beg, ne, l;
+        if (!group_unit<CH>(P, ptr, unit, seg, beg, ne, l)) continue;
+        const int np = ne << lgH;
         float acc = 0.f;
         for (int p0 = lane; p0 < np; p0 += G * U) {
             float v[U];
@@ -386,7 +639,10 @@ segment_sum_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ p
             for (int u = 0; u < U; ++u) acc += v[u];
         }
         for (int o = H; o < G; o <<= 1) acc += __shfl_xor(acc, o, G);
-        if (lane < H) out[seg * H + h] = acc;
+        if (lane < H) {
+            if (CH) P.part[unit * H + h] = acc;
+            else out[seg * H + h] = acc;
+        }
     }
 }
 
@@ -419,17 +675,29 @@ struct GatFusedArgs {
     float slope;
 };
 
-template <typename T, int LPR, int NV>
-__global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p) {
+// CH: the units are the chunks of long segments (partial rows [acc | max | sum], unnormalised);
+// otherwise the segments, long ones skipped.
+template <typename T, int LPR, int NV, bool CH>
+__global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, LongPlan P) {
     constexpr int EV = Vec<T>::N;
     constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     const int F = p.H * p.D;
     const T* __restrict__ src = static_cast<const T*>(p.x);
-    for (int64_t seg = (int64_t)blockIdx.x * GPB + tid / LPR; seg < p.n_seg;
-         seg += (int64_t)gridDim.x * GPB) {
-        const int beg = p.ptr[seg], end = p.ptr[seg + 1];
+    const int64_t n_units = CH ? P.n_chunk : p.n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * GPB + tid / LPR; unit < n_units;
+         unit += (int64_t)gridDim.x * GPB) {
+        int64_t seg;
+        int beg, end;
+        if (CH) {
+            chunk_range(P, p.ptr, unit, seg, beg, end);
+        } else {
+            seg = unit;
+            beg = p.ptr[seg];
+            end = p.ptr[seg + 1];
+            if (end - beg > P.split) continue;         // a long segment: its chunks
+        }
         float acc[NV][EV] = {};
         float m[NV], s[NV], erv[NV];
         int head[NV];
@@ -489,6 +757,22 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p) {
                 }
             }
         }
+        if (CH) {
+            float* __restrict__ pr = P.part + unit * (F + 2 * p.H);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int o = (q * LPR + lane) * EV;
+                if (o < F) {
+#pragma unroll
+                    for (int t = 0; t < EV; ++t) pr[o + t] = acc[q][t];
+                    if (o % p.D == 0) {
+                        pr[F + head[q]] = m[q];
+                        pr[F + p.H + head[q]] = s[q];
+                    }
+                }
+            }
+            continue;
+        }
         T* __restrict__ out = static_cast<T*>(p.out) + seg * F;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -509,17 +793,22 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p) {
 // a[e,h] = exp(LeakyReLU(el[u,h] + er[v,h] + ee[rel,h]) - lse[v,h]) in CSR edge order (the
 // attention the fused forward did not store; its backward needs it). Group layout of
 // gat_softmax_fwd_group: (edge, head) pairs flattened per segment, coalesced H-vectors.
+template <bool CH>
 __global__ void __launch_bounds__(kBlock)
 gat_attn_lse_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                    const uint8_t* __restrict__ rel, const float* __restrict__ ee,
                    const float* __restrict__ el, const float* __restrict__ er,
                    const float* __restrict__ lse, int64_t n_seg, int H, int lgH, float slope,
-                   float* __restrict__ a) {
+                   float* __restrict__ a, LongPlan P) {
     constexpr int G = kGatGroup, U = kGatUn;
     const int lane = threadIdx.x & (G - 1), h = lane & (H - 1);
-    for (int64_t seg = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; seg < n_seg;
-         seg += (int64_t)gridDim.x * (kBlock / G)) {
-        const int beg = ptr[seg], np = (ptr[seg + 1] - beg) << lgH;
+    const int64_t n_units = CH ? P.n_chunk : n_seg;
+    for (int64_t unit = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G; unit < n_units;
+         unit += (int64_t)gridDim.x * (kBlock / G)) {
+        int64_t seg;
+        int beg, ne, lg_;
+        if (!group_unit<CH>(P, ptr, unit, seg, beg, ne, lg_)) continue;
+        const int np = ne << lgH;
         const float erv = er[seg * H + h], l = lse[seg * H + h];
         for (int p0 = lane; p0 < np; p0 += G * U) {
             float sc[U];
@@ -539,16 +828,27 @@ gat_attn_lse_group(const int32_t* __restrict__ ptr, const int32_t* __restrict__ 
 }
 
 template <typename T>
-int dispatch_gat_fused(GatFusedArgs p, hipStream_t stream) {
+int dispatch_gat_fused(GatFusedArgs p, const regnn_seg_plan* pl, hipStream_t stream) {
     constexpr int EV = Vec<T>::N;
     const int F = p.H * p.D;
     if (p.D <= 0 || p.D % EV || p.H <= 0) return REGNN_EUNSUPPORTED;
     const int nvec = F / EV;
+    const LongPlan P = long_plan(pl);
 #define REGNN_GATF(LPR, NV)                                                                   \
     if (nvec <= (LPR) * (NV)) {                                                               \
-        hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV>),                                \
-                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p); \
+        hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, false>),                         \
+                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p, P); \
         REGNN_LAUNCH_CHECK();                                                                 \
+        if (P.n_chunk > 0) {                                                                  \
+            hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, true>),                      \
+                               dim3(grid_for(P.n_chunk, kBlock / (LPR))), dim3(kBlock), 0, stream, \
+                               p, P);                                                         \
+            const int64_t base = run_tree(pl, 1, F + 2 * p.H, F, p.H, p.D, stream);           \
+            hipLaunchKernelGGL(seg_emit_softmax<T>, dim3(long_grid(P.n_long)), dim3(kBlock),  \
+                               0, stream, P.part, P.chunk_off, base, pl->n_levels, P.long_ids, \
+                               P.n_long, F, p.H, p.D, static_cast<T*>(p.out), p.lse);         \
+            REGNN_LAUNCH_CHECK();                                                             \
+        }                                                                                     \
         return REGNN_OK;                                                                      \
     }
     REGNN_GATF(16, 1)
@@ -630,27 +930,44 @@ extern "C" {
 
 int regnn_gat_softmax_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                           const float* ee_table, const float* el, const float* er, int64_t n_seg,
-                          int32_t H, float slope, float* a, hipStream_t stream) {
+                          int32_t H, float slope, float* a, const regnn_seg_plan* plan,
+                          hipStream_t stream) {
     if (!ptr || !idx || !el || !er || !a || H <= 0 || n_seg < 0 || (ee_table && !rel))
         return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     const int lg = gat_log2(H);
-    if (lg >= 0)
-        hipLaunchKernelGGL(gat_softmax_fwd_group, dim3(grid_for(n_seg, kBlock / kGatGroup)),
-                           dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, n_seg, H, lg,
-                           slope, a);
-    else
+    if (lg < 0) {
         hipLaunchKernelGGL(gat_softmax_fwd_generic, dim3(grid_for(n_seg * H, kBlock)),
                            dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, n_seg, H,
                            slope, a);
+        REGNN_LAUNCH_CHECK();
+        return REGNN_OK;
+    }
+    if (const int rc = check_plan(plan, 2 * H)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
+    const LongPlan P = long_plan(plan);
+    hipLaunchKernelGGL(gat_softmax_fwd_group<0>, dim3(grid_for(n_seg, kBlock / kGatGroup)),
+                       dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, n_seg, H, lg,
+                       slope, a, P, nullptr);
     REGNN_LAUNCH_CHECK();
+    if (P.n_chunk > 0) {
+        const dim3 grid(grid_for(P.n_chunk, kBlock / kGatGroup));
+        hipLaunchKernelGGL(gat_softmax_fwd_group<1>, grid, dim3(kBlock), 0, stream, ptr, idx, rel,
+                           ee_table, el, er, n_seg, H, lg, slope, a, P, nullptr);
+        const int64_t base = run_tree(plan, 1, 2 * H, 0, H, 1, stream);
+        const float* fin = P.part + base * 2 * H;
+        hipLaunchKernelGGL(gat_softmax_fwd_group<2>, grid, dim3(kBlock), 0, stream, ptr, idx, rel,
+                           ee_table, el, er, n_seg, H, lg, slope, a, P, fin);
+        REGNN_LAUNCH_CHECK();
+    }
     return REGNN_OK;
 }
 
 int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                           const float* ee_table, const float* el, const float* er, const float* a,
                           const float* ga, int64_t n_seg, int32_t H, float slope, float* gs_out,
-                          float* ger, float* slab, int32_t n_rel, hipStream_t stream) {
+                          float* ger, float* slab, int32_t n_rel, const regnn_seg_plan* plan,
+                          hipStream_t stream) {
     if (!ptr || !idx || !el || !er || !a || !ga || !gs_out || !ger || H <= 0 || n_seg < 0)
         return REGNN_EINVAL;
     if ((ee_table || slab) && !rel) return REGNN_EINVAL;
@@ -658,79 +975,134 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
     if (n_seg == 0) return REGNN_OK;
     const size_t lds = slab ? size_t(n_rel) * kBlock * sizeof(float) : 0;
     const int lg = gat_log2(H);
-    if (lg >= 0)
-        hipLaunchKernelGGL(gat_softmax_bwd_group, dim3(grid_for(n_seg, kBlock / kGatGroup)),
-                           dim3(kBlock), lds, stream, ptr, idx, rel, ee_table, el, er, a, ga,
-                           n_seg, H, lg, slope, gs_out, ger, slab, n_rel);
-    else
+    if (lg < 0) {
         hipLaunchKernelGGL(gat_softmax_bwd_generic, dim3(grid_for(n_seg * H, kBlock)),
                            dim3(kBlock), lds, stream, ptr, idx, rel, ee_table, el, er, a, ga,
                            n_seg, H, slope, gs_out, ger, slab, n_rel);
+        REGNN_LAUNCH_CHECK();
+        return REGNN_OK;
+    }
+    if (const int rc = check_plan(plan, H)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
+    const LongPlan P = long_plan(plan);
+    const int g0 = grid_for(n_seg, kBlock / kGatGroup);
+    hipLaunchKernelGGL(gat_softmax_bwd_group<0>, dim3(g0), dim3(kBlock), lds, stream, ptr, idx,
+                       rel, ee_table, el, er, a, ga, n_seg, H, lg, slope, gs_out, ger, slab,
+                       n_rel, P, nullptr);
     REGNN_LAUNCH_CHECK();
+    if (P.n_chunk > 0) {
+        // the slab's rows past the per-segment pass hold the chunk pass's relation bins
+        // (regnn_slab_rows() = 2 kMaxGrid >= both grids)
+        const dim3 grid(grid_for(P.n_chunk, kBlock / kGatGroup));
+        hipLaunchKernelGGL(gat_softmax_bwd_group<1>, grid, dim3(kBlock), 0, stream, ptr, idx, rel,
+                           ee_table, el, er, a, ga, n_seg, H, lg, slope, gs_out, ger, nullptr,
+                           n_rel, P, nullptr);
+        int64_t base = run_tree(plan, 0, H, H, H, 1, stream);
+        hipLaunchKernelGGL(gat_softmax_bwd_group<2>, grid, dim3(kBlock), lds, stream, ptr, idx,
+                           rel, ee_table, el, er, a, ga, n_seg, H, lg, slope, gs_out, ger,
+                           slab ? slab + int64_t(g0) * n_rel * H : nullptr, n_rel, P,
+                           P.part + base * H);
+        base = run_tree(plan, 0, H, H, H, 1, stream);
+        hipLaunchKernelGGL(seg_emit_sum<float>, dim3(long_grid(P.n_long)), dim3(kBlock), 0,
+                           stream, P.part, P.chunk_off, base, plan->n_levels, P.long_ids,
+                           P.n_long, H, ger);
+        REGNN_LAUNCH_CHECK();
+    }
     return REGNN_OK;
 }
 
 int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                         const float* ee_table, const float* el, const float* er, const void* x,
                         void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
-                        int32_t dtype, hipStream_t stream) {
+                        int32_t dtype, const regnn_seg_plan* plan, hipStream_t stream) {
     if (!ptr || !idx || !el || !er || !x || !out || !lse || n_seg < 0 || (ee_table && !rel))
         return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
+    if (const int rc = check_plan(plan, int64_t(H) * D + 2 * H)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     GatFusedArgs p{ptr, idx, rel, ee_table, el, er, x, out, lse, n_seg, H, D, slope};
-    if (dtype == REGNN_F32) return dispatch_gat_fused<float>(p, stream);
-    if (dtype == REGNN_BF16) return dispatch_gat_fused<bf16_t>(p, stream);
+    if (dtype == REGNN_F32) return dispatch_gat_fused<float>(p, plan, stream);
+    if (dtype == REGNN_BF16) return dispatch_gat_fused<bf16_t>(p, plan, stream);
     return REGNN_EUNSUPPORTED;
 }
 
 int regnn_gat_attn_lse(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                        const float* ee_table, const float* el, const float* er, const float* lse,
-                       int64_t n_seg, int32_t H, float slope, float* a, hipStream_t stream) {
+                       int64_t n_seg, int32_t H, float slope, float* a, const regnn_seg_plan* plan,
+                       hipStream_t stream) {
     if (!ptr || !idx || !el || !er || !lse || !a || H <= 0 || n_seg < 0 || (ee_table && !rel))
         return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     const int lg = gat_log2(H);
     if (lg < 0) return REGNN_EUNSUPPORTED;
-    hipLaunchKernelGGL(gat_attn_lse_group, dim3(grid_for(n_seg, kBlock / kGatGroup)), dim3(kBlock),
-                       0, stream, ptr, idx, rel, ee_table, el, er, lse, n_seg, H, lg, slope, a);
+    if (const int rc = check_plan(plan, 0)) return rc;
+    const LongPlan P = long_plan(plan);
+    hipLaunchKernelGGL(gat_attn_lse_group<false>, dim3(grid_for(n_seg, kBlock / kGatGroup)),
+                       dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, lse, n_seg, H, lg,
+                       slope, a, P);
     REGNN_LAUNCH_CHECK();
+    if (P.n_chunk > 0) {
+        hipLaunchKernelGGL(gat_attn_lse_group<true>, dim3(grid_for(P.n_chunk, kBlock / kGatGroup)),
+                           dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, lse, n_seg,
+                           H, lg, slope, a, P);
+        REGNN_LAUNCH_CHECK();
+    }
     return REGNN_OK;
 }
 
 int regnn_spmm_heads_fwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
                          const float* a, const void* x, void* y, int64_t n_seg, int32_t H,
-                         int32_t D, int32_t dtype, hipStream_t stream) {
+                         int32_t D, int32_t dtype, const regnn_seg_plan* plan, hipStream_t stream) {
     if (!ptr || !idx || !a || !x || !y || n_seg < 0) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
+    if (const int rc = check_plan(plan, int64_t(H) * D)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     HeadArgs p{ptr, idx, perm, a, x, nullptr, y, nullptr, n_seg, H, D};
-    if (dtype == REGNN_F32) return dispatch_heads<float, false>(p, stream);
-    if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, false>(p, stream);
+    if (dtype == REGNN_F32) return dispatch_heads<float, false>(p, plan, stream);
+    if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, false>(p, plan, stream);
     return REGNN_EUNSUPPORTED;
 }
 
 int regnn_spmm_heads_bwd(const int32_t* ptr, const int32_t* idx, const int32_t* perm,
                          const float* a, const void* g, const void* x, void* gx, float* ga,
-                         int64_t n_seg, int32_t H, int32_t D, int32_t dtype, hipStream_t stream) {
+                         int64_t n_seg, int32_t H, int32_t D, int32_t dtype,
+                         const regnn_seg_plan* plan, hipStream_t stream) {
     if (!ptr || !idx || !a || !g || !x || !gx || !ga || n_seg < 0) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
+    if (const int rc = check_plan(plan, int64_t(H) * D)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     HeadArgs p{ptr, idx, perm, a, g, x, gx, ga, n_seg, H, D};
-    if (dtype == REGNN_F32) return dispatch_heads<float, true>(p, stream);
-    if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, true>(p, stream);
+    if (dtype == REGNN_F32) return dispatch_heads<float, true>(p, plan, stream);
+    if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, true>(p, plan, stream);
     return REGNN_EUNSUPPORTED;
 }
 
 int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals, int64_t n_seg,
-                      int32_t H, float* out, hipStream_t stream) {
+                      int32_t H, float* out, const regnn_seg_plan* plan, hipStream_t stream) {
     if (!ptr || !vals || !out || H <= 0 || n_seg < 0) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     const int lg = gat_log2(H);
-    if (lg >= 0)
-        hipLaunchKernelGGL(segment_sum_group, dim3(grid_for(n_seg, kBlock / kGatGroup)),
-                           dim3(kBlock), 0, stream, ptr, perm, vals, n_seg, H, lg, out);
-    else
+    if (lg < 0) {
         hipLaunchKernelGGL(segment_sum_generic, dim3(grid_for(n_seg * H, kBlock)), dim3(kBlock),
                            0, stream, ptr, perm, vals, n_seg, H, out);
+        REGNN_LAUNCH_CHECK();
+        return REGNN_OK;
+    }
+    if (const int rc = check_plan(plan, H)) return rc;
+    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
+    const LongPlan P = long_plan(plan);
+    hipLaunchKernelGGL(segment_sum_group<false>, dim3(grid_for(n_seg, kBlock / kGatGroup)),
+                       dim3(kBlock), 0, stream, ptr, perm, vals, n_seg, H, lg, out, P);
     REGNN_LAUNCH_CHECK();
+    if (P.n_chunk > 0) {
+        hipLaunchKernelGGL(segment_sum_group<true>, dim3(grid_for(P.n_chunk, kBlock / kGatGroup)),
+                           dim3(kBlock), 0, stream, ptr, perm, vals, n_seg, H, lg, out, P);
+        const int64_t base = run_tree(plan, 0, H, H, H, 1, stream);
+        hipLaunchKernelGGL(seg_emit_sum<float>, dim3(long_grid(P.n_long)), dim3(kBlock), 0,
+                           stream, P.part, P.chunk_off, base, plan->n_levels, P.long_ids,
+                           P.n_long, H, out);
+        REGNN_LAUNCH_CHECK();
+    }
     return REGNN_OK;
 }
 

@@ -65,14 +65,15 @@ _SIG = {
     "regnn_edge_softmax_bwd": ([P, P, P, P, I64, I32, P, P, I32, P], ctypes.c_int),
     "regnn_gat_scores": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_rel_reduce": ([P, I64, I32, P, I32, P], ctypes.c_int),
-    "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
-    "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P],
+    "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P, P], ctypes.c_int),
+    "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P, P],
                               ctypes.c_int),
-    "regnn_spmm_heads_fwd": ([P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
-    "regnn_gat_fused_fwd": ([P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I32, P], ctypes.c_int),
-    "regnn_gat_attn_lse": ([P, P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
-    "regnn_spmm_heads_bwd": ([P, P, P, P, P, P, P, P, I64, I32, I32, I32, P], ctypes.c_int),
-    "regnn_segment_sum": ([P, P, P, I64, I32, P, P], ctypes.c_int),
+    "regnn_spmm_heads_fwd": ([P, P, P, P, P, P, I64, I32, I32, I32, P, P], ctypes.c_int),
+    "regnn_gat_fused_fwd": ([P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I32, P, P],
+                            ctypes.c_int),
+    "regnn_gat_attn_lse": ([P, P, P, P, P, P, P, I64, I32, F32, P, P, P], ctypes.c_int),
+    "regnn_spmm_heads_bwd": ([P, P, P, P, P, P, P, P, I64, I32, I32, I32, P, P], ctypes.c_int),
+    "regnn_segment_sum": ([P, P, P, I64, I32, P, P, P], ctypes.c_int),
     "regnn_col_sum": ([P, I64, I32, P, P], ctypes.c_int),
     "regnn_type_project": ([P, I64, I32, I32, I32, P, P, P, P, ctypes.c_uint32, F32, I64, P, P, P],
                            ctypes.c_int),
@@ -99,7 +100,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 24
+ABI_VERSION = 25
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -32,6 +32,37 @@ def _reduce(slab, width, out=None, accumulate=False):
     return out
 
 
+class _SegPlanC(ctypes.Structure):
+    """regnn_seg_plan (include/regnn_hip.h): a SegPlan for the GAT / per-head kernels."""
+    _fields_ = [("split", ctypes.c_int32), ("chunk", ctypes.c_int32),
+                ("long_ids", ctypes.c_void_p), ("n_long", ctypes.c_int32),
+                ("chunk_long", ctypes.c_void_p), ("chunk_off", ctypes.c_void_p),
+                ("n_chunk", ctypes.c_int32), ("level_sb", ctypes.c_void_p),
+                ("n_levels", ctypes.c_int32), ("level_desc", ctypes.c_void_p),
+                ("partial_rows", ctypes.c_int64), ("partial", ctypes.c_void_p),
+                ("partial_floats", ctypes.c_int64)]
+
+
+class _GatPlan:
+    """a SegPlan as the C struct, with a partial buffer `width` floats wide (0: none). .ptr is
+    the struct's address (None: no long segments); the object keeps the buffers alive."""
+
+    def __init__(self, plan, width, device):
+        self.ptr, self.part = None, None
+        if plan is None or plan.n_chunk == 0:
+            return
+        if width:
+            self.part = torch.empty(plan.partial_rows * width, dtype=torch.float32,
+                                    device=device)
+        self.c = _SegPlanC(plan.split, plan.chunk, L.ptr(plan.long_ids), plan.n_long,
+                           L.ptr(plan.chunk_long), L.ptr(plan.chunk_off), plan.n_chunk,
+                           L.ptr(plan.level_sb), plan.n_levels,
+                           ctypes.cast(plan.level_desc, ctypes.c_void_p), plan.partial_rows,
+                           L.ptr(self.part), 0 if self.part is None else self.part.numel())
+        self.plan = plan
+        self.ptr = ctypes.addressof(self.c)
+
+
 def _plan_args(plan, F, device):
     if plan.n_chunk == 0:
         return (0, 0, None, 0, None, None, 0, None, None, 0, None), None
@@ -640,10 +671,11 @@ class _GatAttention(torch.autograd.Function):
             L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), None, None,
                    L.ptr(gmax), 1e-16, rg.n_dst, H, L.ptr(a), L.stream())
         else:
+            gp = _GatPlan(getattr(rg, "csr_plan", None), 2 * H, el.device)
             with timed("gat_softmax_fwd", rg.E * (5 + 12 * H) + rg.n_dst * 8 * H):
                 L.call("regnn_gat_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), rel,
                        L.ptr(t), L.ptr(el), L.ptr(er), rg.n_dst, H, float(slope), L.ptr(a),
-                       L.stream())
+                       gp.ptr, L.stream())
         ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
         ctx.tab_shape = None if ee_tab is None else ee_tab.shape
         ctx.save_for_backward(el, er, t, a)
@@ -658,14 +690,16 @@ class _GatAttention(torch.autograd.Function):
         ger = torch.empty_like(er)
         n_rel = t.shape[0] if t is not None else 0
         slab = _slab(n_rel * H, el.device) if (t is not None and ctx.needs_input_grad[2]) else None
+        gp = _GatPlan(getattr(rg, "csr_plan", None), H, el.device)
         with timed("gat_softmax_bwd", rg.E * (5 + 16 * H) + rg.n_dst * 12 * H):
             L.call("regnn_gat_softmax_bwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
                    L.ptr(ctx.pack.rel_csr if t is not None else None), L.ptr(t), L.ptr(el),
                    L.ptr(er), L.ptr(a), L.ptr(ga), rg.n_dst, H, float(ctx.slope), L.ptr(gs),
-                   L.ptr(ger), L.ptr(slab), n_rel, L.stream())
+                   L.ptr(ger), L.ptr(slab), n_rel, gp.ptr, L.stream())
         gel = torch.empty(rg.n_src, H, dtype=torch.float32, device=el.device)
+        gq = _GatPlan(getattr(rg, "csc_plan", None), H, el.device)
         L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
-               L.ptr(gel), L.stream())
+               L.ptr(gel), gq.ptr, L.stream())
         g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
         return gel, ger, g_tab, None, None, None, None
 
@@ -813,8 +847,9 @@ class _HeadSpmm(torch.autograd.Function):
         y = torch.empty(rg.n_dst, H, D, dtype=ft.dtype, device=ft.device)
         s_ = ft.element_size()
         with timed("spmm_heads_fwd", rg.E * (H * D * s_ + 4 * H + 4) + rg.n_dst * (H * D * s_ + 4)):
+            gp = _GatPlan(getattr(rg, "csr_plan", None), H * D, ft.device)
             L.call("regnn_spmm_heads_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), None, L.ptr(a),
-                   L.ptr(ft), L.ptr(y), rg.n_dst, H, D, L.dtype_code(ft), L.stream())
+                   L.ptr(ft), L.ptr(y), rg.n_dst, H, D, L.dtype_code(ft), gp.ptr, L.stream())
         ctx.rg = rg
         ctx.save_for_backward(a, ft)
         return y
@@ -830,9 +865,10 @@ class _HeadSpmm(torch.autograd.Function):
         s_ = ft.element_size()
         with timed("spmm_heads_bwd",
                    rg.E * (H * D * s_ + 8 * H + 8) + rg.n_src * (2 * H * D * s_ + 4)):
+            gq = _GatPlan(getattr(rg, "csc_plan", None), H * D, ft.device)
             L.call("regnn_spmm_heads_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
                    L.ptr(rg.csc2csr), L.ptr(a), L.ptr(gy), L.ptr(ft), L.ptr(gft), L.ptr(ga),
-                   rg.n_src, H, D, L.dtype_code(ft), L.stream())
+                   rg.n_src, H, D, L.dtype_code(ft), gq.ptr, L.stream())
         return ga, gft, None
 
 
@@ -853,9 +889,10 @@ class _GatFused(torch.autograd.Function):
         s_ = ft.element_size()
         with timed("gat_fused_fwd", rg.E * (H * D * s_ + 4 * H + 5) +
                    rg.n_dst * (H * D * s_ + 8 * H + 4)):
+            gp = _GatPlan(getattr(rg, "csr_plan", None), H * D + 2 * H, ft.device)
             L.call("regnn_gat_fused_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
                    L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(ft), L.ptr(out), L.ptr(lse), rg.n_dst, H,
-                   D, float(slope), L.dtype_code(ft), L.stream())
+                   D, float(slope), L.dtype_code(ft), gp.ptr, L.stream())
         ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
         ctx.tab_shape = None if ee_tab is None else ee_tab.shape
         ctx.save_for_backward(el, er, t, ft, lse)
@@ -871,27 +908,30 @@ class _GatFused(torch.autograd.Function):
         with timed("gat_attn_lse", rg.E * (5 + 8 * H) + rg.n_dst * 8 * H):
             L.call("regnn_gat_attn_lse", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
                    L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(lse), rg.n_dst, H, float(slope),
-                   L.ptr(a), L.stream())
+                   L.ptr(a), _GatPlan(getattr(rg, "csr_plan", None), 0, ft.device).ptr, L.stream())
         gy = gy.contiguous().to(ft.dtype)
         gft = torch.empty_like(ft)
         ga = torch.empty_like(a)
         s_ = ft.element_size()
         with timed("spmm_heads_bwd",
                    rg.E * (H * D * s_ + 8 * H + 8) + rg.n_src * (2 * H * D * s_ + 4)):
+            gq = _GatPlan(getattr(rg, "csc_plan", None), H * D, ft.device)
             L.call("regnn_spmm_heads_bwd", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
                    L.ptr(rg.csc2csr), L.ptr(a), L.ptr(gy), L.ptr(ft), L.ptr(gft), L.ptr(ga),
-                   rg.n_src, H, D, L.dtype_code(ft), L.stream())
+                   rg.n_src, H, D, L.dtype_code(ft), gq.ptr, L.stream())
         gs = torch.empty_like(a)
         ger = torch.empty_like(er)
         n_rel = t.shape[0] if t is not None else 0
         slab = _slab(n_rel * H, el.device) if (t is not None and ctx.needs_input_grad[2]) else None
         with timed("gat_softmax_bwd", rg.E * (5 + 16 * H) + rg.n_dst * 12 * H):
+            gp = _GatPlan(getattr(rg, "csr_plan", None), H, el.device)
             L.call("regnn_gat_softmax_bwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
                    L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(a), L.ptr(ga), rg.n_dst, H,
-                   float(slope), L.ptr(gs), L.ptr(ger), L.ptr(slab), n_rel, L.stream())
+                   float(slope), L.ptr(gs), L.ptr(ger), L.ptr(slab), n_rel, gp.ptr, L.stream())
         gel = torch.empty(rg.n_src, H, dtype=torch.float32, device=el.device)
+        gq = _GatPlan(getattr(rg, "csc_plan", None), H, el.device)
         L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
-               L.ptr(gel), L.stream())
+               L.ptr(gel), gq.ptr, L.stream())
         g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
         return gel, ger, g_tab, gft, None, None, None
 

@@ -54,3 +54,71 @@ def test_gat_fused_matches_unfused(H, D, use_ee):
     for name, a, b in zip(["out", "g_ft", "g_el", "g_er", "g_tab"], outs[0], outs[1]):
         err = (a - b).abs().max().item() / _rel(a)
         assert err <= 1e-5, f"{name}: rel err {err:.3e}"
+
+
+def _hub_graph(N=4000, E=120000, R=7, seed=3):
+    """hubs on both sides: destinations Pareto(1.1) (rows of ~10^4 in-edges, the CSR chunk path)
+    and half the sources Pareto too (the CSC chunk path of the transposed kernels)."""
+    from regnn_hip.graph import RelGraph
+    rng = np.random.default_rng(seed)
+    dst = np.minimum((rng.pareto(1.1, E) * 3).astype(np.int64), N - 1)
+    src = rng.integers(0, N, E)
+    half = rng.random(E) < 0.5
+    src[half] = np.minimum((rng.pareto(1.1, int(half.sum())) * 5).astype(np.int64), N - 1)
+    rel = rng.integers(1, R + 1, E)
+    keep = np.arange(N)
+    src = np.concatenate([src, keep]); dst = np.concatenate([dst, keep])
+    rel = np.concatenate([rel, np.full(N, R)])
+    rg = RelGraph(src, dst, N, DEV)
+    return rg, torch.from_numpy(rel).to(DEV)
+
+
+def _gat_reference(rg, rel_csr, el, er, tab, ft, slope):
+    """fp64 torch restatement of layer/REGATConv.py:80-92 over the CSR edge list."""
+    ptr = rg.csr_ptr.long()
+    src = rg.csr_idx.long()
+    dst = torch.repeat_interleave(torch.arange(rg.n_dst, device=DEV), ptr[1:] - ptr[:-1])
+    s = el[src] + er[dst] + (tab[rel_csr.long()] if tab is not None else 0.0)
+    s = torch.nn.functional.leaky_relu(s, slope)
+    H = s.shape[1]
+    m = torch.full((rg.n_dst, H), -torch.inf, dtype=s.dtype, device=DEV)
+    m = m.scatter_reduce(0, dst[:, None].expand(-1, H), s, reduce="amax", include_self=True)
+    ex = torch.exp(s - m[dst])
+    den = torch.zeros(rg.n_dst, H, dtype=s.dtype, device=DEV).index_add(0, dst, ex)
+    a = ex / den[dst]
+    out = torch.zeros(rg.n_dst, H, ft.shape[2], dtype=s.dtype, device=DEV)
+    return out.index_add(0, dst, a[:, :, None] * ft[src])
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_gat_long_rows_vs_fp64(fused):
+    """rows far past the chunk split on both sides (regnn_seg_plan: chunk partials + fixed-order
+    tree for the online softmax, the per-head sums, the softmax backward's dots and sums and the
+    segment sums): forward and every gradient against an fp64 restatement at 1e-5."""
+    from regnn_hip import ops
+    rg, e_feat = _hub_graph()
+    assert rg.csr_plan.n_long > 0 and rg.csc_plan.n_long > 0
+    deg = (rg.csr_ptr[1:] - rg.csr_ptr[:-1]).max().item()
+    assert deg > 20 * rg.csr_plan.chunk                 # a segment of many chunks (tree levels)
+    N, H, D = rg.n_dst, 8, 32
+    g = torch.Generator(device=DEV).manual_seed(2)
+    ft0 = torch.randn(N, H, D, generator=g, device=DEV)
+    el0 = torch.randn(N, H, generator=g, device=DEV)
+    er0 = torch.randn(N, H, generator=g, device=DEV)
+    tab0 = torch.randn(7, H, generator=g, device=DEV) * 0.5
+    pack = rg.rel_pack(e_feat, num_rel=7)
+    gy = torch.randn(N, H, D, generator=g, device=DEV)
+    ft, el, er, tab = (t.clone().requires_grad_(True) for t in (ft0, el0, er0, tab0))
+    if fused:
+        y = ops.gat_fused(rg, el, er, ft, tab, pack, 0.2)
+    else:
+        y = ops.head_spmm(rg, ops.gat_attention(rg, el, er, tab, pack, 0.2), ft)
+    y.backward(gy)
+    got = [y.detach(), ft.grad, el.grad, er.grad, tab.grad]
+    ref_in = [t.double().clone().requires_grad_(True) for t in (el0, er0, tab0, ft0)]
+    yr = _gat_reference(rg, pack.rel_csr, *ref_in, 0.2)
+    yr.backward(gy.double())
+    want = [yr.detach(), ref_in[3].grad, ref_in[0].grad, ref_in[1].grad, ref_in[2].grad]
+    for name, a, b in zip(["out", "g_ft", "g_el", "g_er", "g_tab"], got, want):
+        err = (a.double() - b).abs().max().item() / _rel(b)
+        assert err <= 1e-5, f"{name}: rel err {err:.3e}"
