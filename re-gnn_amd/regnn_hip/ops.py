@@ -906,9 +906,10 @@ class _GatFused(torch.autograd.Function):
         rel = pack.rel_csr if t is not None else None
         a = torch.empty(rg.E, H, dtype=torch.float32, device=ft.device)
         with timed("gat_attn_lse", rg.E * (5 + 8 * H) + rg.n_dst * 8 * H):
+            gp0 = _GatPlan(getattr(rg, "csr_plan", None), 0, ft.device)   # alive for the call
             L.call("regnn_gat_attn_lse", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
                    L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(lse), rg.n_dst, H, float(slope),
-                   L.ptr(a), _GatPlan(getattr(rg, "csr_plan", None), 0, ft.device).ptr, L.stream())
+                   L.ptr(a), gp0.ptr, L.stream())
         gy = gy.contiguous().to(ft.dtype)
         gft = torch.empty_like(ft)
         ga = torch.empty_like(a)
