@@ -167,7 +167,7 @@ inline size_t agg0_lds(int T, int K) {
            sizeof(float);
 }
 
-template <int K, int NT>                   // NT: register slots of w_vt per lane (T <= NT <= MT)
+template <int K, int NT>                   // NT: per-type register accumulators (T <= NT <= MT)
 __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
     constexpr int KB = K / 16;             // float4 steps of the projection per type
@@ -201,17 +201,19 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
-        // ---- gather: S_vt accumulated in the row's LDS slots (each lane its own 4 * VPL
-        // features of every type), w_vt in registers
+        // ---- gather: S_vt and w_vt accumulated per type in registers (each lane its own
+        // 4 * VPL features), then the row's S tile written to LDS
         const int v = base + sub;
+        // (per-type sums in registers: measured faster than a read-modify-write of the LDS
+        // tile per edge)
         float wsum[NT];
+        float4 racc[NT][VPL];
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) wsum[tt] = 0.f;
-        for (int tt = 0; tt < T; ++tt)
+        for (int tt = 0; tt < NT; ++tt) {
+            wsum[tt] = 0.f;
 #pragma unroll
-            for (int p = 0; p < VPL; ++p)
-                *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) =
-                    make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int p = 0; p < VPL; ++p) racc[tt][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         if (v < n) {
             const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
             for (int c0 = e0; c0 < e1; c0 += 16) {
@@ -244,17 +246,16 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
                     for (int u = 0; u < UN; ++u) {
                         if (t[u] < 0) continue;
 #pragma unroll
-                        for (int tt = 0; tt < NT; ++tt)
-                            if (tt == t[u]) wsum[tt] += wt[u];
-                        float* sp = St + sub * SR + t[u] * K + 4 * l;
+                        for (int tt = 0; tt < NT; ++tt) {
+                            if (tt != t[u]) continue;
+                            wsum[tt] += wt[u];
 #pragma unroll
-                        for (int p = 0; p < VPL; ++p) {
-                            float4 a4 = *reinterpret_cast<float4*>(sp + 64 * p);
-                            a4.x = fmaf(wt[u], x[u][p].x, a4.x);
-                            a4.y = fmaf(wt[u], x[u][p].y, a4.y);
-                            a4.z = fmaf(wt[u], x[u][p].z, a4.z);
-                            a4.w = fmaf(wt[u], x[u][p].w, a4.w);
-                            *reinterpret_cast<float4*>(sp + 64 * p) = a4;
+                            for (int p = 0; p < VPL; ++p) {
+                                racc[tt][p].x = fmaf(wt[u], x[u][p].x, racc[tt][p].x);
+                                racc[tt][p].y = fmaf(wt[u], x[u][p].y, racc[tt][p].y);
+                                racc[tt][p].z = fmaf(wt[u], x[u][p].z, racc[tt][p].z);
+                                racc[tt][p].w = fmaf(wt[u], x[u][p].w, racc[tt][p].w);
+                            }
                         }
                     }
                 }
@@ -263,11 +264,13 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
             if (tt < T) {
-                if (v < n)
 #pragma unroll
-                    for (int p = 0; p < VPL; ++p)
+                for (int p = 0; p < VPL; ++p) {
+                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = racc[tt][p];
+                    if (v < n)
                         *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l + 64 * p) =
-                            *reinterpret_cast<const float4*>(St + sub * SR + tt * K + 4 * l + 64 * p);
+                            racc[tt][p];
+                }
                 if (l == 0) {
                     sw[sub * MT + tt] = wsum[tt];
                     if (v < n) A.s_w[int64_t(v) * T + tt] = wsum[tt];
