@@ -535,7 +535,8 @@ class NSTrainer:
         self.opt.step()
 
     def capture(self, warmup=2):
-        """capture the step as HIP graphs: [fwd/bwd] (+ the eager all-reduce) + [optimizer]."""
+        """capture the step as HIP graphs: [fwd/bwd + optimizer] on one rank; [fwd/bwd] (+ the
+        eager all-reduce) + [optimizer] on several."""
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         st0 = [s.state.clone() for s in self.slots]
@@ -550,6 +551,9 @@ class NSTrainer:
             s.state[2:4].copy_(s0[2:4])
             s.state[5:6].copy_(s0[5:6])
         self.cur, self._primed, self._trained = 0, False, 0
+        # one rank: the optimizer step joins the step's graph (no graph boundary, no host gap
+        # between the backward and Adam); several: the gradient all-reduce runs between graphs
+        fold_opt = self.world == 1
         if self.pipelined:
             self._prime()                      # slot 0's batch, before the first replay
             torch.cuda.synchronize(self.device)
@@ -557,15 +561,23 @@ class NSTrainer:
             for cur in (0, 1):                 # one graph per slot parity
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
+                    # (Adam after the join: measured faster than before it, the graph then
+                    # ends on one queue)
                     self._pipelined_body(cur)
+                    if fold_opt:
+                        self.opt.step()
                 g1.append(g)
         else:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self._forward_backward()
-        g2 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g2):
-            self.opt.step()
+                if fold_opt:
+                    self.opt.step()
+        g2 = None
+        if not fold_opt:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self.opt.step()
         self.graphs = (g1, g2)
 
     def replay(self):
@@ -576,8 +588,9 @@ class NSTrainer:
             self._trained, self.cur = self.cur, 1 - self.cur
         else:
             g1.replay()
-        self._exchange()
-        g2.replay()
+        if g2 is not None:
+            self._exchange()
+            g2.replay()
 
     def edges_total(self):
         """aggregated edges of every batch sampled so far (device counters: one host sync;
