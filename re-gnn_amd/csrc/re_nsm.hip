@@ -655,20 +655,28 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     __syncthreads();
     // ---- 4. gh = g W: wave w -> features 16w + cc, rows 4q + r
     {
-        f32x4 dg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         const int k = 16 * w + cc;
-#pragma unroll 2
-        for (int b = 0; b < CT; ++b) {         // classes 16b + 4q + i, i = instruction
+        // classes 16b + 4q + i (i = instruction); two class tiles per iteration on two
+        // independent accumulators, every LDS read of the pair issued before its products
+        auto step = [&](int b, f32x4 d) {
             const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
             const int c0 = 16 * b + 4 * q;
-            f32x4& dd = dg[b & 1];             // two independent chains
-            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, Wl[head_sw(c0 + 0, k)], dd, 0, 0, 0);
-            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, Wl[head_sw(c0 + 1, k)], dd, 0, 0, 0);
-            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, Wl[head_sw(c0 + 2, k)], dd, 0, 0, 0);
-            dd = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, Wl[head_sw(c0 + 3, k)], dd, 0, 0, 0);
+            const float w0 = Wl[head_sw(c0 + 0, k)], w1 = Wl[head_sw(c0 + 1, k)];
+            const float w2 = Wl[head_sw(c0 + 2, k)], w3 = Wl[head_sw(c0 + 3, k)];
+            d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, w0, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, w1, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, w2, d, 0, 0, 0);
+            return __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, w3, d, 0, 0, 0);
+        };
+        f32x4 dg0 = {0.f, 0.f, 0.f, 0.f}, dg1 = {0.f, 0.f, 0.f, 0.f};
+        int b = 0;
+        for (; b + 1 < CT; b += 2) {
+            dg0 = step(b, dg0);
+            dg1 = step(b + 1, dg1);
         }
+        if (b < CT) dg0 = step(b, dg0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg[0][r] + dg[1][r];
+        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
     }
     __syncthreads();
     // ---- 5. LayerNorm / relu / dropout backward -> ga; per-feature row terms to red
