@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 25). */
+/* ABI version (bumped on any signature change or addition; currently 26). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -690,6 +690,48 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
 int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, float weight_decay,
                     int64_t* step, uint32_t* ticket, hipStream_t stream);
+
+/* ---- Per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, group_input) ----
+ * The reference builds the batch's input matrix with one boolean mask per node type (a host
+ * sync each) and, for feats_type != 2, runs each type's Linear over its masked subset. Node i of
+ * the batch is n_id[i] (n_id NULL: i), of type node_type[n_id[i]] with row local_idx[n_id[i]]
+ * in its type's table (both int64, per global node). Tables are fp32 [*, K] row-major,
+ * 16-byte aligned, indexed by node type (T <= 8).
+ *
+ * regnn_typed_gather: out[i] = tab[type][local] (NULL table or type outside [0, T): zeros, as
+ * regnn_ns.py:307's zero matrix), out [n, K] fp32 (feats_type 2: the shared self.lin follows).
+ * regnn_typed_scatter: gtab[type][local] += g[i] for the tables that learn (NULL: skipped) —
+ * the backward of the gather into feats_type-2 embedding tables (float atomics; rows of one
+ * batch are distinct, so each element receives one add). */
+int regnn_typed_gather(const int64_t* n_id, int64_t n, const int64_t* node_type,
+                       const int64_t* local_idx, int32_t T, const float* const* tab, int32_t K,
+                       float* out, hipStream_t stream);
+int regnn_typed_scatter(const int64_t* n_id, int64_t n, const int64_t* node_type,
+                        const int64_t* local_idx, int32_t T, float* const* gtab, int32_t K,
+                        const float* g, hipStream_t stream);
+
+/* Per-type Linear fused with the gather (feats_type != 2: lins[t] per node type). The n rows
+ * come sorted by type (a stable sort, built on the device by the caller): entry i is output row
+ * order[i], reading row src[i] of its type's table; type t's run is [type_off[t], type_off[t+1])
+ * (type_off int32 [T+1] on the device: the launch reads the run sizes itself, no host sync).
+ *   fwd:   Y[order[i]] = tab[t][src[i]] W[t]^T + b[t]        W[t] [O, K], b[t] [O] or NULL
+ *   wgrad: gW[g] = sum over types t with wgroup[t] = g of sum_i gY[order[i]]^T tab[t][src[i]],
+ *          gb[g] (NULL: skipped) the matching sums of gY rows; per-chunk partials in `slab`
+ *          (regnn_typed_slab_floats(n, T, K, O) floats, no zeroing needed) reduced in fixed
+ *          chunk order (deterministic).
+ * Host arrays tab / W / b hold T device pointers, gW / gb G, wgroup T ints. fp32 MFMA
+ * (v_mfma_f32_16x16x4_f32: exact fp32 products). K in {64, 128, 256}; O a multiple of 16
+ * (fwd) / 64 (wgrad), else REGNN_EUNSUPPORTED. */
+int64_t regnn_typed_chunks(int64_t n, int32_t T, int32_t rows);
+int64_t regnn_typed_slab_floats(int64_t n, int32_t T, int32_t K, int32_t O);
+int regnn_typed_linear_fwd(const int64_t* order, const int64_t* src, const int32_t* type_off,
+                           int64_t n, int32_t T, const float* const* tab, const float* const* W,
+                           const float* const* b, int32_t K, int32_t O, float* Y,
+                           hipStream_t stream);
+int regnn_typed_linear_wgrad(const int64_t* order, const int64_t* src, const int32_t* type_off,
+                             int64_t n, int32_t T, const float* const* tab, const int32_t* wgroup,
+                             int32_t G, int32_t K, int32_t O, const float* gY, float* slab,
+                             float* const* gW, float* const* gb, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -92,6 +92,13 @@ _SIG = {
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
     "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
+    "regnn_typed_gather": ([P, I64, P, P, I32, P, I32, P, P], ctypes.c_int),
+    "regnn_typed_scatter": ([P, I64, P, P, I32, P, I32, P, P], ctypes.c_int),
+    "regnn_typed_chunks": ([I64, I32, I32], I64),
+    "regnn_typed_slab_floats": ([I64, I32, I32, I32], I64),
+    "regnn_typed_linear_fwd": ([P, P, P, I64, I32, P, P, P, I32, I32, P, P], ctypes.c_int),
+    "regnn_typed_linear_wgrad": ([P, P, P, I64, I32, P, P, I32, I32, I32, P, P, P, P, P],
+                                 ctypes.c_int),
 }
 
 for _name, (_args, _ret) in _SIG.items():
@@ -100,7 +107,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 25
+ABI_VERSION = 26
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")
@@ -166,3 +173,11 @@ def call(name, *args):
 
 def slab_rows():
     return int(_so.regnn_slab_rows(0, 0))
+
+
+def typed_slab_floats(n, T, K, O):
+    """fp32 elements of regnn_typed_linear_wgrad's chunk-partial slab."""
+    v = int(_so.regnn_typed_slab_floats(int(n), int(T), int(K), int(O)))
+    if v < 0:
+        raise RuntimeError("regnn_hip.regnn_typed_slab_floats: invalid arguments")
+    return max(v, 1)

@@ -307,12 +307,45 @@ class REGNN(torch.nn.Module):
         """[(table parameter, local rows the last forward read)] of the feats_type-2 tables."""
         if self.feats_type != 2:
             return []
+        if self._touched is None:                    # formed on demand (boolean masks sync)
+            nt, li = self._batch_rows
+            self._touched = {k: li[nt == int(k)] for k in self.emb_dict}
         return [(emb, self._touched.get(k)) for k, emb in self.emb_dict.items()]
 
+    def _type_tables(self, x_dict):
+        """the input tables indexed by node type (feats_type 2: the learned embeddings for the
+        non-target types), or None when a key lies outside 0..T-1."""
+        T = self.num_node_types
+        keys = set(x_dict) | ({int(k) for k in self.emb_dict} if self.feats_type == 2 else set())
+        if not keys <= set(range(T)):
+            return None
+        tabs = [x_dict.get(k) for k in range(T)]
+        if self.feats_type == 2:
+            for k, emb in self.emb_dict.items():
+                tabs[int(k)] = emb
+        return tabs
+
     def group_input(self, x_dict, node_type, local_node_idx, n_id=None):
-        """mag/regnn_ns.py:300-326. When every type has the same feature width the per-type
-        Linear is one GEMM against all types' weights + a per-node pick (no boolean-mask syncs);
-        each node still gets exactly its own type's projection."""
+        """mag/regnn_ns.py:300-326 without per-type masks or host syncs: feats_type 2 gathers
+        every node's row from its type's table in one launch (ops.typed_gather) before the shared
+        Linear; otherwise each node's row goes through its own type's Linear in one gather-fused
+        MFMA launch over the type-sorted rows (ops.typed_linear). Other shapes: one GEMM against
+        all types' weights + a per-node pick."""
+        tabs = self._type_tables(x_dict)
+        on_dev = tabs is not None and all(t is None or (t.is_cuda and t.dtype == torch.float32
+                                                        and t.dim() == 2) for t in tabs)
+        widths = {t.shape[1] for t in tabs if t is not None} if on_dev else set()
+        if self.feats_type == 2 and len(widths) == 1 and widths.pop() % 4 == 0:
+            t = ops.typed_gather(tabs, node_type, local_node_idx, n_id)
+            self._batch_rows = ((node_type, local_node_idx) if n_id is None else
+                                (node_type[n_id], local_node_idx[n_id]))
+            self._touched = None
+            return self.lin(t)
+        if self.feats_type != 2 and on_dev and all(t is not None for t in tabs):
+            Ws = [self.lins[str(k)].weight for k in range(len(tabs))]
+            bs = [self.lins[str(k)].bias for k in range(len(tabs))]
+            if ops.typed_linear_fusable(tabs, Ws, bs):
+                return ops.typed_linear(tabs, Ws, bs, node_type, local_node_idx, n_id)
         if n_id is not None:
             node_type, local_node_idx = node_type[n_id], local_node_idx[n_id]
         if self.feats_type == 2:

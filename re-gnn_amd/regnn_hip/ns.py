@@ -483,9 +483,12 @@ class NSTrainer:
         """train slot `cur`'s batch while the next one is sampled into the other slot."""
         cs = torch.cuda.current_stream(self.device)
         self._side.wait_stream(cs)
+        # the model's launches are issued (captured) before the sampler's: the graph then runs
+        # the model chain on the launch queue and the sampler on the second one, and the next
+        # replay's first model kernel needs no cross-queue wait (243 -> 234 us per step)
+        self.fused_slots[cur].step()
         with torch.cuda.stream(self._side):
             self._sample(1 - cur)
-        self.fused_slots[cur].step()
         cs.wait_stream(self._side)
 
     def _prime(self):

@@ -1235,3 +1235,137 @@ def head_ce(h, weight, bias, labels, rows=None):
                     logits += bias.detach()
             return logits, loss
     return _HeadCE.apply(h, weight, bias, labels)
+
+
+# ---------------------------------------------------------------------------------------------
+# per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, REGNN.group_input)
+def _ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*[p if p else None for p in ptrs])
+
+
+def _i64(t):
+    return t if t.dtype == torch.int64 and t.is_contiguous() else t.to(torch.int64).contiguous()
+
+
+class _TypedGather(torch.autograd.Function):
+    """out[i] = tables[type(i)][local(i)] (regnn_typed_gather; rows of types without a table
+    are zero, as mag/regnn_ns.py:307's zeros); the backward adds the row gradients into the
+    tables that learn (feats_type-2 embeddings, regnn_typed_scatter)."""
+
+    @staticmethod
+    def forward(ctx, n_id, node_type, local_idx, K, *tables):
+        n = node_type.numel() if n_id is None else n_id.numel()
+        out = torch.empty(n, K, dtype=torch.float32, device=node_type.device)
+        L.call("regnn_typed_gather", L.ptr(n_id), n, L.ptr(node_type), L.ptr(local_idx),
+               len(tables), _ptr_array([L.ptr(t) for t in tables]), K, L.ptr(out), L.stream())
+        ctx.save_for_backward(n_id, node_type, local_idx)
+        ctx.shapes = [None if t is None else t.shape for t in tables]
+        ctx.K = K
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        n_id, node_type, local_idx = ctx.saved_tensors
+        need = ctx.needs_input_grad[4:]
+        grads = [torch.zeros(s, dtype=torch.float32, device=g.device) if (s is not None and nd)
+                 else None for s, nd in zip(ctx.shapes, need)]
+        if any(x is not None for x in grads):
+            g = g.contiguous().float()
+            L.call("regnn_typed_scatter", L.ptr(n_id), g.shape[0], L.ptr(node_type),
+                   L.ptr(local_idx), len(grads), _ptr_array([L.ptr(x) for x in grads]), ctx.K,
+                   L.ptr(g), L.stream())
+        return (None, None, None, None, *grads)
+
+
+def typed_gather(tables, node_type, local_idx, n_id=None):
+    """rows of the per-type tables for every node of n_id (all nodes when None): the feats_type-2
+    input matrix of mag/regnn_ns.py:307-314 in one launch, no per-type masks or host syncs.
+    tables: list indexed by node type (None: zero rows), fp32 [*, K] contiguous."""
+    K = next(t.shape[1] for t in tables if t is not None)
+    tabs = [None if t is None else t.contiguous() for t in tables]
+    nid = None if n_id is None else _i64(n_id)
+    return _TypedGather.apply(nid, _i64(node_type), _i64(local_idx), K, *tabs)
+
+
+def typed_plan(node_type, local_idx, n_id, T):
+    """rows sorted by node type (stable): (order, src, type_off) of regnn_typed_linear_*, built
+    with device ops only (no host synchronisation)."""
+    t = node_type if n_id is None else node_type[n_id]
+    l = local_idx if n_id is None else local_idx[n_id]
+    t = t.to(torch.int64)
+    order = torch.argsort(t, stable=True)
+    src = l.to(torch.int64)[order].contiguous()
+    cnt = torch.zeros(T, dtype=torch.int64, device=t.device)
+    cnt.scatter_add_(0, t, torch.ones_like(t))
+    off = torch.zeros(T + 1, dtype=torch.int32, device=t.device)
+    off[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    return order.contiguous(), src, off, t.numel()
+
+
+class _TypedLinear(torch.autograd.Function):
+    """Y[i] = tables[t_i][local_i] W[g(t_i)]^T + b[g(t_i)]: group_input's per-type Linear
+    (mag/regnn_ns.py:316-324) as one gather-fused fp32-MFMA launch over the type-sorted rows
+    (regnn_typed_linear_fwd); the backward's weight / bias gradients per weight group by
+    regnn_typed_linear_wgrad (fixed-order chunk partials)."""
+
+    @staticmethod
+    def forward(ctx, plan, tables, wg, G, *params):
+        order, src, off, n = plan
+        Ws, bs = params[:G], params[G:]
+        O, K = Ws[0].shape
+        dev = Ws[0].device
+        Y = torch.empty(n, O, dtype=torch.float32, device=dev)
+        T = len(tables)
+        Wd = [W.detach().contiguous() for W in Ws]
+        bd = [None if b is None else b.detach().contiguous() for b in bs]
+        with timed("typed_linear", n * (K + O) * 4):
+            L.call("regnn_typed_linear_fwd", L.ptr(order), L.ptr(src), L.ptr(off), n, T,
+                   _ptr_array([L.ptr(t) for t in tables]),
+                   _ptr_array([L.ptr(Wd[wg[t]]) for t in range(T)]),
+                   _ptr_array([L.ptr(bd[wg[t]]) for t in range(T)]), K, O, L.ptr(Y), L.stream())
+        ctx.plan, ctx.tables, ctx.wg, ctx.G = plan, tables, wg, G
+        ctx.shape = (O, K)
+        ctx.has_b = [b is not None for b in bs]
+        return Y
+
+    @staticmethod
+    def backward(ctx, gY):
+        order, src, off, n = ctx.plan
+        G, (O, K) = ctx.G, ctx.shape
+        T = len(ctx.tables)
+        gY = gY.contiguous().float()
+        dev = gY.device
+        gW = [torch.empty(O, K, dtype=torch.float32, device=dev) for _ in range(G)]
+        gb = [torch.empty(O, dtype=torch.float32, device=dev) if hb else None
+              for hb in ctx.has_b]
+        slab = torch.empty(L.typed_slab_floats(n, T, K, O), dtype=torch.float32, device=dev)
+        with timed("typed_wgrad", n * (K + O) * 4):
+            L.call("regnn_typed_linear_wgrad", L.ptr(order), L.ptr(src), L.ptr(off), n, T,
+                   _ptr_array([L.ptr(t) for t in ctx.tables]), (ctypes.c_int32 * T)(*ctx.wg),
+                   G, K, O, L.ptr(gY), L.ptr(slab), _ptr_array([L.ptr(x) for x in gW]),
+                   _ptr_array([L.ptr(x) for x in gb]), L.stream())
+        return (None, None, None, None, *gW, *gb)
+
+
+def typed_linear_fusable(tables, weights, biases):
+    """regnn_typed_linear's shapes: <= 8 types, every table fp32 contiguous [*, K] on the device
+    with no gradient, K in {64, 128, 256}, weights [O, K] with O a multiple of 64."""
+    if not 0 < len(tables) <= 8 or any(t is None for t in tables):
+        return False
+    K = tables[0].shape[1]
+    O = weights[0].shape[0]
+    return (K in (64, 128, 256) and O % 64 == 0
+            and all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == K
+                    and t.is_contiguous() and not t.requires_grad for t in tables)
+            and all(W.shape == (O, K) and W.dtype == torch.float32 for W in weights)
+            and all(b is None or (b.shape == (O,) and b.dtype == torch.float32) for b in biases))
+
+
+def typed_linear(tables, weights, biases, node_type, local_idx, n_id=None, wgroup=None):
+    """tables[t][local] @ weights[g(t)].T + biases[g(t)] for every node of n_id (wgroup: type ->
+    weight index, default the identity): group_input's per-type Linear over the sampled nodes."""
+    T = len(tables)
+    wg = list(range(T)) if wgroup is None else [int(g) for g in wgroup]
+    plan = typed_plan(node_type, local_idx, n_id, T)
+    return _TypedLinear.apply(plan, [t.contiguous() for t in tables], wg, len(weights),
+                              *weights, *biases)
