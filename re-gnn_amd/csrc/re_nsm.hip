@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
                     my_w = tab[A.rel[c0 + l]];
                 }
                 // UN edges' rows in flight per lane, then their accumulation in edge order
-                constexpr int UN = 4;
+                constexpr int UN = 8;
                 for (int j = 0; j < m; j += UN) {
                     int t[UN];
                     float wt[UN];
@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             const int m = min(16, e1 - c0);
             const int my_u = l < m ? A.idx[c0 + l] : 0;
             const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
-            constexpr int UN = 4;
+            constexpr int UN = 8;
             for (int j = 0; j < m; j += UN) {
                 float4 x[UN];
                 float wt[UN];
@@ -1065,7 +1065,7 @@ __global__ void __launch_bounds__(kBlock) rel0_kernel(Rel0Args A) {
                 my_r = int(A.rel[c0 + l]);
             }
             const int lo_lo = int(uint32_t(uint64_t(my_lo))), lo_hi = int(uint64_t(my_lo) >> 32);
-            constexpr int UN = 4;                  // edges in flight per lane
+            constexpr int UN = 8;                  // edges in flight per lane
             for (int j = 0; j < m; j += UN) {
                 int r[UN];
                 float dsum[UN];

@@ -18,7 +18,8 @@ if not os.path.exists(LIB):
         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
         "There is no CPU fallback.")
 
-_so = ctypes.CDLL(LIB)
+# REGNN_LIB: another build of the same ABI (A/B measurements of kernel variants, tools/ab_lib.sh)
+_so = ctypes.CDLL(os.environ.get("REGNN_LIB", LIB))
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32

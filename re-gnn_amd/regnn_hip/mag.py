@@ -66,22 +66,32 @@ class REGCNConv(torch.nn.Module):
     def forward(self, x, edge_index, edge_type=None, target_node_type=None,
                 return_weights=False):
         x_src, x_target = x
-        xs = torch.matmul(x_src, self.weight)                                    # :102
         tab = F.leaky_relu(self.relation_weight * self.scaling_factor)           # :110-111
         # mean of ew * x_j over in-edges incl. self loops, + bias (:113,129,142-148); the
         # use_softmax / degree-normalised ew of :116-126 is computed there but propagate() gets
         # the raw edge_weight, so neither changes the output (only return_weights shows ew)
         if getattr(edge_index, "is_ns_block", False):             # device-sampled block
-            blk = edge_index
-            out = ops.ns_spmm(blk, xs, tab, bias=self.bias)
+            # aggregate first, project second: mean_e(ew x_j) W = mean_e(ew (x_j W)) (the
+            # reference projects every source row first, :101-107), so the GEMM and its two
+            # backward GEMMs run over the block's targets, not its sources (~11x fewer rows at
+            # fan-out [25, 20]); the residual x_target W folds into the same product (:104,131)
+            agg = ops.ns_spmm(edge_index, x_src, tab)
+            if self.residual:
+                agg = agg + x_target
+            out = torch.addmm(self.bias, agg, self.weight)
+            if self.use_norm in ('bn', 'ln'):
+                out = self.norm(out)                                             # :134-135
+            if return_weights:
+                return out, self._edge_weights(edge_index, edge_type, target_node_type, tab,
+                                               x_target.shape[0]), tab
+            return out
+        xs = torch.matmul(x_src, self.weight)                                    # :102
+        if isinstance(edge_index, tuple):           # pre-built (RelGraph, RelPack) block
+            rg, pack = edge_index
         else:
-            if isinstance(edge_index, tuple):       # pre-built (RelGraph, RelPack) block
-                rg, pack = edge_index
-            else:
-                rg, pack = make_block(edge_index, edge_type, target_node_type, x_src.shape[0],
-                                      x_target.shape[0], self.num_edge_types,
-                                      self.self_loop_type)
-            out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
+            rg, pack = make_block(edge_index, edge_type, target_node_type, x_src.shape[0],
+                                  x_target.shape[0], self.num_edge_types, self.self_loop_type)
+        out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
         if self.residual:
             out = out + torch.matmul(x_target, self.weight)                      # :104,131-132
         if self.use_norm in ('bn', 'ln'):
