@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 26). */
+/* ABI version (bumped on any signature change or addition; currently 27). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -638,6 +638,12 @@ typedef struct regnn_nsm_params {
     float* g_out_w;
     float* g_out_b;
     float* loss;              /* [1]: mean nll over the batch targets with a label >= 0 */
+    int32_t n_edge_types;     /* relations < n_edge_types are edges; n_edge_types + type: self loops */
+    int32_t rel_slots;        /* 1: every (target type, source type) pair has at most one edge
+                                 relation (the caller checked the graph once): layer 0 sums its
+                                 rows per source type unweighted and the relation-table gradient
+                                 comes from those sums (no second pass over the edges; needs
+                                 u_self / u_rel); 0: the edge pass */
 } regnn_nsm_params;
 
 typedef struct regnn_nsm_work {
@@ -670,6 +676,8 @@ typedef struct regnn_nsm_work {
     float* beta;              /* cap[L-1] * T */
     float* nvalid;            /* 1 float: labelled targets of the batch */
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
+    float* u_self;            /* rel_slots: cap[L-1] * k_in, each row's self-loop input row */
+    int32_t* u_rel;           /* rel_slots: cap[L-1] * (T + 1), relation of each source-type slot */
 } regnn_nsm_work;
 
 /* Floats of the per-block partial slab regnn_nsm_step needs for these parameters and a batch

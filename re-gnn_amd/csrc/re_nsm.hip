@@ -157,6 +157,10 @@ struct Agg0Args {
     const int32_t* n_id; const int64_t* labels; float* nvalid;
     float* s_agg; float* s_w;
     float* a; float* stats; float* xs_next; float* gxs_next;
+    // relation-slot mode (RS): s_agg / s_w hold the unweighted sums / counts of the non-self
+    // edges per source type, u_self the self loop's input row, u_rel [n][T + 1] the relation of
+    // each slot (-1: none; slot T: the self loop)
+    int n_et; float* u_self; int32_t* u_rel;
 };
 
 // LDS: S tile [16][T*K + 4] (after the projection: W_1 [64][64] and the h rows [16][64]) |
@@ -167,7 +171,12 @@ inline size_t agg0_lds(int T, int K) {
            sizeof(float);
 }
 
-template <int K, int NT>                   // NT: per-type register accumulators (T <= NT <= MT)
+// RS (relation slots, when every (target type, source type) pair has at most one relation
+// besides the self loop): the input rows are summed per source type WITHOUT the relation weight
+// (U_vt; the self loop's row x_v kept apart), so that S_vt = tab[r_vt] U_vt + [t = type(v)]
+// tab[r_self] x_v and the relation-table gradient needs no second gather of the edges' rows:
+// d tab[r_vt] = <U_vt, Z_vt> + cnt_vt beta_vt, d tab[r_self] = <x_v, Z_v,type(v)> + beta (bwd0).
+template <int K, int NT, bool RS>          // NT: per-type register accumulators (T <= NT <= MT)
 __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
     constexpr int KB = K / 16;             // float4 steps of the projection per type
@@ -208,34 +217,43 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
         // tile per edge)
         float wsum[NT];
         float4 racc[NT][VPL];
+        int rel_t[NT];                             // RS: each slot's relation (-1: none)
+        float4 xself[VPL];                         // RS: the self loop's input row
+        int r_self = -1;
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
             wsum[tt] = 0.f;
+            rel_t[tt] = -1;
 #pragma unroll
             for (int p = 0; p < VPL; ++p) racc[tt][p] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#pragma unroll
+        for (int p = 0; p < VPL; ++p) xself[p] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (v < n) {
             const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
             for (int c0 = e0; c0 < e1; c0 += 16) {
                 const int m = min(16, e1 - c0);
                 int my_t = 0, my_lo = 0;           // table rows < 2^31 (checked by the host)
                 float my_w = 0.f;
+                int my_r = 0;
                 if (l < m) {
                     my_t = A.edge_type[c0 + l];
                     my_lo = int(A.edge_off[c0 + l]);
-                    my_w = tab[A.rel[c0 + l]];
+                    my_r = A.rel[c0 + l];
+                    my_w = tab[my_r];
                 }
                 // UN edges' rows in flight per lane, then their accumulation in edge order
                 constexpr int UN = 8;
                 for (int j = 0; j < m; j += UN) {
-                    int t[UN];
+                    int t[UN], ru[UN];
                     float wt[UN];
                     float4 x[UN][VPL];
 #pragma unroll
                     for (int u = 0; u < UN; ++u) {
                         const int jj = min(j + u, m - 1);
                         t[u] = __shfl(my_t, gl + jj, 64);
-                        wt[u] = __shfl(my_w, gl + jj, 64);
+                        if constexpr (RS) ru[u] = __shfl(my_r, gl + jj, 64);
+                        else wt[u] = __shfl(my_w, gl + jj, 64);
                         const int64_t lo = __shfl(my_lo, gl + jj, 64);
                         const float* xr = pick(A.xt.p, t[u]) + lo * K + 4 * l;
 #pragma unroll
@@ -245,36 +263,77 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
 #pragma unroll
                     for (int u = 0; u < UN; ++u) {
                         if (t[u] < 0) continue;
+                        if constexpr (RS) {
+                            if (ru[u] >= A.n_et) {         // the self loop (one per row)
+                                r_self = ru[u];
+#pragma unroll
+                                for (int p = 0; p < VPL; ++p) xself[p] = x[u][p];
+                                continue;
+                            }
+                        }
 #pragma unroll
                         for (int tt = 0; tt < NT; ++tt) {
                             if (tt != t[u]) continue;
-                            wsum[tt] += wt[u];
+                            if constexpr (RS) {
+                                wsum[tt] += 1.f;
+                                rel_t[tt] = ru[u];
 #pragma unroll
-                            for (int p = 0; p < VPL; ++p) {
-                                racc[tt][p].x = fmaf(wt[u], x[u][p].x, racc[tt][p].x);
-                                racc[tt][p].y = fmaf(wt[u], x[u][p].y, racc[tt][p].y);
-                                racc[tt][p].z = fmaf(wt[u], x[u][p].z, racc[tt][p].z);
-                                racc[tt][p].w = fmaf(wt[u], x[u][p].w, racc[tt][p].w);
+                                for (int p = 0; p < VPL; ++p) {
+                                    racc[tt][p].x += x[u][p].x;
+                                    racc[tt][p].y += x[u][p].y;
+                                    racc[tt][p].z += x[u][p].z;
+                                    racc[tt][p].w += x[u][p].w;
+                                }
+                            } else {
+                                wsum[tt] += wt[u];
+#pragma unroll
+                                for (int p = 0; p < VPL; ++p) {
+                                    racc[tt][p].x = fmaf(wt[u], x[u][p].x, racc[tt][p].x);
+                                    racc[tt][p].y = fmaf(wt[u], x[u][p].y, racc[tt][p].y);
+                                    racc[tt][p].z = fmaf(wt[u], x[u][p].z, racc[tt][p].z);
+                                    racc[tt][p].w = fmaf(wt[u], x[u][p].w, racc[tt][p].w);
+                                }
                             }
                         }
                     }
                 }
             }
         }
+        const int tau = r_self - A.n_et;           // RS: the row's node type
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
             if (tt < T) {
+                float wr = 1.f, ws = 0.f;              // RS: S = wr U + ws x_self
+                if constexpr (RS) {
+                    wr = rel_t[tt] >= 0 ? tab[rel_t[tt]] : 0.f;
+                    ws = (tt == tau) ? tab[r_self] : 0.f;
+                }
 #pragma unroll
                 for (int p = 0; p < VPL; ++p) {
-                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = racc[tt][p];
+                    float4 sv = racc[tt][p];
+                    if constexpr (RS)
+                        sv = make_float4(fmaf(ws, xself[p].x, wr * sv.x), fmaf(ws, xself[p].y, wr * sv.y),
+                                         fmaf(ws, xself[p].z, wr * sv.z), fmaf(ws, xself[p].w, wr * sv.w));
+                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = sv;
                     if (v < n)
                         *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l + 64 * p) =
                             racc[tt][p];
                 }
                 if (l == 0) {
-                    sw[sub * MT + tt] = wsum[tt];
-                    if (v < n) A.s_w[int64_t(v) * T + tt] = wsum[tt];
+                    sw[sub * MT + tt] = RS ? fmaf(wr, wsum[tt], ws) : wsum[tt];
+                    if (v < n) {
+                        A.s_w[int64_t(v) * T + tt] = wsum[tt];
+                        if constexpr (RS) A.u_rel[int64_t(v) * (T + 1) + tt] = rel_t[tt];
+                    }
                 }
+            }
+        }
+        if constexpr (RS) {
+            if (v < n) {
+#pragma unroll
+                for (int p = 0; p < VPL; ++p)
+                    *reinterpret_cast<float4*>(A.u_self + int64_t(v) * K + 4 * l + 64 * p) = xself[p];
+                if (l == 0) A.u_rel[int64_t(v) * (T + 1) + T] = r_self;
             }
         }
         __syncthreads();
@@ -909,6 +968,9 @@ struct Bwd0Args {
     const int32_t* sizes; int hop; int T;
     const float* inv; const float* ga; const float* s_agg; const float* s_w; const float* wc;
     float* z; float* beta; float* slab;
+    // relation-slot mode (bwd0_rs_kernel): layer 0's relation table, agg0's self rows and slot
+    // relations; relation dots -> rslab[t * gridDim.x + block][F]
+    const float* tab; const float* u_self; const int32_t* u_rel; int n_rel, n_et; float* rslab;
 };
 
 template <int K>
@@ -1031,6 +1093,204 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
             for (int i = 0; i < 4; ++i)
                 o[(16 * (KB * w + a) + 4 * q + i) * F + 16 * jb + c] = acc[a][jb][i];
     if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
+}
+
+// bwd0 in relation-slot mode (agg0<.., RS = true>): the S tile is re-formed per row as
+// wr U_vt + ws x_v (wr = tab[r_vt], ws = tab[r_self] when the row's type is t), the gradient
+// products as bwd0_kernel's, and the relation-table dots come from the same Z fragments:
+//   d tab[r_vt] += <U_vt, Z_vt> + cnt_vt beta_vt,   d tab[r_self] += <x_v, Z_vt> + beta_vt
+// (no Z / beta to HBM, no second pass over the edges). Row r of the tile keeps its own column
+// of the relation bins in LDS (fixed summation order: deterministic), one slab row per block.
+inline size_t bwd0_rs_lds(int K, int n_rel) {
+    return sizeof(float) * (size_t(K) * (F + 4) + F + 2 * 16 * (K + 4) + 16 * (F + 16) +
+                            16 * (F + 4) + F + 16 * 4 + 16 * 2 + 4 * 16 * 2 + size_t(n_rel) * 16);
+}
+
+template <int K>
+__global__ void __launch_bounds__(kBlock) bwd0_rs_kernel(Bwd0Args A) {
+    constexpr int XS = K + 4, GS = F + 16, G2 = F + 4, WS = F + 4;
+    constexpr int KB = K / 64;                // k blocks per wave
+    constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile
+    extern __shared__ float sm[];
+    float* Wk = sm;                           // [K][WS]
+    float* bc = Wk + K * WS;                  // [F]
+    float* ush = bc + F;                      // [16][XS] U_vt
+    float* xsh = ush + 16 * XS;               // [16][XS] x_v (self loop rows)
+    float* gsh = xsh + 16 * XS;               // [16][GS]
+    float* gs2 = gsh + 16 * GS;               // [16][G2]
+    float* tabl = gs2 + 16 * G2;              // [F]
+    float* rm = tabl + F;                     // [16][4]: wr, ws, cnt, beta
+    int* rr = reinterpret_cast<int*>(rm + 64);  // [16][2]: r_vt (or -1), r_self (or -1)
+    float* dred = reinterpret_cast<float*>(rr + 32);   // [4 waves][16][2]
+    float* bins = dred + 128;                 // [n_rel][16]
+    const int t = blockIdx.y, T = A.T;
+    const float* wct = A.wc + int64_t(t) * (K + 1) * F;
+    for (int e = threadIdx.x; e < K * F; e += kBlock) {      // wcT[j][k] -> Wk[k][j]
+        const int j = e / K, k = e - j * K;
+        Wk[k * WS + j] = wct[e];
+    }
+    if (threadIdx.x < F) {
+        bc[threadIdx.x] = wct[K * F + threadIdx.x];
+        tabl[threadIdx.x] = A.tab[threadIdx.x];
+    }
+    for (int i = threadIdx.x; i < A.n_rel * 16; i += kBlock) bins[i] = 0.f;
+    const int n = A.sizes[A.hop];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int gr = threadIdx.x >> 4, gj = threadIdx.x & 15;
+    f32x4 acc[KB][4];
+#pragma unroll
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) acc[a][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    float4 ur[XV], xr[XV], gv;
+    float cntv = 0.f;
+    int relv = -1, rsv = -1;
+    auto load = [&](int v0) {
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            const bool ok = v0 + r < n;
+            ur[u] = ok ? *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[u] = ok ? *reinterpret_cast<const float4*>(A.u_self + int64_t(v0 + r) * K + 4 * k4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int v = v0 + gr;
+        if (v < n) {
+            const float iv = A.inv[v];
+            const float4 g4 = *reinterpret_cast<const float4*>(A.ga + int64_t(v) * F + 4 * gj);
+            gv = make_float4(iv * g4.x, iv * g4.y, iv * g4.z, iv * g4.w);
+        } else {
+            gv = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (threadIdx.x < 16) {
+            const int vv = v0 + threadIdx.x;
+            const bool ok = vv < n;
+            cntv = ok ? A.s_w[int64_t(vv) * T + t] : 0.f;
+            relv = ok ? A.u_rel[int64_t(vv) * (T + 1) + t] : -1;
+            rsv = ok ? A.u_rel[int64_t(vv) * (T + 1) + T] : -1;
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile * 16 < n) load(tile * 16);
+    for (; tile * 16 < n; tile += gridDim.x) {
+        const int v0 = tile * 16;
+        if (threadIdx.x < 16) {                // row meta: S = wr U + ws x_self
+            const bool self = rsv >= 0 && rsv - A.n_et == t;
+            const float wr = relv >= 0 ? tabl[relv] : 0.f;
+            const float ws = self ? tabl[rsv] : 0.f;
+            rm[4 * threadIdx.x] = wr;
+            rm[4 * threadIdx.x + 1] = ws;
+            rm[4 * threadIdx.x + 2] = cntv;
+            rr[2 * threadIdx.x] = (relv >= 0 && cntv > 0.f) ? relv : -1;
+            rr[2 * threadIdx.x + 1] = self ? rsv : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            *reinterpret_cast<float4*>(ush + r * XS + 4 * k4) = ur[u];
+            *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[u];
+        }
+        *reinterpret_cast<float4*>(gsh + gr * GS + 4 * gj) = gv;
+        *reinterpret_cast<float4*>(gs2 + gr * G2 + 4 * gj) = gv;
+        __syncthreads();
+        if ((tile + gridDim.x) * 16 < n) load((tile + gridDim.x) * 16);
+        if (threadIdx.x < F) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bsum = fmaf(fmaf(rm[4 * r], rm[4 * r + 2], rm[4 * r + 1]), gsh[r * GS + threadIdx.x], bsum);
+        }
+        // gW partial over the re-formed S rows
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            const float wr = rm[4 * r], ws = rm[4 * r + 1];
+            float bv[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+#pragma unroll
+            for (int a = 0; a < KB; ++a) {
+                const int k = 16 * (KB * w + a) + c;
+                const float av = fmaf(ws, xsh[r * XS + k], wr * ush[r * XS + k]);
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
+            }
+        }
+        // Z fragments (wave w -> k blocks KB*w .. +KB-1) dotted with U and x_self
+        float pu[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < KB; ++a) {
+            const int kb = KB * w + a;
+            f32x4 zc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < F / 16; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
+                const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw.x, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw.y, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw.z, zc, 0, 0, 0);
+                zc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw.w, zc, 0, 0, 0);
+            }
+            // zc[r] = Z[row 4 q + r][k = 16 kb + c]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                pu[r] = fmaf(zc[r], ush[(4 * q + r) * XS + 16 * kb + c], pu[r]);
+                ps[r] = fmaf(zc[r], xsh[(4 * q + r) * XS + 16 * kb + c], ps[r]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            pu[r] = group_sum<16>(pu[r]);
+            ps[r] = group_sum<16>(ps[r]);
+        }
+        if (c == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                dred[(w * 16 + 4 * q + r) * 2] = pu[r];
+                dred[(w * 16 + 4 * q + r) * 2 + 1] = ps[r];
+            }
+        }
+        {                                      // beta_vt = <b_c[t], G_v>
+            const float4 g4 = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
+            float bt = bc[4 * gj] * g4.x + bc[4 * gj + 1] * g4.y + bc[4 * gj + 2] * g4.z +
+                       bc[4 * gj + 3] * g4.w;
+            bt = group_sum<16>(bt);
+            if (gj == 0) rm[4 * gr + 3] = bt;
+        }
+        __syncthreads();
+        if (threadIdx.x < 16) {                // row r's relation dots into its bin column
+            const int r = threadIdx.x;
+            const float du = ((dred[(0 * 16 + r) * 2] + dred[(1 * 16 + r) * 2]) +
+                              dred[(2 * 16 + r) * 2]) + dred[(3 * 16 + r) * 2];
+            const float ds = ((dred[(0 * 16 + r) * 2 + 1] + dred[(1 * 16 + r) * 2 + 1]) +
+                              dred[(2 * 16 + r) * 2 + 1]) + dred[(3 * 16 + r) * 2 + 1];
+            const float bt = rm[4 * r + 3];
+            if (rr[2 * r] >= 0) bins[rr[2 * r] * 16 + r] += fmaf(rm[4 * r + 2], bt, du);
+            if (rr[2 * r + 1] >= 0) bins[rr[2 * r + 1] * 16 + r] += ds + bt;
+        }
+        __syncthreads();
+    }
+    float* o = A.slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
+#pragma unroll
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                o[(16 * (KB * w + a) + 4 * q + i) * F + 16 * jb + c] = acc[a][jb][i];
+    if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
+    __syncthreads();
+    if (threadIdx.x < F) {
+        float sr = 0.f;
+        if (threadIdx.x < A.n_rel)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sr += bins[threadIdx.x * 16 + r];
+        A.rslab[(int64_t(t) * gridDim.x + blockIdx.x) * F + threadIdx.x] = sr;
+    }
 }
 
 // rel0 (layer 0 backward, the edge half): d tab[r] = sum_{e: rel_e = r} inv_v <ga_v, xs0[u_e]>
@@ -1269,8 +1529,9 @@ inline SlabLayout slab_layout(const regnn_nsm_params* p, int cap0) {
     SlabLayout s{};
     int64_t o = 0;
     for (int l = 0; l < ML; ++l) {        // relation dots of layer l: rel0 (l = 0), agg_bwd
-        s.rel[l] = o;
-        if (l < p->n_layers) o += int64_t(kAggBlocks) * F;
+        s.rel[l] = o;                     // layer 0: rel0's or bwd0_rs's (T x kProjBlocks) rows
+        if (l < p->n_layers)
+            o += int64_t(l == 0 && kProjBlocks * MT > kAggBlocks ? kProjBlocks * MT : kAggBlocks) * F;
     }
     for (int l = 0; l < ML; ++l) {        // post_bwd of layer l < L-1
         s.post[l] = o;
@@ -1360,6 +1621,11 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     }
     const SlabLayout S = slab_layout(p, w->cap[0]);
     const Drop drop = make_drop(p->p_drop);
+    // relation-slot mode: the caller vouches that every (target type, source type) pair has at
+    // most one relation besides the self loops (relation ids >= n_edge_types)
+    const bool rs = p->rel_slots != 0;
+    if (rs && (!w->u_self || !w->u_rel || p->n_edge_types < 0 || p->n_edge_types + T > p->n_rel[0]))
+        return REGNN_EINVAL;
     Ptrs lin_w{}, lin_b{}, xt{}, rw{};
     for (int t = 0; t < T; ++t) {
         lin_w.p[t] = p->lin_w[t];
@@ -1386,18 +1652,21 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         A.state = w->state; A.drop = drop; A.w_next = p->conv_w[1];
         A.s_agg = w->s_agg; A.s_w = w->s_w;
         A.a = w->a[0]; A.stats = w->stats[0]; A.xs_next = w->xs[1]; A.gxs_next = w->gxs[1];
+        A.n_et = p->n_edge_types; A.u_self = w->u_self; A.u_rel = w->u_rel;
         int grid = (w->cap[h] + 15) / 16;
         if (grid > 2048) grid = 2048;
         const size_t lds = agg0_lds(T, K);
-#define AGG0_CASE(KK, NN)                                                                      \
-        if (K == KK && (NN == MT || T <= NN)) {                                                \
+#define AGG0_CASE(KK, NN, RS)                                                                  \
+        if (K == KK && (NN == MT || T <= NN) && rs == RS) {                                    \
             static size_t done = 0;                                                            \
-            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<KK, NN>), lds, &done))     \
+            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<KK, NN, RS>), lds, &done)) \
                 return REGNN_EUNSUPPORTED;                                                     \
-            hipLaunchKernelGGL((agg0_kernel<KK, NN>), dim3(grid), dim3(kBlock), lds, stream, A); \
+            hipLaunchKernelGGL((agg0_kernel<KK, NN, RS>), dim3(grid), dim3(kBlock), lds, stream, A); \
             REGNN_LAUNCH_CHECK();                                                              \
         } else
-        AGG0_CASE(128, 4) AGG0_CASE(128, MT) AGG0_CASE(64, 4) AGG0_CASE(64, MT)
+        AGG0_CASE(128, 4, true) AGG0_CASE(128, MT, true) AGG0_CASE(64, 4, true)
+        AGG0_CASE(64, MT, true) AGG0_CASE(128, 4, false) AGG0_CASE(128, MT, false)
+        AGG0_CASE(64, 4, false) AGG0_CASE(64, MT, false)
             return REGNN_EUNSUPPORTED;
 #undef AGG0_CASE
     }
@@ -1464,11 +1733,28 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         B.inv = w->blk_inv[h]; B.ga = w->ga[0]; B.s_agg = w->s_agg; B.s_w = w->s_w; B.wc = w->wc;
         B.z = w->z; B.beta = w->beta; B.slab = w->slab + S.proj;
         const dim3 grid(kProjBlocks, T);
-        if (K == 128)
+        if (rs) {
+            B.tab = w->tabs; B.u_self = w->u_self; B.u_rel = w->u_rel;
+            B.n_rel = p->n_rel[0]; B.n_et = p->n_edge_types; B.rslab = w->slab + S.rel[0];
+            const size_t lds = bwd0_rs_lds(K, p->n_rel[0]);
+            static size_t done128 = 0, done64 = 0;
+            const void* kfn = K == 128 ? reinterpret_cast<const void*>(&bwd0_rs_kernel<128>)
+                                       : reinterpret_cast<const void*>(&bwd0_rs_kernel<64>);
+            if (!set_lds(kfn, lds, K == 128 ? &done128 : &done64)) return REGNN_EUNSUPPORTED;
+            if (K == 128)
+                hipLaunchKernelGGL(bwd0_rs_kernel<128>, grid, dim3(kBlock), lds, stream, B);
+            else
+                hipLaunchKernelGGL(bwd0_rs_kernel<64>, grid, dim3(kBlock), lds, stream, B);
+            REGNN_LAUNCH_CHECK();
+        } else if (K == 128) {
             hipLaunchKernelGGL(bwd0_kernel<128>, grid, dim3(kBlock), 0, stream, B);
-        else
+        } else {
             hipLaunchKernelGGL(bwd0_kernel<64>, grid, dim3(kBlock), 0, stream, B);
+        }
         REGNN_LAUNCH_CHECK();
+    }
+    if (!rs) {
+        const int h = L - 1;
         Rel0Args R{};
         R.sizes = w->sizes; R.hop = h; R.T = T;
         R.ptr = w->blk_ptr[h]; R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
@@ -1494,8 +1780,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         J.add(hp + int64_t(C) * (F + 1) + 2 * F, hw, nh, F, p->g_ln_w[L - 1]);
         J.add(hp + int64_t(C) * (F + 1) + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
         for (int l = 0; l < L; ++l)
-            J.add(w->slab + S.rel[l], F, kAggBlocks, p->n_rel[l], p->g_conv_rw[l], kOpRel,
-                  p->conv_rw[l]);
+            J.add(w->slab + S.rel[l], F, (l == 0 && rs) ? kProjBlocks * T : kAggBlocks,
+                  p->n_rel[l], p->g_conv_rw[l], kOpRel, p->conv_rw[l]);
         for (int l = 0; l + 1 < L; ++l) {
             const float* pp = w->slab + S.post[l];
             J.add(pp, kPostW, kPostBlocks, F * F, p->g_conv_w[l + 1]);

@@ -218,7 +218,8 @@ class _NsmParams(ctypes.Structure):
                 ("ln_w", _P * _ML), ("ln_b", _P * _ML), ("out_w", _P), ("out_b", _P),
                 ("g_lin_w", _P * _MT), ("g_lin_b", _P * _MT), ("g_conv_w", _P * _ML),
                 ("g_conv_b", _P * _ML), ("g_conv_rw", _P * _ML), ("g_ln_w", _P * _ML),
-                ("g_ln_b", _P * _ML), ("g_out_w", _P), ("g_out_b", _P), ("loss", _P)]
+                ("g_ln_b", _P * _ML), ("g_out_w", _P), ("g_out_b", _P), ("loss", _P),
+                ("n_edge_types", ctypes.c_int32), ("rel_slots", ctypes.c_int32)]
 
 
 class _NsmWork(ctypes.Structure):
@@ -228,7 +229,8 @@ class _NsmWork(ctypes.Structure):
                 ("blk_inv", _P * _ML), ("ntype", _P), ("local", _P), ("labels", _P),
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
-                ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P)]
+                ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
+                ("u_self", _P), ("u_rel", _P)]
 
 
 def fused_unsupported(model, x_dict):
@@ -259,6 +261,40 @@ def fused_unsupported(model, x_dict):
     if model.out_lin.weight.shape[0] > 448 or model.out_lin.weight.shape[1] != 64:
         return "out_lin must be 64 -> <= 448"
     return None
+
+
+# "auto": layer 0's relation-slot mode wherever the graph allows it; "off": the edge pass
+# (rel0) always (tests compare the two)
+REL_SLOTS = {"mode": "auto"}
+
+
+def relation_slots_ok(sampler, T):
+    """regnn_nsm_params.rel_slots: True when every (target type, source type) pair of the graph
+    has at most one edge relation (ogbn-mag's typed relations: each edge type joins one source
+    type to one target type), so layer 0 may sum its input rows per source type unweighted.
+    One pass over the graph's edges, cached on the graph."""
+    rg = sampler.rg
+    key = ("_regnn_rel_slots", sampler.num_edge_types, T)
+    cache = getattr(rg, "_regnn_rel_slots", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    dev = rg.device
+    ptr = rg.csr_ptr.to(torch.int64)
+    present = torch.zeros(_MT * _MT * 256, dtype=torch.bool, device=dev)
+    step = 1 << 26
+    for a in range(0, rg.E, step):
+        b = min(rg.E, a + step)
+        pos = torch.arange(a, b, device=dev)
+        dst = torch.searchsorted(ptr, pos, right=True) - 1
+        st = sampler.ntype[rg.csr_idx[a:b].to(torch.int64)].to(torch.int64)
+        dt = sampler.ntype[dst].to(torch.int64)
+        r = sampler.etype_csr[a:b].to(torch.int64)
+        ok = (st >= 0) & (st < T) & (dt >= 0) & (dt < T)
+        present[((dt * _MT + st) * 256 + r)[ok]] = True
+    per_pair = present.view(_MT * _MT, 256).sum(1)
+    ok = bool((per_pair <= 1).all().item())
+    rg._regnn_rel_slots = (key, ok)
+    return ok
 
 
 class FusedStep:
@@ -336,6 +372,11 @@ class FusedStep:
         W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
         W.nvalid = ptr(z(1))
+        P.n_edge_types = int(sampler.num_edge_types)
+        P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))
+        if P.rel_slots:
+            W.u_self = ptr(z(n0, K))
+            W.u_rel = ptr(torch.full((n0, T + 1), -1, dtype=torch.int32, device=dev))
         W.slab = ptr(z(_slab_floats(P, caps[0])))
         self.model, self.sampler, self.n_layers = model, sampler, nl
 

@@ -308,13 +308,18 @@ def _nsm_seed(st, layer):
     return _mix((st[0] & M) ^ _mix(((st[1] << 40) ^ (st[3] << 8) ^ (layer + 0x51ED27)) & M))
 
 
+@pytest.mark.parametrize("rel_slots", ["auto", "off"])
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
-def test_fused_step_matches_module_path(monkeypatch, dropout):
+def test_fused_step_matches_module_path(monkeypatch, dropout, rel_slots):
     """regnn_nsm_step (the model's forward / nll / backward in eight launches) against the
     mag.REGNN autograd path on the same sampled batch: loss and every parameter gradient at
-    1e-5. With dropout the module path gets the fused step's hash masks (oracle.dropout_mask of
-    the documented per-layer seed) in place of torch's RNG."""
+    1e-5, with layer 0's relation-table gradient from the per-source-type slot sums (the
+    ogbn-mag schema allows it) and from the edge pass. With dropout the module path gets the
+    fused step's hash masks (oracle.dropout_mask of the documented per-layer seed) in place of
+    torch's RNG."""
     from oracle import regnn_oracle as O
+    from regnn_hip import ns
+    monkeypatch.setitem(ns.REL_SLOTS, "mode", rel_slots)
     d = _mag(0.003, seed=6, F=128, hidden=64, classes=37, dropout=dropout)
     m_mod, m_fus = d["model"](1), d["model"](1)
     m_mod.train(); m_fus.train()
@@ -322,6 +327,7 @@ def test_fused_step_matches_module_path(monkeypatch, dropout):
     tr_m.fused = None                                   # the module (autograd) path
     tr_f, _ = _setup_trainer(d, m_fus, batch=96, sizes=(7, 5))
     assert tr_f.fused is not None
+    assert tr_f.fused.P.rel_slots == (1 if rel_slots == "auto" else 0)
     tr_f._forward_backward()
     torch.cuda.synchronize()
     st = tr_f.sampler.state.cpu().tolist()

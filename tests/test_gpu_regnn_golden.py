@@ -67,7 +67,9 @@ def test_regnn_autograd_path_vs_reference(name):
 
 def test_regnn_fused_step_vs_reference():
     """regnn_ns_hop reproduces the fixture's sampled batch; regnn_nsm_step's loss and every
-    gradient match the reference REGNN's."""
+    gradient match the reference REGNN's. (The fixture's relations are drawn at random, not
+    one per (target type, source type) pair, so layer 0 takes the edge pass here; the
+    relation-slot mode is checked on the ogbn-mag-shaped graphs of test_gpu_ns_engine.py.)"""
     from regnn_hip.graph import RelGraph
     from regnn_hip.ns import DeviceSampler, FusedStep
     d = G.load("mag_regnn_ft3")
@@ -85,6 +87,7 @@ def test_regnn_fused_step_vs_reference():
     y_flat[:m["counts"][0]] = torch.from_numpy(d["y"])
     loss = torch.zeros((), device=DEV)
     fs = FusedStep(model, ds, x_dict, nt, loc, y_flat, loss)
+    assert fs.P.rel_slots == 0
     with pytest.raises(RuntimeError):                  # the hops have not run since
         fs.step()
     ds.set_seed(m["seed"], m["epoch"], m["batch_idx"])
