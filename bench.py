@@ -155,7 +155,7 @@ def run_ns_epoch(args, dev):
                                             "cores, hidden 512, real ogbn-mag"}}
 
 
-def ns_step_bytes(sz, K, C, L=2, F=64, T=4):
+def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False):
     """algorithmic HBM bytes of one fused NS model step (regnn_nsm_step) at the sampled sizes
     sz (regnn_ns_hop sizes: sz[h] = rows after h hops, sz[8 + h] = edges of hop h's block,
     self loops included): every row / index / feature byte a kernel must read or write once.
@@ -164,14 +164,21 @@ def ns_step_bytes(sz, K, C, L=2, F=64, T=4):
              + 3*F*4 a, xs_next, gxs_next + 16 stats / ptr / inv)
       bwd0   n x (T*K*4 S + F*4 ga + T*K*4 Z + T*8 w / beta + 4)
       rel0   E x (K*4 input row again + 13) + n x (T*K*4 Z + T*4 beta)
+    With rel_slots (regnn_nsm_params.rel_slots) agg0 also writes each row's self-loop input row
+    and slot relations (n x (K*4 + 4*(T+1))), bwd0 reads them back and writes no Z / beta
+    (n x (T*K*4 U + K*4 + 4*(T+1) + F*4 + 4*T + 4)), and there is no rel0.
     Layers 1 .. L-2: agg E x (F*4 + 5) + n x (4*F*4 + 20); agg_bwd E x (2*F*4 + 5) + n x (F*4 + 12).
     post_bwd of layers 0 .. L-2: n x (3*F*4 + 8). Head (layer L-1): E0 x (F*4 + 5) + n0 x (F*4 +
     24) + out_lin; its agg_bwd E0 x (2*F*4 + 5) + n0 x (F*4 + 12)."""
     f = 4 * F
     n, E = sz[L - 1], sz[8 + L - 1]
     b = E * (4 * K + 13) + n * (T * 4 * K + 4 * T + 3 * f + 16)       # agg0
-    b += n * (2 * T * 4 * K + f + 8 * T + 4)                            # bwd0
-    b += E * (4 * K + 13) + n * (T * 4 * K + 4 * T)                     # rel0
+    if rel_slots:
+        b += n * (4 * K + 4 * (T + 1))                                  # agg0: self rows, slots
+        b += n * (T * 4 * K + 4 * K + 4 * (T + 1) + f + 4 * T + 4)      # bwd0
+    else:
+        b += n * (2 * T * 4 * K + f + 8 * T + 4)                        # bwd0
+        b += E * (4 * K + 13) + n * (T * 4 * K + 4 * T)                 # rel0
     for l in range(1, L - 1):                                           # agg / agg_bwd
         h = L - 1 - l
         b += sz[8 + h] * (f + 5) + sz[h] * (4 * f + 20)
@@ -195,7 +202,8 @@ def run_ns(args, dev):
     for _ in range(5):
         tr.step()
         if tr.fused is not None:
-            nsm_bytes.append(ns_step_bytes(tr.sampler.sizes.cpu().tolist(), 128, 349))
+            nsm_bytes.append(ns_step_bytes(tr.sampler.sizes.cpu().tolist(), 128, 349,
+                                           rel_slots=bool(tr.fused.P.rel_slots)))
     torch.cuda.synchronize()
     kstats = profile.summary()
     profile.enable(False)
@@ -263,7 +271,8 @@ def run_ns(args, dev):
         launches, mean_ms, total_ms, _ = kstats["nsm_step"]
         b = statistics.mean(nsm_bytes)
         ach = b / (mean_ms / 1e3) / 1e9
-        res["ns_roofline"] = {"bound": "hbm", "kernel": "regnn_nsm_step (8 launches)",
+        nl = 7 if tr.fused.P.rel_slots else 8
+        res["ns_roofline"] = {"bound": "hbm", "kernel": f"regnn_nsm_step ({nl} launches)",
                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": ach / HBM_PEAK_GBS, "launch_ms": mean_ms,
                               "algorithmic_bytes_per_launch": b}

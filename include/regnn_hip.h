@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 27). */
+/* ABI version (bumped on any signature change or addition; currently 28). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -691,13 +691,14 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
 
 /* Adam step over flat buffers (replaces torch.optim.Adam.step, mag/regnn_ns.py:407, for
  * parameters laid out in one flat bucket): with weight decay wd the gradient is g + wd * p
- * (torch's L2 form), t = *step + 1, m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
+ * (torch's L2 form; g = grad_scale * grad, e.g. 1 / ranks after a SUM all-reduce, so the
+ * data-parallel mean needs no separate pass), t = *step + 1, m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
  * p -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps). *step (int64) and *ticket
  * (uint32, zero-filled once) live on the device; the launch advances *step itself, so a
  * captured graph needs no host update. */
 int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, float weight_decay,
-                    int64_t* step, uint32_t* ticket, hipStream_t stream);
+                    float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream);
 
 /* ---- Per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, group_input) ----
  * The reference builds the batch's input matrix with one boolean mask per node type (a host

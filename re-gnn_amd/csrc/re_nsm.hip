@@ -1487,7 +1487,7 @@ __global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
 __global__ void __launch_bounds__(kBlock)
 adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                  float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                 float wd, int64_t* __restrict__ step, unsigned* __restrict__ ticket) {
+                 float wd, float gscale, int64_t* __restrict__ step, unsigned* __restrict__ ticket) {
     __shared__ bool last;
     const int64_t t = step[0] + 1;
     const double bc1 = 1.0 - pow(double(b1), double(t));
@@ -1496,7 +1496,7 @@ adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __re
     const float bc2_sqrt = float(sqrt(bc2));
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n;
          i += int64_t(gridDim.x) * kBlock) {
-        float gi = g[i];
+        float gi = g[i] * gscale;              // gscale: 1 / ranks after a SUM all-reduce
         const float pi = p[i];
         if (wd != 0.f) gi = gi + wd * pi;
         const float mi = m[i], vi = v[i];
@@ -1816,13 +1816,13 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
 
 int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, float weight_decay,
-                    int64_t* step, uint32_t* ticket, hipStream_t stream) {
+                    float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream) {
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !ticket || n < 0) return REGNN_EINVAL;
     if (n == 0) return REGNN_OK;
     int64_t grid = (n + kBlock - 1) / kBlock;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(adam_flat_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, stream, param, grad,
-                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step, ticket);
+                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, grad_scale, step, ticket);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

@@ -92,7 +92,7 @@ _SIG = {
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
-    "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
+    "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
     "regnn_typed_gather": ([P, I64, P, P, I32, P, I32, P, P], ctypes.c_int),
     "regnn_typed_scatter": ([P, I64, P, P, I32, P, I32, P, P], ctypes.c_int),
     "regnn_typed_chunks": ([I64, I32, I32], I64),
@@ -108,7 +108,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 27
+ABI_VERSION = 28
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

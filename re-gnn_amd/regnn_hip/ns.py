@@ -413,11 +413,15 @@ class FlatAdam:
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), \
             float(weight_decay)
+        # the gradient's factor inside the launch (NSTrainer: 1 / ranks, the DP mean of the
+        # SUM all-reduce, with no separate division pass)
+        self.grad_scale = 1.0
 
     def step(self):
         L.call("regnn_adam_flat", L.ptr(self.p), L.ptr(self.g), L.ptr(self.m), L.ptr(self.v),
                self.p.numel(), self.lr, float(self.betas[0]), float(self.betas[1]), self.eps,
-               self.weight_decay, L.ptr(self.step_count), L.ptr(self.ticket), L.stream())
+               self.weight_decay, self.grad_scale, L.ptr(self.step_count), L.ptr(self.ticket),
+               L.stream())
 
 
 class NSTrainer:
@@ -464,6 +468,9 @@ class NSTrainer:
                 p.data = self.pflat[o:o + p.numel()].view_as(p)
                 o += p.numel()
             self.opt = opt = FlatAdam(self.pflat, self.flat, **(adam or {}))
+            # the data-parallel mean of the SUM all-reduce, inside Adam's launch: no division
+            # pass between the exchange and the update (p.grad holds the rank sum)
+            opt.grad_scale = 1.0 / self.world
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in eight HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
@@ -570,7 +577,8 @@ class NSTrainer:
         if self.world > 1:
             import torch.distributed as dist
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-            self.flat.div_(self.world)
+            if not isinstance(self.opt, FlatAdam):       # FlatAdam takes the mean itself
+                self.flat.div_(self.world)
 
     def step(self):
         """one eager step (host-launched; no host synchronisation)."""

@@ -384,10 +384,11 @@ def test_fused_step_graph_replay_tracks_eager(flat_adam):
     assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
 
 
-@pytest.mark.parametrize("wd", [0.0, 1e-3])
-def test_flat_adam_matches_torch_adam(wd):
+@pytest.mark.parametrize("wd,gs", [(0.0, 1.0), (1e-3, 1.0), (0.0, 0.125)])
+def test_flat_adam_matches_torch_adam(wd, gs):
     """regnn_adam_flat (the NS trainer's one-launch optimizer) against torch.optim.Adam over
-    the same gradients for 4 steps, with and without weight decay."""
+    the same gradients for 4 steps, with and without weight decay; grad_scale 1/8 (the mean of
+    an 8-rank SUM all-reduce) against torch's Adam on the divided gradient."""
     from regnn_hip.ns import FlatAdam
     g = torch.Generator(device=DEV).manual_seed(5)
     shapes = [(64, 128), (64,), (11,), (349, 64)]
@@ -396,10 +397,11 @@ def test_flat_adam_matches_torch_adam(wd):
     pflat = torch.cat([p.detach().reshape(-1) for p in ref]).clone()
     gflat = torch.zeros_like(pflat)
     fa = FlatAdam(pflat, gflat, lr=1e-2, weight_decay=wd)
+    fa.grad_scale = gs
     for _ in range(4):
         grads = [torch.randn(s, generator=g, device=DEV) for s in shapes]
         for p, gr in zip(ref, grads):
-            p.grad = gr.clone()
+            p.grad = gr * gs
         gflat.copy_(torch.cat([gr.reshape(-1) for gr in grads]))
         opt.step()
         fa.step()
