@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 28). */
+/* ABI version (bumped on any signature change or addition; currently 29). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -565,7 +565,10 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * sets sizes[hop + 1] and sizes[8 + hop], adds the block's edges to state[5]. Optional (all
  * three or none): with local = the per-node row in its type's table (mag local_node_idx), also
  * writes each block edge's source node type edge_type [cap_e] int32 and table row edge_off
- * [cap_e] int64 (what the fused step's layer 0 gathers by). */
+ * [cap_e] int64 (what the fused step's layer 0 gathers by). meta_only (needs the three): the
+ * hop whose sources only feed layer 0 by (type, row) — no first-seen de-duplication, no n_id
+ * append (sizes[hop + 1] = sizes[hop]), blk_idx of the sampled edges not written; blk_ptr,
+ * blk_rel, blk_pos, inv, the self loops and the edge meta as above (3 launches instead of 6). */
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
@@ -573,6 +576,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
+                 int32_t meta_only,
                  hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]

@@ -183,7 +183,7 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                int32_t* __restrict__ blk_idx, uint8_t* __restrict__ blk_rel,
                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv,
                uint64_t* __restrict__ status, const int64_t* __restrict__ local,
-               int32_t* __restrict__ e_type, int64_t* __restrict__ e_off) {
+               int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean) {
     __shared__ int lds[kBlock / 64 + 1];
     __shared__ int s_prefix;
     const int n = sizes[hop];
@@ -258,6 +258,7 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
         blk_ptr[cap] = E;
         sizes[8 + hop] = E;
         state[5] += E;
+        if (lean) sizes[hop + 1] = n;  // meta-only hop: no new nodes are recorded
     }
 }
 
@@ -272,17 +273,24 @@ ns_place_kernel(const int32_t* __restrict__ samp, const int32_t* __restrict__ sp
                 int cap, int k, const int64_t* __restrict__ state, const uint8_t* __restrict__ etype,
                 const uint64_t* __restrict__ g2l, uint64_t* __restrict__ first,
                 const int32_t* __restrict__ blk_ptr, uint8_t* __restrict__ blk_rel,
-                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc) {
+                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc,
+                const int32_t* __restrict__ ntype, const int64_t* __restrict__ local,
+                int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean) {
     const int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (s >= int64_t(cap) * k) return;
     const int i = int(s / k), r = int(s - int64_t(i) * k);
     if (i >= sizes[hop] || r >= scnt[i]) return;
-    const uint32_t stamp = ns_stamp(state, hop);
     const int bp = blk_ptr[i] + r;
     const int u = samp[s], p = spos[s];
     gsrc[bp] = u;
     blk_rel[bp] = etype[p];
     blk_pos[bp] = p;
+    if (lean) {                        // meta-only hop: the source's type and table row, no dedup
+        e_type[bp] = ntype[u];
+        e_off[bp] = local[u];
+        return;
+    }
+    const uint32_t stamp = ns_stamp(state, hop);
     if (uint32_t(g2l[u] >> 32) != stamp)
         atomicMin(reinterpret_cast<unsigned long long*>(first + u),
                   (unsigned long long)first_key(stamp, bp));
@@ -461,12 +469,14 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
-                 hipStream_t stream) {
+                 int32_t meta_only, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
         return REGNN_EINVAL;
-    if (!!local != !!edge_type || !!local != !!edge_off) return REGNN_EINVAL;
+    if (!!local != !!edge_type || !!local != !!edge_off || (meta_only && !local))
+        return REGNN_EINVAL;
+    const int lean = meta_only ? 1 : 0;
     if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
     const int64_t cap_e = int64_t(cap_dst) * (k + 1);
     if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
@@ -477,13 +487,15 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     hipLaunchKernelGGL(ns_rows_kernel, dim3((cap_dst + kNsRowsTile - 1) / kNsRowsTile),
                        dim3(kBlock), 0, stream, scnt, n_id, ntype, num_edge_types, sizes, hop,
                        cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, gsrc, inv, status, local,
-                       edge_type, edge_off);
+                       edge_type, edge_off, lean);
     REGNN_LAUNCH_CHECK();
     const int64_t slots = int64_t(cap_dst) * k;
     hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, stream, samp, spos, scnt, sizes, hop, cap_dst, k, state,
-                       etype, g2l, first, blk_ptr, blk_rel, blk_pos, gsrc);
+                       etype, g2l, first, blk_ptr, blk_rel, blk_pos, gsrc, ntype, local, edge_type,
+                       edge_off, lean);
     REGNN_LAUNCH_CHECK();
+    if (lean) return REGNN_OK;         // no dedup, no n_id append, no local source ids
     hipLaunchKernelGGL(ns_flags_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes, hop,
                        state, g2l, first, flag, tiles, n_tiles);
     REGNN_LAUNCH_CHECK();

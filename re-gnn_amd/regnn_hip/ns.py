@@ -124,6 +124,9 @@ class DeviceSampler:
             self.blocks.append(blk)
         self.local, self.edge_meta = None, [None] * len(self.sizes_k)
         self.meta_fresh = [False] * len(self.sizes_k)
+        # meta_only[h]: hop h writes only the edge meta its consumer reads (regnn_ns_hop
+        # meta_only: no de-duplication, n_id not extended, sampled blk_idx unwritten)
+        self.meta_only = [False] * len(self.sizes_k)
 
     def enable_edge_meta(self, local_node_idx, hop):
         """also write hop `hop`'s per-edge source node type and table row (regnn_ns_hop's
@@ -142,7 +145,9 @@ class DeviceSampler:
                L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes),
                None if self.stamp_src is None else L.ptr(self.stamp_src), L.stream())
 
-    def run_hops(self):
+    def run_hops(self, meta_only=True):
+        """every hop of the current batch; meta_only=False runs hops marked meta_only in full
+        (a consumer that reads n_id / the local source ids, e.g. the module path)."""
         rg = self.rg
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
@@ -155,6 +160,7 @@ class DeviceSampler:
                    L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos), L.ptr(blk.inv),
                    *((L.ptr(self.local), L.ptr(self.edge_meta[h][0]), L.ptr(self.edge_meta[h][1]))
                      if self.edge_meta[h] is not None else (None, None, None)),
+                   int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
 
@@ -266,6 +272,9 @@ def fused_unsupported(model, x_dict):
 # "auto": layer 0's relation-slot mode wherever the graph allows it; "off": the edge pass
 # (rel0) always (tests compare the two)
 REL_SLOTS = {"mode": "auto"}
+# "on": the fused step's last sampler hop runs meta-only (no dedup / n_id append); "off": the
+# full hop (tests that inspect the outermost n_id / local ids)
+LEAN_LAST_HOP = {"mode": "on"}
 
 
 def relation_slots_ok(sampler, T):
@@ -368,6 +377,9 @@ class FusedStep:
             W.ga[l] = ptr(z(n_dst, 64))
         n0 = caps[nl - 1]
         et, eo = sampler.enable_edge_meta(local_node_idx, nl - 1)
+        # layer 0 reads its block's sources by (type, table row) only: the last hop skips the
+        # first-seen de-duplication and the local ids nothing here reads
+        sampler.meta_only[nl - 1] = LEAN_LAST_HOP["mode"] != "off"
         W.edge_type, W.edge_off = ptr(et), ptr(eo)
         W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
@@ -560,7 +572,7 @@ class NSTrainer:
         s = self.slots[0]
         self._trained = 0
         s.batch_from_perm(self.perm, self.rank, self.world)
-        s.run_hops()
+        s.run_hops(meta_only=False)            # the module path reads n_id and local ids
         B = s.B
         n_id = s.n_id.to(torch.int64)
         out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,

@@ -65,13 +65,17 @@ def test_regnn_autograd_path_vs_reference(name):
         _check(k, got[k], v)
 
 
-def test_regnn_fused_step_vs_reference():
+def test_regnn_fused_step_vs_reference(monkeypatch):
     """regnn_ns_hop reproduces the fixture's sampled batch; regnn_nsm_step's loss and every
     gradient match the reference REGNN's. (The fixture's relations are drawn at random, not
     one per (target type, source type) pair, so layer 0 takes the edge pass here; the
     relation-slot mode is checked on the ogbn-mag-shaped graphs of test_gpu_ns_engine.py.)"""
+    from regnn_hip import ns
     from regnn_hip.graph import RelGraph
     from regnn_hip.ns import DeviceSampler, FusedStep
+    # the full last hop (this test checks the outermost n_id and local ids against the fixture;
+    # the meta-only hop is checked against the full one in test_gpu_ns_engine.py)
+    monkeypatch.setitem(ns.LEAN_LAST_HOP, "mode", "off")
     d = G.load("mag_regnn_ft3")
     m = d["meta"]
     N = int(sum(m["counts"]))
