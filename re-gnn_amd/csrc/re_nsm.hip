@@ -192,17 +192,6 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     float* tab = at + 16 * F;              // [F]
     if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
     const int n = A.sizes[A.hop];
-    if (blockIdx.x == 0) {                 // the labelled-target count the head divides by
-        __shared__ int s_valid;
-        if (threadIdx.x == 0) s_valid = 0;
-        __syncthreads();
-        const int n0 = A.sizes[0];
-        int cnt = 0;
-        for (int i = threadIdx.x; i < n0; i += kBlock) cnt += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
-        atomicAdd(&s_valid, cnt);          // integer count: order-independent
-        __syncthreads();
-        if (threadIdx.x == 0) *A.nvalid = float(s_valid);
-    }
     __syncthreads();
     const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
@@ -591,6 +580,12 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     const int v = blockIdx.x * kHeadRows + sub;
     const bool act = v < n;
     const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
+    // the labelled-target count nll_loss divides by: every block counts the batch's targets
+    // itself (loads in flight during the staging); block 0 also hands it to finalize
+    __shared__ int s_valid;
+    if (threadIdx.x == 0) s_valid = 0;
+    int cnt_valid = 0;
+    for (int i = threadIdx.x; i < n; i += kBlock) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
     {                                      // out_lin.weight -> LDS: thread (row c = tid/16 + 16i,
         constexpr int UB = 8;              // float4 tid%16), UB rows in flight
         const int k4 = (threadIdx.x & 15) * 4;
@@ -612,6 +607,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     }
     if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
     __syncthreads();
+    atomicAdd(&s_valid, cnt_valid);        // integer count: order-independent
     // ---- 1. aggregation, LayerNorm, relu, dropout
     const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
@@ -663,7 +659,8 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     __syncthreads();
-    const int n_valid = int(*A.nvalid);    // agg0's count of labelled targets
+    const int n_valid = s_valid;           // complete: the aggregation's barrier came after the adds
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     // ---- 2. z = h W^T + b -> zs (classes >= C: -inf)
     for (int ct = w; ct < CT; ct += kBlock / 64) {
         const int c = 16 * ct + cc;
