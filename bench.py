@@ -128,8 +128,7 @@ def run_ns_epoch(args, dev):
     tr.capture(warmup=2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.replay()
+    tr.run_steps(steps)
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
     model = info["model"].eval()
@@ -210,19 +209,19 @@ def run_ns(args, dev):
     use_graph = args.graph != "off"
     if use_graph:
         tr.capture(warmup=2)
-        run = tr.replay
+        run_k = tr.run_steps               # step pairs as one graph replay where they fit
     else:
-        run = tr.step
-    for _ in range(args.warmup):
-        run()
+        def run_k(k):
+            for _ in range(k):
+                tr.step()
+    run_k(args.warmup)
     torch.cuda.synchronize()
     e0 = tr.edges_total()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
+    run_k(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -631,6 +631,18 @@ class NSTrainer:
                     if fold_opt:
                         self.opt.step()
                 g1.append(g)
+            self.graph_groups = {}
+            if fold_opt:
+                # 2 and 4 steps back to back in one graph (the slot parity returns to 0):
+                # run_steps replays them for runs of steps, one graph boundary (~9 us of queue
+                # idle between replays) per group instead of per step
+                for n in (4, 2):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        for i in range(n):
+                            self._pipelined_body(i & 1)
+                            self.opt.step()
+                    self.graph_groups[n] = g
         else:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
@@ -643,6 +655,22 @@ class NSTrainer:
             with torch.cuda.graph(g2):
                 self.opt.step()
         self.graphs = (g1, g2)
+
+    def run_steps(self, k):
+        """k training steps as graph replays (capture() first): runs of 4 or 2 steps starting at
+        slot 0 replay the multi-step graphs, the rest the one-step graphs; the same steps as k
+        replay()s."""
+        k = int(k)
+        groups = getattr(self, "graph_groups", {})
+        while k > 0:
+            n = next((n for n in sorted(groups, reverse=True) if n <= k), 0)
+            if n and self.cur == 0 and self._primed:
+                groups[n].replay()
+                self._trained = 1                  # slot 1's batch trained last; cur back to 0
+                k -= n
+            else:
+                self.replay()
+                k -= 1
 
     def replay(self):
         g1, g2 = self.graphs
