@@ -580,34 +580,33 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     const int v = blockIdx.x * kHeadRows + sub;
     const bool act = v < n;
     const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
-    // the labelled-target count nll_loss divides by: every block counts the batch's targets
-    // itself (loads in flight during the staging); block 0 also hands it to finalize
-    __shared__ int s_valid;
-    if (threadIdx.x == 0) s_valid = 0;
-    int cnt_valid = 0;
-    for (int i = threadIdx.x; i < n; i += kBlock) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
-    {                                      // out_lin.weight -> LDS: thread (row c = tid/16 + 16i,
-        constexpr int UB = 8;              // float4 tid%16), UB rows in flight
-        const int k4 = (threadIdx.x & 15) * 4;
-        for (int i0 = 0; i0 < CT; i0 += UB) {
-            float4 wv[UB];
-#pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                const int c = (threadIdx.x >> 4) + 16 * (i0 + u);
-                wv[u] = i0 + u < CT && c < C
-                            ? *reinterpret_cast<const float4*>(A.w_out + int64_t(c) * F + k4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                const int c = (threadIdx.x >> 4) + 16 * (i0 + u);
-                if (i0 + u < CT) *reinterpret_cast<float4*>(Wl + head_sw(c, k4)) = wv[u];
-            }
+    {   // out_lin.weight -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPRs, in flight while
+        // the aggregation's first loads go out). One wave instruction fills 4 rows (1 KiB) of
+        // the image linearly; the XOR swizzle is applied to the per-lane SOURCE: lane L writes
+        // slot L%16 of row c, which holds W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw). Pad rows
+        // c >= C read row C-1 (finite values; their classes are masked everywhere).
+        const int L64 = threadIdx.x & 63;
+        for (int i = threadIdx.x >> 6; i < CT * 4; i += kBlock / 64) {
+            const int c = 4 * i + (L64 >> 4);
+            const int cs = c < C ? c : C - 1;
+            const float* src = A.w_out + int64_t(cs) * F + 4 * ((L64 & 15) ^ (c & 15));
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)src,
+                (__attribute__((address_space(3))) void*)(Wl + 4 * i * F), 16, 0, 0);
         }
+    }
+    // the labelled-target count nll_loss divides by: every block counts the batch's targets
+    // itself while the weight DMA lands (per-wave integer sums); block 0 hands it to finalize
+    __shared__ int wcnt[kBlock / 64];
+    {
+        int cnt_valid = 0;
+        for (int i = threadIdx.x; i < n; i += kBlock) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cnt_valid += __shfl_xor(cnt_valid, o, 64);
+        if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = cnt_valid;
     }
     if (threadIdx.x < F) tab[threadIdx.x] = A.tab[threadIdx.x];
     __syncthreads();
-    atomicAdd(&s_valid, cnt_valid);        // integer count: order-independent
     // ---- 1. aggregation, LayerNorm, relu, dropout
     const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
@@ -659,7 +658,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     __syncthreads();
-    const int n_valid = s_valid;           // complete: the aggregation's barrier came after the adds
+    const int n_valid = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
     if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     // ---- 2. z = h W^T + b -> zs (classes >= C: -inf)
     for (int ct = w; ct < CT; ct += kBlock / 64) {
