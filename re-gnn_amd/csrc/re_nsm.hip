@@ -1401,10 +1401,12 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     if (e < J.width) {
         const float* src = J.src + e;
         int p = grp;
-        for (; p + 24 < J.nparts; p += 32) {
-            const float v0 = src[int64_t(p) * J.pstride], v1 = src[int64_t(p + 8) * J.pstride];
-            const float v2 = src[int64_t(p + 16) * J.pstride], v3 = src[int64_t(p + 24) * J.pstride];
-            s += v0; s += v1; s += v2; s += v3;
+        for (; p + 56 < J.nparts; p += 64) {           // 8 partial rows in flight per thread
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[int64_t(p + 8 * u) * J.pstride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
         }
         for (; p < J.nparts; p += 8) s += src[int64_t(p) * J.pstride];
     }
