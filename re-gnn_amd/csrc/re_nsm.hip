@@ -288,6 +288,21 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
                 }
             }
         }
+        // the projection's first W_c fragment and W_1 (both independent of the gather) are
+        // requested before the S tile's stores and barrier, so their L2 latency overlaps them
+        constexpr int HB = KB / 2;             // float4 steps per half type
+        float4 bcur[HB], bnext[HB];
+        auto bload = [&](int step, float4 (&dst)[HB]) {
+            const int tt = step >> 1, h0 = (step & 1) * HB;
+            const float* wt = A.wc + int64_t(tt) * (K + 1) * F + (16 * w + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+        };
+        bload(0, bcur);
+        float4 wn[F * F / 4 / kBlock];         // W_1, staged into the S tile once it is read
+#pragma unroll
+        for (int i = 0; i < F * F / 4 / kBlock; ++i)
+            wn[i] = reinterpret_cast<const float4*>(A.w_next)[threadIdx.x + kBlock * i];
         const int tau = r_self - A.n_et;           // RS: the row's node type
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
@@ -329,15 +344,6 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
         // ---- project: D[v][j] = sum_t S_vt W_c[t]  (v = 4q + r, j = 16w + c); type t + 1's
         // W_c columns are loaded while type t's products run
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
-        constexpr int HB = KB / 2;             // float4 steps per half type
-        float4 bcur[HB], bnext[HB];
-        auto bload = [&](int step, float4 (&dst)[HB]) {
-            const int tt = step >> 1, h0 = (step & 1) * HB;
-            const float* wt = A.wc + int64_t(tt) * (K + 1) * F + (16 * w + c) * K + 4 * q + 16 * h0;
-#pragma unroll
-            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
-        };
-        bload(0, bcur);
         for (int step = 0; step < 2 * T; ++step) {
             if (step + 1 < 2 * T) bload(step + 1, bnext);
             const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
@@ -352,10 +358,6 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
 #pragma unroll
             for (int b = 0; b < HB; ++b) bcur[b] = bnext[b];
         }
-        float4 wn[F * F / 4 / kBlock];         // W_1, staged into the S tile once it is read
-#pragma unroll
-        for (int i = 0; i < F * F / 4 / kBlock; ++i)
-            wn[i] = reinterpret_cast<const float4*>(A.w_next)[threadIdx.x + kBlock * i];
         {
             const int j = 16 * w + c;
             const float bj = A.bias[j];
