@@ -17,6 +17,17 @@ class _Frame(dict):
     pass
 
 
+class _EdgeEnd(torch.Tensor):
+    """One end of ``g.edges()`` on a device graph: the device id tensor (DGL semantics) whose Python
+    iteration reads a host copy made once per graph, so run_regnn.py:94-99's per-edge
+    ``u.cpu().item()`` loop costs no device round trip per edge. Tensor ops return plain tensors."""
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    def __iter__(self):
+        return iter(self._host)
+
+
 class DGLGraph:
     """Directed multigraph in caller edge order (DGL semantics: edge e is src[e] -> dst[e]).
 
@@ -85,7 +96,18 @@ class DGLGraph:
     number_of_edges = num_edges
 
     def edges(self, form="uv", order="eid"):
-        return self._src, self._dst
+        if self._src.device.type == "cpu":
+            return self._src, self._dst
+        ends = self.__dict__.get("_edge_ends")
+        if ends is None or ends[0]._host.numel() != self._src.numel():
+            host = torch.stack([self._src, self._dst]).cpu()       # one copy, one sync
+            ends = []
+            for dev_ids, h in zip((self._src, self._dst), host):
+                e = torch.Tensor._make_subclass(_EdgeEnd, dev_ids)
+                e._host = h
+                ends.append(e)
+            self._edge_ends = ends = tuple(ends)
+        return ends
 
     def in_degrees(self, v=None):
         deg = torch.bincount(self._dst, minlength=self._n)

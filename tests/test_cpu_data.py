@@ -59,3 +59,16 @@ def test_csr_lookup_absent_and_duplicates():
                       shape=(3, 3))
     got = data.csr_lookup(m, [0, 2, 1, 0], [1, 0, 1, 0])
     assert got.tolist() == [3.0, 5.0, 0.0, 0.0]          # duplicates summed, absent -> 0
+
+
+def test_edge_end_iterates_host_copy_and_ops_return_plain_tensors():
+    """dgl.graph._EdgeEnd (what g.edges() returns on a device graph): iteration reads the host
+    copy (run_regnn.py:94-99's loop costs no device round trip per edge); every tensor op gives a
+    plain tensor. Checked here on host tensors; tests/test_gpu_configs.py checks the device case."""
+    from dgl.graph import _EdgeEnd
+    ids = torch.tensor([3, 1, 4, 1, 5])
+    e = torch.Tensor._make_subclass(_EdgeEnd, ids)
+    e._host = ids.clone() + 10                      # distinguishable from the tensor's data
+    assert [int(u.item()) for u in e] == [13, 11, 14, 11, 15]
+    assert type(e + 0) is torch.Tensor and type(e[1:]) is torch.Tensor
+    assert torch.equal(e + 0, ids) and e.data_ptr() == ids.data_ptr()

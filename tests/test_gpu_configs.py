@@ -162,3 +162,26 @@ def test_imdb_remixhop_vs_oracle(tmp_path):
     got = _grads(net)
     for k, v in want_g.items():
         _check(k, got[k], v, 1e-5)
+
+
+def test_reference_edge_loop_on_device_graph():
+    """run_regnn.py:84-99 as written: g.to(device), then e_feat from a Python loop over
+    zip(*g.edges()) with u.cpu().item(). The ends are device tensors (DGL semantics) whose
+    iteration reads one host copy, and the relation ids equal the vectorised build's."""
+    import time
+    import dgl
+    from regnn_hip import data, synth
+    gd = synth.acm_like(seed=1, device="cpu")
+    adjM, _, _, wsl2 = data.matrices_from_edges(gd["src"].numpy(), gd["dst"].numpy(),
+                                                gd["rel"].numpy(), gd["N"], int(gd["R"]) - 3)
+    g = dgl.add_self_loop(dgl.remove_self_loop(dgl.DGLGraph(adjM))).to(DEV)
+    s, d = g.edges()
+    assert s.is_cuda and d.is_cuda and type(s * 1) is torch.Tensor
+    t0 = time.perf_counter()
+    e_feat = []
+    for u, v in zip(*g.edges()):
+        e_feat.append(wsl2[(u.cpu().item(), v.cpu().item())])
+    dt = time.perf_counter() - t0
+    _, e_vec = data.build_graph(adjM, wsl2, device=DEV)
+    assert torch.equal(torch.tensor(e_feat, dtype=torch.long), e_vec.cpu())
+    print(f"{len(e_feat)} edges in {dt:.2f} s")
