@@ -108,9 +108,11 @@ prep_kernel(int T, int K, Ptrs lin_w, Ptrs lin_b, const float* __restrict__ w0, 
         float s = 0.f;
         if (k < K) {
             const float* W = pick(lin_w.p, t);
+#pragma unroll 32                                     // operand loads in flight, not one by one
             for (int o = 0; o < F; ++o) s = fmaf(W[int64_t(o) * K + k], w0[o * F + j], s);
         } else {
             const float* bb = pick(lin_b.p, t);
+#pragma unroll 32
             for (int o = 0; o < F; ++o) s = fmaf(bb[o], w0[o * F + j], s);
         }
         // wcT[t]: W_c[t]^T row-major [64][K], then b_c[t] [64]
@@ -1489,17 +1491,27 @@ adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __re
                  float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
                  float wd, float gscale, int64_t* __restrict__ step, unsigned* __restrict__ ticket) {
     __shared__ bool last;
+    // the first element's operands are requested together with the step count (independent
+    // loads: one memory latency, not two, before the first update)
+    const int64_t i0 = int64_t(blockIdx.x) * kBlock + threadIdx.x, stride = int64_t(gridDim.x) * kBlock;
+    float g0 = 0.f, p0 = 0.f, m0 = 0.f, v0 = 0.f;
+    if (i0 < n) {
+        g0 = g[i0]; p0 = p[i0]; m0 = m[i0]; v0 = v[i0];
+    }
     const int64_t t = step[0] + 1;
     const double bc1 = 1.0 - pow(double(b1), double(t));
     const double bc2 = 1.0 - pow(double(b2), double(t));
     const float step_size = float(double(lr) / bc1);
     const float bc2_sqrt = float(sqrt(bc2));
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n;
-         i += int64_t(gridDim.x) * kBlock) {
-        float gi = g[i] * gscale;              // gscale: 1 / ranks after a SUM all-reduce
-        const float pi = p[i];
+    for (int64_t i = i0; i < n; i += stride) {
+        float gi, pi, mi, vi;
+        if (i == i0) {
+            gi = g0; pi = p0; mi = m0; vi = v0;
+        } else {
+            gi = g[i]; pi = p[i]; mi = m[i]; vi = v[i];
+        }
+        gi *= gscale;                          // gscale: 1 / ranks after a SUM all-reduce
         if (wd != 0.f) gi = gi + wd * pi;
-        const float mi = m[i], vi = v[i];
         const float mn = mi + (1.f - b1) * (gi - mi);                 // exp_avg.lerp_(grad, 1-b1)
         const float vn = vi * b2 + (1.f - b2) * gi * gi;               // mul_(b2).addcmul_
         m[i] = mn;
@@ -1507,11 +1519,10 @@ adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __re
         const float denom = sqrtf(vn) / bc2_sqrt + eps;
         p[i] = pi - step_size * (mn / denom);
     }
+    // the ticket only orders every block's read of step[0] (its value is consumed above) before
+    // the last block's store of it; the parameter stores need no fence before it
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    }
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     __syncthreads();
     if (last && threadIdx.x == 0) {
         step[0] = t;
