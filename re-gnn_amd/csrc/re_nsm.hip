@@ -1386,18 +1386,19 @@ struct Job {
 constexpr int kMaxJobs = 32;
 
 struct FinArgs {
-    Job job[kMaxJobs];
     int n_jobs;
     float alpha;
+    int start[kMaxJobs];     // first block of each job: the block -> job search reads 2 lines of
+                             // kernel arguments at once instead of walking the 48-byte Jobs
+    Job job[kMaxJobs];
 };
 
 __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     __shared__ float red[8][33];
-    int b = blockIdx.x, ji = 0;
-    while (ji < A.n_jobs - 1 && b >= A.job[ji].blocks) {
-        b -= A.job[ji].blocks;
-        ++ji;
-    }
+    int ji = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
+    const int b = blockIdx.x - A.start[ji];
     const Job J = A.job[ji];
     const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int e = b * 32 + el;
@@ -1584,6 +1585,7 @@ struct JobList {
     int blocks = 0;
     void add(const float* src, int64_t pstride, int nparts, int width, float* dst, int op = kOpCopy,
              const float* aux = nullptr) {
+        A.start[A.n_jobs] = blocks;
         Job& j = A.job[A.n_jobs++];
         j.src = src; j.pstride = pstride; j.nparts = nparts; j.width = width; j.dst = dst;
         j.op = op; j.aux = aux; j.blocks = (width + 31) / 32;
