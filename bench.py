@@ -12,14 +12,18 @@ synchronisation inside a step). The graph and features are replicated on every r
 scaling: 512 targets per rank per step). value = aggregated edges (every sampled block's edges
 incl. self loops, summed over ranks) / max-over-ranks time.
 
+The top-level "roofline" is that of `value`'s own kernel, the fused NS model step
+(regnn_nsm_step): algorithmic bytes (ns_step_bytes) / HIP-event time ("frac"), and the HBM bytes
+rocprofv3 counted for the same kernels ("traffic", "frac_hbm", from profiles/pmc_ns_fp32.json
+when it matches the kernel code and config).
+
 At N = 1 the line also carries, on the same graph generator:
   * "full_batch": the full-graph REGCN training step on mag_like(10) (input Linear, 2 x
     REGraphConv fwd+bwd, out_lin, CE, Adam) -- the REGraphConv SpMM whose HBM roofline
-    north_star gates (>= 40 %); the top-level "roofline" is that SpMM's, with the algorithmic
-    fraction ("frac") and the fraction of HBM bytes measured by rocprofv3 PMC counters
-    ("frac_hbm", from the committed summary of the same graph, dtype and kernel code);
-  * "cpu_baseline": oracle/cpu_regcn.py (torch.sparse CSR restatement of the REGraphConv stack,
-    BASELINE.md §3) on the host cores.
+    north_star gates (>= 40 %), with its own "roofline" (algorithmic "frac", PMC "frac_hbm");
+  * "cpu_baseline": oracle/cpu_ns.py, the same NS training step on the host cores (sampler
+    spec, REGNN fwd+bwd as the reference composes it, nll, Adam; mag_like(1)), with the
+    full-graph REGraphConv stack (oracle/cpu_regcn.py) under "full_batch".
 
 Launch: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ns|mag|dblp|acm|imdb|...]
@@ -265,25 +269,34 @@ def run_ns(args, dev):
     }
     res["config"]["engine"] = "fused regnn_nsm_step" if tr.fused is not None else "module"
     if "nsm_step" in kstats and nsm_bytes:
-        # the fused model step (eight launches): algorithmic bytes of its reads and writes at the
-        # profiled steps' sampled sizes (ns_step_bytes) / its device time
+        # the roofline of `value`'s own kernel: the fused model step (regnn_nsm_step), its
+        # algorithmic bytes at the profiled steps' sampled sizes (ns_step_bytes) / its HIP-event
+        # time; HBM bytes from the committed rocprofv3 FETCH_SIZE + WRITE_SIZE summary of the
+        # same kernels (profiles/pmc_ns_fp32.json) when it matches this kernel code and config
         launches, mean_ms, total_ms, _ = kstats["nsm_step"]
         b = statistics.mean(nsm_bytes)
         ach = b / (mean_ms / 1e3) / 1e9
-        nl = 7 if tr.fused.P.rel_slots else 8
-        res["ns_roofline"] = {"bound": "hbm", "kernel": f"regnn_nsm_step ({nl} launches)",
-                              "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": ach / HBM_PEAK_GBS, "launch_ms": mean_ms,
-                              "algorithmic_bytes_per_launch": b}
+        traffic, pmc_status = pmc_traffic_ns(args)
+        hbm = None if traffic is None else traffic / (mean_ms / 1e3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": f"regnn_nsm_step ({tr.fused.launches()} "
+                                                     f"launches: {', '.join(tr.fused.kernels())})",
+                           "workload": "ns step (value)", "achieved": ach,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                           "traffic": traffic, "achieved_hbm": hbm,
+                           "frac_hbm": None if hbm is None else hbm / HBM_PEAK_GBS,
+                           "pmc": pmc_status, "launch_ms": mean_ms, "launches": launches,
+                           "algorithmic_bytes_per_launch": b,
+                           "note": "algorithmic bytes: bench.ns_step_bytes (DESIGN.md §4b); the "
+                                   "step is latency-bound (dependent phases), not byte-bound"}
     cand = {k: v for k, v in kstats.items() if k in ("ns_spmm_fwd", "ns_spmm_bwd")}
     if cand:
         dom = max(cand, key=lambda k: cand[k][2])
         launches, mean_ms, total_ms, total_bytes = cand[dom]
         ach = total_bytes / (total_ms / 1e3) / 1e9
-        res["ns_roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach,
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                              "launch_ms": mean_ms,
-                              "algorithmic_bytes_per_launch": total_bytes / launches}
+        res["roofline"] = {"bound": "hbm", "kernel": dom, "workload": "ns step (module path)",
+                           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": ach / HBM_PEAK_GBS, "traffic": None, "launch_ms": mean_ms,
+                           "algorithmic_bytes_per_launch": total_bytes / launches}
     del tr
     torch.cuda.empty_cache()
     return res
@@ -416,6 +429,25 @@ def pmc_traffic(wl, dtype, rg, op):
     if op not in rec:
         return None, f"PMC summary has no {op}"
     return rec[op]["bytes_per_launch"], "ok"
+
+
+def pmc_traffic_ns(args):
+    """HBM bytes per fused NS model step from the committed rocprofv3 PMC summary
+    (tools/gpu_pmc_ns.sh: FETCH_SIZE / WRITE_SIZE of the regnn::nsm kernels, separate passes,
+    copy-calibrated), or (None, reason) when it was measured on other kernel code or config."""
+    from regnn_hip.build import NS_PMC_SOURCES, kernel_hash
+    path = os.path.join(ROOT, "profiles", "pmc_ns_fp32.json")
+    if not os.path.exists(path):
+        return None, "no PMC summary committed"
+    with open(path) as f:
+        rec = json.load(f)
+    want = {"scale": args.scale, "batch": args.batch, "fanout": [25, 20], "hidden": 64,
+            "dropout": args.dropout}
+    if rec.get("config") != want:
+        return None, f"PMC summary is for another config ({rec.get('config')})"
+    if rec.get("code_hash") != kernel_hash(NS_PMC_SOURCES):
+        return None, "PMC summary is for other kernel code (stale: re-run tools/gpu_pmc_ns.sh)"
+    return rec["nsm_step"]["bytes_per_launch"], "ok"
 
 
 def run_full(args, dev, wl):
@@ -622,9 +654,8 @@ def main():
     if args.workload == "ns":
         result = run_ns(args, dev)
         if world == 1 and not args.no_full_batch:
-            fb = run_full(args, dev, "mag")
-            result["roofline"] = fb.pop("roofline")
-            result["full_batch"] = fb
+            # the full-graph REGraphConv step: north_star's SpMM roofline gate, under its own key
+            result["full_batch"] = run_full(args, dev, "mag")
     elif args.workload == "ns_infer":
         result = run_other_ns_infer(args, dev)
     elif args.workload == "ns_epoch":
@@ -642,13 +673,29 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, threads = cpu_baseline()
         mag_key = [k for k in cb if k.startswith("mag_like")][0]
-        result["cpu_baseline"] = {
+        full = {
             "value": cb[mag_key]["edges_per_s"], "unit": "edges/s", "cores": threads,
             "kind": "port", "cpu_model": _cpu_model(),
             "sample": (f"oracle/cpu_regcn.py (torch.sparse CSR fwd+bwd of REGraphConv x2, "
                        f"hidden 64, fp32) on {mag_key} N={cb[mag_key]['N']:,} "
                        f"E={cb[mag_key]['E']:,}; median of 10 after 3 warm-ups"),
             "dblp_like": cb["dblp_like"], mag_key: cb[mag_key]}
+        if args.workload == "ns":
+            # the workload `value` measures: the NS training step on the host cores
+            from oracle import cpu_ns
+            t, e, info = cpu_ns.step_baseline(scale=1.0, steps=10, warm=3, threads=threads)
+            result["cpu_baseline"] = {
+                "value": e / t, "unit": "edges/s", "cores": info["threads"], "kind": "port",
+                "cpu_model": _cpu_model(), "ms_per_step": t * 1e3,
+                "aggregated_edges_per_step": e,
+                "sample": (f"oracle/cpu_ns.py: the NS training step (the sampler spec, REGNN "
+                           f"regcn/LN fwd+bwd with index_add scatter as the reference composes "
+                           f"it, nll, Adam) on mag_like(1) N={info['N']:,} E={info['E']:,}, "
+                           f"batch {info['batch']} x {info['sizes']}, hidden 64, 349 classes, "
+                           f"dropout 0.5; median of 10 steps after 3 warm-ups"),
+                "full_batch": full}
+        else:
+            result["cpu_baseline"] = full
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -6,7 +6,6 @@ the stream is torch's current HIP stream, so kernels order with surrounding torc
 """
 import ctypes
 import os
-import threading
 
 import torch
 
@@ -126,14 +125,28 @@ def dtype_code(t):
     raise TypeError(f"regnn_hip: unsupported feature dtype {t.dtype} (float32 / bfloat16)")
 
 
-# Device of the pointers formed for the call being assembled: ``call(name, ptr(a), ...,
-# stream())`` evaluates ptr() first, so stream() picks the current stream of the TENSORS'
-# device (not of torch's current device) and call() runs the launch under that device.
-_tls = threading.local()
+# Device of a call: every pointer ptr() forms is an int tagged with its tensor's device, so
+# call() reads the devices from its own arguments (no state carried between calls: a failure
+# while arguments are assembled cannot leak into the next launch). stream() is a placeholder
+# that call() replaces with the current stream of the TENSORS' device (not of torch's current
+# device), and the launch runs under that device.
+class DevPtr(int):
+    """Tensor.data_ptr() tagged with the tensor's device index (.dev); passes as a plain int."""
+
+    def __new__(cls, value, dev):
+        o = int.__new__(cls, value)
+        o.dev = dev
+        return o
 
 
-def _reset():
-    _tls.dev, _tls.mixed = None, False
+class _StreamArg:
+    """stream() placeholder: call() substitutes the current HIP stream of the call's device."""
+
+    def __repr__(self):
+        return "<regnn_hip current stream>"
+
+
+_STREAM = _StreamArg()
 
 
 def ptr(t):
@@ -141,28 +154,23 @@ def ptr(t):
     if t is None:
         return None
     if not t.is_cuda:
-        _reset()
         raise RuntimeError("regnn_hip kernels need ROCm device tensors (there is no CPU path)")
-    d = t.device.index
-    cur = getattr(_tls, "dev", None)
-    if cur is None:
-        _tls.dev = d
-    elif cur != d:
-        _tls.mixed = True
-    return t.data_ptr()
+    return DevPtr(t.data_ptr(), t.device.index)
 
 
 def stream():
-    """current HIP stream of the device the call's tensors live on (torch's current device
-    when no tensor pointer was formed yet)."""
-    return torch.cuda.current_stream(getattr(_tls, "dev", None)).cuda_stream
+    """the current HIP stream of the call's device, filled in by call()."""
+    return _STREAM
 
 
 def call(name, *args):
-    dev, mixed = getattr(_tls, "dev", None), getattr(_tls, "mixed", False)
-    _reset()
-    if mixed:
+    devs = {a.dev for a in args if isinstance(a, DevPtr)}
+    if len(devs) > 1:
         raise RuntimeError(f"regnn_hip.{name}: tensors on different devices")
+    dev = devs.pop() if devs else None
+    if any(a is _STREAM for a in args):
+        s = torch.cuda.current_stream(dev).cuda_stream
+        args = tuple(s if a is _STREAM else a for a in args)
     if dev is not None and dev != torch.cuda.current_device():
         with torch.cuda.device(dev):
             rc = getattr(_so, name)(*args)

@@ -262,6 +262,9 @@ def fused_unsupported(model, x_dict):
     dims = {int(x_dict[k].shape[1]) for k in keys}
     if len(dims) != 1 or dims.pop() not in (64, 128):
         return "input widths must be equal, 64 or 128"
+    K = int(x_dict[keys[0]].shape[1])
+    if len(keys) * (K + 1) > 600:              # regnn_nsm_step's composed-map bound
+        return f"{len(keys)} node types x input width {K} exceed the fused step's tables"
     if any(x_dict[k].dtype != torch.float32 or not x_dict[k].is_contiguous() for k in keys):
         return "inputs must be contiguous fp32"
     if model.out_lin.weight.shape[0] > 448 or model.out_lin.weight.shape[1] != 64:
@@ -392,6 +395,17 @@ class FusedStep:
         W.slab = ptr(z(_slab_floats(P, caps[0])))
         self.model, self.sampler, self.n_layers = model, sampler, nl
 
+    def kernels(self):
+        """the kernels one regnn_nsm_step launches, in order (bench.py's roofline label)."""
+        ks = ["prep", "agg0"] + ["agg"] * (self.n_layers - 2) + ["head"]
+        ks += ["agg_bwd", "post_bwd"] * (self.n_layers - 1)
+        ks += ["bwd0_rs" if self.P.rel_slots else "bwd0"]
+        ks += [] if self.P.rel_slots else ["rel0"]
+        return ks + ["finalize", "chain"]
+
+    def launches(self):
+        return len(self.kernels())
+
     def step(self):
         if not self.sampler.meta_fresh[self.n_layers - 1]:
             raise RuntimeError("run the sampler's hops after building FusedStep: layer 0 reads the "
@@ -463,7 +477,13 @@ class NSTrainer:
         self.perm = self.train_idx.clone()
         self.shuffle, self.seed = shuffle, int(seed)
         self.x_dict, self.node_type, self.local_node_idx = x_dict, node_type, local_node_idx
+        self.edge_type = torch.as_tensor(edge_type).to(dev, torch.int64)
         self.y_flat = y_global.reshape(-1).to(dev, torch.int64)
+        # the module path hands 'regcn' / self_loop_type 2 the capacity-sized device blocks (no
+        # host sync: capturable); every other REGNN conv (regat, regatv2, other self-loop types)
+        # gets the PyG-style exact-size adjs and edge types (one host sync per step)
+        self._blocks_ok = (getattr(model, "model", None) == "regcn" and
+                           getattr(model, "self_loop_type", None) == 2)
         self.params = [p for p in model.parameters() if p.requires_grad]
         n = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -573,13 +593,23 @@ class NSTrainer:
         self._trained = 0
         s.batch_from_perm(self.perm, self.rank, self.world)
         s.run_hops(meta_only=False)            # the module path reads n_id and local ids
-        B = s.B
-        n_id = s.n_id.to(torch.int64)
-        out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
-                         self.local_node_idx)
-        y = self.y_flat[n_id[:B]]
-        valid = torch.arange(B, device=self.device) < s.sizes[0]
-        y = torch.where(valid, y, torch.full_like(y, -100))
+        if self._blocks_ok:
+            B = s.B
+            n_id = s.n_id.to(torch.int64)
+            out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
+                             self.local_node_idx)
+            y = self.y_flat[n_id[:B]]
+            valid = torch.arange(B, device=self.device) < s.sizes[0]
+            y = torch.where(valid, y, torch.full_like(y, -100))
+        else:
+            # exact sizes (host sync) and the reference's (edge_index, e_id, size) adjs,
+            # outermost hop first (mag/regnn_ns.py:399-403)
+            n_total, hops = s.exact_adjs()
+            adjs = [(ei, e_id, size) for ei, e_id, size, _blk, _cnt in hops[::-1]]
+            n_id = s.n_id[:n_total].to(torch.int64)
+            out = self.model(n_id, self.x_dict, adjs, self.edge_type, self.node_type,
+                             self.local_node_idx)
+            y = self.y_flat[n_id[:hops[0][2][1]]]
         loss = F.nll_loss(out, y)                     # mean over the batch's targets
         loss.backward()
         with torch.no_grad():
@@ -598,22 +628,63 @@ class NSTrainer:
         self._exchange()
         self.opt.step()
 
+    def _train_state(self):
+        """parameters and optimizer state, for capture() to undo its warm-up steps."""
+        if isinstance(self.opt, FlatAdam):
+            o = self.opt
+            return [t.clone() for t in (o.p, o.m, o.v, o.step_count)], None
+        st = {id(p): {k: v.clone() for k, v in s.items() if torch.is_tensor(v)}
+              for p, s in self.opt.state.items()}
+        return [p.detach().clone() for p in self.params], st
+
+    def _restore_train_state(self, saved):
+        flat, st = saved
+        with torch.no_grad():
+            if st is None:
+                o = self.opt
+                for dst, src in zip((o.p, o.m, o.v, o.step_count), flat):
+                    dst.copy_(src)
+                return
+            for p, src in zip(self.params, flat):
+                p.copy_(src)
+            # state tensors the warm-up created (Adam: step, exp_avg, exp_avg_sq) go back to
+            # their initial zeros in place: the captured graph keeps their addresses
+            for p, s in self.opt.state.items():
+                prev = st.get(id(p), {})
+                for k, v in s.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if k in prev:
+                        v.copy_(prev[k])
+                    else:
+                        v.zero_()
+
     def capture(self, warmup=2):
         """capture the step as HIP graphs: [fwd/bwd + optimizer] on one rank; [fwd/bwd] (+ the
-        eager all-reduce) + [optimizer] on several."""
+        eager all-reduce) + [optimizer] on several. The `warmup` eager steps that precede the
+        capture (kernel selection, lazy optimizer state) are undone: parameters, optimizer
+        moments and step count, and the sampler's batch / edge counters are restored, so the
+        first replay trains the epoch's first batch from the same model as an eager step would.
+        Only the dedup stamps move on (they must stay monotone)."""
+        if self.fused is None and not self._blocks_ok:
+            raise ValueError("this model's module path reads exact-size adjs (a host sync per "
+                             "step) and cannot be captured; run step() eagerly")
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         st0 = [s.state.clone() for s in self.slots]
+        saved = self._train_state()
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self.step()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        self._restore_train_state(saved)
         # warm-up steps do not advance the epoch (batch counter, edge counter); the dedup stamp
         # (state[4]) stays monotone: the tables still hold the warm-up steps' stamps
         for s, s0 in zip(self.slots, st0):
             s.state[2:4].copy_(s0[2:4])
             s.state[5:6].copy_(s0[5:6])
+        torch.cuda.synchronize(self.device)
         self.cur, self._primed, self._trained = 0, False, 0
         # one rank: the optimizer step joins the step's graph (no graph boundary, no host gap
         # between the backward and Adam); several: the gradient all-reduce runs between graphs

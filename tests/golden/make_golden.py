@@ -517,9 +517,124 @@ def gen_regnn():
                   self_loop_type=2, dropout=0.0), st)
 
 
+def _mag_schema_graph(rng, counts):
+    """A small heterogeneous graph with ogbn-mag's schema, built the way mag/regnn_ns.py:91-105,
+    141-142 builds the real one: the 4 raw relations (author-affiliated_with-institution,
+    author-writes-paper, paper-cites-paper, paper-has_topic-field_of_study) in the dataset's
+    edge_index_dict order, the 3 reverse relations appended, cites made undirected, then PyG's
+    group_hetero_graph: node types numbered in num_nodes_dict order (ogbn-mag: author 0,
+    field_of_study 1, institution 2, paper 3), global ids type by type, edge_type = the
+    relation's position in edge_index_dict. [ext] PyG semantics restated here: to_undirected =
+    coalesce(cat(ei, flip(ei))) (rows sorted by (row, col), duplicates dropped);
+    group_hetero_graph concatenates the relations' edges in dict order. Every relation joins one
+    source node type to one target node type (regnn_nsm_params.rel_slots holds)."""
+    A, Fd, I, P = 0, 1, 2, 3
+    off = np.concatenate([[0], np.cumsum(counts)[:-1]])
+
+    def rnd(st, dt, n, hub_dst=None, hub_frac=0.0):
+        s = rng.integers(0, counts[st], n)
+        d = rng.integers(0, counts[dt], n)
+        if hub_dst is not None:                       # a few hub targets: rows past the fan-out
+            m = rng.random(n) < hub_frac
+            d[m] = rng.integers(0, hub_dst, int(m.sum()))
+        return np.stack([s, d])
+
+    rels = {}
+    rels[("author", "affiliated_with", "institution")] = (A, I, rnd(A, I, 260))
+    rels[("author", "writes", "paper")] = (A, P, rnd(A, P, 700, hub_dst=3, hub_frac=0.12))
+    cites = rnd(P, P, 500, hub_dst=2, hub_frac=0.1)
+    rels[("paper", "has_topic", "field_of_study")] = (P, Fd, rnd(P, Fd, 420, hub_dst=2,
+                                                                   hub_frac=0.15))
+    r, c = rels[("author", "affiliated_with", "institution")][2]
+    rels[("institution", "to", "author")] = (I, A, np.stack([c, r]))
+    r, c = rels[("author", "writes", "paper")][2]
+    rels[("paper", "to", "author")] = (P, A, np.stack([c, r]))
+    r, c = rels[("paper", "has_topic", "field_of_study")][2]
+    rels[("field_of_study", "to", "paper")] = (Fd, P, np.stack([c, r]))
+    ei = np.concatenate([cites, cites[::-1]], 1)
+    ei = np.unique(ei[0] * counts[P] + ei[1])
+    cites = np.stack([ei // counts[P], ei % counts[P]])
+    order = [("author", "affiliated_with", "institution"), ("author", "writes", "paper"),
+             ("paper", "cites", "paper"), ("paper", "has_topic", "field_of_study"),
+             ("institution", "to", "author"), ("paper", "to", "author"),
+             ("field_of_study", "to", "paper")]
+    rels[("paper", "cites", "paper")] = (P, P, cites)
+    src, dst, et = [], [], []
+    for i, key in enumerate(order):
+        st, dt, e = rels[key]
+        src.append(e[0] + off[st])
+        dst.append(e[1] + off[dt])
+        et.append(np.full(e.shape[1], i))
+    src, dst, et = (np.concatenate(v).astype(np.int64) for v in (src, dst, et))
+    o = np.argsort(dst, kind="stable")             # edge ids = CSR positions (dst-major, stable)
+    ntype = np.repeat(np.arange(4), counts).astype(np.int64)
+    local = np.concatenate([np.arange(c) for c in counts]).astype(np.int64)
+    return src[o], dst[o], et[o], ntype, local, int(off[P])
+
+
+def gen_regnn_schema():
+    """The benchmarked NS mode pinned to the reference: the reference REGNN
+    on an ogbn-mag-schema graph (one relation per (source type, target type) pair: the fused
+    step's relation-slot mode applies), K = 128 input rows (feats_type 3), hidden 64, 349
+    classes, fan-out [25, 20] (mag/regnn_ns.py defaults), dropout 0, nll_loss, every gradient."""
+    from types import SimpleNamespace
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import sampler_oracle as SO
+    rng = np.random.default_rng(77)
+    counts = [170, 40, 14, 130]                    # author, field_of_study, institution, paper
+    src, dst, edge_type, ntype, local, p0 = _mag_schema_graph(rng, counts)
+    N = int(sum(counts))
+    ptr = np.zeros(N + 1, np.int64)
+    np.add.at(ptr, dst + 1, 1)
+    ptr = np.cumsum(ptr)
+    batch = (p0 + rng.choice(counts[3], 24, replace=False)).astype(np.int64)
+    batch[:3] = p0 + np.arange(3)                  # the hub papers among the targets
+    sizes, seed, epoch, batch_idx = [25, 20], 123, 0, 5
+    _, n_id, adjs = SO.neighbor_sample(ptr, src, batch.tolist(), sizes, seed, epoch, batch_idx)
+    K, H, C = 128, 64, 349
+    y = np.full(N, -1, np.int64)
+    y[p0:] = rng.integers(0, C, counts[3])
+    args = SimpleNamespace(model="regcn", feats_type=3, self_loop_type=2, no_re=False)
+    REGNN = _reference_regnn_class(args, {t: counts[t] for t in range(4)}, 3, regnn_layers)
+    torch.manual_seed(12)
+    model = REGNN(K, H, C, 1, 2, 10.0, 0.0, {t: K for t in range(4)}, 7, False, False,
+                  use_norm="ln")
+    _set_params(model, rng, ew_alpha=10.0)
+    model.eval()
+    x_dict = {t: torch.from_numpy((f32(rng, counts[t], K) if t == 3 else
+                                   rng.uniform(-0.5, 0.5, (counts[t], K)).astype(np.float32))
+                                  .astype(np.float64)) for t in range(4)}
+    t_adjs = [(torch.tensor([s_, d_], dtype=torch.int64), torch.tensor(e_, dtype=torch.int64), sz)
+              for s_, d_, e_, sz in adjs]
+    out = model(torch.tensor(n_id), x_dict, t_adjs, torch.from_numpy(edge_type),
+                torch.from_numpy(ntype), torch.from_numpy(local))
+    loss = torch.nn.functional.nll_loss(out, torch.from_numpy(y[batch]))
+    loss.backward()
+    st = dict(src=src, dst=dst, edge_type=edge_type, ntype=ntype, local=local, y=y, batch=batch,
+              n_id=np.asarray(n_id, np.int64), logp=out, loss=loss.detach())
+    for t, x in x_dict.items():
+        st[f"x{t}"] = x.numpy().astype(np.float32)
+    for h, (s_, d_, e_, sz) in enumerate(adjs):
+        st[f"adj{h}_src"], st[f"adj{h}_dst"] = np.asarray(s_), np.asarray(d_)
+        st[f"adj{h}_eid"] = np.asarray(e_)
+        st[f"adj{h}_size"] = np.asarray(sz)
+    _pack("p_", _params(model), st)
+    _pack("grad_", _grads(model), st)
+    save("mag_regnn_schema", dict(model="mag.REGNN", feats_type=3, in_channels=K, hidden=H,
+                                  classes=C, num_layers=2, scaling_factor=10.0, num_edge_types=7,
+                                  counts=counts, target_type=3, target_offset=p0, y_global=True,
+                                  sizes=sizes, seed=seed, epoch=epoch, batch_idx=batch_idx,
+                                  use_norm="ln", self_loop_type=2, dropout=0.0,
+                                  schema="ogbn-mag"), st)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float64)
-    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat", "regnn"]
+    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat", "regnn", "schema"]
     if "layers" in which:
         gen_layers()
     if "models" in which:
@@ -532,3 +647,5 @@ if __name__ == "__main__":
         gen_mag_gat()
     if "regnn" in which:
         gen_regnn()
+    if "schema" in which:
+        gen_regnn_schema()

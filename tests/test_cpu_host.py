@@ -99,3 +99,20 @@ def test_row_cnt_histogram():
     np.add.at(want, (dst, rel - 1), 1)
     want[np.bincount(dst, minlength=N) > 16] = 0
     assert np.array_equal(cnt.numpy().astype(np.int64), want)
+
+
+def test_fused_ns_gate_matches_kernel_limits():
+    """ns.fused_unsupported refuses what regnn_nsm_step would reject (T * (K + 1) > 600 with
+    K = 128 means at most 4 node types), so engine='auto' falls back to the module path instead
+    of failing at the first step."""
+    import torch
+    from regnn_hip import mag, ns
+
+    def gate(T, K):
+        m = mag.REGNN(K, 64, 11, 2, 10.0, 0.0, {k: K for k in range(T)}, 7, use_norm="ln",
+                      self_loop_type=2)
+        return ns.fused_unsupported(m, {k: torch.zeros(3, K) for k in range(T)})
+    assert gate(4, 128) is None
+    assert gate(8, 64) is None
+    assert gate(5, 128) is not None
+    assert gate(2, 96) is not None

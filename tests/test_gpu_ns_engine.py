@@ -132,15 +132,51 @@ def test_trainer_step_matches_pyg_path():
         assert ok, f"{n}: rel err {err:.3e}"
 
 
+@pytest.mark.parametrize("model_kind", ["regat", "regcn_sl1"])
+def test_trainer_module_path_other_models(model_kind):
+    """NSTrainer's module path for the REGNN convs the device blocks do not cover (mag REGATConv;
+    REGCNConv with self_loop_type 1): exact-size PyG adjs and the real edge types, the same loss
+    and gradients as NeighborSampler + mag.train_step on the same batch; capture() refuses."""
+    from regnn_hip import mag
+    from regnn_hip.sampler import NeighborSampler
+    d = _mag(0.003, seed=1)
+
+    def make():
+        torch.manual_seed(0)
+        if model_kind == "regat":
+            return mag.REGNN(16, 8, 5, 2, 10.0, 0.0, {k: 16 for k in d["x_dict"]}, 7,
+                             use_norm="ln", self_loop_type=2, model="regat", heads=2).to(DEV)
+        return mag.REGNN(16, 32, 5, 2, 10.0, 0.0, {k: 16 for k in d["x_dict"]}, 7,
+                         use_norm="ln", self_loop_type=1).to(DEV)
+    m_api, m_eng = make(), make()
+    smp = NeighborSampler(d["rg"], torch.arange(d["n_paper"], device=DEV), [6, 4], batch_size=64,
+                          shuffle=True, seed=3)
+    batch = next(iter(smp))
+    loss_api = mag.train_step(m_api, torch.optim.SGD(m_api.parameters(), lr=0.0), batch,
+                              d["x_dict"], d["edge_type"], d["node_type"], d["local"], d["y"], 1)
+    tr, _ = _setup_trainer(d, m_eng)
+    assert tr.fused is None
+    tr._forward_backward()
+    torch.cuda.synchronize()
+    la = float(loss_api.detach())
+    assert abs(float(tr.loss) - la) <= 1e-5 * max(1.0, abs(la))
+    gp = dict(m_api.named_parameters())
+    for n, p in m_eng.named_parameters():
+        if gp[n].grad is None:
+            assert not p.grad.any(), n
+            continue
+        ok, err = G.close(p.grad.cpu().numpy(), gp[n].grad.cpu().numpy().astype(np.float64), 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+    with pytest.raises(ValueError):
+        tr.capture(warmup=1)
+
+
 def test_trainer_graph_replay_tracks_eager():
     d = _mag(0.003, seed=2)
     tr_e, _ = _setup_trainer(d, d["model"](7), batch=128, sizes=(10, 5))
     tr_g, _ = _setup_trainer(d, d["model"](7), batch=128, sizes=(10, 5))
-    # capture's warm-up runs optimizer steps: give the eager twin the same steps
+    # capture() undoes its warm-up steps: the first replay trains the epoch's first batch
     tr_g.capture(warmup=2)
-    for _ in range(2):
-        tr_e.step()
-    tr_e.set_epoch(0)                                  # the epoch again from its first batch
     le, lg = [], []
     for _ in range(6):
         tr_e.step()
@@ -167,10 +203,7 @@ def test_pipelined_trainer_matches_unpipelined(graph):
     tr_p, tr_u = make(True), make(False)
     assert tr_p.pipelined and not tr_u.pipelined
     if graph:
-        tr_p.capture(warmup=2)
-        for _ in range(2):
-            tr_u.step()
-        tr_u.set_epoch(0)
+        tr_p.capture(warmup=2)                          # warm-up steps undone by capture()
     run_p = tr_p.replay if graph else tr_p.step
     lp, lu = [], []
     for i in range(7):
@@ -294,6 +327,33 @@ def test_ns_step_mag10_scale():
         assert np.allclose(y[v], want, rtol=1e-5, atol=1e-5)
 
 
+def test_ns_step_mag10_fused_matches_module_path():
+    """the benchmarked mode at its own size: mag_like(10), batch 512, fan-out
+    [25, 20], K = 128, hidden 64, 349 classes, relation slots on and the meta-only last hop.
+    The fused step's loss and every parameter gradient equal the mag.REGNN autograd path's (pinned
+    to the reference REGNN by tests/test_gpu_regnn_golden.py) on the same sampled batch at 1e-5,
+    dropout off."""
+    d = _mag(10.0, seed=0, F=128, hidden=64, classes=349)
+    m_mod, m_fus = d["model"](3), d["model"](3)
+    m_mod.train(); m_fus.train()
+    tr_f, _ = _setup_trainer(d, m_fus, batch=512, sizes=(25, 20), seed=123)
+    assert tr_f.fused is not None and tr_f.fused.P.rel_slots == 1
+    assert tr_f.sampler.meta_only[1]
+    tr_m, _ = _setup_trainer(d, m_mod, batch=512, sizes=(25, 20), seed=123)
+    tr_m.fused = None
+    tr_f._forward_backward()
+    tr_m._forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(tr_m.sampler.sizes[8:10], tr_f.sampler.sizes[8:10])
+    assert int(tr_f.sampler.sizes[9]) > 100_000                 # the full-size layer-0 block
+    lm, lf = float(tr_m.loss), float(tr_f.loss)
+    assert abs(lm - lf) <= 1e-5 * max(1.0, abs(lm)), (lm, lf)
+    gm = dict(m_mod.named_parameters())
+    for n, p in m_fus.named_parameters():
+        ok, err = G.close(p.grad.cpu().numpy(), gm[n].grad.cpu().numpy().astype(np.float64), 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+
+
 def _sample_row_global(row_idx, t, k, seed, base):
     d = row_idx.size
     if d <= k:
@@ -380,10 +440,7 @@ def test_fused_step_graph_replay_tracks_eager(flat_adam):
                          d["node_type"], d["local"], d["y"], 7, seed=3, adam=dict(lr=1e-2))
     tr_e, tr_g = make(), make()
     assert tr_e.fused is not None and tr_g.fused is not None
-    tr_g.capture(warmup=2)
-    for _ in range(2):
-        tr_e.step()
-    tr_e.set_epoch(0)                                  # the epoch again from its first batch
+    tr_g.capture(warmup=2)                             # warm-up steps undone by capture()
     le, lg = [], []
     for _ in range(5):
         tr_e.step()

@@ -65,18 +65,22 @@ def test_regnn_autograd_path_vs_reference(name):
         _check(k, got[k], v)
 
 
-def test_regnn_fused_step_vs_reference(monkeypatch):
+@pytest.mark.parametrize("name,lean", [("mag_regnn_ft3", "off"), ("mag_regnn_schema", "on"),
+                                       ("mag_regnn_schema", "off")])
+def test_regnn_fused_step_vs_reference(monkeypatch, name, lean):
     """regnn_ns_hop reproduces the fixture's sampled batch; regnn_nsm_step's loss and every
-    gradient match the reference REGNN's. (The fixture's relations are drawn at random, not
-    one per (target type, source type) pair, so layer 0 takes the edge pass here; the
-    relation-slot mode is checked on the ogbn-mag-shaped graphs of test_gpu_ns_engine.py.)"""
+    gradient match the reference REGNN's.
+    * mag_regnn_ft3: relations drawn at random (not one per (target type, source type) pair),
+      so layer 0 takes the edge pass (rel_slots 0); the full last hop, whose outermost n_id and
+      per-edge local ids are checked against the fixture;
+    * mag_regnn_schema: the ogbn-mag schema (make_golden._mag_schema_graph), K = 128, hidden
+      64, 349 classes, fan-out [25, 20] -- the mode bench.py times: relation slots on and the
+      meta-only last hop (n_id checked up to the layer-0 targets), and the full hop."""
     from regnn_hip import ns
     from regnn_hip.graph import RelGraph
     from regnn_hip.ns import DeviceSampler, FusedStep
-    # the full last hop (this test checks the outermost n_id and local ids against the fixture;
-    # the meta-only hop is checked against the full one in test_gpu_ns_engine.py)
-    monkeypatch.setitem(ns.LEAN_LAST_HOP, "mode", "off")
-    d = G.load("mag_regnn_ft3")
+    monkeypatch.setitem(ns.LEAN_LAST_HOP, "mode", lean)
+    d = G.load(name)
     m = d["meta"]
     N = int(sum(m["counts"]))
     rg = RelGraph(torch.from_numpy(d["src"]), torch.from_numpy(d["dst"]), N, DEV)
@@ -87,25 +91,38 @@ def test_regnn_fused_step_vs_reference(monkeypatch):
     for p in model.parameters():
         p.grad = torch.zeros_like(p)
     x_dict, _, _, nt, loc = _inputs(d)
-    y_flat = torch.full((N,), -1, dtype=torch.int64)
-    y_flat[:m["counts"][0]] = torch.from_numpy(d["y"])
+    if m.get("y_global"):
+        y_flat = torch.from_numpy(d["y"])
+    else:
+        y_flat = torch.full((N,), -1, dtype=torch.int64)
+        y_flat[:m["counts"][0]] = torch.from_numpy(d["y"])
     loss = torch.zeros((), device=DEV)
     fs = FusedStep(model, ds, x_dict, nt, loc, y_flat, loss)
-    assert fs.P.rel_slots == 0
+    assert fs.P.rel_slots == (1 if m.get("schema") == "ogbn-mag" else 0)
+    L_ = len(m["sizes"])
+    assert ds.meta_only[L_ - 1] == (lean == "on")
     with pytest.raises(RuntimeError):                  # the hops have not run since
         fs.step()
     ds.set_seed(m["seed"], m["epoch"], m["batch_idx"])
     ds.set_targets(torch.from_numpy(d["batch"]).to(DEV))
     ds.run_hops()
-    n_tot = int(ds.sizes[len(m["sizes"])])
-    assert ds.n_id[:n_tot].cpu().numpy().tolist() == d["n_id"].tolist()
-    # the sampler's per-edge source type / table row of the last hop (layer 0's block)
-    et, eo = ds.edge_meta[len(m["sizes"]) - 1]
-    blk = ds.blocks[len(m["sizes"]) - 1]
-    E = int(ds.sizes[8 + len(m["sizes"]) - 1])
-    g = ds.n_id.long()[blk.csr_idx[:E].long()]
-    assert torch.equal(et[:E].long(), nt.to(DEV).long()[g])
-    assert torch.equal(eo[:E], loc.to(DEV).long()[g])
+    # the sampled blocks' sizes: hop h's (n_src, n_dst) of the fixture (adjs outermost first)
+    for h in range(L_):
+        n_src, n_dst = (int(v) for v in d[f"adj{L_ - 1 - h}_size"])
+        assert int(ds.sizes[h]) == n_dst
+        E_h = int(ds.sizes[8 + h])
+        assert E_h == d[f"adj{L_ - 1 - h}_src"].size + n_dst          # + one self loop per row
+    n_chk = int(ds.sizes[L_ if lean == "off" else L_ - 1])
+    assert ds.n_id[:n_chk].cpu().numpy().tolist() == d["n_id"][:n_chk].tolist()
+    if lean == "off":
+        assert n_chk == d["n_id"].size
+        # the sampler's per-edge source type / table row of the last hop (layer 0's block)
+        et, eo = ds.edge_meta[L_ - 1]
+        blk = ds.blocks[L_ - 1]
+        E = int(ds.sizes[8 + L_ - 1])
+        g = ds.n_id.long()[blk.csr_idx[:E].long()]
+        assert torch.equal(et[:E].long(), nt.to(DEV).long()[g])
+        assert torch.equal(eo[:E], loc.to(DEV).long()[g])
     fs.step()
     torch.cuda.synchronize()
     _check("loss", loss, d["loss"])
