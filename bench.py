@@ -284,8 +284,8 @@ def run_ns(args, dev):
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                            "traffic": traffic, "achieved_hbm": hbm,
                            "frac_hbm": None if hbm is None else hbm / HBM_PEAK_GBS,
-                           "pmc": pmc_status, "launch_ms": mean_ms, "launches": launches,
-                           "algorithmic_bytes_per_launch": b,
+                           "pmc": pmc_status, "launch_ms": mean_ms,
+                           "profiled_launches": launches, "algorithmic_bytes_per_launch": b,
                            "note": "algorithmic bytes: bench.ns_step_bytes (DESIGN.md §4b); the "
                                    "step is latency-bound (dependent phases), not byte-bound"}
     cand = {k: v for k, v in kstats.items() if k in ("ns_spmm_fwd", "ns_spmm_bwd")}
