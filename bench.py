@@ -158,22 +158,35 @@ def run_ns_epoch(args, dev):
                                             "cores, hidden 512, real ogbn-mag"}}
 
 
-def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False):
+def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False, two_layer=True, adam_params=0):
     """algorithmic HBM bytes of one fused NS model step (regnn_nsm_step) at the sampled sizes
     sz (regnn_ns_hop sizes: sz[h] = rows after h hops, sz[8 + h] = edges of hop h's block,
-    self loops included): every row / index / feature byte a kernel must read or write once.
-    Layer 0 (block L-1: n rows, E edges, T node types):
-      agg0   E x (K*4 gathered input row + 13 type / row / relation) + n x (T*K*4 S + T*4 w
-             + 3*F*4 a, xs_next, gxs_next + 16 stats / ptr / inv)
-      bwd0   n x (T*K*4 S + F*4 ga + T*K*4 Z + T*8 w / beta + 4)
-      rel0   E x (K*4 input row again + 13) + n x (T*K*4 Z + T*4 beta)
-    With rel_slots (regnn_nsm_params.rel_slots) agg0 also writes each row's self-loop input row
-    and slot relations (n x (K*4 + 4*(T+1))), bwd0 reads them back and writes no Z / beta
-    (n x (T*K*4 U + K*4 + 4*(T+1) + F*4 + 4*T + 4)), and there is no rel0.
-    Layers 1 .. L-2: agg E x (F*4 + 5) + n x (4*F*4 + 20); agg_bwd E x (2*F*4 + 5) + n x (F*4 + 12).
-    post_bwd of layers 0 .. L-2: n x (3*F*4 + 8). Head (layer L-1): E0 x (F*4 + 5) + n0 x (F*4 +
-    24) + out_lin; its agg_bwd E0 x (2*F*4 + 5) + n0 x (F*4 + 12)."""
+    self loops included): every row / index / feature byte a kernel must read or write once
+    (per-block partial slabs are not counted: they are the reductions' own traffic).
+
+    Two-layer step (re_nsm2.hip; n1 = layer 0's target rows, E1 its edges, n0 / E0 layer 1's):
+      agg0      E1 x (K*4 gathered input row + 13 type / row / relation) + n1 x (T*K*4 per-type
+                sums + 4*T counts + 4*F each for a, h0, P + 8*F gradient accumulators zeroed
+                + 16 stats / ptr / inv); relation slots: + n1 x (K*4 self row + 4*(T+1) slots)
+      head      E0 x 2 x (F*4 h0 row + 5) (aggregation, then the transposed pass) + E0 x 8*F
+                (fixed-point accumulators) + n0 x 24 + 4*C*F + 4*F*F
+      bwd0      n1 x (8*F accumulators + 4*F a + 4*F P + 12 stats / inv + T*K*4 per-type sums +
+                4*T counts); relation slots: + n1 x (K*4 self row + 4*(T+1) slots); else
+                + n1 x (T*K*4 Z + 4*T beta) and rel0's E1 x (K*4 + 13) + n1 x (T*K*4 + 4*T)
+      Adam      24 B per parameter (p, m, v read and written) when it runs inside the step
+    The L-layer composed-map form (two_layer=False) keeps round 2's model."""
     f = 4 * F
+    if two_layer and L == 2:
+        n1, E1, n0, E0 = sz[1], sz[9], sz[0], sz[8]
+        b = E1 * (4 * K + 13) + n1 * (T * 4 * K + 4 * T + 3 * f + 2 * f + 16)
+        b += E0 * 2 * (f + 5) + E0 * 2 * f + n0 * 24 + 4 * C * F + 4 * F * F
+        b += n1 * (2 * f + f + f + 12 + T * 4 * K + 4 * T)
+        if rel_slots:
+            b += 2 * n1 * (4 * K + 4 * (T + 1))
+        else:
+            b += n1 * (T * 4 * K + 4 * T)
+            b += E1 * (4 * K + 13) + n1 * (T * 4 * K + 4 * T)
+        return b + 24 * adam_params
     n, E = sz[L - 1], sz[8 + L - 1]
     b = E * (4 * K + 13) + n * (T * 4 * K + 4 * T + 3 * f + 16)       # agg0
     if rel_slots:
@@ -205,8 +218,10 @@ def run_ns(args, dev):
     for _ in range(5):
         tr.step()
         if tr.fused is not None:
-            nsm_bytes.append(ns_step_bytes(tr.sampler.sizes.cpu().tolist(), 128, 349,
-                                           rel_slots=bool(tr.fused.P.rel_slots)))
+            nsm_bytes.append(ns_step_bytes(
+                tr.sampler.sizes.cpu().tolist(), 128, 349, rel_slots=bool(tr.fused.P.rel_slots),
+                two_layer=tr.fused.two_layer,
+                adam_params=tr.flat.numel() if tr.adam_fused else 0))
     torch.cuda.synchronize()
     kstats = profile.summary()
     profile.enable(False)

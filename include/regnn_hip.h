@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 29). */
+/* ABI version (bumped on any signature change or addition; currently 30). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -608,8 +608,15 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  * per target row and source type, then projected). Dropout masks are this build's hash
  * (regnn_spmm_fwd_dropout's spec) keyed on s = mix64(state[0] ^ mix64((state[1] << 40) ^
  * (state[3] << 8) ^ (layer + 0x51ED27))) (seed, epoch, global batch), row = target row of the
- * layer's block, 4 features per 16-byte vector. The transposed aggregation of layers >= 1
- * uses float atomics (as regnn_ns_spmm_bwd); every other reduction is fixed-order.
+ * layer's block, 4 features per 16-byte vector.
+ *
+ * L = 2 (the reference's default num_layers; C <= 432): 4 launches (5 without rel_slots), the
+ * group_input Linear and each conv's x @ W applied after their layer's aggregation (linearity:
+ * mean_e(ew x_e) W = mean_e(ew x_e W)), the transposed aggregation of layer 1 as 2^-40
+ * fixed-point integer sums, every other reduction fixed-order: the step is bitwise
+ * reproducible; optionally the Adam update of regnn_nsm_work.adam in the last launch.
+ * L = 3, 4 (or C > 432): the composed-map form above, 8+ launches, layer >= 1 transposed
+ * aggregations with float atomics (as regnn_ns_spmm_bwd).
  * --------------------------------------------------------------------------------------- */
 #define REGNN_NSM_MAX_TYPES 8
 #define REGNN_NSM_MAX_LAYERS 4
@@ -682,7 +689,28 @@ typedef struct regnn_nsm_work {
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
     float* u_self;            /* rel_slots: cap[L-1] * k_in, each row's self-loop input row */
     int32_t* u_rel;           /* rel_slots: cap[L-1] * (T + 1), relation of each source-type slot */
+    /* the two-layer step (L = 2, C <= 432): */
+    uint64_t* gacc;           /* cap[1] * 64: layer 0 rows' gradient as 2^-40 fixed point (the
+                                 transposed aggregation's integer sums: order-independent) */
+    float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
+    const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
 } regnn_nsm_work;
+
+/* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*
+ * pointer of regnn_nsm_params a view into it; gradients outside [grad_base, grad_base + n) are
+ * written but not stepped): regnn_adam_flat's arithmetic and step counter, applied by the
+ * two-layer step's last launch right after each gradient element's reduction (one rank: no
+ * all-reduce between the backward and the update). */
+typedef struct regnn_nsm_adam {
+    float* param;
+    float* exp_avg;
+    float* exp_avg_sq;
+    const float* grad_base;
+    int64_t n;
+    float lr, beta1, beta2, eps, weight_decay, grad_scale;
+    int64_t* step;
+    uint32_t* ticket;
+} regnn_nsm_adam;
 
 /* Floats of the per-block partial slab regnn_nsm_step needs for these parameters and a batch
  * capacity cap0 (= regnn_nsm_work.cap[0]). */
@@ -690,7 +718,8 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0);
 
 /* One forward + loss + backward of the model over the current batch (after regnn_ns_batch and
  * the L regnn_ns_hop calls of the step): writes every g_* buffer (overwritten, not accumulated)
- * and *loss. 8 kernel launches for L = 2 (L in [2, 4]), none of them sized from the host. */
+ * and *loss (and, with w->adam, updates the parameters). 4 kernel launches for L = 2 with
+ * rel_slots (L in [2, 4]), none of them sized from the host. */
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
 
 /* Adam step over flat buffers (replaces torch.optim.Adam.step, mag/regnn_ns.py:407, for

@@ -1508,10 +1508,30 @@ struct JobList {
 using namespace regnn;
 using namespace regnn::nsm;
 
+int regnn_nsm_rel0(const regnn_nsm_params* p, const regnn_nsm_work* w, float* slab,
+                   hipStream_t stream) {
+    const int T = p->n_types, K = p->k_in, L = p->n_layers, h = L - 1;
+    Ptrs xt{};
+    for (int t = 0; t < T; ++t) xt.p[t] = p->x_tab[t];
+    Rel0Args R{};
+    R.sizes = w->sizes; R.hop = h; R.T = T;
+    R.ptr = w->blk_ptr[h]; R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
+    R.edge_off = w->edge_off; R.xt = xt; R.z = w->z; R.beta = w->beta;
+    R.slab = slab; R.n_rel = p->n_rel[0];
+    const size_t lds = size_t(p->n_rel[0]) * kBlock * sizeof(float);
+    if (K == 128)
+        hipLaunchKernelGGL(rel0_kernel<128>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
+    else
+        hipLaunchKernelGGL(rel0_kernel<64>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
 extern "C" {
 
 int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
     if (!p || cap0 <= 0) return -1;
+    if (regnn_nsm2_covers(p)) return regnn_nsm2_slab_floats(p, cap0);
     return slab_layout(p, cap0).total;
 }
 
@@ -1541,13 +1561,15 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
             return REGNN_EINVAL;
         if (l < L - 1 && (!w->a[l] || !w->stats[l])) return REGNN_EINVAL;
     }
-    const SlabLayout S = slab_layout(p, w->cap[0]);
-    const Drop drop = make_drop(p->p_drop);
     // relation-slot mode: the caller vouches that every (target type, source type) pair has at
     // most one relation besides the self loops (relation ids >= n_edge_types)
     const bool rs = p->rel_slots != 0;
     if (rs && (!w->u_self || !w->u_rel || p->n_edge_types < 0 || p->n_edge_types + T > p->n_rel[0]))
         return REGNN_EINVAL;
+    if (regnn_nsm2_covers(p)) return regnn_nsm2_step(p, w, stream);
+    if (w->adam) return REGNN_EUNSUPPORTED;          // the fused optimizer: two-layer step only
+    const SlabLayout S = slab_layout(p, w->cap[0]);
+    const Drop drop = make_drop(p->p_drop);
     Ptrs lin_w{}, lin_b{}, xt{}, rw{};
     for (int t = 0; t < T; ++t) {
         lin_w.p[t] = p->lin_w[t];
@@ -1676,18 +1698,8 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
         REGNN_LAUNCH_CHECK();
     }
     if (!rs) {
-        const int h = L - 1;
-        Rel0Args R{};
-        R.sizes = w->sizes; R.hop = h; R.T = T;
-        R.ptr = w->blk_ptr[h]; R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
-        R.edge_off = w->edge_off; R.xt = xt; R.z = w->z; R.beta = w->beta;
-        R.slab = w->slab + S.rel[0]; R.n_rel = p->n_rel[0];
-        const size_t lds = size_t(p->n_rel[0]) * kBlock * sizeof(float);
-        if (K == 128)
-            hipLaunchKernelGGL(rel0_kernel<128>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
-        else
-            hipLaunchKernelGGL(rel0_kernel<64>, dim3(kAggBlocks), dim3(kBlock), lds, stream, R);
-        REGNN_LAUNCH_CHECK();
+        const int rc = regnn_nsm_rel0(p, w, w->slab + S.rel[0], stream);
+        if (rc != REGNN_OK) return rc;
     }
     // 7. reductions of every partial into the gradients (and the composed map's gradient)
     {

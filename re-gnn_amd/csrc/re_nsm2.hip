@@ -1,0 +1,1320 @@
+// Two-layer fused NS model step (regnn_nsm_step with L = 2, the reference's num_layers default):
+// the REGNN of mag/regnn_ns.py:216-346 ('regcn', self_loop_type 2, LayerNorm, hidden 64) forward
+// + nll_loss + backward over the blocks regnn_ns_hop wrote, in four launches (five without
+// relation slots), every reduction in a fixed order or exact: two runs of a step give bitwise
+// equal gradients. Optionally the Adam update of every parameter ends the last launch.
+//
+//   agg0      layer 0 (group_input mag/regnn_ns.py:300-326 + REGCNConv mag/regnn_layers.py:
+//             80-150): the sampled input rows summed per target row and source type, projected
+//             in two fp32-MFMA stages -- P = sum_t (S_t W_t^T + w_t b_t) (group_input's Linear,
+//             moved after the mean aggregation by linearity) and a = inv (P W_0) + bias (the
+//             conv's x @ W) -- then LayerNorm, relu, dropout -> h0. Keeps P, a and the LN stats
+//             for the backward; zeroes the rows' fixed-point gradient accumulators.
+//   head      layer 1 aggregated first and projected second (a = inv (sum_e tab[r_e] h0[u_e]) W_1
+//             + bias, the same linearity), LayerNorm, relu, dropout, out_lin, log_softmax,
+//             nll_loss (mean over the labelled targets) and the backward to GH = inv ga W_1^T,
+//             then layer 1's transposed aggregation gh0[u_e] += tab[r_e] GH[v] over the block's
+//             edges as 64-bit fixed-point integer atomics (integer sums: exact in any order) and
+//             the relation-table dots <h0[u_e], GH[v]>.
+//   bwd0      layer 0's backward per target row: the LayerNorm / relu / dropout backward from
+//             gh0, gP = inv ga W_0^T, the W_0 gradient P^T (inv ga); per source type t the
+//             weight gradient gP^T S_t, the bias term, and the relation-table dots from
+//             Z_t = gP W_t (relation slots: <U_t, Z_t> in registers; else Z and beta for rel0).
+//   rel0      (no relation slots) layer 0's relation-table dots edge by edge (re_nsm.hip).
+//   finalize  every gradient as a fixed-order sum of per-block partials; with an optimizer
+//             attached, Adam (regnn_adam_flat's arithmetic) on each element right after its sum.
+#include "re_nsm_common.h"
+
+namespace regnn {
+namespace nsm2 {
+using namespace regnn::nsm;
+
+constexpr int kRows = 16;                  // target rows per block (one MFMA row tile)
+constexpr int kBwdBlocks = 128;            // bwd0 blocks per node type (static slab layout)
+constexpr int kMaxCT = 27;                 // class tiles of 16 (C <= 432: the head's LDS)
+constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
+constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
+
+// contributions are rounded to 2^-40 (|x| < 2^23 per accumulated entry): gradient rows of a
+// mean loss are many orders of magnitude inside that range, and the rounding (<= 4.6e-13 per
+// term) is far below fp32 resolution of the sums it feeds
+__device__ __forceinline__ unsigned long long to_fix(float x) {
+    return (unsigned long long)__float2ll_rn(x * kFixScale);
+}
+
+__device__ __forceinline__ float from_fix(unsigned long long q) {
+    return float((long long)q) * kFixInv;
+}
+
+// relation table entry j of LeakyReLU(alpha * relation_weight) (mag/regnn_layers.py:109-111)
+__device__ __forceinline__ float rel_tab(const float* rw, int nr, float alpha, int j) {
+    if (j >= nr) return 0.f;
+    const float x = rw[j] * alpha;
+    return x > 0.f ? x : 0.01f * x;
+}
+
+#define MFMA4(av, b0, b1, b2, b3, d)                                 \
+    d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).x, (b0), d, 0, 0, 0); \
+    d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).y, (b1), d, 0, 0, 0); \
+    d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).z, (b2), d, 0, 0, 0); \
+    d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).w, (b3), d, 0, 0, 0)
+
+// ---------------------------------------------------------------------------------------------
+// agg0. MFMA lane (c, q) of wave w: A = tile row c, k = 16 b + 4 q + i (i: the 4 instructions of
+// a float4), B = column 16 w + c; D row 4 q + r, column 16 w + c.
+struct Agg0Args {
+    const int32_t* sizes; int hop;
+    const int32_t* ptr; const uint8_t* rel; const float* inv;
+    const int32_t* edge_type; const int64_t* edge_off; Ptrs xt; int T;
+    Ptrs lin_w; Ptrs lin_b;                // lins[t].weight [64][K] (row j, column k), bias [64]
+    const float* rw; int n_rel; float alpha;
+    const float* w0; const float* bias; const float* ln_w; const float* ln_b;
+    const int64_t* state; Drop drop;
+    float* s_agg; float* s_w;
+    float* a; float* stats; float* h; float* p; unsigned long long* gacc;
+    // relation slots (RS): s_agg / s_w hold the unweighted sums / counts of the non-self edges
+    // per source type, u_self the self loop's input row, u_rel [n][T + 1] each slot's relation
+    int n_et; float* u_self; int32_t* u_rel;
+};
+
+// LDS: S tile [16][T K + 4] | s_w [16][MT] | P [16][68] | pre-LN rows [16][64] | table [64]
+inline size_t agg0_lds(int T, int K) {
+    return (size_t(16) * (T * K + 4) + 16 * MT + 16 * 68 + 16 * F + F) * sizeof(float);
+}
+
+template <int K, int NT, bool RS>
+__global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
+    constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
+    constexpr int KB = K / 16;
+    constexpr int HB = KB / 2;             // float4 steps per half type
+    extern __shared__ float sm[];
+    const int T = A.T;
+    const int SR = T * K + 4;
+    float* St = sm;                        // [16][SR]
+    float* sw = St + 16 * SR;              // [16][MT]
+    float* Pt = sw + 16 * MT;              // [16][68]
+    float* at = Pt + 16 * 68;              // [16][F]
+    float* tab = at + 16 * F;              // [F]
+    if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    const int n = A.sizes[A.hop];
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
+    const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
+    float w0c[16];                         // W_0[16 b + 4 q + i][16 w + c]: the second stage's B
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w0c[4 * b + i] = A.w0[(16 * b + 4 * q + i) * F + 16 * w + c];
+    const float bj = A.bias[16 * w + c];
+    __syncthreads();
+    for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
+        // ---- gather: per-type register sums of this lane's 4 * VPL features
+        const int v = base + sub;
+        float wsum[NT];
+        float4 racc[NT][VPL];
+        int rel_t[NT];
+        float4 xself[VPL];
+        int r_self = -1;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            wsum[tt] = 0.f;
+            rel_t[tt] = -1;
+#pragma unroll
+            for (int p = 0; p < VPL; ++p) racc[tt][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int p = 0; p < VPL; ++p) xself[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (v < n) {
+            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            for (int c0 = e0; c0 < e1; c0 += 16) {
+                const int m = min(16, e1 - c0);
+                int my_t = 0, my_lo = 0;           // table rows < 2^31 (checked by the host)
+                float my_w = 0.f;
+                int my_r = 0;
+                if (l < m) {
+                    my_t = A.edge_type[c0 + l];
+                    my_lo = int(A.edge_off[c0 + l]);
+                    my_r = A.rel[c0 + l];
+                    my_w = tab[my_r];
+                }
+                constexpr int UN = 8;              // edges' rows in flight per lane
+                for (int j = 0; j < m; j += UN) {
+                    int t[UN], ru[UN];
+                    float wt[UN];
+                    float4 x[UN][VPL];
+#pragma unroll
+                    for (int u = 0; u < UN; ++u) {
+                        const int jj = min(j + u, m - 1);
+                        t[u] = __shfl(my_t, gl + jj, 64);
+                        if constexpr (RS) ru[u] = __shfl(my_r, gl + jj, 64);
+                        else wt[u] = __shfl(my_w, gl + jj, 64);
+                        const int64_t lo = __shfl(my_lo, gl + jj, 64);
+                        const float* xr = pick(A.xt.p, t[u]) + lo * K + 4 * l;
+#pragma unroll
+                        for (int p = 0; p < VPL; ++p) x[u][p] = *reinterpret_cast<const float4*>(xr + 64 * p);
+                        if (j + u >= m) t[u] = -1;     // padding: loaded (a valid row), not added
+                    }
+#pragma unroll
+                    for (int u = 0; u < UN; ++u) {
+                        if (t[u] < 0) continue;
+                        if constexpr (RS) {
+                            if (ru[u] >= A.n_et) {         // the self loop (one per row)
+                                r_self = ru[u];
+#pragma unroll
+                                for (int p = 0; p < VPL; ++p) xself[p] = x[u][p];
+                                continue;
+                            }
+                        }
+#pragma unroll
+                        for (int tt = 0; tt < NT; ++tt) {
+                            if (tt != t[u]) continue;
+                            if constexpr (RS) {
+                                wsum[tt] += 1.f;
+                                rel_t[tt] = ru[u];
+#pragma unroll
+                                for (int p = 0; p < VPL; ++p) {
+                                    racc[tt][p].x += x[u][p].x;
+                                    racc[tt][p].y += x[u][p].y;
+                                    racc[tt][p].z += x[u][p].z;
+                                    racc[tt][p].w += x[u][p].w;
+                                }
+                            } else {
+                                wsum[tt] += wt[u];
+#pragma unroll
+                                for (int p = 0; p < VPL; ++p) {
+                                    racc[tt][p].x = fmaf(wt[u], x[u][p].x, racc[tt][p].x);
+                                    racc[tt][p].y = fmaf(wt[u], x[u][p].y, racc[tt][p].y);
+                                    racc[tt][p].z = fmaf(wt[u], x[u][p].z, racc[tt][p].z);
+                                    racc[tt][p].w = fmaf(wt[u], x[u][p].w, racc[tt][p].w);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        // the first stage's first W_t fragment is requested before the S tile's stores
+        float4 bcur[HB], bnext[HB];
+        auto bload = [&](int step, float4 (&dst)[HB]) {
+            const int tt = step >> 1, h0 = (step & 1) * HB;
+            const float* wt = pick(A.lin_w.p, tt) + (16 * w + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+        };
+        bload(0, bcur);
+        const int tau = r_self - A.n_et;           // RS: the row's node type
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            if (tt < T) {
+                float wr = 1.f, ws = 0.f;              // RS: S = wr U + ws x_self
+                if constexpr (RS) {
+                    wr = rel_t[tt] >= 0 ? tab[rel_t[tt]] : 0.f;
+                    ws = (tt == tau) ? tab[r_self] : 0.f;
+                }
+#pragma unroll
+                for (int p = 0; p < VPL; ++p) {
+                    float4 sv = racc[tt][p];
+                    if constexpr (RS)
+                        sv = make_float4(fmaf(ws, xself[p].x, wr * sv.x), fmaf(ws, xself[p].y, wr * sv.y),
+                                         fmaf(ws, xself[p].z, wr * sv.z), fmaf(ws, xself[p].w, wr * sv.w));
+                    *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l + 64 * p) = sv;
+                    if (v < n)
+                        *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l + 64 * p) =
+                            racc[tt][p];
+                }
+                if (l == 0) {
+                    sw[sub * MT + tt] = RS ? fmaf(wr, wsum[tt], ws) : wsum[tt];
+                    if (v < n) {
+                        A.s_w[int64_t(v) * T + tt] = wsum[tt];
+                        if constexpr (RS) A.u_rel[int64_t(v) * (T + 1) + tt] = rel_t[tt];
+                    }
+                }
+            }
+        }
+        if constexpr (RS) {
+            if (v < n) {
+#pragma unroll
+                for (int p = 0; p < VPL; ++p)
+                    *reinterpret_cast<float4*>(A.u_self + int64_t(v) * K + 4 * l + 64 * p) = xself[p];
+                if (l == 0) A.u_rel[int64_t(v) * (T + 1) + T] = r_self;
+            }
+        }
+        __syncthreads();
+        // ---- stage 1: P[v][j] = sum_t S_vt W_t[j][:] + w_vt b_t[j]; type t + 1's rows of W_t
+        // are loaded while type t's products run
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        for (int step = 0; step < 2 * T; ++step) {
+            if (step + 1 < 2 * T) bload(step + 1, bnext);
+            const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                MFMA4(av, bcur[b].x, bcur[b].y, bcur[b].z, bcur[b].w, d);
+            }
+#pragma unroll
+            for (int b = 0; b < HB; ++b) bcur[b] = bnext[b];
+        }
+        {
+            const int j = 16 * w + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int vr = 4 * q + r;
+                float bsum = 0.f;
+                for (int tt = 0; tt < T; ++tt) bsum = fmaf(sw[vr * MT + tt], pick(A.lin_b.p, tt)[j], bsum);
+                Pt[vr * 68 + j] = d[r] + bsum;
+            }
+        }
+        __syncthreads();
+        // ---- stage 2: a = inv (P W_0) + bias
+        {
+            f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(Pt + c * 68 + 16 * b + 4 * q);
+                MFMA4(av, w0c[4 * b], w0c[4 * b + 1], w0c[4 * b + 2], w0c[4 * b + 3], d2);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int vr = 4 * q + r, vv = base + vr;
+                const float iv = vv < n ? A.inv[vv] : 0.f;
+                at[vr * F + 16 * w + c] = fmaf(iv, d2[r], bj);
+            }
+        }
+        __syncthreads();
+        // ---- epilogue: P and a kept, LayerNorm, relu, dropout -> h0; gradient accumulators 0
+        if (v < n) {
+            *reinterpret_cast<float4*>(A.p + int64_t(v) * F + 4 * l) =
+                *reinterpret_cast<const float4*>(Pt + sub * 68 + 4 * l);
+            const float4 a4 = *reinterpret_cast<const float4*>(at + sub * F + 4 * l);
+            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+            *reinterpret_cast<float4*>(A.a + int64_t(v) * F + 4 * l) = a4;
+            const float mean = group_sum<16>(av[0] + av[1] + av[2] + av[3]) * (1.f / F);
+            const float dd[4] = {av[0] - mean, av[1] - mean, av[2] - mean, av[3] - mean};
+            const float var = group_sum<16>(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2] + dd[3] * dd[3]) * (1.f / F);
+            const float rstd = rsqrtf(var + kLnEps);
+            if (l == 0) reinterpret_cast<float2*>(A.stats)[v] = make_float2(mean, rstd);
+            const float gws[4] = {gw.x, gw.y, gw.z, gw.w}, gbs[4] = {gb.x, gb.y, gb.z, gb.w};
+            float mk[4];
+            drop_factors(key, A.drop, v, l, mk);
+            float hv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) hv[cc] = fmaxf(fmaf(dd[cc] * rstd, gws[cc], gbs[cc]), 0.f) * mk[cc];
+            *reinterpret_cast<float4*>(A.h + int64_t(v) * F + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+            ulonglong2* gz = reinterpret_cast<ulonglong2*>(A.gacc + int64_t(v) * F + 4 * l);
+            gz[0] = make_ulonglong2(0ull, 0ull);
+            gz[1] = make_ulonglong2(0ull, 0ull);
+        }
+        __syncthreads();                       // the tiles are reused by the next rows
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// head: 16 target rows per block.
+//   1. Hagg[v] = sum_e tab[r_e] h0[u_e] (16 lanes per row) -> LDS;
+//   2. a = inv (Hagg W_1) + bias (MFMA, W_1 fragments from L2 in registers);
+//   3. LayerNorm, relu, dropout -> h (16 lanes per row);
+//   4. z = h W_out^T + b_out (class tiles over the waves), log_softmax, nll, g = (softmax -
+//      onehot) / n_valid, gh = g W_out, LayerNorm / relu / dropout backward -> ga, G = inv ga;
+//   5. partials: out_lin weight g^T h, its bias, conv bias / LN terms, the loss;
+//   6. GH = G W_1^T and the W_1 partial Hagg^T G (MFMA);
+//   7. the block's edges again: gh0[u_e] += tab[r_e] GH[v] (fixed-point atomics), relation
+//      dots <h0[u_e], GH[v]> per row, summed over the rows in order.
+// out_lin.weight staged by LDS-DMA into an XOR-swizzled image (head_sw), as re_nsm.hip's head.
+// Slab row per block: [C*64 g out_w | C g out_b | 64 conv bias | 64 LN beta | 64 LN gamma |
+//                      1 loss | 64*64 g W_1 | 64 relation dots]
+struct HeadArgs {
+    const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
+    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const float* rw; int n_rel; float alpha;
+    const float* h; const float* w1; const float* bias; const float* ln_w; const float* ln_b;
+    const int64_t* state; Drop drop;
+    const float* w_out; const float* b_out; int C;
+    unsigned long long* gacc; float* nvalid; float* part; int64_t part_w;
+};
+
+inline int64_t head_part_width(int C) {
+    return (int64_t(C) * (F + 1) + 3 * F + 1 + F * F + F + 3) & ~3ll;
+}
+__host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }
+__host__ __device__ inline int head_wl(int C) {
+    const int wl = ((C + 15) / 16) * 16 * F, red = 3 * 16 * F + 16 * 68;
+    return wl > red ? wl : red;
+}
+inline size_t head_lds(int C) {
+    return (size_t(head_wl(C)) + 16 * head_cp(C) + 16 * 68 + 16 * 80 + 16 * 68 + 16 * 68) *
+           sizeof(float);
+}
+
+__device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c & 15) << 2)); }
+
+__global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
+    extern __shared__ float hl[];
+    const int C = A.C, CT = (C + 15) / 16, CP = head_cp(C);
+    float* Wl = hl;                        // W_out image; after step 4: red [3][16][64], GH [16][68]
+    float* zs = Wl + head_wl(C);           // [16][CP]: z, then g; after step 5: relation dots
+    float* hs = zs + 16 * CP;              // [16][68]: h (row reads), then G
+    float* hs2 = hs + 16 * 68;             // [16][80]: h (column reads)
+    float* ghs = hs2 + 16 * 80;            // [16][68]: a, then gh
+    float* hg = ghs + 16 * 68;             // [16][68]: Hagg
+    float* red = Wl;
+    float* gH = Wl + 3 * 16 * F;
+    float* bins = zs;                      // [16][64]
+    __shared__ float tab[F];
+    __shared__ float lrow[kRows];
+    __shared__ int wcnt[kBlock / 64];
+    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
+    const int n = A.sizes[0];
+    const int v = blockIdx.x * kRows + sub;
+    const bool act = v < n;
+    const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
+    {   // out_lin.weight -> LDS by LDS-DMA; lane L writes slot L%16 of row c, which holds
+        // W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw); pad rows c >= C read row C-1
+        const int L64 = threadIdx.x & 63;
+        for (int i = threadIdx.x >> 6; i < CT * 4; i += kBlock / 64) {
+            const int c = 4 * i + (L64 >> 4);
+            const int cs = c < C ? c : C - 1;
+            const float* src = A.w_out + int64_t(cs) * F + 4 * ((L64 & 15) ^ (c & 15));
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)src,
+                (__attribute__((address_space(3))) void*)(Wl + 4 * i * F), 16, 0, 0);
+        }
+    }
+    float w1c[16];                         // W_1[16 b + 4 q + i][16 w + cc]: step 2's B operand
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w1c[4 * b + i] = A.w1[(16 * b + 4 * q + i) * F + 16 * w + cc];
+    {   // the labelled-target count nll_loss divides by, while the DMA lands
+        int cnt_valid = 0;
+        for (int i = threadIdx.x; i < n; i += kBlock) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cnt_valid += __shfl_xor(cnt_valid, o, 64);
+        if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = cnt_valid;
+    }
+    if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    __syncthreads();
+    // ---- 1. Hagg
+    {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (act) {
+            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            for (int c0 = e0; c0 < e1; c0 += 16) {
+                const int m = min(16, e1 - c0);
+                const int my_u = l < m ? A.idx[c0 + l] : 0;
+                const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
+                constexpr int UN = 8;
+                for (int j = 0; j < m; j += UN) {
+                    float4 x[UN];
+                    float wt[UN];
+#pragma unroll
+                    for (int u = 0; u < UN; ++u) {
+                        const int jj = min(j + u, m - 1);
+                        const int uu = __shfl(my_u, gl + jj, 64);
+                        wt[u] = j + u < m ? tab[__shfl(my_r, gl + jj, 64)] : 0.f;
+                        x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu) * F + 4 * l);
+                    }
+#pragma unroll
+                    for (int u = 0; u < UN; ++u) {
+                        if (j + u >= m) break;
+                        s0 = fmaf(wt[u], x[u].x, s0); s1 = fmaf(wt[u], x[u].y, s1);
+                        s2 = fmaf(wt[u], x[u].z, s2); s3 = fmaf(wt[u], x[u].w, s3);
+                    }
+                }
+            }
+        }
+        *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
+    }
+    __syncthreads();
+    // ---- 2. a = inv (Hagg W_1) + bias -> ghs
+    {
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float4 av = *reinterpret_cast<const float4*>(hg + cc * 68 + 16 * b + 4 * q);
+            MFMA4(av, w1c[4 * b], w1c[4 * b + 1], w1c[4 * b + 2], w1c[4 * b + 3], d);
+        }
+        const int j = 16 * w + cc;
+        const float bj = A.bias[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int vr = 4 * q + r, vv = blockIdx.x * kRows + vr;
+            const float iv = vv < n ? A.inv[vv] : 0.f;
+            ghs[vr * 68 + j] = fmaf(iv, d[r], bj);
+        }
+    }
+    __syncthreads();
+    // ---- 3. LayerNorm, relu, dropout
+    const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
+    const float gwf[4] = {gw4.x, gw4.y, gw4.z, gw4.w}, gbf[4] = {gb4.x, gb4.y, gb4.z, gb4.w};
+    float xhat[4] = {0.f, 0.f, 0.f, 0.f}, mfac[4] = {0.f, 0.f, 0.f, 0.f}, rstd = 0.f;
+    float hv[4] = {0.f, 0.f, 0.f, 0.f};
+    const float ivv = act ? A.inv[v] : 0.f;
+    if (act) {
+        const float4 a4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
+        const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+        const float mean = group_sum<16>(a[0] + a[1] + a[2] + a[3]) * (1.f / F);
+        const float d[4] = {a[0] - mean, a[1] - mean, a[2] - mean, a[3] - mean};
+        rstd = rsqrtf(group_sum<16>(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) *
+                          (1.f / F) + kLnEps);
+        const uint32_t key = A.drop.on ? layer_key(A.state, 1) : 0u;
+        drop_factors(key, A.drop, v, l, mfac);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xhat[i] = d[i] * rstd;
+            hv[i] = fmaxf(fmaf(xhat[i], gwf[i], gbf[i]), 0.f) * mfac[i];
+        }
+    }
+    *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    __syncthreads();
+    const int n_valid = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
+    // ---- 4a. z = h W^T + b -> zs (classes >= C: -inf)
+    for (int ct = w; ct < CT; ct += kBlock / 64) {
+        const int c = 16 * ct + cc;
+        f32x4 dz = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < F / 16; ++b) {
+            const float4 av = *reinterpret_cast<const float4*>(hs + cc * 68 + 16 * b + 4 * q);
+            const float4 bv = *reinterpret_cast<const float4*>(Wl + head_sw(c, 16 * b + 4 * q));
+            MFMA4(av, bv.x, bv.y, bv.z, bv.w, dz);
+        }
+        const float bo = c < C ? A.b_out[c] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zs[(4 * q + r) * CP + c] = c < C ? dz[r] + bo : -INFINITY;
+    }
+    __syncthreads();
+    // ---- 4b. log_softmax, nll, g
+    {                                      // lane l holds classes l + 16 i of row sub
+        float zr[kMaxCT];
+        float zmax = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            zr[i] = i < CT ? zs[sub * CP + l + 16 * i] : -INFINITY;
+            zmax = fmaxf(zmax, zr[i]);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
+        float se = 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            zr[i] = expf(zr[i] - zmax);        // classes >= C: exp(-inf) = 0
+            se += zr[i];
+        }
+        se = group_sum<16>(se);
+        const float lse = zmax + logf(se), rse = 1.f / se;
+        const float zy = y >= 0 ? zs[sub * CP + y] : 0.f;
+        if (l == 0) lrow[sub] = y >= 0 ? lse - zy : 0.f;
+        const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxCT; ++i) {
+            const int c = l + 16 * i;
+            if (i < CT)
+                zs[sub * CP + c] = act && c < C ? (zr[i] * rse - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
+        }
+    }
+    __syncthreads();
+    // ---- 4c. gh = g W: wave w -> features 16 w + cc, rows 4 q + r
+    {
+        const int k = 16 * w + cc;
+        auto step = [&](int b, f32x4 d) {
+            const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
+            const int c0 = 16 * b + 4 * q;
+            const float w0 = Wl[head_sw(c0 + 0, k)], w1 = Wl[head_sw(c0 + 1, k)];
+            const float w2 = Wl[head_sw(c0 + 2, k)], w3 = Wl[head_sw(c0 + 3, k)];
+            MFMA4(av, w0, w1, w2, w3, d);
+            return d;
+        };
+        f32x4 dg0 = {0.f, 0.f, 0.f, 0.f}, dg1 = {0.f, 0.f, 0.f, 0.f};
+        int b = 0;
+        for (; b + 1 < CT; b += 2) {
+            dg0 = step(b, dg0);
+            dg1 = step(b + 1, dg1);
+        }
+        if (b < CT) dg0 = step(b, dg0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
+    }
+    __syncthreads();
+    // ---- 4d. LayerNorm / relu / dropout backward -> ga; G = inv ga -> hs; row terms -> red
+    float4 w1r[4];                         // W_1[16 w + cc][16 b + 4 q ..]: step 6's B operand
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        w1r[b] = *reinterpret_cast<const float4*>(A.w1 + (16 * w + cc) * F + 16 * b + 4 * q);
+    {
+        const float4 g4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
+        const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+        float gy[4], gx[4];
+        float p1 = 0.f, p2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float yv = fmaf(xhat[i], gwf[i], gbf[i]);
+            gy[i] = act && yv > 0.f ? g[i] * mfac[i] : 0.f;
+            gx[i] = gy[i] * gwf[i];
+            p1 += gx[i];
+            p2 += gx[i] * xhat[i];
+        }
+        const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
+        float ga[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ga[i] = act ? rstd * (gx[i] - m1 - xhat[i] * m2) : 0.f;
+        *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) =
+            make_float4(ivv * ga[0], ivv * ga[1], ivv * ga[2], ivv * ga[3]);
+        *reinterpret_cast<float4*>(red + (0 * 16 + sub) * F + 4 * l) = make_float4(ga[0], ga[1], ga[2], ga[3]);
+        *reinterpret_cast<float4*>(red + (1 * 16 + sub) * F + 4 * l) = make_float4(gy[0], gy[1], gy[2], gy[3]);
+        *reinterpret_cast<float4*>(red + (2 * 16 + sub) * F + 4 * l) =
+            make_float4(gy[0] * xhat[0], gy[1] * xhat[1], gy[2] * xhat[2], gy[3] * xhat[3]);
+    }
+    __syncthreads();
+    float* o = A.part + int64_t(blockIdx.x) * A.part_w;
+    const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
+    const int64_t o_w1 = o_loss + 1, o_r1 = o_w1 + F * F;
+    // ---- 5. out_lin weight partial D[c][k] = sum_v g[v][c] h[v][k], its bias, row terms
+    for (int ct = w; ct < CT; ct += kBlock / 64) {
+        f32x4 dw[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) dw[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            const float av = zs[r * CP + 16 * ct + cc];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+                dw[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, hs2[r * 80 + 16 * kb + cc], dw[kb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * ct + 4 * q + r;
+                if (c < C) o[int64_t(c) * F + 16 * kb + cc] = dw[kb][r];
+            }
+    }
+    for (int c = threadIdx.x; c < C; c += kBlock) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc += zs[r * CP + c];
+        o[o_ob + c] = acc;
+    }
+    if (threadIdx.x < 3 * F) {                                 // conv bias, LN beta, LN gamma
+        const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc += red[(which * 16 + r) * F + f];
+        o[o_cb + threadIdx.x] = acc;
+    }
+    if (threadIdx.x == 0) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc += lrow[r];
+        o[o_loss] = acc;
+    }
+    __syncthreads();                       // zs / red free: relation dots and GH go there
+    // ---- 6. GH = G W_1^T -> gH; W_1 partial D[k][j] = sum_v Hagg[v][k] G[v][j]
+    {
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float4 av = *reinterpret_cast<const float4*>(hs + cc * 68 + 16 * b + 4 * q);
+            MFMA4(av, w1r[b].x, w1r[b].y, w1r[b].z, w1r[b].w, d);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gH[(4 * q + r) * 68 + 16 * w + cc] = d[r];
+        f32x4 dw[4];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) dw[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            const float av = hg[r * 68 + 16 * w + cc];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+                dw[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, hs[r * 68 + 16 * jb + cc], dw[jb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[o_w1 + (16 * w + 4 * q + i) * F + 16 * jb + cc] = dw[jb][i];
+    }
+    for (int i = threadIdx.x; i < 16 * F; i += kBlock) bins[i] = 0.f;
+    __syncthreads();
+    // ---- 7. transposed aggregation into layer 0's rows + relation dots
+    if (act) {
+        const float4 g4 = *reinterpret_cast<const float4*>(gH + sub * 68 + 4 * l);
+        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        for (int c0 = e0; c0 < e1; c0 += 16) {
+            const int m = min(16, e1 - c0);
+            const int my_u = l < m ? A.idx[c0 + l] : 0;
+            const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
+            constexpr int UN = 8;
+            for (int j = 0; j < m; j += UN) {
+                float4 x[UN];
+                int uu[UN], rr[UN];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    const int jj = min(j + u, m - 1);
+                    uu[u] = __shfl(my_u, gl + jj, 64);
+                    rr[u] = __shfl(my_r, gl + jj, 64);
+                    x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu[u]) * F + 4 * l);
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    if (j + u >= m) break;     // uniform over the row's 16 lanes
+                    const float dot = group_sum<16>(x[u].x * g4.x + x[u].y * g4.y +
+                                                    x[u].z * g4.z + x[u].w * g4.w);
+                    if (l == 0) bins[sub * F + rr[u]] += dot;
+                    const float wt = tab[rr[u]];
+                    unsigned long long* dst = A.gacc + int64_t(uu[u]) * F + 4 * l;
+                    atomicAdd(dst + 0, to_fix(wt * g4.x));
+                    atomicAdd(dst + 1, to_fix(wt * g4.y));
+                    atomicAdd(dst + 2, to_fix(wt * g4.z));
+                    atomicAdd(dst + 3, to_fix(wt * g4.w));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < F) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc += bins[r * F + threadIdx.x];
+        o[o_r1 + threadIdx.x] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bwd0: block (b, t) takes 16-row tiles b, b + gridDim.x, ... of layer 0's targets; the next
+// tile's rows are prefetched into registers while this one is processed. Per tile:
+//   front  (16 lanes per row) gh0 = fixed-point sums / 2^40, LayerNorm / relu / dropout backward
+//          -> ga, G0 = inv ga; t = 0 also sums ga, gy, gy * xhat (conv bias, LN beta / gamma);
+//   gP     = G0 W_0^T (MFMA; W_0 rows from L2 in registers); t = 0: W_0 partial P^T G0;
+//   type t gW_t partial gP^T S_t (stored [64][K], lins[t].weight's layout), gb_t = sum w_t gP,
+//          Z_t = gP W_t (MFMA, W_t staged in LDS k-major): relation slots: the relation dots
+//          <U_t, Z_t> + cnt beta and <x_self, Z_t> + beta in per-row bin columns (no Z to HBM);
+//          else Z, beta -> HBM for rel0.
+struct Bwd0Args {
+    const int32_t* sizes; int hop; int T;
+    const float* inv; const unsigned long long* gacc; const float* a; const float* stats;
+    const float* ln_w; const float* ln_b; const int64_t* state; Drop drop;
+    const float* p; const float* w0;
+    const float* s_agg; const float* s_w; Ptrs lin_w; Ptrs lin_b;
+    const float* rw; int n_rel; float alpha; int n_et;
+    const float* u_self; const int32_t* u_rel;
+    float* z; float* beta;
+    float* slab;     // [t][block][(K + 1) * 64]: g W_t ([64][K]) | g b_t
+    float* rslab;    // relation slots: [t][block][64] relation dots
+    float* slab0;    // [block][64 * 64 + 3 * 64]: g W_0 | g conv bias | g LN beta | g LN gamma
+};
+
+constexpr int kPost0W = F * F + 3 * F;
+
+template <int K, bool RS>
+constexpr size_t bwd0_lds_floats(int n_rel) {
+    return size_t(K) * (F + 4) + F + 16 * (K + 4) * (RS ? 2 : 1) + 16 * (F + 16) + 16 * (F + 4) +
+           2 * 16 * 68 + F + 16 * 4 + 16 * 2 + 4 * 16 * 2 + size_t(n_rel) * 16;
+}
+
+template <int K, bool RS>
+__global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
+    constexpr int XS = K + 4, GS = F + 16, G2 = F + 4, WS = F + 4;
+    constexpr int KB = K / 64;                // k blocks per wave
+    constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile of a K-wide row
+    extern __shared__ float sm[];
+    float* Wk = sm;                           // [K][WS]: W_t k-major; at the end the row terms
+    float* bc = Wk + K * WS;                  // [F] b_t
+    float* ush = bc + F;                      // [16][XS] U_t (RS) or S_t
+    float* xsh = ush + 16 * XS;               // [16][XS] x_self (RS only)
+    float* gsh = xsh + (RS ? 16 * XS : 0);    // [16][GS] gP
+    float* gs2 = gsh + 16 * GS;               // [16][G2] gP
+    float* g0s = gs2 + 16 * G2;               // [16][68] G0
+    float* psh = g0s + 16 * 68;               // [16][68] P (t = 0)
+    float* tabl = psh + 16 * 68;              // [F]
+    float* rm = tabl + F;                     // [16][4]: wr, ws, cnt, beta
+    int* rr = reinterpret_cast<int*>(rm + 64);  // [16][2]: r_vt (or -1), r_self (or -1)
+    float* dred = reinterpret_cast<float*>(rr + 32);   // [4 waves][16][2]
+    float* bins = dred + 128;                 // [n_rel][16]
+    const int t = blockIdx.y, T = A.T;
+    const bool t0 = t == 0;
+    const float* wt = pick(A.lin_w.p, t);
+    for (int e = threadIdx.x; e < K * F; e += kBlock) {       // W_t[j][k] -> Wk[k][j]
+        const int j = e / K, k = e - j * K;
+        Wk[k * WS + j] = wt[e];
+    }
+    if (threadIdx.x < F) {
+        bc[threadIdx.x] = pick(A.lin_b.p, t)[threadIdx.x];
+        tabl[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    }
+    if constexpr (RS)
+        for (int i = threadIdx.x; i < A.n_rel * 16; i += kBlock) bins[i] = 0.f;
+    const int n = A.sizes[A.hop];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int gr = threadIdx.x >> 4, gj = threadIdx.x & 15;
+    const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
+    const float4 lw4 = reinterpret_cast<const float4*>(A.ln_w)[gj];
+    const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[gj];
+    const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
+    float4 w0r[4];                            // W_0[16 w + c][16 b + 4 q ..]: gP's B operand
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        w0r[b] = *reinterpret_cast<const float4*>(A.w0 + (16 * w + c) * F + 16 * b + 4 * q);
+    f32x4 acc[KB][4], acc0[4];
+#pragma unroll
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) acc[a][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) acc0[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
+    // prefetched rows of the next tile
+    float4 ur[XV], xr[XV];
+    ulonglong2 gq0, gq1;
+    float4 a4, p4;
+    float2 st2;
+    float ivv = 0.f, cntv = 0.f;
+    int relv = -1, rsv = -1;
+    auto load = [&](int v0) {
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            const bool ok = v0 + r < n;
+            ur[u] = ok ? *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (RS)
+                xr[u] = ok ? *reinterpret_cast<const float4*>(A.u_self + int64_t(v0 + r) * K + 4 * k4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int v = v0 + gr;
+        if (v < n) {
+            const ulonglong2* g = reinterpret_cast<const ulonglong2*>(A.gacc + int64_t(v) * F + 4 * gj);
+            gq0 = g[0];
+            gq1 = g[1];
+            a4 = *reinterpret_cast<const float4*>(A.a + int64_t(v) * F + 4 * gj);
+            st2 = reinterpret_cast<const float2*>(A.stats)[v];
+            ivv = A.inv[v];
+            if (t0) p4 = *reinterpret_cast<const float4*>(A.p + int64_t(v) * F + 4 * gj);
+        }
+        if (threadIdx.x < 16) {
+            const int vv = v0 + threadIdx.x;
+            const bool ok = vv < n;
+            cntv = ok ? A.s_w[int64_t(vv) * T + t] : 0.f;
+            if constexpr (RS) {
+                relv = ok ? A.u_rel[int64_t(vv) * (T + 1) + t] : -1;
+                rsv = ok ? A.u_rel[int64_t(vv) * (T + 1) + T] : -1;
+            }
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile * 16 < n) load(tile * 16);
+    __syncthreads();
+    for (; tile * 16 < n; tile += gridDim.x) {
+        const int v0 = tile * 16;
+        // ---- front: LayerNorm / relu / dropout backward of row v0 + gr, features 4 gj ..
+        {
+            const int v = v0 + gr;
+            const bool ok = v < n;
+            float g0[4] = {0.f, 0.f, 0.f, 0.f};
+            if (ok) {
+                const float gh[4] = {from_fix(gq0.x), from_fix(gq0.y), from_fix(gq1.x), from_fix(gq1.y)};
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                float mk[4];
+                drop_factors(key, A.drop, v, gj, mk);
+                float xh[4], gy[4], gx[4], p1 = 0.f, p2 = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    xh[i] = (av[i] - st2.x) * st2.y;
+                    const float yv = fmaf(xh[i], lw[i], lb[i]);
+                    gy[i] = yv > 0.f ? gh[i] * mk[i] : 0.f;
+                    gx[i] = gy[i] * lw[i];
+                    p1 += gx[i];
+                    p2 += gx[i] * xh[i];
+                }
+                const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float ga = st2.y * (gx[i] - m1 - xh[i] * m2);
+                    g0[i] = ivv * ga;
+                    if (t0) {
+                        sga[i] += ga;
+                        sgy[i] += gy[i];
+                        sgyx[i] += gy[i] * xh[i];
+                    }
+                }
+            }
+            *reinterpret_cast<float4*>(g0s + gr * 68 + 4 * gj) = make_float4(g0[0], g0[1], g0[2], g0[3]);
+            if (t0)
+                *reinterpret_cast<float4*>(psh + gr * 68 + 4 * gj) = ok ? p4 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (threadIdx.x < 16) {                // row meta: S = wr U + ws x_self (RS)
+            if constexpr (RS) {
+                const bool self = rsv >= 0 && rsv - A.n_et == t;
+                rm[4 * threadIdx.x] = relv >= 0 ? tabl[relv] : 0.f;
+                rm[4 * threadIdx.x + 1] = self ? tabl[rsv] : 0.f;
+                rr[2 * threadIdx.x] = (relv >= 0 && cntv > 0.f) ? relv : -1;
+                rr[2 * threadIdx.x + 1] = self ? rsv : -1;
+            } else {
+                rm[4 * threadIdx.x] = 1.f;
+                rm[4 * threadIdx.x + 1] = 0.f;
+            }
+            rm[4 * threadIdx.x + 2] = cntv;
+        }
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int e = threadIdx.x + kBlock * u;
+            const int r = e / (K / 4), k4 = e - r * (K / 4);
+            *reinterpret_cast<float4*>(ush + r * XS + 4 * k4) = ur[u];
+            if constexpr (RS) *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[u];
+        }
+        __syncthreads();
+        if ((tile + gridDim.x) * 16 < n) load((tile + gridDim.x) * 16);
+        // ---- gP = G0 W_0^T -> gsh / gs2; t = 0: W_0 partial D[k][j] = sum_v P[v][k] G0[v][j]
+        {
+            f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(g0s + c * 68 + 16 * b + 4 * q);
+                MFMA4(av, w0r[b].x, w0r[b].y, w0r[b].z, w0r[b].w, d);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                gsh[(4 * q + r) * GS + 16 * w + c] = d[r];
+                gs2[(4 * q + r) * G2 + 16 * w + c] = d[r];
+            }
+            if (t0) {
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    const int r = 4 * st + q;
+                    const float av = psh[r * 68 + 16 * w + c];
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb)
+                        acc0[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, g0s[r * 68 + 16 * jb + c], acc0[jb], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < F) {                 // g b_t = sum_v w_vt gP_v
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float wv = RS ? fmaf(rm[4 * r], rm[4 * r + 2], rm[4 * r + 1]) : rm[4 * r + 2];
+                bsum = fmaf(wv, gsh[r * GS + threadIdx.x], bsum);
+            }
+        }
+        // g W_t partial D[k][j] = sum_v S_vt[k] gP_v[j] over the tile's (re-formed) S rows
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int r = 4 * st + q;
+            const float wr = rm[4 * r], ws = rm[4 * r + 1];
+            float bv[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+#pragma unroll
+            for (int a = 0; a < KB; ++a) {
+                const int k = 16 * (KB * w + a) + c;
+                const float av = RS ? fmaf(ws, xsh[r * XS + k], wr * ush[r * XS + k]) : ush[r * XS + k];
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
+            }
+        }
+        // Z_t = gP W_t (wave w -> k blocks KB w ..): relation dots (RS) or Z to HBM
+        float pu[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < KB; ++a) {
+            const int kb = KB * w + a;
+            f32x4 zc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < F / 16; ++b) {
+                const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
+                const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
+                MFMA4(av, bw.x, bw.y, bw.z, bw.w, zc);
+            }
+            // zc[r] = Z[row 4 q + r][k = 16 kb + c]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (RS) {
+                    pu[r] = fmaf(zc[r], ush[(4 * q + r) * XS + 16 * kb + c], pu[r]);
+                    ps[r] = fmaf(zc[r], xsh[(4 * q + r) * XS + 16 * kb + c], ps[r]);
+                } else {
+                    const int v = v0 + 4 * q + r;
+                    if (v < n) A.z[(int64_t(v) * T + t) * K + 16 * kb + c] = zc[r];
+                }
+            }
+        }
+        if constexpr (RS) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                pu[r] = group_sum<16>(pu[r]);
+                ps[r] = group_sum<16>(ps[r]);
+            }
+            if (c == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    dred[(w * 16 + 4 * q + r) * 2] = pu[r];
+                    dred[(w * 16 + 4 * q + r) * 2 + 1] = ps[r];
+                }
+            }
+        }
+        {                                      // beta_vt = <b_t, gP_v>
+            const float4 g4 = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
+            float bt = bc[4 * gj] * g4.x + bc[4 * gj + 1] * g4.y + bc[4 * gj + 2] * g4.z +
+                       bc[4 * gj + 3] * g4.w;
+            bt = group_sum<16>(bt);
+            if (gj == 0) {
+                if constexpr (RS) rm[4 * gr + 3] = bt;
+                else if (v0 + gr < n) A.beta[int64_t(v0 + gr) * T + t] = bt;
+            }
+        }
+        __syncthreads();
+        if constexpr (RS) {
+            if (threadIdx.x < 16) {            // row r's relation dots into its bin column
+                const int r = threadIdx.x;
+                const float du = ((dred[(0 * 16 + r) * 2] + dred[(1 * 16 + r) * 2]) +
+                                  dred[(2 * 16 + r) * 2]) + dred[(3 * 16 + r) * 2];
+                const float ds = ((dred[(0 * 16 + r) * 2 + 1] + dred[(1 * 16 + r) * 2 + 1]) +
+                                  dred[(2 * 16 + r) * 2 + 1]) + dred[(3 * 16 + r) * 2 + 1];
+                const float bt = rm[4 * r + 3];
+                if (rr[2 * r] >= 0) bins[rr[2 * r] * 16 + r] += fmaf(rm[4 * r + 2], bt, du);
+                if (rr[2 * r + 1] >= 0) bins[rr[2 * r + 1] * 16 + r] += ds + bt;
+            }
+            __syncthreads();
+        }
+    }
+    // ---- partials: g W_t as [64][K] (lins[t].weight's layout), g b_t
+    float* o = A.slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
+#pragma unroll
+    for (int a = 0; a < KB; ++a)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                o[int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q + i] = acc[a][jb][i];
+    if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
+    if constexpr (RS) {
+        if (threadIdx.x < F) {
+            float sr = 0.f;
+            if (threadIdx.x < A.n_rel)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sr += bins[threadIdx.x * 16 + r];
+            A.rslab[(int64_t(t) * gridDim.x + blockIdx.x) * F + threadIdx.x] = sr;
+        }
+    }
+    if (t0) {
+        float* o0 = A.slab0 + int64_t(blockIdx.x) * kPost0W;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o0[(16 * w + 4 * q + i) * F + 16 * jb + c] = acc0[jb][i];
+        __syncthreads();                       // Wk free: the row terms, summed over the rows
+        float* rt = Wk;                        // [3][16][64]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            rt[(0 * 16 + gr) * F + 4 * gj + i] = sga[i];
+            rt[(1 * 16 + gr) * F + 4 * gj + i] = sgy[i];
+            rt[(2 * 16 + gr) * F + 4 * gj + i] = sgyx[i];
+        }
+        __syncthreads();
+        if (threadIdx.x < 3 * F) {
+            const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s += rt[(which * 16 + r) * F + f];
+            o0[F * F + threadIdx.x] = s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// finalize: every gradient a fixed-order sum of per-block partials (re_nsm.hip's job table);
+// with the optimizer attached, element e of a job's destination (a view into the flat gradient
+// bucket) is followed by Adam on parameter (dst + e - grad_base) of the flat buffers.
+enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2 };
+
+struct Job {
+    const float* src;
+    int64_t pstride;
+    int nparts, width, op, adam;
+    float* dst;
+    const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
+};
+
+struct AdamArgs {
+    float* p; float* m; float* v; const float* gbase; int64_t n;
+    float lr, b1, b2, eps, wd, gscale;
+    int64_t* step; unsigned* ticket; int on;
+};
+
+constexpr int kMaxJobs = 32;
+
+struct FinArgs {
+    int n_jobs;
+    float alpha;
+    int start[kMaxJobs];
+    Job job[kMaxJobs];
+    AdamArgs adam;
+};
+
+__global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
+    __shared__ float red[8][33];
+    __shared__ int64_t s_t;
+    __shared__ bool last;
+    int ji = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
+    const int b = blockIdx.x - A.start[ji];
+    const Job J = A.job[ji];
+    if (A.adam.on && threadIdx.x == 0) s_t = A.adam.step[0] + 1;
+    const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    const int e = b * 32 + el;
+    float s = 0.f;
+    if (e < J.width) {
+        const float* src = J.src + e;
+        int p = grp;
+        for (; p + 56 < J.nparts; p += 64) {           // 8 partial rows in flight per thread
+            float vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + 8 * u) * J.pstride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += vv[u];
+        }
+        for (; p < J.nparts; p += 8) s += src[int64_t(p) * J.pstride];
+    }
+    red[grp][el] = s;
+    __syncthreads();
+    if (threadIdx.x < 32 && e < J.width) {
+        const float tot = ((red[0][el] + red[1][el]) + (red[2][el] + red[3][el])) +
+                          ((red[4][el] + red[5][el]) + (red[6][el] + red[7][el]));
+        float out = tot;
+        if (J.op == kOpRel) {
+            const float x = J.aux[e] * A.alpha;                // d tab / d rw (LeakyReLU)
+            out = tot * A.alpha * (x > 0.f ? 1.f : 0.01f);
+        } else if (J.op == kOpLoss) {
+            const float nv = *J.aux;
+            out = nv > 0.f ? tot / nv : 0.f;
+        }
+        J.dst[e] = out;
+        const AdamArgs& O = A.adam;
+        const int64_t i = (J.dst + e) - O.gbase;
+        // torch.optim.Adam (regnn_adam_flat's arithmetic); a gradient outside the bucket (a
+        // frozen parameter's scratch buffer) is not stepped
+        if (O.on && J.adam && i >= 0 && i < O.n) {
+            const int64_t t = s_t;
+            const double bc1 = 1.0 - pow(double(O.b1), double(t));
+            const double bc2 = 1.0 - pow(double(O.b2), double(t));
+            const float step_size = float(double(O.lr) / bc1);
+            const float bc2_sqrt = float(sqrt(bc2));
+            float gi = out * O.gscale;
+            const float pi = O.p[i], mi = O.m[i], vi = O.v[i];
+            if (O.wd != 0.f) gi = gi + O.wd * pi;
+            const float mn = mi + (1.f - O.b1) * (gi - mi);
+            const float vn = vi * O.b2 + (1.f - O.b2) * gi * gi;
+            O.m[i] = mn;
+            O.v[i] = vn;
+            O.p[i] = pi - step_size * (mn / (sqrtf(vn) / bc2_sqrt + O.eps));
+        }
+    }
+    if (A.adam.on) {
+        // every block read the step count before its ticket (the barrier above waited for the
+        // load); the last block to finish advances it
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(A.adam.ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (last && threadIdx.x == 0) {
+            A.adam.step[0] = s_t;
+            A.adam.ticket[0] = 0u;
+        }
+    }
+}
+
+struct JobList {
+    FinArgs A{};
+    int blocks = 0;
+    void add(const float* src, int64_t pstride, int nparts, int width, float* dst, int op = kOpCopy,
+             const float* aux = nullptr) {
+        A.start[A.n_jobs] = blocks;
+        Job& j = A.job[A.n_jobs++];
+        j.src = src; j.pstride = pstride; j.nparts = nparts; j.width = width; j.dst = dst;
+        j.op = op; j.aux = aux; j.adam = op != kOpLoss;
+        blocks += (width + 31) / 32;
+    }
+};
+
+struct Slab2 {
+    int64_t head, rel0, proj, post0, total;
+    int head_blocks, rel0_rows;
+};
+
+inline Slab2 slab2(const regnn_nsm_params* p, int cap0) {
+    Slab2 s{};
+    s.head_blocks = (cap0 + kRows - 1) / kRows;
+    int64_t o = 0;
+    s.head = o;
+    o += int64_t(s.head_blocks) * head_part_width(p->n_classes);
+    s.rel0 = o;                                // bwd0's (RS) or rel0's relation rows
+    s.rel0_rows = p->rel_slots ? p->n_types * kBwdBlocks : kAggBlocks;
+    o += int64_t(p->n_types * kBwdBlocks > kAggBlocks ? p->n_types * kBwdBlocks : kAggBlocks) * F;
+    s.proj = o;
+    o += int64_t(p->n_types) * kBwdBlocks * (p->k_in + 1) * F;
+    s.post0 = o;
+    o += int64_t(kBwdBlocks) * kPost0W;
+    s.total = o;
+    return s;
+}
+
+}  // namespace nsm2
+}  // namespace regnn
+
+using namespace regnn;
+using namespace regnn::nsm2;
+
+// entry points used by re_nsm.hip's regnn_nsm_step / regnn_nsm_slab_floats for L = 2
+int64_t regnn_nsm2_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
+    return slab2(p, cap0).total;
+}
+
+bool regnn_nsm2_covers(const regnn_nsm_params* p) {
+    return p->n_layers == 2 && p->n_classes <= 16 * kMaxCT &&
+           head_lds(p->n_classes) <= size_t(160 * 1024 - 1024);
+}
+
+int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
+    const int T = p->n_types, K = p->k_in, C = p->n_classes;
+    const bool rs = p->rel_slots != 0;
+    if (!w->gacc || !w->p0 || !w->xs[1] || !w->a[0] || !w->stats[0]) return REGNN_EINVAL;
+    const regnn_nsm_adam* ad = w->adam;
+    if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step ||
+               !ad->ticket))
+        return REGNN_EINVAL;
+    const Slab2 S = slab2(p, w->cap[0]);
+    const Drop drop = make_drop(p->p_drop);
+    Ptrs lin_w{}, lin_b{}, xt{};
+    for (int t = 0; t < T; ++t) {
+        lin_w.p[t] = p->lin_w[t];
+        lin_b.p[t] = p->lin_b[t];
+        xt.p[t] = p->x_tab[t];
+    }
+    // 1. layer 0
+    {
+        const int h = 1;
+        Agg0Args A{};
+        A.sizes = w->sizes; A.hop = h;
+        A.ptr = w->blk_ptr[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.edge_type = w->edge_type; A.edge_off = w->edge_off; A.xt = xt; A.T = T;
+        A.lin_w = lin_w; A.lin_b = lin_b;
+        A.rw = p->conv_rw[0]; A.n_rel = p->n_rel[0]; A.alpha = p->alpha;
+        A.w0 = p->conv_w[0]; A.bias = p->conv_b[0]; A.ln_w = p->ln_w[0]; A.ln_b = p->ln_b[0];
+        A.state = w->state; A.drop = drop;
+        A.s_agg = w->s_agg; A.s_w = w->s_w;
+        A.a = w->a[0]; A.stats = w->stats[0]; A.h = w->xs[1]; A.p = w->p0;
+        A.gacc = reinterpret_cast<unsigned long long*>(w->gacc);
+        A.n_et = p->n_edge_types; A.u_self = w->u_self; A.u_rel = w->u_rel;
+        int grid = (w->cap[h] + 15) / 16;
+        if (grid > 2048) grid = 2048;
+        const size_t lds = agg0_lds(T, K);
+#define AGG0_CASE(KK, NN, RS)                                                                  \
+        if (K == KK && (NN == MT || T <= NN) && rs == RS) {                                    \
+            static size_t done = 0;                                                            \
+            if (!set_lds(reinterpret_cast<const void*>(&agg0_kernel<KK, NN, RS>), lds, &done)) \
+                return REGNN_EUNSUPPORTED;                                                     \
+            hipLaunchKernelGGL((agg0_kernel<KK, NN, RS>), dim3(grid), dim3(kBlock), lds, stream, A); \
+            REGNN_LAUNCH_CHECK();                                                              \
+        } else
+        AGG0_CASE(128, 4, true) AGG0_CASE(128, MT, true) AGG0_CASE(64, 4, true)
+        AGG0_CASE(64, MT, true) AGG0_CASE(128, 4, false) AGG0_CASE(128, MT, false)
+        AGG0_CASE(64, 4, false) AGG0_CASE(64, MT, false)
+            return REGNN_EUNSUPPORTED;
+#undef AGG0_CASE
+    }
+    // 2. layer 1 + head + loss + backward to GH, transposed aggregation into layer 0's rows
+    const int64_t hw = head_part_width(C);
+    {
+        HeadArgs H{};
+        H.sizes = w->sizes; H.n_id = w->n_id; H.labels = w->labels;
+        H.ptr = w->blk_ptr[0]; H.idx = w->blk_idx[0]; H.rel = w->blk_rel[0]; H.inv = w->blk_inv[0];
+        H.rw = p->conv_rw[1]; H.n_rel = p->n_rel[1]; H.alpha = p->alpha;
+        H.h = w->xs[1]; H.w1 = p->conv_w[1]; H.bias = p->conv_b[1];
+        H.ln_w = p->ln_w[1]; H.ln_b = p->ln_b[1]; H.state = w->state; H.drop = drop;
+        H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
+        H.gacc = reinterpret_cast<unsigned long long*>(w->gacc); H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
+        const size_t lds = head_lds(C);
+        static size_t done = 0;
+        if (!set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
+            return REGNN_EUNSUPPORTED;
+        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kBlock), lds, stream, H);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 3. layer 0's backward
+    {
+        Bwd0Args B{};
+        B.sizes = w->sizes; B.hop = 1; B.T = T;
+        B.inv = w->blk_inv[1];
+        B.gacc = reinterpret_cast<const unsigned long long*>(w->gacc); B.a = w->a[0]; B.stats = w->stats[0];
+        B.ln_w = p->ln_w[0]; B.ln_b = p->ln_b[0]; B.state = w->state; B.drop = drop;
+        B.p = w->p0; B.w0 = p->conv_w[0];
+        B.s_agg = w->s_agg; B.s_w = w->s_w; B.lin_w = lin_w; B.lin_b = lin_b;
+        B.rw = p->conv_rw[0]; B.n_rel = p->n_rel[0]; B.alpha = p->alpha; B.n_et = p->n_edge_types;
+        B.u_self = w->u_self; B.u_rel = w->u_rel; B.z = w->z; B.beta = w->beta;
+        B.slab = w->slab + S.proj; B.rslab = w->slab + S.rel0; B.slab0 = w->slab + S.post0;
+        const dim3 grid(kBwdBlocks, T);
+#define BWD0_CASE(KK, RS)                                                                      \
+        if (K == KK && rs == RS) {                                                             \
+            static size_t done = 0;                                                            \
+            const size_t lds = bwd0_lds_floats<KK, RS>(p->n_rel[0]) * sizeof(float);           \
+            if (!set_lds(reinterpret_cast<const void*>(&bwd0_kernel<KK, RS>), lds, &done))     \
+                return REGNN_EUNSUPPORTED;                                                     \
+            hipLaunchKernelGGL((bwd0_kernel<KK, RS>), grid, dim3(kBlock), lds, stream, B);     \
+            REGNN_LAUNCH_CHECK();                                                              \
+        } else
+        BWD0_CASE(128, true) BWD0_CASE(64, true) BWD0_CASE(128, false) BWD0_CASE(64, false)
+            return REGNN_EUNSUPPORTED;
+#undef BWD0_CASE
+    }
+    // 4. no relation slots: layer 0's relation dots edge by edge (re_nsm.hip's rel0)
+    if (!rs) {
+        const int rc = regnn_nsm_rel0(p, w, w->slab + S.rel0, stream);
+        if (rc != REGNN_OK) return rc;
+    }
+    // 5. fixed-order reductions (+ Adam)
+    {
+        JobList J;
+        J.A.alpha = p->alpha;
+        const float* hp = w->slab + S.head;
+        const int nh = S.head_blocks;
+        const int64_t o_cb = int64_t(C) * (F + 1), o_w1 = o_cb + 3 * F + 1;
+        J.add(hp, hw, nh, C * F, p->g_out_w);
+        J.add(hp + int64_t(C) * F, hw, nh, C, p->g_out_b);
+        J.add(hp + o_cb, hw, nh, F, p->g_conv_b[1]);
+        J.add(hp + o_cb + F, hw, nh, F, p->g_ln_b[1]);
+        J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
+        J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
+        J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
+        J.add(hp + o_w1 + F * F, hw, nh, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
+        J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
+        const int64_t pw = int64_t(K + 1) * F;
+        for (int t = 0; t < T; ++t) {
+            const float* src = w->slab + S.proj + int64_t(t) * kBwdBlocks * pw;
+            J.add(src, pw, kBwdBlocks, K * F, p->g_lin_w[t]);
+            J.add(src + int64_t(K) * F, pw, kBwdBlocks, F, p->g_lin_b[t]);
+        }
+        const float* p0 = w->slab + S.post0;
+        J.add(p0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
+        J.add(p0 + F * F, kPost0W, kBwdBlocks, F, p->g_conv_b[0]);
+        J.add(p0 + F * F + F, kPost0W, kBwdBlocks, F, p->g_ln_b[0]);
+        J.add(p0 + F * F + 2 * F, kPost0W, kBwdBlocks, F, p->g_ln_w[0]);
+        if (ad) {
+            AdamArgs& O = J.A.adam;
+            O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;
+            O.n = ad->n;
+            O.lr = ad->lr; O.b1 = ad->beta1; O.b2 = ad->beta2; O.eps = ad->eps;
+            O.wd = ad->weight_decay; O.gscale = ad->grad_scale; O.step = ad->step;
+            O.ticket = ad->ticket; O.on = 1;
+        }
+        hipLaunchKernelGGL(finalize_kernel, dim3(J.blocks), dim3(kBlock), 0, stream, J.A);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}

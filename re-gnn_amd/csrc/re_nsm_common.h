@@ -101,3 +101,11 @@ inline bool set_lds(const void* k, size_t bytes, size_t* done) {
 
 }  // namespace nsm
 }  // namespace regnn
+
+// the two-layer step (re_nsm2.hip), dispatched by regnn_nsm_step / regnn_nsm_slab_floats
+bool regnn_nsm2_covers(const regnn_nsm_params* p);
+int64_t regnn_nsm2_slab_floats(const regnn_nsm_params* p, int32_t cap0);
+int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
+// re_nsm.hip's edge pass of layer 0's relation-table dots (rel0), into `slab` (kAggBlocks rows)
+int regnn_nsm_rel0(const regnn_nsm_params* p, const regnn_nsm_work* w, float* slab,
+                   hipStream_t stream);

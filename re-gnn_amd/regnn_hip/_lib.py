@@ -107,7 +107,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 29
+ABI_VERSION = 30
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

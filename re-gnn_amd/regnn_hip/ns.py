@@ -236,7 +236,20 @@ class _NsmWork(ctypes.Structure):
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
-                ("u_self", _P), ("u_rel", _P)]
+                ("u_self", _P), ("u_rel", _P), ("gacc", _P), ("p0", _P), ("adam", _P)]
+
+
+class _NsmAdam(ctypes.Structure):
+    """regnn_nsm_adam (include/regnn_hip.h)."""
+    _fields_ = [("param", _P), ("exp_avg", _P), ("exp_avg_sq", _P), ("grad_base", _P),
+                ("n", ctypes.c_int64), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("grad_scale", ctypes.c_float),
+                ("step", _P), ("ticket", _P)]
+
+
+# regnn_nsm_step's two-layer form (re_nsm2.hip): L = 2 and at most 432 classes (its head's LDS)
+TWO_LAYER_MAX_CLASSES = 432
 
 
 def fused_unsupported(model, x_dict):
@@ -275,6 +288,9 @@ def fused_unsupported(model, x_dict):
 # "auto": layer 0's relation-slot mode wherever the graph allows it; "off": the edge pass
 # (rel0) always (tests compare the two)
 REL_SLOTS = {"mode": "auto"}
+# "on": a one-rank FlatAdam trainer runs Adam inside the two-layer step's last launch; "off":
+# the separate regnn_adam_flat launch (tests compare the two)
+FUSED_ADAM = {"mode": "on"}
 # "on": the fused step's last sampler hop runs meta-only (no dedup / n_id append); "off": the
 # full hop (tests that inspect the outermost n_id / local ids)
 LEAN_LAST_HOP = {"mode": "on"}
@@ -387,6 +403,12 @@ class FusedStep:
         W.s_agg, W.z = ptr(z(n0, T, K)), ptr(z(n0, T, K))
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
         W.nvalid = ptr(z(1))
+        # the two-layer step: layer 0 rows' fixed-point gradient sums and group_input's projection
+        self.two_layer = nl == 2 and C <= TWO_LAYER_MAX_CLASSES
+        if self.two_layer:
+            W.gacc = ptr(torch.zeros(caps[1] * 64, dtype=torch.int64, device=dev))
+            W.p0 = ptr(z(caps[1], 64))
+        self.adam = None
         P.n_edge_types = int(sampler.num_edge_types)
         P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))
         if P.rel_slots:
@@ -395,8 +417,26 @@ class FusedStep:
         W.slab = ptr(z(_slab_floats(P, caps[0])))
         self.model, self.sampler, self.n_layers = model, sampler, nl
 
+    def attach_adam(self, opt, grad_flat):
+        """the optimizer step joins the last launch (two-layer step): Adam on each parameter
+        element right after its gradient's reduction. opt: FlatAdam over the flat parameter
+        bucket whose gradient bucket is grad_flat (every parameter's .grad a view into it)."""
+        if not self.two_layer:
+            raise ValueError("the fused optimizer needs the two-layer step")
+        A = self.adam = _NsmAdam()
+        A.param, A.exp_avg, A.exp_avg_sq = opt.p.data_ptr(), opt.m.data_ptr(), opt.v.data_ptr()
+        A.grad_base, A.n = grad_flat.data_ptr(), grad_flat.numel()
+        A.lr, A.beta1, A.beta2, A.eps = opt.lr, float(opt.betas[0]), float(opt.betas[1]), opt.eps
+        A.weight_decay, A.grad_scale = opt.weight_decay, opt.grad_scale
+        A.step, A.ticket = opt.step_count.data_ptr(), opt.ticket.data_ptr()
+        self.keep.extend([opt.p, opt.m, opt.v, grad_flat, opt.step_count, opt.ticket])
+        self.W.adam = ctypes.addressof(A)
+
     def kernels(self):
         """the kernels one regnn_nsm_step launches, in order (bench.py's roofline label)."""
+        if self.two_layer:
+            ks = ["agg0", "head", "bwd0"] + ([] if self.P.rel_slots else ["rel0"])
+            return ks + ["finalize+adam" if self.adam is not None else "finalize"]
         ks = ["prep", "agg0"] + ["agg"] * (self.n_layers - 2) + ["head"]
         ks += ["agg_bwd", "post_bwd"] * (self.n_layers - 1)
         ks += ["bwd0_rs" if self.P.rel_slots else "bwd0"]
@@ -521,6 +561,13 @@ class NSTrainer:
             self.fused_slots = [self.fused, FusedStep(model, s1, x_dict, node_type,
                                                       local_node_idx, self.y_flat, self.loss)]
             self._side = torch.cuda.Stream(device=dev)
+        # one rank, FlatAdam, two-layer step: the optimizer runs inside the step's last launch
+        # (no all-reduce sits between the backward and the update)
+        self.adam_fused = (self.fused is not None and self.fused.two_layer and self.world == 1
+                           and isinstance(self.opt, FlatAdam) and FUSED_ADAM["mode"] != "off")
+        if self.adam_fused:
+            for fs in (self.fused_slots if self.pipelined else [self.fused]):
+                fs.attach_adam(self.opt, self.flat)
         self.graphs = None
         self.epoch = -1
         self.set_epoch(0)
@@ -622,11 +669,15 @@ class NSTrainer:
             if not isinstance(self.opt, FlatAdam):       # FlatAdam takes the mean itself
                 self.flat.div_(self.world)
 
+    def _opt_step(self):
+        if not self.adam_fused:                 # else: inside the step's last launch
+            self.opt.step()
+
     def step(self):
         """one eager step (host-launched; no host synchronisation)."""
         self._forward_backward()
         self._exchange()
-        self.opt.step()
+        self._opt_step()
 
     def _train_state(self):
         """parameters and optimizer state, for capture() to undo its warm-up steps."""
@@ -700,7 +751,7 @@ class NSTrainer:
                     # ends on one queue)
                     self._pipelined_body(cur)
                     if fold_opt:
-                        self.opt.step()
+                        self._opt_step()
                 g1.append(g)
             self.graph_groups = {}
             if fold_opt:
@@ -712,14 +763,14 @@ class NSTrainer:
                     with torch.cuda.graph(g):
                         for i in range(n):
                             self._pipelined_body(i & 1)
-                            self.opt.step()
+                            self._opt_step()
                     self.graph_groups[n] = g
         else:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self._forward_backward()
                 if fold_opt:
-                    self.opt.step()
+                    self._opt_step()
         g2 = None
         if not fold_opt:
             g2 = torch.cuda.CUDAGraph()

@@ -20,16 +20,16 @@ def load(d):
 
 
 def model_kernel(name):
-    return "regnn::nsm::" in name and "adam_flat" not in name
+    return "regnn::nsm" in name and "adam_flat" not in name      # nsm:: and nsm2:: kernels
 
 
 def per_step(disp):
     tot, per_k = 0.0, defaultdict(float)
-    steps = sum(1 for _, n, _ in disp if "nsm::agg0" in n)
+    steps = sum(1 for _, n, _ in disp if "regnn::nsm" in n and "agg0_kernel" in n)
     for _, n, v in disp:
         if model_kernel(n):
             tot += v
-            short = n.split("(")[0].replace("void ", "").replace("regnn::nsm::", "")
+            short = n.split("(")[0].replace("void ", "").replace("regnn::", "")
             per_k[short] += v
     return tot, per_k, steps
 
