@@ -544,8 +544,10 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
  *  Block output (mag/regnn_layers.py:90-99 with self_loop_type 2): blk_ptr [cap_dst+1],
  *  blk_idx [cap_e] (local source ids; row i's self loop last), blk_rel [cap_e] uint8 (edge type
  *  etype[csr position], or num_edge_types + ntype[target] for the loop), blk_pos [cap_e] (CSR
- *  position of the sampled edge in the global graph, -1 for the loop), inv [cap_dst] =
- *  1 / (sampled + 1) (torch_scatter 'mean', mag/regnn_layers.py:37). Rows >= sizes[hop] empty.
+ *  position of the sampled edge in the global graph, -1 for the loop), blk_row [cap_e] (the
+ *  target row of each edge: the transposed pass of the fused step walks edges, not rows),
+ *  inv [cap_dst] = 1 / (sampled + 1) (torch_scatter 'mean', mag/regnn_layers.py:37). Rows >=
+ *  sizes[hop] empty.
  * --------------------------------------------------------------------------------------- */
 
 /* Step prologue: rank r of `world` takes global batch g = (r + state[2] * world) mod nb of the
@@ -575,9 +577,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
-                 float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
-                 int32_t meta_only,
-                 hipStream_t stream);
+                 int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
+                 int64_t* edge_off, int32_t meta_only, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -610,7 +611,7 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  * (state[3] << 8) ^ (layer + 0x51ED27))) (seed, epoch, global batch), row = target row of the
  * layer's block, 4 features per 16-byte vector.
  *
- * L = 2 (the reference's default num_layers; C <= 432): 4 launches (5 without rel_slots), the
+ * L = 2 (the reference's default num_layers; C <= 432): 5 launches (6 without rel_slots), the
  * group_input Linear and each conv's x @ W applied after their layer's aggregation (linearity:
  * mean_e(ew x_e) W = mean_e(ew x_e W)), the transposed aggregation of layer 1 as 2^-40
  * fixed-point integer sums, every other reduction fixed-order: the step is bitwise
@@ -694,6 +695,8 @@ typedef struct regnn_nsm_work {
                                  transposed aggregation's integer sums: order-independent) */
     float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
     const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
+    float* gh1;               /* cap[0] * 64: G W_1^T of layer 1's target rows (its transposed pass) */
+    const int32_t* blk_row0;  /* hop 0's block: each edge's target row (regnn_ns_hop blk_row) */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*
@@ -718,7 +721,7 @@ int64_t regnn_nsm_slab_floats(const regnn_nsm_params* p, int32_t cap0);
 
 /* One forward + loss + backward of the model over the current batch (after regnn_ns_batch and
  * the L regnn_ns_hop calls of the step): writes every g_* buffer (overwritten, not accumulated)
- * and *loss (and, with w->adam, updates the parameters). 4 kernel launches for L = 2 with
+ * and *loss (and, with w->adam, updates the parameters). 5 kernel launches for L = 2 with
  * rel_slots (L in [2, 4]), none of them sized from the host. */
 int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream);
 

@@ -181,7 +181,8 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                const int32_t* __restrict__ ntype, int num_edge_types, int32_t* __restrict__ sizes,
                int hop, int cap, int64_t* __restrict__ state, int32_t* __restrict__ blk_ptr,
                int32_t* __restrict__ blk_idx, uint8_t* __restrict__ blk_rel,
-               int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc, float* __restrict__ inv,
+               int32_t* __restrict__ blk_pos, int32_t* __restrict__ blk_row,
+               int32_t* __restrict__ gsrc, float* __restrict__ inv,
                uint64_t* __restrict__ status, const int64_t* __restrict__ local,
                int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean) {
     __shared__ int lds[kBlock / 64 + 1];
@@ -241,6 +242,7 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                 blk_idx[lp] = i;
                 blk_rel[lp] = uint8_t(rels[j] + num_edge_types);
                 blk_pos[lp] = -1;
+                blk_row[lp] = i;
                 gsrc[lp] = -1;
                 inv[i] = 1.f / float(vals[j]);
                 if (e_type) {
@@ -273,7 +275,8 @@ ns_place_kernel(const int32_t* __restrict__ samp, const int32_t* __restrict__ sp
                 int cap, int k, const int64_t* __restrict__ state, const uint8_t* __restrict__ etype,
                 const uint64_t* __restrict__ g2l, uint64_t* __restrict__ first,
                 const int32_t* __restrict__ blk_ptr, uint8_t* __restrict__ blk_rel,
-                int32_t* __restrict__ blk_pos, int32_t* __restrict__ gsrc,
+                int32_t* __restrict__ blk_pos, int32_t* __restrict__ blk_row,
+                int32_t* __restrict__ gsrc,
                 const int32_t* __restrict__ ntype, const int64_t* __restrict__ local,
                 int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean) {
     const int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -285,6 +288,7 @@ ns_place_kernel(const int32_t* __restrict__ samp, const int32_t* __restrict__ sp
     gsrc[bp] = u;
     blk_rel[bp] = etype[p];
     blk_pos[bp] = p;
+    blk_row[bp] = i;
     if (lean) {                        // meta-only hop: the source's type and table row, no dedup
         e_type[bp] = ntype[u];
         e_off[bp] = local[u];
@@ -468,11 +472,11 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  uint64_t* g2l, uint64_t* first, int32_t* samp, int32_t* spos, int32_t* scnt,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
-                 float* inv, const int64_t* local, int32_t* edge_type, int64_t* edge_off,
-                 int32_t meta_only, hipStream_t stream) {
+                 int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
+                 int64_t* edge_off, int32_t meta_only, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
-        !blk_rel || !blk_pos || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
+        !blk_rel || !blk_pos || !blk_row || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
         return REGNN_EINVAL;
     if (!!local != !!edge_type || !!local != !!edge_off || (meta_only && !local))
         return REGNN_EINVAL;
@@ -486,13 +490,13 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_rows_kernel, dim3((cap_dst + kNsRowsTile - 1) / kNsRowsTile),
                        dim3(kBlock), 0, stream, scnt, n_id, ntype, num_edge_types, sizes, hop,
-                       cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, gsrc, inv, status, local,
+                       cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, blk_row, gsrc, inv, status, local,
                        edge_type, edge_off, lean);
     REGNN_LAUNCH_CHECK();
     const int64_t slots = int64_t(cap_dst) * k;
     hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, stream, samp, spos, scnt, sizes, hop, cap_dst, k, state,
-                       etype, g2l, first, blk_ptr, blk_rel, blk_pos, gsrc, ntype, local, edge_type,
+                       etype, g2l, first, blk_ptr, blk_rel, blk_pos, blk_row, gsrc, ntype, local, edge_type,
                        edge_off, lean);
     REGNN_LAUNCH_CHECK();
     if (lean) return REGNN_OK;         // no dedup, no n_id append, no local source ids

@@ -1,6 +1,6 @@
 // Two-layer fused NS model step (regnn_nsm_step with L = 2, the reference's num_layers default):
 // the REGNN of mag/regnn_ns.py:216-346 ('regcn', self_loop_type 2, LayerNorm, hidden 64) forward
-// + nll_loss + backward over the blocks regnn_ns_hop wrote, in four launches (five without
+// + nll_loss + backward over the blocks regnn_ns_hop wrote, in five launches (six without
 // relation slots), every reduction in a fixed order or exact: two runs of a step give bitwise
 // equal gradients. Optionally the Adam update of every parameter ends the last launch.
 //
@@ -12,10 +12,10 @@
 //             for the backward; zeroes the rows' fixed-point gradient accumulators.
 //   head      layer 1 aggregated first and projected second (a = inv (sum_e tab[r_e] h0[u_e]) W_1
 //             + bias, the same linearity), LayerNorm, relu, dropout, out_lin, log_softmax,
-//             nll_loss (mean over the labelled targets) and the backward to GH = inv ga W_1^T,
-//             then layer 1's transposed aggregation gh0[u_e] += tab[r_e] GH[v] over the block's
-//             edges as 64-bit fixed-point integer atomics (integer sums: exact in any order) and
-//             the relation-table dots <h0[u_e], GH[v]>.
+//             nll_loss (mean over the labelled targets) and the backward to GH = inv ga W_1^T.
+//   scatter   layer 1's transposed aggregation, one 16-lane group per edge over every CU:
+//             gh0[u_e] += tab[r_e] GH[v_e] as 64-bit fixed-point integer atomics (integer sums:
+//             exact in any order) and the relation-table dots <h0[u_e], GH[v_e]>.
 //   bwd0      layer 0's backward per target row: the LayerNorm / relu / dropout backward from
 //             gh0, gP = inv ga W_0^T, the W_0 gradient P^T (inv ga); per source type t the
 //             weight gradient gP^T S_t, the bias term, and the relation-table dots from
@@ -53,6 +53,19 @@ __device__ __forceinline__ float rel_tab(const float* rw, int nr, float alpha, i
     return x > 0.f ? x : 0.01f * x;
 }
 
+// phase timestamps of an instrumented build (-DREGNN_NSM2_PHASES, tools/nsm2_phases.py only):
+// thread 0 of blocks < 32 records wall_clock64() at marked points of each kernel
+#ifdef REGNN_NSM2_PHASES
+__device__ unsigned long long g_nsm2_phase[4][32][16];
+#define PH(kern, k)                                                                            \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < 32 && blockIdx.y == 0)                             \
+            g_nsm2_phase[kern][blockIdx.x][k] = wall_clock64();                                \
+    } while (0)
+#else
+#define PH(kern, k) do {} while (0)
+#endif
+
 #define MFMA4(av, b0, b1, b2, b3, d)                                 \
     d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).x, (b0), d, 0, 0, 0); \
     d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).y, (b1), d, 0, 0, 0); \
@@ -77,13 +90,14 @@ struct Agg0Args {
     int n_et; float* u_self; int32_t* u_rel;
 };
 
-// LDS: S tile [16][T K + 4] | s_w [16][MT] | P [16][68] | pre-LN rows [16][64] | table [64]
+// LDS: S tile [16][T K + 4] | s_w [16][MT] | P [16][68] | pre-LN rows [16][64] | table [64] |
+// W_0 [64][64]
 inline size_t agg0_lds(int T, int K) {
-    return (size_t(16) * (T * K + 4) + 16 * MT + 16 * 68 + 16 * F + F) * sizeof(float);
+    return (size_t(16) * (T * K + 4) + 16 * MT + 16 * 68 + 16 * F + F + F * F) * sizeof(float);
 }
 
 template <int K, int NT, bool RS>
-__global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
+__global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
     constexpr int VPL = K / 64;            // float4 per lane of a K-wide row (16 lanes per row)
     constexpr int KB = K / 16;
     constexpr int HB = KB / 2;             // float4 steps per half type
@@ -95,19 +109,18 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
     float* Pt = sw + 16 * MT;              // [16][68]
     float* at = Pt + 16 * 68;              // [16][F]
     float* tab = at + 16 * F;              // [F]
+    float* w0s = tab + F;                  // [F][F]: W_0 (the second stage's B operand)
     if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    for (int i = threadIdx.x; i < F * F / 4; i += kBlock)
+        reinterpret_cast<float4*>(w0s)[i] = reinterpret_cast<const float4*>(A.w0)[i];
     const int n = A.sizes[A.hop];
     const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
     const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
     const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
-    float w0c[16];                         // W_0[16 b + 4 q + i][16 w + c]: the second stage's B
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w0c[4 * b + i] = A.w0[(16 * b + 4 * q + i) * F + 16 * w + c];
     const float bj = A.bias[16 * w + c];
+    PH(0, 0);
     __syncthreads();
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
         // ---- gather: per-type register sums of this lane's 4 * VPL features
@@ -203,6 +216,7 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
 #pragma unroll
             for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
         };
+        PH(0, 1);
         bload(0, bcur);
         const int tau = r_self - A.n_et;           // RS: the row's node type
 #pragma unroll
@@ -242,6 +256,7 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
             }
         }
         __syncthreads();
+        PH(0, 2);
         // ---- stage 1: P[v][j] = sum_t S_vt W_t[j][:] + w_vt b_t[j]; type t + 1's rows of W_t
         // are loaded while type t's products run
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
@@ -267,13 +282,15 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
             }
         }
         __syncthreads();
+        PH(0, 3);
         // ---- stage 2: a = inv (P W_0) + bias
         {
             f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const float4 av = *reinterpret_cast<const float4*>(Pt + c * 68 + 16 * b + 4 * q);
-                MFMA4(av, w0c[4 * b], w0c[4 * b + 1], w0c[4 * b + 2], w0c[4 * b + 3], d2);
+                const float* wb = w0s + (16 * b + 4 * q) * F + 16 * w + c;     // W_0[k][16 w + c]
+                MFMA4(av, wb[0], wb[F], wb[2 * F], wb[3 * F], d2);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -307,6 +324,7 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
             gz[1] = make_ulonglong2(0ull, 0ull);
         }
         __syncthreads();                       // the tiles are reused by the next rows
+        PH(0, 4);
     }
 }
 
@@ -318,12 +336,10 @@ __global__ void __launch_bounds__(kBlock) agg0_kernel(Agg0Args A) {
 //   4. z = h W_out^T + b_out (class tiles over the waves), log_softmax, nll, g = (softmax -
 //      onehot) / n_valid, gh = g W_out, LayerNorm / relu / dropout backward -> ga, G = inv ga;
 //   5. partials: out_lin weight g^T h, its bias, conv bias / LN terms, the loss;
-//   6. GH = G W_1^T and the W_1 partial Hagg^T G (MFMA);
-//   7. the block's edges again: gh0[u_e] += tab[r_e] GH[v] (fixed-point atomics), relation
-//      dots <h0[u_e], GH[v]> per row, summed over the rows in order.
+//   6. GH = G W_1^T -> HBM (the scatter's rows) and the W_1 partial Hagg^T G (MFMA).
 // out_lin.weight staged by LDS-DMA into an XOR-swizzled image (head_sw), as re_nsm.hip's head.
 // Slab row per block: [C*64 g out_w | C g out_b | 64 conv bias | 64 LN beta | 64 LN gamma |
-//                      1 loss | 64*64 g W_1 | 64 relation dots]
+//                      1 loss | 64*64 g W_1]
 struct HeadArgs {
     const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
     const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
@@ -331,11 +347,11 @@ struct HeadArgs {
     const float* h; const float* w1; const float* bias; const float* ln_w; const float* ln_b;
     const int64_t* state; Drop drop;
     const float* w_out; const float* b_out; int C;
-    unsigned long long* gacc; float* nvalid; float* part; int64_t part_w;
+    float* gh; float* nvalid; float* part; int64_t part_w;
 };
 
 inline int64_t head_part_width(int C) {
-    return (int64_t(C) * (F + 1) + 3 * F + 1 + F * F + F + 3) & ~3ll;
+    return (int64_t(C) * (F + 1) + 3 * F + 1 + F * F + 3) & ~3ll;
 }
 __host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }
 __host__ __device__ inline int head_wl(int C) {
@@ -352,15 +368,13 @@ __device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c &
 __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     extern __shared__ float hl[];
     const int C = A.C, CT = (C + 15) / 16, CP = head_cp(C);
-    float* Wl = hl;                        // W_out image; after step 4: red [3][16][64], GH [16][68]
-    float* zs = Wl + head_wl(C);           // [16][CP]: z, then g; after step 5: relation dots
+    float* Wl = hl;                        // W_out image; after step 4: red [3][16][64]
+    float* zs = Wl + head_wl(C);           // [16][CP]: z, then g
     float* hs = zs + 16 * CP;              // [16][68]: h (row reads), then G
     float* hs2 = hs + 16 * 68;             // [16][80]: h (column reads)
     float* ghs = hs2 + 16 * 80;            // [16][68]: a, then gh
     float* hg = ghs + 16 * 68;             // [16][68]: Hagg
     float* red = Wl;
-    float* gH = Wl + 3 * 16 * F;
-    float* bins = zs;                      // [16][64]
     __shared__ float tab[F];
     __shared__ float lrow[kRows];
     __shared__ int wcnt[kBlock / 64];
@@ -395,7 +409,9 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
         if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = cnt_valid;
     }
     if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    PH(1, 0);
     __syncthreads();
+    PH(1, 1);
     // ---- 1. Hagg
     {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -428,6 +444,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
         *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
     }
     __syncthreads();
+    PH(1, 2);
     // ---- 2. a = inv (Hagg W_1) + bias -> ghs
     {
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
@@ -471,6 +488,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     __syncthreads();
+    PH(1, 3);
     const int n_valid = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
     if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     // ---- 4a. z = h W^T + b -> zs (classes >= C: -inf)
@@ -540,6 +558,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
         for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
     }
     __syncthreads();
+    PH(1, 4);
     // ---- 4d. LayerNorm / relu / dropout backward -> ga; G = inv ga -> hs; row terms -> red
     float4 w1r[4];                         // W_1[16 w + cc][16 b + 4 q ..]: step 6's B operand
 #pragma unroll
@@ -572,7 +591,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     __syncthreads();
     float* o = A.part + int64_t(blockIdx.x) * A.part_w;
     const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
-    const int64_t o_w1 = o_loss + 1, o_r1 = o_w1 + F * F;
+    const int64_t o_w1 = o_loss + 1;
     // ---- 5. out_lin weight partial D[c][k] = sum_v g[v][c] h[v][k], its bias, row terms
     for (int ct = w; ct < CT; ct += kBlock / 64) {
         f32x4 dw[4];
@@ -613,8 +632,8 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
         for (int r = 0; r < kRows; ++r) acc += lrow[r];
         o[o_loss] = acc;
     }
-    __syncthreads();                       // zs / red free: relation dots and GH go there
-    // ---- 6. GH = G W_1^T -> gH; W_1 partial D[k][j] = sum_v Hagg[v][k] G[v][j]
+    PH(1, 5);
+    // ---- 6. GH = G W_1^T -> HBM; W_1 partial D[k][j] = sum_v Hagg[v][k] G[v][j]
     {
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -623,7 +642,10 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             MFMA4(av, w1r[b].x, w1r[b].y, w1r[b].z, w1r[b].w, d);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gH[(4 * q + r) * 68 + 16 * w + cc] = d[r];
+        for (int r = 0; r < 4; ++r) {
+            const int vv = blockIdx.x * kRows + 4 * q + r;
+            if (vv < n) A.gh[int64_t(vv) * F + 16 * w + cc] = d[r];
+        }
         f32x4 dw[4];
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) dw[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -640,49 +662,72 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[o_w1 + (16 * w + 4 * q + i) * F + 16 * jb + cc] = dw[jb][i];
     }
-    for (int i = threadIdx.x; i < 16 * F; i += kBlock) bins[i] = 0.f;
+    PH(1, 7);
+}
+
+// ---------------------------------------------------------------------------------------------
+// scatter: layer 1's transposed aggregation over hop 0's block, a 16-lane group per edge e
+// (grid-stride over every CU): gh0[u_e] += tab[r_e] GH[v_e] (4 features per lane, 2^-40 fixed
+// point, integer atomics: the sums are exact in any order) and the relation-table dot
+// <h0[u_e], GH[v_e]> into the group's bin (its own edges in order), then the block's groups
+// summed in order -> one slab row of relation dots per block.
+struct ScatArgs {
+    const int32_t* sizes; const int32_t* idx; const uint8_t* rel; const int32_t* row;
+    const float* gh; const float* h; const float* rw; int n_rel; float alpha;
+    unsigned long long* gacc; float* slab;
+};
+
+constexpr int kScatBlocks = 512;
+
+__global__ void __launch_bounds__(kBlock) scatter_kernel(ScatArgs A) {
+    __shared__ float bins[16][F];
+    __shared__ float tab[F];
+    for (int i = threadIdx.x; i < 16 * F; i += kBlock) (&bins[0][0])[i] = 0.f;
+    if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
     __syncthreads();
-    // ---- 7. transposed aggregation into layer 0's rows + relation dots
-    if (act) {
-        const float4 g4 = *reinterpret_cast<const float4*>(gH + sub * 68 + 4 * l);
-        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
-        for (int c0 = e0; c0 < e1; c0 += 16) {
-            const int m = min(16, e1 - c0);
-            const int my_u = l < m ? A.idx[c0 + l] : 0;
-            const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
-            constexpr int UN = 8;
-            for (int j = 0; j < m; j += UN) {
-                float4 x[UN];
-                int uu[UN], rr[UN];
-#pragma unroll
-                for (int u = 0; u < UN; ++u) {
-                    const int jj = min(j + u, m - 1);
-                    uu[u] = __shfl(my_u, gl + jj, 64);
-                    rr[u] = __shfl(my_r, gl + jj, 64);
-                    x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu[u]) * F + 4 * l);
-                }
-#pragma unroll
-                for (int u = 0; u < UN; ++u) {
-                    if (j + u >= m) break;     // uniform over the row's 16 lanes
-                    const float dot = group_sum<16>(x[u].x * g4.x + x[u].y * g4.y +
-                                                    x[u].z * g4.z + x[u].w * g4.w);
-                    if (l == 0) bins[sub * F + rr[u]] += dot;
-                    const float wt = tab[rr[u]];
-                    unsigned long long* dst = A.gacc + int64_t(uu[u]) * F + 4 * l;
-                    atomicAdd(dst + 0, to_fix(wt * g4.x));
-                    atomicAdd(dst + 1, to_fix(wt * g4.y));
-                    atomicAdd(dst + 2, to_fix(wt * g4.z));
-                    atomicAdd(dst + 3, to_fix(wt * g4.w));
-                }
-            }
+    const int E = A.sizes[8];
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int stride = gridDim.x * 16;
+    int e = blockIdx.x * 16 + grp;
+    for (; e + stride < E; e += 2 * stride) {            // two edges in flight per group
+        const int e2 = e + stride;
+        const int v0 = A.row[e], u0 = A.idx[e], r0 = A.rel[e];
+        const int v1 = A.row[e2], u1 = A.idx[e2], r1 = A.rel[e2];
+        const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(v0) * F + 4 * l);
+        const float4 x0 = *reinterpret_cast<const float4*>(A.h + int64_t(u0) * F + 4 * l);
+        const float4 g1 = *reinterpret_cast<const float4*>(A.gh + int64_t(v1) * F + 4 * l);
+        const float4 x1 = *reinterpret_cast<const float4*>(A.h + int64_t(u1) * F + 4 * l);
+        const float d0 = group_sum<16>(x0.x * g0.x + x0.y * g0.y + x0.z * g0.z + x0.w * g0.w);
+        const float d1 = group_sum<16>(x1.x * g1.x + x1.y * g1.y + x1.z * g1.z + x1.w * g1.w);
+        if (l == 0) {
+            bins[grp][r0] += d0;
+            bins[grp][r1] += d1;
         }
+        const float w0 = tab[r0], w1 = tab[r1];
+        unsigned long long* p0 = A.gacc + int64_t(u0) * F + 4 * l;
+        unsigned long long* p1 = A.gacc + int64_t(u1) * F + 4 * l;
+        atomicAdd(p0 + 0, to_fix(w0 * g0.x)); atomicAdd(p0 + 1, to_fix(w0 * g0.y));
+        atomicAdd(p0 + 2, to_fix(w0 * g0.z)); atomicAdd(p0 + 3, to_fix(w0 * g0.w));
+        atomicAdd(p1 + 0, to_fix(w1 * g1.x)); atomicAdd(p1 + 1, to_fix(w1 * g1.y));
+        atomicAdd(p1 + 2, to_fix(w1 * g1.z)); atomicAdd(p1 + 3, to_fix(w1 * g1.w));
+    }
+    if (e < E) {
+        const int v0 = A.row[e], u0 = A.idx[e], r0 = A.rel[e];
+        const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(v0) * F + 4 * l);
+        const float4 x0 = *reinterpret_cast<const float4*>(A.h + int64_t(u0) * F + 4 * l);
+        const float d0 = group_sum<16>(x0.x * g0.x + x0.y * g0.y + x0.z * g0.z + x0.w * g0.w);
+        if (l == 0) bins[grp][r0] += d0;
+        const float w0 = tab[r0];
+        unsigned long long* p0 = A.gacc + int64_t(u0) * F + 4 * l;
+        atomicAdd(p0 + 0, to_fix(w0 * g0.x)); atomicAdd(p0 + 1, to_fix(w0 * g0.y));
+        atomicAdd(p0 + 2, to_fix(w0 * g0.z)); atomicAdd(p0 + 3, to_fix(w0 * g0.w));
     }
     __syncthreads();
     if (threadIdx.x < F) {
-        float acc = 0.f;
+        float s = 0.f;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) acc += bins[r * F + threadIdx.x];
-        o[o_r1 + threadIdx.x] = acc;
+        for (int g = 0; g < 16; ++g) s += bins[g][threadIdx.x];
+        A.slab[int64_t(blockIdx.x) * F + threadIdx.x] = s;
     }
 }
 
@@ -810,8 +855,10 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         }
     };
     int tile = blockIdx.x;
+    PH(2, 0);
     if (tile * 16 < n) load(tile * 16);
     __syncthreads();
+    PH(2, 1);
     for (; tile * 16 < n; tile += gridDim.x) {
         const int v0 = tile * 16;
         // ---- front: LayerNorm / relu / dropout backward of row v0 + gr, features 4 gj ..
@@ -984,6 +1031,7 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
             __syncthreads();
         }
     }
+    PH(2, 2);
     // ---- partials: g W_t as [64][K] (lins[t].weight's layout), g b_t
     float* o = A.slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
 #pragma unroll
@@ -1061,15 +1109,32 @@ struct FinArgs {
 __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     __shared__ float red[8][33];
     __shared__ int64_t s_t;
+    __shared__ float s_step, s_bc2;
     __shared__ bool last;
     int ji = 0;
 #pragma unroll
     for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
     const int b = blockIdx.x - A.start[ji];
     const Job J = A.job[ji];
-    if (A.adam.on && threadIdx.x == 0) s_t = A.adam.step[0] + 1;
+    const AdamArgs& O = A.adam;
+    PH(3, 0);
     const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int e = b * 32 + el;
+    // the optimizer's operands of this thread's element, requested before the partial sums
+    const int64_t i = (J.dst + e) - O.gbase;
+    const bool stepped = O.on && J.adam && threadIdx.x < 32 && e < J.width && i >= 0 && i < O.n;
+    float pi = 0.f, mi = 0.f, vi = 0.f;
+    if (stepped) {
+        pi = O.p[i]; mi = O.m[i]; vi = O.v[i];
+    }
+    if (O.on && threadIdx.x == 64) {           // the bias corrections, once per block
+        const int64_t t = O.step[0] + 1;
+        const double bc1 = 1.0 - pow(double(O.b1), double(t));
+        const double bc2 = 1.0 - pow(double(O.b2), double(t));
+        s_t = t;
+        s_step = float(double(O.lr) / bc1);
+        s_bc2 = float(sqrt(bc2));
+    }
     float s = 0.f;
     if (e < J.width) {
         const float* src = J.src + e;
@@ -1085,6 +1150,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     }
     red[grp][el] = s;
     __syncthreads();
+    PH(3, 1);
     if (threadIdx.x < 32 && e < J.width) {
         const float tot = ((red[0][el] + red[1][el]) + (red[2][el] + red[3][el])) +
                           ((red[4][el] + red[5][el]) + (red[6][el] + red[7][el]));
@@ -1097,37 +1163,30 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
             out = nv > 0.f ? tot / nv : 0.f;
         }
         J.dst[e] = out;
-        const AdamArgs& O = A.adam;
-        const int64_t i = (J.dst + e) - O.gbase;
         // torch.optim.Adam (regnn_adam_flat's arithmetic); a gradient outside the bucket (a
         // frozen parameter's scratch buffer) is not stepped
-        if (O.on && J.adam && i >= 0 && i < O.n) {
-            const int64_t t = s_t;
-            const double bc1 = 1.0 - pow(double(O.b1), double(t));
-            const double bc2 = 1.0 - pow(double(O.b2), double(t));
-            const float step_size = float(double(O.lr) / bc1);
-            const float bc2_sqrt = float(sqrt(bc2));
+        if (stepped) {
             float gi = out * O.gscale;
-            const float pi = O.p[i], mi = O.m[i], vi = O.v[i];
             if (O.wd != 0.f) gi = gi + O.wd * pi;
             const float mn = mi + (1.f - O.b1) * (gi - mi);
             const float vn = vi * O.b2 + (1.f - O.b2) * gi * gi;
             O.m[i] = mn;
             O.v[i] = vn;
-            O.p[i] = pi - step_size * (mn / (sqrtf(vn) / bc2_sqrt + O.eps));
+            O.p[i] = pi - s_step * (mn / (sqrtf(vn) / s_bc2 + O.eps));
         }
     }
-    if (A.adam.on) {
+    if (O.on) {
         // every block read the step count before its ticket (the barrier above waited for the
         // load); the last block to finish advances it
         __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(A.adam.ticket, 1u) == gridDim.x - 1;
+        if (threadIdx.x == 0) last = atomicAdd(O.ticket, 1u) == gridDim.x - 1;
         __syncthreads();
         if (last && threadIdx.x == 0) {
-            A.adam.step[0] = s_t;
-            A.adam.ticket[0] = 0u;
+            O.step[0] = s_t;
+            O.ticket[0] = 0u;
         }
     }
+    PH(3, 2);
 }
 
 struct JobList {
@@ -1144,7 +1203,7 @@ struct JobList {
 };
 
 struct Slab2 {
-    int64_t head, rel0, proj, post0, total;
+    int64_t head, scat, rel0, proj, post0, total;
     int head_blocks, rel0_rows;
 };
 
@@ -1154,6 +1213,8 @@ inline Slab2 slab2(const regnn_nsm_params* p, int cap0) {
     int64_t o = 0;
     s.head = o;
     o += int64_t(s.head_blocks) * head_part_width(p->n_classes);
+    s.scat = o;                                // layer 1's relation dots, per scatter block
+    o += int64_t(kScatBlocks) * F;
     s.rel0 = o;                                // bwd0's (RS) or rel0's relation rows
     s.rel0_rows = p->rel_slots ? p->n_types * kBwdBlocks : kAggBlocks;
     o += int64_t(p->n_types * kBwdBlocks > kAggBlocks ? p->n_types * kBwdBlocks : kAggBlocks) * F;
@@ -1171,6 +1232,12 @@ inline Slab2 slab2(const regnn_nsm_params* p, int cap0) {
 using namespace regnn;
 using namespace regnn::nsm2;
 
+#ifdef REGNN_NSM2_PHASES
+extern "C" int regnn_nsm2_phases(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsm2_phase), sizeof(g_nsm2_phase)) == hipSuccess ? 0 : 3;
+}
+#endif
+
 // entry points used by re_nsm.hip's regnn_nsm_step / regnn_nsm_slab_floats for L = 2
 int64_t regnn_nsm2_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
     return slab2(p, cap0).total;
@@ -1184,7 +1251,8 @@ bool regnn_nsm2_covers(const regnn_nsm_params* p) {
 int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     const int T = p->n_types, K = p->k_in, C = p->n_classes;
     const bool rs = p->rel_slots != 0;
-    if (!w->gacc || !w->p0 || !w->xs[1] || !w->a[0] || !w->stats[0]) return REGNN_EINVAL;
+    if (!w->gacc || !w->p0 || !w->gh1 || !w->blk_row0 || !w->xs[1] || !w->a[0] || !w->stats[0])
+        return REGNN_EINVAL;
     const regnn_nsm_adam* ad = w->adam;
     if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step ||
                !ad->ticket))
@@ -1239,7 +1307,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         H.h = w->xs[1]; H.w1 = p->conv_w[1]; H.bias = p->conv_b[1];
         H.ln_w = p->ln_w[1]; H.ln_b = p->ln_b[1]; H.state = w->state; H.drop = drop;
         H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
-        H.gacc = reinterpret_cast<unsigned long long*>(w->gacc); H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
+        H.gh = w->gh1; H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
         const size_t lds = head_lds(C);
         static size_t done = 0;
         if (!set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
@@ -1247,7 +1315,17 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kBlock), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
-    // 3. layer 0's backward
+    // 3. layer 1's transposed aggregation into layer 0's rows
+    {
+        ScatArgs G{};
+        G.sizes = w->sizes; G.idx = w->blk_idx[0]; G.rel = w->blk_rel[0]; G.row = w->blk_row0;
+        G.gh = w->gh1; G.h = w->xs[1]; G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1];
+        G.alpha = p->alpha; G.gacc = reinterpret_cast<unsigned long long*>(w->gacc);
+        G.slab = w->slab + S.scat;
+        hipLaunchKernelGGL(scatter_kernel, dim3(kScatBlocks), dim3(kBlock), 0, stream, G);
+        REGNN_LAUNCH_CHECK();
+    }
+    // 4. layer 0's backward
     {
         Bwd0Args B{};
         B.sizes = w->sizes; B.hop = 1; B.T = T;
@@ -1273,12 +1351,12 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
             return REGNN_EUNSUPPORTED;
 #undef BWD0_CASE
     }
-    // 4. no relation slots: layer 0's relation dots edge by edge (re_nsm.hip's rel0)
+    // 5. no relation slots: layer 0's relation dots edge by edge (re_nsm.hip's rel0)
     if (!rs) {
         const int rc = regnn_nsm_rel0(p, w, w->slab + S.rel0, stream);
         if (rc != REGNN_OK) return rc;
     }
-    // 5. fixed-order reductions (+ Adam)
+    // 6. fixed-order reductions (+ Adam)
     {
         JobList J;
         J.A.alpha = p->alpha;
@@ -1292,7 +1370,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
         J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
         J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
-        J.add(hp + o_w1 + F * F, hw, nh, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
+        J.add(w->slab + S.scat, F, kScatBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
         J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
         const int64_t pw = int64_t(K + 1) * F;
         for (int t = 0; t < T; ++t) {

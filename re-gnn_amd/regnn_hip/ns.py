@@ -36,13 +36,15 @@ class NSBlock:
 
     csr_ptr [n_dst+1] int32, csr_idx [E] local source ids (row v's self loop last), rel [E]
     uint8 0-based relation (edge type; num_edge_types + node type for the loop), pos [E] CSR
-    position of the sampled edge in the global graph (-1: loop), inv [n_dst] 1/(sampled + 1).
+    position of the sampled edge in the global graph (-1: loop), row [E] each edge's target row,
+    inv [n_dst] 1/(sampled + 1).
     n_dst / n_src / E are host ints: exact sizes (API path) or capacities (device engine)."""
 
     is_ns_block = True
 
-    def __init__(self, ptr, idx, rel, pos, inv, n_dst, n_src, E, device):
+    def __init__(self, ptr, idx, rel, pos, inv, n_dst, n_src, E, device, row=None):
         self.csr_ptr, self.csr_idx, self.rel, self.pos, self.inv = ptr, idx, rel, pos, inv
+        self.row = row
         self.n_dst, self.n_src, self.E = int(n_dst), int(n_src), int(E)
         self.device = device
 
@@ -120,7 +122,8 @@ class DeviceSampler:
                                       flag=z(ce, torch.uint8), tiles=z(nt + 1),
                                       status=z((cd + 1023) // 1024, torch.int64)))
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
-                          torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev)
+                          torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev,
+                          row=z(ce))
             self.blocks.append(blk)
         self.local, self.edge_meta = None, [None] * len(self.sizes_k)
         self.meta_fresh = [False] * len(self.sizes_k)
@@ -157,7 +160,8 @@ class DeviceSampler:
                    L.ptr(self.first), L.ptr(b["samp"]), L.ptr(b["spos"]), L.ptr(b["scnt"]),
                    L.ptr(b["gsrc"]), L.ptr(b["flag"]), L.ptr(b["tiles"]), L.ptr(b["status"]),
                    L.ptr(blk.csr_ptr),
-                   L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos), L.ptr(blk.inv),
+                   L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos), L.ptr(blk.row),
+                   L.ptr(blk.inv),
                    *((L.ptr(self.local), L.ptr(self.edge_meta[h][0]), L.ptr(self.edge_meta[h][1]))
                      if self.edge_meta[h] is not None else (None, None, None)),
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
@@ -236,7 +240,8 @@ class _NsmWork(ctypes.Structure):
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
-                ("u_self", _P), ("u_rel", _P), ("gacc", _P), ("p0", _P), ("adam", _P)]
+                ("u_self", _P), ("u_rel", _P), ("gacc", _P), ("p0", _P), ("adam", _P),
+                ("gh1", _P), ("blk_row0", _P)]
 
 
 class _NsmAdam(ctypes.Structure):
@@ -408,6 +413,8 @@ class FusedStep:
         if self.two_layer:
             W.gacc = ptr(torch.zeros(caps[1] * 64, dtype=torch.int64, device=dev))
             W.p0 = ptr(z(caps[1], 64))
+            W.gh1 = ptr(z(caps[0], 64))
+            W.blk_row0 = ptr(sampler.blocks[0].row)
         self.adam = None
         P.n_edge_types = int(sampler.num_edge_types)
         P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))
@@ -435,7 +442,7 @@ class FusedStep:
     def kernels(self):
         """the kernels one regnn_nsm_step launches, in order (bench.py's roofline label)."""
         if self.two_layer:
-            ks = ["agg0", "head", "bwd0"] + ([] if self.P.rel_slots else ["rel0"])
+            ks = ["agg0", "head", "scatter", "bwd0"] + ([] if self.P.rel_slots else ["rel0"])
             return ks + ["finalize+adam" if self.adam is not None else "finalize"]
         ks = ["prep", "agg0"] + ["agg"] * (self.n_layers - 2) + ["head"]
         ks += ["agg_bwd", "post_bwd"] * (self.n_layers - 1)
