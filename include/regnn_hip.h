@@ -570,7 +570,11 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * [cap_e] int64 (what the fused step's layer 0 gathers by). meta_only (needs the three): the
  * hop whose sources only feed layer 0 by (type, row) — no first-seen de-duplication, no n_id
  * append (sizes[hop + 1] = sizes[hop]), blk_idx of the sampled edges not written; blk_ptr,
- * blk_rel, blk_pos, inv, the self loops and the edge meta as above (3 launches instead of 6). */
+ * blk_rel, blk_pos, inv, the self loops and the edge meta as above (3 launches instead of 6).
+ * Optional (all three or none, not with meta_only): the block's transposed index -- csc_cnt
+ * [cap_e] (scratch), csc_ptr [cap_e + 1] (source i's edges are csc_ent[csc_ptr[i] ..
+ * csc_ptr[i + 1]) over the n_{hop+1} sources), csc_ent [cap_e] = target row << 8 | relation;
+ * the order inside a segment is unspecified (one more launch; cap_e <= 32768). */
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
@@ -578,7 +582,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
-                 int64_t* edge_off, int32_t meta_only, hipStream_t stream);
+                 int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
+                 int32_t* csc_ent, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -690,13 +695,12 @@ typedef struct regnn_nsm_work {
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
     float* u_self;            /* rel_slots: cap[L-1] * k_in, each row's self-loop input row */
     int32_t* u_rel;           /* rel_slots: cap[L-1] * (T + 1), relation of each source-type slot */
-    /* the two-layer step (L = 2, C <= 432): */
-    uint64_t* gacc;           /* cap[1] * 64: layer 0 rows' gradient as 2^-40 fixed point (the
-                                 transposed aggregation's integer sums: order-independent) */
+    /* the two-layer step (L = 2, C <= 432, hop 0's edge capacity <= 32768): */
     float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
     const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
     float* gh1;               /* cap[0] * 64: G W_1^T of layer 1's target rows (its transposed pass) */
-    const int32_t* blk_row0;  /* hop 0's block: each edge's target row (regnn_ns_hop blk_row) */
+    const int32_t* csc_ptr0;  /* hop 0's transposed index (regnn_ns_hop csc_ptr / csc_ent) */
+    const int32_t* csc_ent0;
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

@@ -184,9 +184,13 @@ ns_rows_kernel(const int32_t* __restrict__ scnt, const int32_t* __restrict__ n_i
                int32_t* __restrict__ blk_pos, int32_t* __restrict__ blk_row,
                int32_t* __restrict__ gsrc, float* __restrict__ inv,
                uint64_t* __restrict__ status, const int64_t* __restrict__ local,
-               int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean) {
+               int32_t* __restrict__ e_type, int64_t* __restrict__ e_off, int lean,
+               int32_t* __restrict__ csc_cnt, int cap_e) {
     __shared__ int lds[kBlock / 64 + 1];
     __shared__ int s_prefix;
+    if (csc_cnt)                       // the transposed index's per-source counters (resolve adds)
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < cap_e; i += gridDim.x * kBlock)
+            csc_cnt[i] = 0;
     const int n = sizes[hop];
     const uint32_t stamp = ns_stamp(state, hop);
     const int tile = blockIdx.x;
@@ -387,15 +391,69 @@ __global__ void __launch_bounds__(kBlock)
 ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes, int hop,
                   const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx, int cap_e,
                   const int32_t* __restrict__ ntype, const int64_t* __restrict__ local,
-                  int32_t* __restrict__ e_type, int64_t* __restrict__ e_off) {
+                  int32_t* __restrict__ e_type, int64_t* __restrict__ e_off,
+                  int32_t* __restrict__ csc_cnt) {
     const int bp = blockIdx.x * kBlock + threadIdx.x;
     if (bp >= cap_e || bp >= sizes[8 + hop]) return;
     const int u = gsrc[bp];
-    if (u < 0) return;
-    blk_idx[bp] = int32_t(uint32_t(g2l[u]));
-    if (e_type) {
-        e_type[bp] = ntype[u];
-        e_off[bp] = local[u];
+    int lid;
+    if (u < 0) {                       // the self loop (written by ns_rows_kernel)
+        lid = blk_idx[bp];
+    } else {
+        lid = int32_t(uint32_t(g2l[u]));
+        blk_idx[bp] = lid;
+        if (e_type) {
+            e_type[bp] = ntype[u];
+            e_off[bp] = local[u];
+        }
+    }
+    if (csc_cnt) atomicAdd(csc_cnt + lid, 1);        // integer: exact in any order
+}
+
+// The block's transposed index (one workgroup): csc_ptr = exclusive scan of the per-source edge
+// counts over the n_{hop+1} sources, then every edge's entry (target row << 8 | relation) placed
+// in its source's segment. The order inside a segment follows the LDS cursor atomics (not
+// deterministic); the consumer's sums over a segment are exact fixed-point integer sums, so its
+// results do not depend on it. Cursors in LDS: n_{hop+1} <= kCscMax.
+constexpr int kCscThreads = 1024;
+constexpr int kCscMax = 32768;
+
+__global__ void __launch_bounds__(kCscThreads)
+ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ blk_idx,
+              const int32_t* __restrict__ blk_row, const uint8_t* __restrict__ blk_rel,
+              const int32_t* __restrict__ csc_cnt, int32_t* __restrict__ csc_ptr,
+              int32_t* __restrict__ csc_ent) {
+    __shared__ int cur[kCscMax];
+    __shared__ int lds[kCscThreads / 64 + 1];
+    const int n = sizes[hop + 1], E = sizes[8 + hop];
+    constexpr int IT = 8;
+    int carry = 0;
+    for (int base = 0; base < n; base += kCscThreads * IT) {
+        const int i0 = base + threadIdx.x * IT;
+        int v[IT], s = 0;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            v[j] = i0 + j < n ? csc_cnt[i0 + j] : 0;
+            s += v[j];
+        }
+        int total;
+        int off = carry + block_exscan<kCscThreads>(s, lds, &total);
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            if (i0 + j < n) {
+                csc_ptr[i0 + j] = off;
+                cur[i0 + j] = off;
+            }
+            off += v[j];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) csc_ptr[n] = carry;
+    __syncthreads();
+    for (int bp = threadIdx.x; bp < E; bp += kCscThreads) {
+        const int u = blk_idx[bp];
+        const int slot = atomicAdd(cur + u, 1);
+        csc_ent[slot] = (blk_row[bp] << 8) | int(blk_rel[bp]);
     }
 }
 
@@ -473,25 +531,30 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* gsrc, uint8_t* flag, int32_t* tiles, uint64_t* status,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
-                 int64_t* edge_off, int32_t meta_only, hipStream_t stream) {
+                 int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
+                 int32_t* csc_ent, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !blk_row || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
         return REGNN_EINVAL;
     if (!!local != !!edge_type || !!local != !!edge_off || (meta_only && !local))
         return REGNN_EINVAL;
+    const bool csc = csc_cnt != nullptr;
+    if (csc != (csc_ptr != nullptr) || csc != (csc_ent != nullptr) || (csc && meta_only))
+        return REGNN_EINVAL;
     const int lean = meta_only ? 1 : 0;
     if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
     const int64_t cap_e = int64_t(cap_dst) * (k + 1);
     if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
     const int n_tiles = int((cap_e + kNsTile - 1) / kNsTile);
+    if (csc && cap_e > kCscMax) return REGNN_EUNSUPPORTED;
     hipLaunchKernelGGL(ns_sample_kernel, dim3((cap_dst + 3) / 4), dim3(kBlock), 0, stream, ptr,
                        idx, n_id, sizes, hop, cap_dst, k, state, g2l, samp, spos, scnt);
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_rows_kernel, dim3((cap_dst + kNsRowsTile - 1) / kNsRowsTile),
                        dim3(kBlock), 0, stream, scnt, n_id, ntype, num_edge_types, sizes, hop,
                        cap_dst, state, blk_ptr, blk_idx, blk_rel, blk_pos, blk_row, gsrc, inv, status, local,
-                       edge_type, edge_off, lean);
+                       edge_type, edge_off, lean, csc_cnt, int(cap_e));
     REGNN_LAUNCH_CHECK();
     const int64_t slots = int64_t(cap_dst) * k;
     hipLaunchKernelGGL(ns_place_kernel, dim3(unsigned((slots + kBlock - 1) / kBlock)),
@@ -508,8 +571,13 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, int(cap_e), ntype, local,
-                       edge_type, edge_off);
+                       edge_type, edge_off, csc_cnt);
     REGNN_LAUNCH_CHECK();
+    if (csc) {
+        hipLaunchKernelGGL(ns_csc_kernel, dim3(1), dim3(kCscThreads), 0, stream, sizes, hop, blk_idx,
+                           blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent);
+        REGNN_LAUNCH_CHECK();
+    }
     return REGNN_OK;
 }
 

@@ -9,15 +9,17 @@
 //             in two fp32-MFMA stages -- P = sum_t (S_t W_t^T + w_t b_t) (group_input's Linear,
 //             moved after the mean aggregation by linearity) and a = inv (P W_0) + bias (the
 //             conv's x @ W) -- then LayerNorm, relu, dropout -> h0. Keeps P, a and the LN stats
-//             for the backward; zeroes the rows' fixed-point gradient accumulators.
+//             for the backward.
 //   head      layer 1 aggregated first and projected second (a = inv (sum_e tab[r_e] h0[u_e]) W_1
 //             + bias, the same linearity), LayerNorm, relu, dropout, out_lin, log_softmax,
 //             nll_loss (mean over the labelled targets) and the backward to GH = inv ga W_1^T.
-//   scatter   layer 1's transposed aggregation, one 16-lane group per edge over every CU:
-//             gh0[u_e] += tab[r_e] GH[v_e] as 64-bit fixed-point integer atomics (integer sums:
-//             exact in any order) and the relation-table dots <h0[u_e], GH[v_e]>.
-//   bwd0      layer 0's backward per target row: the LayerNorm / relu / dropout backward from
-//             gh0, gP = inv ga W_0^T, the W_0 gradient P^T (inv ga); per source type t the
+//   gather    layer 1's transposed aggregation as a gather over the sampler's transposed index
+//             of hop 0's block (a 16-lane group per layer-0 row, every CU): gh0[u] = sum over u's
+//             edges of tab[r] GH[v] and the relation-table dots <h0[u], GH[v]>, both as exact
+//             2^-40 fixed-point integer sums (the segment order does not matter), then the
+//             LayerNorm / relu / dropout backward -> G0 = inv ga0 rows and their row terms.
+//   bwd0      layer 0's backward per target row: gP = G0 W_0^T, the W_0 gradient P^T G0; per
+//             source type t the
 //             weight gradient gP^T S_t, the bias term, and the relation-table dots from
 //             Z_t = gP W_t (relation slots: <U_t, Z_t> in registers; else Z and beta for rel0).
 //   rel0      (no relation slots) layer 0's relation-table dots edge by edge (re_nsm.hip).
@@ -35,9 +37,9 @@ constexpr int kMaxCT = 27;                 // class tiles of 16 (C <= 432: the h
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
 
-// contributions are rounded to 2^-40 (|x| < 2^23 per accumulated entry): gradient rows of a
-// mean loss are many orders of magnitude inside that range, and the rounding (<= 4.6e-13 per
-// term) is far below fp32 resolution of the sums it feeds
+// terms are rounded to 2^-40 (|x| < 2^23 per accumulated entry): gradient rows of a mean loss
+// are many orders of magnitude inside that range, and the rounding (<= 4.6e-13 per term) is far
+// below fp32 resolution of the sums it feeds
 __device__ __forceinline__ unsigned long long to_fix(float x) {
     return (unsigned long long)__float2ll_rn(x * kFixScale);
 }
@@ -84,7 +86,7 @@ struct Agg0Args {
     const float* w0; const float* bias; const float* ln_w; const float* ln_b;
     const int64_t* state; Drop drop;
     float* s_agg; float* s_w;
-    float* a; float* stats; float* h; float* p; unsigned long long* gacc;
+    float* a; float* stats; float* h; float* p;
     // relation slots (RS): s_agg / s_w hold the unweighted sums / counts of the non-self edges
     // per source type, u_self the self loop's input row, u_rel [n][T + 1] each slot's relation
     int n_et; float* u_self; int32_t* u_rel;
@@ -300,7 +302,7 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
             }
         }
         __syncthreads();
-        // ---- epilogue: P and a kept, LayerNorm, relu, dropout -> h0; gradient accumulators 0
+        // ---- epilogue: P and a kept, LayerNorm, relu, dropout -> h0
         if (v < n) {
             *reinterpret_cast<float4*>(A.p + int64_t(v) * F + 4 * l) =
                 *reinterpret_cast<const float4*>(Pt + sub * 68 + 4 * l);
@@ -319,9 +321,6 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) hv[cc] = fmaxf(fmaf(dd[cc] * rstd, gws[cc], gbs[cc]), 0.f) * mk[cc];
             *reinterpret_cast<float4*>(A.h + int64_t(v) * F + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-            ulonglong2* gz = reinterpret_cast<ulonglong2*>(A.gacc + int64_t(v) * F + 4 * l);
-            gz[0] = make_ulonglong2(0ull, 0ull);
-            gz[1] = make_ulonglong2(0ull, 0ull);
         }
         __syncthreads();                       // the tiles are reused by the next rows
         PH(0, 4);
@@ -666,85 +665,124 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// scatter: layer 1's transposed aggregation over hop 0's block, a 16-lane group per edge e
-// (grid-stride over every CU): gh0[u_e] += tab[r_e] GH[v_e] (4 features per lane, 2^-40 fixed
-// point, integer atomics: the sums are exact in any order) and the relation-table dot
-// <h0[u_e], GH[v_e]> into the group's bin (its own edges in order), then the block's groups
-// summed in order -> one slab row of relation dots per block.
-struct ScatArgs {
-    const int32_t* sizes; const int32_t* idx; const uint8_t* rel; const int32_t* row;
-    const float* gh; const float* h; const float* rw; int n_rel; float alpha;
-    unsigned long long* gacc; float* slab;
+// gather: a 16-lane group per layer-0 row u (grid-stride over every CU), 4 features per lane:
+//   gh0[u] = sum over u's edges e of hop 0's block (the sampler's transposed index) of
+//            tab[r_e] GH[v_e], and the relation dots <h0[u], GH[v_e]>: exact 2^-40 fixed-point
+//            integer sums (registers / LDS), so the segment order does not matter;
+//   h0 re-formed from a0, the LN stats and the dropout mask; the LayerNorm / relu / dropout
+//   backward -> G0[u] = inv0[u] ga0[u] (HBM, bwd0's rows), and the rows' sums of ga0, gy and
+//   gy xhat (conv bias, LN beta / gamma) per group, summed over the block's groups in order.
+// Slab row per block: [64 relation dots | 64 sum ga0 | 64 sum gy | 64 sum gy xhat]
+struct GathArgs {
+    const int32_t* sizes; int hop;
+    const int32_t* cptr; const int32_t* cent; const float* gh;
+    const float* a; const float* stats; const float* inv;
+    const float* ln_w; const float* ln_b; const int64_t* state; Drop drop;
+    const float* rw; int n_rel; float alpha;
+    float* g0; float* slab;
 };
 
-constexpr int kScatBlocks = 512;
+constexpr int kGathBlocks = 512;
+constexpr int kGathW = 4 * F;
 
-__global__ void __launch_bounds__(kBlock) scatter_kernel(ScatArgs A) {
-    __shared__ float bins[16][F];
+__global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
+    __shared__ unsigned long long bins[F];
     __shared__ float tab[F];
-    for (int i = threadIdx.x; i < 16 * F; i += kBlock) (&bins[0][0])[i] = 0.f;
-    if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
-    __syncthreads();
-    const int E = A.sizes[8];
-    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const int stride = gridDim.x * 16;
-    int e = blockIdx.x * 16 + grp;
-    for (; e + stride < E; e += 2 * stride) {            // two edges in flight per group
-        const int e2 = e + stride;
-        const int v0 = A.row[e], u0 = A.idx[e], r0 = A.rel[e];
-        const int v1 = A.row[e2], u1 = A.idx[e2], r1 = A.rel[e2];
-        const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(v0) * F + 4 * l);
-        const float4 x0 = *reinterpret_cast<const float4*>(A.h + int64_t(u0) * F + 4 * l);
-        const float4 g1 = *reinterpret_cast<const float4*>(A.gh + int64_t(v1) * F + 4 * l);
-        const float4 x1 = *reinterpret_cast<const float4*>(A.h + int64_t(u1) * F + 4 * l);
-        const float d0 = group_sum<16>(x0.x * g0.x + x0.y * g0.y + x0.z * g0.z + x0.w * g0.w);
-        const float d1 = group_sum<16>(x1.x * g1.x + x1.y * g1.y + x1.z * g1.z + x1.w * g1.w);
-        if (l == 0) {
-            bins[grp][r0] += d0;
-            bins[grp][r1] += d1;
-        }
-        const float w0 = tab[r0], w1 = tab[r1];
-        unsigned long long* p0 = A.gacc + int64_t(u0) * F + 4 * l;
-        unsigned long long* p1 = A.gacc + int64_t(u1) * F + 4 * l;
-        atomicAdd(p0 + 0, to_fix(w0 * g0.x)); atomicAdd(p0 + 1, to_fix(w0 * g0.y));
-        atomicAdd(p0 + 2, to_fix(w0 * g0.z)); atomicAdd(p0 + 3, to_fix(w0 * g0.w));
-        atomicAdd(p1 + 0, to_fix(w1 * g1.x)); atomicAdd(p1 + 1, to_fix(w1 * g1.y));
-        atomicAdd(p1 + 2, to_fix(w1 * g1.z)); atomicAdd(p1 + 3, to_fix(w1 * g1.w));
-    }
-    if (e < E) {
-        const int v0 = A.row[e], u0 = A.idx[e], r0 = A.rel[e];
-        const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(v0) * F + 4 * l);
-        const float4 x0 = *reinterpret_cast<const float4*>(A.h + int64_t(u0) * F + 4 * l);
-        const float d0 = group_sum<16>(x0.x * g0.x + x0.y * g0.y + x0.z * g0.z + x0.w * g0.w);
-        if (l == 0) bins[grp][r0] += d0;
-        const float w0 = tab[r0];
-        unsigned long long* p0 = A.gacc + int64_t(u0) * F + 4 * l;
-        atomicAdd(p0 + 0, to_fix(w0 * g0.x)); atomicAdd(p0 + 1, to_fix(w0 * g0.y));
-        atomicAdd(p0 + 2, to_fix(w0 * g0.z)); atomicAdd(p0 + 3, to_fix(w0 * g0.w));
-    }
-    __syncthreads();
+    __shared__ float rt[3][16][F];
     if (threadIdx.x < F) {
-        float s = 0.f;
+        bins[threadIdx.x] = 0ull;
+        tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
+    }
+    __syncthreads();
+    const int n = A.sizes[A.hop];
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
+    const float4 lw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
+    const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
+    float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int u = blockIdx.x * 16 + grp; u < n; u += gridDim.x * 16) {
+        const int c0 = A.cptr[u], c1 = A.cptr[u + 1];
+        const float4 a4 = *reinterpret_cast<const float4*>(A.a + int64_t(u) * F + 4 * l);
+        const float2 st = reinterpret_cast<const float2*>(A.stats)[u];
+        const float iv = A.inv[u];
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        float mk[4], xh[4], yv[4], h0[4];
+        drop_factors(key, A.drop, u, l, mk);
 #pragma unroll
-        for (int g = 0; g < 16; ++g) s += bins[g][threadIdx.x];
-        A.slab[int64_t(blockIdx.x) * F + threadIdx.x] = s;
+        for (int i = 0; i < 4; ++i) {
+            xh[i] = (av[i] - st.x) * st.y;
+            yv[i] = fmaf(xh[i], lw[i], lb[i]);
+            h0[i] = fmaxf(yv[i], 0.f) * mk[i];
+        }
+        unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
+        for (int j = c0; j < c1; j += 2) {               // two entries in flight
+            const bool two = j + 1 < c1;                 // uniform over the group
+            const int pk0 = A.cent[j], pk1 = two ? A.cent[j + 1] : pk0;
+            const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(pk0 >> 8) * F + 4 * l);
+            const float4 g1 = *reinterpret_cast<const float4*>(A.gh + int64_t(pk1 >> 8) * F + 4 * l);
+            const float t0 = tab[pk0 & 255], t1 = two ? tab[pk1 & 255] : 0.f;
+            acc[0] += to_fix(t0 * g0.x) + to_fix(t1 * g1.x);
+            acc[1] += to_fix(t0 * g0.y) + to_fix(t1 * g1.y);
+            acc[2] += to_fix(t0 * g0.z) + to_fix(t1 * g1.z);
+            acc[3] += to_fix(t0 * g0.w) + to_fix(t1 * g1.w);
+            const float d0 = group_sum<16>(h0[0] * g0.x + h0[1] * g0.y + h0[2] * g0.z + h0[3] * g0.w);
+            const float d1 = group_sum<16>(h0[0] * g1.x + h0[1] * g1.y + h0[2] * g1.z + h0[3] * g1.w);
+            if (l == 0) {
+                atomicAdd(bins + (pk0 & 255), to_fix(d0));          // LDS, integer: exact
+                if (two) atomicAdd(bins + (pk1 & 255), to_fix(d1));
+            }
+        }
+        float gy[4], gx[4], p1 = 0.f, p2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            gy[i] = yv[i] > 0.f ? from_fix(acc[i]) * mk[i] : 0.f;
+            gx[i] = gy[i] * lw[i];
+            p1 += gx[i];
+            p2 += gx[i] * xh[i];
+        }
+        const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
+        float ga[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ga[i] = st.y * (gx[i] - m1 - xh[i] * m2);
+            sga[i] += ga[i];
+            sgy[i] += gy[i];
+            sgyx[i] += gy[i] * xh[i];
+        }
+        *reinterpret_cast<float4*>(A.g0 + int64_t(u) * F + 4 * l) =
+            make_float4(iv * ga[0], iv * ga[1], iv * ga[2], iv * ga[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        rt[0][grp][4 * l + i] = sga[i];
+        rt[1][grp][4 * l + i] = sgy[i];
+        rt[2][grp][4 * l + i] = sgyx[i];
+    }
+    __syncthreads();
+    float* o = A.slab + int64_t(blockIdx.x) * kGathW;
+    if (threadIdx.x < F) o[threadIdx.x] = float((long long)bins[threadIdx.x]) * kFixInv;
+    if (threadIdx.x < 3 * F) {
+        const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
+        float sum = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) sum += rt[which][g][f];
+        o[F + threadIdx.x] = sum;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // bwd0: block (b, t) takes 16-row tiles b, b + gridDim.x, ... of layer 0's targets; the next
 // tile's rows are prefetched into registers while this one is processed. Per tile:
-//   front  (16 lanes per row) gh0 = fixed-point sums / 2^40, LayerNorm / relu / dropout backward
-//          -> ga, G0 = inv ga; t = 0 also sums ga, gy, gy * xhat (conv bias, LN beta / gamma);
-//   gP     = G0 W_0^T (MFMA; W_0 rows from L2 in registers); t = 0: W_0 partial P^T G0;
+//   gP     = G0 W_0^T (MFMA; G0 = the gather's rows, W_0 rows from L2 in registers); t = 0: the
+//          W_0 partial P^T G0;
 //   type t gW_t partial gP^T S_t (stored [64][K], lins[t].weight's layout), gb_t = sum w_t gP,
 //          Z_t = gP W_t (MFMA, W_t staged in LDS k-major): relation slots: the relation dots
 //          <U_t, Z_t> + cnt beta and <x_self, Z_t> + beta in per-row bin columns (no Z to HBM);
 //          else Z, beta -> HBM for rel0.
 struct Bwd0Args {
     const int32_t* sizes; int hop; int T;
-    const float* inv; const unsigned long long* gacc; const float* a; const float* stats;
-    const float* ln_w; const float* ln_b; const int64_t* state; Drop drop;
+    const float* g0;
     const float* p; const float* w0;
     const float* s_agg; const float* s_w; Ptrs lin_w; Ptrs lin_b;
     const float* rw; int n_rel; float alpha; int n_et;
@@ -752,10 +790,10 @@ struct Bwd0Args {
     float* z; float* beta;
     float* slab;     // [t][block][(K + 1) * 64]: g W_t ([64][K]) | g b_t
     float* rslab;    // relation slots: [t][block][64] relation dots
-    float* slab0;    // [block][64 * 64 + 3 * 64]: g W_0 | g conv bias | g LN beta | g LN gamma
+    float* slab0;    // [block][64 * 64]: g W_0
 };
 
-constexpr int kPost0W = F * F + 3 * F;
+constexpr int kPost0W = F * F;
 
 template <int K, bool RS>
 constexpr size_t bwd0_lds_floats(int n_rel) {
@@ -798,10 +836,6 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     const int n = A.sizes[A.hop];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
     const int gr = threadIdx.x >> 4, gj = threadIdx.x & 15;
-    const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
-    const float4 lw4 = reinterpret_cast<const float4*>(A.ln_w)[gj];
-    const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[gj];
-    const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
     float4 w0r[4];                            // W_0[16 w + c][16 b + 4 q ..]: gP's B operand
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -814,13 +848,10 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) acc0[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bsum = 0.f;
-    float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
     // prefetched rows of the next tile
     float4 ur[XV], xr[XV];
-    ulonglong2 gq0, gq1;
-    float4 a4, p4;
-    float2 st2;
-    float ivv = 0.f, cntv = 0.f;
+    float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), p4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float cntv = 0.f;
     int relv = -1, rsv = -1;
     auto load = [&](int v0) {
 #pragma unroll
@@ -835,15 +866,12 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
                            : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const int v = v0 + gr;
-        if (v < n) {
-            const ulonglong2* g = reinterpret_cast<const ulonglong2*>(A.gacc + int64_t(v) * F + 4 * gj);
-            gq0 = g[0];
-            gq1 = g[1];
-            a4 = *reinterpret_cast<const float4*>(A.a + int64_t(v) * F + 4 * gj);
-            st2 = reinterpret_cast<const float2*>(A.stats)[v];
-            ivv = A.inv[v];
-            if (t0) p4 = *reinterpret_cast<const float4*>(A.p + int64_t(v) * F + 4 * gj);
-        }
+        const bool okv = v < n;
+        g4 = okv ? *reinterpret_cast<const float4*>(A.g0 + int64_t(v) * F + 4 * gj)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t0)
+            p4 = okv ? *reinterpret_cast<const float4*>(A.p + int64_t(v) * F + 4 * gj)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
         if (threadIdx.x < 16) {
             const int vv = v0 + threadIdx.x;
             const bool ok = vv < n;
@@ -861,42 +889,8 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     PH(2, 1);
     for (; tile * 16 < n; tile += gridDim.x) {
         const int v0 = tile * 16;
-        // ---- front: LayerNorm / relu / dropout backward of row v0 + gr, features 4 gj ..
-        {
-            const int v = v0 + gr;
-            const bool ok = v < n;
-            float g0[4] = {0.f, 0.f, 0.f, 0.f};
-            if (ok) {
-                const float gh[4] = {from_fix(gq0.x), from_fix(gq0.y), from_fix(gq1.x), from_fix(gq1.y)};
-                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-                float mk[4];
-                drop_factors(key, A.drop, v, gj, mk);
-                float xh[4], gy[4], gx[4], p1 = 0.f, p2 = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    xh[i] = (av[i] - st2.x) * st2.y;
-                    const float yv = fmaf(xh[i], lw[i], lb[i]);
-                    gy[i] = yv > 0.f ? gh[i] * mk[i] : 0.f;
-                    gx[i] = gy[i] * lw[i];
-                    p1 += gx[i];
-                    p2 += gx[i] * xh[i];
-                }
-                const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float ga = st2.y * (gx[i] - m1 - xh[i] * m2);
-                    g0[i] = ivv * ga;
-                    if (t0) {
-                        sga[i] += ga;
-                        sgy[i] += gy[i];
-                        sgyx[i] += gy[i] * xh[i];
-                    }
-                }
-            }
-            *reinterpret_cast<float4*>(g0s + gr * 68 + 4 * gj) = make_float4(g0[0], g0[1], g0[2], g0[3]);
-            if (t0)
-                *reinterpret_cast<float4*>(psh + gr * 68 + 4 * gj) = ok ? p4 : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        *reinterpret_cast<float4*>(g0s + gr * 68 + 4 * gj) = g4;
+        if (t0) *reinterpret_cast<float4*>(psh + gr * 68 + 4 * gj) = p4;
         if (threadIdx.x < 16) {                // row meta: S = wr U + ws x_self (RS)
             if constexpr (RS) {
                 const bool self = rsv >= 0 && rsv - A.n_et == t;
@@ -1057,22 +1051,6 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) o0[(16 * w + 4 * q + i) * F + 16 * jb + c] = acc0[jb][i];
-        __syncthreads();                       // Wk free: the row terms, summed over the rows
-        float* rt = Wk;                        // [3][16][64]
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            rt[(0 * 16 + gr) * F + 4 * gj + i] = sga[i];
-            rt[(1 * 16 + gr) * F + 4 * gj + i] = sgy[i];
-            rt[(2 * 16 + gr) * F + 4 * gj + i] = sgyx[i];
-        }
-        __syncthreads();
-        if (threadIdx.x < 3 * F) {
-            const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
-            float s = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s += rt[(which * 16 + r) * F + f];
-            o0[F * F + threadIdx.x] = s;
-        }
     }
 }
 
@@ -1203,7 +1181,7 @@ struct JobList {
 };
 
 struct Slab2 {
-    int64_t head, scat, rel0, proj, post0, total;
+    int64_t head, gath, rel0, proj, post0, total;
     int head_blocks, rel0_rows;
 };
 
@@ -1213,8 +1191,8 @@ inline Slab2 slab2(const regnn_nsm_params* p, int cap0) {
     int64_t o = 0;
     s.head = o;
     o += int64_t(s.head_blocks) * head_part_width(p->n_classes);
-    s.scat = o;                                // layer 1's relation dots, per scatter block
-    o += int64_t(kScatBlocks) * F;
+    s.gath = o;                                // the gather's relation dots and row terms
+    o += int64_t(kGathBlocks) * kGathW;
     s.rel0 = o;                                // bwd0's (RS) or rel0's relation rows
     s.rel0_rows = p->rel_slots ? p->n_types * kBwdBlocks : kAggBlocks;
     o += int64_t(p->n_types * kBwdBlocks > kAggBlocks ? p->n_types * kBwdBlocks : kAggBlocks) * F;
@@ -1251,7 +1229,8 @@ bool regnn_nsm2_covers(const regnn_nsm_params* p) {
 int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     const int T = p->n_types, K = p->k_in, C = p->n_classes;
     const bool rs = p->rel_slots != 0;
-    if (!w->gacc || !w->p0 || !w->gh1 || !w->blk_row0 || !w->xs[1] || !w->a[0] || !w->stats[0])
+    if (!w->p0 || !w->gh1 || !w->csc_ptr0 || !w->csc_ent0 || !w->xs[1] || !w->a[0] ||
+        !w->stats[0] || !w->ga[0])
         return REGNN_EINVAL;
     const regnn_nsm_adam* ad = w->adam;
     if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step ||
@@ -1278,7 +1257,6 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         A.state = w->state; A.drop = drop;
         A.s_agg = w->s_agg; A.s_w = w->s_w;
         A.a = w->a[0]; A.stats = w->stats[0]; A.h = w->xs[1]; A.p = w->p0;
-        A.gacc = reinterpret_cast<unsigned long long*>(w->gacc);
         A.n_et = p->n_edge_types; A.u_self = w->u_self; A.u_rel = w->u_rel;
         int grid = (w->cap[h] + 15) / 16;
         if (grid > 2048) grid = 2048;
@@ -1315,24 +1293,22 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kBlock), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
-    // 3. layer 1's transposed aggregation into layer 0's rows
+    // 3. layer 1's transposed aggregation (a gather), layer 0's LayerNorm backward
     {
-        ScatArgs G{};
-        G.sizes = w->sizes; G.idx = w->blk_idx[0]; G.rel = w->blk_rel[0]; G.row = w->blk_row0;
-        G.gh = w->gh1; G.h = w->xs[1]; G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1];
-        G.alpha = p->alpha; G.gacc = reinterpret_cast<unsigned long long*>(w->gacc);
-        G.slab = w->slab + S.scat;
-        hipLaunchKernelGGL(scatter_kernel, dim3(kScatBlocks), dim3(kBlock), 0, stream, G);
+        GathArgs G{};
+        G.sizes = w->sizes; G.hop = 1; G.cptr = w->csc_ptr0; G.cent = w->csc_ent0; G.gh = w->gh1;
+        G.a = w->a[0]; G.stats = w->stats[0]; G.inv = w->blk_inv[1];
+        G.ln_w = p->ln_w[0]; G.ln_b = p->ln_b[0]; G.state = w->state; G.drop = drop;
+        G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1]; G.alpha = p->alpha;
+        G.g0 = w->ga[0]; G.slab = w->slab + S.gath;
+        hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kBlock), 0, stream, G);
         REGNN_LAUNCH_CHECK();
     }
     // 4. layer 0's backward
     {
         Bwd0Args B{};
         B.sizes = w->sizes; B.hop = 1; B.T = T;
-        B.inv = w->blk_inv[1];
-        B.gacc = reinterpret_cast<const unsigned long long*>(w->gacc); B.a = w->a[0]; B.stats = w->stats[0];
-        B.ln_w = p->ln_w[0]; B.ln_b = p->ln_b[0]; B.state = w->state; B.drop = drop;
-        B.p = w->p0; B.w0 = p->conv_w[0];
+        B.g0 = w->ga[0]; B.p = w->p0; B.w0 = p->conv_w[0];
         B.s_agg = w->s_agg; B.s_w = w->s_w; B.lin_w = lin_w; B.lin_b = lin_b;
         B.rw = p->conv_rw[0]; B.n_rel = p->n_rel[0]; B.alpha = p->alpha; B.n_et = p->n_edge_types;
         B.u_self = w->u_self; B.u_rel = w->u_rel; B.z = w->z; B.beta = w->beta;
@@ -1370,7 +1346,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
         J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
         J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
-        J.add(w->slab + S.scat, F, kScatBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
+        const float* gs = w->slab + S.gath;
+        J.add(gs, kGathW, kGathBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
         J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
         const int64_t pw = int64_t(K + 1) * F;
         for (int t = 0; t < T; ++t) {
@@ -1378,11 +1355,10 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
             J.add(src, pw, kBwdBlocks, K * F, p->g_lin_w[t]);
             J.add(src + int64_t(K) * F, pw, kBwdBlocks, F, p->g_lin_b[t]);
         }
-        const float* p0 = w->slab + S.post0;
-        J.add(p0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
-        J.add(p0 + F * F, kPost0W, kBwdBlocks, F, p->g_conv_b[0]);
-        J.add(p0 + F * F + F, kPost0W, kBwdBlocks, F, p->g_ln_b[0]);
-        J.add(p0 + F * F + 2 * F, kPost0W, kBwdBlocks, F, p->g_ln_w[0]);
+        J.add(w->slab + S.post0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
+        J.add(gs + F, kGathW, kGathBlocks, F, p->g_conv_b[0]);
+        J.add(gs + 2 * F, kGathW, kGathBlocks, F, p->g_ln_b[0]);
+        J.add(gs + 3 * F, kGathW, kGathBlocks, F, p->g_ln_w[0]);
         if (ad) {
             AdamArgs& O = J.A.adam;
             O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;

@@ -127,6 +127,7 @@ class DeviceSampler:
             self.blocks.append(blk)
         self.local, self.edge_meta = None, [None] * len(self.sizes_k)
         self.meta_fresh = [False] * len(self.sizes_k)
+        self.csc = [None] * len(self.sizes_k)      # per hop: (cnt, ptr, ent) or None
         # meta_only[h]: hop h writes only the edge meta its consumer reads (regnn_ns_hop
         # meta_only: no de-duplication, n_id not extended, sampled blk_idx unwritten)
         self.meta_only = [False] * len(self.sizes_k)
@@ -140,6 +141,16 @@ class DeviceSampler:
                                torch.zeros(ce, dtype=torch.int64, device=self.device))
         self.meta_fresh[hop] = False          # written by the next run_hops
         return self.edge_meta[hop]
+
+    def enable_csc(self, hop):
+        """also build hop `hop`'s transposed index (regnn_ns_hop csc_*: per local source, its
+        edges' target row << 8 | relation), what the fused step's transposed pass gathers by."""
+        ce = self.blocks[hop].csr_idx.numel()
+        if ce > 32768:
+            raise ValueError(f"the transposed index needs <= 32768 block edges, got {ce}")
+        z = lambda n: torch.zeros(n, dtype=torch.int32, device=self.device)  # noqa: E731
+        self.csc[hop] = (z(ce), z(ce + 1), z(ce))
+        return self.csc[hop]
 
     # -- the per-step device work ------------------------------------------------------------
     def batch_from_perm(self, perm, rank=0, world=1):
@@ -165,6 +176,8 @@ class DeviceSampler:
                    *((L.ptr(self.local), L.ptr(self.edge_meta[h][0]), L.ptr(self.edge_meta[h][1]))
                      if self.edge_meta[h] is not None else (None, None, None)),
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
+                   *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
+                     else (None, None, None)),
                    L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
 
@@ -240,8 +253,8 @@ class _NsmWork(ctypes.Structure):
                 ("wc", _P), ("gwc", _P), ("tabs", _P), ("xs", _P * _ML), ("gxs", _P * _ML),
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
-                ("u_self", _P), ("u_rel", _P), ("gacc", _P), ("p0", _P), ("adam", _P),
-                ("gh1", _P), ("blk_row0", _P)]
+                ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
+                ("csc_ptr0", _P), ("csc_ent0", _P)]
 
 
 class _NsmAdam(ctypes.Structure):
@@ -409,12 +422,13 @@ class FusedStep:
         W.s_w, W.beta = ptr(z(n0, T)), ptr(z(n0, T))
         W.nvalid = ptr(z(1))
         # the two-layer step: layer 0 rows' fixed-point gradient sums and group_input's projection
-        self.two_layer = nl == 2 and C <= TWO_LAYER_MAX_CLASSES
+        self.two_layer = (nl == 2 and C <= TWO_LAYER_MAX_CLASSES and
+                          sampler.blocks[0].csr_idx.numel() <= 32768)
         if self.two_layer:
-            W.gacc = ptr(torch.zeros(caps[1] * 64, dtype=torch.int64, device=dev))
             W.p0 = ptr(z(caps[1], 64))
             W.gh1 = ptr(z(caps[0], 64))
-            W.blk_row0 = ptr(sampler.blocks[0].row)
+            _, cptr, cent = sampler.csc[0] or sampler.enable_csc(0)
+            W.csc_ptr0, W.csc_ent0 = ptr(cptr), ptr(cent)
         self.adam = None
         P.n_edge_types = int(sampler.num_edge_types)
         P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))
@@ -442,7 +456,7 @@ class FusedStep:
     def kernels(self):
         """the kernels one regnn_nsm_step launches, in order (bench.py's roofline label)."""
         if self.two_layer:
-            ks = ["agg0", "head", "scatter", "bwd0"] + ([] if self.P.rel_slots else ["rel0"])
+            ks = ["agg0", "head", "gather", "bwd0"] + ([] if self.P.rel_slots else ["rel0"])
             return ks + ["finalize+adam" if self.adam is not None else "finalize"]
         ks = ["prep", "agg0"] + ["agg"] * (self.n_layers - 2) + ["head"]
         ks += ["agg_bwd", "post_bwd"] * (self.n_layers - 1)

@@ -564,7 +564,7 @@ def test_two_layer_step_bitwise_reproducible(monkeypatch, rel_slots):
         m.train()
         tr, _ = _setup_trainer(d, m, batch=128, sizes=(10, 6))
         assert tr.fused is not None and tr.fused.two_layer
-        assert tr.fused.kernels()[:4] == ["agg0", "head", "scatter", "bwd0"]
+        assert tr.fused.kernels()[:4] == ["agg0", "head", "gather", "bwd0"]
         tr._forward_backward()
         torch.cuda.synchronize()
         outs.append((float(tr.loss), [p.grad.clone() for p in m.parameters()]))
@@ -613,3 +613,38 @@ def test_fused_adam_equals_separate_adam(monkeypatch):
         x, y = x[keep], y[keep]
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), (x.double() - y.double()).abs().max()
     assert int(a.opt.step_count) == int(b.opt.step_count) == 8
+
+
+def test_block_transposed_index():
+    """regnn_ns_hop's transposed index of a block (csc_ptr / csc_ent): per local source u, the
+    multiset of (target row << 8 | relation) over the block edges whose source is u, and the
+    block's per-edge target rows (blk_row)."""
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.ns import DeviceSampler
+    rng = np.random.default_rng(12)
+    N, E = 5000, 80000
+    dst = np.minimum((rng.pareto(1.1, E) * 4).astype(np.int64), N - 1)
+    src = np.where(rng.random(E) < 0.3, rng.integers(0, 40, E), rng.integers(0, N, E))
+    rg = RelGraph(src, dst, N, DEV)
+    ds = DeviceSampler(rg, [12, 5], 150, etype=torch.from_numpy(rng.integers(0, 7, E)),
+                       ntype=torch.from_numpy(rng.integers(0, 4, N)), num_edge_types=7)
+    _, cptr, cent = ds.enable_csc(0)
+    ds.set_seed(5, 0, 1)
+    ds.set_targets(torch.from_numpy(rng.permutation(N)[:150]).to(DEV))
+    ds.run_hops()
+    sz = ds.sizes.cpu().tolist()
+    n_dst, n_src, Eb = sz[0], sz[1], sz[8]
+    blk = ds.blocks[0]
+    ptr = blk.csr_ptr[:n_dst + 1].cpu().numpy()
+    idx = blk.csr_idx[:Eb].cpu().numpy()
+    rel = blk.rel[:Eb].cpu().numpy().astype(np.int64)
+    row = blk.row[:Eb].cpu().numpy()
+    assert np.array_equal(row, np.repeat(np.arange(n_dst), np.diff(ptr)))
+    cp = cptr[:n_src + 1].cpu().numpy()
+    ce = cent[:Eb].cpu().numpy().astype(np.int64)
+    assert cp[0] == 0 and cp[-1] == Eb and np.all(np.diff(cp) >= 1)   # every source has an edge
+    want = [[] for _ in range(n_src)]
+    for bp in range(Eb):
+        want[idx[bp]].append((int(row[bp]) << 8) | int(rel[bp]))
+    for u in range(n_src):
+        assert sorted(ce[cp[u]:cp[u + 1]].tolist()) == sorted(want[u]), u
