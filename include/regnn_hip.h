@@ -571,10 +571,11 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * hop whose sources only feed layer 0 by (type, row) — no first-seen de-duplication, no n_id
  * append (sizes[hop + 1] = sizes[hop]), blk_idx of the sampled edges not written; blk_ptr,
  * blk_rel, blk_pos, inv, the self loops and the edge meta as above (3 launches instead of 6).
- * Optional (all three or none, not with meta_only): the block's transposed index -- csc_cnt
+ * Optional (all four or none, not with meta_only): the block's transposed index -- csc_cnt
  * [cap_e] (scratch), csc_ptr [cap_e + 1] (source i's edges are csc_ent[csc_ptr[i] ..
- * csc_ptr[i + 1]) over the n_{hop+1} sources), csc_ent [cap_e] = target row << 8 | relation;
- * the order inside a segment is unspecified (one more launch; cap_e <= 32768). */
+ * csc_ptr[i + 1]) over the n_{hop+1} sources), csc_ent [cap_e] = target row << 8 | relation
+ * (the order inside a segment is unspecified), csc_long [cap_e + 1] = the number of sources
+ * with more than 16 edges, then their ids ascending (one more launch; cap_e <= 32768). */
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
@@ -583,7 +584,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
                  int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
-                 int32_t* csc_ent, hipStream_t stream);
+                 int32_t* csc_ent, int32_t* csc_long, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -699,8 +700,9 @@ typedef struct regnn_nsm_work {
     float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
     const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
     float* gh1;               /* cap[0] * 64: G W_1^T of layer 1's target rows (its transposed pass) */
-    const int32_t* csc_ptr0;  /* hop 0's transposed index (regnn_ns_hop csc_ptr / csc_ent) */
-    const int32_t* csc_ent0;
+    const int32_t* csc_ptr0;  /* hop 0's transposed index (regnn_ns_hop csc_ptr / csc_ent / */
+    const int32_t* csc_ent0;  /* csc_long) */
+    const int32_t* csc_long0;
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

@@ -414,41 +414,51 @@ ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ 
 // counts over the n_{hop+1} sources, then every edge's entry (target row << 8 | relation) placed
 // in its source's segment. The order inside a segment follows the LDS cursor atomics (not
 // deterministic); the consumer's sums over a segment are exact fixed-point integer sums, so its
-// results do not depend on it. Cursors in LDS: n_{hop+1} <= kCscMax.
+// results do not depend on it. Also the sources with more than kCscShort edges, ascending
+// (csc_long[0] = their number, csc_long[1 ..] = the ids): the consumer gives each a whole
+// workgroup. Cursors in LDS: n_{hop+1} <= kCscMax.
 constexpr int kCscThreads = 1024;
 constexpr int kCscMax = 32768;
+constexpr int kCscShort = 16;
 
 __global__ void __launch_bounds__(kCscThreads)
 ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ blk_idx,
               const int32_t* __restrict__ blk_row, const uint8_t* __restrict__ blk_rel,
               const int32_t* __restrict__ csc_cnt, int32_t* __restrict__ csc_ptr,
-              int32_t* __restrict__ csc_ent) {
+              int32_t* __restrict__ csc_ent, int32_t* __restrict__ csc_long) {
     __shared__ int cur[kCscMax];
     __shared__ int lds[kCscThreads / 64 + 1];
     const int n = sizes[hop + 1], E = sizes[8 + hop];
     constexpr int IT = 8;
-    int carry = 0;
+    int carry = 0, lcarry = 0;
     for (int base = 0; base < n; base += kCscThreads * IT) {
         const int i0 = base + threadIdx.x * IT;
-        int v[IT], s = 0;
+        int v[IT], s = 0, nl = 0;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             v[j] = i0 + j < n ? csc_cnt[i0 + j] : 0;
             s += v[j];
+            nl += v[j] > kCscShort ? 1 : 0;
         }
-        int total;
+        int total, ltotal;
         int off = carry + block_exscan<kCscThreads>(s, lds, &total);
+        int loff = lcarry + block_exscan<kCscThreads>(nl, lds, &ltotal);
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             if (i0 + j < n) {
                 csc_ptr[i0 + j] = off;
                 cur[i0 + j] = off;
+                if (v[j] > kCscShort) csc_long[1 + loff++] = i0 + j;
             }
             off += v[j];
         }
         carry += total;
+        lcarry += ltotal;
     }
-    if (threadIdx.x == 0) csc_ptr[n] = carry;
+    if (threadIdx.x == 0) {
+        csc_ptr[n] = carry;
+        csc_long[0] = lcarry;
+    }
     __syncthreads();
     for (int bp = threadIdx.x; bp < E; bp += kCscThreads) {
         const int u = blk_idx[bp];
@@ -532,7 +542,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
                  int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
-                 int32_t* csc_ent, hipStream_t stream) {
+                 int32_t* csc_ent, int32_t* csc_long, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !blk_row || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
@@ -540,7 +550,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     if (!!local != !!edge_type || !!local != !!edge_off || (meta_only && !local))
         return REGNN_EINVAL;
     const bool csc = csc_cnt != nullptr;
-    if (csc != (csc_ptr != nullptr) || csc != (csc_ent != nullptr) || (csc && meta_only))
+    if (csc != (csc_ptr != nullptr) || csc != (csc_ent != nullptr) ||
+        csc != (csc_long != nullptr) || (csc && meta_only))
         return REGNN_EINVAL;
     const int lean = meta_only ? 1 : 0;
     if (k < 1 || k > 64) return REGNN_EUNSUPPORTED;
@@ -575,7 +586,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     REGNN_LAUNCH_CHECK();
     if (csc) {
         hipLaunchKernelGGL(ns_csc_kernel, dim3(1), dim3(kCscThreads), 0, stream, sizes, hop, blk_idx,
-                           blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent);
+                           blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent, csc_long);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

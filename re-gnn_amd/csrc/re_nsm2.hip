@@ -665,17 +665,22 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// gather: a 16-lane group per layer-0 row u (grid-stride over every CU), 4 features per lane:
+// gather: layer 0's rows u (hop 0's sources), 4 features per lane of a 16-lane group:
 //   gh0[u] = sum over u's edges e of hop 0's block (the sampler's transposed index) of
 //            tab[r_e] GH[v_e], and the relation dots <h0[u], GH[v_e]>: exact 2^-40 fixed-point
-//            integer sums (registers / LDS), so the segment order does not matter;
+//            integer sums (registers / LDS), so neither the segment order nor the split of a
+//            segment over groups changes a bit;
 //   h0 re-formed from a0, the LN stats and the dropout mask; the LayerNorm / relu / dropout
-//   backward -> G0[u] = inv0[u] ga0[u] (HBM, bwd0's rows), and the rows' sums of ga0, gy and
-//   gy xhat (conv bias, LN beta / gamma) per group, summed over the block's groups in order.
+//   backward -> G0[u] = inv0[u] ga0[u] (HBM, bwd0's rows) and the rows' sums of ga0, gy and
+//   gy xhat (conv bias, LN beta / gamma).
+// Rows with <= kShort edges: one group each (grid-stride), the entries loaded lane-parallel and
+// their GH rows 8 in flight. Longer rows (the hubs: the sampler's ascending csc_long list): a
+// whole workgroup each, the segment's 16-entry chunks over its groups, the partial sums added in
+// LDS. Row terms per group in a fixed row order, summed over the groups in order.
 // Slab row per block: [64 relation dots | 64 sum ga0 | 64 sum gy | 64 sum gy xhat]
 struct GathArgs {
     const int32_t* sizes; int hop;
-    const int32_t* cptr; const int32_t* cent; const float* gh;
+    const int32_t* cptr; const int32_t* cent; const int32_t* clong; const float* gh;
     const float* a; const float* stats; const float* inv;
     const float* ln_w; const float* ln_b; const int64_t* state; Drop drop;
     const float* rw; int n_rel; float alpha;
@@ -684,9 +689,89 @@ struct GathArgs {
 
 constexpr int kGathBlocks = 512;
 constexpr int kGathW = 4 * F;
+constexpr int kShort = 16;                 // = re_ns.hip kCscShort
+
+struct RowIn {                             // one lane's 4 features of layer 0's row u
+    float xh[4], yv[4], mk[4], h0[4], rstd, iv;
+};
+
+__device__ __forceinline__ RowIn row_in(const GathArgs& A, uint32_t key, int u, int l,
+                                         const float (&lw)[4], const float (&lb)[4]) {
+    RowIn R;
+    const float4 a4 = *reinterpret_cast<const float4*>(A.a + int64_t(u) * F + 4 * l);
+    const float2 st = reinterpret_cast<const float2*>(A.stats)[u];
+    R.iv = A.inv[u];
+    R.rstd = st.y;
+    const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+    drop_factors(key, A.drop, u, l, R.mk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        R.xh[i] = (av[i] - st.x) * st.y;
+        R.yv[i] = fmaf(R.xh[i], lw[i], lb[i]);
+        R.h0[i] = fmaxf(R.yv[i], 0.f) * R.mk[i];
+    }
+    return R;
+}
+
+// `m` entries of a segment starting at c (m <= 16, uniform over the group): fixed-point sums of
+// tab[r] GH[v] into acc and the relation dots into the block's bins
+__device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab,
+                                             unsigned long long* bins, int c, int m, int l,
+                                             int gl, const RowIn& R,
+                                             unsigned long long (&acc)[4]) {
+    const int my = l < m ? A.cent[c + l] : 0;
+    constexpr int UN = 8;
+    for (int j = 0; j < m; j += UN) {
+        int pk[UN];
+        float4 g[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            pk[u] = __shfl(my, gl + min(j + u, m - 1), 64);
+            g[u] = *reinterpret_cast<const float4*>(A.gh + int64_t(pk[u] >> 8) * F + 4 * l);
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            if (j + u >= m) break;             // uniform over the group
+            const float t = tab[pk[u] & 255];
+            acc[0] += to_fix(t * g[u].x);
+            acc[1] += to_fix(t * g[u].y);
+            acc[2] += to_fix(t * g[u].z);
+            acc[3] += to_fix(t * g[u].w);
+            const float d = group_sum<16>(R.h0[0] * g[u].x + R.h0[1] * g[u].y +
+                                          R.h0[2] * g[u].z + R.h0[3] * g[u].w);
+            if (l == 0) atomicAdd(bins + (pk[u] & 255), to_fix(d));      // LDS, exact
+        }
+    }
+}
+
+// the LayerNorm / relu / dropout backward of row u from its sums; G0 row to HBM, row terms
+__device__ __forceinline__ void row_bwd(const GathArgs& A, int u, int l, const RowIn& R,
+                                        const float (&lw)[4], const unsigned long long (&acc)[4],
+                                        float (&sga)[4], float (&sgy)[4], float (&sgyx)[4]) {
+    float gy[4], gx[4], p1 = 0.f, p2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        gy[i] = R.yv[i] > 0.f ? from_fix(acc[i]) * R.mk[i] : 0.f;
+        gx[i] = gy[i] * lw[i];
+        p1 += gx[i];
+        p2 += gx[i] * R.xh[i];
+    }
+    const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
+    float ga[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ga[i] = R.rstd * (gx[i] - m1 - R.xh[i] * m2);
+        sga[i] += ga[i];
+        sgy[i] += gy[i];
+        sgyx[i] += gy[i] * R.xh[i];
+    }
+    *reinterpret_cast<float4*>(A.g0 + int64_t(u) * F + 4 * l) =
+        make_float4(R.iv * ga[0], R.iv * ga[1], R.iv * ga[2], R.iv * ga[3]);
+}
 
 __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     __shared__ unsigned long long bins[F];
+    __shared__ unsigned long long lgh[F];
     __shared__ float tab[F];
     __shared__ float rt[3][16][F];
     if (threadIdx.x < F) {
@@ -695,63 +780,41 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     }
     __syncthreads();
     const int n = A.sizes[A.hop];
-    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
     const float4 lw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
     const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
     float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
+    // ---- rows with <= kShort edges: one group each
     for (int u = blockIdx.x * 16 + grp; u < n; u += gridDim.x * 16) {
-        const int c0 = A.cptr[u], c1 = A.cptr[u + 1];
-        const float4 a4 = *reinterpret_cast<const float4*>(A.a + int64_t(u) * F + 4 * l);
-        const float2 st = reinterpret_cast<const float2*>(A.stats)[u];
-        const float iv = A.inv[u];
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        float mk[4], xh[4], yv[4], h0[4];
-        drop_factors(key, A.drop, u, l, mk);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            xh[i] = (av[i] - st.x) * st.y;
-            yv[i] = fmaf(xh[i], lw[i], lb[i]);
-            h0[i] = fmaxf(yv[i], 0.f) * mk[i];
-        }
+        const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
+        if (m > kShort) continue;              // a hub: the workgroup pass below
+        const RowIn R = row_in(A, key, u, l, lw, lb);
         unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        for (int j = c0; j < c1; j += 2) {               // two entries in flight
-            const bool two = j + 1 < c1;                 // uniform over the group
-            const int pk0 = A.cent[j], pk1 = two ? A.cent[j + 1] : pk0;
-            const float4 g0 = *reinterpret_cast<const float4*>(A.gh + int64_t(pk0 >> 8) * F + 4 * l);
-            const float4 g1 = *reinterpret_cast<const float4*>(A.gh + int64_t(pk1 >> 8) * F + 4 * l);
-            const float t0 = tab[pk0 & 255], t1 = two ? tab[pk1 & 255] : 0.f;
-            acc[0] += to_fix(t0 * g0.x) + to_fix(t1 * g1.x);
-            acc[1] += to_fix(t0 * g0.y) + to_fix(t1 * g1.y);
-            acc[2] += to_fix(t0 * g0.z) + to_fix(t1 * g1.z);
-            acc[3] += to_fix(t0 * g0.w) + to_fix(t1 * g1.w);
-            const float d0 = group_sum<16>(h0[0] * g0.x + h0[1] * g0.y + h0[2] * g0.z + h0[3] * g0.w);
-            const float d1 = group_sum<16>(h0[0] * g1.x + h0[1] * g1.y + h0[2] * g1.z + h0[3] * g1.w);
-            if (l == 0) {
-                atomicAdd(bins + (pk0 & 255), to_fix(d0));          // LDS, integer: exact
-                if (two) atomicAdd(bins + (pk1 & 255), to_fix(d1));
-            }
-        }
-        float gy[4], gx[4], p1 = 0.f, p2 = 0.f;
+        gather_chunk(A, tab, bins, c0, m, l, gl, R, acc);
+        row_bwd(A, u, l, R, lw, acc, sga, sgy, sgyx);
+    }
+    // ---- hub rows: a workgroup each, 16-entry chunks over the groups
+    const int n_long = A.clong[0];
+    for (int li = blockIdx.x; li < n_long; li += gridDim.x) {
+        const int u = A.clong[1 + li];
+        const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
+        const RowIn R = row_in(A, key, u, l, lw, lb);
+        if (threadIdx.x < F) lgh[threadIdx.x] = 0ull;
+        __syncthreads();
+        unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
+        for (int k = grp; 16 * k < m; k += 16)
+            gather_chunk(A, tab, bins, c0 + 16 * k, min(16, m - 16 * k), l, gl, R, acc);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            gy[i] = yv[i] > 0.f ? from_fix(acc[i]) * mk[i] : 0.f;
-            gx[i] = gy[i] * lw[i];
-            p1 += gx[i];
-            p2 += gx[i] * xh[i];
+        for (int i = 0; i < 4; ++i) atomicAdd(lgh + 4 * l + i, acc[i]);   // LDS, exact
+        __syncthreads();
+        if (grp == 0) {
+            const unsigned long long tot[4] = {lgh[4 * l], lgh[4 * l + 1], lgh[4 * l + 2],
+                                               lgh[4 * l + 3]};
+            row_bwd(A, u, l, R, lw, tot, sga, sgy, sgyx);
         }
-        const float m1 = group_sum<16>(p1) * (1.f / F), m2 = group_sum<16>(p2) * (1.f / F);
-        float ga[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ga[i] = st.y * (gx[i] - m1 - xh[i] * m2);
-            sga[i] += ga[i];
-            sgy[i] += gy[i];
-            sgyx[i] += gy[i] * xh[i];
-        }
-        *reinterpret_cast<float4*>(A.g0 + int64_t(u) * F + 4 * l) =
-            make_float4(iv * ga[0], iv * ga[1], iv * ga[2], iv * ga[3]);
+        __syncthreads();
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1229,7 +1292,7 @@ bool regnn_nsm2_covers(const regnn_nsm_params* p) {
 int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     const int T = p->n_types, K = p->k_in, C = p->n_classes;
     const bool rs = p->rel_slots != 0;
-    if (!w->p0 || !w->gh1 || !w->csc_ptr0 || !w->csc_ent0 || !w->xs[1] || !w->a[0] ||
+    if (!w->p0 || !w->gh1 || !w->csc_ptr0 || !w->csc_ent0 || !w->csc_long0 || !w->xs[1] || !w->a[0] ||
         !w->stats[0] || !w->ga[0])
         return REGNN_EINVAL;
     const regnn_nsm_adam* ad = w->adam;
@@ -1296,7 +1359,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     // 3. layer 1's transposed aggregation (a gather), layer 0's LayerNorm backward
     {
         GathArgs G{};
-        G.sizes = w->sizes; G.hop = 1; G.cptr = w->csc_ptr0; G.cent = w->csc_ent0; G.gh = w->gh1;
+        G.sizes = w->sizes; G.hop = 1; G.cptr = w->csc_ptr0; G.cent = w->csc_ent0;
+        G.clong = w->csc_long0; G.gh = w->gh1;
         G.a = w->a[0]; G.stats = w->stats[0]; G.inv = w->blk_inv[1];
         G.ln_w = p->ln_w[0]; G.ln_b = p->ln_b[0]; G.state = w->state; G.drop = drop;
         G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1]; G.alpha = p->alpha;

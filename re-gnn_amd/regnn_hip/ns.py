@@ -149,7 +149,7 @@ class DeviceSampler:
         if ce > 32768:
             raise ValueError(f"the transposed index needs <= 32768 block edges, got {ce}")
         z = lambda n: torch.zeros(n, dtype=torch.int32, device=self.device)  # noqa: E731
-        self.csc[hop] = (z(ce), z(ce + 1), z(ce))
+        self.csc[hop] = (z(ce), z(ce + 1), z(ce), z(ce + 1))
         return self.csc[hop]
 
     # -- the per-step device work ------------------------------------------------------------
@@ -177,7 +177,7 @@ class DeviceSampler:
                      if self.edge_meta[h] is not None else (None, None, None)),
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
-                     else (None, None, None)),
+                     else (None, None, None, None)),
                    L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
 
@@ -254,7 +254,7 @@ class _NsmWork(ctypes.Structure):
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
-                ("csc_ptr0", _P), ("csc_ent0", _P)]
+                ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P)]
 
 
 class _NsmAdam(ctypes.Structure):
@@ -427,8 +427,8 @@ class FusedStep:
         if self.two_layer:
             W.p0 = ptr(z(caps[1], 64))
             W.gh1 = ptr(z(caps[0], 64))
-            _, cptr, cent = sampler.csc[0] or sampler.enable_csc(0)
-            W.csc_ptr0, W.csc_ent0 = ptr(cptr), ptr(cent)
+            _, cptr, cent, clong = sampler.csc[0] or sampler.enable_csc(0)
+            W.csc_ptr0, W.csc_ent0, W.csc_long0 = ptr(cptr), ptr(cent), ptr(clong)
         self.adam = None
         P.n_edge_types = int(sampler.num_edge_types)
         P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))

@@ -628,7 +628,7 @@ def test_block_transposed_index():
     rg = RelGraph(src, dst, N, DEV)
     ds = DeviceSampler(rg, [12, 5], 150, etype=torch.from_numpy(rng.integers(0, 7, E)),
                        ntype=torch.from_numpy(rng.integers(0, 4, N)), num_edge_types=7)
-    _, cptr, cent = ds.enable_csc(0)
+    _, cptr, cent, clong = ds.enable_csc(0)
     ds.set_seed(5, 0, 1)
     ds.set_targets(torch.from_numpy(rng.permutation(N)[:150]).to(DEV))
     ds.run_hops()
@@ -648,3 +648,6 @@ def test_block_transposed_index():
         want[idx[bp]].append((int(row[bp]) << 8) | int(rel[bp]))
     for u in range(n_src):
         assert sorted(ce[cp[u]:cp[u + 1]].tolist()) == sorted(want[u]), u
+    cl = clong.cpu().numpy()
+    longs = np.nonzero(np.diff(cp) > 16)[0]
+    assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
