@@ -575,7 +575,13 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * [cap_e] (scratch), csc_ptr [cap_e + 1] (source i's edges are csc_ent[csc_ptr[i] ..
  * csc_ptr[i + 1]) over the n_{hop+1} sources), csc_ent [cap_e] = target row << 8 | relation
  * (the order inside a segment is unspecified), csc_long [cap_e + 1] = the number of sources
- * with more than 16 edges, then their ids ascending (one more launch; cap_e <= 32768). */
+ * with more than 16 edges, then their ids ascending (one more launch; cap_e <= 32768).
+ * strided = 1: the block in the fixed-stride layout instead of the CSR -- row i's edges at
+ * [i S, i S + cnt_i) (S = k + 1, cnt_i = scnt[i], sampled positions ascending), its self loop at
+ * i S + cnt_i, the other slots empty (blk_idx -1); blk_ptr is not written. Sampling and
+ * placement run as one launch (no row-offset scan): 5 launches with de-duplication (4 without
+ * the transposed index), 1 meta-only. sizes[8 + hop] must be zero on entry (regnn_ns_batch
+ * zeroes sizes[8 ..]); the hop adds its edges to it and to state[5]. */
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
@@ -584,7 +590,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
                  int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
-                 int32_t* csc_ent, int32_t* csc_long, hipStream_t stream);
+                 int32_t* csc_ent, int32_t* csc_long, int32_t strided, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -703,6 +709,8 @@ typedef struct regnn_nsm_work {
     const int32_t* csc_ptr0;  /* hop 0's transposed index (regnn_ns_hop csc_ptr / csc_ent / */
     const int32_t* csc_ent0;  /* csc_long) */
     const int32_t* csc_long0;
+    int32_t stride[REGNN_NSM_MAX_LAYERS];        /* per hop: 0 = CSR block, else its fixed stride */
+    const int32_t* blk_cnt[REGNN_NSM_MAX_LAYERS]; /* per hop (strided): sampled edges per row */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

@@ -109,6 +109,7 @@ ns_batch_kernel(const int64_t* __restrict__ perm, int64_t n_perm, int B, int ran
         }
         sizes[0] = int32_t(cnt);
     }
+    if (threadIdx.x < 8) sizes[8 + threadIdx.x] = 0;   // strided hops add their edges per block
     __syncthreads();
     for (int i = threadIdx.x; i < s_cnt; i += blockDim.x) n_id[i] = int32_t(perm[s_start + i]);
 }
@@ -162,6 +163,124 @@ ns_sample_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
         spos[o + rank] = b + slot;
     }
     if (lane == 0) scnt[i] = k;
+}
+
+// Strided layout (the fused engine's blocks): row i owns slots [i S, i S + S), S = k + 1 -- its
+// sampled edges in ascending position order, then its self loop at i S + cnt_i, the rest empty
+// (gsrc -2, blk_idx -1). A slot's position is known at sampling time, so the sampling wave also
+// writes what ns_rows_kernel + ns_place_kernel write in the CSR layout (no prefix scan): relation,
+// CSR position, target row, the dedup candidate (first-seen order over the slots = the CSR order
+// restricted to the edges); meta-only (lean): the source's type / table row instead. Edge counts
+// are added per block into sizes[8 + hop] (zeroed by ns_batch_kernel / set_targets) and state[5].
+constexpr int kNsStrWaves = 16;            // targets per block
+
+__global__ void __launch_bounds__(64 * kNsStrWaves)
+ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                         const uint8_t* __restrict__ etype, const int32_t* __restrict__ ntype,
+                         int num_edge_types, const int32_t* __restrict__ n_id,
+                         int32_t* __restrict__ sizes, int hop, int cap, int k,
+                         int64_t* __restrict__ state, uint64_t* __restrict__ g2l,
+                         uint64_t* __restrict__ first, int32_t* __restrict__ scnt,
+                         int32_t* __restrict__ gsrc, int32_t* __restrict__ blk_idx,
+                         uint8_t* __restrict__ blk_rel, int32_t* __restrict__ blk_pos,
+                         int32_t* __restrict__ blk_row, float* __restrict__ inv,
+                         const int64_t* __restrict__ local, int32_t* __restrict__ e_type,
+                         int64_t* __restrict__ e_off, int lean, int32_t* __restrict__ csc_cnt) {
+    __shared__ int wsum[kNsStrWaves];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * kNsStrWaves + wv;
+    const int n = sizes[hop];
+    const int S = k + 1;
+    const int64_t base = int64_t(i) * S;
+    if (csc_cnt && i < cap)                    // the transposed index's counters (resolve adds)
+        for (int q = lane; q < S; q += 64) csc_cnt[base + q] = 0;
+    int cnt = -1;                              // -1: no row (past the batch)
+    if (i < cap && i >= n) {
+        if (!lean)
+            for (int q = lane; q < S; q += 64) {
+                gsrc[base + q] = -2;
+                blk_idx[base + q] = -1;
+            }
+        if (lane == 0) {
+            scnt[i] = 0;
+            inv[i] = 1.f;
+        }
+    } else if (i < n) {
+        const uint32_t stamp = ns_stamp(state, hop);
+        const uint64_t seed = ns_hop_seed(state, hop);
+        const int t = n_id[i];
+        if (!lean && lane == 0) g2l[t] = (uint64_t(stamp) << 32) | uint32_t(i);
+        const int b = ptr[t], d = ptr[t + 1] - b;
+        cnt = d < k ? d : k;
+        int slot = lane < d ? lane : -1, rank = lane;  // deg <= k: every position, in order
+        if (d > k) {                               // Floyd (regnn_sample_fill's spec)
+            slot = -1;
+            int filled = 0;
+            for (int j = d - k; j < d; ++j) {
+                const uint32_t r = ns_hash(seed, uint64_t(t), uint64_t(j));
+                const int pos = int((uint64_t(r) * uint64_t(j + 1)) >> 32);
+                const bool seen = __any(slot == pos);
+                const int pick = seen ? j : pos;
+                if (lane == filled) slot = pick;
+                ++filled;
+            }
+            rank = 0;
+            for (int m = 0; m < k; ++m) {
+                const int other = __shfl(slot, m, 64);
+                rank += (lane < k && other < slot) ? 1 : 0;
+            }
+        }
+        if (lane < cnt) {
+            const int p = b + slot;
+            const int u = idx[p];
+            const int64_t bp = base + rank;
+            blk_rel[bp] = etype[p];
+            if (lean) {
+                e_type[bp] = ntype[u];
+                e_off[bp] = local[u];
+            } else {
+                gsrc[bp] = u;
+                blk_pos[bp] = p;
+                blk_row[bp] = i;
+                if (uint32_t(g2l[u] >> 32) != stamp)      // not (yet) known as a target: a
+                    atomicMin(reinterpret_cast<unsigned long long*>(first + u),   // candidate
+                              (unsigned long long)((uint64_t(~stamp) << 32) | uint32_t(bp)));
+            }
+        } else if (lane == cnt) {                  // the self loop closes the row
+            const int64_t bp = base + cnt;
+            const int tt = ntype[t];
+            blk_rel[bp] = uint8_t(num_edge_types + tt);
+            if (lean || e_type) {
+                e_type[bp] = tt;
+                e_off[bp] = local[t];
+            }
+            if (!lean) {
+                gsrc[bp] = -1;
+                blk_idx[bp] = i;
+                blk_pos[bp] = -1;
+                blk_row[bp] = i;
+            }
+        } else if (!lean && lane < S) {
+            gsrc[base + lane] = -2;
+            blk_idx[base + lane] = -1;
+        }
+        if (lane == 0) {
+            scnt[i] = cnt;
+            inv[i] = 1.f / float(cnt + 1);
+        }
+    }
+    if (lane == 0) wsum[wv] = cnt + 1;          // edges of the row, self loop included
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int e = 0;
+#pragma unroll
+        for (int q = 0; q < kNsStrWaves; ++q) e += wsum[q];
+        if (e) {
+            atomicAdd(sizes + 8 + hop, e);
+            atomicAdd(reinterpret_cast<unsigned long long*>(state + 5), (unsigned long long)e);
+        }
+        if (lean && blockIdx.x == 0) sizes[hop + 1] = n;
+    }
 }
 
 // row offsets (sampled count + the self loop), 1/in-count and the self-loop entries: one tile of
@@ -310,10 +429,10 @@ __global__ void __launch_bounds__(kBlock)
 ns_flags_kernel(const int32_t* __restrict__ gsrc, int32_t* __restrict__ sizes, int hop,
                 const int64_t* __restrict__ state, const uint64_t* __restrict__ g2l,
                 const uint64_t* __restrict__ first, uint8_t* __restrict__ flag,
-                int32_t* __restrict__ tiles, int n_tiles) {
+                int32_t* __restrict__ tiles, int n_tiles, int cap_strided) {
     __shared__ int lds[kBlock / 64 + 1];
     __shared__ bool last;
-    const int E = sizes[8 + hop];
+    const int E = cap_strided ? cap_strided : sizes[8 + hop];
     const uint32_t stamp = ns_stamp(state, hop);
     const int base = blockIdx.x * kNsTile + threadIdx.x * 4;
     int c = 0;
@@ -359,9 +478,9 @@ __global__ void __launch_bounds__(kBlock)
 ns_finish_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes, int hop,
                  const int64_t* __restrict__ state, const uint8_t* __restrict__ flag,
                  const int32_t* __restrict__ tiles, uint64_t* __restrict__ g2l,
-                 int32_t* __restrict__ n_id) {
+                 int32_t* __restrict__ n_id, int cap_strided) {
     __shared__ int lds[kBlock / 64 + 1];
-    const int E = sizes[8 + hop];
+    const int E = cap_strided ? cap_strided : sizes[8 + hop];
     const int n = sizes[hop];
     const uint32_t stamp = ns_stamp(state, hop);
     const int base = blockIdx.x * kNsTile + threadIdx.x * 4;
@@ -392,10 +511,11 @@ ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ 
                   const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx, int cap_e,
                   const int32_t* __restrict__ ntype, const int64_t* __restrict__ local,
                   int32_t* __restrict__ e_type, int64_t* __restrict__ e_off,
-                  int32_t* __restrict__ csc_cnt) {
+                  int32_t* __restrict__ csc_cnt, int strided) {
     const int bp = blockIdx.x * kBlock + threadIdx.x;
-    if (bp >= cap_e || bp >= sizes[8 + hop]) return;
+    if (bp >= cap_e || (!strided && bp >= sizes[8 + hop])) return;
     const int u = gsrc[bp];
+    if (u == -2) return;               // an empty slot of the strided layout
     int lid;
     if (u < 0) {                       // the self loop (written by ns_rows_kernel)
         lid = blk_idx[bp];
@@ -425,10 +545,10 @@ __global__ void __launch_bounds__(kCscThreads)
 ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ blk_idx,
               const int32_t* __restrict__ blk_row, const uint8_t* __restrict__ blk_rel,
               const int32_t* __restrict__ csc_cnt, int32_t* __restrict__ csc_ptr,
-              int32_t* __restrict__ csc_ent, int32_t* __restrict__ csc_long) {
+              int32_t* __restrict__ csc_ent, int32_t* __restrict__ csc_long, int cap_strided) {
     __shared__ int cur[kCscMax];
     __shared__ int lds[kCscThreads / 64 + 1];
-    const int n = sizes[hop + 1], E = sizes[8 + hop];
+    const int n = sizes[hop + 1], E = cap_strided ? cap_strided : sizes[8 + hop];
     constexpr int IT = 8;
     int carry = 0, lcarry = 0;
     for (int base = 0; base < n; base += kCscThreads * IT) {
@@ -462,6 +582,7 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
     __syncthreads();
     for (int bp = threadIdx.x; bp < E; bp += kCscThreads) {
         const int u = blk_idx[bp];
+        if (u < 0) continue;           // an empty slot of the strided layout
         const int slot = atomicAdd(cur + u, 1);
         csc_ent[slot] = (blk_row[bp] << 8) | int(blk_rel[bp]);
     }
@@ -542,7 +663,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* blk_ptr, int32_t* blk_idx, uint8_t* blk_rel, int32_t* blk_pos,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
                  int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
-                 int32_t* csc_ent, int32_t* csc_long, hipStream_t stream) {
+                 int32_t* csc_ent, int32_t* csc_long, int32_t strided, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !g2l || !first ||
         !samp || !spos || !scnt || !gsrc || !flag || !tiles || !status || !blk_ptr || !blk_idx ||
         !blk_rel || !blk_pos || !blk_row || !inv || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
@@ -559,6 +680,34 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
     const int n_tiles = int((cap_e + kNsTile - 1) / kNsTile);
     if (csc && cap_e > kCscMax) return REGNN_EUNSUPPORTED;
+    if (strided) {
+        // sampling + placement in one launch, no row-offset scan (the layout above)
+        hipLaunchKernelGGL(ns_sample_strided_kernel,
+                           dim3(unsigned((cap_dst + kNsStrWaves - 1) / kNsStrWaves)),
+                           dim3(64 * kNsStrWaves), 0, stream, ptr, idx, etype, ntype,
+                           num_edge_types, n_id, sizes, hop, cap_dst, k, state, g2l, first, scnt,
+                           gsrc, blk_idx, blk_rel, blk_pos, blk_row, inv, local, edge_type,
+                           edge_off, lean, csc_cnt);
+        REGNN_LAUNCH_CHECK();
+        if (lean) return REGNN_OK;
+        const int ce = int(cap_e);
+        hipLaunchKernelGGL(ns_flags_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes,
+                           hop, state, g2l, first, flag, tiles, n_tiles, ce);
+        REGNN_LAUNCH_CHECK();
+        hipLaunchKernelGGL(ns_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes,
+                           hop, state, flag, tiles, g2l, n_id, ce);
+        REGNN_LAUNCH_CHECK();
+        hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce, ntype,
+                           local, edge_type, edge_off, csc_cnt, 1);
+        REGNN_LAUNCH_CHECK();
+        if (csc) {
+            hipLaunchKernelGGL(ns_csc_kernel, dim3(1), dim3(kCscThreads), 0, stream, sizes, hop,
+                               blk_idx, blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent, csc_long, ce);
+            REGNN_LAUNCH_CHECK();
+        }
+        return REGNN_OK;
+    }
     hipLaunchKernelGGL(ns_sample_kernel, dim3((cap_dst + 3) / 4), dim3(kBlock), 0, stream, ptr,
                        idx, n_id, sizes, hop, cap_dst, k, state, g2l, samp, spos, scnt);
     REGNN_LAUNCH_CHECK();
@@ -575,18 +724,18 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     REGNN_LAUNCH_CHECK();
     if (lean) return REGNN_OK;         // no dedup, no n_id append, no local source ids
     hipLaunchKernelGGL(ns_flags_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes, hop,
-                       state, g2l, first, flag, tiles, n_tiles);
+                       state, g2l, first, flag, tiles, n_tiles, 0);
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes, hop,
-                       state, flag, tiles, g2l, n_id);
+                       state, flag, tiles, g2l, n_id, 0);
     REGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, int(cap_e), ntype, local,
-                       edge_type, edge_off, csc_cnt);
+                       edge_type, edge_off, csc_cnt, 0);
     REGNN_LAUNCH_CHECK();
     if (csc) {
         hipLaunchKernelGGL(ns_csc_kernel, dim3(1), dim3(kCscThreads), 0, stream, sizes, hop, blk_idx,
-                           blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent, csc_long);
+                           blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent, csc_long, 0);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

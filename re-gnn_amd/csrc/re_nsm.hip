@@ -1229,7 +1229,8 @@ __global__ void __launch_bounds__(kBlock) bwd0_rs_kernel(Bwd0Args A) {
 // and table row). 16 lanes per target row, lane-private relation bins -> one slab row per block.
 struct Rel0Args {
     const int32_t* sizes; int hop; int T;
-    const int32_t* ptr; const uint8_t* rel; const int32_t* edge_type; const int64_t* edge_off;
+    const int32_t* ptr; const int32_t* cnt; int stride;
+    const uint8_t* rel; const int32_t* edge_type; const int64_t* edge_off;
     Ptrs xt; const float* z; const float* beta; float* slab; int n_rel;
 };
 
@@ -1245,7 +1246,8 @@ __global__ void __launch_bounds__(kBlock) rel0_kernel(Rel0Args A) {
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
         const int v = base + sub;
         if (v >= n) continue;
-        const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+        int e0, e1;
+        row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
         for (int c0 = e0; c0 < e1; c0 += 16) {
             const int m = min(16, e1 - c0);
             int my_t = 0, my_r = 0;
@@ -1515,7 +1517,8 @@ int regnn_nsm_rel0(const regnn_nsm_params* p, const regnn_nsm_work* w, float* sl
     for (int t = 0; t < T; ++t) xt.p[t] = p->x_tab[t];
     Rel0Args R{};
     R.sizes = w->sizes; R.hop = h; R.T = T;
-    R.ptr = w->blk_ptr[h]; R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
+    R.ptr = w->blk_ptr[h]; R.cnt = w->blk_cnt[h]; R.stride = w->stride[h];
+    R.rel = w->blk_rel[h]; R.edge_type = w->edge_type;
     R.edge_off = w->edge_off; R.xt = xt; R.z = w->z; R.beta = w->beta;
     R.slab = slab; R.n_rel = p->n_rel[0];
     const size_t lds = size_t(p->n_rel[0]) * kBlock * sizeof(float);
@@ -1567,7 +1570,10 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     if (rs && (!w->u_self || !w->u_rel || p->n_edge_types < 0 || p->n_edge_types + T > p->n_rel[0]))
         return REGNN_EINVAL;
     if (regnn_nsm2_covers(p)) return regnn_nsm2_step(p, w, stream);
-    if (w->adam) return REGNN_EUNSUPPORTED;          // the fused optimizer: two-layer step only
+    // the fused optimizer and the strided blocks: two-layer step only
+    if (w->adam) return REGNN_EUNSUPPORTED;
+    for (int h = 0; h < L; ++h)
+        if (w->stride[h]) return REGNN_EUNSUPPORTED;
     const SlabLayout S = slab_layout(p, w->cap[0]);
     const Drop drop = make_drop(p->p_drop);
     Ptrs lin_w{}, lin_b{}, xt{}, rw{};

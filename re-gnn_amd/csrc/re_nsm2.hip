@@ -79,7 +79,7 @@ __device__ unsigned long long g_nsm2_phase[4][32][16];
 // a float4), B = column 16 w + c; D row 4 q + r, column 16 w + c.
 struct Agg0Args {
     const int32_t* sizes; int hop;
-    const int32_t* ptr; const uint8_t* rel; const float* inv;
+    const int32_t* ptr; const int32_t* cnt; int stride; const uint8_t* rel; const float* inv;
     const int32_t* edge_type; const int64_t* edge_off; Ptrs xt; int T;
     Ptrs lin_w; Ptrs lin_b;                // lins[t].weight [64][K] (row j, column k), bias [64]
     const float* rw; int n_rel; float alpha;
@@ -142,7 +142,8 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
 #pragma unroll
         for (int p = 0; p < VPL; ++p) xself[p] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (v < n) {
-            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            int e0, e1;
+            row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
             for (int c0 = e0; c0 < e1; c0 += 16) {
                 const int m = min(16, e1 - c0);
                 int my_t = 0, my_lo = 0;           // table rows < 2^31 (checked by the host)
@@ -341,7 +342,8 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
 //                      1 loss | 64*64 g W_1]
 struct HeadArgs {
     const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
-    const int32_t* ptr; const int32_t* idx; const uint8_t* rel; const float* inv;
+    const int32_t* ptr; const int32_t* cnt; int stride;
+    const int32_t* idx; const uint8_t* rel; const float* inv;
     const float* rw; int n_rel; float alpha;
     const float* h; const float* w1; const float* bias; const float* ln_w; const float* ln_b;
     const int64_t* state; Drop drop;
@@ -415,7 +417,8 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         if (act) {
-            const int e0 = A.ptr[v], e1 = A.ptr[v + 1];
+            int e0, e1;
+            row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
             for (int c0 = e0; c0 < e1; c0 += 16) {
                 const int m = min(16, e1 - c0);
                 const int my_u = l < m ? A.idx[c0 + l] : 0;
@@ -1295,6 +1298,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     if (!w->p0 || !w->gh1 || !w->csc_ptr0 || !w->csc_ent0 || !w->csc_long0 || !w->xs[1] || !w->a[0] ||
         !w->stats[0] || !w->ga[0])
         return REGNN_EINVAL;
+    for (int h = 0; h < 2; ++h)
+        if (w->stride[h] < 0 || (w->stride[h] && !w->blk_cnt[h])) return REGNN_EINVAL;
     const regnn_nsm_adam* ad = w->adam;
     if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step ||
                !ad->ticket))
@@ -1312,7 +1317,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         const int h = 1;
         Agg0Args A{};
         A.sizes = w->sizes; A.hop = h;
-        A.ptr = w->blk_ptr[h]; A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
+        A.ptr = w->blk_ptr[h]; A.cnt = w->blk_cnt[h]; A.stride = w->stride[h];
+        A.rel = w->blk_rel[h]; A.inv = w->blk_inv[h];
         A.edge_type = w->edge_type; A.edge_off = w->edge_off; A.xt = xt; A.T = T;
         A.lin_w = lin_w; A.lin_b = lin_b;
         A.rw = p->conv_rw[0]; A.n_rel = p->n_rel[0]; A.alpha = p->alpha;
@@ -1343,7 +1349,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     {
         HeadArgs H{};
         H.sizes = w->sizes; H.n_id = w->n_id; H.labels = w->labels;
-        H.ptr = w->blk_ptr[0]; H.idx = w->blk_idx[0]; H.rel = w->blk_rel[0]; H.inv = w->blk_inv[0];
+        H.ptr = w->blk_ptr[0]; H.cnt = w->blk_cnt[0]; H.stride = w->stride[0];
+        H.idx = w->blk_idx[0]; H.rel = w->blk_rel[0]; H.inv = w->blk_inv[0];
         H.rw = p->conv_rw[1]; H.n_rel = p->n_rel[1]; H.alpha = p->alpha;
         H.h = w->xs[1]; H.w1 = p->conv_w[1]; H.bias = p->conv_b[1];
         H.ln_w = p->ln_w[1]; H.ln_b = p->ln_b[1]; H.state = w->state; H.drop = drop;

@@ -77,6 +77,19 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// the edge range of a block's row v: CSR (stride 0) or the fixed-stride layout of regnn_ns_hop
+// strided (row v at v * stride, its cnt[v] sampled edges then its self loop)
+__device__ __forceinline__ void row_range(const int32_t* ptr, const int32_t* cnt, int stride,
+                                          int v, int& e0, int& e1) {
+    if (stride) {
+        e0 = v * stride;
+        e1 = e0 + cnt[v] + 1;
+    } else {
+        e0 = ptr[v];
+        e1 = ptr[v + 1];
+    }
+}
+
 inline Drop make_drop(float p) {
     Drop d{};
     d.on = p > 0.f;

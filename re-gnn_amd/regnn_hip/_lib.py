@@ -87,7 +87,7 @@ _SIG = {
     "regnn_sample_fill": ([P, P, P, I64, I32, U64, P, P, P, P], ctypes.c_int),
     "regnn_ns_batch": ([P, I64, I32, I32, I32, P, P, P, P, P], ctypes.c_int),
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
-                      P, P, P, P, P, P, I32, P, P, P, P, P], ctypes.c_int),
+                      P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),

@@ -127,7 +127,11 @@ class DeviceSampler:
             self.blocks.append(blk)
         self.local, self.edge_meta = None, [None] * len(self.sizes_k)
         self.meta_fresh = [False] * len(self.sizes_k)
-        self.csc = [None] * len(self.sizes_k)      # per hop: (cnt, ptr, ent) or None
+        self.csc = [None] * len(self.sizes_k)      # per hop: (cnt, ptr, ent, long) or None
+        # strided: every hop's block in the fixed-stride layout (row i at i (k + 1), regnn_ns_hop
+        # strided) -- the two-layer fused step's layout; False: the CSR layout the module path,
+        # exact_adjs and the PyG-style API read
+        self.strided = False
         # meta_only[h]: hop h writes only the edge meta its consumer reads (regnn_ns_hop
         # meta_only: no de-duplication, n_id not extended, sampled blk_idx unwritten)
         self.meta_only = [False] * len(self.sizes_k)
@@ -178,7 +182,7 @@ class DeviceSampler:
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
                      else (None, None, None, None)),
-                   L.stream())
+                   int(self.strided), L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
 
     def set_seed(self, base_seed, epoch, batch_idx):
@@ -198,6 +202,7 @@ class DeviceSampler:
             raise ValueError(f"{n} targets exceed the sampler's batch capacity {self.B}")
         self.n_id[:n].copy_(targets.to(torch.int32))
         self.sizes[0:1].fill_(n)
+        self.sizes[8:16].zero_()               # strided hops add their edge counts
 
     def model_blocks(self):
         """blocks in the model's layer order (outermost hop first, PyG adjs[::-1])."""
@@ -254,7 +259,8 @@ class _NsmWork(ctypes.Structure):
                 ("a", _P * _ML), ("stats", _P * _ML), ("ga", _P * _ML), ("edge_type", _P), ("edge_off", _P),
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
-                ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P)]
+                ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P),
+                ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML)]
 
 
 class _NsmAdam(ctypes.Structure):
@@ -306,6 +312,10 @@ def fused_unsupported(model, x_dict):
 # "auto": layer 0's relation-slot mode wherever the graph allows it; "off": the edge pass
 # (rel0) always (tests compare the two)
 REL_SLOTS = {"mode": "auto"}
+# "on": the two-layer fused step's sampler writes its blocks in the fixed-stride layout (no
+# row-offset scan, sampling and placement in one launch); "off": the CSR blocks (tests that
+# inspect them, and the comparison of the two)
+STRIDED = {"mode": "on"}
 # "on": a one-rank FlatAdam trainer runs Adam inside the two-layer step's last launch; "off":
 # the separate regnn_adam_flat launch (tests compare the two)
 FUSED_ADAM = {"mode": "on"}
@@ -429,6 +439,12 @@ class FusedStep:
             W.gh1 = ptr(z(caps[0], 64))
             _, cptr, cent, clong = sampler.csc[0] or sampler.enable_csc(0)
             W.csc_ptr0, W.csc_ent0, W.csc_long0 = ptr(cptr), ptr(cent), ptr(clong)
+            # the blocks in the fixed-stride layout: sampling and placement in one launch per hop
+            sampler.strided = STRIDED["mode"] != "off"
+            if sampler.strided:
+                for h, k in enumerate(sampler.sizes_k):
+                    W.stride[h] = k + 1
+                    W.blk_cnt[h] = ptr(sampler.hop_bufs[h]["scnt"])
         self.adam = None
         P.n_edge_types = int(sampler.num_edge_types)
         P.rel_slots = int(REL_SLOTS["mode"] != "off" and relation_slots_ok(sampler, T))

@@ -273,12 +273,13 @@ def test_ns_step_mag10_scale():
     model = d["model"]()
     model.train()
     from regnn_hip import ns
-    old_mode = ns.LEAN_LAST_HOP["mode"]
+    old_mode, old_str = ns.LEAN_LAST_HOP["mode"], ns.STRIDED["mode"]
     ns.LEAN_LAST_HOP["mode"] = "off"             # this test inspects the outermost n_id
+    ns.STRIDED["mode"] = "off"                   # and the CSR blocks
     try:
         tr, _ = _setup_trainer(d, model, batch=512, sizes=(25, 20), seed=123)
     finally:
-        ns.LEAN_LAST_HOP["mode"] = old_mode
+        ns.LEAN_LAST_HOP["mode"], ns.STRIDED["mode"] = old_mode, old_str
     tr.step()
     torch.cuda.synchronize()
     assert np.isfinite(float(tr.loss))
@@ -488,12 +489,14 @@ def test_meta_only_last_hop_matches_full_hop():
     outs = []
     for mode in ("off", "on"):
         ns.LEAN_LAST_HOP["mode"] = mode
+        ns.STRIDED["mode"] = "off"               # the CSR blocks are compared
         try:
             model = d["model"](2)
             model.train()
             tr, _ = _setup_trainer(d, model, batch=80, sizes=(6, 5))
         finally:
             ns.LEAN_LAST_HOP["mode"] = "on"
+            ns.STRIDED["mode"] = "on"
         assert tr.fused is not None
         tr._forward_backward()
         torch.cuda.synchronize()
@@ -651,3 +654,57 @@ def test_block_transposed_index():
     cl = clong.cpu().numpy()
     longs = np.nonzero(np.diff(cp) > 16)[0]
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
+
+
+def test_strided_blocks_match_csr(monkeypatch):
+    """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
+    launch) against the CSR layout on the same batches: the same n_id, sizes, per-row edges
+    (local source, relation, CSR position, target row; the meta-only hop's source type / table
+    row), 1/in-counts and transposed index; and the two-layer fused step's loss and gradients
+    bitwise equal over both layouts."""
+    from regnn_hip import ns
+    d = _mag(0.003, seed=10, F=128, hidden=64, classes=19, dropout=0.5)
+    trs, models = [], []
+    for mode in ("off", "on"):
+        monkeypatch.setitem(ns.STRIDED, "mode", mode)
+        m = d["model"](6)
+        m.train()
+        tr, _ = _setup_trainer(d, m, batch=120, sizes=(9, 7))
+        assert tr.sampler.strided == (mode == "on")
+        trs.append(tr)
+        models.append(m)
+    a, b = trs                                   # CSR, strided
+    for _ in range(2):
+        a._forward_backward()
+        b._forward_backward()
+        torch.cuda.synchronize()
+        sa, sb = a.sampler, b.sampler
+        assert torch.equal(sa.sizes, sb.sizes)
+        n1 = int(sa.sizes[1])
+        assert torch.equal(sa.n_id[:n1], sb.n_id[:n1])
+        for h, k in enumerate(sa.sizes_k):
+            S, n_dst = k + 1, int(sa.sizes[h])
+            ba, bb = sa.blocks[h], sb.blocks[h]
+            ptr = ba.csr_ptr[:n_dst + 1].cpu().numpy()
+            cnt = sb.hop_bufs[h]["scnt"][:n_dst].cpu().numpy()
+            assert np.array_equal(np.diff(ptr), cnt + 1)
+            assert torch.equal(ba.inv[:n_dst], bb.inv[:n_dst])
+            pos = np.concatenate([np.arange(i * S, i * S + cnt[i] + 1) for i in range(n_dst)])
+            pos_t = torch.from_numpy(pos).to(DEV)
+            E = int(ptr[-1])
+            assert torch.equal(ba.rel[:E], bb.rel[pos_t])
+            if sa.meta_only[h]:
+                for ma, mb in zip(sa.edge_meta[h], sb.edge_meta[h]):
+                    assert torch.equal(ma[:E], mb[pos_t])
+            else:
+                for xa, xb in ((ba.csr_idx, bb.csr_idx), (ba.pos, bb.pos), (ba.row, bb.row)):
+                    assert torch.equal(xa[:E], xb[pos_t])
+        ca, cb = sa.csc[0], sb.csc[0]
+        n0 = int(sa.sizes[1])
+        assert torch.equal(ca[1][:n0 + 1], cb[1][:n0 + 1])          # csc_ptr
+        assert torch.equal(ca[3][:1], cb[3][:1])                      # hub count
+        E0 = int(sa.sizes[8])
+        assert torch.equal(torch.sort(ca[2][:E0])[0], torch.sort(cb[2][:E0])[0])
+        assert float(a.loss) == float(b.loss)
+        for pa, pb in zip(models[0].parameters(), models[1].parameters()):
+            assert torch.equal(pa.grad, pb.grad)

@@ -116,13 +116,20 @@ def test_regnn_fused_step_vs_reference(monkeypatch, name, lean):
     assert ds.n_id[:n_chk].cpu().numpy().tolist() == d["n_id"][:n_chk].tolist()
     if lean == "off":
         assert n_chk == d["n_id"].size
-        # the sampler's per-edge source type / table row of the last hop (layer 0's block)
+        # the sampler's per-edge source type / table row of the last hop (layer 0's block; in
+        # the strided layout, its non-empty slots)
         et, eo = ds.edge_meta[L_ - 1]
         blk = ds.blocks[L_ - 1]
-        E = int(ds.sizes[8 + L_ - 1])
-        g = ds.n_id.long()[blk.csr_idx[:E].long()]
-        assert torch.equal(et[:E].long(), nt.to(DEV).long()[g])
-        assert torch.equal(eo[:E], loc.to(DEV).long()[g])
+        if ds.strided:
+            ix = blk.csr_idx.long()
+            keep = ix >= 0
+        else:
+            E = int(ds.sizes[8 + L_ - 1])
+            ix = blk.csr_idx[:E].long()
+            keep = torch.ones_like(ix, dtype=torch.bool)
+        g = ds.n_id.long()[ix[keep]]
+        assert torch.equal(et[:ix.numel()][keep].long(), nt.to(DEV).long()[g])
+        assert torch.equal(eo[:ix.numel()][keep], loc.to(DEV).long()[g])
     fs.step()
     torch.cuda.synchronize()
     _check("loss", loss, d["loss"])
