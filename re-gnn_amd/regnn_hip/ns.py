@@ -163,9 +163,11 @@ class DeviceSampler:
                L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes),
                None if self.stamp_src is None else L.ptr(self.stamp_src), L.stream())
 
-    def run_hops(self, meta_only=True):
+    def run_hops(self, meta_only=True, strided=None):
         """every hop of the current batch; meta_only=False runs hops marked meta_only in full
-        (a consumer that reads n_id / the local source ids, e.g. the module path)."""
+        (a consumer that reads n_id / the local source ids, e.g. the module path); strided=False
+        writes the CSR blocks whatever self.strided says (None: self.strided)."""
+        strided = self.strided if strided is None else bool(strided)
         rg = self.rg
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
@@ -182,7 +184,7 @@ class DeviceSampler:
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
                      else (None, None, None, None)),
-                   int(self.strided), L.stream())
+                   int(strided), L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
 
     def set_seed(self, base_seed, epoch, batch_idx):
@@ -451,7 +453,8 @@ class FusedStep:
         if P.rel_slots:
             W.u_self = ptr(z(n0, K))
             W.u_rel = ptr(torch.full((n0, T + 1), -1, dtype=torch.int32, device=dev))
-        W.slab = ptr(z(_slab_floats(P, caps[0])))
+        self.slab = z(_slab_floats(P, caps[0]))
+        W.slab = ptr(self.slab)
         self.model, self.sampler, self.n_layers = model, sampler, nl
 
     def attach_adam(self, opt, grad_flat):
@@ -676,7 +679,8 @@ class NSTrainer:
         s = self.slots[0]
         self._trained = 0
         s.batch_from_perm(self.perm, self.rank, self.world)
-        s.run_hops(meta_only=False)            # the module path reads n_id and local ids
+        # the module path reads n_id, the local ids and the CSR blocks
+        s.run_hops(meta_only=False, strided=False)
         if self._blocks_ok:
             B = s.B
             n_id = s.n_id.to(torch.int64)

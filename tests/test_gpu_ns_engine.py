@@ -627,7 +627,7 @@ def test_block_transposed_index():
     rng = np.random.default_rng(12)
     N, E = 5000, 80000
     dst = np.minimum((rng.pareto(1.1, E) * 4).astype(np.int64), N - 1)
-    src = np.where(rng.random(E) < 0.3, rng.integers(0, 40, E), rng.integers(0, N, E))
+    src = np.where(rng.random(E) < 0.6, rng.integers(0, 3, E), rng.integers(0, N, E))  # 3 hubs
     rg = RelGraph(src, dst, N, DEV)
     ds = DeviceSampler(rg, [12, 5], 150, etype=torch.from_numpy(rng.integers(0, 7, E)),
                        ntype=torch.from_numpy(rng.integers(0, 4, N)), num_edge_types=7)
