@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 30). */
+/* ABI version (bumped on any signature change or addition; currently 31). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -604,6 +604,29 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
                       const float* rel_table, const float* out_scale, const float* g,
                       const float* x, float* gx, float* slab, int32_t n_rel, int64_t n_rows,
                       int32_t F, hipStream_t stream);
+
+/* Typed aggregation of raw input rows over a sampled block (layer 0 of the NS REGNN at any hidden
+ * width; mag/regnn_ns.py:300-326 group_input + mag/regnn_layers.py:101-148, replacing the
+ * reference's per-type Linear over every sampled node and x_src @ W before propagate):
+ *   S[v][t][:] = sum_{e in row v, ntype[n_id[idx_e]] = t} rel_table[rel_e] tables[t][local[n_id[idx_e]]][:]
+ *   wsum[v][t] = sum over the same edges of rel_table[rel_e]
+ * for v < n_rows (rows with ptr[v] == ptr[v + 1] get zeros). The caller projects
+ * a = inv (S W_c + wsum b_c) + bias with W_c[t] = W_t^T W_0, b_c[t] = b_t W_0 (linearity).
+ * K in {64, 128} fp32 (rows 16-byte aligned), 1 <= n_types <= 8, tables[t] non-null. */
+int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                       const float* rel_table, const int32_t* n_id, const int32_t* ntype,
+                       const int64_t* local, const float* const* tables, int32_t n_types,
+                       int32_t K, int64_t n_rows, float* S, float* wsum, hipStream_t stream);
+
+/* Relation-table gradient of regnn_ns_typed_agg: slab[b][r] = block b's partial of
+ * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (LDS float atomics: the
+ * order within a block is run-dependent, as regnn_ns_spmm_bwd). Launches slab_rows blocks; reduce
+ * the slab with regnn_rel_reduce. n_rel <= 256. */
+int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const int32_t* n_id, const int32_t* ntype, const int64_t* local,
+                           const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
+                           const float* gS, const float* gw, float* slab, int32_t n_rel,
+                           int32_t slab_rows, hipStream_t stream);
 
 
 /* ---------------------------------------------------------------------------------------

@@ -922,6 +922,78 @@ attn_dots_bwd_kernel(const float* __restrict__ ft, const float* __restrict__ al,
     }
 }
 
+// The same backward for rows whose F / 4 float4 columns divide the block (D % 4 == 0, so a float4
+// lies inside one head): thread = (row group g, float4 column cv); the block's RG = 256 / CPL row
+// groups stride over its rows, each thread keeping UN rows' ft loads in flight; gel / ger are read
+// once per (row, head) by the lanes of that head (broadcast within the wave). The row-group partial
+// sums are combined in LDS in a fixed order, one slab row per block.
+template <int UN>
+__global__ void __launch_bounds__(kBlock)
+attn_dots_bwd_vec_kernel(const float4* __restrict__ ft, const float4* __restrict__ al,
+                         const float4* __restrict__ ar, const float* __restrict__ gel,
+                         const float* __restrict__ ger, int64_t N, int H, int D, int CPL,
+                         int64_t rpb, float4* __restrict__ gft, float* __restrict__ slab) {
+    extern __shared__ float4 part[];       // [RG][2 CPL]
+    const int RG = kBlock / CPL;
+    const int g = threadIdx.x / CPL, cv = threadIdx.x - g * CPL;
+    const int h = (4 * cv) / D;
+    const int64_t r0 = (int64_t)blockIdx.x * rpb;
+    const int64_t r1 = min(N, r0 + rpb);
+    const float4 a_l = al[cv], a_r = ar[cv];
+    float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), sr = sl;
+    int64_t n = r0 + g;
+    for (; n + (UN - 1) * RG < r1; n += UN * RG) {
+        float4 x[UN];
+        float gl[UN], gr[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int64_t m = n + (int64_t)u * RG;
+            x[u] = ft[m * CPL + cv];
+            gl[u] = gel[m * H + h];
+            gr[u] = ger[m * H + h];
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int64_t m = n + (int64_t)u * RG;
+            float4 o;
+            o.x = fmaf(gl[u], a_l.x, gr[u] * a_r.x);
+            o.y = fmaf(gl[u], a_l.y, gr[u] * a_r.y);
+            o.z = fmaf(gl[u], a_l.z, gr[u] * a_r.z);
+            o.w = fmaf(gl[u], a_l.w, gr[u] * a_r.w);
+            gft[m * CPL + cv] = o;
+            sl.x = fmaf(gl[u], x[u].x, sl.x); sl.y = fmaf(gl[u], x[u].y, sl.y);
+            sl.z = fmaf(gl[u], x[u].z, sl.z); sl.w = fmaf(gl[u], x[u].w, sl.w);
+            sr.x = fmaf(gr[u], x[u].x, sr.x); sr.y = fmaf(gr[u], x[u].y, sr.y);
+            sr.z = fmaf(gr[u], x[u].z, sr.z); sr.w = fmaf(gr[u], x[u].w, sr.w);
+        }
+    }
+    for (; n < r1; n += RG) {
+        const float4 x = ft[n * CPL + cv];
+        const float gl = gel[n * H + h], gr = ger[n * H + h];
+        float4 o;
+        o.x = fmaf(gl, a_l.x, gr * a_r.x);
+        o.y = fmaf(gl, a_l.y, gr * a_r.y);
+        o.z = fmaf(gl, a_l.z, gr * a_r.z);
+        o.w = fmaf(gl, a_l.w, gr * a_r.w);
+        gft[n * CPL + cv] = o;
+        sl.x = fmaf(gl, x.x, sl.x); sl.y = fmaf(gl, x.y, sl.y);
+        sl.z = fmaf(gl, x.z, sl.z); sl.w = fmaf(gl, x.w, sl.w);
+        sr.x = fmaf(gr, x.x, sr.x); sr.y = fmaf(gr, x.y, sr.y);
+        sr.z = fmaf(gr, x.z, sr.z); sr.w = fmaf(gr, x.w, sr.w);
+    }
+    part[g * 2 * CPL + cv] = sl;
+    part[g * 2 * CPL + CPL + cv] = sr;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * CPL; i += kBlock) {
+        float4 s = part[i];
+        for (int k = 1; k < RG; ++k) {
+            const float4 p = part[k * 2 * CPL + i];
+            s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+        }
+        reinterpret_cast<float4*>(slab + (int64_t)blockIdx.x * 8 * CPL)[i] = s;
+    }
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -1123,8 +1195,22 @@ int regnn_attn_dots_bwd(const float* ft, const float* attn_l, const float* attn_
         D <= 0 || slab_rows <= 0)
         return REGNN_EINVAL;
     const int64_t rpb = N > 0 ? (N + slab_rows - 1) / slab_rows : 1;
-    hipLaunchKernelGGL(attn_dots_bwd_kernel, dim3(slab_rows), dim3(kBlock), 0, stream, ft,
-                       attn_l, attn_r, gel, ger, N, H, D, rpb, gft, slab);
+    const int F = H * D, CPL = F / 4;
+    const bool vec = D % 4 == 0 && CPL <= kBlock && kBlock % CPL == 0 &&
+                     (reinterpret_cast<uintptr_t>(ft) | reinterpret_cast<uintptr_t>(gft) |
+                      reinterpret_cast<uintptr_t>(attn_l) | reinterpret_cast<uintptr_t>(attn_r) |
+                      reinterpret_cast<uintptr_t>(slab)) % 16 == 0;
+    if (vec) {
+        hipLaunchKernelGGL(attn_dots_bwd_vec_kernel<4>, dim3(slab_rows), dim3(kBlock),
+                           size_t(kBlock / CPL) * 2 * CPL * sizeof(float4), stream,
+                           reinterpret_cast<const float4*>(ft),
+                           reinterpret_cast<const float4*>(attn_l),
+                           reinterpret_cast<const float4*>(attn_r), gel, ger, N, H, D, CPL, rpb,
+                           reinterpret_cast<float4*>(gft), slab);
+    } else {
+        hipLaunchKernelGGL(attn_dots_bwd_kernel, dim3(slab_rows), dim3(kBlock), 0, stream, ft,
+                           attn_l, attn_r, gel, ger, N, H, D, rpb, gft, slab);
+    }
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

@@ -1,0 +1,256 @@
+// Typed block aggregation of raw input rows: layer 0 of the neighbour-sampled REGNN at any hidden
+// width (mag/regnn_ns.py:300-346 with the reference default hidden 512, mag/regnn_ns.py:43).
+//
+// The reference projects every sampled node's raw row through its type's Linear (group_input,
+// mag/regnn_ns.py:300-326: ~280 k rows x 128 -> hidden per step at fan-out [25, 20]) and then
+// through the first conv's weight (mag/regnn_layers.py:102) before the mean aggregation. Both
+// maps are linear, so for target row v of layer 0's block
+//     a_v = inv_v sum_e tab[r_e] (x_e W_t(e)^T + b_t(e)) W_0 + bias
+//         = inv_v sum_t (S_vt W_t^T + w_vt b_t) W_0 + bias,
+//     S_vt = sum_{e in v, type(src_e) = t} tab[r_e] x_src_e,   w_vt = sum_{same e} tab[r_e],
+// and the projections run over the ~13 k target rows only. This file forms S and w from the raw
+// input tables (the gather: each sampled edge reads its source's raw K-float row once) and, in
+// the backward, the relation-table gradient
+//     d tab[r] = sum_{e: r_e = r} (<x_src_e, gS_v,t(e)> + gw_v,t(e)).
+// The GEMMs (S W_c, its two backward products) stay on hipBLASLt.
+#include "regnn_common.h"
+
+namespace regnn {
+namespace nsagg {
+
+constexpr int kMT = 8;                     // node types (REGNN_NSM_MAX_TYPES)
+
+struct Tabs {
+    const float* p[kMT];
+};
+
+template <int N>
+__device__ __forceinline__ const float* pick_tab(const Tabs& t, int i) {
+    const float* r = t.p[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+        if (i == k) r = t.p[k];
+    return r;
+}
+
+// one edge's metadata, formed by one lane of the row's group (its four dependent loads run in
+// parallel over the row's edges) and broadcast to the group: source type, source row in its
+// type's table, tab[r_e] (tab may be null), relation id
+template <int LPR>
+__device__ __forceinline__ void edge_meta(const int32_t* idx, const uint8_t* rel, const float* tab,
+                                          const int32_t* n_id, const int32_t* ntype,
+                                          const int64_t* local, int e, int e1, int& t,
+                                          int64_t& row, float& w, int& r) {
+    t = 0; row = 0; w = 0.f; r = 0;
+    if (e < e1) {
+        const int u = idx[e];
+        r = rel[e];
+        const int g = n_id[u];
+        t = ntype[g];
+        row = local[g];
+        w = tab ? tab[r] : 0.f;
+    }
+}
+
+// S [n_rows][T][K], w [n_rows][T]. LPR = K / 4 lanes per row, 64 / LPR rows per wave.
+template <int K, int NT>
+__global__ void __launch_bounds__(kBlock)
+typed_agg_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                 const uint8_t* __restrict__ rel, const float* __restrict__ tab,
+                 const int32_t* __restrict__ n_id, const int32_t* __restrict__ ntype,
+                 const int64_t* __restrict__ local, Tabs xt, int T, int64_t n_rows,
+                 float* __restrict__ S, float* __restrict__ wsum) {
+    constexpr int LPR = K / 4;
+    constexpr int RPW = 64 / LPR;
+    constexpr int UN = 4;
+    const int lane = threadIdx.x & 63, l = lane % LPR, gl = lane - l;
+    const int64_t rows_per_block = int64_t(kBlock / 64) * RPW;
+    for (int64_t v0 = int64_t(blockIdx.x) * rows_per_block; v0 < n_rows;
+         v0 += int64_t(gridDim.x) * rows_per_block) {
+        const int64_t v = v0 + (threadIdx.x >> 6) * RPW + lane / LPR;
+        if (v >= n_rows) continue;
+        float4 acc[NT];
+        float ws[NT];
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ws[k] = 0.f;
+        }
+        const int e0 = ptr[v], e1 = ptr[v + 1];
+        for (int c = e0; c < e1; c += LPR) {
+            int mt, mr;
+            int64_t mrow;
+            float mw;
+            edge_meta<LPR>(idx, rel, tab, n_id, ntype, local, c + l, e1, mt, mrow, mw, mr);
+            const int m = min(LPR, e1 - c);
+            for (int j = 0; j < m; j += UN) {
+                float4 x[UN];
+                int tt[UN];
+                float ww[UN];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    const int src = gl + min(j + u, m - 1);
+                    tt[u] = __shfl(mt, src, 64);
+                    const int64_t rw = __shfl(mrow, src, 64);
+                    ww[u] = j + u < m ? __shfl(mw, src, 64) : 0.f;
+                    x[u] = reinterpret_cast<const float4*>(pick_tab<NT>(xt, tt[u]))[rw * LPR + l];
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+#pragma unroll
+                    for (int k = 0; k < NT; ++k) {
+                        if (tt[u] == k) {
+                            acc[k].x = fmaf(ww[u], x[u].x, acc[k].x);
+                            acc[k].y = fmaf(ww[u], x[u].y, acc[k].y);
+                            acc[k].z = fmaf(ww[u], x[u].z, acc[k].z);
+                            acc[k].w = fmaf(ww[u], x[u].w, acc[k].w);
+                            ws[k] += ww[u];
+                        }
+                    }
+                }
+            }
+        }
+        float4* srow = reinterpret_cast<float4*>(S + v * int64_t(T) * K);
+#pragma unroll
+        for (int k = 0; k < NT; ++k)
+            if (k < T) srow[k * LPR + l] = acc[k];
+        if (l < T) {
+            float s = ws[0];
+#pragma unroll
+            for (int k = 1; k < NT; ++k)
+                if (l == k) s = ws[k];
+            wsum[v * T + l] = s;
+        }
+    }
+}
+
+// d tab[r] = sum_e <x_src_e, gS[v, t_e]> + gw[v, t_e]: per-block relation bins in LDS, one slab
+// row [n_rel] per block (the caller reduces the slab in a fixed order)
+template <int K, int NT>
+__global__ void __launch_bounds__(kBlock)
+typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                     const uint8_t* __restrict__ rel, const int32_t* __restrict__ n_id,
+                     const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, Tabs xt,
+                     int T, int64_t n_rows, const float* __restrict__ gS,
+                     const float* __restrict__ gw, float* __restrict__ slab, int n_rel) {
+    constexpr int LPR = K / 4;
+    constexpr int RPW = 64 / LPR;
+    constexpr int UN = 4;
+    __shared__ float bins[256];
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) bins[r] = 0.f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, l = lane % LPR, gl = lane - l;
+    const int64_t rows_per_block = int64_t(kBlock / 64) * RPW;
+    for (int64_t v0 = int64_t(blockIdx.x) * rows_per_block; v0 < n_rows;
+         v0 += int64_t(gridDim.x) * rows_per_block) {
+        const int64_t v = v0 + (threadIdx.x >> 6) * RPW + lane / LPR;
+        if (v >= n_rows) continue;
+        const int e0 = ptr[v], e1 = ptr[v + 1];
+        if (e0 == e1) continue;
+        float4 g[NT];
+        const float4* grow = reinterpret_cast<const float4*>(gS + v * int64_t(T) * K);
+#pragma unroll
+        for (int k = 0; k < NT; ++k) g[k] = k < T ? grow[k * LPR + l] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float gwl = l < T ? gw[v * T + l] : 0.f;
+        for (int c = e0; c < e1; c += LPR) {
+            int mt, mr;
+            int64_t mrow;
+            float mw;
+            edge_meta<LPR>(idx, rel, nullptr, n_id, ntype, local, c + l, e1, mt, mrow, mw, mr);
+            (void)mw;
+            const int m = min(LPR, e1 - c);
+            for (int j = 0; j < m; j += UN) {
+                float4 x[UN];
+                int tt[UN], rr[UN];
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    const int src = gl + min(j + u, m - 1);
+                    tt[u] = __shfl(mt, src, 64);
+                    rr[u] = __shfl(mr, src, 64);
+                    const int64_t rw = __shfl(mrow, src, 64);
+                    x[u] = reinterpret_cast<const float4*>(pick_tab<NT>(xt, tt[u]))[rw * LPR + l];
+                }
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {
+                    float4 gg = g[0];
+#pragma unroll
+                    for (int k = 1; k < NT; ++k)
+                        if (tt[u] == k) gg = g[k];
+                    float d = x[u].x * gg.x + x[u].y * gg.y + x[u].z * gg.z + x[u].w * gg.w;
+                    d = group_sum<LPR>(d);
+                    const float b = __shfl(gwl, gl + tt[u], 64);
+                    if (l == 0 && j + u < m) atomicAdd(bins + rr[u], d + b);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
+}
+
+}  // namespace nsagg
+}  // namespace regnn
+
+using namespace regnn;
+using namespace regnn::nsagg;
+
+extern "C" {
+
+int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                       const float* rel_table, const int32_t* n_id, const int32_t* ntype,
+                       const int64_t* local, const float* const* tables, int32_t n_types,
+                       int32_t K, int64_t n_rows, float* S, float* wsum, hipStream_t stream) {
+    if (!ptr || !idx || !rel || !rel_table || !n_id || !ntype || !local || !tables || !S ||
+        !wsum || n_types <= 0 || n_types > kMT || n_rows < 0)
+        return REGNN_EINVAL;
+    Tabs xt{};
+    for (int t = 0; t < n_types; ++t) {
+        if (!tables[t]) return REGNN_EINVAL;
+        xt.p[t] = tables[t];
+    }
+    if (n_rows == 0) return REGNN_OK;
+    const int lpr = K / 4;
+    const int64_t rpb = int64_t(kBlock / 64) * (64 / lpr);
+    int64_t grid = (n_rows + rpb - 1) / rpb;
+    if (grid > kMaxGrid) grid = kMaxGrid;
+#define AGG_CASE(KK, N)                                                                        \
+    if (K == KK && n_types <= N) {                                                             \
+        hipLaunchKernelGGL((typed_agg_kernel<KK, N>), dim3((unsigned)grid), dim3(kBlock), 0,   \
+                           stream, ptr, idx, rel, rel_table, n_id, ntype, local, xt, n_types,  \
+                           n_rows, S, wsum);                                                   \
+        REGNN_LAUNCH_CHECK();                                                                  \
+        return REGNN_OK;                                                                       \
+    }
+    AGG_CASE(64, 4) AGG_CASE(64, 8) AGG_CASE(128, 4) AGG_CASE(128, 8)
+#undef AGG_CASE
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
+                           const int32_t* n_id, const int32_t* ntype, const int64_t* local,
+                           const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
+                           const float* gS, const float* gw, float* slab, int32_t n_rel,
+                           int32_t slab_rows, hipStream_t stream) {
+    if (!ptr || !idx || !rel || !n_id || !ntype || !local || !tables || !gS || !gw || !slab ||
+        n_types <= 0 || n_types > kMT || n_rows < 0 || n_rel <= 0 || n_rel > 256 ||
+        slab_rows <= 0)
+        return REGNN_EINVAL;
+    Tabs xt{};
+    for (int t = 0; t < n_types; ++t) {
+        if (!tables[t]) return REGNN_EINVAL;
+        xt.p[t] = tables[t];
+    }
+#define BWD_CASE(KK, N)                                                                        \
+    if (K == KK && n_types <= N) {                                                             \
+        hipLaunchKernelGGL((typed_agg_bwd_kernel<KK, N>), dim3((unsigned)slab_rows),           \
+                           dim3(kBlock), 0, stream, ptr, idx, rel, n_id, ntype, local, xt,     \
+                           n_types, n_rows, gS, gw, slab, n_rel);                              \
+        REGNN_LAUNCH_CHECK();                                                                  \
+        return REGNN_OK;                                                                       \
+    }
+    BWD_CASE(64, 4) BWD_CASE(64, 8) BWD_CASE(128, 4) BWD_CASE(128, 8)
+#undef BWD_CASE
+    return REGNN_EUNSUPPORTED;
+}
+
+}  // extern "C"

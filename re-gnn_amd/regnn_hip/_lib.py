@@ -89,6 +89,9 @@ _SIG = {
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
+    "regnn_ns_typed_agg": ([P, P, P, P, P, P, P, P, I32, I32, I64, P, P, P], ctypes.c_int),
+    "regnn_ns_typed_agg_bwd": ([P, P, P, P, P, P, P, I32, I32, I64, P, P, P, I32, I32, P],
+                               ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
     "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
@@ -107,7 +110,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 30
+ABI_VERSION = 31
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -61,7 +61,7 @@ def source_hash():
 # sources alone key the summaries, so a change elsewhere (e.g. the NS engine) keeps them valid
 PMC_SOURCES = ("re_spmm.hip", "re_dense.hip", "regnn_common.h")
 # the fused NS model step's kernels (profiles/pmc_ns_fp32.json)
-NS_PMC_SOURCES = ("re_nsm.hip", "re_nsm_common.h", "regnn_common.h")
+NS_PMC_SOURCES = ("re_nsm.hip", "re_nsm2.hip", "re_nsm_common.h", "regnn_common.h")
 
 
 def kernel_hash(names=PMC_SOURCES):

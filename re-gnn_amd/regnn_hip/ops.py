@@ -609,6 +609,88 @@ def ns_spmm(blk, x, tab=None, bias=None):
     return _NsSpmm.apply(x, tab, bias, blk)
 
 
+
+class _NsTypedAgg(torch.autograd.Function):
+    """S[v, t] = sum_{e in v, type(src) = t} tab[rel_e] x_src (raw input rows read through n_id /
+    node type / local row), w[v, t] = sum of the same tab[rel_e] (regnn_ns_typed_agg); backward:
+    the relation-table gradient only (the input tables are data, feats_type 3)."""
+
+    @staticmethod
+    def forward(ctx, tab, blk, n_id, tables, node_type, local_idx):
+        T, K = len(tables), int(tables[0].shape[1])
+        dev = tables[0].device
+        S = torch.empty(blk.n_dst, T, K, dtype=torch.float32, device=dev)
+        w = torch.empty(blk.n_dst, T, dtype=torch.float32, device=dev)
+        t = tab.detach().float().contiguous()
+        n_id = _i32(n_id)
+        node_type, local_idx = _cached_cast(node_type, torch.int32), _cached_cast(local_idx, torch.int64)
+        arr = _ptr_array([L.ptr(x) for x in tables])
+        with timed("ns_typed_agg", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
+            L.call("regnn_ns_typed_agg", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx), L.ptr(blk.rel),
+                   L.ptr(t), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx), arr, T, K,
+                   blk.n_dst, L.ptr(S), L.ptr(w), L.stream())
+        ctx.blk, ctx.tables, ctx.idx = blk, tables, (n_id, node_type, local_idx)
+        ctx.n_rel, ctx.tab_shape = t.numel(), tab.shape
+        return S, w
+
+    @staticmethod
+    def backward(ctx, gS, gw):
+        if not ctx.needs_input_grad[0]:
+            return (None,) * 6
+        blk, tables = ctx.blk, ctx.tables
+        n_id, node_type, local_idx = ctx.idx
+        T, K = len(tables), int(tables[0].shape[1])
+        dev = tables[0].device
+        gS = torch.zeros(blk.n_dst, T, K, device=dev) if gS is None else gS.contiguous().float()
+        gw = torch.zeros(blk.n_dst, T, device=dev) if gw is None else gw.contiguous().float()
+        rows = L.slab_rows()
+        slab = torch.empty(rows, ctx.n_rel, dtype=torch.float32, device=dev)
+        with timed("ns_typed_agg_bwd", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
+            L.call("regnn_ns_typed_agg_bwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
+                   L.ptr(blk.rel), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx),
+                   _ptr_array([L.ptr(x) for x in tables]), T, K, blk.n_dst, L.ptr(gS), L.ptr(gw),
+                   L.ptr(slab), ctx.n_rel, rows, L.stream())
+        return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None, None, None
+
+
+_CAST_CACHE = {}
+
+
+def _cached_cast(t, dtype):
+    """t as a contiguous `dtype` tensor, converted once per (storage, version): the per-node
+    tables (node type, local row) are graph-sized and constant across steps."""
+    if t.dtype == dtype and t.is_contiguous():
+        return t
+    key = (t.data_ptr(), t.numel(), t.dtype, dtype, t.device)
+    hit = _CAST_CACHE.get(key)
+    if hit is not None and hit[0] is t and hit[1] == t._version:
+        return hit[2]
+    out = t.to(dtype).contiguous()
+    if len(_CAST_CACHE) > 16:
+        _CAST_CACHE.clear()
+    _CAST_CACHE[key] = (t, t._version, out)
+    return out
+
+
+def ns_typed_agg(blk, tab, n_id, tables, node_type, local_idx):
+    """layer 0's sampled-block aggregation of the RAW input rows per source node type (the NS
+    REGNN's group_input Linear and first conv weight moved after the mean by linearity,
+    mag/regnn_ns.py:300-326 + mag/regnn_layers.py:101-148): returns S [n_dst, T, K] and the
+    per-type weight sums w [n_dst, T]; differentiable in tab."""
+    return _NsTypedAgg.apply(tab, blk, n_id, tables, node_type, local_idx)
+
+
+def ns_typed_agg_ok(tables):
+    """regnn_ns_typed_agg's operand contract: 1..8 fp32 contiguous device tables of one width
+    64 or 128."""
+    if not tables or len(tables) > 8 or any(t is None for t in tables):
+        return False
+    K = tables[0].shape[1] if tables[0].dim() == 2 else -1
+    return K in (64, 128) and all(
+        t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == K and
+        t.is_contiguous() and t.data_ptr() % 16 == 0 for t in tables)
+
+
 # ---------------------------------------------------------------------------------------------
 class _EdgeSpmm(torch.autograd.Function):
     """y[v] = sum_{e: u->v} ew[e] * x[u]; ew per edge in the caller's edge order."""
@@ -823,7 +905,8 @@ class _AttnDots(torch.autograd.Function):
         gel = torch.zeros(N, H, device=ft.device) if gel is None else gel.contiguous().float()
         ger = torch.zeros(N, H, device=ft.device) if ger is None else ger.contiguous().float()
         gft = torch.empty_like(ft)
-        rows = max(1, min(256, N))
+        # one slab row per block: ~256+ rows per block, up to 2048 blocks (8 per CU)
+        rows = max(1, min(2048, -(-N // 256)))
         slab = torch.empty(rows, 2 * H * D, dtype=torch.float32, device=ft.device)
         with timed("attn_dots_bwd", 4 * (2 * N * H * D + 2 * N * H)):
             L.call("regnn_attn_dots_bwd", L.ptr(ft), L.ptr(al), L.ptr(ar), L.ptr(gel), L.ptr(ger),
@@ -1241,6 +1324,10 @@ def head_ce(h, weight, bias, labels, rows=None):
 # per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, REGNN.group_input)
 def _ptr_array(ptrs):
     return (ctypes.c_void_p * len(ptrs))(*[p if p else None for p in ptrs])
+
+
+def _i32(t):
+    return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
 
 
 def _i64(t):

@@ -70,3 +70,93 @@ def test_ns_dp_two_ranks_one_gpu():
     for ta, tb in zip(a["targets"], b["targets"]):
         assert not np.array_equal(ta, tb)                               # different batches
     assert all(np.isfinite(x["loss"]).all() for x in (a, b))
+
+
+def _union_worker(rank, world, port, q):
+    """rank r of 2 trains the fused step on half r of a fixed 64-target batch (the same hop seed
+    as the union: samples are keyed on (hop seed, node)), all-reduces the flat gradient bucket and
+    takes FlatAdam's step with grad_scale = 1/2 (what bench.py runs at world > 1); rank 0 then runs
+    one world-1 step on the union (Adam inside the step's last launch)."""
+    try:
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "re-gnn_amd"))
+        from test_gpu_ns_engine import _mag
+        from regnn_hip.ns import NSTrainer
+        d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.0)
+        union = torch.randperm(d["n_paper"], generator=torch.Generator().manual_seed(0))[:64]
+        union = union.to("cuda")
+
+        def trainer(w, r):
+            return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 64,
+                             torch.arange(d["n_paper"], device="cuda"), d["x_dict"],
+                             d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=9,
+                             rank=r, world=w, adam=dict(lr=1e-2), pipeline=False)
+
+        def one_step(tr, targets):
+            s = tr.slots[0]
+            s.set_seed(11, 0, 4)
+            s.set_targets(targets)
+            s.run_hops()
+            tr.fused.step()
+            tr._exchange()
+            tr._opt_step()
+            torch.cuda.synchronize()
+
+        tr = trainer(world, rank)
+        assert tr.fused is not None and tr.fused.two_layer and not tr.adam_fused
+        assert tr.opt.grad_scale == 0.5
+        one_step(tr, union[32 * rank:32 * (rank + 1)])
+        out = {"grad_sum": tr.flat.cpu().numpy().copy(), "param": tr.pflat.cpu().numpy().copy()}
+        dist.barrier()
+        dist.destroy_process_group()
+        if rank == 0:
+            tu = trainer(1, 0)
+            assert tu.adam_fused
+            one_step(tu, union)
+            out["union_grad"] = tu.flat.cpu().numpy().copy()
+            out["union_param"] = tu.pflat.cpu().numpy().copy()
+            out["param0"] = torch.cat([p.detach().reshape(-1) for p in
+                                       d["model"](5).parameters()]).cpu().numpy()
+        q.put((rank, out))
+    except Exception as e:                      # surface the failure in the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_ns_dp_fused_union_equals_allreduced_halves():
+    """the data-parallel contract of the fused step the bench runs. Two ranks
+    (gloo, one GPU) each run regnn_nsm_step on half of a batch; the SUM all-reduce plus FlatAdam's
+    grad_scale = 1/2 give the gradient and the Adam update of one world-1 step on the union batch
+    (mag/regnn_ns.py:405-407 under DistributedDataParallel)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + ((os.getpid() + 500) % 1000)
+    procs = [ctx.Process(target=_union_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), f"rank {r}: {res[r]}"
+    a, b = res[0], res[1]
+    assert np.array_equal(a["grad_sum"], b["grad_sum"])
+    assert np.array_equal(a["param"], b["param"])
+    g_dp = 0.5 * a["grad_sum"].astype(np.float64)
+    g_u = a["union_grad"].astype(np.float64)
+    scale = max(1e-3, float(np.abs(g_u).max()))
+    assert np.abs(g_dp - g_u).max() <= 2e-6 * scale, np.abs(g_dp - g_u).max()
+    # Adam's first step moves each element by lr * g / (|g| + eps): equal wherever the gradient
+    # is not within rounding of zero
+    moved = np.abs(a["union_param"] - a["param0"])
+    assert moved.max() > 1e-3
+    sure = np.abs(g_u) > 1e-4 * scale
+    d = np.abs(a["param"].astype(np.float64) - a["union_param"])
+    assert d[sure].max() <= 1e-6, d[sure].max()
+    assert d.max() <= 2.01e-2

@@ -1,0 +1,120 @@
+"""Layer 0 of the NS REGNN with group_input folded in (mag.REGNN._typed_first_layer over
+regnn_ns_typed_agg): the raw input rows aggregated per source node type, projected after the mean
+by the composed W_t^T W_0 -- the module path at any hidden width (the reference default hidden
+512, mag/regnn_ns.py:43). Loss and every parameter gradient must equal the reference-ordered path
+(group_input over every sampled node, then x_src @ W, then the mean: mag/regnn_ns.py:300-346,
+mag/regnn_layers.py:101-148) on the same sampled batch."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _golden as G  # noqa: E402
+from test_gpu_ns_engine import _mag, DEV  # noqa: E402
+
+
+def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96):
+    from regnn_hip import mag
+    from regnn_hip.ns import NSTrainer
+    old = mag.TYPED_AGG["mode"]
+    mag.TYPED_AGG["mode"] = "auto" if typed else "off"
+    try:
+        torch.manual_seed(7)
+        K = int(d["x_dict"][0].shape[1])
+        m = mag.REGNN(K, hidden, 13, 2, 10.0, dropout, {k: K for k in d["x_dict"]}, 7,
+                      use_norm="ln", self_loop_type=2, residual=residual).to(DEV)
+        with torch.no_grad():
+            for conv in m.convs:
+                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, 11, device=DEV))
+                conv.bias.normal_(0, 0.1)
+        m.train()
+        opt = torch.optim.SGD(m.parameters(), lr=0.0)
+        tr = NSTrainer(m, opt, d["rg"], [6, 4], batch, torch.arange(d["n_paper"], device=DEV),
+                       d["x_dict"], d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=3,
+                       engine="module")
+        seen = []
+        orig = m._typed_first_layer
+
+        def spy(*a, **k):
+            out = orig(*a, **k)
+            seen.append(out is not None)
+            return out
+        m._typed_first_layer = spy
+        torch.manual_seed(11)                  # the model-level dropout's torch RNG
+        tr._forward_backward()
+        torch.cuda.synchronize()
+        assert seen == [typed]
+        return float(tr.loss), {n: p.grad.detach().double().cpu().numpy().copy()
+                                for n, p in m.named_parameters()}
+    finally:
+        mag.TYPED_AGG["mode"] = old
+
+
+@pytest.mark.parametrize("K,hidden,residual", [(128, 512, False), (128, 64, False),
+                                               (64, 128, True)])
+def test_typed_first_layer_matches_reference_order(K, hidden, residual):
+    d = _mag(0.003, seed=2, F=K)
+    la, ga = _grads_one_step(d, hidden, True, 0.0, residual)
+    lb, gb = _grads_one_step(d, hidden, False, 0.0, residual)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+    # the relation table of layer 0 has a gradient through the typed aggregation
+    assert np.abs(ga["convs.0.relation_weight"]).max() > 0
+
+
+def test_typed_agg_against_fp64_sums():
+    """S / w rows of regnn_ns_typed_agg against fp64 sums over the block's CSR rows, and its
+    relation-table gradient against autograd of the fp64 restatement."""
+    from regnn_hip import ops
+    from regnn_hip.ns import DeviceSampler
+    d = _mag(0.003, seed=4, F=128)
+    s = DeviceSampler(d["rg"], [6, 4], 64, etype=d["edge_type"], ntype=d["node_type"],
+                      num_edge_types=7)
+    s.set_seed(5, 0, 1)
+    s.set_targets(torch.arange(64, device=DEV) * 3)
+    s.run_hops(meta_only=False, strided=False)
+    blk = s.blocks[1]                           # layer 0's block (the outer hop)
+    sz = s.sizes.cpu().tolist()
+    n_dst, E = sz[1], sz[9]
+    tables = [d["x_dict"][k] for k in range(4)]
+    rw = torch.linspace(-0.05, 0.2, 11, device=DEV, requires_grad=True)
+    tab = torch.nn.functional.leaky_relu(rw * 10.0)
+    n_id = s.n_id.to(torch.int64)
+    S, w = ops.ns_typed_agg(blk, tab, n_id, tables, d["node_type"], d["local"])
+    gS = torch.randn_like(S)
+    gw = torch.randn_like(w)
+    (S * gS).sum().add((w * gw).sum()).backward()
+    # fp64 restatement
+    ptr = blk.csr_ptr[:n_dst + 1].cpu().numpy()
+    idx = blk.csr_idx[:E].cpu().numpy()
+    rel = blk.rel[:E].cpu().numpy().astype(np.int64)
+    nid = n_id.cpu().numpy()
+    nt = d["node_type"].cpu().numpy()
+    lo = d["local"].cpu().numpy()
+    X = [t.double().cpu().numpy() for t in tables]
+    rw64 = torch.tensor(rw.detach().cpu().numpy(), dtype=torch.float64, requires_grad=True)
+    tab64 = torch.nn.functional.leaky_relu(rw64 * 10.0)
+    e_dst = np.repeat(np.arange(n_dst), np.diff(ptr))
+    g_src = nid[idx]
+    e_t = nt[g_src]
+    e_x = np.stack([X[e_t[i]][lo[g_src[i]]] for i in range(E)])
+    wt = tab64[torch.from_numpy(rel)]
+    S64 = torch.zeros(n_dst, 4, 128, dtype=torch.float64)
+    w64 = torch.zeros(n_dst, 4, dtype=torch.float64)
+    flat = torch.from_numpy(e_dst * 4 + e_t)
+    S64.view(-1, 128).index_add_(0, flat, wt[:, None] * torch.from_numpy(e_x))
+    w64.view(-1).index_add_(0, flat, wt)
+    ok, err = G.close(S[:n_dst].detach().cpu().numpy(), S64.detach().numpy(), 1e-5)
+    assert ok, err
+    ok, err = G.close(w[:n_dst].detach().cpu().numpy(), w64.detach().numpy(), 1e-5)
+    assert ok, err
+    ((S64 * gS[:n_dst].double().cpu()).sum() + (w64 * gw[:n_dst].double().cpu()).sum()).backward()
+    ok, err = G.close(rw.grad.cpu().numpy(), rw64.grad.numpy(), 1e-5)
+    assert ok, err
