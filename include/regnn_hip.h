@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 31). */
+/* ABI version (bumped on any signature change or addition; currently 32). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -604,6 +604,19 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
                       const float* rel_table, const float* out_scale, const float* g,
                       const float* x, float* gx, float* slab, int32_t n_rel, int64_t n_rows,
                       int32_t F, hipStream_t stream);
+
+/* regnn_ns_spmm_bwd as a gather over the block's transposed index (regnn_ns_hop csc_ptr /
+ * csc_ent: per local source u its entries (target row v << 8 | relation r)):
+ *   gx[u] = sum_{entries of u} rel_table[r] out_scale[v] g[v]      (every row u < cap_rows
+ *           written once; rows u >= sizes[size_idx] (the batch's sources) get zeros)
+ *   slab[b][r] (optional) = block b's partial of sum out_scale[v] <g[v], x[u]> over relation r
+ *   (launches slab_rows blocks; reduce with regnn_rel_reduce; LDS float bins).
+ * sizes may be null (then every row < cap_rows is live). F in {64, 128, 256, 512, 1024, 2048}. */
+int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_long,
+                          const float* rel_table, const float* out_scale, const float* g,
+                          const float* x, float* gx, float* slab, int32_t n_rel,
+                          const int32_t* sizes, int32_t size_idx, int64_t cap_rows, int32_t F,
+                          int32_t slab_rows, hipStream_t stream);
 
 /* Typed aggregation of raw input rows over a sampled block (layer 0 of the NS REGNN at any hidden
  * width; mag/regnn_ns.py:300-326 group_input + mag/regnn_layers.py:101-148, replacing the

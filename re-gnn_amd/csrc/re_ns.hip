@@ -637,11 +637,157 @@ ns_spmm_bwd_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ 
     for (int r = threadIdx.x; r < n_rel; r += blockDim.x) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
 }
 
+// The same backward as a gather over the block's transposed index (regnn_ns_hop csc_*: per local
+// source u its entries (target row v << 8 | relation r)): gx[u] = sum tab[r] s[v] g[v], every row
+// written once (no zero fill, no atomics to HBM); the relation dots s[v] <g[v], x[u]> from the
+// source row held in registers, per-block LDS bins -> one slab row per block. F = 4 LPR VPL.
+// Rows with <= kCscShort entries: one LPR-lane group each, UN entries' rows in flight; the hub
+// rows (the sampler's csc_long list): a workgroup each, its groups taking interleaved entries,
+// the group partials added in LDS in group order.
+template <int LPR, int VPL>
+__device__ __forceinline__ void csc_entries(const int32_t* __restrict__ cent,
+                                            const float* __restrict__ tab,
+                                            const float* __restrict__ out_scale,
+                                            const float* __restrict__ g, float* bins, bool dots,
+                                            int c0, int c1, int step, int l, int gl,
+                                            const float4 (&xr)[VPL], float4 (&acc)[VPL]) {
+    constexpr int F = 4 * LPR * VPL;
+    constexpr int UN = 8;
+    for (int c = c0; c < c1; c += UN * step) {
+        int vv[UN], rr[UN];
+        float ww[UN], ss[UN];
+        float4 gv[UN][VPL];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int cc = c + u * step;
+            const int en = cc < c1 ? cent[cc] : 0;
+            vv[u] = en >> 8;
+            rr[u] = en & 255;
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            ss[u] = out_scale ? out_scale[vv[u]] : 1.f;
+            ww[u] = (c + u * step < c1) ? (tab ? tab[rr[u]] : 1.f) * ss[u] : 0.f;
+#pragma unroll
+            for (int p = 0; p < VPL; ++p)
+                gv[u][p] = *reinterpret_cast<const float4*>(g + int64_t(vv[u]) * F + 4 * (l + LPR * p));
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            float d = 0.f;
+#pragma unroll
+            for (int p = 0; p < VPL; ++p) {
+                acc[p].x = fmaf(ww[u], gv[u][p].x, acc[p].x);
+                acc[p].y = fmaf(ww[u], gv[u][p].y, acc[p].y);
+                acc[p].z = fmaf(ww[u], gv[u][p].z, acc[p].z);
+                acc[p].w = fmaf(ww[u], gv[u][p].w, acc[p].w);
+                d = fmaf(gv[u][p].w, xr[p].w, fmaf(gv[u][p].z, xr[p].z,
+                         fmaf(gv[u][p].y, xr[p].y, fmaf(gv[u][p].x, xr[p].x, d))));
+            }
+            if (dots) {
+                d = group_sum<LPR>(d);
+                if (l == 0 && c + u * step < c1) atomicAdd(bins + rr[u], ss[u] * d);
+            }
+        }
+    }
+    (void)gl;
+}
+
+template <int LPR, int VPL>
+__global__ void __launch_bounds__(kBlock)
+ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restrict__ cent,
+                       const int32_t* __restrict__ clong, const float* __restrict__ tab,
+                       const float* __restrict__ out_scale, const float* __restrict__ g,
+                       const float* __restrict__ x, float* __restrict__ gx,
+                       float* __restrict__ slab, int n_rel, const int32_t* __restrict__ sizes,
+                       int size_idx, int64_t cap_rows) {
+    constexpr int F = 4 * LPR * VPL;
+    constexpr int NG = kBlock / LPR;       // row groups per block
+    __shared__ float bins[256];
+    __shared__ float4 part[NG * LPR * VPL];
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) bins[r] = 0.f;
+    __syncthreads();
+    const bool dots = slab != nullptr;
+    const int l = threadIdx.x % LPR, grp = threadIdx.x / LPR, gl = (threadIdx.x & 63) - l;
+    const int64_t n_rows = sizes ? min(cap_rows, int64_t(sizes[size_idx])) : cap_rows;
+    // ---- rows with <= kCscShort entries (and the rows past the batch: zeros)
+    for (int64_t u = int64_t(blockIdx.x) * NG + grp; u < cap_rows; u += int64_t(gridDim.x) * NG) {
+        const bool live = u < n_rows;
+        const int c0 = live ? cptr[u] : 0, c1 = live ? cptr[u + 1] : 0;
+        if (c1 - c0 > kCscShort) continue;     // a hub: the workgroup pass below
+        float4 acc[VPL], xr[VPL];
+#pragma unroll
+        for (int p = 0; p < VPL; ++p) {
+            acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[p] = dots && live ? *reinterpret_cast<const float4*>(x + u * F + 4 * (l + LPR * p))
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        csc_entries<LPR, VPL>(cent, tab, out_scale, g, bins, dots, c0, c1, 1, l, gl, xr, acc);
+#pragma unroll
+        for (int p = 0; p < VPL; ++p)
+            *reinterpret_cast<float4*>(gx + u * F + 4 * (l + LPR * p)) = acc[p];
+    }
+    // ---- hub rows: a workgroup each
+    const int n_long = clong ? clong[0] : 0;
+    for (int li = blockIdx.x; li < n_long; li += gridDim.x) {
+        const int64_t u = clong[1 + li];
+        const int c0 = cptr[u], c1 = cptr[u + 1];
+        float4 acc[VPL], xr[VPL];
+#pragma unroll
+        for (int p = 0; p < VPL; ++p) {
+            acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[p] = dots ? *reinterpret_cast<const float4*>(x + u * F + 4 * (l + LPR * p))
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        csc_entries<LPR, VPL>(cent, tab, out_scale, g, bins, dots, c0 + grp, c1, NG, l, gl, xr, acc);
+#pragma unroll
+        for (int p = 0; p < VPL; ++p) part[(grp * VPL + p) * LPR + l] = acc[p];
+        __syncthreads();
+        for (int i = threadIdx.x; i < LPR * VPL; i += kBlock) {
+            float4 s4 = part[i];
+            for (int k = 1; k < NG; ++k) {
+                const float4 q = part[k * LPR * VPL + i];
+                s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+            }
+            const int p = i / LPR, ll = i % LPR;
+            *reinterpret_cast<float4*>(gx + u * F + 4 * (ll + LPR * p)) = s4;
+        }
+        __syncthreads();
+    }
+    if (!dots) return;
+    __syncthreads();
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
+}
+
 }  // namespace regnn
 
 using namespace regnn;
 
 extern "C" {
+
+int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_long,
+                          const float* rel_table, const float* out_scale, const float* g,
+                          const float* x, float* gx, float* slab, int32_t n_rel,
+                          const int32_t* sizes, int32_t size_idx, int64_t cap_rows, int32_t F,
+                          int32_t slab_rows, hipStream_t stream) {
+    if (!csc_ptr || !csc_ent || !g || !gx || cap_rows < 0 || F <= 0 || n_rel < 0 || n_rel > 256 ||
+        (slab && (!x || n_rel == 0 || slab_rows <= 0)) || (sizes && size_idx < 0))
+        return REGNN_EINVAL;
+    if (cap_rows == 0) return REGNN_OK;
+    const int grid = slab ? slab_rows : kMaxGrid;
+#define NSC_CASE(L, V)                                                                         \
+    if (F == 4 * L * V) {                                                                      \
+        hipLaunchKernelGGL((ns_spmm_bwd_csc_kernel<L, V>), dim3(grid), dim3(kBlock), 0,        \
+                           stream, csc_ptr, csc_ent, csc_long, rel_table, out_scale, g, x, gx, \
+                           slab, n_rel, sizes, size_idx, cap_rows);                            \
+        REGNN_LAUNCH_CHECK();                                                                  \
+        return REGNN_OK;                                                                       \
+    }
+    NSC_CASE(16, 1) NSC_CASE(32, 1) NSC_CASE(64, 1) NSC_CASE(64, 2) NSC_CASE(64, 4)
+    NSC_CASE(64, 8)
+#undef NSC_CASE
+    return REGNN_EUNSUPPORTED;
+}
 
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
                    int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,

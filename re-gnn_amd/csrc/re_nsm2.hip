@@ -740,8 +740,10 @@ __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab
             acc[1] += to_fix(t * g[u].y);
             acc[2] += to_fix(t * g[u].z);
             acc[3] += to_fix(t * g[u].w);
-            const float d = group_sum<16>(R.h0[0] * g[u].x + R.h0[1] * g[u].y +
-                                          R.h0[2] * g[u].z + R.h0[3] * g[u].w);
+            // an explicit fma chain: the entry's slot u in the (atomically ordered) segment must
+            // not change how its dot is contracted, or the exact sums see different terms
+            const float d = group_sum<16>(fmaf(R.h0[3], g[u].w, fmaf(R.h0[2], g[u].z,
+                                               fmaf(R.h0[1], g[u].y, R.h0[0] * g[u].x))));
             if (l == 0) atomicAdd(bins + (pk[u] & 255), to_fix(d));      // LDS, exact
         }
     }

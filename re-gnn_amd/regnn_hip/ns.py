@@ -593,6 +593,15 @@ class NSTrainer:
         if engine != "module" and why is None:
             self.fused = FusedStep(model, self.slots[0], x_dict, node_type, local_node_idx,
                                    self.y_flat, self.loss)
+        if self.fused is None and self._blocks_ok:
+            # the module path's last layer (hop 0's block) differentiates through a gather over
+            # the sampler's transposed index of that block (regnn_ns_spmm_bwd_csc: no float
+            # atomics into the source rows' gradient)
+            s0 = self.slots[0]
+            if s0.blocks[0].csr_idx.numel() <= 32768:
+                _, cptr, cent, clong = s0.csc[0] or s0.enable_csc(0)
+                b0 = s0.blocks[0]
+                b0.csc, b0.csc_cap = (cptr, cent, clong, s0.sizes, 1), s0.caps[1]
         self.pipelined = self.fused is not None and bool(pipeline)
         if self.pipelined:
             s1 = DeviceSampler(rg, sizes, batch_size, num_edge_types=num_edge_types,

@@ -562,6 +562,12 @@ def re_spmm_fused(rg, x, tab=None, pack=None, post=None, bias=None, residual=Non
 _NO_PLAN = (0, 0, None, 0, None, None, 0, None, None, 0, None)
 
 
+_CSC_WIDTHS = (64, 128, 256, 512, 1024, 2048)   # regnn_ns_spmm_bwd_csc's F = 4 LPR VPL
+# "auto": a sampled block carrying its transposed index differentiates by the CSC gather; "off":
+# the atomic scatter (tests compare the two)
+NS_CSC = {"mode": "auto"}
+
+
 class _NsSpmm(torch.autograd.Function):
     """y[v] = inv[v] * sum_{e in row v} tab[rel_e] * x[idx_e] + bias over a sampled block
     (regnn_hip.ns.NSBlock: rows <= fan-out + 1, no long-row plan, no host sizes)."""
@@ -590,8 +596,25 @@ class _NsSpmm(torch.autograd.Function):
         need_x, need_tab, _, = ctx.needs_input_grad[:3]
         gy = gy.contiguous().float()
         F = x.shape[1]
-        gx = torch.zeros_like(x)
         n_rel = t.numel() if t is not None else 0
+        csc = getattr(blk, "csc", None)
+        if csc is not None and NS_CSC["mode"] != "off" and F in _CSC_WIDTHS and \
+                x.shape[0] <= blk.csc_cap:
+            # a gather over the sampler's transposed index: every row written once, no atomics
+            cptr, cent, clong, sizes, size_idx = csc
+            gx = torch.empty_like(x)
+            rows = L.slab_rows()
+            slab = (torch.empty(rows, n_rel, dtype=torch.float32, device=x.device)
+                    if (need_tab and t is not None) else None)
+            with timed("ns_spmm_bwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_bwd")):
+                L.call("regnn_ns_spmm_bwd_csc", L.ptr(cptr), L.ptr(cent), L.ptr(clong), L.ptr(t),
+                       L.ptr(blk.inv),
+                       L.ptr(gy), L.ptr(x), L.ptr(gx), L.ptr(slab), n_rel, L.ptr(sizes), size_idx,
+                       x.shape[0], F, rows, L.stream())
+            g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
+            g_bias = gy.sum(0) if ctx.needs_input_grad[2] else None
+            return (gx if need_x else None), g_tab, g_bias, None
+        gx = torch.zeros_like(x)
         slab = _slab(n_rel, x.device) if (need_tab and t is not None) else None
         with timed("ns_spmm_bwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_bwd")):
             L.call("regnn_ns_spmm_bwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),

@@ -19,10 +19,11 @@ from test_gpu_ns_engine import _mag, DEV  # noqa: E402
 
 
 def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96):
-    from regnn_hip import mag
+    from regnn_hip import mag, ops
     from regnn_hip.ns import NSTrainer
-    old = mag.TYPED_AGG["mode"]
-    mag.TYPED_AGG["mode"] = "auto" if typed else "off"
+    old, old_csc = mag.TYPED_AGG["mode"], ops.NS_CSC["mode"]
+    # the reference-ordered run also takes the atomic scatter backward of the last layer
+    mag.TYPED_AGG["mode"] = ops.NS_CSC["mode"] = "auto" if typed else "off"
     try:
         torch.manual_seed(7)
         K = int(d["x_dict"][0].shape[1])
@@ -52,11 +53,11 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96):
         return float(tr.loss), {n: p.grad.detach().double().cpu().numpy().copy()
                                 for n, p in m.named_parameters()}
     finally:
-        mag.TYPED_AGG["mode"] = old
+        mag.TYPED_AGG["mode"], ops.NS_CSC["mode"] = old, old_csc
 
 
 @pytest.mark.parametrize("K,hidden,residual", [(128, 512, False), (128, 64, False),
-                                               (64, 128, True)])
+                                               (64, 128, True), (128, 256, False)])
 def test_typed_first_layer_matches_reference_order(K, hidden, residual):
     d = _mag(0.003, seed=2, F=K)
     la, ga = _grads_one_step(d, hidden, True, 0.0, residual)
