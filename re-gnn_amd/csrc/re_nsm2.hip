@@ -27,12 +27,22 @@
 //             attached, Adam (regnn_adam_flat's arithmetic) on each element right after its sum.
 #include "re_nsm_common.h"
 
+#include <cstdlib>
+
 namespace regnn {
 namespace nsm2 {
 using namespace regnn::nsm;
 
 constexpr int kRows = 16;                  // target rows per block (one MFMA row tile)
-constexpr int kBwdBlocks = 128;            // bwd0 blocks per node type (static slab layout)
+// bwd0 blocks per node type and gather blocks (the slab layout follows them). The defaults are
+// the measured choice; REGNN_NSM_BWD_BLOCKS / REGNN_NSM_GATH_BLOCKS override them for A/B runs
+// (read once per process, so regnn_nsm_slab_floats and regnn_nsm_step agree).
+inline int env_blocks(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v >= 16 && v <= 4096 ? v : dflt;
+}
+static const int kBwdBlocks = env_blocks("REGNN_NSM_BWD_BLOCKS", 128);
 constexpr int kMaxCT = 27;                 // class tiles of 16 (C <= 432: the head's LDS)
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
@@ -351,9 +361,11 @@ struct HeadArgs {
     float* gh; float* nvalid; float* part; int64_t part_w;
 };
 
-inline int64_t head_part_width(int C) {
-    return (int64_t(C) * (F + 1) + 3 * F + 1 + F * F + 3) & ~3ll;
+// o_w1 (the W_1 partial) starts on a 16-byte boundary: finalize sums it with float4 loads
+__host__ __device__ inline int64_t head_o_w1(int C) {
+    return (int64_t(C) * (F + 1) + 3 * F + 1 + 3) & ~3ll;
 }
+inline int64_t head_part_width(int C) { return head_o_w1(C) + F * F; }
 __host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }
 __host__ __device__ inline int head_wl(int C) {
     const int wl = ((C + 15) / 16) * 16 * F, red = 3 * 16 * F + 16 * 68;
@@ -593,7 +605,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     __syncthreads();
     float* o = A.part + int64_t(blockIdx.x) * A.part_w;
     const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
-    const int64_t o_w1 = o_loss + 1;
+    const int64_t o_w1 = head_o_w1(C);
     // ---- 5. out_lin weight partial D[c][k] = sum_v g[v][c] h[v][k], its bias, row terms
     for (int ct = w; ct < CT; ct += kBlock / 64) {
         f32x4 dw[4];
@@ -690,7 +702,7 @@ struct GathArgs {
     float* g0; float* slab;
 };
 
-constexpr int kGathBlocks = 512;
+static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 512);
 constexpr int kGathW = 4 * F;
 constexpr int kShort = 16;                 // = re_ns.hip kCscShort
 
@@ -1131,7 +1143,7 @@ enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2 };
 struct Job {
     const float* src;
     int64_t pstride;
-    int nparts, width, op, adam;
+    int nparts, width, op, adam, vec;    // vec: 4 elements per thread (float4 partial rows)
     float* dst;
     const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
 };
@@ -1152,19 +1164,92 @@ struct FinArgs {
     AdamArgs adam;
 };
 
-__global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
-    __shared__ float red[8][33];
-    __shared__ int64_t s_t;
-    __shared__ float s_step, s_bc2;
-    __shared__ bool last;
-    int ji = 0;
+// the bias corrections of this step, once per block (thread 64)
+__device__ __forceinline__ void adam_consts(const AdamArgs& O, int64_t& s_t, float& s_step,
+                                            float& s_bc2) {
+    if (O.on && threadIdx.x == 64) {
+        const int64_t t = O.step[0] + 1;
+        const double bc1 = 1.0 - pow(double(O.b1), double(t));
+        const double bc2 = 1.0 - pow(double(O.b2), double(t));
+        s_t = t;
+        s_step = float(double(O.lr) / bc1);
+        s_bc2 = float(sqrt(bc2));
+    }
+}
+
+// torch.optim.Adam on one element (regnn_adam_flat's arithmetic)
+__device__ __forceinline__ void adam_elem(const AdamArgs& O, int64_t i, float g, float pi,
+                                          float mi, float vi, float s_step, float s_bc2) {
+    float gi = g * O.gscale;
+    if (O.wd != 0.f) gi = gi + O.wd * pi;
+    const float mn = mi + (1.f - O.b1) * (gi - mi);
+    const float vn = vi * O.b2 + (1.f - O.b2) * gi * gi;
+    O.m[i] = mn;
+    O.v[i] = vn;
+    O.p[i] = pi - s_step * (mn / (sqrtf(vn) / s_bc2 + O.eps));
+}
+
+// 4 consecutive elements per thread: 32 float4 columns x 8 partial groups per block, the same
+// per-element summation order as the scalar path (partials grp, grp + 8, ...; groups combined
+// in a fixed tree)
+__device__ __forceinline__ void finalize_vec(const FinArgs& A, const Job& J, const AdamArgs& O,
+                                             int b, int el, int grp, int64_t& s_t, float& s_step,
+                                             float& s_bc2) {
+    __shared__ float4 red4[8][33];
+    const int e = (b * 32 + el) * 4;
+    const int64_t i = (J.dst + e) - O.gbase;
+    const bool stepped = O.on && J.adam && threadIdx.x < 32 && e < J.width && i >= 0 && i < O.n;
+    float pi[4] = {0.f, 0.f, 0.f, 0.f}, mi[4] = {0.f, 0.f, 0.f, 0.f}, vi[4] = {0.f, 0.f, 0.f, 0.f};
+    if (stepped) {
 #pragma unroll
-    for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
-    const int b = blockIdx.x - A.start[ji];
-    const Job J = A.job[ji];
-    const AdamArgs& O = A.adam;
-    PH(3, 0);
-    const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+        for (int k = 0; k < 4; ++k) {
+            pi[k] = O.p[i + k]; mi[k] = O.m[i + k]; vi[k] = O.v[i + k];
+        }
+    }
+    adam_consts(O, s_t, s_step, s_bc2);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < J.width) {
+        const float4* src = reinterpret_cast<const float4*>(J.src + e);
+        const int64_t ps = J.pstride / 4;
+        int p = grp;
+        for (; p + 56 < J.nparts; p += 64) {
+            float4 vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + 8 * u) * ps];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s.x += vv[u].x; s.y += vv[u].y; s.z += vv[u].z; s.w += vv[u].w;
+            }
+        }
+        for (; p < J.nparts; p += 8) {
+            const float4 v = src[int64_t(p) * ps];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    }
+    red4[grp][el] = s;
+    __syncthreads();
+    if (threadIdx.x < 32 && e < J.width) {
+        float4 r[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) r[g] = red4[g][el];
+        float4 tot;
+        tot.x = ((r[0].x + r[1].x) + (r[2].x + r[3].x)) + ((r[4].x + r[5].x) + (r[6].x + r[7].x));
+        tot.y = ((r[0].y + r[1].y) + (r[2].y + r[3].y)) + ((r[4].y + r[5].y) + (r[6].y + r[7].y));
+        tot.z = ((r[0].z + r[1].z) + (r[2].z + r[3].z)) + ((r[4].z + r[5].z) + (r[6].z + r[7].z));
+        tot.w = ((r[0].w + r[1].w) + (r[2].w + r[3].w)) + ((r[4].w + r[5].w) + (r[6].w + r[7].w));
+        *reinterpret_cast<float4*>(J.dst + e) = tot;
+        if (stepped) {
+            const float t4[4] = {tot.x, tot.y, tot.z, tot.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) adam_elem(O, i + k, t4[k], pi[k], mi[k], vi[k], s_step, s_bc2);
+        }
+    }
+}
+
+__device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, const AdamArgs& O,
+                                                int b, int el, int grp, int64_t& s_t,
+                                                float& s_step, float& s_bc2) {
+    __shared__ float red[8][33];
     const int e = b * 32 + el;
     // the optimizer's operands of this thread's element, requested before the partial sums
     const int64_t i = (J.dst + e) - O.gbase;
@@ -1173,14 +1258,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     if (stepped) {
         pi = O.p[i]; mi = O.m[i]; vi = O.v[i];
     }
-    if (O.on && threadIdx.x == 64) {           // the bias corrections, once per block
-        const int64_t t = O.step[0] + 1;
-        const double bc1 = 1.0 - pow(double(O.b1), double(t));
-        const double bc2 = 1.0 - pow(double(O.b2), double(t));
-        s_t = t;
-        s_step = float(double(O.lr) / bc1);
-        s_bc2 = float(sqrt(bc2));
-    }
+    adam_consts(O, s_t, s_step, s_bc2);
     float s = 0.f;
     if (e < J.width) {
         const float* src = J.src + e;
@@ -1211,19 +1289,30 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
         J.dst[e] = out;
         // torch.optim.Adam (regnn_adam_flat's arithmetic); a gradient outside the bucket (a
         // frozen parameter's scratch buffer) is not stepped
-        if (stepped) {
-            float gi = out * O.gscale;
-            if (O.wd != 0.f) gi = gi + O.wd * pi;
-            const float mn = mi + (1.f - O.b1) * (gi - mi);
-            const float vn = vi * O.b2 + (1.f - O.b2) * gi * gi;
-            O.m[i] = mn;
-            O.v[i] = vn;
-            O.p[i] = pi - s_step * (mn / (sqrtf(vn) / s_bc2 + O.eps));
-        }
+        if (stepped) adam_elem(O, i, out, pi, mi, vi, s_step, s_bc2);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
+    __shared__ int64_t s_t;
+    __shared__ float s_step, s_bc2;
+    __shared__ bool last;
+    int ji = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
+    const int b = blockIdx.x - A.start[ji];
+    const Job J = A.job[ji];
+    const AdamArgs& O = A.adam;
+    PH(3, 0);
+    const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    if (J.vec) {                               // block-uniform
+        finalize_vec(A, J, O, b, el, grp, s_t, s_step, s_bc2);
+    } else {
+        finalize_scalar(A, J, O, b, el, grp, s_t, s_step, s_bc2);
     }
     if (O.on) {
-        // every block read the step count before its ticket (the barrier above waited for the
-        // load); the last block to finish advances it
+        // every block read the step count before its ticket (the barrier in the sum waited for
+        // the load); the last block to finish advances it
         __syncthreads();
         if (threadIdx.x == 0) last = atomicAdd(O.ticket, 1u) == gridDim.x - 1;
         __syncthreads();
@@ -1244,7 +1333,10 @@ struct JobList {
         Job& j = A.job[A.n_jobs++];
         j.src = src; j.pstride = pstride; j.nparts = nparts; j.width = width; j.dst = dst;
         j.op = op; j.aux = aux; j.adam = op != kOpLoss;
-        blocks += (width + 31) / 32;
+        j.vec = op == kOpCopy && width % 4 == 0 && pstride % 4 == 0 &&
+                reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(dst) % 16 == 0;
+        blocks += j.vec ? (width / 4 + 31) / 32 : (width + 31) / 32;
     }
 };
 
@@ -1411,7 +1503,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         J.A.alpha = p->alpha;
         const float* hp = w->slab + S.head;
         const int nh = S.head_blocks;
-        const int64_t o_cb = int64_t(C) * (F + 1), o_w1 = o_cb + 3 * F + 1;
+        const int64_t o_cb = int64_t(C) * (F + 1), o_w1 = head_o_w1(C);
         J.add(hp, hw, nh, C * F, p->g_out_w);
         J.add(hp + int64_t(C) * F, hw, nh, C, p->g_out_b);
         J.add(hp + o_cb, hw, nh, F, p->g_conv_b[1]);

@@ -565,20 +565,22 @@ class NSTrainer:
         self._blocks_ok = (getattr(model, "model", None) == "regcn" and
                            getattr(model, "self_loop_type", None) == 2)
         self.params = [p for p in model.parameters() if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        o = 0
+        # every parameter starts on a 16-byte boundary of the flat buckets (the fused step's
+        # finalize sums and steps 4 aligned elements per thread); the pad elements stay zero
+        self.offsets, o = [], 0
         for p in self.params:
+            self.offsets.append(o)
+            o += (p.numel() + 3) // 4 * 4
+        self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
+        for p, o in zip(self.params, self.offsets):
             p.grad = self.flat[o:o + p.numel()].view_as(p)
-            o += p.numel()
         if opt is None:
             # the parameters become views of one flat bucket too, and one launch updates them
             # all (FlatAdam; `adam` = torch.optim.Adam's keyword arguments)
-            self.pflat = torch.cat([p.detach().reshape(-1) for p in self.params]).contiguous()
-            o = 0
-            for p in self.params:
+            self.pflat = torch.zeros_like(self.flat)
+            for p, o in zip(self.params, self.offsets):
+                self.pflat[o:o + p.numel()].copy_(p.detach().reshape(-1))
                 p.data = self.pflat[o:o + p.numel()].view_as(p)
-                o += p.numel()
             self.opt = opt = FlatAdam(self.pflat, self.flat, **(adam or {}))
             # the data-parallel mean of the SUM all-reduce, inside Adam's launch: no division
             # pass between the exchange and the update (p.grad holds the rank sum)
@@ -618,6 +620,8 @@ class NSTrainer:
             for fs in (self.fused_slots if self.pipelined else [self.fused]):
                 fs.attach_adam(self.opt, self.flat)
         self.graphs = None
+        # tests: all-reduce the bucket even with one rank (the captured-exchange path on one GPU)
+        self._force_exchange = False
         self.epoch = -1
         self.set_epoch(0)
 
@@ -713,7 +717,7 @@ class NSTrainer:
             self.loss.copy_(loss.detach())
 
     def _exchange(self):
-        if self.world > 1:
+        if self.world > 1 or self._force_exchange:
             import torch.distributed as dist
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             if not isinstance(self.opt, FlatAdam):       # FlatAdam takes the mean itself
@@ -760,13 +764,23 @@ class NSTrainer:
                     else:
                         v.zero_()
 
-    def capture(self, warmup=2):
+    def capture(self, warmup=2, exchange_in_graph=None):
         """capture the step as HIP graphs: [fwd/bwd + optimizer] on one rank; [fwd/bwd] (+ the
         eager all-reduce) + [optimizer] on several. The `warmup` eager steps that precede the
         capture (kernel selection, lazy optimizer state) are undone: parameters, optimizer
         moments and step count, and the sampler's batch / edge counters are restored, so the
         first replay trains the epoch's first batch from the same model as an eager step would.
-        Only the dedup stamps move on (they must stay monotone)."""
+        Only the dedup stamps move on (they must stay monotone).
+
+        exchange_in_graph (several ranks; default: env REGNN_NS_GRAPH_ALLREDUCE=1): the RCCL
+        all-reduce and Adam are captured into the step's graph too, so a step is one replay with
+        no host-issued collective and no second graph boundary (and runs of 2 / 4 steps become
+        one replay, as with one rank). Off by default: the eager exchange is the tested path on
+        8 GPUs."""
+        import os
+        if exchange_in_graph is None:
+            exchange_in_graph = os.environ.get("REGNN_NS_GRAPH_ALLREDUCE") == "1"
+        multi = self.world > 1 or self._force_exchange
         if self.fused is None and not self._blocks_ok:
             raise ValueError("this model's module path reads exact-size adjs (a host sync per "
                              "step) and cannot be captured; run step() eagerly")
@@ -788,8 +802,10 @@ class NSTrainer:
         torch.cuda.synchronize(self.device)
         self.cur, self._primed, self._trained = 0, False, 0
         # one rank: the optimizer step joins the step's graph (no graph boundary, no host gap
-        # between the backward and Adam); several: the gradient all-reduce runs between graphs
-        fold_opt = self.world == 1
+        # between the backward and Adam); several: the gradient all-reduce runs between graphs,
+        # or inside the graph with exchange_in_graph
+        fold_opt = not multi or bool(exchange_in_graph)
+        in_graph = multi and fold_opt
         if self.pipelined:
             self._prime()                      # slot 0's batch, before the first replay
             torch.cuda.synchronize(self.device)
@@ -800,6 +816,8 @@ class NSTrainer:
                     # (Adam after the join: measured faster than before it, the graph then
                     # ends on one queue)
                     self._pipelined_body(cur)
+                    if in_graph:
+                        self._exchange()
                     if fold_opt:
                         self._opt_step()
                 g1.append(g)
@@ -813,12 +831,16 @@ class NSTrainer:
                     with torch.cuda.graph(g):
                         for i in range(n):
                             self._pipelined_body(i & 1)
+                            if in_graph:
+                                self._exchange()
                             self._opt_step()
                     self.graph_groups[n] = g
         else:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self._forward_backward()
+                if in_graph:
+                    self._exchange()
                 if fold_opt:
                     self._opt_step()
         g2 = None
@@ -855,6 +877,10 @@ class NSTrainer:
         if g2 is not None:
             self._exchange()
             g2.replay()
+
+    def param_vector(self):
+        """the parameters in model order without the bucket's alignment pads."""
+        return torch.cat([p.detach().reshape(-1) for p in self.params])
 
     def edges_total(self):
         """aggregated edges of every batch sampled so far (device counters: one host sync;

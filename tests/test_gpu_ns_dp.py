@@ -111,7 +111,8 @@ def _union_worker(rank, world, port, q):
         assert tr.fused is not None and tr.fused.two_layer and not tr.adam_fused
         assert tr.opt.grad_scale == 0.5
         one_step(tr, union[32 * rank:32 * (rank + 1)])
-        out = {"grad_sum": tr.flat.cpu().numpy().copy(), "param": tr.pflat.cpu().numpy().copy()}
+        out = {"grad_sum": tr.flat.cpu().numpy().copy(),
+               "param": tr.param_vector().cpu().numpy().copy()}
         dist.barrier()
         dist.destroy_process_group()
         if rank == 0:
@@ -119,7 +120,8 @@ def _union_worker(rank, world, port, q):
             assert tu.adam_fused
             one_step(tu, union)
             out["union_grad"] = tu.flat.cpu().numpy().copy()
-            out["union_param"] = tu.pflat.cpu().numpy().copy()
+            out["layout"] = [(o, p.numel()) for o, p in zip(tu.offsets, tu.params)]
+            out["union_param"] = tu.param_vector().cpu().numpy().copy()
             out["param0"] = torch.cat([p.detach().reshape(-1) for p in
                                        d["model"](5).parameters()]).cpu().numpy()
         q.put((rank, out))
@@ -148,7 +150,7 @@ def test_ns_dp_fused_union_equals_allreduced_halves():
     a, b = res[0], res[1]
     assert np.array_equal(a["grad_sum"], b["grad_sum"])
     assert np.array_equal(a["param"], b["param"])
-    g_dp = 0.5 * a["grad_sum"].astype(np.float64)
+    g_dp = 0.5 * a["grad_sum"].astype(np.float64)          # padded buckets, same layout
     g_u = a["union_grad"].astype(np.float64)
     scale = max(1e-3, float(np.abs(g_u).max()))
     assert np.abs(g_dp - g_u).max() <= 2e-6 * scale, np.abs(g_dp - g_u).max()
@@ -156,7 +158,61 @@ def test_ns_dp_fused_union_equals_allreduced_halves():
     # is not within rounding of zero
     moved = np.abs(a["union_param"] - a["param0"])
     assert moved.max() > 1e-3
-    sure = np.abs(g_u) > 1e-4 * scale
     d = np.abs(a["param"].astype(np.float64) - a["union_param"])
+    g_uv = np.concatenate([g_u[o:o + n] for o, n in a["layout"]])
+    sure = np.abs(g_uv) > 1e-4 * scale
     assert d[sure].max() <= 1e-6, d[sure].max()
     assert d.max() <= 2.01e-2
+
+
+def _graph_allreduce_worker(port, q):
+    try:
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "re-gnn_amd"))
+        from test_gpu_ns_engine import _mag
+        from regnn_hip.ns import NSTrainer
+        d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.3)
+
+        def make():
+            return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 64,
+                             torch.arange(d["n_paper"], device="cuda"), d["x_dict"],
+                             d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=9,
+                             adam=dict(lr=1e-2))
+        ta, tb = make(), make()
+        ta._force_exchange = True              # the RCCL all-reduce inside the captured graph
+        ta.capture(warmup=1, exchange_in_graph=True)
+        tb.capture(warmup=1)
+        assert ta.graphs[1] is None and sorted(ta.graph_groups) == [2, 4]
+        out = []
+        for i in range(3):
+            ta.run_steps(2) if i == 1 else ta.replay()
+            tb.run_steps(2) if i == 1 else tb.replay()
+            torch.cuda.synchronize()
+            out.append((float(ta.loss), float(tb.loss), bool(torch.equal(ta.pflat, tb.pflat))))
+        dist.destroy_process_group()
+        q.put(out)
+    except Exception as e:
+        import traceback
+        q.put(repr(e) + traceback.format_exc())
+
+
+def test_ns_allreduce_captured_in_step_graph():
+    """NSTrainer.capture(exchange_in_graph=True): the flat-bucket RCCL all-reduce captured inside
+    the step's HIP graph (one replay per step, runs of steps as one replay) on a one-rank NCCL
+    group; it must replay and train exactly as the one-rank graph without the exchange."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + ((os.getpid() + 250) % 1000)
+    p = ctx.Process(target=_graph_allreduce_worker, args=(port, q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert not isinstance(res, str), res
+    for la, lb, same in res:
+        assert la == lb and same

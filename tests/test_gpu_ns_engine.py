@@ -607,11 +607,9 @@ def test_fused_adam_equals_separate_adam(monkeypatch):
     # regnn_adam_flat (weight decay moves it) but, as torch.optim.Adam skips a parameter without
     # a gradient, not by the fused optimizer
     keep = torch.ones_like(a.pflat, dtype=torch.bool)
-    o = 0
-    for name, p in a.model.named_parameters():
+    for (name, p), o in zip(a.model.named_parameters(), a.offsets):
         if name.startswith("norm."):
             keep[o:o + p.numel()] = False
-        o += p.numel()
     for x, y in ((a.pflat, b.pflat), (a.opt.m, b.opt.m), (a.opt.v, b.opt.v)):
         x, y = x[keep], y[keep]
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), (x.double() - y.double()).abs().max()

@@ -1,0 +1,8 @@
+# DP tests (captured all-reduce), h512 NS bench at mag-10x, h512 epoch context at mag-1x
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out &&
+tools/gpu_step.sh 600 gpurun_out/t_dp.log python -u -m pytest tests/test_gpu_ns_dp.py -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
+grep -E "passed|failed|FAILED|Error" gpurun_out/t_dp.log | tail -8 &&
+tools/gpu_step.sh 300 gpurun_out/b_ns512.log python bench.py --workload ns --hidden 512 --no-full-batch --no-cpu-baseline &&
+grep '^{' gpurun_out/b_ns512.log | cut -c1-300 &&
+tools/gpu_step.sh 300 gpurun_out/b_epoch512.log python bench.py --workload ns_epoch --scale 1 --hidden 512 --no-cpu-baseline &&
+grep '^{' gpurun_out/b_epoch512.log | cut -c1-400
