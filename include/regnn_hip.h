@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 32). */
+/* ABI version (bumped on any signature change or addition; currently 33). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -747,6 +747,10 @@ typedef struct regnn_nsm_work {
     const int32_t* csc_long0;
     int32_t stride[REGNN_NSM_MAX_LAYERS];        /* per hop: 0 = CSR block, else its fixed stride */
     const int32_t* blk_cnt[REGNN_NSM_MAX_LAYERS]; /* per hop (strided): sampled edges per row */
+    int32_t part;             /* two-layer step: 0 = every launch; 1 = the forward, the head and
+                                 layer 1's transposed pass (agg0, head, gather); 2 = the rest
+                                 (bwd0, rel0, finalize). A caller orders other work between the
+                                 two parts (NSTrainer joins the sampler stream there). */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

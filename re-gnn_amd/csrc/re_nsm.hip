@@ -1569,8 +1569,10 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
     const bool rs = p->rel_slots != 0;
     if (rs && (!w->u_self || !w->u_rel || p->n_edge_types < 0 || p->n_edge_types + T > p->n_rel[0]))
         return REGNN_EINVAL;
+    if (w->part < 0 || w->part > 2) return REGNN_EINVAL;
     if (regnn_nsm2_covers(p)) return regnn_nsm2_step(p, w, stream);
-    // the fused optimizer and the strided blocks: two-layer step only
+    // the fused optimizer, the strided blocks and the split into parts: two-layer step only
+    if (w->part) return REGNN_EUNSUPPORTED;
     if (w->adam) return REGNN_EUNSUPPORTED;
     for (int h = 0; h < L; ++h)
         if (w->stride[h]) return REGNN_EUNSUPPORTED;

@@ -132,11 +132,17 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
     const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l];
     const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l];
     const float bj = A.bias[16 * w + c];
+    float lbj[NT];                         // lins[t].bias[16 w + c]: stage 1's bias terms
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) lbj[tt] = tt < T ? pick(A.lin_b.p, tt)[16 * w + c] : 0.f;
     PH(0, 0);
     __syncthreads();
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
         // ---- gather: per-type register sums of this lane's 4 * VPL features
         const int v = base + sub;
+        float iv4[4];                      // stage 2's row scales, requested before the gather
+#pragma unroll
+        for (int r = 0; r < 4; ++r) iv4[r] = base + 4 * q + r < n ? A.inv[base + 4 * q + r] : 0.f;
         float wsum[NT];
         float4 racc[NT][VPL];
         int rel_t[NT];
@@ -290,7 +296,9 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
             for (int r = 0; r < 4; ++r) {
                 const int vr = 4 * q + r;
                 float bsum = 0.f;
-                for (int tt = 0; tt < T; ++tt) bsum = fmaf(sw[vr * MT + tt], pick(A.lin_b.p, tt)[j], bsum);
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt)
+                    if (tt < T) bsum = fmaf(sw[vr * MT + tt], lbj[tt], bsum);
                 Pt[vr * 68 + j] = d[r] + bsum;
             }
         }
@@ -306,11 +314,7 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
                 MFMA4(av, wb[0], wb[F], wb[2 * F], wb[3 * F], d2);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int vr = 4 * q + r, vv = base + vr;
-                const float iv = vv < n ? A.inv[vv] : 0.f;
-                at[vr * F + 16 * w + c] = fmaf(iv, d2[r], bj);
-            }
+            for (int r = 0; r < 4; ++r) at[(4 * q + r) * F + 16 * w + c] = fmaf(iv4[r], d2[r], bj);
         }
         __syncthreads();
         // ---- epilogue: P and a kept, LayerNorm, relu, dropout -> h0
@@ -391,12 +395,23 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     __shared__ float tab[F];
     __shared__ float lrow[kRows];
     __shared__ int wcnt[kBlock / 64];
+    __shared__ float bo_s[16 * kMaxCT];    // out_lin.bias (classes >= C: 0)
     const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
     const int n = A.sizes[0];
     const int v = blockIdx.x * kRows + sub;
     const bool act = v < n;
     const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
+    // step 2's bias / row scales and step 4a's out_lin.bias, requested with the staging (their
+    // latency off the MFMA phases)
+    const float bj2 = A.bias[16 * w + cc];
+    float iv2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int vv = blockIdx.x * kRows + 4 * q + r;
+        iv2[r] = vv < n ? A.inv[vv] : 0.f;
+    }
+    for (int c = threadIdx.x; c < 16 * kMaxCT; c += kBlock) bo_s[c] = c < A.C ? A.b_out[c] : 0.f;
     {   // out_lin.weight -> LDS by LDS-DMA; lane L writes slot L%16 of row c, which holds
         // W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw); pad rows c >= C read row C-1
         const int L64 = threadIdx.x & 63;
@@ -468,13 +483,8 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             MFMA4(av, w1c[4 * b], w1c[4 * b + 1], w1c[4 * b + 2], w1c[4 * b + 3], d);
         }
         const int j = 16 * w + cc;
-        const float bj = A.bias[j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int vr = 4 * q + r, vv = blockIdx.x * kRows + vr;
-            const float iv = vv < n ? A.inv[vv] : 0.f;
-            ghs[vr * 68 + j] = fmaf(iv, d[r], bj);
-        }
+        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + j] = fmaf(iv2[r], d[r], bj2);
     }
     __syncthreads();
     // ---- 3. LayerNorm, relu, dropout
@@ -515,7 +525,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             const float4 bv = *reinterpret_cast<const float4*>(Wl + head_sw(c, 16 * b + 4 * q));
             MFMA4(av, bv.x, bv.y, bv.z, bv.w, dz);
         }
-        const float bo = c < C ? A.b_out[c] : 0.f;
+        const float bo = bo_s[c];
 #pragma unroll
         for (int r = 0; r < 4; ++r) zs[(4 * q + r) * CP + c] = c < C ? dz[r] + bo : -INFINITY;
     }
@@ -1383,7 +1393,7 @@ int64_t regnn_nsm2_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
 
 bool regnn_nsm2_covers(const regnn_nsm_params* p) {
     return p->n_layers == 2 && p->n_classes <= 16 * kMaxCT &&
-           head_lds(p->n_classes) <= size_t(160 * 1024 - 1024);
+           head_lds(p->n_classes) <= size_t(160 * 1024 - 2560);
 }
 
 int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
@@ -1406,8 +1416,9 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         lin_b.p[t] = p->lin_b[t];
         xt.p[t] = p->x_tab[t];
     }
+    const bool first = w->part != 2, second = w->part != 1;
     // 1. layer 0
-    {
+    if (first) {
         const int h = 1;
         Agg0Args A{};
         A.sizes = w->sizes; A.hop = h;
@@ -1440,7 +1451,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     }
     // 2. layer 1 + head + loss + backward to GH, transposed aggregation into layer 0's rows
     const int64_t hw = head_part_width(C);
-    {
+    if (first) {
         HeadArgs H{};
         H.sizes = w->sizes; H.n_id = w->n_id; H.labels = w->labels;
         H.ptr = w->blk_ptr[0]; H.cnt = w->blk_cnt[0]; H.stride = w->stride[0];
@@ -1458,7 +1469,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         REGNN_LAUNCH_CHECK();
     }
     // 3. layer 1's transposed aggregation (a gather), layer 0's LayerNorm backward
-    {
+    if (first) {
         GathArgs G{};
         G.sizes = w->sizes; G.hop = 1; G.cptr = w->csc_ptr0; G.cent = w->csc_ent0;
         G.clong = w->csc_long0; G.gh = w->gh1;
@@ -1469,6 +1480,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kBlock), 0, stream, G);
         REGNN_LAUNCH_CHECK();
     }
+    if (!second) return REGNN_OK;
     // 4. layer 0's backward
     {
         Bwd0Args B{};

@@ -15,12 +15,13 @@ synchronisation, so one training step is one HIP-graph replay.
 The sampled indices follow the build's sampler spec (oracle/sampler_oracle.py, bit-exact).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib as L
-from .profile import timed
+from .profile import enabled as profile_enabled, timed
 
 M64 = (1 << 64) - 1
 
@@ -262,7 +263,7 @@ class _NsmWork(ctypes.Structure):
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
                 ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P),
-                ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML)]
+                ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML), ("part", ctypes.c_int32)]
 
 
 class _NsmAdam(ctypes.Structure):
@@ -321,6 +322,9 @@ STRIDED = {"mode": "on"}
 # "on": a one-rank FlatAdam trainer runs Adam inside the two-layer step's last launch; "off":
 # the separate regnn_adam_flat launch (tests compare the two)
 FUSED_ADAM = {"mode": "on"}
+# "on": the pipelined trainer joins the sampler stream between the step's two parts (before
+# layer 0's backward); "off": after the whole step (A/B)
+SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
 # "on": the fused step's last sampler hop runs meta-only (no dedup / n_id append); "off": the
 # full hop (tests that inspect the outermost n_id / local ids)
 LEAN_LAST_HOP = {"mode": "on"}
@@ -486,7 +490,17 @@ class FusedStep:
     def launches(self):
         return len(self.kernels())
 
-    def step(self):
+    def step(self, part=0):
+        """part 0: the whole step; 1 / 2 (two-layer step): agg0 + head + gather / bwd0 +
+        finalize, so the caller can order other work (the sampler's join) between them."""
+        if part and not self.two_layer:
+            raise ValueError("the step splits into parts only in its two-layer form")
+        self.W.part = int(part)
+        if part == 2:
+            with torch.cuda.device(self.device):
+                L.call("regnn_nsm_step", ctypes.addressof(self.P), ctypes.addressof(self.W),
+                       torch.cuda.current_stream(self.device).cuda_stream)
+            return
         if not self.sampler.meta_fresh[self.n_layers - 1]:
             raise RuntimeError("run the sampler's hops after building FusedStep: layer 0 reads the "
                                "per-edge source type / table row they write")
@@ -666,10 +680,17 @@ class NSTrainer:
         # the model's launches are issued (captured) before the sampler's: the graph then runs
         # the model chain on the launch queue and the sampler on the second one, and the next
         # replay's first model kernel needs no cross-queue wait (243 -> 234 us per step)
-        self.fused_slots[cur].step()
+        fs = self.fused_slots[cur]
+        # (the profiled eager steps of bench.py time the step as one event: unsplit)
+        split = fs.two_layer and SPLIT_JOIN["mode"] != "off" and not profile_enabled()
+        fs.step(part=1 if split else 0)
         with torch.cuda.stream(self._side):
             self._sample(1 - cur)
+        # the join sits between layer 1's transposed pass and layer 0's backward (the sampler is
+        # done by then): the next step's first kernel then waits on its own queue only
         cs.wait_stream(self._side)
+        if split:
+            fs.step(part=2)
 
     def _prime(self):
         if not self._primed:

@@ -12,6 +12,10 @@ _enabled = False
 _events = {}
 
 
+def enabled():
+    return _enabled
+
+
 def enable(on=True):
     global _enabled
     _enabled = on
