@@ -144,14 +144,15 @@ ns_sample_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
         return;
     }
     int slot = -1;
-    int filled = 0;
-    for (int j = d - k; j < d; ++j) {
-        const uint32_t r = ns_hash(seed, uint64_t(t), uint64_t(j));
-        const int pos = int((uint64_t(r) * uint64_t(j + 1)) >> 32);
+    // lane i < k forms draw i's position up front (one hash per lane instead of k); the Floyd
+    // resolution then walks the draws in order
+    const int jl = d - k + lane;
+    const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
+                                       uint64_t(jl + 1)) >> 32) : 0;
+    for (int i = 0; i < k; ++i) {
+        const int pos = __shfl(my_pos, i, 64);
         const bool seen = __any(slot == pos);
-        const int pick = seen ? j : pos;
-        if (lane == filled) slot = pick;
-        ++filled;
+        if (lane == i) slot = seen ? d - k + i : pos;
     }
     int rank = 0;
     for (int m = 0; m < k; ++m) {
@@ -215,14 +216,13 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
         int slot = lane < d ? lane : -1, rank = lane;  // deg <= k: every position, in order
         if (d > k) {                               // Floyd (regnn_sample_fill's spec)
             slot = -1;
-            int filled = 0;
-            for (int j = d - k; j < d; ++j) {
-                const uint32_t r = ns_hash(seed, uint64_t(t), uint64_t(j));
-                const int pos = int((uint64_t(r) * uint64_t(j + 1)) >> 32);
+            const int jl = d - k + lane;         // draw i's position formed by lane i up front
+            const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
+                                               uint64_t(jl + 1)) >> 32) : 0;
+            for (int i = 0; i < k; ++i) {
+                const int pos = __shfl(my_pos, i, 64);
                 const bool seen = __any(slot == pos);
-                const int pick = seen ? j : pos;
-                if (lane == filled) slot = pick;
-                ++filled;
+                if (lane == i) slot = seen ? d - k + i : pos;
             }
             rank = 0;
             for (int m = 0; m < k; ++m) {
