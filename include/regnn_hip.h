@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 33). */
+/* ABI version (bumped on any signature change or addition; currently 34). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -623,13 +623,16 @@ int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const 
  * reference's per-type Linear over every sampled node and x_src @ W before propagate):
  *   S[v][t][:] = sum_{e in row v, ntype[n_id[idx_e]] = t} rel_table[rel_e] tables[t][local[n_id[idx_e]]][:]
  *   wsum[v][t] = sum over the same edges of rel_table[rel_e]
- * for v < n_rows (rows with ptr[v] == ptr[v + 1] get zeros). The caller projects
+ * for v < n_rows (rows with ptr[v] == ptr[v + 1] get zeros). With e_type / e_off (a meta-only
+ * hop's per-edge source node type and table row, regnn_ns_hop) the edge's type and row are read
+ * from them and idx / n_id / ntype / local may be null. The caller projects
  * a = inv (S W_c + wsum b_c) + bias with W_c[t] = W_t^T W_0, b_c[t] = b_t W_0 (linearity).
  * K in {64, 128} fp32 (rows 16-byte aligned), 1 <= n_types <= 8, tables[t] non-null. */
 int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                        const float* rel_table, const int32_t* n_id, const int32_t* ntype,
-                       const int64_t* local, const float* const* tables, int32_t n_types,
-                       int32_t K, int64_t n_rows, float* S, float* wsum, hipStream_t stream);
+                       const int64_t* local, const int32_t* e_type, const int64_t* e_off,
+                       const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
+                       float* S, float* wsum, hipStream_t stream);
 
 /* Relation-table gradient of regnn_ns_typed_agg: slab[b][r] = block b's partial of
  * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (LDS float atomics: the
@@ -637,6 +640,7 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
  * the slab with regnn_rel_reduce. n_rel <= 256. */
 int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            const int32_t* n_id, const int32_t* ntype, const int64_t* local,
+                           const int32_t* e_type, const int64_t* e_off,
                            const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
                            const float* gS, const float* gw, float* slab, int32_t n_rel,
                            int32_t slab_rows, hipStream_t stream);
@@ -659,12 +663,12 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
  * (state[3] << 8) ^ (layer + 0x51ED27))) (seed, epoch, global batch), row = target row of the
  * layer's block, 4 features per 16-byte vector.
  *
- * L = 2 (the reference's default num_layers; C <= 432): 5 launches (6 without rel_slots), the
+ * L = 2 (the reference's default num_layers; C <= 416): 5 launches (6 without rel_slots), the
  * group_input Linear and each conv's x @ W applied after their layer's aggregation (linearity:
  * mean_e(ew x_e) W = mean_e(ew x_e W)), the transposed aggregation of layer 1 as 2^-40
  * fixed-point integer sums, every other reduction fixed-order: the step is bitwise
  * reproducible; optionally the Adam update of regnn_nsm_work.adam in the last launch.
- * L = 3, 4 (or C > 432): the composed-map form above, 8+ launches, layer >= 1 transposed
+ * L = 3, 4 (or C > 416): the composed-map form above, 8+ launches, layer >= 1 transposed
  * aggregations with float atomics (as regnn_ns_spmm_bwd).
  * --------------------------------------------------------------------------------------- */
 #define REGNN_NSM_MAX_TYPES 8
@@ -738,7 +742,7 @@ typedef struct regnn_nsm_work {
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
     float* u_self;            /* rel_slots: cap[L-1] * k_in, each row's self-loop input row */
     int32_t* u_rel;           /* rel_slots: cap[L-1] * (T + 1), relation of each source-type slot */
-    /* the two-layer step (L = 2, C <= 432, hop 0's edge capacity <= 32768): */
+    /* the two-layer step (L = 2, C <= 416, hop 0's edge capacity <= 32768): */
     float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
     const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
     float* gh1;               /* cap[0] * 64: G W_1^T of layer 1's target rows (its transposed pass) */

@@ -36,18 +36,27 @@ __device__ __forceinline__ const float* pick_tab(const Tabs& t, int i) {
 // one edge's metadata, formed by one lane of the row's group (its four dependent loads run in
 // parallel over the row's edges) and broadcast to the group: source type, source row in its
 // type's table, tab[r_e] (tab may be null), relation id
+// (e_type / e_off: the sampler's per-edge source type and table row of a meta-only hop, read
+// directly instead of through the local id, n_id, node type and local row)
+struct EdgeSrc {
+    const int32_t* idx; const int32_t* n_id; const int32_t* ntype; const int64_t* local;
+    const int32_t* e_type; const int64_t* e_off;
+};
+
 template <int LPR>
-__device__ __forceinline__ void edge_meta(const int32_t* idx, const uint8_t* rel, const float* tab,
-                                          const int32_t* n_id, const int32_t* ntype,
-                                          const int64_t* local, int e, int e1, int& t,
-                                          int64_t& row, float& w, int& r) {
+__device__ __forceinline__ void edge_meta(const EdgeSrc& E, const uint8_t* rel, const float* tab,
+                                          int e, int e1, int& t, int64_t& row, float& w, int& r) {
     t = 0; row = 0; w = 0.f; r = 0;
     if (e < e1) {
-        const int u = idx[e];
         r = rel[e];
-        const int g = n_id[u];
-        t = ntype[g];
-        row = local[g];
+        if (E.e_type) {
+            t = E.e_type[e];
+            row = E.e_off[e];
+        } else {
+            const int g = E.n_id[E.idx[e]];
+            t = E.ntype[g];
+            row = E.local[g];
+        }
         w = tab ? tab[r] : 0.f;
     }
 }
@@ -55,10 +64,8 @@ __device__ __forceinline__ void edge_meta(const int32_t* idx, const uint8_t* rel
 // S [n_rows][T][K], w [n_rows][T]. LPR = K / 4 lanes per row, 64 / LPR rows per wave.
 template <int K, int NT>
 __global__ void __launch_bounds__(kBlock)
-typed_agg_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
-                 const uint8_t* __restrict__ rel, const float* __restrict__ tab,
-                 const int32_t* __restrict__ n_id, const int32_t* __restrict__ ntype,
-                 const int64_t* __restrict__ local, Tabs xt, int T, int64_t n_rows,
+typed_agg_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __restrict__ rel,
+                 const float* __restrict__ tab, Tabs xt, int T, int64_t n_rows,
                  float* __restrict__ S, float* __restrict__ wsum) {
     constexpr int LPR = K / 4;
     constexpr int RPW = 64 / LPR;
@@ -81,7 +88,7 @@ typed_agg_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
             int mt, mr;
             int64_t mrow;
             float mw;
-            edge_meta<LPR>(idx, rel, tab, n_id, ntype, local, c + l, e1, mt, mrow, mw, mr);
+            edge_meta<LPR>(E, rel, tab, c + l, e1, mt, mrow, mw, mr);
             const int m = min(LPR, e1 - c);
             for (int j = 0; j < m; j += UN) {
                 float4 x[UN];
@@ -128,10 +135,8 @@ typed_agg_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
 // row [n_rel] per block (the caller reduces the slab in a fixed order)
 template <int K, int NT>
 __global__ void __launch_bounds__(kBlock)
-typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
-                     const uint8_t* __restrict__ rel, const int32_t* __restrict__ n_id,
-                     const int32_t* __restrict__ ntype, const int64_t* __restrict__ local, Tabs xt,
-                     int T, int64_t n_rows, const float* __restrict__ gS,
+typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __restrict__ rel,
+                     Tabs xt, int T, int64_t n_rows, const float* __restrict__ gS,
                      const float* __restrict__ gw, float* __restrict__ slab, int n_rel) {
     constexpr int LPR = K / 4;
     constexpr int RPW = 64 / LPR;
@@ -156,7 +161,7 @@ typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict_
             int mt, mr;
             int64_t mrow;
             float mw;
-            edge_meta<LPR>(idx, rel, nullptr, n_id, ntype, local, c + l, e1, mt, mrow, mw, mr);
+            edge_meta<LPR>(E, rel, nullptr, c + l, e1, mt, mrow, mw, mr);
             (void)mw;
             const int m = min(LPR, e1 - c);
             for (int j = 0; j < m; j += UN) {
@@ -196,12 +201,22 @@ using namespace regnn::nsagg;
 
 extern "C" {
 
+static bool edge_src(const int32_t* idx, const int32_t* n_id, const int32_t* ntype,
+                     const int64_t* local, const int32_t* e_type, const int64_t* e_off,
+                     EdgeSrc& E) {
+    E = EdgeSrc{idx, n_id, ntype, local, e_type, e_off};
+    if (e_type || e_off) return e_type && e_off;
+    return idx && n_id && ntype && local;
+}
+
 int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                        const float* rel_table, const int32_t* n_id, const int32_t* ntype,
-                       const int64_t* local, const float* const* tables, int32_t n_types,
-                       int32_t K, int64_t n_rows, float* S, float* wsum, hipStream_t stream) {
-    if (!ptr || !idx || !rel || !rel_table || !n_id || !ntype || !local || !tables || !S ||
-        !wsum || n_types <= 0 || n_types > kMT || n_rows < 0)
+                       const int64_t* local, const int32_t* e_type, const int64_t* e_off,
+                       const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
+                       float* S, float* wsum, hipStream_t stream) {
+    EdgeSrc E;
+    if (!ptr || !rel || !rel_table || !tables || !S || !wsum || n_types <= 0 || n_types > kMT ||
+        n_rows < 0 || !edge_src(idx, n_id, ntype, local, e_type, e_off, E))
         return REGNN_EINVAL;
     Tabs xt{};
     for (int t = 0; t < n_types; ++t) {
@@ -216,8 +231,7 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
 #define AGG_CASE(KK, N)                                                                        \
     if (K == KK && n_types <= N) {                                                             \
         hipLaunchKernelGGL((typed_agg_kernel<KK, N>), dim3((unsigned)grid), dim3(kBlock), 0,   \
-                           stream, ptr, idx, rel, rel_table, n_id, ntype, local, xt, n_types,  \
-                           n_rows, S, wsum);                                                   \
+                           stream, ptr, E, rel, rel_table, xt, n_types, n_rows, S, wsum);      \
         REGNN_LAUNCH_CHECK();                                                                  \
         return REGNN_OK;                                                                       \
     }
@@ -228,12 +242,14 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
 
 int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            const int32_t* n_id, const int32_t* ntype, const int64_t* local,
+                           const int32_t* e_type, const int64_t* e_off,
                            const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
                            const float* gS, const float* gw, float* slab, int32_t n_rel,
                            int32_t slab_rows, hipStream_t stream) {
-    if (!ptr || !idx || !rel || !n_id || !ntype || !local || !tables || !gS || !gw || !slab ||
-        n_types <= 0 || n_types > kMT || n_rows < 0 || n_rel <= 0 || n_rel > 256 ||
-        slab_rows <= 0)
+    EdgeSrc E;
+    if (!ptr || !rel || !tables || !gS || !gw || !slab || n_types <= 0 || n_types > kMT ||
+        n_rows < 0 || n_rel <= 0 || n_rel > 256 || slab_rows <= 0 ||
+        !edge_src(idx, n_id, ntype, local, e_type, e_off, E))
         return REGNN_EINVAL;
     Tabs xt{};
     for (int t = 0; t < n_types; ++t) {
@@ -243,8 +259,8 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
 #define BWD_CASE(KK, N)                                                                        \
     if (K == KK && n_types <= N) {                                                             \
         hipLaunchKernelGGL((typed_agg_bwd_kernel<KK, N>), dim3((unsigned)slab_rows),           \
-                           dim3(kBlock), 0, stream, ptr, idx, rel, n_id, ntype, local, xt,     \
-                           n_types, n_rows, gS, gw, slab, n_rel);                              \
+                           dim3(kBlock), 0, stream, ptr, E, rel, xt, n_types, n_rows, gS, gw,  \
+                           slab, n_rel);                                                       \
         REGNN_LAUNCH_CHECK();                                                                  \
         return REGNN_OK;                                                                       \
     }

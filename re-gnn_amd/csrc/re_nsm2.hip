@@ -43,7 +43,7 @@ inline int env_blocks(const char* name, int dflt) {
     return v >= 16 && v <= 4096 ? v : dflt;
 }
 static const int kBwdBlocks = env_blocks("REGNN_NSM_BWD_BLOCKS", 128);
-constexpr int kMaxCT = 27;                 // class tiles of 16 (C <= 432: the head's LDS)
+constexpr int kMaxCT = 27;                 // class tiles of 16 (the head's LDS holds C <= 416)
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
 
@@ -376,13 +376,17 @@ __host__ __device__ inline int head_wl(int C) {
     return wl > red ? wl : red;
 }
 inline size_t head_lds(int C) {
-    return (size_t(head_wl(C)) + 16 * head_cp(C) + 16 * 68 + 16 * 80 + 16 * 68 + 16 * 68) *
-           sizeof(float);
+    return (size_t(head_wl(C)) + 16 * head_cp(C) + 16 * 68 + 16 * 80 + 16 * 68 + 16 * 68 +
+            16 * 68) * sizeof(float);
 }
 
 __device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c & 15) << 2)); }
 
-__global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
+// 8 waves: the row phases (16 rows x 16 lanes) run on threads 0..255, the class-tile loops (logits,
+// gh, the out_lin partial) on all 8 waves
+constexpr int kHeadThreads = 512;
+
+__global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
     extern __shared__ float hl[];
     const int C = A.C, CT = (C + 15) / 16, CP = head_cp(C);
     float* Wl = hl;                        // W_out image; after step 4: red [3][16][64]
@@ -391,31 +395,34 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     float* hs2 = hs + 16 * 68;             // [16][80]: h (column reads)
     float* ghs = hs2 + 16 * 80;            // [16][68]: a, then gh
     float* hg = ghs + 16 * 68;             // [16][68]: Hagg
+    float* ghp = hg + 16 * 68;             // [16][68]: gh over the second half of the classes
     float* red = Wl;
     __shared__ float tab[F];
     __shared__ float lrow[kRows];
-    __shared__ int wcnt[kBlock / 64];
+    __shared__ int wcnt[kHeadThreads / 64];
     __shared__ float bo_s[16 * kMaxCT];    // out_lin.bias (classes >= C: 0)
-    const int l = threadIdx.x & 15, sub = threadIdx.x >> 4, gl = threadIdx.x & 48;
+    const bool rowt = threadIdx.x < kBlock;    // the row phases' threads
+    const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 15, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
+    const int wq = w & 3, wh = w >> 2;        // feature tile, class half (step 4c)
     const int n = A.sizes[0];
     const int v = blockIdx.x * kRows + sub;
-    const bool act = v < n;
+    const bool act = rowt && v < n;
     const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
     // step 2's bias / row scales and step 4a's out_lin.bias, requested with the staging (their
     // latency off the MFMA phases)
-    const float bj2 = A.bias[16 * w + cc];
+    const float bj2 = A.bias[16 * wq + cc];
     float iv2[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int vv = blockIdx.x * kRows + 4 * q + r;
         iv2[r] = vv < n ? A.inv[vv] : 0.f;
     }
-    for (int c = threadIdx.x; c < 16 * kMaxCT; c += kBlock) bo_s[c] = c < A.C ? A.b_out[c] : 0.f;
+    for (int c = threadIdx.x; c < 16 * kMaxCT; c += kHeadThreads) bo_s[c] = c < A.C ? A.b_out[c] : 0.f;
     {   // out_lin.weight -> LDS by LDS-DMA; lane L writes slot L%16 of row c, which holds
         // W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw); pad rows c >= C read row C-1
         const int L64 = threadIdx.x & 63;
-        for (int i = threadIdx.x >> 6; i < CT * 4; i += kBlock / 64) {
+        for (int i = threadIdx.x >> 6; i < CT * 4; i += kHeadThreads / 64) {
             const int c = 4 * i + (L64 >> 4);
             const int cs = c < C ? c : C - 1;
             const float* src = A.w_out + int64_t(cs) * F + 4 * ((L64 & 15) ^ (c & 15));
@@ -428,10 +435,10 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) w1c[4 * b + i] = A.w1[(16 * b + 4 * q + i) * F + 16 * w + cc];
+        for (int i = 0; i < 4; ++i) w1c[4 * b + i] = A.w1[(16 * b + 4 * q + i) * F + 16 * wq + cc];
     {   // the labelled-target count nll_loss divides by, while the DMA lands
         int cnt_valid = 0;
-        for (int i = threadIdx.x; i < n; i += kBlock) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+        for (int i = threadIdx.x; i < n; i += kHeadThreads) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) cnt_valid += __shfl_xor(cnt_valid, o, 64);
         if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = cnt_valid;
@@ -470,12 +477,12 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
                 }
             }
         }
-        *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
+        if (rowt) *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
     }
     __syncthreads();
     PH(1, 2);
     // ---- 2. a = inv (Hagg W_1) + bias -> ghs
-    {
+    if (w < 4) {
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -509,14 +516,17 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             hv[i] = fmaxf(fmaf(xhat[i], gwf[i], gbf[i]), 0.f) * mfac[i];
         }
     }
-    *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-    *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    if (rowt) {
+        *reinterpret_cast<float4*>(hs + sub * 68 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        *reinterpret_cast<float4*>(hs2 + sub * 80 + 4 * l) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    }
     __syncthreads();
     PH(1, 3);
-    const int n_valid = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+    const int n_valid = ((wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3])) +
+                        ((wcnt[4] + wcnt[5]) + (wcnt[6] + wcnt[7]));
     if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     // ---- 4a. z = h W^T + b -> zs (classes >= C: -inf)
-    for (int ct = w; ct < CT; ct += kBlock / 64) {
+    for (int ct = w; ct < CT; ct += kHeadThreads / 64) {
         const int c = 16 * ct + cc;
         f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -531,7 +541,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     }
     __syncthreads();
     // ---- 4b. log_softmax, nll, g
-    {                                      // lane l holds classes l + 16 i of row sub
+    if (rowt) {                            // lane l holds classes l + 16 i of row sub
         float zr[kMaxCT];
         float zmax = -INFINITY;
 #pragma unroll
@@ -560,9 +570,10 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
         }
     }
     __syncthreads();
-    // ---- 4c. gh = g W: wave w -> features 16 w + cc, rows 4 q + r
+    // ---- 4c. gh = g W: wave w -> features 16 wq + cc, rows 4 q + r, class tiles of half wh
     {
-        const int k = 16 * w + cc;
+        const int k = 16 * wq + cc;
+        const int cth = (CT + 1) / 2, b0 = wh ? cth : 0, b1 = wh ? CT : cth;
         auto step = [&](int b, f32x4 d) {
             const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
             const int c0 = 16 * b + 4 * q;
@@ -572,14 +583,15 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
             return d;
         };
         f32x4 dg0 = {0.f, 0.f, 0.f, 0.f}, dg1 = {0.f, 0.f, 0.f, 0.f};
-        int b = 0;
-        for (; b + 1 < CT; b += 2) {
+        int b = b0;
+        for (; b + 1 < b1; b += 2) {
             dg0 = step(b, dg0);
             dg1 = step(b + 1, dg1);
         }
-        if (b < CT) dg0 = step(b, dg0);
+        if (b < b1) dg0 = step(b, dg0);
+        float* gd = wh ? ghp : ghs;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
+        for (int r = 0; r < 4; ++r) gd[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
     }
     __syncthreads();
     PH(1, 4);
@@ -587,10 +599,11 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     float4 w1r[4];                         // W_1[16 w + cc][16 b + 4 q ..]: step 6's B operand
 #pragma unroll
     for (int b = 0; b < 4; ++b)
-        w1r[b] = *reinterpret_cast<const float4*>(A.w1 + (16 * w + cc) * F + 16 * b + 4 * q);
-    {
-        const float4 g4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
-        const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+        w1r[b] = *reinterpret_cast<const float4*>(A.w1 + (16 * wq + cc) * F + 16 * b + 4 * q);
+    if (rowt) {
+        const float4 ga4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
+        const float4 gb4 = *reinterpret_cast<const float4*>(ghp + sub * 68 + 4 * l);
+        const float g[4] = {ga4.x + gb4.x, ga4.y + gb4.y, ga4.z + gb4.z, ga4.w + gb4.w};
         float gy[4], gx[4];
         float p1 = 0.f, p2 = 0.f;
 #pragma unroll
@@ -617,7 +630,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
     const int64_t o_w1 = head_o_w1(C);
     // ---- 5. out_lin weight partial D[c][k] = sum_v g[v][c] h[v][k], its bias, row terms
-    for (int ct = w; ct < CT; ct += kBlock / 64) {
+    for (int ct = w; ct < CT; ct += kHeadThreads / 64) {
         f32x4 dw[4];
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) dw[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -637,7 +650,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
                 if (c < C) o[int64_t(c) * F + 16 * kb + cc] = dw[kb][r];
             }
     }
-    for (int c = threadIdx.x; c < C; c += kBlock) {
+    for (int c = threadIdx.x; c < C; c += kHeadThreads) {
         float acc = 0.f;
 #pragma unroll
         for (int r = 0; r < kRows; ++r) acc += zs[r * CP + c];
@@ -658,7 +671,7 @@ __global__ void __launch_bounds__(kBlock) head_kernel(HeadArgs A) {
     }
     PH(1, 5);
     // ---- 6. GH = G W_1^T -> HBM; W_1 partial D[k][j] = sum_v Hagg[v][k] G[v][j]
-    {
+    if (w < 4) {
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -1465,7 +1478,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         static size_t done = 0;
         if (!set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
             return REGNN_EUNSUPPORTED;
-        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kBlock), lds, stream, H);
+        hipLaunchKernelGGL(head_kernel, dim3(S.head_blocks), dim3(kHeadThreads), lds, stream, H);
         REGNN_LAUNCH_CHECK();
     }
     // 3. layer 1's transposed aggregation (a gather), layer 0's LayerNorm backward

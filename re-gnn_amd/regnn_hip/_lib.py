@@ -91,8 +91,8 @@ _SIG = {
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_ns_spmm_bwd_csc": ([P, P, P, P, P, P, P, P, P, I32, P, I32, I64, I32, I32, P],
                               ctypes.c_int),
-    "regnn_ns_typed_agg": ([P, P, P, P, P, P, P, P, I32, I32, I64, P, P, P], ctypes.c_int),
-    "regnn_ns_typed_agg_bwd": ([P, P, P, P, P, P, P, I32, I32, I64, P, P, P, I32, I32, P],
+    "regnn_ns_typed_agg": ([P, P, P, P, P, P, P, P, P, P, I32, I32, I64, P, P, P], ctypes.c_int),
+    "regnn_ns_typed_agg_bwd": ([P, P, P, P, P, P, P, P, P, I32, I32, I64, P, P, P, I32, I32, P],
                                ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
@@ -112,7 +112,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 33
+ABI_VERSION = 34
 if _so.regnn_abi_version() != ABI_VERSION:
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "
                       "rebuild the library")

@@ -404,6 +404,16 @@ class REGNN(torch.nn.Module):
             self._ftab = cache = (sig, table, offs)
         return cache[1], cache[2]
 
+    def typed_first_layer_ok(self, x_dict):
+        """True when _typed_first_layer takes layer 0 of a device-block batch (NSTrainer then lets
+        the sampler's last hop run meta-only: nothing reads its sources' local ids)."""
+        if (TYPED_AGG["mode"] == "off" or self.model != 'regcn' or self.feats_type == 2 or
+                self.self_loop_type != 2):
+            return False
+        tabs = self._type_tables(x_dict)
+        return (tabs is not None and ops.ns_typed_agg_ok(tabs) and
+                self.convs[0].relation_weight.numel() <= 256)
+
     def _typed_first_layer(self, n_id, x_dict, adjs, node_type, local_node_idx):
         """layer 0 over a device block with group_input folded in (None: not applicable).
 
@@ -448,6 +458,9 @@ class REGNN(torch.nn.Module):
     def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
         ntype = node_type[n_id]
         x = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx)
+        if x is None and adjs and getattr(tuple(adjs[0])[0], "meta_only", False):
+            raise RuntimeError("layer 0's block was sampled meta-only (no local source ids): "
+                               "only the typed first layer (TYPED_AGG) can read it")
         start = 0
         if x is not None:                      # layer 0 done (group_input folded in)
             ntype = ntype[:tuple(adjs[0])[2][1]]

@@ -275,8 +275,8 @@ class _NsmAdam(ctypes.Structure):
                 ("step", _P), ("ticket", _P)]
 
 
-# regnn_nsm_step's two-layer form (re_nsm2.hip): L = 2 and at most 432 classes (its head's LDS)
-TWO_LAYER_MAX_CLASSES = 432
+# regnn_nsm_step's two-layer form (re_nsm2.hip): L = 2 and at most 416 classes (its head's LDS)
+TWO_LAYER_MAX_CLASSES = 416
 
 
 def fused_unsupported(model, x_dict):
@@ -325,6 +325,9 @@ FUSED_ADAM = {"mode": "on"}
 # "on": the pipelined trainer joins the sampler stream between the step's two parts (before
 # layer 0's backward); "off": after the whole step (A/B)
 SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
+# "on": the module path's last hop runs meta-only when the model's layer 0 is the typed first
+# layer (mag.REGNN.typed_first_layer_ok); "off": the full hop (A/B, tests)
+MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
 # "on": the fused step's last sampler hop runs meta-only (no dedup / n_id append); "off": the
 # full hop (tests that inspect the outermost n_id / local ids)
 LEAN_LAST_HOP = {"mode": "on"}
@@ -609,6 +612,18 @@ class NSTrainer:
         if engine != "module" and why is None:
             self.fused = FusedStep(model, self.slots[0], x_dict, node_type, local_node_idx,
                                    self.y_flat, self.loss)
+        self._module_lean = False
+        if (self.fused is None and self._blocks_ok and MODULE_LEAN_HOP["mode"] != "off" and
+                getattr(model, "typed_first_layer_ok", lambda _x: False)(x_dict)):
+            # layer 0 reads its block through the sampler's per-edge source type / table row
+            # (mag.REGNN._typed_first_layer): the last hop runs meta-only, as for the fused step
+            s0 = self.slots[0]
+            last = len(s0.sizes_k) - 1
+            et, eo = s0.enable_edge_meta(local_node_idx, last)
+            s0.meta_only[last] = True
+            blk = s0.blocks[last]
+            blk.edge_meta, blk.meta_only = (et, eo), True
+            self._module_lean = True
         if self.fused is None and self._blocks_ok:
             # the module path's last layer (hop 0's block) differentiates through a gather over
             # the sampler's transposed index of that block (regnn_ns_spmm_bwd_csc: no float
@@ -714,7 +729,7 @@ class NSTrainer:
         self._trained = 0
         s.batch_from_perm(self.perm, self.rank, self.world)
         # the module path reads n_id, the local ids and the CSR blocks
-        s.run_hops(meta_only=False, strided=False)
+        s.run_hops(meta_only=self._module_lean, strided=False)
         if self._blocks_ok:
             B = s.B
             n_id = s.n_id.to(torch.int64)

@@ -645,14 +645,22 @@ class _NsTypedAgg(torch.autograd.Function):
         S = torch.empty(blk.n_dst, T, K, dtype=torch.float32, device=dev)
         w = torch.empty(blk.n_dst, T, dtype=torch.float32, device=dev)
         t = tab.detach().float().contiguous()
-        n_id = _i32(n_id)
-        node_type, local_idx = _cached_cast(node_type, torch.int32), _cached_cast(local_idx, torch.int64)
+        meta = getattr(blk, "edge_meta", None)
+        if meta is not None:
+            # a meta-only hop: each edge's source type / table row straight from the sampler
+            n_id = node_type = local_idx = None
+            e_type, e_off = meta
+        else:
+            n_id = _i32(n_id)
+            node_type = _cached_cast(node_type, torch.int32)
+            local_idx = _cached_cast(local_idx, torch.int64)
+            e_type = e_off = None
         arr = _ptr_array([L.ptr(x) for x in tables])
         with timed("ns_typed_agg", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
             L.call("regnn_ns_typed_agg", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx), L.ptr(blk.rel),
-                   L.ptr(t), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx), arr, T, K,
-                   blk.n_dst, L.ptr(S), L.ptr(w), L.stream())
-        ctx.blk, ctx.tables, ctx.idx = blk, tables, (n_id, node_type, local_idx)
+                   L.ptr(t), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx), L.ptr(e_type),
+                   L.ptr(e_off), arr, T, K, blk.n_dst, L.ptr(S), L.ptr(w), L.stream())
+        ctx.blk, ctx.tables, ctx.idx = blk, tables, (n_id, node_type, local_idx, e_type, e_off)
         ctx.n_rel, ctx.tab_shape = t.numel(), tab.shape
         return S, w
 
@@ -661,7 +669,7 @@ class _NsTypedAgg(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             return (None,) * 6
         blk, tables = ctx.blk, ctx.tables
-        n_id, node_type, local_idx = ctx.idx
+        n_id, node_type, local_idx, e_type, e_off = ctx.idx
         T, K = len(tables), int(tables[0].shape[1])
         dev = tables[0].device
         gS = torch.zeros(blk.n_dst, T, K, device=dev) if gS is None else gS.contiguous().float()
@@ -671,6 +679,7 @@ class _NsTypedAgg(torch.autograd.Function):
         with timed("ns_typed_agg_bwd", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
             L.call("regnn_ns_typed_agg_bwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
                    L.ptr(blk.rel), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx),
+                   L.ptr(e_type), L.ptr(e_off),
                    _ptr_array([L.ptr(x) for x in tables]), T, K, blk.n_dst, L.ptr(gS), L.ptr(gw),
                    L.ptr(slab), ctx.n_rel, rows, L.stream())
         return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None, None, None
