@@ -138,6 +138,20 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
     PH(0, 0);
     __syncthreads();
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
+        // stage 1's first two W_t fragments are requested before the gather (their L2 latency
+        // under it); stage 1 then keeps two fragments in flight
+        constexpr int PD = NT <= 4 ? 2 : 1;      // fragments in flight (8 node types: 1, VGPRs)
+        float4 bq[PD + 1][HB];
+        auto bload = [&](int step, float4 (&dst)[HB]) {
+            const int tt = step >> 1, h0 = (step & 1) * HB;
+            const float* wt = pick(A.lin_w.p, tt) + (16 * w + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+        };
+        if constexpr (PD == 2) {                     // 2 T >= 2: a type has two halves
+            bload(0, bq[0]);
+            bload(1, bq[1]);
+        }
         // ---- gather: per-type register sums of this lane's 4 * VPL features
         const int v = base + sub;
         float iv4[4];                      // stage 2's row scales, requested before the gather
@@ -227,16 +241,8 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
                 }
             }
         }
-        // the first stage's first W_t fragment is requested before the S tile's stores
-        float4 bcur[HB], bnext[HB];
-        auto bload = [&](int step, float4 (&dst)[HB]) {
-            const int tt = step >> 1, h0 = (step & 1) * HB;
-            const float* wt = pick(A.lin_w.p, tt) + (16 * w + c) * K + 4 * q + 16 * h0;
-#pragma unroll
-            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
-        };
         PH(0, 1);
-        bload(0, bcur);
+        if constexpr (PD == 1) bload(0, bq[0]);      // (8 node types: after the gather)
         const int tau = r_self - A.n_et;           // RS: the row's node type
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
@@ -279,16 +285,32 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
         // ---- stage 1: P[v][j] = sum_t S_vt W_t[j][:] + w_vt b_t[j]; type t + 1's rows of W_t
         // are loaded while type t's products run
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
-        for (int step = 0; step < 2 * T; ++step) {
-            if (step + 1 < 2 * T) bload(step + 1, bnext);
-            const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
+        if constexpr (PD == 2) {
 #pragma unroll
-            for (int b = 0; b < HB; ++b) {
-                const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
-                MFMA4(av, bcur[b].x, bcur[b].y, bcur[b].z, bcur[b].w, d);
+            for (int step = 0; step < 2 * NT; ++step) {
+                if (step < 2 * T) {
+                    if (step + 2 < 2 * T) bload(step + 2, bq[(step + 2) % 3]);
+                    const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
+#pragma unroll
+                    for (int b = 0; b < HB; ++b) {
+                        const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                        const float4 bv = bq[step % 3][b];
+                        MFMA4(av, bv.x, bv.y, bv.z, bv.w, d);
+                    }
+                }
             }
+        } else {
+            for (int step = 0; step < 2 * T; ++step) {
+                if (step + 1 < 2 * T) bload(step + 1, bq[1]);
+                const float* sa = St + c * SR + (step >> 1) * K + 16 * (step & 1) * HB + 4 * q;
 #pragma unroll
-            for (int b = 0; b < HB; ++b) bcur[b] = bnext[b];
+                for (int b = 0; b < HB; ++b) {
+                    const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                    MFMA4(av, bq[0][b].x, bq[0][b].y, bq[0][b].z, bq[0][b].w, d);
+                }
+#pragma unroll
+                for (int b = 0; b < HB; ++b) bq[0][b] = bq[1][b];
+            }
         }
         {
             const int j = 16 * w + c;
