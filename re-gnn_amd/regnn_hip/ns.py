@@ -325,6 +325,10 @@ FUSED_ADAM = {"mode": "on"}
 # "on": the pipelined trainer joins the sampler stream between the step's two parts (before
 # layer 0's backward); "off": after the whole step (A/B)
 SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
+# "on": the module path (device blocks) samples the next batch on a second stream while the
+# model trains on this one, as the fused step does; "off" (default: at hidden 512, mag-10x the
+# overlapped sampler slowed the dense kernels more than it hid, 1.045 -> 1.09 ms per step)
+MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "off")}
 # "on": the module path's last hop runs meta-only when the model's layer 0 is the typed first
 # layer (mag.REGNN.typed_first_layer_ok); "off": the full hop (A/B, tests)
 MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
@@ -612,34 +616,24 @@ class NSTrainer:
         if engine != "module" and why is None:
             self.fused = FusedStep(model, self.slots[0], x_dict, node_type, local_node_idx,
                                    self.y_flat, self.loss)
-        self._module_lean = False
-        if (self.fused is None and self._blocks_ok and MODULE_LEAN_HOP["mode"] != "off" and
-                getattr(model, "typed_first_layer_ok", lambda _x: False)(x_dict)):
-            # layer 0 reads its block through the sampler's per-edge source type / table row
-            # (mag.REGNN._typed_first_layer): the last hop runs meta-only, as for the fused step
-            s0 = self.slots[0]
-            last = len(s0.sizes_k) - 1
-            et, eo = s0.enable_edge_meta(local_node_idx, last)
-            s0.meta_only[last] = True
-            blk = s0.blocks[last]
-            blk.edge_meta, blk.meta_only = (et, eo), True
-            self._module_lean = True
+        # the module path on device blocks (regcn, self-loop type 2): capturable, and pipelined
+        # like the fused step (the next batch sampled on a second stream)
+        self._module_lean = (self.fused is None and self._blocks_ok and
+                             MODULE_LEAN_HOP["mode"] != "off" and
+                             getattr(model, "typed_first_layer_ok", lambda _x: False)(x_dict))
         if self.fused is None and self._blocks_ok:
-            # the module path's last layer (hop 0's block) differentiates through a gather over
-            # the sampler's transposed index of that block (regnn_ns_spmm_bwd_csc: no float
-            # atomics into the source rows' gradient)
-            s0 = self.slots[0]
-            if s0.blocks[0].csr_idx.numel() <= 32768:
-                _, cptr, cent, clong = s0.csc[0] or s0.enable_csc(0)
-                b0 = s0.blocks[0]
-                b0.csc, b0.csc_cap = (cptr, cent, clong, s0.sizes, 1), s0.caps[1]
-        self.pipelined = self.fused is not None and bool(pipeline)
+            self._setup_module_slot(self.slots[0])
+        self.pipelined = bool(pipeline) and (self.fused is not None or
+                                             (self._blocks_ok and MODULE_PIPELINE["mode"] != "off"))
         if self.pipelined:
             s1 = DeviceSampler(rg, sizes, batch_size, num_edge_types=num_edge_types,
                                share=self.slots[0])
             self.slots.append(s1)
-            self.fused_slots = [self.fused, FusedStep(model, s1, x_dict, node_type,
-                                                      local_node_idx, self.y_flat, self.loss)]
+            if self.fused is not None:
+                self.fused_slots = [self.fused, FusedStep(model, s1, x_dict, node_type,
+                                                          local_node_idx, self.y_flat, self.loss)]
+            else:
+                self._setup_module_slot(s1)
             self._side = torch.cuda.Stream(device=dev)
         # one rank, FlatAdam, two-layer step: the optimizer runs inside the step's last launch
         # (no all-reduce sits between the backward and the update)
@@ -653,6 +647,23 @@ class NSTrainer:
         self._force_exchange = False
         self.epoch = -1
         self.set_epoch(0)
+
+    def _setup_module_slot(self, s):
+        """the module path's per-slot sampler outputs: with the typed first layer
+        (mag.REGNN._typed_first_layer) the last hop runs meta-only and layer 0 reads its block
+        through the per-edge source type / table row; the last layer (hop 0's block)
+        differentiates through a gather over that block's transposed index
+        (regnn_ns_spmm_bwd_csc: no float atomics into the source rows' gradient)."""
+        if self._module_lean:
+            last = len(s.sizes_k) - 1
+            et, eo = s.enable_edge_meta(self.local_node_idx, last)
+            s.meta_only[last] = True
+            blk = s.blocks[last]
+            blk.edge_meta, blk.meta_only = (et, eo), True
+        if s.blocks[0].csr_idx.numel() <= 32768:
+            _, cptr, cent, clong = s.csc[0] or s.enable_csc(0)
+            b0 = s.blocks[0]
+            b0.csc, b0.csc_cap = (cptr, cent, clong, s.sizes, 1), s.caps[1]
 
     # -- epochs ----------------------------------------------------------------------------------
     def steps_per_epoch(self):
@@ -686,12 +697,21 @@ class NSTrainer:
         n = len(self.slots)
         s = self.slots[slot]
         s.batch_from_perm(self.perm, self.rank + slot * self.world, n * self.world)
-        s.run_hops()
+        if self.fused is not None:
+            s.run_hops()
+        else:                                 # the module path reads the CSR blocks
+            s.run_hops(meta_only=self._module_lean, strided=False)
 
     def _pipelined_body(self, cur):
         """train slot `cur`'s batch while the next one is sampled into the other slot."""
         cs = torch.cuda.current_stream(self.device)
         self._side.wait_stream(cs)
+        if self.fused is None:                # the module path
+            self._module_step(self.slots[cur])
+            with torch.cuda.stream(self._side):
+                self._sample(1 - cur)
+            cs.wait_stream(self._side)
+            return
         # the model's launches are issued (captured) before the sampler's: the graph then runs
         # the model chain on the launch queue and the sampler on the second one, and the next
         # replay's first model kernel needs no cross-queue wait (243 -> 234 us per step)
@@ -724,12 +744,18 @@ class NSTrainer:
             self._sample(0)
             self.fused.step()
             return
-        self.flat.zero_()
-        s = self.slots[0]
+        if self.pipelined:
+            self._prime()
+            self._pipelined_body(self.cur)
+            self._trained, self.cur = self.cur, 1 - self.cur
+            return
         self._trained = 0
-        s.batch_from_perm(self.perm, self.rank, self.world)
-        # the module path reads n_id, the local ids and the CSR blocks
-        s.run_hops(meta_only=self._module_lean, strided=False)
+        self._sample(0)
+        self._module_step(self.slots[0])
+
+    def _module_step(self, s):
+        """the mag.REGNN autograd forward / nll / backward on sampler slot s's batch."""
+        self.flat.zero_()
         if self._blocks_ok:
             B = s.B
             n_id = s.n_id.to(torch.int64)

@@ -188,12 +188,19 @@ def test_trainer_graph_replay_tracks_eager():
     assert tr_g.edges_total() > 0
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_pipelined_trainer_matches_unpipelined(graph):
+@pytest.mark.parametrize("graph,engine", [(False, "fused"), (True, "fused"), (False, "module"),
+                                          (True, "module")])
+def test_pipelined_trainer_matches_unpipelined(monkeypatch, graph, engine):
     """two sampler slots (the next batch sampled on a second stream while the model trains)
-    give the unpipelined batch sequence, dropout masks and losses, across an epoch change."""
+    give the unpipelined batch sequence, dropout masks and losses, across an epoch change; for
+    the fused step and for the module path at hidden 128 (the typed first layer, meta-only last
+    hop; dropout off: the module path draws torch's RNG)."""
+    from regnn_hip import ns
     from regnn_hip.ns import NSTrainer
-    d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.4)
+    monkeypatch.setitem(ns.MODULE_PIPELINE, "mode", "on")
+    fused = engine == "fused"
+    d = _mag(0.002, seed=8, F=128, hidden=64 if fused else 128, classes=13,
+             dropout=0.4 if fused else 0.0)
 
     def make(pipe):
         return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 100,
@@ -202,6 +209,7 @@ def test_pipelined_trainer_matches_unpipelined(graph):
                          pipeline=pipe)
     tr_p, tr_u = make(True), make(False)
     assert tr_p.pipelined and not tr_u.pipelined
+    assert (tr_p.fused is not None) == fused and (fused or tr_p._module_lean)
     if graph:
         tr_p.capture(warmup=2)                          # warm-up steps undone by capture()
     run_p = tr_p.replay if graph else tr_p.step
