@@ -19,6 +19,8 @@
 // n_id = targets, then new sources in first-seen order over the target-major edge list.
 #include "regnn_common.h"
 
+#include <cstdlib>
+
 namespace regnn {
 
 constexpr int kNsTile = 1024;        // block positions per flag tile (256 threads x 4)
@@ -173,8 +175,11 @@ ns_sample_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ id
 // CSR position, target row, the dedup candidate (first-seen order over the slots = the CSR order
 // restricted to the edges); meta-only (lean): the source's type / table row instead. Edge counts
 // are added per block into sizes[8 + hop] (zeroed by ns_batch_kernel / set_targets) and state[5].
-constexpr int kNsStrWaves = 16;            // targets per block
+// G lanes per target: 64, or 32 (two targets per wave) when the row's k + 1 slots fit in 32 lanes
+// (fan-outs <= 31: half the waves and half the sampling instructions of a hop)
+constexpr int kNsStrWaves = 16;            // waves per block
 
+template <int G>
 __global__ void __launch_bounds__(64 * kNsStrWaves)
 ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                          const uint8_t* __restrict__ etype, const int32_t* __restrict__ ntype,
@@ -187,18 +192,21 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
                          int32_t* __restrict__ blk_row, float* __restrict__ inv,
                          const int64_t* __restrict__ local, int32_t* __restrict__ e_type,
                          int64_t* __restrict__ e_off, int lean, int32_t* __restrict__ csc_cnt) {
-    __shared__ int wsum[kNsStrWaves];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * kNsStrWaves + wv;
+    constexpr int TPW = 64 / G;                // targets per wave
+    __shared__ int wsum[kNsStrWaves * TPW];
+    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = wl % G, tl = wv * TPW + wl / G;   // lane within the target's group
+    const uint64_t gmask = G == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
+    const int i = blockIdx.x * (kNsStrWaves * TPW) + tl;
     const int n = sizes[hop];
     const int S = k + 1;
     const int64_t base = int64_t(i) * S;
     if (csc_cnt && i < cap)                    // the transposed index's counters (resolve adds)
-        for (int q = lane; q < S; q += 64) csc_cnt[base + q] = 0;
+        for (int q = lane; q < S; q += G) csc_cnt[base + q] = 0;
     int cnt = -1;                              // -1: no row (past the batch)
     if (i < cap && i >= n) {
         if (!lean)
-            for (int q = lane; q < S; q += 64) {
+            for (int q = lane; q < S; q += G) {
                 gsrc[base + q] = -2;
                 blk_idx[base + q] = -1;
             }
@@ -220,13 +228,13 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
             const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
                                                uint64_t(jl + 1)) >> 32) : 0;
             for (int i = 0; i < k; ++i) {
-                const int pos = __shfl(my_pos, i, 64);
-                const bool seen = __any(slot == pos);
+                const int pos = __shfl(my_pos, i, G);
+                const bool seen = (__ballot(slot == pos) & gmask) != 0;
                 if (lane == i) slot = seen ? d - k + i : pos;
             }
             rank = 0;
             for (int m = 0; m < k; ++m) {
-                const int other = __shfl(slot, m, 64);
+                const int other = __shfl(slot, m, G);
                 rank += (lane < k && other < slot) ? 1 : 0;
             }
         }
@@ -269,12 +277,12 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
             inv[i] = 1.f / float(cnt + 1);
         }
     }
-    if (lane == 0) wsum[wv] = cnt + 1;          // edges of the row, self loop included
+    if (lane == 0) wsum[tl] = cnt + 1;          // edges of the row, self loop included
     __syncthreads();
     if (threadIdx.x == 0) {
         int e = 0;
 #pragma unroll
-        for (int q = 0; q < kNsStrWaves; ++q) e += wsum[q];
+        for (int q = 0; q < kNsStrWaves * TPW; ++q) e += wsum[q];
         if (e) {
             atomicAdd(sizes + 8 + hop, e);
             atomicAdd(reinterpret_cast<unsigned long long*>(state + 5), (unsigned long long)e);
@@ -763,6 +771,14 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
 
 using namespace regnn;
 
+// two targets per wave in the strided sampler: REGNN_NS_HALF_WAVES=1 (off by default — measured
+// 136.6 vs 135.0 us per fused step at hidden 64: the sampler runs beside the model, and its
+// instruction count is not what the step waits on)
+static bool ns_half_waves() {
+    const char* v = getenv("REGNN_NS_HALF_WAVES");   // read per launch: tests switch it
+    return v && v[0] == '1';
+}
+
 extern "C" {
 
 int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_long,
@@ -828,12 +844,20 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     if (csc && cap_e > kCscMax) return REGNN_EUNSUPPORTED;
     if (strided) {
         // sampling + placement in one launch, no row-offset scan (the layout above)
-        hipLaunchKernelGGL(ns_sample_strided_kernel,
-                           dim3(unsigned((cap_dst + kNsStrWaves - 1) / kNsStrWaves)),
-                           dim3(64 * kNsStrWaves), 0, stream, ptr, idx, etype, ntype,
-                           num_edge_types, n_id, sizes, hop, cap_dst, k, state, g2l, first, scnt,
-                           gsrc, blk_idx, blk_rel, blk_pos, blk_row, inv, local, edge_type,
-                           edge_off, lean, csc_cnt);
+        if (k + 1 <= 32 && ns_half_waves())
+            hipLaunchKernelGGL(ns_sample_strided_kernel<32>,
+                               dim3(unsigned((cap_dst + 2 * kNsStrWaves - 1) / (2 * kNsStrWaves))),
+                               dim3(64 * kNsStrWaves), 0, stream, ptr, idx, etype, ntype,
+                               num_edge_types, n_id, sizes, hop, cap_dst, k, state, g2l, first,
+                               scnt, gsrc, blk_idx, blk_rel, blk_pos, blk_row, inv, local,
+                               edge_type, edge_off, lean, csc_cnt);
+        else
+            hipLaunchKernelGGL(ns_sample_strided_kernel<64>,
+                               dim3(unsigned((cap_dst + kNsStrWaves - 1) / kNsStrWaves)),
+                               dim3(64 * kNsStrWaves), 0, stream, ptr, idx, etype, ntype,
+                               num_edge_types, n_id, sizes, hop, cap_dst, k, state, g2l, first,
+                               scnt, gsrc, blk_idx, blk_rel, blk_pos, blk_row, inv, local,
+                               edge_type, edge_off, lean, csc_cnt);
         REGNN_LAUNCH_CHECK();
         if (lean) return REGNN_OK;
         const int ce = int(cap_e);

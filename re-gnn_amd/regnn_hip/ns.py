@@ -329,6 +329,12 @@ SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
 # model trains on this one, as the fused step does; "off" (default: at hidden 512, mag-10x the
 # overlapped sampler slowed the dense kernels more than it hid, 1.045 -> 1.09 ms per step)
 MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "off")}
+# the fused engine's sampling lookahead G: 2G sampler slots, each step samples the batch trained
+# G steps later, and a G-step graph trains G slots while the sampler fills the other G on the
+# second queue with one fork (the graph's root) and one join (its end) -- instead of a fork and
+# a join per step, each a few us of queue idle on the model's chain. G = 1: two slots, the
+# next batch sampled during this step and joined before layer 0's backward.
+AHEAD = {"steps": int(os.environ.get("REGNN_NS_AHEAD", "4"))}
 # "on": the module path's last hop runs meta-only when the model's layer 0 is the typed first
 # layer (mag.REGNN.typed_first_layer_ok); "off": the full hop (A/B, tests)
 MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
@@ -560,10 +566,12 @@ class NSTrainer:
     The gradients live in one flat fp32 bucket (p.grad are views of it): one RCCL all-reduce
     per step for world > 1 (mag.flat_grad_allreduce's exchange), outside the captured graph.
 
-    pipeline (fused engine): two sampler slots; while the model trains on one slot's batch, the
-    next batch is sampled into the other on a second stream (the reference's NeighborSampler
-    prefetches batches with DataLoader workers, mag/regnn_ns.py:206-208). Slot s deals global
-    batches as rank + s * world of 2 * world, so the batch sequence is the unpipelined one."""
+    pipeline: 2 * ahead sampler slots (AHEAD; the module path: ahead 1); while the model trains
+    on one slot's batch, the batch `ahead` steps later is sampled into another on a second
+    stream (the reference's NeighborSampler prefetches batches with DataLoader workers,
+    mag/regnn_ns.py:206-208). Slot s deals global batches as rank + s * world of
+    2 * ahead * world and the slots train round robin, so the batch sequence is the
+    unpipelined one."""
 
     def __init__(self, model, opt, rg, sizes, batch_size, train_idx, x_dict, edge_type,
                  node_type, local_node_idx, y_global, num_edge_types, seed=0, rank=0, world=1,
@@ -625,15 +633,19 @@ class NSTrainer:
             self._setup_module_slot(self.slots[0])
         self.pipelined = bool(pipeline) and (self.fused is not None or
                                              (self._blocks_ok and MODULE_PIPELINE["mode"] != "off"))
+        # the sampling lookahead (fused engine; the module path samples one batch ahead)
+        self.ahead = max(1, int(AHEAD["steps"])) if self.pipelined and self.fused is not None else 1
         if self.pipelined:
-            s1 = DeviceSampler(rg, sizes, batch_size, num_edge_types=num_edge_types,
-                               share=self.slots[0])
-            self.slots.append(s1)
+            for _ in range(2 * self.ahead - 1):
+                self.slots.append(DeviceSampler(rg, sizes, batch_size,
+                                                num_edge_types=num_edge_types,
+                                                share=self.slots[0]))
             if self.fused is not None:
-                self.fused_slots = [self.fused, FusedStep(model, s1, x_dict, node_type,
-                                                          local_node_idx, self.y_flat, self.loss)]
+                self.fused_slots = [self.fused] + [
+                    FusedStep(model, s, x_dict, node_type, local_node_idx, self.y_flat, self.loss)
+                    for s in self.slots[1:]]
             else:
-                self._setup_module_slot(s1)
+                self._setup_module_slot(self.slots[1])
             self._side = torch.cuda.Stream(device=dev)
         # one rank, FlatAdam, two-layer step: the optimizer runs inside the step's last launch
         # (no all-reduce sits between the backward and the update)
@@ -703,13 +715,15 @@ class NSTrainer:
             s.run_hops(meta_only=self._module_lean, strided=False)
 
     def _pipelined_body(self, cur):
-        """train slot `cur`'s batch while the next one is sampled into the other slot."""
+        """train slot `cur`'s batch while the batch of `ahead` steps later is sampled into slot
+        cur + ahead (mod 2 ahead; ahead 1: the next batch into the other slot)."""
         cs = torch.cuda.current_stream(self.device)
+        nxt = (cur + self.ahead) % len(self.slots)
         self._side.wait_stream(cs)
         if self.fused is None:                # the module path
             self._module_step(self.slots[cur])
             with torch.cuda.stream(self._side):
-                self._sample(1 - cur)
+                self._sample(nxt)
             cs.wait_stream(self._side)
             return
         # the model's launches are issued (captured) before the sampler's: the graph then runs
@@ -717,19 +731,43 @@ class NSTrainer:
         # replay's first model kernel needs no cross-queue wait (243 -> 234 us per step)
         fs = self.fused_slots[cur]
         # (the profiled eager steps of bench.py time the step as one event: unsplit)
-        split = fs.two_layer and SPLIT_JOIN["mode"] != "off" and not profile_enabled()
+        split = (self.ahead == 1 and fs.two_layer and SPLIT_JOIN["mode"] != "off" and
+                 not profile_enabled())
         fs.step(part=1 if split else 0)
         with torch.cuda.stream(self._side):
-            self._sample(1 - cur)
+            self._sample(nxt)
         # the join sits between layer 1's transposed pass and layer 0's backward (the sampler is
         # done by then): the next step's first kernel then waits on its own queue only
         cs.wait_stream(self._side)
         if split:
             fs.step(part=2)
 
+    def _ahead_group(self, start, in_graph):
+        """`ahead` steps from slot `start` (0 or ahead) as one unit: the model trains slots
+        start .. start + ahead - 1 (sampled earlier) on the launch stream while the sampler fills
+        the other `ahead` slots on the second one; one fork before, one join after."""
+        cs = torch.cuda.current_stream(self.device)
+        G, n = self.ahead, len(self.slots)
+        self._side.wait_stream(cs)
+        # the model's launches first (captured first: the graph runs them on the launch queue)
+        for i in range(G):
+            self.fused_slots[start + i].step()
+            if in_graph:
+                self._exchange()
+            self._opt_step()
+        with torch.cuda.stream(self._side):
+            for i in range(G):
+                self._sample((start + G + i) % n)
+        cs.wait_stream(self._side)
+
+    def _advance(self):
+        self._trained, self.cur = self.cur, (self.cur + 1) % len(self.slots)
+
     def _prime(self):
+        """the sampled window ahead of slot cur: slots cur .. cur + ahead - 1."""
         if not self._primed:
-            self._sample(self.cur)
+            for i in range(self.ahead):
+                self._sample((self.cur + i) % len(self.slots))
             self._primed = True
 
     def _forward_backward(self):
@@ -739,7 +777,7 @@ class NSTrainer:
             if self.pipelined:
                 self._prime()
                 self._pipelined_body(self.cur)
-                self._trained, self.cur = self.cur, 1 - self.cur
+                self._advance()
                 return
             self._sample(0)
             self.fused.step()
@@ -747,7 +785,7 @@ class NSTrainer:
         if self.pipelined:
             self._prime()
             self._pipelined_body(self.cur)
-            self._trained, self.cur = self.cur, 1 - self.cur
+            self._advance()
             return
         self._trained = 0
         self._sample(0)
@@ -872,7 +910,7 @@ class NSTrainer:
             self._prime()                      # slot 0's batch, before the first replay
             torch.cuda.synchronize(self.device)
             g1 = []
-            for cur in (0, 1):                 # one graph per slot parity
+            for cur in range(len(self.slots)):   # one graph per slot
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     # (Adam after the join: measured faster than before it, the graph then
@@ -884,7 +922,14 @@ class NSTrainer:
                         self._opt_step()
                 g1.append(g)
             self.graph_groups = {}
-            if fold_opt:
+            if fold_opt and self.ahead > 1:
+                # one G-step graph per half of the slots: (G, start) -> graph
+                for start in (0, self.ahead):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._ahead_group(start, in_graph)
+                    self.graph_groups[(self.ahead, start)] = g
+            elif fold_opt:
                 # 2 and 4 steps back to back in one graph (the slot parity returns to 0):
                 # run_steps replays them for runs of steps, one graph boundary (~9 us of queue
                 # idle between replays) per group instead of per step
@@ -918,7 +963,19 @@ class NSTrainer:
         replay()s."""
         k = int(k)
         groups = getattr(self, "graph_groups", {})
+        G = self.ahead
         while k > 0:
+            if G > 1:
+                g = groups.get((G, self.cur)) if k >= G else None
+                if g is None:
+                    self.replay()
+                    k -= 1
+                    continue
+                self._prime()
+                g.replay()
+                self._trained, self.cur = self.cur + G - 1, (self.cur + G) % len(self.slots)
+                k -= G
+                continue
             n = next((n for n in sorted(groups, reverse=True) if n <= k), 0)
             if n and self.cur == 0 and self._primed:
                 groups[n].replay()
@@ -933,7 +990,7 @@ class NSTrainer:
         if self.pipelined:
             self._prime()                      # after set_epoch: the new epoch's first batch
             g1[self.cur].replay()
-            self._trained, self.cur = self.cur, 1 - self.cur
+            self._advance()
         else:
             g1.replay()
         if g2 is not None:

@@ -525,12 +525,16 @@ def test_meta_only_last_hop_matches_full_hop():
         assert torch.equal(ga, gb), (ga - gb).abs().max()
 
 
-def test_run_steps_pair_graph_matches_single_replays():
-    """run_steps (runs of 4 / 2 steps as one multi-step graph replay) trains the same batches to
-    the same losses and bitwise the same parameters as one-step replays, across an epoch
-    boundary (the two-layer step is bitwise reproducible: VERDICT r2 item 8)."""
+@pytest.mark.parametrize("ahead", [1, 4])
+def test_run_steps_pair_graph_matches_single_replays(monkeypatch, ahead):
+    """run_steps (ahead 1: runs of 4 / 2 steps as one multi-step graph replay; ahead 4: 4-step
+    graphs whose sampler fills the other four slots) trains the same batches to the same losses
+    and bitwise the same parameters as one-step replays, across an epoch boundary (the
+    two-layer step is bitwise reproducible: VERDICT r2 item 8)."""
     d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.4)
+    from regnn_hip import ns
     from regnn_hip.ns import NSTrainer
+    monkeypatch.setitem(ns.AHEAD, "steps", ahead)
 
     def make():
         return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 100,
@@ -539,7 +543,8 @@ def test_run_steps_pair_graph_matches_single_replays():
     ta, tb = make(), make()
     ta.capture(warmup=1)
     tb.capture(warmup=1)
-    assert sorted(ta.graph_groups) == [2, 4]
+    assert ta.ahead == ahead and len(ta.slots) == 2 * ahead
+    assert sorted(ta.graph_groups) == ([2, 4] if ahead == 1 else [(4, 0), (4, 4)])
     for k in (4, 3, 2, 7):              # odd counts end on a single replay
         ta.run_steps(k)
         for _ in range(k):
@@ -662,13 +667,16 @@ def test_block_transposed_index():
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
 
 
-def test_strided_blocks_match_csr(monkeypatch):
+@pytest.mark.parametrize("half_waves", ["0", "1"])
+def test_strided_blocks_match_csr(monkeypatch, half_waves):
     """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
     launch) against the CSR layout on the same batches: the same n_id, sizes, per-row edges
     (local source, relation, CSR position, target row; the meta-only hop's source type / table
     row), 1/in-counts and transposed index; and the two-layer fused step's loss and gradients
-    bitwise equal over both layouts."""
+    bitwise equal over both layouts. half_waves "1": the strided sampler with two targets per
+    wave (fan-outs 9 and 7 fit 32 lanes)."""
     from regnn_hip import ns
+    monkeypatch.setenv("REGNN_NS_HALF_WAVES", half_waves)
     d = _mag(0.003, seed=10, F=128, hidden=64, classes=19, dropout=0.5)
     trs, models = [], []
     for mode in ("off", "on"):
