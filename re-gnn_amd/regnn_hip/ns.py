@@ -526,6 +526,13 @@ class FusedStep:
                    torch.cuda.current_stream(self.device).cuda_stream)
 
 
+def _capturing(g):
+    """capture into g with the thread-local error mode: with several ranks the process group's
+    watchdog thread polls the eager all-reduces' events meanwhile, which the global mode counts
+    as an illegal call during capture (it invalidates the capture at random)."""
+    return torch.cuda.graph(g, capture_error_mode="thread_local")
+
+
 def _slab_floats(P, cap0):
     n = int(L._so.regnn_nsm_slab_floats(ctypes.addressof(P), int(cap0)))
     if n <= 0:
@@ -744,23 +751,32 @@ class NSTrainer:
         if split:
             fs.step(part=2)
 
-    def _ahead_group(self, start, in_graph):
-        """`ahead` steps from slot `start` (0 or ahead) as one unit: the model trains slots
-        start .. start + ahead - 1 (sampled earlier) on the launch stream while the sampler fills
-        the other `ahead` slots on the second one; one fork before, one join after."""
+    def _ahead_group(self, start, m, in_graph):
+        """m <= ahead steps from slot `start` as one unit: the model trains slots
+        start .. start + m - 1 (sampled earlier: slots cur .. cur + ahead - 1 always are) on the
+        launch stream while the sampler fills slots start + ahead .. start + ahead + m - 1 (those
+        trained last) on the second one; one fork before, one join after."""
         cs = torch.cuda.current_stream(self.device)
         G, n = self.ahead, len(self.slots)
         self._side.wait_stream(cs)
         # the model's launches first (captured first: the graph runs them on the launch queue)
-        for i in range(G):
-            self.fused_slots[start + i].step()
+        for i in range(m):
+            self.fused_slots[(start + i) % n].step()
             if in_graph:
                 self._exchange()
             self._opt_step()
         with torch.cuda.stream(self._side):
-            for i in range(G):
+            for i in range(m):
                 self._sample((start + G + i) % n)
         cs.wait_stream(self._side)
+
+    def _group_sizes(self):
+        """the multi-step graph lengths at lookahead > 1: ahead, ahead / 2, .., 2 (descending)."""
+        out, m = [], self.ahead
+        while m >= 2:
+            out.append(m)
+            m //= 2
+        return out
 
     def _advance(self):
         self._trained, self.cur = self.cur, (self.cur + 1) % len(self.slots)
@@ -894,15 +910,7 @@ class NSTrainer:
             for _ in range(warmup):
                 self.step()
         torch.cuda.current_stream(self.device).wait_stream(side)
-        torch.cuda.synchronize(self.device)
-        self._restore_train_state(saved)
-        # warm-up steps do not advance the epoch (batch counter, edge counter); the dedup stamp
-        # (state[4]) stays monotone: the tables still hold the warm-up steps' stamps
-        for s, s0 in zip(self.slots, st0):
-            s.state[2:4].copy_(s0[2:4])
-            s.state[5:6].copy_(s0[5:6])
-        torch.cuda.synchronize(self.device)
-        self.cur, self._primed, self._trained = 0, False, 0
+        self._undo_steps(saved, st0)
         # one rank: the optimizer step joins the step's graph (no graph boundary, no host gap
         # between the backward and Adam); several: the gradient all-reduce runs between graphs,
         # or inside the graph with exchange_in_graph
@@ -914,7 +922,7 @@ class NSTrainer:
             g1 = []
             for cur in range(len(self.slots)):   # one graph per slot
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with _capturing(g):
                     # (Adam after the join: measured faster than before it, the graph then
                     # ends on one queue)
                     self._pipelined_body(cur)
@@ -925,19 +933,22 @@ class NSTrainer:
                 g1.append(g)
             self.graph_groups = {}
             if fold_opt and self.ahead > 1:
-                # one G-step graph per half of the slots: (G, start) -> graph
-                for start in (0, self.ahead):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
-                        self._ahead_group(start, in_graph)
-                    self.graph_groups[(self.ahead, start)] = g
+                # (m, start) -> m steps from slot start as one graph, m = ahead, ahead / 2, .. 2
+                # and every start (run_steps covers any step count from any slot with few
+                # replays: a run of k steps takes ~k / ahead graph boundaries and joins)
+                for m in self._group_sizes():
+                    for start in range(len(self.slots)):
+                        g = torch.cuda.CUDAGraph()
+                        with _capturing(g):
+                            self._ahead_group(start, m, in_graph)
+                        self.graph_groups[(m, start)] = g
             elif fold_opt:
                 # 2 and 4 steps back to back in one graph (the slot parity returns to 0):
                 # run_steps replays them for runs of steps, one graph boundary (~9 us of queue
                 # idle between replays) per group instead of per step
                 for n in (4, 2):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    with _capturing(g):
                         for i in range(n):
                             self._pipelined_body(i & 1)
                             if in_graph:
@@ -946,7 +957,7 @@ class NSTrainer:
                     self.graph_groups[n] = g
         else:
             g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
+            with _capturing(g1):
                 self._forward_backward()
                 if in_graph:
                     self._exchange()
@@ -955,9 +966,34 @@ class NSTrainer:
         g2 = None
         if not fold_opt:
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
+            with _capturing(g2):
                 self.opt.step()
         self.graphs = (g1, g2)
+        if self.pipelined and fold_opt and self.ahead > 1:
+            # every graph's first launch is slow (tens of us: the runtime's one-time work per
+            # executable graph); replay each once here, walking the slots in training order,
+            # and undo those steps as the warm-up's
+            n = len(self.slots)
+            for m in self._group_sizes():
+                for _ in range(n):             # start advances by m + 1 (odd: every slot)
+                    self.graph_groups[(m, self.cur)].replay()
+                    self.cur = (self.cur + m) % n
+                    g1[self.cur].replay()
+                    self.cur = (self.cur + 1) % n
+            self._undo_steps(saved, st0)
+
+    def _undo_steps(self, saved, st0):
+        """undo eager or replayed steps taken inside capture(): parameters, optimizer state,
+        the sampler's batch and edge counters (not the dedup stamp, state[4]: it stays
+        monotone, the tables still hold the undone steps' stamps); slot 0 .. ahead - 1 are
+        sampled again by the next step (_prime)."""
+        torch.cuda.synchronize(self.device)
+        self._restore_train_state(saved)
+        for s, s0 in zip(self.slots, st0):
+            s.state[2:4].copy_(s0[2:4])
+            s.state[5:6].copy_(s0[5:6])
+        torch.cuda.synchronize(self.device)
+        self.cur, self._primed, self._trained = 0, False, 0
 
     def run_steps(self, k):
         """k training steps as graph replays (capture() first): runs of 4 or 2 steps starting at
@@ -965,18 +1001,19 @@ class NSTrainer:
         replay()s."""
         k = int(k)
         groups = getattr(self, "graph_groups", {})
-        G = self.ahead
         while k > 0:
-            if G > 1:
-                g = groups.get((G, self.cur)) if k >= G else None
+            if self.ahead > 1:
+                m = next((m for m in self._group_sizes() if m <= k), 1)
+                g = groups.get((m, self.cur))
                 if g is None:
                     self.replay()
                     k -= 1
                     continue
                 self._prime()
                 g.replay()
-                self._trained, self.cur = self.cur + G - 1, (self.cur + G) % len(self.slots)
-                k -= G
+                n = len(self.slots)
+                self._trained, self.cur = (self.cur + m - 1) % n, (self.cur + m) % n
+                k -= m
                 continue
             n = next((n for n in sorted(groups, reverse=True) if n <= k), 0)
             if n and self.cur == 0 and self._primed:

@@ -544,7 +544,8 @@ def test_run_steps_pair_graph_matches_single_replays(monkeypatch, ahead):
     ta.capture(warmup=1)
     tb.capture(warmup=1)
     assert ta.ahead == ahead and len(ta.slots) == 2 * ahead
-    assert sorted(ta.graph_groups) == ([2, 4] if ahead == 1 else [(4, 0), (4, 4)])
+    assert sorted(ta.graph_groups) == ([2, 4] if ahead == 1 else
+                                       [(m, c) for m in (2, 4) for c in range(8)])
     for k in (4, 3, 2, 7):              # odd counts end on a single replay
         ta.run_steps(k)
         for _ in range(k):

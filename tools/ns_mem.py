@@ -17,12 +17,17 @@ def main():
     tr, info = bench.build_ns(args, dev)
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated(dev)
+    import time
+    t0 = time.perf_counter()
     tr.capture(warmup=2)
+    torch.cuda.synchronize()
+    tc = time.perf_counter() - t0
     tr.run_steps(16)
     torch.cuda.synchronize()
     print(f"ahead {tr.ahead}: slots {len(tr.slots)}, allocated {base / 2**30:.2f} GiB at build, "
           f"{torch.cuda.memory_allocated(dev) / 2**30:.2f} GiB after capture, peak "
-          f"{torch.cuda.max_memory_allocated(dev) / 2**30:.2f} GiB")
+          f"{torch.cuda.max_memory_allocated(dev) / 2**30:.2f} GiB; capture {tc:.2f} s "
+          f"({len(tr.graph_groups)} multi-step graphs)")
 
 
 if __name__ == "__main__":
