@@ -57,6 +57,13 @@ def log(*a):
 
 
 def setup_dist(n):
+    if os.environ.get("REGNN_NS_FORCE_EXCHANGE") == "1" and n == 1:
+        # one-rank rehearsal of the several-rank NS step structure (NSTrainer.rehearse_exchange)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        torch.cuda.set_device(0)
+        return 0, 1, torch.device("cuda", 0)
     if n > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # RCCL ("nccl"); REGNN_DIST_BACKEND=gloo rehearses several ranks on one device
         dist.init_process_group(os.environ.get("REGNN_DIST_BACKEND", "nccl"))
@@ -112,6 +119,8 @@ def build_ns(args, dev, hidden=None):
     tr = NSTrainer(model, None, rg, [25, 20], args.batch, torch.arange(n_paper, device=dev),
                    x_dict, edge_type, node_type, local_node_idx, y_global, 7, seed=123,
                    rank=rank, world=world, adam=dict(lr=1e-3))
+    if os.environ.get("REGNN_NS_FORCE_EXCHANGE") == "1":
+        tr.rehearse_exchange()
     torch.cuda.synchronize()
     log(f"[bench] ns: N={gd['N']:,} E={rg.E:,} built in {time.time() - t0:.1f}s; "
         f"{tr.steps_per_epoch()} steps/epoch/rank, capacities {tr.sampler.caps}")
@@ -277,6 +286,10 @@ def run_ns(args, dev):
             "nodes": info["N"], "edges": info["E"], "relations": 11, "hidden": 64,
             "batch_per_rank": args.batch, "global_batch": args.batch * world,
             "fanout": [25, 20], "parallelism": f"dp{world}",
+            "grad_exchange": (None if world == 1 and not tr._force_exchange else
+                              "eager all-reduce between graphs" if use_graph and tr.graphs[1] is not None
+                              else "all-reduce captured in the step graph" if use_graph else "eager"),
+            "lookahead": tr.ahead,
             "hip_graph": use_graph, "aggregated_edges_per_step_per_rank": edges / world / args.steps,
             "final_loss": loss,
         },

@@ -890,14 +890,38 @@ class NSTrainer:
         first replay trains the epoch's first batch from the same model as an eager step would.
         Only the dedup stamps move on (they must stay monotone).
 
-        exchange_in_graph (several ranks; default: env REGNN_NS_GRAPH_ALLREDUCE=1): the RCCL
-        all-reduce and Adam are captured into the step's graph too, so a step is one replay with
-        no host-issued collective and no second graph boundary (and runs of 2 / 4 steps become
-        one replay, as with one rank). Off by default: the eager exchange is the tested path on
-        8 GPUs."""
+        exchange_in_graph (several ranks): the RCCL all-reduce and Adam are captured into the
+        step's graph too, so a step is one replay with no host-issued collective and no second
+        graph boundary, and runs of steps become one replay per lookahead group as with one rank.
+        Default: on with an RCCL ("nccl") process group, off with gloo (a host collective cannot
+        be captured); env REGNN_NS_GRAPH_ALLREDUCE=0 / 1 overrides. Measured on one GPU with the
+        several-rank structure (rehearse_exchange): 157-160 us per step with the eager exchange
+        between graphs, 127 us captured (125.8 one rank). A capture that fails falls back to the
+        eager exchange."""
         import os
+        multi = self.world > 1 or self._force_exchange
         if exchange_in_graph is None:
-            exchange_in_graph = os.environ.get("REGNN_NS_GRAPH_ALLREDUCE") == "1"
+            env = os.environ.get("REGNN_NS_GRAPH_ALLREDUCE")
+            if env is not None:
+                exchange_in_graph = env == "1"
+            else:
+                import torch.distributed as dist
+                exchange_in_graph = (multi and dist.is_available() and dist.is_initialized() and
+                                     dist.get_backend() == "nccl")
+        if multi and exchange_in_graph:
+            saved_state = ([s.state.clone() for s in self.slots], self._train_state())
+            try:
+                return self._capture(warmup, True)
+            except RuntimeError as e:          # torch.AcceleratorError is a RuntimeError
+                import warnings
+                warnings.warn(f"capturing the all-reduce into the step graph failed ({e}); "
+                              "falling back to the eager exchange between graphs")
+                torch.cuda.synchronize(self.device)
+                self._undo_steps(saved_state[1], saved_state[0])
+                self.graphs, self.graph_groups = None, {}
+        return self._capture(warmup, exchange_in_graph)
+
+    def _capture(self, warmup, exchange_in_graph):
         multi = self.world > 1 or self._force_exchange
         if self.fused is None and not self._blocks_ok:
             raise ValueError("this model's module path reads exact-size adjs (a host sync per "
@@ -1035,6 +1059,17 @@ class NSTrainer:
         if g2 is not None:
             self._exchange()
             g2.replay()
+
+    def rehearse_exchange(self):
+        """the several-rank step structure on one rank (a timing rehearsal on one GPU, with a
+        one-rank process group initialised): the bucket all-reduce after the backward and Adam
+        as its own launch after it. Call before capture()."""
+        self._force_exchange = True
+        if self.adam_fused:
+            self.adam_fused = False
+            for fs in (self.fused_slots if self.pipelined else [self.fused]):
+                fs.adam = None
+                fs.W.adam = None
 
     def param_vector(self):
         """the parameters in model order without the bucket's alignment pads."""
