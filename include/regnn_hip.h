@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature change or addition; currently 34). */
+/* ABI version (bumped on any signature or semantics change; currently 35). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -769,8 +769,8 @@ typedef struct regnn_nsm_adam {
     const float* grad_base;
     int64_t n;
     float lr, beta1, beta2, eps, weight_decay, grad_scale;
-    int64_t* step;
-    uint32_t* ticket;
+    int64_t* step;      /* advanced once per step by the launch before the update (device) */
+    uint32_t* ticket;   /* unused by regnn_nsm_step since ABI 35 (kept: the struct's layout) */
 } regnn_nsm_adam;
 
 /* Floats of the per-block partial slab regnn_nsm_step needs for these parameters and a batch

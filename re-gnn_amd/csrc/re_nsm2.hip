@@ -916,6 +916,7 @@ struct Bwd0Args {
     float* slab;     // [t][block][(K + 1) * 64]: g W_t ([64][K]) | g b_t
     float* rslab;    // relation slots: [t][block][64] relation dots
     float* slab0;    // [block][64 * 64]: g W_0
+    int64_t* adam_step;  // the fused Adam's step count (advanced here, read by finalize) or null
 };
 
 constexpr int kPost0W = F * F;
@@ -933,6 +934,9 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile of a K-wide row
     extern __shared__ float sm[];
     float* Wk = sm;                           // [K][WS]: W_t k-major; at the end the row terms
+    // the fused Adam's step count advances here, the launch before finalize, which reads it:
+    // no completion ticket among finalize's blocks (their contended atomic was its tail)
+    if (A.adam_step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) A.adam_step[0] += 1;
     float* bc = Wk + K * WS;                  // [F] b_t
     float* ush = bc + F;                      // [16][XS] U_t (RS) or S_t
     float* xsh = ush + 16 * XS;               // [16][XS] x_self (RS only)
@@ -1189,6 +1193,7 @@ struct Job {
     const float* src;
     int64_t pstride;
     int nparts, width, op, adam, vec;    // vec: 4 elements per thread (float4 partial rows)
+    int cb;                  // columns (elements, or float4 columns if vec) per block: 32, 16, 8
     float* dst;
     const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
 };
@@ -1196,7 +1201,7 @@ struct Job {
 struct AdamArgs {
     float* p; float* m; float* v; const float* gbase; int64_t n;
     float lr, b1, b2, eps, wd, gscale;
-    int64_t* step; unsigned* ticket; int on;
+    const int64_t* step; int on;           // step: this step's t (bwd0 advanced it)
 };
 
 constexpr int kMaxJobs = 32;
@@ -1213,7 +1218,7 @@ struct FinArgs {
 __device__ __forceinline__ void adam_consts(const AdamArgs& O, int64_t& s_t, float& s_step,
                                             float& s_bc2) {
     if (O.on && threadIdx.x == 64) {
-        const int64_t t = O.step[0] + 1;
+        const int64_t t = O.step[0];
         const double bc1 = 1.0 - pow(double(O.b1), double(t));
         const double bc2 = 1.0 - pow(double(O.b2), double(t));
         s_t = t;
@@ -1234,16 +1239,40 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& O, int64_t i, float g,
     O.p[i] = pi - s_step * (mn / (sqrtf(vn) / s_bc2 + O.eps));
 }
 
-// 4 consecutive elements per thread: 32 float4 columns x 8 partial groups per block, the same
-// per-element summation order as the scalar path (partials grp, grp + 8, ...; groups combined
-// in a fixed tree)
+// the G = 256 / cb group sums of one column, combined in a fixed tree (8-wide trees, then
+// pairwise over the 8-group chunks)
+template <typename V, typename Add>
+__device__ __forceinline__ V group_tree(const V* red, int cb, int el, Add add) {
+    const int G = kBlock / cb;
+    V c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (8 * k < G) {
+            const V* r = red + 8 * k * cb + el;
+            c[k] = add(add(add(r[0], r[cb]), add(r[2 * cb], r[3 * cb])),
+                       add(add(r[4 * cb], r[5 * cb]), add(r[6 * cb], r[7 * cb])));
+        }
+    }
+    if (G == 8) return c[0];
+    if (G == 16) return add(c[0], c[1]);
+    return add(add(c[0], c[1]), add(c[2], c[3]));
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// 4 consecutive elements per thread: cb float4 columns x 256 / cb partial groups per block
+// (narrow jobs get more groups: fewer dependent load rounds over their partial rows); partials
+// grp, grp + G, ... summed in order, the groups in a fixed tree
 __device__ __forceinline__ void finalize_vec(const FinArgs& A, const Job& J, const AdamArgs& O,
                                              int b, int el, int grp, int64_t& s_t, float& s_step,
                                              float& s_bc2) {
-    __shared__ float4 red4[8][33];
-    const int e = (b * 32 + el) * 4;
+    __shared__ float4 red4[kBlock];
+    const int cb = J.cb, G = kBlock / cb;
+    const int e = (b * cb + el) * 4;
     const int64_t i = (J.dst + e) - O.gbase;
-    const bool stepped = O.on && J.adam && threadIdx.x < 32 && e < J.width && i >= 0 && i < O.n;
+    const bool stepped = O.on && J.adam && grp == 0 && e < J.width && i >= 0 && i < O.n;
     float pi[4] = {0.f, 0.f, 0.f, 0.f}, mi[4] = {0.f, 0.f, 0.f, 0.f}, vi[4] = {0.f, 0.f, 0.f, 0.f};
     if (stepped) {
 #pragma unroll
@@ -1257,31 +1286,24 @@ __device__ __forceinline__ void finalize_vec(const FinArgs& A, const Job& J, con
         const float4* src = reinterpret_cast<const float4*>(J.src + e);
         const int64_t ps = J.pstride / 4;
         int p = grp;
-        for (; p + 56 < J.nparts; p += 64) {
+        for (; p + 7 * G < J.nparts; p += 8 * G) {
             float4 vv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + 8 * u) * ps];
+            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + G * u) * ps];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 s.x += vv[u].x; s.y += vv[u].y; s.z += vv[u].z; s.w += vv[u].w;
             }
         }
-        for (; p < J.nparts; p += 8) {
+        for (; p < J.nparts; p += G) {
             const float4 v = src[int64_t(p) * ps];
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
     }
-    red4[grp][el] = s;
+    red4[grp * cb + el] = s;
     __syncthreads();
-    if (threadIdx.x < 32 && e < J.width) {
-        float4 r[8];
-#pragma unroll
-        for (int g = 0; g < 8; ++g) r[g] = red4[g][el];
-        float4 tot;
-        tot.x = ((r[0].x + r[1].x) + (r[2].x + r[3].x)) + ((r[4].x + r[5].x) + (r[6].x + r[7].x));
-        tot.y = ((r[0].y + r[1].y) + (r[2].y + r[3].y)) + ((r[4].y + r[5].y) + (r[6].y + r[7].y));
-        tot.z = ((r[0].z + r[1].z) + (r[2].z + r[3].z)) + ((r[4].z + r[5].z) + (r[6].z + r[7].z));
-        tot.w = ((r[0].w + r[1].w) + (r[2].w + r[3].w)) + ((r[4].w + r[5].w) + (r[6].w + r[7].w));
+    if (grp == 0 && e < J.width) {
+        const float4 tot = group_tree(red4, cb, el, add4);
         *reinterpret_cast<float4*>(J.dst + e) = tot;
         if (stepped) {
             const float t4[4] = {tot.x, tot.y, tot.z, tot.w};
@@ -1294,11 +1316,12 @@ __device__ __forceinline__ void finalize_vec(const FinArgs& A, const Job& J, con
 __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, const AdamArgs& O,
                                                 int b, int el, int grp, int64_t& s_t,
                                                 float& s_step, float& s_bc2) {
-    __shared__ float red[8][33];
-    const int e = b * 32 + el;
+    __shared__ float red[kBlock];
+    const int cb = J.cb, G = kBlock / cb;
+    const int e = b * cb + el;
     // the optimizer's operands of this thread's element, requested before the partial sums
     const int64_t i = (J.dst + e) - O.gbase;
-    const bool stepped = O.on && J.adam && threadIdx.x < 32 && e < J.width && i >= 0 && i < O.n;
+    const bool stepped = O.on && J.adam && grp == 0 && e < J.width && i >= 0 && i < O.n;
     float pi = 0.f, mi = 0.f, vi = 0.f;
     if (stepped) {
         pi = O.p[i]; mi = O.m[i]; vi = O.v[i];
@@ -1308,21 +1331,20 @@ __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, 
     if (e < J.width) {
         const float* src = J.src + e;
         int p = grp;
-        for (; p + 56 < J.nparts; p += 64) {           // 8 partial rows in flight per thread
+        for (; p + 7 * G < J.nparts; p += 8 * G) {     // 8 partial rows in flight per thread
             float vv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + 8 * u) * J.pstride];
+            for (int u = 0; u < 8; ++u) vv[u] = src[int64_t(p + G * u) * J.pstride];
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += vv[u];
         }
-        for (; p < J.nparts; p += 8) s += src[int64_t(p) * J.pstride];
+        for (; p < J.nparts; p += G) s += src[int64_t(p) * J.pstride];
     }
-    red[grp][el] = s;
+    red[grp * cb + el] = s;
     __syncthreads();
     PH(3, 1);
-    if (threadIdx.x < 32 && e < J.width) {
-        const float tot = ((red[0][el] + red[1][el]) + (red[2][el] + red[3][el])) +
-                          ((red[4][el] + red[5][el]) + (red[6][el] + red[7][el]));
+    if (grp == 0 && e < J.width) {
+        const float tot = group_tree(red, cb, el, [](float a, float b) { return a + b; });
         float out = tot;
         if (J.op == kOpRel) {
             const float x = J.aux[e] * A.alpha;                // d tab / d rw (LeakyReLU)
@@ -1341,7 +1363,6 @@ __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, 
 __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     __shared__ int64_t s_t;
     __shared__ float s_step, s_bc2;
-    __shared__ bool last;
     int ji = 0;
 #pragma unroll
     for (int i = 1; i < kMaxJobs; ++i) ji += (i < A.n_jobs && int(blockIdx.x) >= A.start[i]);
@@ -1349,22 +1370,11 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     const Job J = A.job[ji];
     const AdamArgs& O = A.adam;
     PH(3, 0);
-    const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    const int el = threadIdx.x % J.cb, grp = threadIdx.x / J.cb;
     if (J.vec) {                               // block-uniform
         finalize_vec(A, J, O, b, el, grp, s_t, s_step, s_bc2);
     } else {
         finalize_scalar(A, J, O, b, el, grp, s_t, s_step, s_bc2);
-    }
-    if (O.on) {
-        // every block read the step count before its ticket (the barrier in the sum waited for
-        // the load); the last block to finish advances it
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(O.ticket, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (last && threadIdx.x == 0) {
-            O.step[0] = s_t;
-            O.ticket[0] = 0u;
-        }
     }
     PH(3, 2);
 }
@@ -1381,7 +1391,9 @@ struct JobList {
         j.vec = op == kOpCopy && width % 4 == 0 && pstride % 4 == 0 &&
                 reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
                 reinterpret_cast<uintptr_t>(dst) % 16 == 0;
-        blocks += j.vec ? (width / 4 + 31) / 32 : (width + 31) / 32;
+        const int cols = j.vec ? width / 4 : width;
+        j.cb = cols <= 8 ? 8 : cols <= 16 ? 16 : 32;
+        blocks += (cols + j.cb - 1) / j.cb;
     }
 };
 
@@ -1440,8 +1452,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     for (int h = 0; h < 2; ++h)
         if (w->stride[h] < 0 || (w->stride[h] && !w->blk_cnt[h])) return REGNN_EINVAL;
     const regnn_nsm_adam* ad = w->adam;
-    if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step ||
-               !ad->ticket))
+    if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step))
         return REGNN_EINVAL;
     const Slab2 S = slab2(p, w->cap[0]);
     const Drop drop = make_drop(p->p_drop);
@@ -1525,6 +1536,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         B.rw = p->conv_rw[0]; B.n_rel = p->n_rel[0]; B.alpha = p->alpha; B.n_et = p->n_edge_types;
         B.u_self = w->u_self; B.u_rel = w->u_rel; B.z = w->z; B.beta = w->beta;
         B.slab = w->slab + S.proj; B.rslab = w->slab + S.rel0; B.slab0 = w->slab + S.post0;
+        B.adam_step = ad ? ad->step : nullptr;
         const dim3 grid(kBwdBlocks, T);
 #define BWD0_CASE(KK, RS)                                                                      \
         if (K == KK && rs == RS) {                                                             \
@@ -1576,8 +1588,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
             O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;
             O.n = ad->n;
             O.lr = ad->lr; O.b1 = ad->beta1; O.b2 = ad->beta2; O.eps = ad->eps;
-            O.wd = ad->weight_decay; O.gscale = ad->grad_scale; O.step = ad->step;
-            O.ticket = ad->ticket; O.on = 1;
+            O.wd = ad->weight_decay; O.gscale = ad->grad_scale; O.step = ad->step; O.on = 1;
         }
         hipLaunchKernelGGL(finalize_kernel, dim3(J.blocks), dim3(kBlock), 0, stream, J.A);
         REGNN_LAUNCH_CHECK();
