@@ -1420,38 +1420,61 @@ __global__ void __launch_bounds__(kBlock) chain_kernel(ChainArgs A) {
 // decay added to the gradient). The step count lives on the device: every block uses
 // t = step[0] + 1 and the last block to finish stores it (ticket), so a captured graph advances
 // it on every replay.
+// one element of torch.optim.Adam (L2 weight decay added to the gradient)
+__device__ __forceinline__ void adam_one(float gi, float& pi, float& mi, float& vi, float b1,
+                                         float b2, float eps, float wd, float gscale,
+                                         float step_size, float bc2_sqrt) {
+    gi *= gscale;                              // gscale: 1 / ranks after a SUM all-reduce
+    if (wd != 0.f) gi = gi + wd * pi;
+    mi = mi + (1.f - b1) * (gi - mi);                                  // exp_avg.lerp_(grad, 1-b1)
+    vi = vi * b2 + (1.f - b2) * gi * gi;                               // mul_(b2).addcmul_
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+}
+
+// V = 4: four elements per thread through float4 (n % 4 == 0, 16-byte aligned buffers): a
+// quarter of the blocks, so a quarter of the completion tickets on the one counter (each block's
+// returning atomic on it serialises at the end of the launch)
+template <int V>
 __global__ void __launch_bounds__(kBlock)
 adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                  float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
                  float wd, float gscale, int64_t* __restrict__ step, unsigned* __restrict__ ticket) {
+    using VT = typename std::conditional<V == 4, float4, float>::type;
     __shared__ bool last;
-    // the first element's operands are requested together with the step count (independent
-    // loads: one memory latency, not two, before the first update)
+    // the first operands are requested together with the step count (independent loads: one
+    // memory latency, not two, before the first update)
+    const int64_t nv = n / V;
     const int64_t i0 = int64_t(blockIdx.x) * kBlock + threadIdx.x, stride = int64_t(gridDim.x) * kBlock;
-    float g0 = 0.f, p0 = 0.f, m0 = 0.f, v0 = 0.f;
-    if (i0 < n) {
-        g0 = g[i0]; p0 = p[i0]; m0 = m[i0]; v0 = v[i0];
+    VT g0{}, p0{}, m0{}, v0{};
+    if (i0 < nv) {
+        g0 = reinterpret_cast<const VT*>(g)[i0]; p0 = reinterpret_cast<const VT*>(p)[i0];
+        m0 = reinterpret_cast<const VT*>(m)[i0]; v0 = reinterpret_cast<const VT*>(v)[i0];
     }
     const int64_t t = step[0] + 1;
     const double bc1 = 1.0 - pow(double(b1), double(t));
     const double bc2 = 1.0 - pow(double(b2), double(t));
     const float step_size = float(double(lr) / bc1);
     const float bc2_sqrt = float(sqrt(bc2));
-    for (int64_t i = i0; i < n; i += stride) {
-        float gi, pi, mi, vi;
+    for (int64_t i = i0; i < nv; i += stride) {
+        VT gi, pi, mi, vi;
         if (i == i0) {
             gi = g0; pi = p0; mi = m0; vi = v0;
         } else {
-            gi = g[i]; pi = p[i]; mi = m[i]; vi = v[i];
+            gi = reinterpret_cast<const VT*>(g)[i]; pi = reinterpret_cast<const VT*>(p)[i];
+            mi = reinterpret_cast<const VT*>(m)[i]; vi = reinterpret_cast<const VT*>(v)[i];
         }
-        gi *= gscale;                          // gscale: 1 / ranks after a SUM all-reduce
-        if (wd != 0.f) gi = gi + wd * pi;
-        const float mn = mi + (1.f - b1) * (gi - mi);                 // exp_avg.lerp_(grad, 1-b1)
-        const float vn = vi * b2 + (1.f - b2) * gi * gi;               // mul_(b2).addcmul_
-        m[i] = mn;
-        v[i] = vn;
-        const float denom = sqrtf(vn) / bc2_sqrt + eps;
-        p[i] = pi - step_size * (mn / denom);
+        if constexpr (V == 4) {
+            adam_one(gi.x, pi.x, mi.x, vi.x, b1, b2, eps, wd, gscale, step_size, bc2_sqrt);
+            adam_one(gi.y, pi.y, mi.y, vi.y, b1, b2, eps, wd, gscale, step_size, bc2_sqrt);
+            adam_one(gi.z, pi.z, mi.z, vi.z, b1, b2, eps, wd, gscale, step_size, bc2_sqrt);
+            adam_one(gi.w, pi.w, mi.w, vi.w, b1, b2, eps, wd, gscale, step_size, bc2_sqrt);
+        } else {
+            adam_one(gi, pi, mi, vi, b1, b2, eps, wd, gscale, step_size, bc2_sqrt);
+        }
+        reinterpret_cast<VT*>(m)[i] = mi;
+        reinterpret_cast<VT*>(v)[i] = vi;
+        reinterpret_cast<VT*>(p)[i] = pi;
     }
     // the ticket only orders every block's read of step[0] (its value is consumed above) before
     // the last block's store of it; the parameter stores need no fence before it
@@ -1761,10 +1784,18 @@ int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_
                     float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream) {
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !ticket || n < 0) return REGNN_EINVAL;
     if (n == 0) return REGNN_OK;
-    int64_t grid = (n + kBlock - 1) / kBlock;
+    auto al = [](const void* q) { return reinterpret_cast<uintptr_t>(q) % 16 == 0; };
+    const bool vec = n % 4 == 0 && al(param) && al(grad) && al(exp_avg) && al(exp_avg_sq);
+    int64_t grid = (n / (vec ? 4 : 1) + kBlock - 1) / kBlock;
     if (grid > 1024) grid = 1024;
-    hipLaunchKernelGGL(adam_flat_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, stream, param, grad,
-                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, grad_scale, step, ticket);
+    if (vec)
+        hipLaunchKernelGGL(adam_flat_kernel<4>, dim3(unsigned(grid)), dim3(kBlock), 0, stream, param,
+                           grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay,
+                           grad_scale, step, ticket);
+    else
+        hipLaunchKernelGGL(adam_flat_kernel<1>, dim3(unsigned(grid)), dim3(kBlock), 0, stream, param,
+                           grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay,
+                           grad_scale, step, ticket);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

@@ -526,6 +526,45 @@ class FusedStep:
                    torch.cuda.current_stream(self.device).cuda_stream)
 
 
+def group_sizes(ahead):
+    """the multi-step graph lengths at lookahead `ahead` > 1: ahead, ahead / 2, .., 2."""
+    out, m = [], int(ahead)
+    while m >= 2:
+        out.append(m)
+        m //= 2
+    return out
+
+
+def plan_run(cur, k, ahead, n_slots, have=lambda m, start: True):
+    """the replays NSTrainer.run_steps issues for k steps from slot `cur` at lookahead `ahead`
+    > 1: [(m, start)], m = 1 for a one-step graph; the longest captured group (`have`) that
+    fits the remaining steps, from wherever cur stands."""
+    out = []
+    while k > 0:
+        m = next((m for m in group_sizes(ahead) if m <= k), 1)
+        if m > 1 and not have(m, cur):
+            m = 1
+        out.append((m, cur))
+        cur = (cur + m) % n_slots
+        k -= m
+    return out
+
+
+def warm_walk(ahead, n_slots):
+    """the replays capture() runs once each (a graph's first launch is slow), in training order
+    from slot 0: for every group length m, n_slots times a group then one single step (the start
+    advances by m + 1, odd, so it visits every slot) -- every (m, start) group and every
+    one-step graph."""
+    out, cur = [], 0
+    for m in group_sizes(ahead):
+        for _ in range(n_slots):
+            out.append((m, cur))
+            cur = (cur + m) % n_slots
+            out.append((1, cur))
+            cur = (cur + 1) % n_slots
+    return out
+
+
 def _capturing(g):
     """capture into g with the thread-local error mode: with several ranks the process group's
     watchdog thread polls the eager all-reduces' events meanwhile, which the global mode counts
@@ -771,12 +810,7 @@ class NSTrainer:
         cs.wait_stream(self._side)
 
     def _group_sizes(self):
-        """the multi-step graph lengths at lookahead > 1: ahead, ahead / 2, .., 2 (descending)."""
-        out, m = [], self.ahead
-        while m >= 2:
-            out.append(m)
-            m //= 2
-        return out
+        return group_sizes(self.ahead)
 
     def _advance(self):
         self._trained, self.cur = self.cur, (self.cur + 1) % len(self.slots)
@@ -998,12 +1032,10 @@ class NSTrainer:
             # executable graph); replay each once here, walking the slots in training order,
             # and undo those steps as the warm-up's
             n = len(self.slots)
-            for m in self._group_sizes():
-                for _ in range(n):             # start advances by m + 1 (odd: every slot)
-                    self.graph_groups[(m, self.cur)].replay()
-                    self.cur = (self.cur + m) % n
-                    g1[self.cur].replay()
-                    self.cur = (self.cur + 1) % n
+            for m, start in warm_walk(self.ahead, n):
+                assert start == self.cur
+                (g1[start] if m == 1 else self.graph_groups[(m, start)]).replay()
+                self.cur = (self.cur + m) % n
             self._undo_steps(saved, st0)
 
     def _undo_steps(self, saved, st0):
@@ -1020,25 +1052,22 @@ class NSTrainer:
         self.cur, self._primed, self._trained = 0, False, 0
 
     def run_steps(self, k):
-        """k training steps as graph replays (capture() first): runs of 4 or 2 steps starting at
-        slot 0 replay the multi-step graphs, the rest the one-step graphs; the same steps as k
-        replay()s."""
+        """k training steps as graph replays (capture() first), the same steps as k replay()s:
+        lookahead > 1: the multi-step groups plan_run picks from any slot; lookahead 1: runs of
+        4 or 2 steps from slot 0 as one graph, the rest one-step graphs."""
         k = int(k)
         groups = getattr(self, "graph_groups", {})
-        while k > 0:
-            if self.ahead > 1:
-                m = next((m for m in self._group_sizes() if m <= k), 1)
-                g = groups.get((m, self.cur))
-                if g is None:
+        if self.ahead > 1:
+            n = len(self.slots)
+            for m, start in plan_run(self.cur, k, self.ahead, n, lambda m, c: (m, c) in groups):
+                if m == 1:
                     self.replay()
-                    k -= 1
                     continue
                 self._prime()
-                g.replay()
-                n = len(self.slots)
-                self._trained, self.cur = (self.cur + m - 1) % n, (self.cur + m) % n
-                k -= m
-                continue
+                groups[(m, start)].replay()
+                self._trained, self.cur = (start + m - 1) % n, (start + m) % n
+            return
+        while k > 0:
             n = next((n for n in sorted(groups, reverse=True) if n <= k), 0)
             if n and self.cur == 0 and self._primed:
                 groups[n].replay()
