@@ -25,7 +25,8 @@ At N = 1 the line also carries, on the same graph generator:
     spec, REGNN fwd+bwd as the reference composes it, nll, Adam; mag_like(1)), with the
     full-graph REGraphConv stack (oracle/cpu_regcn.py) under "full_batch".
 
-Launch: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Launch: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or
+    python bench.py --gpus N (starts that launcher itself as a child process), or
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ns|mag|dblp|acm|imdb|...]
 """
 import argparse
@@ -74,6 +75,20 @@ def setup_dist(n):
     local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     return rank, world, torch.device("cuda", local)
+
+
+def self_launch(n):
+    """run this script under `python -m torch.distributed.run --nproc-per-node n` (127.0.0.1, a
+    free port) as a child process; rank 0 prints the JSON line. Returns the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])} {' '.join(sys.argv[1:])}")
+    return subprocess.call(cmd + sys.argv[1:])
 
 
 def _world():
@@ -264,6 +279,15 @@ def run_ns(args, dev):
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
         edges = float(e.item())
     ms = elapsed / args.steps * 1e3
+    exchanged = world > 1 or tr._force_exchange
+    if not exchanged:
+        exchange = None
+    elif not use_graph:
+        exchange = "eager all-reduce after each step"
+    elif tr.exchange_in_graph:
+        exchange = "all-reduce captured in the step graph"
+    else:
+        exchange = "eager all-reduce between graphs"
     res = {
         "metric": METRIC,
         "value": edges / elapsed,
@@ -280,15 +304,15 @@ def run_ns(args, dev):
         "config": {
             "workload": (f"mag/regnn_ns.py REGCN neighbour-sampled train step: device sampler "
                          f"{args.batch} papers/rank x fan-out [25, 20], group_input, 2x REGCNConv "
-                         f"(mean, relation table, LN, ReLU, dropout {args.dropout}), out_lin 349, "
-                         f"nll, backward, RCCL flat-bucket grad all-reduce, Adam; "
-                         f"mag_like(scale={args.scale}) replicated per rank"),
-            "nodes": info["N"], "edges": info["E"], "relations": 11, "hidden": 64,
+                         f"(hidden {args.hidden}, mean, relation table, LN, ReLU, dropout "
+                         f"{args.dropout}), out_lin 349, nll, backward, "
+                         + (f"{dist.get_backend() if dist.is_initialized() else ''} flat-bucket "
+                            f"grad all-reduce ({exchange}), " if exchange else "")
+                         + f"Adam; mag_like(scale={args.scale}) replicated per rank"),
+            "nodes": info["N"], "edges": info["E"], "relations": 11, "hidden": args.hidden,
             "batch_per_rank": args.batch, "global_batch": args.batch * world,
             "fanout": [25, 20], "parallelism": f"dp{world}",
-            "grad_exchange": (None if world == 1 and not tr._force_exchange else
-                              "eager all-reduce between graphs" if use_graph and tr.graphs[1] is not None
-                              else "all-reduce captured in the step graph" if use_graph else "eager"),
+            "grad_exchange": exchange,
             "lookahead": tr.ahead,
             "hip_graph": use_graph, "aggregated_edges_per_step_per_rank": edges / world / args.steps,
             "final_loss": loss,
@@ -469,7 +493,7 @@ def pmc_traffic_ns(args):
         return None, "no PMC summary committed"
     with open(path) as f:
         rec = json.load(f)
-    want = {"scale": args.scale, "batch": args.batch, "fanout": [25, 20], "hidden": 64,
+    want = {"scale": args.scale, "batch": args.batch, "fanout": [25, 20], "hidden": args.hidden,
             "dropout": args.dropout}
     if rec.get("config") != want:
         return None, f"PMC summary is for another config ({rec.get('config')})"
@@ -677,6 +701,10 @@ def main():
     ap.add_argument("--no-full-batch", action="store_true",
                     help="ns at N=1: skip the full-graph roofline leg")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks as a child
+        # torch.distributed.run (this process never touches the GPU) and exit with its code
+        sys.exit(self_launch(args.gpus))
 
     rank, world, dev = setup_dist(args.gpus)
     if args.workload == "ns":
@@ -716,11 +744,17 @@ def main():
                 "value": e / t, "unit": "edges/s", "cores": info["threads"], "kind": "port",
                 "cpu_model": _cpu_model(), "ms_per_step": t * 1e3,
                 "aggregated_edges_per_step": e,
+                "value_aggregated_edges_per_step": result["config"].get(
+                    "aggregated_edges_per_step_per_rank"),
                 "sample": (f"oracle/cpu_ns.py: the NS training step (the sampler spec, REGNN "
                            f"regcn/LN fwd+bwd with index_add scatter as the reference composes "
                            f"it, nll, Adam) on mag_like(1) N={info['N']:,} E={info['E']:,}, "
                            f"batch {info['batch']} x {info['sizes']}, hidden 64, 349 classes, "
-                           f"dropout 0.5; median of 10 steps after 3 warm-ups"),
+                           f"dropout 0.5; median of 10 steps after 3 warm-ups. Same generator "
+                           f"at 1/10 the size of value's mag_like({args.scale:g}): "
+                           f"{e:,.0f} aggregated edges per step here against "
+                           f"{result['config'].get('aggregated_edges_per_step_per_rank', 0):,.0f} "
+                           f"per rank-step in value (both rates are per aggregated edge)"),
                 "full_batch": full}
         else:
             result["cpu_baseline"] = full

@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 35). */
+/* ABI version (bumped on any signature or semantics change; currently 36). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -708,6 +708,10 @@ typedef struct regnn_nsm_params {
                                  rows per source type unweighted and the relation-table gradient
                                  comes from those sums (no second pass over the edges; needs
                                  u_self / u_rel); 0: the edge pass */
+    int32_t two_layer;        /* 1: the caller set up the two-layer form (L = 2, C <= 416, hop 0's
+                                 edge capacity <= 32768, regnn_nsm_work.p0 / gh1 / csc_* set):
+                                 regnn_nsm_step and regnn_nsm_slab_floats take that form only
+                                 then, one decision for both; 0: the composed-map form (ABI 36) */
 } regnn_nsm_params;
 
 typedef struct regnn_nsm_work {

@@ -836,7 +836,7 @@ def remixhop_model(g, feats, rel, P, num_layers, hidden, alpha, gout, p=(0, 1, 2
 # mag REGNN (mag/regnn_ns.py:216-346) + nll_loss (:404), eval mode, on a sampled batch
 # ------------------------------------------------------------------------------------------
 def mag_regnn_model(x_dict, node_type, local, n_id, adjs, edge_type, P, y, feats_type=3,
-                    num_edge_types=7, alpha=10.0, target_node_type=0):
+                    num_edge_types=7, alpha=10.0, target_node_type=0, residual=False):
     """forward + VJP of the reference REGNN for model 'regcn', self_loop_type 2, LayerNorm.
     adjs: [(src_local, dst_local, e_id, (n_src, n_dst))] outermost hop first (PyG order).
     Returns (log-probabilities, mean nll loss, {parameter name: gradient})."""
@@ -865,7 +865,7 @@ def mag_regnn_model(x_dict, node_type, local, n_id, adjs, edge_type, P, y, feats
     for i, (s_, d_, e_, size) in enumerate(adjs):                    # regnn_ns.py:335-343
         ntype = ntype[:size[1]]
         pc = {k[len(f"convs.{i}."):]: v for k, v in P.items() if k.startswith(f"convs.{i}.")}
-        o = MagREGCNConvOracle(size[1], num_edge_types, alpha, residual=False, use_norm="ln")
+        o = MagREGCNConvOracle(size[1], num_edge_types, alpha, residual=residual, use_norm="ln")
         yv = o.forward(x, np.asarray(s_), np.asarray(d_), et[np.asarray(e_)], ntype, pc)
         caches.append((o, yv))
         x = np.maximum(yv, 0)

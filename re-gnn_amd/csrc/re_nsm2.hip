@@ -1438,8 +1438,10 @@ int64_t regnn_nsm2_slab_floats(const regnn_nsm_params* p, int32_t cap0) {
     return slab2(p, cap0).total;
 }
 
+// the caller's two_layer flag decides (it allocated the two-layer buffers: hop 0's edge capacity
+// fits the transposed index), so the slab size and the step always agree
 bool regnn_nsm2_covers(const regnn_nsm_params* p) {
-    return p->n_layers == 2 && p->n_classes <= 16 * kMaxCT &&
+    return p->two_layer == 1 && p->n_layers == 2 && p->n_classes <= 16 * kMaxCT &&
            head_lds(p->n_classes) <= size_t(160 * 1024 - 2560);
 }
 

@@ -58,6 +58,10 @@ class REGCNConv(torch.nn.Module):
 
     def reset_parameters(self):
         init.xavier_uniform_(self.weight)
+        if self.residual:
+            # weight_root IS weight: the reference draws it a second time (:73-74), so a seeded
+            # model's weights (and the RNG stream after them) match the reference's only with it
+            init.xavier_uniform_(self.weight_root)
         init.zeros_(self.bias)
         init.constant_(self.relation_weight, 1.0 / self.scaling_factor)
         if self.use_norm in ('bn', 'ln'):
@@ -295,8 +299,10 @@ class REGNN(torch.nn.Module):
                 for k in sorted(set(num_feature_dict) - {target_node_type})})
             self.lin = Linear(in_channels, self.hidden_dim)
         else:
-            self.lins = ModuleDict({str(k): Linear(d, self.hidden_dim)
-                                    for k, d in num_feature_dict.items()})
+            # created in the reference's order (`for key in set(node_types)`, :248-250): the RNG
+            # stream of a seeded construction then matches
+            self.lins = ModuleDict({str(k): Linear(num_feature_dict[k], self.hidden_dim)
+                                    for k in set(num_feature_dict)})
         if model == 'regcn':                                                # regnn_ns.py:245-270
             convs = [REGCNConv(hidden_channels, hidden_channels, self.num_node_types,
                                num_edge_types, scaling_factor, dropout=dropout,
@@ -315,9 +321,22 @@ class REGNN(torch.nn.Module):
             self.norm = torch.nn.LayerNorm(self.hidden_dim)   # declared, unused in forward
         elif use_norm == 'bn':
             self.norm = torch.nn.BatchNorm1d(self.hidden_dim)
-        if feats_type == 2:
-            for emb in self.emb_dict.values():                              # :289-292
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        """mag/regnn_ns.py:284-298, in its order (a seeded model draws the reference's values)."""
+        if self.feats_type == 2:
+            for emb in self.emb_dict.values():
                 init.xavier_uniform_(emb)
+            self.lin.reset_parameters()
+        else:
+            for lin in self.lins.values():
+                lin.reset_parameters()
+        for conv in self.convs:
+            conv.reset_parameters()
+        self.out_lin.reset_parameters()
+        if hasattr(self, "norm"):
+            self.norm.reset_parameters()
 
     def embedding_tables(self):
         """[(table parameter, local rows the last forward read)] of the feats_type-2 tables."""

@@ -136,6 +136,7 @@ class DeviceSampler:
         # meta_only[h]: hop h writes only the edge meta its consumer reads (regnn_ns_hop
         # meta_only: no de-duplication, n_id not extended, sampled blk_idx unwritten)
         self.meta_only = [False] * len(self.sizes_k)
+        self._csr_fresh = True
 
     def enable_edge_meta(self, local_node_idx, hop):
         """also write hop `hop`'s per-edge source node type and table row (regnn_ns_hop's
@@ -187,6 +188,8 @@ class DeviceSampler:
                      else (None, None, None, None)),
                    int(strided), L.stream())
             self.meta_fresh[h] = self.edge_meta[h] is not None
+        # the blocks now hold the CSR layout (readable by exact_adjs / model_blocks) or not
+        self._csr_fresh = not strided
 
     def set_seed(self, base_seed, epoch, batch_idx):
         """host-driven batches (the PyG-style iterator): seed words + a fresh dedup stamp."""
@@ -207,14 +210,25 @@ class DeviceSampler:
         self.sizes[0:1].fill_(n)
         self.sizes[8:16].zero_()               # strided hops add their edge counts
 
+    def _check_csr(self, what):
+        if self.strided:
+            raise RuntimeError(f"{what} reads CSR blocks, but this sampler writes the fused "
+                               "step's fixed-stride layout (FusedStep set strided = True); call "
+                               "run_hops(strided=False) first and read the blocks before the "
+                               "next fused step")
+
     def model_blocks(self):
         """blocks in the model's layer order (outermost hop first, PyG adjs[::-1])."""
+        if self.strided and not self._csr_fresh:
+            self._check_csr("model_blocks()")
         return self.blocks[::-1]
 
     def exact_adjs(self):
         """PyG-style per-hop output at exact sizes (one host sync): [(edge_index [2, M] local
         (src, dst) without self loops, dst-major; e_id; (n_src, n_dst); NSBlock copy)], hop
         order (innermost first)."""
+        if self.strided and not self._csr_fresh:
+            self._check_csr("exact_adjs()")
         sz = self.sizes.cpu().tolist()
         out = []
         for h in range(len(self.sizes_k)):
@@ -250,7 +264,8 @@ class _NsmParams(ctypes.Structure):
                 ("g_lin_w", _P * _MT), ("g_lin_b", _P * _MT), ("g_conv_w", _P * _ML),
                 ("g_conv_b", _P * _ML), ("g_conv_rw", _P * _ML), ("g_ln_w", _P * _ML),
                 ("g_ln_b", _P * _ML), ("g_out_w", _P), ("g_out_b", _P), ("loss", _P),
-                ("n_edge_types", ctypes.c_int32), ("rel_slots", ctypes.c_int32)]
+                ("n_edge_types", ctypes.c_int32), ("rel_slots", ctypes.c_int32),
+                ("two_layer", ctypes.c_int32)]
 
 
 class _NsmWork(ctypes.Structure):
@@ -455,6 +470,9 @@ class FusedStep:
         # the two-layer step: layer 0 rows' fixed-point gradient sums and group_input's projection
         self.two_layer = (nl == 2 and C <= TWO_LAYER_MAX_CLASSES and
                           sampler.blocks[0].csr_idx.numel() <= 32768)
+        # one decision for the library's slab size and step (regnn_nsm_params.two_layer): a
+        # batch whose hop-0 block exceeds the transposed index runs the composed-map form
+        P.two_layer = int(self.two_layer)
         if self.two_layer:
             W.p0 = ptr(z(caps[1], 64))
             W.gh1 = ptr(z(caps[0], 64))
@@ -703,6 +721,7 @@ class NSTrainer:
             for fs in (self.fused_slots if self.pipelined else [self.fused]):
                 fs.attach_adam(self.opt, self.flat)
         self.graphs = None
+        self.exchange_in_graph = False         # capture() sets it: the all-reduce is in the graphs
         # tests: all-reduce the bucket even with one rank (the captured-exchange path on one GPU)
         self._force_exchange = False
         self.epoch = -1
@@ -944,18 +963,43 @@ class NSTrainer:
                                      dist.get_backend() == "nccl")
         if multi and exchange_in_graph:
             saved_state = ([s.state.clone() for s in self.slots], self._train_state())
+            err = None
             try:
-                return self._capture(warmup, True)
+                # capture only: nothing replays (no collective runs) until every rank agreed
+                self._capture(warmup, True, warm=False)
             except RuntimeError as e:          # torch.AcceleratorError is a RuntimeError
-                import warnings
-                warnings.warn(f"capturing the all-reduce into the step graph failed ({e}); "
-                              "falling back to the eager exchange between graphs")
-                torch.cuda.synchronize(self.device)
-                self._undo_steps(saved_state[1], saved_state[0])
-                self.graphs, self.graph_groups = None, {}
-        return self._capture(warmup, exchange_in_graph)
+                err = e
+            # one decision for all ranks, before any replay: a rank replaying graphs with
+            # captured all-reduces beside one running eager exchanges would hang the group
+            if self._ranks_agree(err is None):
+                self._warm_graphs()
+                self.exchange_in_graph = True
+                return
+            import warnings
+            why = f"this rank: {err}" if err is not None else "another rank's capture failed"
+            warnings.warn(f"capturing the all-reduce into the step graph failed ({why}); every "
+                          "rank falls back to the eager exchange between graphs")
+            torch.cuda.synchronize(self.device)
+            self.graphs, self.graph_groups = None, {}
+            self._undo_steps(saved_state[1], saved_state[0])
+            exchange_in_graph = False
+        self._capture(warmup, bool(exchange_in_graph))
+        self.exchange_in_graph = bool(multi and exchange_in_graph)
 
-    def _capture(self, warmup, exchange_in_graph):
+    def _ranks_agree(self, ok):
+        """True when `ok` holds on every rank (an eager MAX all-reduce of the failure flags; one
+        rank: ok itself)."""
+        import torch.distributed as dist
+        if self.world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return bool(ok)
+        dev = self.device if dist.get_backend() == "nccl" else "cpu"
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        return int(flag.item()) == 0
+
+    def _capture(self, warmup, exchange_in_graph, warm=True):
+        """the eager warm-up steps (undone), then the graphs; warm: replay every multi-step
+        graph once (_warm_graphs) -- capture() defers that until the ranks agreed."""
         multi = self.world > 1 or self._force_exchange
         if self.fused is None and not self._blocks_ok:
             raise ValueError("this model's module path reads exact-size adjs (a host sync per "
@@ -1027,10 +1071,18 @@ class NSTrainer:
             with _capturing(g2):
                 self.opt.step()
         self.graphs = (g1, g2)
+        self._cap_undo = (saved, st0, fold_opt)
+        if warm:
+            self._warm_graphs()
+
+    def _warm_graphs(self):
+        """every graph's first launch is slow (tens of us: the runtime's one-time work per
+        executable graph); replay each once, walking the slots in training order, and undo those
+        steps as the warm-up's (pipelined lookahead groups only)."""
+        saved, st0, fold_opt = self._cap_undo
+        self._cap_undo = None
         if self.pipelined and fold_opt and self.ahead > 1:
-            # every graph's first launch is slow (tens of us: the runtime's one-time work per
-            # executable graph); replay each once here, walking the slots in training order,
-            # and undo those steps as the warm-up's
+            g1 = self.graphs[0]
             n = len(self.slots)
             for m, start in warm_walk(self.ahead, n):
                 assert start == self.cur

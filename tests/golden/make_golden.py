@@ -632,9 +632,106 @@ def gen_regnn_schema():
                                   schema="ogbn-mag"), st)
 
 
+def gen_regnn_ft5():
+    """The reference's default NS model shape: the reference REGNN on the
+    ogbn-mag-schema graph with feats_type 5's unequal input widths (mag/regnn_ns.py:185-194:
+    paper rows = cat(raw 128-d, a 128-d embedding) = 256-d, every other type a 128-d embedding),
+    hidden 128, residual on (:62), LayerNorm, 349 classes, fan-out [25, 20], dropout 0: loss and
+    every gradient."""
+    from types import SimpleNamespace
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import sampler_oracle as SO
+    rng = np.random.default_rng(91)
+    counts = [150, 36, 12, 120]                    # author, field_of_study, institution, paper
+    src, dst, edge_type, ntype, local, p0 = _mag_schema_graph(rng, counts)
+    N = int(sum(counts))
+    ptr = np.zeros(N + 1, np.int64)
+    np.add.at(ptr, dst + 1, 1)
+    ptr = np.cumsum(ptr)
+    batch = (p0 + rng.choice(counts[3], 20, replace=False)).astype(np.int64)
+    batch[:2] = p0 + np.arange(2)
+    sizes, seed, epoch, batch_idx = [25, 20], 5, 2, 3
+    _, n_id, adjs = SO.neighbor_sample(ptr, src, batch.tolist(), sizes, seed, epoch, batch_idx)
+    H, C = 128, 349
+    dims = {0: 128, 1: 128, 2: 128, 3: 256}
+    y = np.full(N, -1, np.int64)
+    y[p0:] = rng.integers(0, C, counts[3])
+    args = SimpleNamespace(model="regcn", feats_type=5, self_loop_type=2, no_re=False)
+    REGNN = _reference_regnn_class(args, {t: counts[t] for t in range(4)}, 3, regnn_layers)
+    torch.manual_seed(13)
+    model = REGNN(128, H, C, 1, 2, 10.0, 0.0, dims, 7, True, False, use_norm="ln")
+    _set_params(model, rng, ew_alpha=10.0)
+    model.eval()
+    x_dict = {t: torch.from_numpy(f32(rng, counts[t], dims[t], scale=0.5).astype(np.float64))
+              for t in range(4)}
+    t_adjs = [(torch.tensor([s_, d_], dtype=torch.int64), torch.tensor(e_, dtype=torch.int64), sz)
+              for s_, d_, e_, sz in adjs]
+    out = model(torch.tensor(n_id), x_dict, t_adjs, torch.from_numpy(edge_type),
+                torch.from_numpy(ntype), torch.from_numpy(local))
+    loss = torch.nn.functional.nll_loss(out, torch.from_numpy(y[batch]))
+    loss.backward()
+    st = dict(src=src, dst=dst, edge_type=edge_type, ntype=ntype, local=local, y=y, batch=batch,
+              n_id=np.asarray(n_id, np.int64), logp=out, loss=loss.detach())
+    for t, x in x_dict.items():
+        st[f"x{t}"] = x.numpy().astype(np.float32)
+    for h, (s_, d_, e_, sz) in enumerate(adjs):
+        st[f"adj{h}_src"], st[f"adj{h}_dst"] = np.asarray(s_), np.asarray(d_)
+        st[f"adj{h}_eid"] = np.asarray(e_)
+        st[f"adj{h}_size"] = np.asarray(sz)
+    _pack("p_", _params(model), st)
+    _pack("grad_", _grads(model), st)
+    save("mag_regnn_ft5_h128", dict(model="mag.REGNN", feats_type=5, in_channels=128, hidden=H,
+                                    classes=C, num_layers=2, scaling_factor=10.0,
+                                    num_edge_types=7, counts=counts, target_type=3,
+                                    target_offset=p0, y_global=True, sizes=sizes, seed=seed,
+                                    epoch=epoch, batch_idx=batch_idx, use_norm="ln",
+                                    self_loop_type=2, dropout=0.0, schema="ogbn-mag",
+                                    residual=True, feature_dims=[dims[t] for t in range(4)]), st)
+
+
+def gen_regnn_init():
+    """Seeded initial parameters of the reference's REGNN (mag/regnn_ns.py:216-298: every module
+    constructed, then reset_parameters() again; REGCNConv draws weight_root = weight a second
+    time when residual, mag/regnn_layers.py:71-78) for a few configurations, drawn in float32
+    (the dtype the build's modules are created in): the build must consume the same RNG stream."""
+    from types import SimpleNamespace
+    _purge(["dgl", "layer", "model", "utils", "regnn_layers", "torch_geometric", "torch_scatter",
+            "torch_sparse", "ogb", "texttable"])
+    _use_paths([SHIM, os.path.join(REF, "mag")])
+    regnn_layers = importlib.import_module("regnn_layers")
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float32)
+    cfgs = [dict(feats_type=3, hidden=64, residual=False, dims=[128, 128, 128, 128], seed=3),
+            dict(feats_type=5, hidden=128, residual=True, dims=[128, 128, 128, 256], seed=4),
+            dict(feats_type=2, hidden=64, residual=True, dims=[128, 128, 128, 128], seed=6)]
+    counts = {0: 30, 1: 9, 2: 5, 3: 20}
+    st, meta = {}, []
+    try:
+        for i, c in enumerate(cfgs):
+            args = SimpleNamespace(model="regcn", feats_type=c["feats_type"], self_loop_type=2,
+                                   no_re=False)
+            REGNN = _reference_regnn_class(args, counts, 3, regnn_layers)
+            torch.manual_seed(c["seed"])
+            m = REGNN(128, c["hidden"], 349, 1, 2, 10.0, 0.5,
+                      {t: c["dims"][t] for t in range(4)}, 7, c["residual"], False,
+                      use_norm="ln")
+            _pack(f"c{i}_p_", _params(m), st)
+            meta.append(dict(c, counts=[counts[t] for t in range(4)], target_type=3,
+                             classes=349, num_layers=2, scaling_factor=10.0, dropout=0.5,
+                             num_edge_types=7, in_channels=128))
+    finally:
+        torch.set_default_dtype(prev)
+    save("mag_regnn_init", dict(configs=meta), st)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float64)
-    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat", "regnn", "schema"]
+    which = sys.argv[1:] or ["layers", "models", "mag", "extra", "maggat", "regnn", "schema",
+                             "ft5", "init"]
     if "layers" in which:
         gen_layers()
     if "models" in which:
@@ -649,3 +746,7 @@ if __name__ == "__main__":
         gen_regnn()
     if "schema" in which:
         gen_regnn_schema()
+    if "ft5" in which:
+        gen_regnn_ft5()
+    if "init" in which:
+        gen_regnn_init()

@@ -216,3 +216,113 @@ def test_ns_allreduce_captured_in_step_graph():
     assert not isinstance(res, str), res
     for la, lb, same in res:
         assert la == lb and same
+
+
+def _fallback_worker(rank, world, port, q):
+    """rank 1's in-graph capture fails (injected), rank 0's succeeds (its captured exchange
+    stubbed: gloo cannot be captured): capture() must agree across ranks and fall back to the
+    eager exchange on BOTH, with the fallback really capturing without the exchange."""
+    try:
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "re-gnn_amd"))
+        import warnings
+        from test_gpu_ns_engine import _mag
+        from regnn_hip.ns import NSTrainer
+        d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.3)
+
+        def make():
+            return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 64,
+                             torch.arange(d["n_paper"], device="cuda"), d["x_dict"],
+                             d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=9,
+                             rank=rank, world=world, adam=dict(lr=1e-2))
+
+        out = {}
+        for mode in ("fallback", "eager"):
+            tr = make()
+            if mode == "fallback":
+                orig = tr._exchange
+
+                def exchange(orig=orig):
+                    if torch.cuda.is_current_stream_capturing():
+                        if rank == 1:
+                            raise RuntimeError("injected: all-reduce capture failed")
+                        return                  # rank 0: a captured collective's stand-in
+                    orig()
+                tr._exchange = exchange
+                with warnings.catch_warnings(record=True) as wl:
+                    warnings.simplefilter("always")
+                    tr.capture(warmup=1, exchange_in_graph=True)
+                out["warned"] = any("falls back" in str(w.message) for w in wl)
+            else:
+                tr.capture(warmup=1, exchange_in_graph=False)
+            out[mode + "_in_graph"] = tr.exchange_in_graph
+            out[mode + "_g2"] = tr.graphs[1] is not None
+            losses = []
+            for k in (3, 1, 2):
+                tr.run_steps(k)
+                torch.cuda.synchronize()
+                losses.append(float(tr.loss))
+            tr.step()                           # and an eager step after the replays
+            torch.cuda.synchronize()
+            out[mode] = tr.pflat.detach().cpu().numpy().copy()
+            out[mode + "_loss"] = losses
+            dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception as e:
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_capture_fallback_agreed_across_ranks():
+    """VERDICT r3 next 1 (a, b): capture(exchange_in_graph=True) failing on one rank only makes
+    every rank fall back to the eager exchange (a MAX all-reduce of the failure flags before any
+    replay), the fallback captures without the exchange, and both ranks then train bitwise the
+    same parameters as a run that chose the eager exchange from the start."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + ((os.getpid() + 750) % 1000)
+    procs = [ctx.Process(target=_fallback_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), f"rank {r}: {res[r]}"
+    a, b = res[0], res[1]
+    for x in (a, b):
+        assert x["warned"]
+        assert not x["fallback_in_graph"] and x["fallback_g2"]
+        assert not x["eager_in_graph"] and x["eager_g2"]
+        assert np.array_equal(x["fallback"], x["eager"])
+        assert x["fallback_loss"] == x["eager_loss"]
+    assert np.array_equal(a["fallback"], b["fallback"])
+    assert np.isfinite(a["eager_loss"]).all()
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher environment starts the
+    two ranks itself (gloo on the box's one GPU) and prints one JSON line with n_gpus 2."""
+    import json
+    import subprocess
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["REGNN_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--scale", "0.2", "--steps", "4", "--warmup", "2"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["grad_exchange"] == "eager all-reduce between graphs"
+    assert rec["value"] > 0

@@ -434,6 +434,28 @@ def test_fused_step_matches_module_path(monkeypatch, dropout, rel_slots):
         assert ok, f"{n}: rel err {err:.3e}"
 
 
+def test_fused_step_large_batch_takes_composed_form():
+    """a batch whose hop-0 block exceeds the transposed index (1300 x 26 = 33,800 >
+    32,768 edges at fan-out 25) runs regnn_nsm_step's composed-map form: the library's slab size
+    and step follow the caller's two_layer flag, and loss / gradients match the module path."""
+    d = _mag(0.003, seed=6, F=128, hidden=64, classes=37, dropout=0.0)
+    m_mod, m_fus = d["model"](1), d["model"](1)
+    tr_m, _ = _setup_trainer(d, m_mod, batch=1300, sizes=(25, 20))
+    tr_m.fused = None
+    tr_f, _ = _setup_trainer(d, m_fus, batch=1300, sizes=(25, 20))
+    assert tr_f.fused is not None and not tr_f.fused.two_layer
+    assert tr_f.fused.P.two_layer == 0
+    tr_f._forward_backward()
+    tr_m._forward_backward()
+    torch.cuda.synchronize()
+    lm, lf = float(tr_m.loss), float(tr_f.loss)
+    assert abs(lm - lf) <= 1e-5 * max(1.0, abs(lm)), (lm, lf)
+    gm = dict(m_mod.named_parameters())
+    for n, p in m_fus.named_parameters():
+        ok, err = G.close(p.grad.cpu().numpy(), gm[n].grad.cpu().numpy().astype(np.float64), 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+
+
 @pytest.mark.parametrize("flat_adam", [False, True])
 def test_fused_step_graph_replay_tracks_eager(flat_adam):
     """the fused step captured in a HIP graph: losses equal the eager twin's step by step

@@ -27,8 +27,10 @@ def _model(d):
     m = d["meta"]
     counts = m["counts"]
     K = m["in_channels"]
+    dims = m.get("feature_dims", [K] * 4)          # feats_type 5: paper rows 256-d, others 128
     model = mag.REGNN(K, m["hidden"], m["classes"], m["num_layers"], m["scaling_factor"], 0.0,
-                      {t: K for t in range(4)}, m["num_edge_types"], use_norm="ln",
+                      {t: dims[t] for t in range(4)}, m["num_edge_types"],
+                      residual=m.get("residual", False), use_norm="ln",
                       self_loop_type=2, feats_type=m["feats_type"],
                       num_nodes_dict={t: counts[t] for t in range(4)}, target_node_type=0)
     P = G.sub(d, "p_", np.float32)
@@ -48,7 +50,11 @@ def _inputs(d):
             torch.from_numpy(d["ntype"]).to(DEV), torch.from_numpy(d["local"]).to(DEV))
 
 
-@pytest.mark.parametrize("name", G.names("mag_regnn_"))
+# (mag_regnn_init holds seeded initial parameters only: tests/test_cpu_mag_init.py)
+REGNN_CASES = [n for n in G.names("mag_regnn_") if n != "mag_regnn_init"]
+
+
+@pytest.mark.parametrize("name", REGNN_CASES)
 def test_regnn_autograd_path_vs_reference(name):
     d = G.load(name)
     model = _model(d)
@@ -133,6 +139,43 @@ def test_regnn_fused_step_vs_reference(monkeypatch, name, lean):
     fs.step()
     torch.cuda.synchronize()
     _check("loss", loss, d["loss"])
+    got = {n: p.grad for n, p in model.named_parameters()}
+    for k, v in G.sub(d, "grad_").items():
+        _check(k, got[k], v)
+
+
+@pytest.mark.parametrize("lean", ["on", "off"])
+def test_regnn_module_step_ft5_vs_reference(monkeypatch, lean):
+    """the reference's default NS model shape outside the fused step --
+    feats_type 5's unequal input widths (paper 256-d, others 128-d), hidden 128, residual --
+    through NSTrainer's module path on the device sampler (typed first layer with the meta-only
+    last hop, or the full hop), against the reference REGNN's loss and every gradient (1e-5)."""
+    from regnn_hip import ns
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.ns import NSTrainer
+    monkeypatch.setitem(ns.MODULE_LEAN_HOP, "mode", lean)
+    d = G.load("mag_regnn_ft5_h128")
+    m = d["meta"]
+    N = int(sum(m["counts"]))
+    rg = RelGraph(torch.from_numpy(d["src"]), torch.from_numpy(d["dst"]), N, DEV)
+    model = _model(d)
+    model.eval()
+    x_dict, _, et, nt, loc = _inputs(d)
+    y = torch.from_numpy(d["y"]).to(DEV).reshape(-1, 1)
+    batch = torch.from_numpy(d["batch"]).to(DEV)
+    tr = NSTrainer(model, None, rg, m["sizes"], batch.numel(), batch, x_dict, et, nt, loc, y,
+                   m["num_edge_types"], seed=m["seed"], engine="auto", pipeline=False)
+    assert tr.fused is None                     # hidden 128 / residual: the module path
+    s = tr.slots[0]
+    s.set_seed(m["seed"], m["epoch"], m["batch_idx"])
+    s.set_targets(batch)
+    s.run_hops(meta_only=tr._module_lean, strided=False)
+    L_ = len(m["sizes"])
+    n_chk = int(s.sizes[L_ - 1 if tr._module_lean else L_])
+    assert s.n_id[:n_chk].cpu().numpy().tolist() == d["n_id"][:n_chk].tolist()
+    tr._module_step(s)
+    torch.cuda.synchronize()
+    _check("loss", tr.loss, d["loss"])
     got = {n: p.grad for n, p in model.named_parameters()}
     for k, v in G.sub(d, "grad_").items():
         _check(k, got[k], v)
