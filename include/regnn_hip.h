@@ -574,14 +574,23 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * Optional (all four or none, not with meta_only): the block's transposed index -- csc_cnt
  * [cap_e] (scratch), csc_ptr [cap_e + 1] (source i's edges are csc_ent[csc_ptr[i] ..
  * csc_ptr[i + 1]) over the n_{hop+1} sources), csc_ent [cap_e] = target row << 8 | relation
- * (the order inside a segment is unspecified), csc_long [cap_e + 1] = the number of sources
- * with more than 16 edges, then their ids ascending (one more launch; cap_e <= 32768).
+ * (the order inside a segment is unspecified), csc_long [REGNN_CSC_LONG_INTS] = the number of
+ * sources with more than 16 edges (hub rows), then their ids ascending; at
+ * [REGNN_CSC_LONG_NPIECE] the number of hub pieces and from [REGNN_CSC_LONG_TAB] one int4 per
+ * piece (source, first entry in csc_ent, entries <= REGNN_CSC_PIECE, li << 16 | piece index
+ * << 8 | pieces of the row), a row's pieces consecutive (one more launch; cap_e <= 32768).
  * strided = 1: the block in the fixed-stride layout instead of the CSR -- row i's edges at
  * [i S, i S + cnt_i) (S = k + 1, cnt_i = scnt[i], sampled positions ascending), its self loop at
  * i S + cnt_i, the other slots empty (blk_idx -1); blk_ptr is not written. Sampling and
  * placement run as one launch (no row-offset scan): 5 launches with de-duplication (4 without
  * the transposed index), 1 meta-only. sizes[8 + hop] must be zero on entry (regnn_ns_batch
  * zeroes sizes[8 ..]); the hop adds its edges to it and to state[5]. */
+#define REGNN_CSC_PIECE 1024
+#define REGNN_CSC_LONG_CAP (32768 / 17 + 1)          /* hub rows of a <= 32768-edge block */
+#define REGNN_CSC_LONG_NPIECE (REGNN_CSC_LONG_CAP + 1)
+#define REGNN_CSC_LONG_TAB (((REGNN_CSC_LONG_NPIECE + 1) + 3) / 4 * 4)
+#define REGNN_CSC_LONG_MAXPIECE (32768 / REGNN_CSC_PIECE + REGNN_CSC_LONG_CAP)
+#define REGNN_CSC_LONG_INTS (REGNN_CSC_LONG_TAB + 4 * REGNN_CSC_LONG_MAXPIECE)
 int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                  int64_t* state, int32_t* sizes, int32_t* n_id, int32_t cap_dst,
@@ -759,6 +768,13 @@ typedef struct regnn_nsm_work {
                                  layer 1's transposed pass (agg0, head, gather); 2 = the rest
                                  (bwd0, rel0, finalize). A caller orders other work between the
                                  two parts (NSTrainer joins the sampler stream there). */
+    /* two-layer step: layer 1's transposed pass gives each piece of a hub row (> 16 entries,
+     * the csc_long0 piece table) a workgroup of its own; the pieces' exact 2^-40 fixed-point
+     * sums meet in hub_acc, the last piece of a row (hub_ticket) finishes it. hub_ticket and
+     * hub_terms zero-filled once by the caller, left zero by every step. */
+    unsigned long long* hub_acc;   /* REGNN_CSC_LONG_MAXPIECE * 64 */
+    int32_t* hub_ticket;           /* REGNN_CSC_LONG_CAP */
+    unsigned long long* hub_terms; /* 3 * 64 */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

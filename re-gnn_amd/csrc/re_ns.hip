@@ -548,6 +548,11 @@ ns_resolve_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ 
 constexpr int kCscThreads = 1024;
 constexpr int kCscMax = 32768;
 constexpr int kCscShort = 16;
+// the hub rows' work table after the ids (include/regnn_hip.h REGNN_CSC_LONG_*): every hub row
+// cut into pieces of <= kCscPiece entries, one int4 (source row, first entry, entries, li << 16 |
+// piece index << 8 | pieces of the row) per piece, pieces of a row consecutive
+constexpr int kCscPiece = REGNN_CSC_PIECE;
+constexpr int kCscLongCap = REGNN_CSC_LONG_CAP;
 
 __global__ void __launch_bounds__(kCscThreads)
 ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restrict__ blk_idx,
@@ -558,34 +563,47 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
     __shared__ int lds[kCscThreads / 64 + 1];
     const int n = sizes[hop + 1], E = cap_strided ? cap_strided : sizes[8 + hop];
     constexpr int IT = 8;
-    int carry = 0, lcarry = 0;
+    int carry = 0, lcarry = 0, pcarry = 0;
+    int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
     for (int base = 0; base < n; base += kCscThreads * IT) {
         const int i0 = base + threadIdx.x * IT;
-        int v[IT], s = 0, nl = 0;
+        int v[IT], s = 0, nl = 0, np = 0;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             v[j] = i0 + j < n ? csc_cnt[i0 + j] : 0;
             s += v[j];
             nl += v[j] > kCscShort ? 1 : 0;
+            np += v[j] > kCscShort ? (v[j] + kCscPiece - 1) / kCscPiece : 0;
         }
-        int total, ltotal;
+        int total, ltotal, ptotal;
         int off = carry + block_exscan<kCscThreads>(s, lds, &total);
         int loff = lcarry + block_exscan<kCscThreads>(nl, lds, &ltotal);
+        int poff = pcarry + block_exscan<kCscThreads>(np, lds, &ptotal);
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             if (i0 + j < n) {
                 csc_ptr[i0 + j] = off;
                 cur[i0 + j] = off;
-                if (v[j] > kCscShort) csc_long[1 + loff++] = i0 + j;
+                if (v[j] > kCscShort) {
+                    const int li = loff++;
+                    csc_long[1 + li] = i0 + j;
+                    const int npc = (v[j] + kCscPiece - 1) / kCscPiece;
+                    for (int k = 0; k < npc; ++k, ++poff)
+                        pieces[poff] = make_int4(i0 + j, off + k * kCscPiece,
+                                                 min(kCscPiece, v[j] - k * kCscPiece),
+                                                 (li << 16) | (k << 8) | npc);
+                }
             }
             off += v[j];
         }
         carry += total;
         lcarry += ltotal;
+        pcarry += ptotal;
     }
     if (threadIdx.x == 0) {
         csc_ptr[n] = carry;
         csc_long[0] = lcarry;
+        csc_long[REGNN_CSC_LONG_NPIECE] = pcarry;
     }
     __syncthreads();
     for (int bp = threadIdx.x; bp < E; bp += kCscThreads) {

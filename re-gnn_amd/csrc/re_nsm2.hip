@@ -74,8 +74,23 @@ __device__ unsigned long long g_nsm2_phase[4][32][16];
         if (threadIdx.x == 0 && blockIdx.x < 32 && blockIdx.y == 0)                             \
             g_nsm2_phase[kern][blockIdx.x][k] = wall_clock64();                                \
     } while (0)
+// entry / exit of every block (kern 0 agg0, 1 head, 2 gather, 3 bwd0, 4 finalize)
+__device__ unsigned long long g_nsm2_edge[5][2][4096];
+// the gather's hub pieces (j < 64): marks along the piece path
+__device__ unsigned long long g_nsm2_gp[64][8];
+#define PG(j, k)                                                                               \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && (j) < 64) g_nsm2_gp[j][k] = wall_clock64();                    \
+    } while (0)
+#define PE(kern, k)                                                                            \
+    do {                                                                                       \
+        const unsigned b_ = blockIdx.x + blockIdx.y * gridDim.x;                               \
+        if (threadIdx.x == 0 && b_ < 4096) g_nsm2_edge[kern][k][b_] = wall_clock64();          \
+    } while (0)
 #else
 #define PH(kern, k) do {} while (0)
+#define PE(kern, k) do {} while (0)
+#define PG(j, k) do {} while (0)
 #endif
 
 #define MFMA4(av, b0, b1, b2, b3, d)                                 \
@@ -97,6 +112,8 @@ struct Agg0Args {
     const int64_t* state; Drop drop;
     float* s_agg; float* s_w;
     float* a; float* stats; float* h; float* p;
+    // the labelled-target count nll_loss divides by (the last block; the head reads it)
+    const int32_t* n_id; const int64_t* labels; float* nvalid;
     // relation slots (RS): s_agg / s_w hold the unweighted sums / counts of the non-self edges
     // per source type, u_self the self loop's input row, u_rel [n][T + 1] each slot's relation
     int n_et; float* u_self; int32_t* u_rel;
@@ -114,6 +131,8 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
     constexpr int KB = K / 16;
     constexpr int HB = KB / 2;             // float4 steps per half type
     extern __shared__ float sm[];
+    PH(0, 12);
+    PE(0, 0);
     const int T = A.T;
     const int SR = T * K + 4;
     float* St = sm;                        // [16][SR]
@@ -136,6 +155,17 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) lbj[tt] = tt < T ? pick(A.lin_b.p, tt)[16 * w + c] : 0.f;
     PH(0, 0);
+    if (blockIdx.x == gridDim.x - 1) {         // block-uniform
+        __shared__ int cntw[kBlock / 64];
+        int cv = 0;
+        const int nb = A.sizes[0];
+        for (int i = threadIdx.x; i < nb; i += kBlock) cv += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cv += __shfl_xor(cv, o, 64);
+        if ((threadIdx.x & 63) == 0) cntw[threadIdx.x >> 6] = cv;
+        __syncthreads();
+        if (threadIdx.x == 0) *A.nvalid = float((cntw[0] + cntw[1]) + (cntw[2] + cntw[3]));
+    }
     __syncthreads();
     for (int base = blockIdx.x * 16; base < n; base += gridDim.x * 16) {
         // stage 1's first two W_t fragments are requested before the gather (their L2 latency
@@ -362,6 +392,270 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
         __syncthreads();                       // the tiles are reused by the next rows
         PH(0, 4);
     }
+    PE(0, 1);
+}
+
+// agg0 for 128-wide input rows: 16 rows x 32 lanes (one float4 of the row per lane), 512 threads,
+// <= 128 VGPRs and ~46 KB of LDS so two blocks share a CU and every tile of a batch (~350 of the
+// capacity's 832) is resident at once; stage 1's eight waves split the node types in two halves
+// whose partial products meet in LDS in a fixed order. Same outputs as agg0_kernel<128, ..>.
+constexpr int kAggW = 512;
+
+inline size_t agg0w_lds(int T) {          // St [16][T K + 4] | sw [16][MT] | Pt [16][68] |
+    return (size_t(16) * (T * 128 + 4) + 16 * MT + 16 * 68 + 16 * F + 16 * F) * sizeof(float);
+}                                         // at [16][64] | red [16][64]
+
+template <int NT, bool RS>
+__global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
+    constexpr int K = 128, HB = K / 32;    // float4 steps per half type (stage 1)
+    extern __shared__ float sm[];
+    PH(0, 12);
+    PE(0, 0);
+    const int T = A.T;
+    const int SR = T * K + 4;
+    float* St = sm;                        // [16][SR]
+    float* sw = St + 16 * SR;              // [16][MT]
+    float* Pt = sw + 16 * MT;              // [16][68]
+    float* at = Pt + 16 * 68;              // [16][F]
+    float* red = at + 16 * F;              // [16][F]: stage 1's second half
+    const int n = A.sizes[A.hop];
+    const int l = threadIdx.x & 31, sub = threadIdx.x >> 5, gl = threadIdx.x & 32;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int ct = w & 3, kh = w >> 2;     // stage 1: column tile, type half
+    if (blockIdx.x == gridDim.x - 1) {     // block-uniform: the labelled-target count
+        __shared__ int cntw[kAggW / 64];
+        int cv = 0;
+        const int nb = A.sizes[0];
+        for (int i = threadIdx.x; i < nb; i += kAggW) cv += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cv += __shfl_xor(cv, o, 64);
+        if (lane == 0) cntw[w] = cv;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int k = 0; k < kAggW / 64; ++k) t += cntw[k];
+            *A.nvalid = float(t);
+        }
+    }
+    const int base = blockIdx.x * 16;
+    if (base >= n) return;                 // block-uniform (the grid is capacity-sized)
+    // the relation table in registers of every lane (n_rel <= 64), read by shuffles
+    const float tabw = rel_tab(A.rw, A.n_rel, A.alpha, lane);
+    // ---- gather: per-type register sums of this lane's 4 features of row v
+    const int v = base + sub;
+    float wsum[NT];
+    float4 racc[NT];
+    int rel_t[NT];
+    float4 xself = make_float4(0.f, 0.f, 0.f, 0.f);
+    int r_self = -1;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        wsum[tt] = 0.f;
+        rel_t[tt] = -1;
+        racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    int e0 = 0, e1 = 0;
+    if (v < n) row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
+    for (int c0 = e0; c0 < e1; c0 += 32) {
+        const int m = min(32, e1 - c0);
+        int my_t = 0, my_lo = 0, my_r = 0;  // table rows < 2^31 (checked by the host)
+        if (l < m) {
+            my_t = A.edge_type[c0 + l];
+            my_lo = int(A.edge_off[c0 + l]);
+            my_r = A.rel[c0 + l];
+        }
+        constexpr int UN = 12;             // edges' rows in flight per lane
+        // (the weighted path's relation weight straight from relation_weight, branch-free: a
+        // shuffle from the table lanes could read lanes of a row already done)
+        float my_w = 0.f;
+        if constexpr (!RS) {
+            const float tr = A.rw[min(my_r, A.n_rel - 1)] * A.alpha;
+            my_w = my_r < A.n_rel ? (tr > 0.f ? tr : 0.01f * tr) : 0.f;
+        }
+        for (int j = 0; j < m; j += UN) {
+            int t[UN], ru[UN];
+            float4 x[UN];
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                const int jj = min(j + u, m - 1);
+                t[u] = __shfl(my_t, gl + jj, 64);
+                if constexpr (RS) ru[u] = __shfl(my_r, gl + jj, 64);
+                else ru[u] = __float_as_int(__shfl(my_w, gl + jj, 64));
+                const int64_t lo = __shfl(my_lo, gl + jj, 64);
+                x[u] = *reinterpret_cast<const float4*>(pick(A.xt.p, t[u]) + lo * K + 4 * l);
+                if (j + u >= m) t[u] = -1;     // padding: loaded (a valid row), not added
+            }
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                if (t[u] < 0) continue;
+                if constexpr (RS) {
+                    if (ru[u] >= A.n_et) {         // the self loop (one per row)
+                        r_self = ru[u];
+                        xself = x[u];
+                        continue;
+                    }
+                }
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    if (tt != t[u]) continue;
+                    if constexpr (RS) {
+                        wsum[tt] += 1.f;
+                        rel_t[tt] = ru[u];
+                        racc[tt].x += x[u].x; racc[tt].y += x[u].y;
+                        racc[tt].z += x[u].z; racc[tt].w += x[u].w;
+                    } else {
+                        const float wt = __int_as_float(ru[u]);
+                        wsum[tt] += wt;
+                        racc[tt].x = fmaf(wt, x[u].x, racc[tt].x);
+                        racc[tt].y = fmaf(wt, x[u].y, racc[tt].y);
+                        racc[tt].z = fmaf(wt, x[u].z, racc[tt].z);
+                        racc[tt].w = fmaf(wt, x[u].w, racc[tt].w);
+                    }
+                }
+            }
+        }
+    }
+    PH(0, 1);
+    const int tau = r_self - A.n_et;           // RS: the row's node type
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        if (tt < T) {
+            float wr = 1.f, ws = 0.f;              // RS: S = wr U + ws x_self
+            if constexpr (RS) {
+                const float tr = __shfl(tabw, max(rel_t[tt], 0), 64);
+                const float tsf = __shfl(tabw, max(r_self, 0), 64);
+                wr = rel_t[tt] >= 0 ? tr : 0.f;
+                ws = (tt == tau) ? tsf : 0.f;
+            }
+            float4 sv = racc[tt];
+            if constexpr (RS)
+                sv = make_float4(fmaf(ws, xself.x, wr * sv.x), fmaf(ws, xself.y, wr * sv.y),
+                                 fmaf(ws, xself.z, wr * sv.z), fmaf(ws, xself.w, wr * sv.w));
+            *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l) = sv;
+            if (v < n)
+                *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l) = racc[tt];
+            if (l == 0) {
+                sw[sub * MT + tt] = RS ? fmaf(wr, wsum[tt], ws) : wsum[tt];
+                if (v < n) {
+                    A.s_w[int64_t(v) * T + tt] = wsum[tt];
+                    if constexpr (RS) A.u_rel[int64_t(v) * (T + 1) + tt] = rel_t[tt];
+                }
+            }
+        }
+    }
+    if constexpr (RS) {
+        if (v < n) {
+            *reinterpret_cast<float4*>(A.u_self + int64_t(v) * K + 4 * l) = xself;
+            if (l == 0) A.u_rel[int64_t(v) * (T + 1) + T] = r_self;
+        }
+    }
+    // stage 2's operands (waves 0..3), requested before stage 1 (their latency under it)
+    float w0c[16], iv4[4];
+    float bj = 0.f;
+    if (w < 4) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w0c[4 * b + i] = A.w0[(16 * b + 4 * q + i) * F + 16 * w + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) iv4[r] = base + 4 * q + r < n ? A.inv[base + 4 * q + r] : 0.f;
+        bj = A.bias[16 * w + c];
+    }
+    __syncthreads();
+    PH(0, 2);
+    // ---- stage 1: wave (ct, kh) forms sum over its half's types of S_t W_t^T for columns
+    // 16 ct + c; W_t fragments from L2, two in flight
+    f32x4 d = {0.f, 0.f, 0.f, 0.f};
+    {
+        float4 bq[3][HB];
+        auto bload = [&](int step, float4 (&dst)[HB]) {     // step: (type tt = kh + 2 (step >> 1), half)
+            const int tt = kh + 2 * (step >> 1), h0 = (step & 1) * HB;
+            const float* wt = pick(A.lin_w.p, tt) + (16 * ct + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+            for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+        };
+        const int nst = 2 * ((T - kh + 1) / 2);             // steps of this half's types
+        if (nst > 0) bload(0, bq[0]);
+        if (nst > 1) bload(1, bq[1]);
+#pragma unroll
+        for (int step = 0; step < NT; ++step) {             // NT >= 2 * ceil(NT / 2) steps bound
+            if (step < nst) {
+                if (step + 2 < nst) bload(step + 2, bq[(step + 2) % 3]);
+                const int tt = kh + 2 * (step >> 1);
+                const float* sa = St + c * SR + tt * K + 16 * (step & 1) * HB + 4 * q;
+#pragma unroll
+                for (int b = 0; b < HB; ++b) {
+                    const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                    const float4 bv = bq[step % 3][b];
+                    MFMA4(av, bv.x, bv.y, bv.z, bv.w, d);
+                }
+            }
+        }
+    }
+    if (kh == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(4 * q + r) * F + 16 * ct + c] = d[r];
+    }
+    __syncthreads();
+    if (kh == 0) {                         // P = half 0 + half 1 + sum_t w_vt b_t
+        const int j = 16 * ct + c;
+        float lbj[NT];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) lbj[tt] = tt < T ? pick(A.lin_b.p, tt)[j] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int vr = 4 * q + r;
+            float bsum = 0.f;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt)
+                if (tt < T) bsum = fmaf(sw[vr * MT + tt], lbj[tt], bsum);
+            Pt[vr * 68 + j] = (d[r] + red[vr * F + j]) + bsum;
+        }
+    }
+    __syncthreads();
+    PH(0, 3);
+    // ---- stage 2: a = inv (P W_0) + bias
+    if (w < 4) {
+        f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float4 av = *reinterpret_cast<const float4*>(Pt + c * 68 + 16 * b + 4 * q);
+            MFMA4(av, w0c[4 * b], w0c[4 * b + 1], w0c[4 * b + 2], w0c[4 * b + 3], d2);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) at[(4 * q + r) * F + 16 * w + c] = fmaf(iv4[r], d2[r], bj);
+    }
+    __syncthreads();
+    // ---- epilogue (threads 0..255: 16 rows x 16 lanes): P and a kept, LayerNorm, relu,
+    // dropout -> h0
+    if (threadIdx.x < kBlock) {
+        const int l16 = threadIdx.x & 15, s16 = threadIdx.x >> 4;
+        const int vv = base + s16;
+        if (vv < n) {
+            const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l16];
+            const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l16];
+            *reinterpret_cast<float4*>(A.p + int64_t(vv) * F + 4 * l16) =
+                *reinterpret_cast<const float4*>(Pt + s16 * 68 + 4 * l16);
+            const float4 a4 = *reinterpret_cast<const float4*>(at + s16 * F + 4 * l16);
+            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+            *reinterpret_cast<float4*>(A.a + int64_t(vv) * F + 4 * l16) = a4;
+            const float mean = group_sum<16>(av[0] + av[1] + av[2] + av[3]) * (1.f / F);
+            const float dd[4] = {av[0] - mean, av[1] - mean, av[2] - mean, av[3] - mean};
+            const float var = group_sum<16>(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2] + dd[3] * dd[3]) * (1.f / F);
+            const float rstd = rsqrtf(var + kLnEps);
+            if (l16 == 0) reinterpret_cast<float2*>(A.stats)[vv] = make_float2(mean, rstd);
+            const float gws[4] = {gw.x, gw.y, gw.z, gw.w}, gbs[4] = {gb.x, gb.y, gb.z, gb.w};
+            const uint32_t key = A.drop.on ? layer_key(A.state, 0) : 0u;
+            float mk[4];
+            drop_factors(key, A.drop, vv, l16, mk);
+            float hv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) hv[cc] = fmaxf(fmaf(dd[cc] * rstd, gws[cc], gbs[cc]), 0.f) * mk[cc];
+            *reinterpret_cast<float4*>(A.h + int64_t(vv) * F + 4 * l16) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        }
+    }
+    PH(0, 4);
+    PE(0, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -408,7 +702,7 @@ __device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c &
 // gh, the out_lin partial) on all 8 waves
 constexpr int kHeadThreads = 512;
 
-__global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
+__global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     extern __shared__ float hl[];
     const int C = A.C, CT = (C + 15) / 16, CP = head_cp(C);
     float* Wl = hl;                        // W_out image; after step 4: red [3][16][64]
@@ -419,32 +713,71 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
     float* hg = ghs + 16 * 68;             // [16][68]: Hagg
     float* ghp = hg + 16 * 68;             // [16][68]: gh over the second half of the classes
     float* red = Wl;
-    __shared__ float tab[F];
     __shared__ float lrow[kRows];
-    __shared__ int wcnt[kHeadThreads / 64];
     __shared__ float bo_s[16 * kMaxCT];    // out_lin.bias (classes >= C: 0)
     const bool rowt = threadIdx.x < kBlock;    // the row phases' threads
     const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 15, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
     const int wq = w & 3, wh = w >> 2;        // feature tile, class half (step 4c)
+    PH(1, 12);
+    PE(1, 0);
     const int n = A.sizes[0];
     const int v = blockIdx.x * kRows + sub;
     const bool act = rowt && v < n;
-    const int64_t y = act ? A.labels[A.n_id[v]] : -1;     // in flight during the staging
-    // step 2's bias / row scales and step 4a's out_lin.bias, requested with the staging (their
-    // latency off the MFMA phases)
-    const float bj2 = A.bias[16 * wq + cc];
-    float iv2[4];
+    // Order of the global requests: the aggregation's chain first (nothing waits behind the
+    // staging), then step 2 / 3's operands, then out_lin's LDS-DMA; the barriers up to step 4a
+    // order LDS only (lds_sync), so the DMA lands under steps 1-3.
+    const int r32 = threadIdx.x >> 5, l32 = threadIdx.x & 31;   // step 4b: 32 lanes per row
+    const int v32 = blockIdx.x * kRows + r32;
+    const int nid32 = v32 < n ? A.n_id[v32] : -1;
+    PH(1, 0);
+    PH(1, 1);
+    // ---- 1. Hagg on waves 0..3 (16 lanes per row, up to 32 entries' rows in flight: one round
+    // of loads for the sampled rows <= 32), while waves 4..7 stage out_lin.weight into its LDS
+    // image (their loads overlap the aggregation's)
+    if (rowt) {
+        const int vr = blockIdx.x * kRows + sub;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (vr < n) {
+            int e0, e1;
+            row_range(A.ptr, A.cnt, A.stride, vr, e0, e1);
+            for (int c0 = e0; c0 < e1; c0 += 32) {
+                const int m = min(32, e1 - c0);
+                const int my_u0 = l < m ? A.idx[c0 + l] : 0;
+                const int my_r0 = l < m ? int(A.rel[c0 + l]) : 0;
+                const int my_u1 = l + 16 < m ? A.idx[c0 + 16 + l] : 0;
+                const int my_r1 = l + 16 < m ? int(A.rel[c0 + 16 + l]) : 0;
+                constexpr int UN = 32;
+                float4 x[UN];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int vv = blockIdx.x * kRows + 4 * q + r;
-        iv2[r] = vv < n ? A.inv[vv] : 0.f;
-    }
-    for (int c = threadIdx.x; c < 16 * kMaxCT; c += kHeadThreads) bo_s[c] = c < A.C ? A.b_out[c] : 0.f;
-    {   // out_lin.weight -> LDS by LDS-DMA; lane L writes slot L%16 of row c, which holds
+                for (int u = 0; u < UN; ++u) {
+                    const int jj = min(u, m - 1);
+                    const int uu = __shfl(jj < 16 ? my_u0 : my_u1, gl + (jj & 15), 64);
+                    x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu) * F + 4 * l);
+                }
+                // each lane's own entries' relation weights (unconditional loads after the
+                // rows are requested), broadcast by shuffles
+                const float tr0 = A.rw[min(my_r0, A.n_rel - 1)] * A.alpha;
+                const float tr1 = A.rw[min(my_r1, A.n_rel - 1)] * A.alpha;
+                const float w0 = my_r0 < A.n_rel ? (tr0 > 0.f ? tr0 : 0.01f * tr0) : 0.f;
+                const float w1 = my_r1 < A.n_rel ? (tr1 > 0.f ? tr1 : 0.01f * tr1) : 0.f;
+#pragma unroll
+                for (int u = 0; u < UN; ++u) {     // predicated, not a break: a loop with a break
+                    if (u < m) {                   // is left rolled and x[] goes to scratch
+                        const float wt = __shfl(u < 16 ? w0 : w1, gl + (u & 15), 64);
+                        s0 = fmaf(wt, x[u].x, s0); s1 = fmaf(wt, x[u].y, s1);
+                        s2 = fmaf(wt, x[u].z, s2); s3 = fmaf(wt, x[u].w, s3);
+                    }
+                }
+            }
+        }
+        *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
+    } else {
+        // out_lin.weight -> LDS: image row i (4 classes) slot L%16 of class c = 4 i + L / 16 holds
         // W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw); pad rows c >= C read row C-1
+        // by LDS-DMA: vmcnt is per wave, so only these four waves wait for it (at the barrier)
         const int L64 = threadIdx.x & 63;
-        for (int i = threadIdx.x >> 6; i < CT * 4; i += kHeadThreads / 64) {
+        for (int i = w - 4; i < CT * 4; i += 4) {
             const int c = 4 * i + (L64 >> 4);
             const int cs = c < C ? c : C - 1;
             const float* src = A.w_out + int64_t(cs) * F + 4 * ((L64 & 15) ^ (c & 15));
@@ -453,54 +786,26 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
                 (__attribute__((address_space(3))) void*)(Wl + 4 * i * F), 16, 0, 0);
         }
     }
+    // steps 2 - 4's operands: the labels and the labelled-target count (agg0 counted it), W_1
+    // fragments, biases, row scales, LayerNorm weights, out_lin.bias
+    const int64_t y = nid32 >= 0 ? A.labels[nid32] : -1;
+    const float nvalid = *A.nvalid;
+    const float bj2 = A.bias[16 * wq + cc];
+    float iv2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int vv = blockIdx.x * kRows + 4 * q + r;
+        iv2[r] = vv < n ? A.inv[vv] : 0.f;
+    }
     float w1c[16];                         // W_1[16 b + 4 q + i][16 w + cc]: step 2's B operand
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) w1c[4 * b + i] = A.w1[(16 * b + 4 * q + i) * F + 16 * wq + cc];
-    {   // the labelled-target count nll_loss divides by, while the DMA lands
-        int cnt_valid = 0;
-        for (int i = threadIdx.x; i < n; i += kHeadThreads) cnt_valid += A.labels[A.n_id[i]] >= 0 ? 1 : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) cnt_valid += __shfl_xor(cnt_valid, o, 64);
-        if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = cnt_valid;
-    }
-    if (threadIdx.x < F) tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
-    PH(1, 0);
-    __syncthreads();
-    PH(1, 1);
-    // ---- 1. Hagg
-    {
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        if (act) {
-            int e0, e1;
-            row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
-            for (int c0 = e0; c0 < e1; c0 += 16) {
-                const int m = min(16, e1 - c0);
-                const int my_u = l < m ? A.idx[c0 + l] : 0;
-                const int my_r = l < m ? int(A.rel[c0 + l]) : 0;
-                constexpr int UN = 8;
-                for (int j = 0; j < m; j += UN) {
-                    float4 x[UN];
-                    float wt[UN];
-#pragma unroll
-                    for (int u = 0; u < UN; ++u) {
-                        const int jj = min(j + u, m - 1);
-                        const int uu = __shfl(my_u, gl + jj, 64);
-                        wt[u] = j + u < m ? tab[__shfl(my_r, gl + jj, 64)] : 0.f;
-                        x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu) * F + 4 * l);
-                    }
-#pragma unroll
-                    for (int u = 0; u < UN; ++u) {
-                        if (j + u >= m) break;
-                        s0 = fmaf(wt[u], x[u].x, s0); s1 = fmaf(wt[u], x[u].y, s1);
-                        s2 = fmaf(wt[u], x[u].z, s2); s3 = fmaf(wt[u], x[u].w, s3);
-                    }
-                }
-            }
-        }
-        if (rowt) *reinterpret_cast<float4*>(hg + sub * 68 + 4 * l) = make_float4(s0, s1, s2, s3);
-    }
+    const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
+    const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
+    const float ivv = act ? A.inv[v] : 0.f;
+    for (int c = threadIdx.x; c < 16 * kMaxCT; c += kHeadThreads) bo_s[c] = c < A.C ? A.b_out[c] : 0.f;
     __syncthreads();
     PH(1, 2);
     // ---- 2. a = inv (Hagg W_1) + bias -> ghs
@@ -515,14 +820,11 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ghs[(4 * q + r) * 68 + j] = fmaf(iv2[r], d[r], bj2);
     }
-    __syncthreads();
+    lds_sync();
     // ---- 3. LayerNorm, relu, dropout
-    const float4 gw4 = reinterpret_cast<const float4*>(A.ln_w)[l];
-    const float4 gb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
     const float gwf[4] = {gw4.x, gw4.y, gw4.z, gw4.w}, gbf[4] = {gb4.x, gb4.y, gb4.z, gb4.w};
     float xhat[4] = {0.f, 0.f, 0.f, 0.f}, mfac[4] = {0.f, 0.f, 0.f, 0.f}, rstd = 0.f;
     float hv[4] = {0.f, 0.f, 0.f, 0.f};
-    const float ivv = act ? A.inv[v] : 0.f;
     if (act) {
         const float4 a4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
         const float a[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -544,9 +846,6 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
     }
     __syncthreads();
     PH(1, 3);
-    const int n_valid = ((wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3])) +
-                        ((wcnt[4] + wcnt[5]) + (wcnt[6] + wcnt[7]));
-    if (blockIdx.x == 0 && threadIdx.x == 0) *A.nvalid = float(n_valid);
     // ---- 4a. z = h W^T + b -> zs (classes >= C: -inf)
     for (int ct = w; ct < CT; ct += kHeadThreads / 64) {
         const int c = 16 * ct + cc;
@@ -562,36 +861,42 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
         for (int r = 0; r < 4; ++r) zs[(4 * q + r) * CP + c] = c < C ? dz[r] + bo : -INFINITY;
     }
     __syncthreads();
-    // ---- 4b. log_softmax, nll, g
-    if (rowt) {                            // lane l holds classes l + 16 i of row sub
-        float zr[kMaxCT];
+    PH(1, 8);
+    // ---- 4b. log_softmax, nll, g: lane l32 of row r32 holds classes l32 + 32 i (all 8 waves)
+    {
+        constexpr int NI = (16 * kMaxCT + 31) / 32;
+        const int CW = 16 * CT;                // classes >= C hold -inf
+        float zr[NI];
         float zmax = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < kMaxCT; ++i) {
-            zr[i] = i < CT ? zs[sub * CP + l + 16 * i] : -INFINITY;
+        for (int i = 0; i < NI; ++i) {
+            const int c = l32 + 32 * i;
+            zr[i] = c < CW ? zs[r32 * CP + c] : -INFINITY;
             zmax = fmaxf(zmax, zr[i]);
         }
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
+        for (int o = 16; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
         float se = 0.f;
 #pragma unroll
-        for (int i = 0; i < kMaxCT; ++i) {
+        for (int i = 0; i < NI; ++i) {
             zr[i] = expf(zr[i] - zmax);        // classes >= C: exp(-inf) = 0
             se += zr[i];
         }
-        se = group_sum<16>(se);
+        se = group_sum<32>(se);
         const float lse = zmax + logf(se), rse = 1.f / se;
-        const float zy = y >= 0 ? zs[sub * CP + y] : 0.f;
-        if (l == 0) lrow[sub] = y >= 0 ? lse - zy : 0.f;
-        const float inv_n = y >= 0 && n_valid > 0 ? 1.f / float(n_valid) : 0.f;
+        const bool ok = v32 < n;
+        const float zy = y >= 0 ? zs[r32 * CP + y] : 0.f;
+        if (l32 == 0) lrow[r32] = y >= 0 ? lse - zy : 0.f;
+        const float inv_n = y >= 0 && nvalid > 0.f ? 1.f / nvalid : 0.f;
 #pragma unroll
-        for (int i = 0; i < kMaxCT; ++i) {
-            const int c = l + 16 * i;
-            if (i < CT)
-                zs[sub * CP + c] = act && c < C ? (zr[i] * rse - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
+        for (int i = 0; i < NI; ++i) {
+            const int c = l32 + 32 * i;
+            if (c < CW)
+                zs[r32 * CP + c] = ok && c < C ? (zr[i] * rse - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
         }
     }
     __syncthreads();
+    PH(1, 9);
     // ---- 4c. gh = g W: wave w -> features 16 wq + cc, rows 4 q + r, class tiles of half wh
     {
         const int k = 16 * wq + cc;
@@ -648,6 +953,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
             make_float4(gy[0] * xhat[0], gy[1] * xhat[1], gy[2] * xhat[2], gy[3] * xhat[3]);
     }
     __syncthreads();
+    PH(1, 10);
     float* o = A.part + int64_t(blockIdx.x) * A.part_w;
     const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
     const int64_t o_w1 = head_o_w1(C);
@@ -722,6 +1028,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs A) {
             for (int i = 0; i < 4; ++i) o[o_w1 + (16 * w + 4 * q + i) * F + 16 * jb + cc] = dw[jb][i];
     }
     PH(1, 7);
+    PE(1, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -745,6 +1052,11 @@ struct GathArgs {
     const float* ln_w; const float* ln_b; const int64_t* state; Drop drop;
     const float* rw; int n_rel; float alpha;
     float* g0; float* slab;
+    // hub rows (> kShort entries): their 16-entry chunks spread over every group of the grid;
+    // exact sums in hub_acc [kLongCap][64], the last chunk's group (hub_ticket) runs the row's
+    // backward and adds its row terms to hub_terms [3][64] (all exact 2^-40 integers; hub_acc /
+    // hub_ticket zeroed by that group, hub_terms by finalize)
+    unsigned long long* hub_acc; int32_t* hub_ticket; unsigned long long* hub_terms;
 };
 
 static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 512);
@@ -775,12 +1087,12 @@ __device__ __forceinline__ RowIn row_in(const GathArgs& A, uint32_t key, int u, 
 
 // `m` entries of a segment starting at c (m <= 16, uniform over the group): fixed-point sums of
 // tab[r] GH[v] into acc and the relation dots into the block's bins
+template <int UN>
 __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab,
                                              unsigned long long* bins, int c, int m, int l,
                                              int gl, const RowIn& R,
                                              unsigned long long (&acc)[4]) {
     const int my = l < m ? A.cent[c + l] : 0;
-    constexpr int UN = 8;
     for (int j = 0; j < m; j += UN) {
         int pk[UN];
         float4 g[UN];
@@ -791,7 +1103,8 @@ __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab
         }
 #pragma unroll
         for (int u = 0; u < UN; ++u) {
-            if (j + u >= m) break;             // uniform over the group
+            if (j + u >= m) continue;          // uniform over the group (continue: the loop
+                                               // unrolls, a break leaves g[] in scratch)
             const float t = tab[pk[u] & 255];
             acc[0] += to_fix(t * g[u].x);
             acc[1] += to_fix(t * g[u].y);
@@ -831,13 +1144,44 @@ __device__ __forceinline__ void row_bwd(const GathArgs& A, int u, int l, const R
         make_float4(R.iv * ga[0], R.iv * ga[1], R.iv * ga[2], R.iv * ga[3]);
 }
 
+// the row's backward for a hub row from its exact totals; its row terms go to hub_terms exactly
+// (which workgroup runs it depends on the atomics' order: integer sums keep the result
+// independent of it)
+__device__ __forceinline__ void hub_row_bwd(const GathArgs& A, int u, int l, const RowIn& R,
+                                            const float (&lw)[4],
+                                            const unsigned long long (&tot)[4]) {
+    float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
+    row_bwd(A, u, l, R, lw, tot, sga, sgy, sgyx);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        atomicAdd(A.hub_terms + 0 * F + 4 * l + i, to_fix(sga[i]));
+        atomicAdd(A.hub_terms + 1 * F + 4 * l + i, to_fix(sgy[i]));
+        atomicAdd(A.hub_terms + 2 * F + 4 * l + i, to_fix(sgyx[i]));
+    }
+}
+
+// Hub rows: the sampler's piece table (REGNN_CSC_LONG_TAB) cuts each into pieces of <= 1024
+// entries; piece j runs on workgroup grid - 1 - j (the blocks past the short rows' range), its
+// 16 groups taking 16 entries at a time with every row in flight, the partial sums added exactly
+// in LDS. A row of one piece finishes there; a longer row's pieces store their sums to
+// hub_acc[j] and the piece that completes the row's ticket sums them (exact) and runs the row's
+// backward (device-scope fences: only for rows past 1024 entries).
 __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     __shared__ unsigned long long bins[F];
     __shared__ unsigned long long lgh[F];
     __shared__ float tab[F];
     __shared__ float rt[3][16][F];
+    __shared__ int s_last;
+    PH(2, 8);
+    PE(2, 0);
+    const int j = int(gridDim.x) - 1 - int(blockIdx.x);    // this block's hub piece, if any
+    const int n_piece = A.clong[REGNN_CSC_LONG_NPIECE];
+    const int4 pc = j < REGNN_CSC_LONG_MAXPIECE
+                        ? reinterpret_cast<const int4*>(A.clong + REGNN_CSC_LONG_TAB)[j]
+                        : make_int4(0, 0, 0, 0);
     if (threadIdx.x < F) {
         bins[threadIdx.x] = 0ull;
+        lgh[threadIdx.x] = 0ull;
         tab[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
     }
     __syncthreads();
@@ -848,35 +1192,61 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
     const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
     float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
-    // ---- rows with <= kShort edges: one group each
-    for (int u = blockIdx.x * 16 + grp; u < n; u += gridDim.x * 16) {
-        const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
-        if (m > kShort) continue;              // a hub: the workgroup pass below
+    if (j < n_piece) {                         // block-uniform
+        const int u = pc.x, e0 = pc.y, cnt = pc.z;
+        const int li = pc.w >> 16, k = (pc.w >> 8) & 255, npc = pc.w & 255;
+        PG(j, 0);
         const RowIn R = row_in(A, key, u, l, lw, lb);
         unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        gather_chunk(A, tab, bins, c0, m, l, gl, R, acc);
-        row_bwd(A, u, l, R, lw, acc, sga, sgy, sgyx);
-    }
-    // ---- hub rows: a workgroup each, 16-entry chunks over the groups
-    const int n_long = A.clong[0];
-    for (int li = blockIdx.x; li < n_long; li += gridDim.x) {
-        const int u = A.clong[1 + li];
-        const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
-        const RowIn R = row_in(A, key, u, l, lw, lb);
-        if (threadIdx.x < F) lgh[threadIdx.x] = 0ull;
-        __syncthreads();
-        unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        for (int k = grp; 16 * k < m; k += 16)
-            gather_chunk(A, tab, bins, c0 + 16 * k, min(16, m - 16 * k), l, gl, R, acc);
+        for (int e = kShort * grp; e < cnt; e += kShort * 16)      // <= 1024 entries: 4 rounds
+            gather_chunk<kShort>(A, tab, bins, e0 + e, min(kShort, cnt - e), l, gl, R, acc);
+        PG(j, 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(lgh + 4 * l + i, acc[i]);   // LDS, exact
         __syncthreads();
-        if (grp == 0) {
-            const unsigned long long tot[4] = {lgh[4 * l], lgh[4 * l + 1], lgh[4 * l + 2],
-                                               lgh[4 * l + 3]};
-            row_bwd(A, u, l, R, lw, tot, sga, sgy, sgyx);
+        PG(j, 2);
+        if (npc == 1) {                        // the whole row in this block (a fixed one):
+            if (grp == 0) {                    // its row terms join the block's own sums
+                const unsigned long long tot[4] = {lgh[4 * l], lgh[4 * l + 1], lgh[4 * l + 2],
+                                                   lgh[4 * l + 3]};
+                row_bwd(A, u, l, R, lw, tot, sga, sgy, sgyx);
+            }
+            PG(j, 3);
+        } else {
+            unsigned long long* ha = A.hub_acc + int64_t(j) * F;
+            if (threadIdx.x < F)
+                __hip_atomic_store(ha + threadIdx.x, lgh[threadIdx.x], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();
+            __syncthreads();
+            if (threadIdx.x == 0) s_last = atomicAdd(A.hub_ticket + li, 1) == npc - 1;
+            __syncthreads();
+            if (s_last) {                      // every piece of row u is in hub_acc
+                __threadfence();
+                if (grp == 0) {
+                    const unsigned long long* h0 = A.hub_acc + int64_t(j - k) * F + 4 * l;
+                    unsigned long long tot[4] = {0ull, 0ull, 0ull, 0ull};
+                    for (int q = 0; q < npc; ++q)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            tot[i] += __hip_atomic_load(h0 + int64_t(q) * F + i, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+                    if (l == 0)
+                        __hip_atomic_store(A.hub_ticket + li, 0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    hub_row_bwd(A, u, l, R, lw, tot);
+                }
+            }
         }
-        __syncthreads();
+    }
+    // ---- rows with <= kShort edges: one group each
+    for (int u = blockIdx.x * 16 + grp; u < n; u += gridDim.x * 16) {
+        const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
+        if (m > kShort) continue;              // a hub: its pieces above
+        const RowIn R = row_in(A, key, u, l, lw, lb);
+        unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
+        gather_chunk<8>(A, tab, bins, c0, m, l, gl, R, acc);
+        row_bwd(A, u, l, R, lw, acc, sga, sgy, sgyx);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -894,6 +1264,8 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
         for (int g = 0; g < 16; ++g) sum += rt[which][g][f];
         o[F + threadIdx.x] = sum;
     }
+    PH(2, 9);
+    PE(2, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -933,6 +1305,8 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     constexpr int KB = K / 64;                // k blocks per wave
     constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile of a K-wide row
     extern __shared__ float sm[];
+    PH(2, 12);
+    PE(3, 0);
     float* Wk = sm;                           // [K][WS]: W_t k-major; at the end the row terms
     // the fused Adam's step count advances here, the launch before finalize, which reads it:
     // no completion ticket among finalize's blocks (their contended atomic was its tail)
@@ -1181,13 +1555,14 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) o0[(16 * w + 4 * q + i) * F + 16 * jb + c] = acc0[jb][i];
     }
+    PE(3, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
 // finalize: every gradient a fixed-order sum of per-block partials (re_nsm.hip's job table);
 // with the optimizer attached, element e of a job's destination (a view into the flat gradient
 // bucket) is followed by Adam on parameter (dst + e - grad_base) of the flat buffers.
-enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2 };
+enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2, kOpFix = 3 };
 
 struct Job {
     const float* src;
@@ -1196,6 +1571,7 @@ struct Job {
     int cb;                  // columns (elements, or float4 columns if vec) per block: 32, 16, 8
     float* dst;
     const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
+    unsigned long long* fix; // kOpFix: 2^-40 fixed-point terms added to the sum, then zeroed
 };
 
 struct AdamArgs {
@@ -1352,6 +1728,9 @@ __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, 
         } else if (J.op == kOpLoss) {
             const float nv = *J.aux;
             out = nv > 0.f ? tot / nv : 0.f;
+        } else if (J.op == kOpFix) {           // the gather's hub rows (exact), then reset
+            out = tot + float((long long)J.fix[e]) * kFixInv;
+            J.fix[e] = 0ull;
         }
         J.dst[e] = out;
         // torch.optim.Adam (regnn_adam_flat's arithmetic); a gradient outside the bucket (a
@@ -1370,6 +1749,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     const Job J = A.job[ji];
     const AdamArgs& O = A.adam;
     PH(3, 0);
+    PE(4, 0);
     const int el = threadIdx.x % J.cb, grp = threadIdx.x / J.cb;
     if (J.vec) {                               // block-uniform
         finalize_vec(A, J, O, b, el, grp, s_t, s_step, s_bc2);
@@ -1377,17 +1757,18 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
         finalize_scalar(A, J, O, b, el, grp, s_t, s_step, s_bc2);
     }
     PH(3, 2);
+    PE(4, 1);
 }
 
 struct JobList {
     FinArgs A{};
     int blocks = 0;
     void add(const float* src, int64_t pstride, int nparts, int width, float* dst, int op = kOpCopy,
-             const float* aux = nullptr) {
+             const float* aux = nullptr, unsigned long long* fix = nullptr) {
         A.start[A.n_jobs] = blocks;
         Job& j = A.job[A.n_jobs++];
         j.src = src; j.pstride = pstride; j.nparts = nparts; j.width = width; j.dst = dst;
-        j.op = op; j.aux = aux; j.adam = op != kOpLoss;
+        j.op = op; j.aux = aux; j.fix = fix; j.adam = op != kOpLoss;
         j.vec = op == kOpCopy && width % 4 == 0 && pstride % 4 == 0 &&
                 reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
                 reinterpret_cast<uintptr_t>(dst) % 16 == 0;
@@ -1431,6 +1812,16 @@ using namespace regnn::nsm2;
 extern "C" int regnn_nsm2_phases(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsm2_phase), sizeof(g_nsm2_phase)) == hipSuccess ? 0 : 3;
 }
+extern "C" int regnn_nsm2_edges(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsm2_edge), sizeof(g_nsm2_edge)) == hipSuccess ? 0 : 3;
+}
+extern "C" int regnn_nsm2_gpieces(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsm2_gp), sizeof(g_nsm2_gp)) == hipSuccess ? 0 : 3;
+}
+extern "C" int regnn_nsm2_edges_reset(void) {
+    static unsigned long long zero[5][2][4096];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_nsm2_edge), zero, sizeof(zero)) == hipSuccess ? 0 : 3;
+}
 #endif
 
 // entry points used by re_nsm.hip's regnn_nsm_step / regnn_nsm_slab_floats for L = 2
@@ -1449,7 +1840,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     const int T = p->n_types, K = p->k_in, C = p->n_classes;
     const bool rs = p->rel_slots != 0;
     if (!w->p0 || !w->gh1 || !w->csc_ptr0 || !w->csc_ent0 || !w->csc_long0 || !w->xs[1] || !w->a[0] ||
-        !w->stats[0] || !w->ga[0])
+        !w->stats[0] || !w->ga[0] || !w->hub_acc || !w->hub_ticket || !w->hub_terms)
         return REGNN_EINVAL;
     for (int h = 0; h < 2; ++h)
         if (w->stride[h] < 0 || (w->stride[h] && !w->blk_cnt[h])) return REGNN_EINVAL;
@@ -1480,7 +1871,22 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         A.s_agg = w->s_agg; A.s_w = w->s_w;
         A.a = w->a[0]; A.stats = w->stats[0]; A.h = w->xs[1]; A.p = w->p0;
         A.n_et = p->n_edge_types; A.u_self = w->u_self; A.u_rel = w->u_rel;
+        A.n_id = w->n_id; A.labels = w->labels; A.nvalid = w->nvalid;
         int grid = (w->cap[h] + 15) / 16;
+        if (K == 128 && T <= 4 && !getenv("REGNN_NSM_AGG0_OLD")) {  // every tile its own block
+            const size_t lds = agg0w_lds(T);
+#define AGG0W_CASE(NN, RS)                                                                     \
+            if (rs == RS) {                                                                    \
+                static size_t done = 0;                                                        \
+                if (!set_lds(reinterpret_cast<const void*>(&agg0w_kernel<NN, RS>), lds, &done)) \
+                    return REGNN_EUNSUPPORTED;                                                 \
+                hipLaunchKernelGGL((agg0w_kernel<NN, RS>), dim3(grid), dim3(kAggW), lds, stream, A); \
+                REGNN_LAUNCH_CHECK();                                                          \
+            } else
+            AGG0W_CASE(4, true) AGG0W_CASE(4, false)
+                return REGNN_EUNSUPPORTED;
+#undef AGG0W_CASE
+        } else {
         if (grid > 2048) grid = 2048;
         const size_t lds = agg0_lds(T, K);
 #define AGG0_CASE(KK, NN, RS)                                                                  \
@@ -1496,6 +1902,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         AGG0_CASE(64, 4, false) AGG0_CASE(64, MT, false)
             return REGNN_EUNSUPPORTED;
 #undef AGG0_CASE
+        }
     }
     // 2. layer 1 + head + loss + backward to GH, transposed aggregation into layer 0's rows
     const int64_t hw = head_part_width(C);
@@ -1525,6 +1932,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         G.ln_w = p->ln_w[0]; G.ln_b = p->ln_b[0]; G.state = w->state; G.drop = drop;
         G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1]; G.alpha = p->alpha;
         G.g0 = w->ga[0]; G.slab = w->slab + S.gath;
+        G.hub_acc = w->hub_acc; G.hub_ticket = w->hub_ticket; G.hub_terms = w->hub_terms;
         hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kBlock), 0, stream, G);
         REGNN_LAUNCH_CHECK();
     }
@@ -1582,9 +1990,10 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
             J.add(src + int64_t(K) * F, pw, kBwdBlocks, F, p->g_lin_b[t]);
         }
         J.add(w->slab + S.post0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
-        J.add(gs + F, kGathW, kGathBlocks, F, p->g_conv_b[0]);
-        J.add(gs + 2 * F, kGathW, kGathBlocks, F, p->g_ln_b[0]);
-        J.add(gs + 3 * F, kGathW, kGathBlocks, F, p->g_ln_w[0]);
+        J.add(gs + F, kGathW, kGathBlocks, F, p->g_conv_b[0], kOpFix, nullptr, w->hub_terms);
+        J.add(gs + 2 * F, kGathW, kGathBlocks, F, p->g_ln_b[0], kOpFix, nullptr, w->hub_terms + F);
+        J.add(gs + 3 * F, kGathW, kGathBlocks, F, p->g_ln_w[0], kOpFix, nullptr,
+              w->hub_terms + 2 * F);
         if (ad) {
             AdamArgs& O = J.A.adam;
             O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;

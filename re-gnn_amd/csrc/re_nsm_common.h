@@ -4,6 +4,8 @@
 #pragma once
 #include "regnn_common.h"
 
+#include <type_traits>
+
 namespace regnn {
 namespace nsm {
 
@@ -70,6 +72,24 @@ __device__ __forceinline__ void drop_factors(uint32_t key, const Drop& d, int64_
 }
 
 __device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+
+// f(std::integral_constant<int, I>) for I = B .. E - 1: register arrays indexed by it keep
+// constant indices (a #pragma unroll loop unrolled after SROA leaves its array in scratch)
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// a workgroup barrier ordering LDS only: this wave's LDS traffic completes (lgkmcnt), global
+// loads stay in flight across it (a __syncthreads() waits for every outstanding global access)
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -155,7 +155,7 @@ class DeviceSampler:
         if ce > 32768:
             raise ValueError(f"the transposed index needs <= 32768 block edges, got {ce}")
         z = lambda n: torch.zeros(n, dtype=torch.int32, device=self.device)  # noqa: E731
-        self.csc[hop] = (z(ce), z(ce + 1), z(ce), z(ce + 1))
+        self.csc[hop] = (z(ce), z(ce + 1), z(ce), z(max(ce + 1, CSC_LONG_INTS)))
         return self.csc[hop]
 
     # -- the per-step device work ------------------------------------------------------------
@@ -278,7 +278,14 @@ class _NsmWork(ctypes.Structure):
                 ("s_agg", _P), ("s_w", _P), ("z", _P), ("beta", _P), ("nvalid", _P), ("slab", _P),
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
                 ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P),
-                ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML), ("part", ctypes.c_int32)]
+                ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML), ("part", ctypes.c_int32),
+                ("hub_acc", _P), ("hub_ticket", _P), ("hub_terms", _P)]
+
+# include/regnn_hip.h REGNN_CSC_LONG_*: hub rows of a <= 32768-edge block, their <= 1024-entry
+# pieces, and the csc_long buffer holding ids + piece table
+_LONG_CAP = 32768 // 17 + 1
+_MAX_PIECE = 32768 // 1024 + _LONG_CAP
+CSC_LONG_INTS = ((_LONG_CAP + 2) + 3) // 4 * 4 + 4 * _MAX_PIECE
 
 
 class _NsmAdam(ctypes.Structure):
@@ -478,6 +485,10 @@ class FusedStep:
             W.gh1 = ptr(z(caps[0], 64))
             _, cptr, cent, clong = sampler.csc[0] or sampler.enable_csc(0)
             W.csc_ptr0, W.csc_ent0, W.csc_long0 = ptr(cptr), ptr(cent), ptr(clong)
+            # exact hub-row sums of layer 1's transposed pass (kept zero between steps)
+            W.hub_acc = ptr(torch.zeros(_MAX_PIECE * 64, dtype=torch.int64, device=dev))
+            W.hub_ticket = ptr(torch.zeros(_LONG_CAP, dtype=torch.int32, device=dev))
+            W.hub_terms = ptr(torch.zeros(3 * 64, dtype=torch.int64, device=dev))
             # the blocks in the fixed-stride layout: sampling and placement in one launch per hop
             sampler.strided = STRIDED["mode"] != "off"
             if sampler.strided:

@@ -30,12 +30,49 @@ def main():
     f = L._so.regnn_nsm2_phases
     f.argtypes = [ctypes.c_void_p]
     buf = np.zeros((4, 32, 16), np.uint64)
+    fe = L._so.regnn_nsm2_edges
+    fe.argtypes = [ctypes.c_void_p]
+    edges = np.zeros((5, 2, 4096), np.uint64)
     for i in range(8):
+        if i == 7:
+            L._so.regnn_nsm2_edges_reset()
         tr.step()
         torch.cuda.synchronize()
     f(buf.ctypes.data)
-    t0 = int(buf[0, :, 0][buf[0, :, 0] > 0].min())
-    names = {0: "agg0", 1: "head", 2: "bwd0", 3: "finalize"}
+    fe(edges.ctypes.data)
+    s = tr.sampler
+    if s.csc[0] is not None:
+        _, cptr, _, clong = s.csc[0]
+        nl = int(clong[0])
+        ids = clong[1:1 + nl].long()
+        m = (cptr[ids + 1] - cptr[ids]).cpu().numpy()
+        print(f"hop-0 block: {int(s.sizes[1])} sources, {int(s.sizes[8])} edges; {nl} hub rows, "
+              f"entries max {m.max() if nl else 0} p50 {np.median(m) if nl else 0} sum {m.sum()}; "
+              f"pieces {int(clong[1929])}")
+    e0 = edges[0, 0][edges[0, 0] > 0]
+    t0 = int(e0.min()) if e0.size else int(buf[0, :, 0][buf[0, :, 0] > 0].min())
+    names = {0: "agg0", 1: "head", 2: "bwd0/gath", 3: "finalize"}
+    if hasattr(L._so, "regnn_nsm2_gpieces"):
+        gp = np.zeros((64, 8), np.uint64)
+        L._so.regnn_nsm2_gpieces.argtypes = [ctypes.c_void_p]
+        L._so.regnn_nsm2_gpieces(gp.ctypes.data)
+        for j in range(64):
+            row = gp[j].astype(np.int64)
+            if row[0] <= 0:
+                continue
+            marks = " ".join(f"{(x - t0) / 100.0:7.2f}" for x in row[:4] if x > 0)
+            print(f"piece {j:2d}: {marks}")
+    for k, nm in enumerate(["agg0", "head", "gather", "bwd0", "finalize"]):
+        en, ex = edges[k, 0].astype(np.int64), edges[k, 1].astype(np.int64)
+        ok = (en > 0) & (ex > 0)
+        if not ok.any():
+            continue
+        en, ex = (en[ok] - t0) / 100.0, (ex[ok] - t0) / 100.0
+        dur = ex - en
+        print(f"{nm:9s} blocks {ok.sum():5d}: entry {en.min():7.2f}..{en.max():7.2f}  exit "
+              f"{ex.min():7.2f}..{ex.max():7.2f} (p50 {np.percentile(ex, 50):7.2f} p90 "
+              f"{np.percentile(ex, 90):7.2f})  dur p50 {np.percentile(dur, 50):6.2f} max "
+              f"{dur.max():6.2f}  slowest block {int(np.nonzero(ok)[0][np.argmax(dur)])}")
     for k in range(4):
         for p in range(16):
             col = buf[k, :, p].astype(np.int64)
