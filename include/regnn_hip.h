@@ -814,6 +814,38 @@ int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_
                     float lr, float beta1, float beta2, float eps, float weight_decay,
                     float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream);
 
+/* ---- fp32-accurate dense GEMM on bf16 MFMA (bf16x6) ----------------------------------------
+ * C = op(A) op(B) (+ beta C), M x N x K, row-major fp32: trans_a: A stored [K][M] (lda >= M),
+ * else [M][K] (lda >= K); trans_b: B stored [N][K], else [K][N]. Each operand is split into three
+ * bf16 parts and the six significant cross products accumulate in fp32 (error ~ fp32 rounding).
+ * Replaces the wide NS model's torch.mm / addmm / nn.Linear products (mag/regnn_ns.py:300-346,
+ * mag/regnn_layers.py:101-107 at hidden 128 .. 512) and their backward products. The operands'
+ * contiguous dimensions (K or M for A, K or N for B) and lda / ldb are multiples of 4, A and B
+ * 16-byte aligned. splits > 1: split-K over `work` (regnn_gemm_x6_work_floats floats), partials
+ * added in split order (bitwise reproducible). */
+int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits);
+int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                  const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                  float beta, float* work, int32_t splits, hipStream_t stream);
+
+/* ---- The wide NS model's per-layer epilogue (mag/regnn_layers.py:131-135 + mag/regnn_ns.py:
+ * 341-343 at hidden H in {64, 128, 256, 512, 1024}) ----------------------------------------------
+ * Forward over n rows of H fp32: a = rs[v] x[v] + bias (+ res[v]) (rs, bias, res optional), y =
+ * dropout(relu(LayerNorm(a; gamma, beta, eps 1e-5))); writes a, stats [n][2] = (mean, rstd) and
+ * y. Dropout (p_drop > 0): the fused NS step's mask spec (regnn_nsm_step) keyed on the sampler
+ * state and `layer`. Backward from gy: gx = rs[v] d a (rs NULL: 1), gres = d a (optional), and
+ * slab [regnn_wide_ln_slab_rows(n, H)][3 H] of per-block partials [sum d a | sum gy' xhat | sum
+ * gy'] (the bias, LN weight and LN bias gradients after regnn_rel_reduce). 16-byte aligned rows. */
+int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, const float* bias,
+                      const float* res, const float* gamma, const float* beta,
+                      const int64_t* state, int32_t layer, float p_drop, float* a, float* stats,
+                      float* y, hipStream_t stream);
+int64_t regnn_wide_ln_slab_rows(int64_t n, int32_t H);
+int regnn_wide_ln_bwd(int64_t n, int32_t H, const float* gy, const float* a, const float* stats,
+                      const float* rs, const float* gamma, const float* beta,
+                      const int64_t* state, int32_t layer, float p_drop, float* gx, float* gres,
+                      float* slab, hipStream_t stream);
+
 /* ---- Per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, group_input) ----
  * The reference builds the batch's input matrix with one boolean mask per node type (a host
  * sync each) and, for feats_type != 2, runs each type's Linear over its masked subset. Node i of

@@ -6,6 +6,8 @@ The sampled block's aggregation (PyG propagate with aggr='mean', message ew * x_
 runs as one HIP SpMM with the relation table, the 1/in-count scale and the bias fused; its
 backward is the fused transposed SpMM + relation-bin SDDMM.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -82,14 +84,14 @@ class REGCNConv(torch.nn.Module):
             agg = ops.ns_spmm(edge_index, x_src, tab)
             if self.residual:
                 agg = agg + x_target
-            out = torch.addmm(self.bias, agg, self.weight)
+            out = ops.mm(agg, self.weight, self.bias)
             if self.use_norm in ('bn', 'ln'):
                 out = self.norm(out)                                             # :134-135
             if return_weights:
                 return out, self._edge_weights(edge_index, edge_type, target_node_type, tab,
                                                x_target.shape[0]), tab
             return out
-        xs = torch.matmul(x_src, self.weight)                                    # :102
+        xs = ops.mm(x_src, self.weight)                                          # :102
         if isinstance(edge_index, tuple):           # pre-built (RelGraph, RelPack) block
             rg, pack = edge_index
         else:
@@ -97,13 +99,22 @@ class REGCNConv(torch.nn.Module):
                                   x_target.shape[0], self.num_edge_types, self.self_loop_type)
         out = ops.re_spmm(rg, xs, tab, pack, post=rg.inv_in_count(), bias=self.bias)
         if self.residual:
-            out = out + torch.matmul(x_target, self.weight)                      # :104,131-132
+            out = out + ops.mm(x_target, self.weight)                            # :104,131-132
         if self.use_norm in ('bn', 'ln'):
             out = self.norm(out)                                                 # :134-135
         if return_weights:
             return out, self._edge_weights(edge_index, edge_type, target_node_type, tab,
                                            x_target.shape[0]), tab
         return out
+
+    def forward_act(self, x_src, x_target, blk, p, state, layer):
+        """forward() on a device-sampled block followed by the model's relu and dropout, the
+        bias / LayerNorm / relu / dropout as one launch (ops.wide_ln_act)."""
+        tab = F.leaky_relu(self.relation_weight * self.scaling_factor)           # :110-111
+        agg = ops.ns_spmm(blk, x_src, tab)
+        if self.residual:
+            agg = agg + x_target
+        return ops.wide_ln_act(ops.mm(agg, self.weight), self.bias, self.norm, p, state, layer)
 
     def _edge_weights(self, edge_index, edge_type, target_node_type, tab, n_dst):
         """ew of mag/regnn_layers.py:110-126 per edge in the reference's order (sampled edges,
@@ -271,6 +282,10 @@ class REGATv2Conv(REGATConv):
 # raw input rows per node type and projects after (REGNN._typed_first_layer); "off": group_input
 # over every sampled node first, as the reference orders it (tests compare the two)
 TYPED_AGG = {"mode": "auto"}
+# "on": at hidden >= 128 the device-block path runs each layer's bias / residual / LayerNorm /
+# relu / dropout as one launch each way (ops.wide_ln_act: regnn_wide_ln_fwd / _bwd); "off":
+# torch's kernels (A/B, tests)
+WIDE_EPI = {"mode": os.environ.get("REGNN_WIDE_EPI", "on")}
 
 
 class REGNN(torch.nn.Module):
@@ -433,7 +448,20 @@ class REGNN(torch.nn.Module):
         return (tabs is not None and ops.ns_typed_agg_ok(tabs) and
                 self.convs[0].relation_weight.numel() <= 256)
 
-    def _typed_first_layer(self, n_id, x_dict, adjs, node_type, local_node_idx):
+    def _wide_epi(self, blk):
+        """(dropout p, state) when the device-block layers may run the fused wide epilogue
+        (ops.wide_ln_act), else None."""
+        if (WIDE_EPI["mode"] == "off" or self.model != 'regcn' or self.hidden_dim < 128 or
+                self.hidden_dim not in ops.WIDE_LN_WIDTHS or
+                any(c.use_norm != 'ln' for c in self.convs)):
+            return None
+        p = float(self.dropout) if self.training else 0.0
+        state = getattr(blk, "state", None)
+        if p > 0 and state is None:
+            return None
+        return p, state
+
+    def _typed_first_layer(self, n_id, x_dict, adjs, node_type, local_node_idx, epi=None):
         """layer 0 over a device block with group_input folded in (None: not applicable).
 
         The reference runs every sampled node's raw row through its type's Linear
@@ -463,28 +491,40 @@ class REGNN(torch.nn.Module):
         lins = [self.lins[str(t)] for t in range(T)]
         w_cat = torch.cat([lin.weight.t() for lin in lins], 0)                  # [T K, H]
         b_cat = torch.stack([lin.bias for lin in lins], 0)                      # [T, H]
-        w_c, b_c = w_cat @ conv.weight, b_cat @ conv.weight
+        # (products on regnn_gemm_x6: fp32-accurate bf16x6 MFMA)
+        w_c, b_c = ops.mm(w_cat, conv.weight), b_cat @ conv.weight
         n = blk.n_dst
-        agg = torch.addmm(torch.mm(w, b_c), S.view(n, T * K), w_c)
-        out = torch.addcmul(conv.bias, agg, blk.inv[:n].view(n, 1))           # mean + bias
+        agg = ops.mm(S.view(n, T * K), w_c, torch.mm(w, b_c))
+        res = None
         if conv.residual:                                                       # :104,131-132
             x_t = self.group_input(x_dict, node_type, local_node_idx, n_id[:n])
-            out = out + x_t @ conv.weight
+            res = ops.mm(x_t, conv.weight)
+        if epi is not None and ops.wide_ln_ok(agg, conv.norm):
+            # mean + bias + residual, LayerNorm, relu, dropout in one launch (:341-343)
+            return ops.wide_ln_act(agg, conv.bias, conv.norm, epi[0], epi[1], 0,
+                                   rs=blk.inv[:n], res=res), True
+        out = torch.addcmul(conv.bias, agg, blk.inv[:n].view(n, 1))           # mean + bias
+        if res is not None:
+            out = out + res
         if conv.use_norm in ('bn', 'ln'):
             out = conv.norm(out)                                                # :134-135
-        return out
+        return out, False
 
     def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
         ntype = node_type[n_id]
-        x = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx)
+        blk0 = tuple(adjs[0])[0] if adjs else None
+        epi = self._wide_epi(blk0) if getattr(blk0, "is_ns_block", False) else None
+        r = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx, epi)
+        x, acted = (None, False) if r is None else r
         if x is None and adjs and getattr(tuple(adjs[0])[0], "meta_only", False):
             raise RuntimeError("layer 0's block was sampled meta-only (no local source ids): "
                                "only the typed first layer (TYPED_AGG) can read it")
         start = 0
         if x is not None:                      # layer 0 done (group_input folded in)
             ntype = ntype[:tuple(adjs[0])[2][1]]
-            x = F.relu(x)
-            x = F.dropout(x, p=self.dropout, training=self.training)
+            if not acted:
+                x = F.relu(x)
+                x = F.dropout(x, p=self.dropout, training=self.training)
             start = 1
         else:
             x = self.group_input(x_dict, node_type, local_node_idx, n_id)
@@ -496,6 +536,11 @@ class REGNN(torch.nn.Module):
             ntype = ntype[:size[1]]
             blk = edge_index if getattr(edge_index, "is_ns_block", False) else \
                 getattr(adj, "block", None)
+            if (blk is not None and getattr(blk, "is_ns_block", False) and epi is not None and
+                    self.self_loop_type == 2 and ops.wide_ln_ok(x, self.convs[i].norm)):
+                ep = self._wide_epi(blk) or epi
+                x = self.convs[i].forward_act(x, x_target, blk, ep[0], ep[1], i)
+                continue                       # (relu and dropout applied in the epilogue)
             if blk is not None and self.model == 'regcn' and self.self_loop_type == 2:
                 x = self.convs[i]((x, x_target), blk)          # relation ids formed on device
             elif (self.model == 'regcn' and self.self_loop_type == 2 and

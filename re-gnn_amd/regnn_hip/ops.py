@@ -1488,3 +1488,131 @@ def typed_linear(tables, weights, biases, node_type, local_idx, n_id=None, wgrou
     plan = typed_plan(node_type, local_idx, n_id, T)
     return _TypedLinear.apply(plan, [t.contiguous() for t in tables], wg, len(weights),
                               *weights, *biases)
+
+
+# ---------------------------------------------------------------------------------------------
+# fp32-accurate dense products on bf16 MFMA (regnn_gemm_x6, bf16x6): the wide NS model's GEMMs
+# ---------------------------------------------------------------------------------------------
+# "on": ops.mm runs regnn_gemm_x6 where it applies; "off": torch (hipBLASLt fp32), A/B
+GEMM_X6 = {"mode": os.environ.get("REGNN_GEMM_X6", "on")}
+
+
+def _gemm_splits(M, N, K):
+    """split-K factor: enough blocks (~512) for a small output over a long reduction."""
+    tiles = -(-M // 64) * -(-N // 64)
+    nk = -(-K // 32)
+    if tiles >= 256 or nk < 8:
+        return 1
+    return int(max(1, min(64, 512 // tiles, nk // 4)))
+
+
+def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
+    """op(a) @ op(b) (+ beta * out) in fp32 accuracy: a [M, K] ([K, M] with trans_a), b [K, N]
+    ([N, K] with trans_b), contiguous fp32 device tensors."""
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm_x6: inner dimensions {K} and {Kb} differ")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+        beta = 0.0
+    S = _gemm_splits(M, N, K)
+    work = (torch.empty(int(L._so.regnn_gemm_x6_work_floats(M, N, S)), dtype=torch.float32,
+                        device=a.device) if S > 1 else None)
+    L.call("regnn_gemm_x6", int(trans_a), int(trans_b), M, N, K, L.ptr(a), a.stride(0), L.ptr(b),
+           b.stride(0), L.ptr(out), out.stride(0), float(beta), L.ptr(work), S, L.stream())
+    return out
+
+
+def gemm_x6_ok(*ts):
+    """the operands regnn_gemm_x6 takes: 2-D contiguous fp32 device tensors, every dimension a
+    multiple of 4 where it is a contiguous one (checked here for both layouts), 16-byte aligned."""
+    return all(t is not None and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and
+               t.is_contiguous() and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0 for t in ts)
+
+
+class _MMx6(torch.autograd.Function):
+    """c + a @ b (c optional, broadcast over rows when 1-D) with regnn_gemm_x6 forward and
+    backward (ga = g b^T, gb = a^T g: split-K over the rows)."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        if c is None:
+            out = gemm_x6(a, b)
+        else:
+            out = (c.expand(a.shape[0], b.shape[1]) if c.dim() == 1 else c).contiguous().clone()
+            gemm_x6(a, b, out=out, beta=1.0)
+        ctx.save_for_backward(a, b)
+        ctx.c_shape = None if c is None else c.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = gemm_x6(g, b, trans_b=True) if ctx.needs_input_grad[0] else None
+        gb = gemm_x6(a, g, trans_a=True) if ctx.needs_input_grad[1] else None
+        gc = None
+        if ctx.needs_input_grad[2]:
+            gc = g.sum(0) if len(ctx.c_shape) == 1 else g
+        return ga, gb, gc
+
+
+def mm(a, b, c=None):
+    """c + a @ b on regnn_gemm_x6 when the operands allow it (else torch)."""
+    if (GEMM_X6["mode"] != "off" and gemm_x6_ok(a, b) and
+            (c is None or (c.is_cuda and c.dtype == torch.float32))):
+        return _MMx6.apply(a, b, c)
+    return a @ b if c is None else (torch.addmm(c, a, b) if c.dim() <= 2 else c + a @ b)
+
+
+# ---------------------------------------------------------------------------------------------
+# the wide NS model's per-layer epilogue: rs x + bias (+ res) -> LayerNorm -> relu -> dropout
+# ---------------------------------------------------------------------------------------------
+WIDE_LN_WIDTHS = (64, 128, 256, 512, 1024)
+
+
+class _WideLn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, res, gamma, beta, rs, state, layer, p):
+        n, H = x.shape
+        a = torch.empty_like(x)
+        y = torch.empty_like(x)
+        stats = torch.empty(n, 2, dtype=torch.float32, device=x.device)
+        L.call("regnn_wide_ln_fwd", n, H, L.ptr(x), L.ptr(rs), L.ptr(bias), L.ptr(res),
+               L.ptr(gamma), L.ptr(beta), L.ptr(state), int(layer), float(p), L.ptr(a),
+               L.ptr(stats), L.ptr(y), L.stream())
+        ctx.save_for_backward(a, stats, rs, gamma, beta, state)
+        ctx.layer, ctx.p, ctx.has_res = int(layer), float(p), res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        a, stats, rs, gamma, beta, state = ctx.saved_tensors
+        n, H = a.shape
+        gy = gy.contiguous()
+        gx = torch.empty_like(a)
+        gres = torch.empty_like(a) if ctx.has_res and ctx.needs_input_grad[2] else None
+        rows = int(L._so.regnn_wide_ln_slab_rows(n, H))
+        slab = torch.empty(rows, 3 * H, dtype=torch.float32, device=a.device)
+        L.call("regnn_wide_ln_bwd", n, H, L.ptr(gy), L.ptr(a), L.ptr(stats), L.ptr(rs),
+               L.ptr(gamma), L.ptr(beta), L.ptr(state), ctx.layer, ctx.p, L.ptr(gx), L.ptr(gres),
+               L.ptr(slab), L.stream())
+        sums = _reduce(slab, 3 * H)
+        g_bias, g_gamma, g_beta = sums[:H], sums[H:2 * H], sums[2 * H:]
+        return (gx, g_bias, gres, g_gamma, g_beta, None, None, None, None)
+
+
+def wide_ln_ok(x, ln):
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and
+            x.shape[1] in WIDE_LN_WIDTHS and isinstance(ln, torch.nn.LayerNorm) and
+            ln.elementwise_affine and abs(ln.eps - 1e-5) < 1e-12 and x.data_ptr() % 16 == 0)
+
+
+def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None):
+    """dropout(relu(LayerNorm(rs * x + bias + res))) in one launch (regnn_wide_ln_fwd), the
+    dropout mask the fused NS step's spec keyed on the sampler `state` and `layer`."""
+    if p > 0 and state is None:
+        raise ValueError("wide_ln_act: dropout needs the sampler state (its mask key)")
+    return _WideLn.apply(x, bias, None if res is None else res.contiguous(), ln.weight, ln.bias,
+                         rs, state if p > 0 else None, layer, float(p))

@@ -1,0 +1,104 @@
+"""regnn_gemm_x6 (bf16x6: fp32 operands split into three bf16 parts, six MFMA products in fp32)
+against fp64 products: every layout, ragged M / N / K tails, split-K, beta accumulation, and the
+autograd wrapper's gradients. Tolerance: 2e-6 x sum_k |a_mk b_kn| (fp32 accumulation over K)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref(a, b, ta, tb):
+    a64, b64 = a.double(), b.double()
+    A = a64.t() if ta else a64
+    B = b64.t() if tb else b64
+    return A @ B, A.abs() @ B.abs()
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(5606, 512, 512), (100, 68, 36), (512, 512, 13312),
+                                   (64, 64, 32), (1, 4, 4), (333, 132, 1000)])
+def test_gemm_x6_layouts(ta, tb, M, N, K):
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(M + 7 * N + 13 * K)
+    a = torch.randn(*((K, M) if ta else (M, K)), generator=g, device=DEV)
+    b = torch.randn(*((N, K) if tb else (K, N)), generator=g, device=DEV)
+    if not (ops.gemm_x6_ok(a) and ops.gemm_x6_ok(b)):
+        pytest.skip("contiguous dimension not a multiple of 4")
+    c = ops.gemm_x6(a, b, trans_a=ta, trans_b=tb)
+    ref, mag = _ref(a, b, ta, tb)
+    err = (c.double() - ref).abs()
+    assert (err <= 2e-6 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+
+
+def test_gemm_x6_beta_and_splits_deterministic():
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    a = torch.randn(13312, 256, generator=g, device=DEV)
+    b = torch.randn(13312, 128, generator=g, device=DEV)
+    c0 = torch.randn(256, 128, generator=g, device=DEV)
+    assert ops._gemm_splits(256, 128, 13312) > 1
+    outs = []
+    for _ in range(2):
+        c = c0.clone()
+        ops.gemm_x6(a, b, trans_a=True, out=c, beta=1.0)
+        outs.append(c)
+    assert torch.equal(outs[0], outs[1])
+    ref = c0.double() + a.double().t() @ b.double()
+    mag = c0.double().abs() + a.double().abs().t() @ b.double().abs()
+    assert ((outs[0].double() - ref).abs() <= 2e-6 * mag).all()
+
+
+def test_mm_autograd_matches_fp64():
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = torch.randn(777, 256, generator=g, device=DEV, requires_grad=True)
+    b = torch.randn(256, 512, generator=g, device=DEV, requires_grad=True)
+    bias = torch.randn(512, generator=g, device=DEV, requires_grad=True)
+    gout = torch.randn(777, 512, generator=g, device=DEV)
+    y = ops.mm(a, b, bias)
+    y.backward(gout)
+    a64, b64, c64 = (t.detach().double().requires_grad_() for t in (a, b, bias))
+    y64 = c64 + a64 @ b64
+    y64.backward(gout.double())
+    for got, want in ((y, y64), (a.grad, a64.grad), (b.grad, b64.grad), (bias.grad, c64.grad)):
+        scale = max(1.0, float(want.abs().max()))
+        assert float((got.double() - want).abs().max()) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("H,dropout,res", [(512, 0.5, True), (128, 0.0, False), (1024, 0.3, False),
+                                           (64, 0.5, True)])
+def test_wide_ln_act_matches_autograd(H, dropout, res):
+    """ops.wide_ln_act (regnn_wide_ln_fwd / _bwd) against torch autograd of rs x + bias + res ->
+    LayerNorm -> relu -> (the same hash mask) in fp64: output and every input gradient."""
+    from oracle import regnn_oracle as O
+    from regnn_hip import ops
+    import test_gpu_ns_engine as E
+    g = torch.Generator(device=DEV).manual_seed(H)
+    n = 1000
+    x = torch.randn(n, H, generator=g, device=DEV, requires_grad=True)
+    rs = torch.rand(n, generator=g, device=DEV) + 0.5
+    bias = torch.randn(H, generator=g, device=DEV, requires_grad=True)
+    r = torch.randn(n, H, generator=g, device=DEV, requires_grad=True) if res else None
+    ln = torch.nn.LayerNorm(H).to(DEV)
+    with torch.no_grad():
+        ln.weight.normal_(1, 0.2)
+        ln.bias.normal_(0, 0.2)
+    state = torch.tensor([123, 2, 0, 9, 0, 0, 0, 0], dtype=torch.int64, device=DEV)
+    gy = torch.randn(n, H, generator=g, device=DEV)
+    y = ops.wide_ln_act(x, bias, ln, dropout, state, 1, rs=rs, res=r)
+    y.backward(gy)
+    keep16 = int(round((1 - dropout) * 65536))
+    mask = torch.from_numpy(O.dropout_mask(E._nsm_seed(state.cpu().tolist(), 1), n, H, 4, keep16)
+                            ).to(DEV) / (keep16 / 65536) if dropout > 0 else 1.0
+    x64, b64 = x.detach().double().requires_grad_(), bias.detach().double().requires_grad_()
+    w64, lb64 = ln.weight.detach().double().requires_grad_(), ln.bias.detach().double().requires_grad_()
+    r64 = r.detach().double().requires_grad_() if res else None
+    a = rs.double()[:, None] * x64 + b64 + (r64 if res else 0)
+    y64 = torch.relu(torch.nn.functional.layer_norm(a, (H,), w64, lb64, 1e-5)) * mask
+    y64.backward(gy.double())
+    pairs = [(y, y64), (x.grad, x64.grad), (bias.grad, b64.grad), (ln.weight.grad, w64.grad),
+             (ln.bias.grad, lb64.grad)] + ([(r.grad, r64.grad)] if res else [])
+    for got, want in pairs:
+        scale = max(1.0, float(want.abs().max()))
+        assert float((got.double() - want).abs().max()) <= 2e-5 * scale

@@ -119,3 +119,64 @@ def test_typed_agg_against_fp64_sums():
     ((S64 * gS[:n_dst].double().cpu()).sum() + (w64 * gw[:n_dst].double().cpu()).sum()).backward()
     ok, err = G.close(rw.grad.cpu().numpy(), rw64.grad.numpy(), 1e-5)
     assert ok, err
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+@pytest.mark.parametrize("hidden,residual", [(256, False), (512, True)])
+def test_wide_epilogue_and_gemm_match_torch_path(monkeypatch, hidden, residual, dropout):
+    """the wide module path's one-launch epilogue (ops.wide_ln_act: bias /
+    residual / LayerNorm / relu / dropout forward and backward) and its fp32-accurate bf16x6
+    GEMMs (ops.mm) against the same step on torch's kernels (hipBLASLt fp32, LayerNorm, relu,
+    dropout), loss and every gradient at 1e-5. With dropout the torch run gets the epilogue's
+    hash masks (oracle.dropout_mask of the fused step's per-layer key) in place of torch's RNG."""
+    from oracle import regnn_oracle as O
+    from regnn_hip import mag, ops
+    from test_gpu_ns_engine import _nsm_seed
+    d = _mag(0.003, seed=4, F=128)
+
+    def run(fast):
+        monkeypatch.setitem(mag.WIDE_EPI, "mode", "on" if fast else "off")
+        monkeypatch.setitem(ops.GEMM_X6, "mode", "on" if fast else "off")
+        calls = []
+        if not fast and dropout > 0:
+            keep16 = int(round((1 - dropout) * 65536))
+            real = torch.nn.functional.dropout
+
+            def hash_dropout(x, p=0.5, training=True, inplace=False):
+                if not training or p == 0:
+                    return real(x, p, training, inplace)
+                layer = len(calls)
+                calls.append(layer)
+                st = tr_box[0].sampler.state.cpu().tolist()
+                mask = O.dropout_mask(_nsm_seed(st, layer), x.shape[0], x.shape[1], 4, keep16)
+                return x * torch.from_numpy(mask).to(x.device, x.dtype) / (keep16 / 65536)
+            monkeypatch.setattr(torch.nn.functional, "dropout", hash_dropout)
+        from regnn_hip.ns import NSTrainer
+        torch.manual_seed(7)
+        m = mag.REGNN(128, hidden, 13, 2, 10.0, dropout, {k: 128 for k in d["x_dict"]}, 7,
+                      use_norm="ln", self_loop_type=2, residual=residual).to(DEV)
+        with torch.no_grad():
+            for conv in m.convs:
+                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, 11, device=DEV))
+                conv.bias.normal_(0, 0.1)
+                conv.norm.weight.normal_(1, 0.1)
+        m.train()
+        tr = NSTrainer(m, None, d["rg"], [6, 4], 96, torch.arange(d["n_paper"], device=DEV),
+                       d["x_dict"], d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=3,
+                       engine="module", pipeline=False)
+        tr_box[0] = tr
+        tr._forward_backward()
+        torch.cuda.synchronize()
+        if not fast and dropout > 0:
+            assert calls == [0, 1]
+        monkeypatch.undo()
+        return float(tr.loss), {n: p.grad.detach().double().cpu().numpy().copy()
+                                for n, p in m.named_parameters()}
+
+    tr_box = [None]
+    la, ga = run(True)
+    lb, gb = run(False)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
