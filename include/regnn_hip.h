@@ -620,12 +620,16 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  *           written once; rows u >= sizes[size_idx] (the batch's sources) get zeros)
  *   slab[b][r] (optional) = block b's partial of sum out_scale[v] <g[v], x[u]> over relation r
  *   (launches slab_rows blocks; reduce with regnn_rel_reduce; LDS float bins).
- * sizes may be null (then every row < cap_rows is live). F in {64, 128, 256, 512, 1024, 2048}. */
+ * sizes may be null (then every row < cap_rows is live). F in {64, 128, 256, 512, 1024, 2048}.
+ * hub_work (optional, regnn_ns_csc_hub_work_floats(F) floats): the hub rows (csc_long's piece
+ * table) are cut into chunks of (256 / min(64, F / 4)) * 8 entries, one workgroup each, and
+ * their sums added per row in chunk order by a second launch (without: a workgroup per hub row). */
+int64_t regnn_ns_csc_hub_work_floats(int32_t F);
 int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_long,
                           const float* rel_table, const float* out_scale, const float* g,
                           const float* x, float* gx, float* slab, int32_t n_rel,
                           const int32_t* sizes, int32_t size_idx, int64_t cap_rows, int32_t F,
-                          int32_t slab_rows, hipStream_t stream);
+                          int32_t slab_rows, float* hub_work, hipStream_t stream);
 
 /* Typed aggregation of raw input rows over a sampled block (layer 0 of the NS REGNN at any hidden
  * width; mag/regnn_ns.py:300-326 group_input + mag/regnn_layers.py:101-148, replacing the

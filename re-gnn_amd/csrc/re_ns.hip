@@ -719,6 +719,42 @@ __device__ __forceinline__ void csc_entries(const int32_t* __restrict__ cent,
     (void)gl;
 }
 
+// The hub rows' chunks (hub_work mode): every piece of the sampler's hub table
+// (REGNN_CSC_LONG_TAB) cut into chunks of kCscChunk entries, one workgroup each; cpre = the
+// exclusive chunk prefix over the pieces (in LDS), returns the chunk count.
+constexpr int kCscUN = 8;                  // csc_entries' rows in flight per lane
+__device__ __forceinline__ int csc_chunk_scan(const int32_t* __restrict__ clong, int chunk,
+                                              int* cpre, int* wsum) {
+    const int n_piece = clong[REGNN_CSC_LONG_NPIECE];
+    const int4* pt = reinterpret_cast<const int4*>(clong + REGNN_CSC_LONG_TAB);
+    int cnt[8], run = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p = 8 * threadIdx.x + j;
+        cnt[j] = p < n_piece ? (pt[p].z + chunk - 1) / chunk : 0;
+        run += cnt[j];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int xv = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(xv, o, 64);
+        if (lane >= o) xv += y;
+    }
+    if (lane == 63) wsum[w] = xv;
+    __syncthreads();
+    int e = xv - run;
+    for (int k = 0; k < w; ++k) e += wsum[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p = 8 * threadIdx.x + j;
+        if (p <= n_piece) cpre[p] = e;
+        if (p < n_piece) e += cnt[j];
+    }
+    __syncthreads();
+    return cpre[n_piece];
+}
+
 template <int LPR, int VPL>
 __global__ void __launch_bounds__(kBlock)
 ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restrict__ cent,
@@ -726,9 +762,10 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
                        const float* __restrict__ out_scale, const float* __restrict__ g,
                        const float* __restrict__ x, float* __restrict__ gx,
                        float* __restrict__ slab, int n_rel, const int32_t* __restrict__ sizes,
-                       int size_idx, int64_t cap_rows) {
+                       int size_idx, int64_t cap_rows, float* __restrict__ hub_work) {
     constexpr int F = 4 * LPR * VPL;
     constexpr int NG = kBlock / LPR;       // row groups per block
+    constexpr int CH = NG * kCscUN;        // hub chunk: one round of every group's rows
     __shared__ float bins[256];
     __shared__ float4 part[NG * LPR * VPL];
     for (int r = threadIdx.x; r < n_rel; r += kBlock) bins[r] = 0.f;
@@ -736,6 +773,46 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
     const bool dots = slab != nullptr;
     const int l = threadIdx.x % LPR, grp = threadIdx.x / LPR, gl = (threadIdx.x & 63) - l;
     const int64_t n_rows = sizes ? min(cap_rows, int64_t(sizes[size_idx])) : cap_rows;
+    if (hub_work) {                            // ---- hub chunks (block-uniform)
+        __shared__ int cpre[REGNN_CSC_LONG_MAXPIECE + 1];
+        __shared__ int wsum[kBlock / 64];
+        const int total = csc_chunk_scan(clong, CH, cpre, wsum);
+        for (int j = int(gridDim.x) - 1 - int(blockIdx.x); j < total; j += gridDim.x) {
+            const int n_piece = clong[REGNN_CSC_LONG_NPIECE];
+            int lo = 0, hi = n_piece - 1;      // the piece p with cpre[p] <= j < cpre[p + 1]
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (cpre[mid] <= j) lo = mid; else hi = mid - 1;
+            }
+            const int4 pc = reinterpret_cast<const int4*>(clong + REGNN_CSC_LONG_TAB)[lo];
+            const int64_t u = pc.x;
+            const int e0 = pc.y + CH * (j - cpre[lo]);
+            const int e1 = min(e0 + CH, pc.y + pc.z);
+            float4 acc[VPL], xr[VPL];
+#pragma unroll
+            for (int p = 0; p < VPL; ++p) {
+                acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+                xr[p] = dots ? *reinterpret_cast<const float4*>(x + u * F + 4 * (l + LPR * p))
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            const int c0 = e0 + kCscUN * grp;
+            csc_entries<LPR, VPL>(cent, tab, out_scale, g, bins, dots, c0, min(c0 + kCscUN, e1),
+                                  1, l, gl, xr, acc);
+#pragma unroll
+            for (int p = 0; p < VPL; ++p) part[(grp * VPL + p) * LPR + l] = acc[p];
+            __syncthreads();
+            for (int i = threadIdx.x; i < LPR * VPL; i += kBlock) {
+                float4 s4 = part[i];
+                for (int k = 1; k < NG; ++k) {
+                    const float4 q = part[k * LPR * VPL + i];
+                    s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+                }
+                const int p = i / LPR, ll = i % LPR;
+                *reinterpret_cast<float4*>(hub_work + int64_t(j) * F + 4 * (ll + LPR * p)) = s4;
+            }
+            __syncthreads();
+        }
+    }
     // ---- rows with <= kCscShort entries (and the rows past the batch: zeros)
     for (int64_t u = int64_t(blockIdx.x) * NG + grp; u < cap_rows; u += int64_t(gridDim.x) * NG) {
         const bool live = u < n_rows;
@@ -753,8 +830,8 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
         for (int p = 0; p < VPL; ++p)
             *reinterpret_cast<float4*>(gx + u * F + 4 * (l + LPR * p)) = acc[p];
     }
-    // ---- hub rows: a workgroup each
-    const int n_long = clong ? clong[0] : 0;
+    // ---- hub rows: a workgroup each (without hub_work)
+    const int n_long = clong && !hub_work ? clong[0] : 0;
     for (int li = blockIdx.x; li < n_long; li += gridDim.x) {
         const int64_t u = clong[1 + li];
         const int c0 = cptr[u], c1 = cptr[u + 1];
@@ -785,6 +862,29 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
     for (int r = threadIdx.x; r < n_rel; r += kBlock) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
 }
 
+// hub_work mode's second launch: each hub row's chunk sums added in chunk order -> gx[u]
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+ns_csc_hub_sum_kernel(const int32_t* __restrict__ clong, int chunk,
+                      const float* __restrict__ hub_work, float* __restrict__ gx) {
+    __shared__ int cpre[REGNN_CSC_LONG_MAXPIECE + 1];
+    __shared__ int wsum[kBlock / 64];
+    csc_chunk_scan(clong, chunk, cpre, wsum);
+    const int n_piece = clong[REGNN_CSC_LONG_NPIECE];
+    const int4* pt = reinterpret_cast<const int4*>(clong + REGNN_CSC_LONG_TAB);
+    for (int p = blockIdx.x; p < n_piece; p += gridDim.x) {
+        const int4 pc = pt[p];
+        if ((pc.w >> 8) & 255) continue;       // not the row's first piece
+        const int npc = pc.w & 255;
+        const int c0 = cpre[p], c1 = cpre[p + npc];
+        for (int f = threadIdx.x; f < F; f += kBlock) {
+            float sacc = 0.f;
+            for (int c = c0; c < c1; ++c) sacc += hub_work[int64_t(c) * F + f];
+            gx[int64_t(pc.x) * F + f] = sacc;
+        }
+    }
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -799,22 +899,35 @@ static bool ns_half_waves() {
 
 extern "C" {
 
+int64_t regnn_ns_csc_hub_work_floats(int32_t F) {
+    // chunks of (256 / LPR) * 8 entries over <= 32768 hub entries, + one partial chunk per piece
+    const int lpr = F >= 256 ? 64 : F / 4;
+    const int ch = (kBlock / lpr) * kCscUN;
+    return int64_t(32768 / ch + REGNN_CSC_LONG_MAXPIECE) * F;
+}
+
 int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_long,
                           const float* rel_table, const float* out_scale, const float* g,
                           const float* x, float* gx, float* slab, int32_t n_rel,
                           const int32_t* sizes, int32_t size_idx, int64_t cap_rows, int32_t F,
-                          int32_t slab_rows, hipStream_t stream) {
+                          int32_t slab_rows, float* hub_work, hipStream_t stream) {
     if (!csc_ptr || !csc_ent || !g || !gx || cap_rows < 0 || F <= 0 || n_rel < 0 || n_rel > 256 ||
         (slab && (!x || n_rel == 0 || slab_rows <= 0)) || (sizes && size_idx < 0))
         return REGNN_EINVAL;
     if (cap_rows == 0) return REGNN_OK;
+    if (hub_work && !csc_long) return REGNN_EINVAL;
     const int grid = slab ? slab_rows : kMaxGrid;
 #define NSC_CASE(L, V)                                                                         \
     if (F == 4 * L * V) {                                                                      \
         hipLaunchKernelGGL((ns_spmm_bwd_csc_kernel<L, V>), dim3(grid), dim3(kBlock), 0,        \
                            stream, csc_ptr, csc_ent, csc_long, rel_table, out_scale, g, x, gx, \
-                           slab, n_rel, sizes, size_idx, cap_rows);                            \
+                           slab, n_rel, sizes, size_idx, cap_rows, hub_work);                  \
         REGNN_LAUNCH_CHECK();                                                                  \
+        if (hub_work) {                                                                        \
+            hipLaunchKernelGGL((ns_csc_hub_sum_kernel<4 * L * V>), dim3(256), dim3(kBlock), 0, \
+                               stream, csc_long, (kBlock / L) * kCscUN, hub_work, gx);         \
+            REGNN_LAUNCH_CHECK();                                                              \
+        }                                                                                      \
         return REGNN_OK;                                                                       \
     }
     NSC_CASE(16, 1) NSC_CASE(32, 1) NSC_CASE(64, 1) NSC_CASE(64, 2) NSC_CASE(64, 4)

@@ -566,6 +566,20 @@ _CSC_WIDTHS = (64, 128, 256, 512, 1024, 2048)   # regnn_ns_spmm_bwd_csc's F = 4 
 # "auto": a sampled block carrying its transposed index differentiates by the CSC gather; "off":
 # the atomic scatter (tests compare the two)
 NS_CSC = {"mode": "auto"}
+# "on": the CSC gather's hub rows in chunks over the grid (regnn_ns_spmm_bwd_csc hub_work);
+# "off": a workgroup per hub row
+NS_CSC_CHUNKED = {"mode": os.environ.get("REGNN_NS_CSC_CHUNKED", "on")}
+# include/regnn_hip.h REGNN_CSC_LONG_INTS (the sampler's csc_long with the hub piece table)
+CSC_LONG_INTS = ((32768 // 17 + 1 + 2) + 3) // 4 * 4 + 4 * (32768 // 1024 + 32768 // 17 + 1)
+_HUB_WORK = {}
+
+
+def _hub_work(F, device):
+    key = (F, device)
+    if key not in _HUB_WORK:
+        _HUB_WORK[key] = torch.empty(int(L._so.regnn_ns_csc_hub_work_floats(F)),
+                                     dtype=torch.float32, device=device)
+    return _HUB_WORK[key]
 
 
 class _NsSpmm(torch.autograd.Function):
@@ -606,11 +620,16 @@ class _NsSpmm(torch.autograd.Function):
             rows = L.slab_rows()
             slab = (torch.empty(rows, n_rel, dtype=torch.float32, device=x.device)
                     if (need_tab and t is not None) else None)
+            # the hub rows chunked over the grid (a workgroup per 8 entries per row group
+            # instead of per hub row: ~500-entry hubs at fan-out 25 dominated at F = 512)
+            hub = None
+            if NS_CSC_CHUNKED["mode"] != "off" and clong.numel() >= CSC_LONG_INTS:
+                hub = _hub_work(F, x.device)
             with timed("ns_spmm_bwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_bwd")):
                 L.call("regnn_ns_spmm_bwd_csc", L.ptr(cptr), L.ptr(cent), L.ptr(clong), L.ptr(t),
                        L.ptr(blk.inv),
                        L.ptr(gy), L.ptr(x), L.ptr(gx), L.ptr(slab), n_rel, L.ptr(sizes), size_idx,
-                       x.shape[0], F, rows, L.stream())
+                       x.shape[0], F, rows, L.ptr(hub), L.stream())
             g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
             g_bias = gy.sum(0) if ctx.needs_input_grad[2] else None
             return (gx if need_x else None), g_tab, g_bias, None

@@ -18,7 +18,7 @@ import _golden as G  # noqa: E402
 from test_gpu_ns_engine import _mag, DEV  # noqa: E402
 
 
-def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96):
+def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(6, 4)):
     from regnn_hip import mag, ops
     from regnn_hip.ns import NSTrainer
     old, old_csc = mag.TYPED_AGG["mode"], ops.NS_CSC["mode"]
@@ -35,7 +35,7 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96):
                 conv.bias.normal_(0, 0.1)
         m.train()
         opt = torch.optim.SGD(m.parameters(), lr=0.0)
-        tr = NSTrainer(m, opt, d["rg"], [6, 4], batch, torch.arange(d["n_paper"], device=DEV),
+        tr = NSTrainer(m, opt, d["rg"], list(sizes), batch, torch.arange(d["n_paper"], device=DEV),
                        d["x_dict"], d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=3,
                        engine="module")
         seen = []
@@ -177,6 +177,24 @@ def test_wide_epilogue_and_gemm_match_torch_path(monkeypatch, hidden, residual, 
     la, ga = run(True)
     lb, gb = run(False)
     assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
+
+
+def test_csc_gather_chunked_hubs_match(monkeypatch):
+    """the module path's transposed gather with the hub rows chunked over the grid
+    (regnn_ns_spmm_bwd_csc hub_work, NS_CSC_CHUNKED on) against a workgroup per hub row: loss and
+    every gradient at 1e-5 (fan-out 25 makes hubs of hundreds of entries at batch 512)."""
+    from regnn_hip import ops
+    d = _mag(0.01, seed=5, F=128)
+    out = {}
+    for mode in ("on", "off"):
+        monkeypatch.setitem(ops.NS_CSC_CHUNKED, "mode", mode)
+        out[mode] = _grads_one_step(d, 256, True, 0.0, batch=512, sizes=(25, 20))
+    la, ga = out["on"]
+    lb, gb = out["off"]
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb))
     for n in gb:
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
