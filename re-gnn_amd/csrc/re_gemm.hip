@@ -6,11 +6,11 @@
 // (mag/regnn_layers.py:101-107 by linearity), the other convs' x @ W, out_lin, and their
 // backward products.
 //
-// Block tile 64 x 64, k-step 32, 256 threads: wave w computes rows 32 (w >> 1) .., columns
-// 32 (w & 1) .. as 2 x 2 MFMA tiles. The next k-step's operands are requested before this
-// step's MFMAs (registers), split into the three bf16 parts and written to the other LDS stage
-// after them: one barrier per k-step. LDS rows of 32 bf16 padded to 40 (80 bytes: the 16 rows of
-// an 8-element fragment read fall on distinct banks).
+// Block tile 128 x 128, k-step 32, 256 threads: wave w computes rows 64 (w >> 1) .., columns
+// 64 (w & 1) .. as 4 x 4 MFMA tiles (96 MFMAs per k-step). The next k-step's operands are
+// requested before this step's MFMAs (registers) and split into the three bf16 parts on their
+// way into LDS. LDS rows of 32 bf16 padded to 40 (80 bytes: the 16 rows of an 8-element
+// fragment read fall on distinct banks).
 //
 // Split-K (splits > 1): block z of the grid's third dimension sums k-steps z, z + splits, ...
 // into its own partial C (work [splits][M][N]); regnn_gemm_x6 then adds the partials in split
@@ -23,9 +23,9 @@ namespace gemm {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 64, BN = 64, BK = 32, RS = 40;
+constexpr int BM = 128, BN = 128, BK = 32, RS = 40;
 constexpr int kThreads = 256;
-constexpr int kStage = 3 * (BM + BN) * RS;       // bf16 per LDS stage: A then B, 3 splits each
+constexpr int kStage = 3 * (BM + BN) * RS;       // bf16 of the LDS stage: A then B, 3 splits each
 
 __device__ __forceinline__ void split3(float x, uint16_t& a, uint16_t& b, uint16_t& c) {
     a = f2bf(x);
@@ -34,135 +34,134 @@ __device__ __forceinline__ void split3(float x, uint16_t& a, uint16_t& b, uint16
     c = f2bf(r - bf2f(b));
 }
 
-// one operand tile (64 rows r = m or n, 32 k) as two float4 per thread:
-//   KC (k contiguous in memory): element (r, k) at p[r * ld + k]; thread t -> rows t / 8 + 32 i,
-//      k = 4 (t % 8)
-//   !KC (r contiguous): element (r, k) at p[k * ld + r]; thread t -> k = t / 16 + 16 i,
-//      r = 4 (t % 16)
+// one operand tile (128 rows r = m or n, 32 k) as 4 quads (row r, k .. k + 3) per thread:
+//   KC (k contiguous): element (r, k) at p[r * ld + k]; quad i of thread t: i' = t + 256 i,
+//      r = i' / 8, k = 4 (i' % 8): one float4 load
+//   !KC (r contiguous): element (r, k) at p[k * ld + r]; i' = t + 256 i, r = i' % 128,
+//      k = 4 (i' / 128): four loads, each coalesced over the wave (consecutive r)
+template <bool KC>
+__device__ __forceinline__ void quad_rk(int i, int& r, int& k) {
+    const int q = threadIdx.x + kThreads * i;
+    if constexpr (KC) { r = q >> 3; k = 4 * (q & 7); }
+    else { r = q & 127; k = 4 * (q >> 7); }
+}
+
 template <bool KC>
 __device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t ld, int64_t r0,
-                                          int64_t nr, int64_t k0, int64_t K, float4 (&v)[2]) {
-    const int t = threadIdx.x;
+                                          int64_t nr, int64_t k0, int64_t K, float4 (&v)[4]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        int64_t r, k;
-        if constexpr (KC) {
-            r = r0 + (t >> 3) + 32 * i;
-            k = k0 + 4 * (t & 7);
-        } else {
-            k = k0 + (t >> 4) + 16 * i;
-            r = r0 + 4 * (t & 15);
-        }
-        const bool ok = r < nr && k < K;          // (the contiguous dim is a multiple of 4)
-        // clamped address, then select: an unconditional load (a load under a branch is
+    for (int i = 0; i < 4; ++i) {
+        int r, k;
+        quad_rk<KC>(i, r, k);
+        const int64_t rr = r0 + r, kk = k0 + k;
+        // clamped addresses, then a select: unconditional loads (a load under a branch is
         // waited on at once)
-        const int64_t rr = ok ? r : 0, kk = ok ? k : 0;
-        const float4 x = *reinterpret_cast<const float4*>(KC ? p + rr * ld + kk : p + kk * ld + rr);
-        v[i] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool rok = rr < nr;
+        const int64_t rc = rok ? rr : 0;
+        if constexpr (KC) {
+            const bool ok = rok && kk < K;         // (K a multiple of 4)
+            const float4 x = *reinterpret_cast<const float4*>(p + rc * ld + (ok ? kk : 0));
+            v[i] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            float e[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = rok && kk + j < K;
+                const float x = p[(ok ? kk + j : 0) * ld + rc];
+                e[j] = ok ? x : 0.f;
+            }
+            v[i] = make_float4(e[0], e[1], e[2], e[3]);
+        }
     }
 }
 
-// the tile's three bf16 splits into LDS [3][64][RS] (row = m or n, column = k)
+// the tile's three bf16 splits into LDS [3][128][RS] (row = m or n, column = k): 8-byte writes
 template <bool KC>
-__device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float4 (&v)[2]) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float4 (&v)[4]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
+        int r, k;
+        quad_rk<KC>(i, r, k);
         const float x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
         uint16_t a[4], b[4], c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) split3(x[j], a[j], b[j], c[j]);
-        if constexpr (KC) {
-            const int r = (t >> 3) + 32 * i, k = 4 * (t & 7);
-            uint16_t* d = s + r * RS + k;
-            *reinterpret_cast<uint2*>(d) = make_uint2(a[0] | (uint32_t(a[1]) << 16), a[2] | (uint32_t(a[3]) << 16));
-            *reinterpret_cast<uint2*>(d + 64 * RS) = make_uint2(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16));
-            *reinterpret_cast<uint2*>(d + 128 * RS) = make_uint2(c[0] | (uint32_t(c[1]) << 16), c[2] | (uint32_t(c[3]) << 16));
-        } else {
-            const int k = (t >> 4) + 16 * i, r = 4 * (t & 15);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                s[(r + j) * RS + k] = a[j];
-                s[(64 + r + j) * RS + k] = b[j];
-                s[(128 + r + j) * RS + k] = c[j];
-            }
-        }
+        uint16_t* d = s + r * RS + k;
+        *reinterpret_cast<uint2*>(d) = make_uint2(a[0] | (uint32_t(a[1]) << 16), a[2] | (uint32_t(a[3]) << 16));
+        *reinterpret_cast<uint2*>(d + BM * RS) = make_uint2(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16));
+        *reinterpret_cast<uint2*>(d + 2 * BM * RS) = make_uint2(c[0] | (uint32_t(c[1]) << 16), c[2] | (uint32_t(c[3]) << 16));
     }
 }
 
 // C[m][n] = sum_k opA[m][k] opB[k][n]; TA: A stored [K][M] (lda >= M), else [M][K]; TB: B
-// stored [N][K], else [K][N]
+// stored [N][K], else [K][N]. Wave w: rows 64 (w >> 1) .., columns 64 (w & 1) .. of the 128 x 128
+// tile as 4 x 4 MFMA tiles (96 MFMAs per k-step against 24 fragment reads from LDS).
 template <bool TA, bool TB>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads, 1)
 gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
                float beta, float* __restrict__ work) {
-    extern __shared__ uint16_t lds[];                 // [2][kStage]
+    extern __shared__ uint16_t lds[];                 // [kStage]
     constexpr bool AKC = !TA, BKC = TB;               // k contiguous in A / B
     const int64_t m0 = int64_t(blockIdx.y) * BM, n0 = int64_t(blockIdx.x) * BN;
     const int z = blockIdx.z, S = gridDim.z;
     const int64_t nk = (K + BK - 1) / BK;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
     const int wr = w >> 1, wc = w & 1;
-    f32x4 acc[2][2];
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 va[2], vb[2];
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 va[4], vb[4];
     int64_t kt = z;
     if (kt < nk) {
         load_tile<AKC>(A, lda, m0, M, kt * BK, K, va);
         load_tile<BKC>(B, ldb, n0, N, kt * BK, K, vb);
+    }
+    const uint16_t* sa = lds;
+    const uint16_t* sb = lds + 3 * BM * RS;
+    for (; kt < nk; kt += S) {
+        __syncthreads();                              // (the previous step's reads are done)
         store_tile<AKC>(lds, va);
         store_tile<BKC>(lds + 3 * BM * RS, vb);
-    }
-    __syncthreads();
-    int st = 0;
-    for (; kt < nk; kt += S) {
-        const bool more = kt + S < nk;
-        if (more) {                                   // the next k-step's operands, in flight
+        __syncthreads();
+        if (kt + S < nk) {                            // the next k-step's operands, in flight
             load_tile<AKC>(A, lda, m0, M, (kt + S) * BK, K, va);
             load_tile<BKC>(B, ldb, n0, N, (kt + S) * BK, K, vb);
         }
-        const uint16_t* sa = lds + st * kStage;
-        const uint16_t* sb = sa + 3 * BM * RS;
-        bf16x8_t a[2][3], b[2][3];
+        bf16x8_t b[4][3];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int s = 0; s < 3; ++s) {
-                a[i][s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * 64 + 32 * wr + 16 * i + c) * RS + 8 * q);
-                b[i][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * 64 + 32 * wc + 16 * i + c) * RS + 8 * q);
+            for (int s = 0; s < 3; ++s)
+                b[j][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * BN + 64 * wc + 16 * j + c) * RS + 8 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bf16x8_t a[3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                a[s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * BM + 64 * wr + 16 * i + c) * RS + 8 * q);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {              // small products first
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
             }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {              // small products first
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
-            }
-        if (more) {
-            uint16_t* d = lds + (st ^ 1) * kStage;
-            store_tile<AKC>(d, va);
-            store_tile<BKC>(d + 3 * BM * RS, vb);
         }
-        __syncthreads();
-        st ^= 1;
     }
     // D lane (q, c): rows 4 q + r of the 16-row tile, column c
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t n = n0 + 32 * wc + 16 * j + c;
+        for (int j = 0; j < 4; ++j) {
+            const int64_t n = n0 + 64 * wc + 16 * j + c;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t m = m0 + 32 * wr + 16 * i + 4 * q + r;
+                const int64_t m = m0 + 64 * wr + 16 * i + 4 * q + r;
                 if (m < M && n < N) {
                     if (S == 1) {
                         float* o = C + m * ldc + n;
@@ -217,7 +216,7 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
     const int64_t gy = (M + BM - 1) / BM, gx = (N + BN - 1) / BN;
     if (gy > 65535 || gx > 65535) return REGNN_EUNSUPPORTED;
     const dim3 grid{unsigned(gx), unsigned(gy), unsigned(splits)};
-    const size_t lds = size_t(2) * kStage * sizeof(uint16_t);
+    const size_t lds = size_t(kStage) * sizeof(uint16_t);
 #define GEMM_CASE(TA_, TB_)                                                                    \
     if (bool(trans_a) == TA_ && bool(trans_b) == TB_) {                                        \
         hipLaunchKernelGGL((gemm_x6_kernel<TA_, TB_>), grid, dim3(kThreads), lds, stream, M, N, K, \

@@ -114,6 +114,8 @@ _SIG = {
 }
 
 for _name, (_args, _ret) in _SIG.items():
+    if os.environ.get("REGNN_LIB") and not hasattr(_so, _name):
+        continue                  # an A/B build of an older tree: calls to it would fail loudly
     _f = getattr(_so, _name)
     _f.argtypes = _args
     _f.restype = _ret

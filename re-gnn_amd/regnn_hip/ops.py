@@ -1517,8 +1517,9 @@ GEMM_X6 = {"mode": os.environ.get("REGNN_GEMM_X6", "on")}
 
 
 def _gemm_splits(M, N, K):
-    """split-K factor: enough blocks (~512) for a small output over a long reduction."""
-    tiles = -(-M // 64) * -(-N // 64)
+    """split-K factor: about two 128 x 128 tiles per CU for a small output over a long
+    reduction (each split keeps >= 4 k-steps of 32)."""
+    tiles = -(-M // 128) * -(-N // 128)
     nk = -(-K // 32)
     if tiles >= 256 or nk < 8:
         return 1
