@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 36). */
+/* ABI version (bumped on any signature or semantics change; currently 37). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -775,10 +775,11 @@ typedef struct regnn_nsm_work {
     /* two-layer step: layer 1's transposed pass gives each piece of a hub row (> 16 entries,
      * the csc_long0 piece table) a workgroup of its own; the pieces' exact 2^-40 fixed-point
      * sums meet in hub_acc, the last piece of a row (hub_ticket) finishes it. hub_ticket and
-     * hub_terms zero-filled once by the caller, left zero by every step. */
+     * hub_terms zero-filled once by the caller, left zero by every step; hub_terms[192] is the
+     * step's fixed-point overflow flag (a term past 2^8: that step's loss reads NaN). */
     unsigned long long* hub_acc;   /* REGNN_CSC_LONG_MAXPIECE * 64 */
     int32_t* hub_ticket;           /* REGNN_CSC_LONG_CAP */
-    unsigned long long* hub_terms; /* 3 * 64 */
+    unsigned long long* hub_terms; /* 3 * 64 + 1 */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

@@ -47,11 +47,23 @@ constexpr int kMaxCT = 27;                 // class tiles of 16 (the head's LDS 
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
 
-// terms are rounded to 2^-40 (|x| < 2^23 per accumulated entry): gradient rows of a mean loss
-// are many orders of magnitude inside that range, and the rounding (<= 4.6e-13 per term) is far
-// below fp32 resolution of the sums it feeds
+// terms are rounded to 2^-40; an int64 sum holds |total| < 2^23. Every term is checked against
+// kFixTermMax = 2^8, so sums of up to 2^15 terms (a hub row's 32768 entries, a block's relation
+// bins) cannot wrap: gradient rows of a mean loss are many orders of magnitude inside that
+// range, and the rounding (<= 4.6e-13 per term) is far below fp32 resolution of the sums it
+// feeds. A term outside it (or NaN) sets the step's overflow flag and the step's loss reads NaN.
+constexpr float kFixTermMax = 256.f;
+// rn(x 2^40) as an int64 for |x 2^40| < 2^51 (= __float2ll_rn(x * 2^40), ties to even): x 2^40
+// is exact in fp64, the fma adds 1.5 2^52 so the rounding lands on the integer in the low
+// mantissa bits; subtracting the constant's bit pattern leaves the two's complement value (two
+// fp64 / two integer instructions instead of the generic f32 -> i64 conversion sequence)
 __device__ __forceinline__ unsigned long long to_fix(float x) {
-    return (unsigned long long)__float2ll_rn(x * kFixScale);
+    const double d = __builtin_fma(double(x), 1099511627776.0, 6755399441055744.0);
+    return (unsigned long long)(__double_as_longlong(d) - 0x4338000000000000ll);
+}
+__device__ __forceinline__ unsigned long long to_fix_chk(float x, bool& bad) {
+    bad |= !(fabsf(x) < kFixTermMax);
+    return to_fix(fminf(fmaxf(x, -kFixTermMax), kFixTermMax));
 }
 
 __device__ __forceinline__ float from_fix(unsigned long long q) {
@@ -665,11 +677,11 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
 //   3. LayerNorm, relu, dropout -> h (16 lanes per row);
 //   4. z = h W_out^T + b_out (class tiles over the waves), log_softmax, nll, g = (softmax -
 //      onehot) / n_valid, gh = g W_out, LayerNorm / relu / dropout backward -> ga, G = inv ga;
-//   5. partials: out_lin weight g^T h, its bias, conv bias / LN terms, the loss;
+//   5. g and h rows -> HBM (finalize forms out_lin's weight gradient g^T h from them over every
+//      row, MFMA tiles on otherwise idle CUs); partials: out_lin bias, conv bias / LN terms, loss;
 //   6. GH = G W_1^T -> HBM (the scatter's rows) and the W_1 partial Hagg^T G (MFMA).
 // out_lin.weight staged by LDS-DMA into an XOR-swizzled image (head_sw), as re_nsm.hip's head.
-// Slab row per block: [C*64 g out_w | C g out_b | 64 conv bias | 64 LN beta | 64 LN gamma |
-//                      1 loss | 64*64 g W_1]
+// Slab row per block: [C g out_b | 64 conv bias | 64 LN beta | 64 LN gamma | 1 loss | 64*64 g W_1]
 struct HeadArgs {
     const int32_t* sizes; const int32_t* n_id; const int64_t* labels;
     const int32_t* ptr; const int32_t* cnt; int stride;
@@ -679,11 +691,12 @@ struct HeadArgs {
     const int64_t* state; Drop drop;
     const float* w_out; const float* b_out; int C;
     float* gh; float* nvalid; float* part; int64_t part_w;
+    float* g_rows; float* h_rows;          // [blocks * 16][C] softmax gradient, [blocks * 16][64] h
 };
 
 // o_w1 (the W_1 partial) starts on a 16-byte boundary: finalize sums it with float4 loads
 __host__ __device__ inline int64_t head_o_w1(int C) {
-    return (int64_t(C) * (F + 1) + 3 * F + 1 + 3) & ~3ll;
+    return (int64_t(C) + 3 * F + 1 + 3) & ~3ll;
 }
 inline int64_t head_part_width(int C) { return head_o_w1(C) + F * F; }
 __host__ __device__ inline int head_cp(int C) { return ((C + 63) / 64) * 64 + 4; }
@@ -955,34 +968,24 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     __syncthreads();
     PH(1, 10);
     float* o = A.part + int64_t(blockIdx.x) * A.part_w;
-    const int64_t o_ob = int64_t(C) * F, o_cb = int64_t(C) * (F + 1), o_loss = o_cb + 3 * F;
+    const int64_t o_ob = 0, o_cb = C, o_loss = o_cb + 3 * F;
     const int64_t o_w1 = head_o_w1(C);
-    // ---- 5. out_lin weight partial D[c][k] = sum_v g[v][c] h[v][k], its bias, row terms
-    for (int ct = w; ct < CT; ct += kHeadThreads / 64) {
-        f32x4 dw[4];
+    // ---- 5. g rows (classes < C) and h rows -> HBM for finalize's out_lin weight tiles
+    {                                      // (the out_lin bias partial from the same reads)
+        float* gr = A.g_rows + int64_t(blockIdx.x) * kRows * C;
+        for (int c = threadIdx.x; c < C; c += kHeadThreads) {
+            float acc = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) dw[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            const int r = 4 * st + q;
-            const float av = zs[r * CP + 16 * ct + cc];
-#pragma unroll
-            for (int kb = 0; kb < 4; ++kb)
-                dw[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, hs2[r * 80 + 16 * kb + cc], dw[kb], 0, 0, 0);
-        }
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int c = 16 * ct + 4 * q + r;
-                if (c < C) o[int64_t(c) * F + 16 * kb + cc] = dw[kb][r];
+            for (int r = 0; r < kRows; ++r) {
+                const float gv = zs[r * CP + c];
+                gr[r * C + c] = gv;
+                acc += gv;
             }
-    }
-    for (int c = threadIdx.x; c < C; c += kHeadThreads) {
-        float acc = 0.f;
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) acc += zs[r * CP + c];
-        o[o_ob + c] = acc;
+            o[o_ob + c] = acc;
+        }
+        float* hr = A.h_rows + int64_t(blockIdx.x) * kRows * F;
+        for (int i = threadIdx.x; i < kRows * F; i += kHeadThreads)
+            hr[i] = hs2[(i >> 6) * 80 + (i & 63)];
     }
     if (threadIdx.x < 3 * F) {                                 // conv bias, LN beta, LN gamma
         const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
@@ -1055,7 +1058,7 @@ struct GathArgs {
     // hub rows (> kShort entries): their 16-entry chunks spread over every group of the grid;
     // exact sums in hub_acc [kLongCap][64], the last chunk's group (hub_ticket) runs the row's
     // backward and adds its row terms to hub_terms [3][64] (all exact 2^-40 integers; hub_acc /
-    // hub_ticket zeroed by that group, hub_terms by finalize)
+    // hub_ticket zeroed by that group, hub_terms by finalize); hub_terms[192]: the overflow flag
     unsigned long long* hub_acc; int32_t* hub_ticket; unsigned long long* hub_terms;
 };
 
@@ -1089,9 +1092,9 @@ __device__ __forceinline__ RowIn row_in(const GathArgs& A, uint32_t key, int u, 
 // tab[r] GH[v] into acc and the relation dots into the block's bins
 template <int UN>
 __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab,
-                                             unsigned long long* bins, int c, int m, int l,
+                                             unsigned long long (&rb)[4], int c, int m, int l,
                                              int gl, const RowIn& R,
-                                             unsigned long long (&acc)[4]) {
+                                             unsigned long long (&acc)[4], bool& bad) {
     const int my = l < m ? A.cent[c + l] : 0;
     for (int j = 0; j < m; j += UN) {
         int pk[UN];
@@ -1106,15 +1109,21 @@ __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab
             if (j + u >= m) continue;          // uniform over the group (continue: the loop
                                                // unrolls, a break leaves g[] in scratch)
             const float t = tab[pk[u] & 255];
-            acc[0] += to_fix(t * g[u].x);
-            acc[1] += to_fix(t * g[u].y);
-            acc[2] += to_fix(t * g[u].z);
-            acc[3] += to_fix(t * g[u].w);
+            acc[0] += to_fix_chk(t * g[u].x, bad);
+            acc[1] += to_fix_chk(t * g[u].y, bad);
+            acc[2] += to_fix_chk(t * g[u].z, bad);
+            acc[3] += to_fix_chk(t * g[u].w, bad);
             // an explicit fma chain: the entry's slot u in the (atomically ordered) segment must
             // not change how its dot is contracted, or the exact sums see different terms
             const float d = group_sum<16>(fmaf(R.h0[3], g[u].w, fmaf(R.h0[2], g[u].z,
                                                fmaf(R.h0[1], g[u].y, R.h0[0] * g[u].x))));
-            if (l == 0) atomicAdd(bins + (pk[u] & 255), to_fix(d));      // LDS, exact
+            // the dot into its relation's bin: lane r % 16, slot r / 16 (registers, exact; LDS
+            // atomics per entry would serialize the groups on the few relations' bins)
+            const unsigned long long dq = to_fix_chk(d, bad);
+            const int r = pk[u] & 255;
+            const bool mine = (r & 15) == l;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) rb[k] += mine && (r >> 4) == k ? dq : 0ull;
         }
     }
 }
@@ -1149,20 +1158,20 @@ __device__ __forceinline__ void row_bwd(const GathArgs& A, int u, int l, const R
 // independent of it)
 __device__ __forceinline__ void hub_row_bwd(const GathArgs& A, int u, int l, const RowIn& R,
                                             const float (&lw)[4],
-                                            const unsigned long long (&tot)[4]) {
+                                            const unsigned long long (&tot)[4], bool& bad) {
     float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
     row_bwd(A, u, l, R, lw, tot, sga, sgy, sgyx);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        atomicAdd(A.hub_terms + 0 * F + 4 * l + i, to_fix(sga[i]));
-        atomicAdd(A.hub_terms + 1 * F + 4 * l + i, to_fix(sgy[i]));
-        atomicAdd(A.hub_terms + 2 * F + 4 * l + i, to_fix(sgyx[i]));
+        atomicAdd(A.hub_terms + 0 * F + 4 * l + i, to_fix_chk(sga[i], bad));
+        atomicAdd(A.hub_terms + 1 * F + 4 * l + i, to_fix_chk(sgy[i], bad));
+        atomicAdd(A.hub_terms + 2 * F + 4 * l + i, to_fix_chk(sgyx[i], bad));
     }
 }
 
 // Hub rows: the sampler's piece table (REGNN_CSC_LONG_TAB) cuts each into pieces of <= 1024
 // entries; piece j runs on workgroup grid - 1 - j (the blocks past the short rows' range), its
-// 16 groups taking 16 entries at a time with every row in flight, the partial sums added exactly
+// 16 groups taking even shares of the entries with up to 16 rows in flight, the partial sums added exactly
 // in LDS. A row of one piece finishes there; a longer row's pieces store their sums to
 // hub_acc[j] and the piece that completes the row's ticket sums them (exact) and runs the row's
 // backward (device-scope fences: only for rows past 1024 entries).
@@ -1192,14 +1201,25 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     const float4 lb4 = reinterpret_cast<const float4*>(A.ln_b)[l];
     const float lw[4] = {lw4.x, lw4.y, lw4.z, lw4.w}, lb[4] = {lb4.x, lb4.y, lb4.z, lb4.w};
     float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
+    bool bad = false;                          // a fixed-point term out of range (to_fix_chk)
+    unsigned long long rb[4] = {0ull, 0ull, 0ull, 0ull};   // relation bins l + 16 k (exact)
     if (j < n_piece) {                         // block-uniform
         const int u = pc.x, e0 = pc.y, cnt = pc.z;
         const int li = pc.w >> 16, k = (pc.w >> 8) & 255, npc = pc.w & 255;
         PG(j, 0);
         const RowIn R = row_in(A, key, u, l, lw, lb);
         unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        for (int e = kShort * grp; e < cnt; e += kShort * 16)      // <= 1024 entries: 4 rounds
-            gather_chunk<kShort>(A, tab, bins, e0 + e, min(kShort, cnt - e), l, gl, R, acc);
+        // the piece's entries in even shares over the 16 groups (a 48-entry row: 3 per group,
+        // not 16 on each of three); chunk width by the share (block-uniform)
+        const int per = (cnt + 15) >> 4, g0 = min(cnt, per * grp), g1 = min(cnt, g0 + per);
+        if (per <= 4) {
+            if (g1 > g0) gather_chunk<4>(A, tab, rb, e0 + g0, g1 - g0, l, gl, R, acc, bad);
+        } else if (per <= 8) {
+            if (g1 > g0) gather_chunk<8>(A, tab, rb, e0 + g0, g1 - g0, l, gl, R, acc, bad);
+        } else {
+            for (int e = g0; e < g1; e += kShort)                  // <= 64 entries: 4 chunks
+                gather_chunk<kShort>(A, tab, rb, e0 + e, min(kShort, g1 - e), l, gl, R, acc, bad);
+        }
         PG(j, 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(lgh + 4 * l + i, acc[i]);   // LDS, exact
@@ -1234,7 +1254,7 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
                     if (l == 0)
                         __hip_atomic_store(A.hub_ticket + li, 0, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-                    hub_row_bwd(A, u, l, R, lw, tot);
+                    hub_row_bwd(A, u, l, R, lw, tot, bad);
                 }
             }
         }
@@ -1245,7 +1265,7 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
         if (m > kShort) continue;              // a hub: its pieces above
         const RowIn R = row_in(A, key, u, l, lw, lb);
         unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        gather_chunk<8>(A, tab, bins, c0, m, l, gl, R, acc);
+        gather_chunk<8>(A, tab, rb, c0, m, l, gl, R, acc, bad);
         row_bwd(A, u, l, R, lw, acc, sga, sgy, sgyx);
     }
 #pragma unroll
@@ -1254,7 +1274,11 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
         rt[1][grp][4 * l + i] = sgy[i];
         rt[2][grp][4 * l + i] = sgyx[i];
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (rb[k]) atomicAdd(bins + l + 16 * k, rb[k]);      // LDS, exact: order-free
     __syncthreads();
+    if (bad) A.hub_terms[3 * F] = 1ull;       // the overflow flag (finalize: NaN loss, reset)
     float* o = A.slab + int64_t(blockIdx.x) * kGathW;
     if (threadIdx.x < F) o[threadIdx.x] = float((long long)bins[threadIdx.x]) * kFixInv;
     if (threadIdx.x < 3 * F) {
@@ -1326,9 +1350,16 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     const int t = blockIdx.y, T = A.T;
     const bool t0 = t == 0;
     const float* wt = pick(A.lin_w.p, t);
-    for (int e = threadIdx.x; e < K * F; e += kBlock) {       // W_t[j][k] -> Wk[k][j]
-        const int j = e / K, k = e - j * K;
-        Wk[k * WS + j] = wt[e];
+    // W_t[j][k] -> Wk[k][j]: lane-consecutive j (conflict-free LDS writes), a float4 of row j
+    // per element group, every load of the thread in flight at once
+#pragma unroll
+    for (int e = threadIdx.x; e < K / 4 * F; e += kBlock) {
+        const int j = e & (F - 1), k4 = e >> 6;
+        const float4 v = *reinterpret_cast<const float4*>(wt + j * K + 4 * k4);
+        Wk[(4 * k4 + 0) * WS + j] = v.x;
+        Wk[(4 * k4 + 1) * WS + j] = v.y;
+        Wk[(4 * k4 + 2) * WS + j] = v.z;
+        Wk[(4 * k4 + 3) * WS + j] = v.w;
     }
     if (threadIdx.x < F) {
         bc[threadIdx.x] = pick(A.lin_b.p, t)[threadIdx.x];
@@ -1535,9 +1566,8 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     for (int a = 0; a < KB; ++a)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                o[int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q + i] = acc[a][jb][i];
+            *reinterpret_cast<float4*>(o + int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q) =
+                make_float4(acc[a][jb][0], acc[a][jb][1], acc[a][jb][2], acc[a][jb][3]);
     if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
     if constexpr (RS) {
         if (threadIdx.x < F) {
@@ -1562,7 +1592,7 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
 // finalize: every gradient a fixed-order sum of per-block partials (re_nsm.hip's job table);
 // with the optimizer attached, element e of a job's destination (a view into the flat gradient
 // bucket) is followed by Adam on parameter (dst + e - grad_base) of the flat buffers.
-enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2, kOpFix = 3 };
+enum { kOpCopy = 0, kOpRel = 1, kOpLoss = 2, kOpFix = 3, kOpOutW = 4 };
 
 struct Job {
     const float* src;
@@ -1570,7 +1600,8 @@ struct Job {
     int nparts, width, op, adam, vec;    // vec: 4 elements per thread (float4 partial rows)
     int cb;                  // columns (elements, or float4 columns if vec) per block: 32, 16, 8
     float* dst;
-    const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count
+    const float* aux;        // kOpRel: relation_weight; kOpLoss: the labelled-target count;
+                             // kOpOutW: the head's h rows (src: its g rows, nparts rows, width C)
     unsigned long long* fix; // kOpFix: 2^-40 fixed-point terms added to the sum, then zeroed
 };
 
@@ -1728,6 +1759,10 @@ __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, 
         } else if (J.op == kOpLoss) {
             const float nv = *J.aux;
             out = nv > 0.f ? tot / nv : 0.f;
+            if (J.fix && J.fix[0]) {           // the gather's fixed-point range was exceeded
+                out = __builtin_nanf("");
+                J.fix[0] = 0ull;
+            }
         } else if (J.op == kOpFix) {           // the gather's hub rows (exact), then reset
             out = tot + float((long long)J.fix[e]) * kFixInv;
             J.fix[e] = 0ull;
@@ -1736,6 +1771,61 @@ __device__ __forceinline__ void finalize_scalar(const FinArgs& A, const Job& J, 
         // torch.optim.Adam (regnn_adam_flat's arithmetic); a gradient outside the bucket (a
         // frozen parameter's scratch buffer) is not stepped
         if (stepped) adam_elem(O, i, out, pi, mi, vi, s_step, s_bc2);
+    }
+}
+
+// out_lin.weight's gradient tile (16 classes x 16 features) of block b = 4 class-tile + feature
+// tile: D[c][k] = sum_v g[v][c] h[v][k] over the head's rows (rows past the batch hold zeros);
+// wave w takes rows w R/4 .., the four row quarters added in a fixed order (MFMA lane (c, q):
+// A = g[v0 + q][c0 + c], B = h[v0 + q][k0 + c]; D row 4 q + r = class, column c = feature)
+__device__ __forceinline__ void finalize_outw(const Job& J, const AdamArgs& O, int b,
+                                              int64_t& s_t, float& s_step, float& s_bc2) {
+    __shared__ float red[4][256];
+    const int C = J.width, R = J.nparts;
+    const int c0 = 16 * (b >> 2), k0 = 16 * (b & 3);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
+    // this thread's element after the reduction: class c0 + t / 16, feature k0 + t % 16
+    const int ec = c0 + (threadIdx.x >> 4), ek = k0 + (threadIdx.x & 15);
+    const int64_t e = int64_t(ec) * F + ek;
+    const int64_t i = (J.dst + e) - O.gbase;
+    const bool stepped = O.on && J.adam && ec < C && i >= 0 && i < O.n;
+    float pi = 0.f, mi = 0.f, vi = 0.f;
+    if (stepped) {
+        pi = O.p[i]; mi = O.m[i]; vi = O.v[i];
+    }
+    adam_consts(O, s_t, s_step, s_bc2);
+    const int rq = ((R + 15) / 16) * 4;        // rows per wave (a multiple of 4)
+    const int v0 = w * rq, v1 = min(R, v0 + rq);
+    const int cl = min(c0 + cc, C - 1);
+    const bool cok = c0 + cc < C;
+    const float* g = J.src + cl;
+    const float* h = J.aux + k0 + cc;
+    f32x4 d = {0.f, 0.f, 0.f, 0.f};
+    constexpr int UN = 32;                     // every row of a 512-row batch in one load round
+    for (int v = v0; v < v1; v += 4 * UN) {
+        float av[UN], bv[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {          // clamped rows (zeroed past the range below)
+            const int vv = v + 4 * u + q;
+            const int vc = vv < v1 ? vv : v0;
+            av[u] = g[int64_t(vc) * C];
+            bv[u] = h[int64_t(vc) * F];
+        }
+        __builtin_amdgcn_sched_barrier(0);      // every load issued before the first MFMA
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const bool ok = v + 4 * u + q < v1;
+            d = __builtin_amdgcn_mfma_f32_16x16x4f32(ok && cok ? av[u] : 0.f, ok ? bv[u] : 0.f, d, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][(4 * q + r) * 16 + cc] = d[r];
+    __syncthreads();
+    if (ec < C) {
+        const int t = threadIdx.x;
+        const float tot = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+        J.dst[e] = tot;
+        if (stepped) adam_elem(O, i, tot, pi, mi, vi, s_step, s_bc2);
     }
 }
 
@@ -1751,7 +1841,9 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(FinArgs A) {
     PH(3, 0);
     PE(4, 0);
     const int el = threadIdx.x % J.cb, grp = threadIdx.x / J.cb;
-    if (J.vec) {                               // block-uniform
+    if (J.op == kOpOutW) {                     // block-uniform
+        finalize_outw(J, O, b, s_t, s_step, s_bc2);
+    } else if (J.vec) {
         finalize_vec(A, J, O, b, el, grp, s_t, s_step, s_bc2);
     } else {
         finalize_scalar(A, J, O, b, el, grp, s_t, s_step, s_bc2);
@@ -1776,10 +1868,18 @@ struct JobList {
         j.cb = cols <= 8 ? 8 : cols <= 16 ? 16 : 32;
         blocks += (cols + j.cb - 1) / j.cb;
     }
+    // out_lin.weight [C][64] = g^T h: g rows [rows][C], h rows [rows][64]; 4 blocks per 16 classes
+    void add_outw(const float* g, const float* h, int rows, int C, float* dst) {
+        A.start[A.n_jobs] = blocks;
+        Job& j = A.job[A.n_jobs++];
+        j.src = g; j.aux = h; j.pstride = 0; j.nparts = rows; j.width = C; j.dst = dst;
+        j.op = kOpOutW; j.fix = nullptr; j.adam = 1; j.vec = 0; j.cb = 16;
+        blocks += 4 * ((C + 15) / 16);
+    }
 };
 
 struct Slab2 {
-    int64_t head, gath, rel0, proj, post0, total;
+    int64_t head, hg, hh, gath, rel0, proj, post0, total;
     int head_blocks, rel0_rows;
 };
 
@@ -1789,6 +1889,10 @@ inline Slab2 slab2(const regnn_nsm_params* p, int cap0) {
     int64_t o = 0;
     s.head = o;
     o += int64_t(s.head_blocks) * head_part_width(p->n_classes);
+    s.hg = o;                                  // the head's g rows [rows][C] and h rows [rows][64]
+    o += int64_t(s.head_blocks) * kRows * p->n_classes;
+    s.hh = o;
+    o += int64_t(s.head_blocks) * kRows * F;
     s.gath = o;                                // the gather's relation dots and row terms
     o += int64_t(kGathBlocks) * kGathW;
     s.rel0 = o;                                // bwd0's (RS) or rel0's relation rows
@@ -1916,6 +2020,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         H.ln_w = p->ln_w[1]; H.ln_b = p->ln_b[1]; H.state = w->state; H.drop = drop;
         H.w_out = p->out_w; H.b_out = p->out_b; H.C = C;
         H.gh = w->gh1; H.nvalid = w->nvalid; H.part = w->slab + S.head; H.part_w = hw;
+        H.g_rows = w->slab + S.hg; H.h_rows = w->slab + S.hh;
         const size_t lds = head_lds(C);
         static size_t done = 0;
         if (!set_lds(reinterpret_cast<const void*>(&head_kernel), lds, &done))
@@ -1972,13 +2077,13 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         J.A.alpha = p->alpha;
         const float* hp = w->slab + S.head;
         const int nh = S.head_blocks;
-        const int64_t o_cb = int64_t(C) * (F + 1), o_w1 = head_o_w1(C);
-        J.add(hp, hw, nh, C * F, p->g_out_w);
-        J.add(hp + int64_t(C) * F, hw, nh, C, p->g_out_b);
+        const int64_t o_cb = C, o_w1 = head_o_w1(C);
+        J.add_outw(w->slab + S.hg, w->slab + S.hh, nh * kRows, C, p->g_out_w);
+        J.add(hp, hw, nh, C, p->g_out_b);
         J.add(hp + o_cb, hw, nh, F, p->g_conv_b[1]);
         J.add(hp + o_cb + F, hw, nh, F, p->g_ln_b[1]);
         J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
-        J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid);
+        J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid, w->hub_terms + 3 * F);
         J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
         const float* gs = w->slab + S.gath;
         J.add(gs, kGathW, kGathBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);

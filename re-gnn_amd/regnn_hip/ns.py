@@ -489,7 +489,7 @@ class FusedStep:
             # exact hub-row sums of layer 1's transposed pass (kept zero between steps)
             W.hub_acc = ptr(torch.zeros(_MAX_PIECE * 64, dtype=torch.int64, device=dev))
             W.hub_ticket = ptr(torch.zeros(_LONG_CAP, dtype=torch.int32, device=dev))
-            W.hub_terms = ptr(torch.zeros(3 * 64, dtype=torch.int64, device=dev))
+            W.hub_terms = ptr(torch.zeros(3 * 64 + 1, dtype=torch.int64, device=dev))
             # the blocks in the fixed-stride layout: sampling and placement in one launch per hop
             sampler.strided = STRIDED["mode"] != "off"
             if sampler.strided:

@@ -456,6 +456,31 @@ def test_fused_step_large_batch_takes_composed_form():
         assert ok, f"{n}: rel err {err:.3e}"
 
 
+def test_fused_step_fixed_point_overflow_reads_nan():
+    """layer 1's transposed pass sums 2^-40 fixed-point terms; a term past the
+    documented range (2^8) flags the step, whose loss then reads NaN (instead of a silently
+    wrapped gradient), and the next in-range step is clean again."""
+    d = _mag(0.003, seed=6, F=128, hidden=64, classes=37, dropout=0.0)
+    m = d["model"](1)
+    m.train()
+    tr, _ = _setup_trainer(d, m, batch=96, sizes=(7, 5), lr=0.0)
+    assert tr.fused is not None and tr.fused.two_layer
+    tr._forward_backward()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(tr.loss))
+    with torch.no_grad():                      # GH rows scale with out_lin.weight (layer 1's
+        w_out = m.out_lin.weight.clone()       # LayerNorm cancels a conv weight scale)
+        m.out_lin.weight.mul_(1e7)
+    tr._forward_backward()
+    torch.cuda.synchronize()
+    assert np.isnan(float(tr.loss))
+    with torch.no_grad():
+        m.out_lin.weight.copy_(w_out)
+    tr._forward_backward()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(tr.loss))
+
+
 @pytest.mark.parametrize("flat_adam", [False, True])
 def test_fused_step_graph_replay_tracks_eager(flat_adam):
     """the fused step captured in a HIP graph: losses equal the eager twin's step by step
