@@ -288,6 +288,9 @@ def run_ns(args, dev):
         exchange = "all-reduce captured in the step graph"
     else:
         exchange = "eager all-reduce between graphs"
+    if exchange and tr._xsplit and tr._early_ok:
+        exchange += (f"; the {tr.n_early} gradients final after layer 1's transposed pass "
+                     "all-reduced on a comm stream under layer 0's backward")
     res = {
         "metric": METRIC,
         "value": edges / elapsed,

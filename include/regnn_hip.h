@@ -780,6 +780,10 @@ typedef struct regnn_nsm_work {
     unsigned long long* hub_acc;   /* REGNN_CSC_LONG_MAXPIECE * 64 */
     int32_t* hub_ticket;           /* REGNN_CSC_LONG_CAP */
     unsigned long long* hub_terms; /* 3 * 64 + 1 */
+    int32_t split_finalize;   /* two-layer step, adam NULL: 1 = part 1 ends with the reduction of
+                                 the gradients final after layer 1's transposed pass (out_lin,
+                                 layer 1, layer 0's conv bias and LayerNorm), part 2 reduces the
+                                 rest (a caller all-reduces the first set while part 2 runs) */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*
@@ -824,14 +828,24 @@ int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_
  * else [M][K] (lda >= K); trans_b: B stored [N][K], else [K][N]. Each operand is split into three
  * bf16 parts and the six significant cross products accumulate in fp32 (error ~ fp32 rounding).
  * Replaces the wide NS model's torch.mm / addmm / nn.Linear products (mag/regnn_ns.py:300-346,
- * mag/regnn_layers.py:101-107 at hidden 128 .. 512) and their backward products. The operands'
- * contiguous dimensions (K or M for A, K or N for B) and lda / ldb are multiples of 4, A and B
- * 16-byte aligned. splits > 1: split-K over `work` (regnn_gemm_x6_work_floats floats), partials
+ * mag/regnn_layers.py:101-107 at hidden 128 .. 512) and their backward products. Operands whose
+ * contiguous dimensions (K or M for A, K or N for B) and lda / ldb are multiples of 4 and whose
+ * bases are 16-byte aligned load 16-byte vectors, any others per element. splits > 1: split-K over `work` (regnn_gemm_x6_work_floats floats), partials
  * added in split order (bitwise reproducible). */
 int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits);
 int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                   float beta, float* work, int32_t splits, hipStream_t stream);
+
+/* Several strided 2-D fp32 copies in one launch: dst[i * cols + j] = src[i * s0 + j * s1] for
+ * each descriptor (the module path's parameter gradients, some of them transposed views, into the
+ * flat gradient bucket: one launch instead of one copy per parameter). */
+typedef struct regnn_copy2d {
+    const float* src;
+    float* dst;
+    int64_t rows, cols, s0, s1;
+} regnn_copy2d;
+int regnn_copy2d_many(const regnn_copy2d* d, int32_t n, hipStream_t stream);
 
 /* ---- The wide NS model's per-layer epilogue (mag/regnn_layers.py:131-135 + mag/regnn_ns.py:
  * 341-343 at hidden H in {64, 128, 256, 512, 1024}) ----------------------------------------------

@@ -46,7 +46,7 @@ __device__ __forceinline__ void quad_rk(int i, int& r, int& k) {
     else { r = q & 127; k = 4 * (q >> 7); }
 }
 
-template <bool KC>
+template <bool KC, bool VEC>
 __device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t ld, int64_t r0,
                                           int64_t nr, int64_t k0, int64_t K, float4 (&v)[4]) {
 #pragma unroll
@@ -58,10 +58,19 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t l
         // waited on at once)
         const bool rok = rr < nr;
         const int64_t rc = rok ? rr : 0;
-        if constexpr (KC) {
+        if constexpr (KC && VEC) {
             const bool ok = rok && kk < K;         // (K a multiple of 4)
             const float4 x = *reinterpret_cast<const float4*>(p + rc * ld + (ok ? kk : 0));
             v[i] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if constexpr (KC) {                 // rows without 16-byte alignment: 4 loads
+            float e[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = rok && kk + j < K;
+                const float x = p[rc * ld + (ok ? kk + j : 0)];
+                e[j] = ok ? x : 0.f;
+            }
+            v[i] = make_float4(e[0], e[1], e[2], e[3]);
         } else {
             float e[4];
 #pragma unroll
@@ -96,8 +105,8 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float
 // C[m][n] = sum_k opA[m][k] opB[k][n]; TA: A stored [K][M] (lda >= M), else [M][K]; TB: B
 // stored [N][K], else [K][N]. Wave w: rows 64 (w >> 1) .., columns 64 (w & 1) .. of the 128 x 128
 // tile as 4 x 4 MFMA tiles (96 MFMAs per k-step against 24 fragment reads from LDS).
-template <bool TA, bool TB>
-__global__ void __launch_bounds__(kThreads, 1)
+template <bool TA, bool TB, bool VEC>
+__global__ void __launch_bounds__(kThreads, 2)
 gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
                float beta, float* __restrict__ work) {
@@ -116,8 +125,8 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
     float4 va[4], vb[4];
     int64_t kt = z;
     if (kt < nk) {
-        load_tile<AKC>(A, lda, m0, M, kt * BK, K, va);
-        load_tile<BKC>(B, ldb, n0, N, kt * BK, K, vb);
+        load_tile<AKC, VEC>(A, lda, m0, M, kt * BK, K, va);
+        load_tile<BKC, VEC>(B, ldb, n0, N, kt * BK, K, vb);
     }
     const uint16_t* sa = lds;
     const uint16_t* sb = lds + 3 * BM * RS;
@@ -127,8 +136,8 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
         store_tile<BKC>(lds + 3 * BM * RS, vb);
         __syncthreads();
         if (kt + S < nk) {                            // the next k-step's operands, in flight
-            load_tile<AKC>(A, lda, m0, M, (kt + S) * BK, K, va);
-            load_tile<BKC>(B, ldb, n0, N, (kt + S) * BK, K, vb);
+            load_tile<AKC, VEC>(A, lda, m0, M, (kt + S) * BK, K, va);
+            load_tile<BKC, VEC>(B, ldb, n0, N, (kt + S) * BK, K, vb);
         }
         bf16x8_t b[4][3];
 #pragma unroll
@@ -189,6 +198,27 @@ gemm_reduce_kernel(int64_t M, int64_t N, const float* __restrict__ work, int S, 
     }
 }
 
+// ---- several strided 2-D fp32 copies in one launch (the module path's parameter gradients into
+// the flat bucket): descriptors by value in the kernel arguments
+constexpr int kCopyMax = 32;
+struct CopyArgs {
+    regnn_copy2d d[kCopyMax];
+    int64_t start[kCopyMax + 1];           // element prefix over the descriptors
+    int n;
+};
+
+__global__ void __launch_bounds__(kThreads) copy2d_kernel(CopyArgs A) {
+    const int64_t total = A.start[A.n];
+    for (int64_t e = int64_t(blockIdx.x) * kThreads + threadIdx.x; e < total;
+         e += int64_t(gridDim.x) * kThreads) {
+        int k = 0;
+        while (k + 1 < A.n && e >= A.start[k + 1]) ++k;
+        const regnn_copy2d& d = A.d[k];
+        const int64_t i = e - A.start[k], r = i / d.cols, c = i - r * d.cols;
+        d.dst[i] = d.src[r * d.s0 + c * d.s1];
+    }
+}
+
 }  // namespace gemm
 }  // namespace regnn
 
@@ -207,22 +237,24 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
     if (M < 0 || N < 0 || K < 0 || splits < 1 || splits > 64) return REGNN_EINVAL;
     if (M == 0 || N == 0) return REGNN_OK;
     if (!A || !B || !C || (splits > 1 && !work)) return REGNN_EINVAL;
-    // 16-byte operand vectors along each operand's contiguous dimension
+    // 16-byte operand vectors along each operand's contiguous dimension where the shapes and
+    // addresses allow (else per-element loads: e.g. out_lin's 349 classes)
     const int64_t ca = trans_a ? M : K, cb = trans_b ? K : N;
-    if (ca % 4 || cb % 4 || lda % 4 || ldb % 4 || reinterpret_cast<uintptr_t>(A) % 16 ||
-        reinterpret_cast<uintptr_t>(B) % 16)
-        return REGNN_EUNSUPPORTED;
+    const bool vec = !(ca % 4 || cb % 4 || lda % 4 || ldb % 4 ||
+                       reinterpret_cast<uintptr_t>(A) % 16 || reinterpret_cast<uintptr_t>(B) % 16);
     if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N) return REGNN_EINVAL;
     const int64_t gy = (M + BM - 1) / BM, gx = (N + BN - 1) / BN;
     if (gy > 65535 || gx > 65535) return REGNN_EUNSUPPORTED;
     const dim3 grid{unsigned(gx), unsigned(gy), unsigned(splits)};
     const size_t lds = size_t(kStage) * sizeof(uint16_t);
-#define GEMM_CASE(TA_, TB_)                                                                    \
-    if (bool(trans_a) == TA_ && bool(trans_b) == TB_) {                                        \
-        hipLaunchKernelGGL((gemm_x6_kernel<TA_, TB_>), grid, dim3(kThreads), lds, stream, M, N, K, \
-                           A, lda, B, ldb, C, ldc, beta, work);                                \
+#define GEMM_CASE(TA_, TB_, V_)                                                                \
+    if (bool(trans_a) == TA_ && bool(trans_b) == TB_ && vec == V_) {                           \
+        hipLaunchKernelGGL((gemm_x6_kernel<TA_, TB_, V_>), grid, dim3(kThreads), lds, stream, M, N, \
+                           K, A, lda, B, ldb, C, ldc, beta, work);                             \
     }
-    GEMM_CASE(false, false) GEMM_CASE(false, true) GEMM_CASE(true, false) GEMM_CASE(true, true)
+    GEMM_CASE(false, false, true) GEMM_CASE(false, true, true) GEMM_CASE(true, false, true)
+    GEMM_CASE(true, true, true) GEMM_CASE(false, false, false) GEMM_CASE(false, true, false)
+    GEMM_CASE(true, false, false) GEMM_CASE(true, true, false)
 #undef GEMM_CASE
     REGNN_LAUNCH_CHECK();
     if (splits > 1) {
@@ -230,6 +262,28 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
         if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, stream, M,
                            N, work, splits, C, ldc, beta);
+        REGNN_LAUNCH_CHECK();
+    }
+    return REGNN_OK;
+}
+
+int regnn_copy2d_many(const regnn_copy2d* d, int32_t n, hipStream_t stream) {
+    if (n < 0 || (n && !d)) return REGNN_EINVAL;
+    for (int32_t b = 0; b < n; b += kCopyMax) {
+        CopyArgs A{};
+        A.n = n - b < kCopyMax ? n - b : kCopyMax;
+        for (int k = 0; k < A.n; ++k) {
+            const regnn_copy2d& x = d[b + k];
+            if (x.rows < 0 || x.cols < 0 || (x.rows * x.cols && (!x.src || !x.dst)))
+                return REGNN_EINVAL;
+            A.d[k] = x;
+            A.start[k + 1] = A.start[k] + x.rows * x.cols;
+        }
+        const int64_t total = A.start[A.n];
+        if (!total) continue;
+        int64_t blocks = (total + kThreads - 1) / kThreads;
+        if (blocks > 2048) blocks = 2048;
+        hipLaunchKernelGGL(copy2d_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, stream, A);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

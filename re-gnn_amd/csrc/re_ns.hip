@@ -710,9 +710,9 @@ __device__ __forceinline__ void csc_entries(const int32_t* __restrict__ cent,
                 d = fmaf(gv[u][p].w, xr[p].w, fmaf(gv[u][p].z, xr[p].z,
                          fmaf(gv[u][p].y, xr[p].y, fmaf(gv[u][p].x, xr[p].x, d))));
             }
-            if (dots) {
+            if (dots) {                        // the group's own bin row, in entry order
                 d = group_sum<LPR>(d);
-                if (l == 0 && c + u * step < c1) atomicAdd(bins + rr[u], ss[u] * d);
+                if (l == 0 && c + u * step < c1) bins[rr[u]] += ss[u] * d;
             }
         }
     }
@@ -766,12 +766,15 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
     constexpr int F = 4 * LPR * VPL;
     constexpr int NG = kBlock / LPR;       // row groups per block
     constexpr int CH = NG * kCscUN;        // hub chunk: one round of every group's rows
-    __shared__ float bins[256];
+    // relation bins per row group (lane 0 of a group adds its entries in order; the groups'
+    // rows are summed in group order at the end: no order-dependent float atomics)
+    __shared__ float gbins[NG][256];
     __shared__ float4 part[NG * LPR * VPL];
-    for (int r = threadIdx.x; r < n_rel; r += kBlock) bins[r] = 0.f;
+    for (int i = threadIdx.x; i < NG * 256; i += kBlock) gbins[i >> 8][i & 255] = 0.f;
     __syncthreads();
     const bool dots = slab != nullptr;
     const int l = threadIdx.x % LPR, grp = threadIdx.x / LPR, gl = (threadIdx.x & 63) - l;
+    float* bins = gbins[grp];
     const int64_t n_rows = sizes ? min(cap_rows, int64_t(sizes[size_idx])) : cap_rows;
     if (hub_work) {                            // ---- hub chunks (block-uniform)
         __shared__ int cpre[REGNN_CSC_LONG_MAXPIECE + 1];
@@ -859,7 +862,11 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
     }
     if (!dots) return;
     __syncthreads();
-    for (int r = threadIdx.x; r < n_rel; r += kBlock) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) {
+        float sr = 0.f;
+        for (int k = 0; k < NG; ++k) sr += gbins[k][r];
+        slab[int64_t(blockIdx.x) * n_rel + r] = sr;
+    }
 }
 
 // hub_work mode's second launch: each hub row's chunk sums added in chunk order -> gx[u]

@@ -1940,6 +1940,43 @@ bool regnn_nsm2_covers(const regnn_nsm_params* p) {
            head_lds(p->n_classes) <= size_t(160 * 1024 - 2560);
 }
 
+// the jobs whose partials are complete after the gather: out_lin, the head's layer-1 terms, the
+// loss, W_1, layer 1's relation table, layer 0's conv bias / LayerNorm (the gather's row terms)
+static void add_early_jobs(JobList& J, const regnn_nsm_params* p, const regnn_nsm_work* w,
+                           const Slab2& S) {
+    const int C = p->n_classes;
+    J.A.alpha = p->alpha;
+    const int64_t hw = head_part_width(C);
+    const float* hp = w->slab + S.head;
+    const int nh = S.head_blocks;
+    const int64_t o_cb = C, o_w1 = head_o_w1(C);
+    J.add_outw(w->slab + S.hg, w->slab + S.hh, nh * kRows, C, p->g_out_w);
+    J.add(hp, hw, nh, C, p->g_out_b);
+    J.add(hp + o_cb, hw, nh, F, p->g_conv_b[1]);
+    J.add(hp + o_cb + F, hw, nh, F, p->g_ln_b[1]);
+    J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
+    J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid, w->hub_terms + 3 * F);
+    J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
+    const float* gs = w->slab + S.gath;
+    J.add(gs, kGathW, kGathBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
+    J.add(gs + F, kGathW, kGathBlocks, F, p->g_conv_b[0], kOpFix, nullptr, w->hub_terms);
+    J.add(gs + 2 * F, kGathW, kGathBlocks, F, p->g_ln_b[0], kOpFix, nullptr, w->hub_terms + F);
+    J.add(gs + 3 * F, kGathW, kGathBlocks, F, p->g_ln_w[0], kOpFix, nullptr, w->hub_terms + 2 * F);
+}
+
+static void launch_finalize(JobList& J, const regnn_nsm_params* p, const regnn_nsm_adam* ad,
+                            hipStream_t stream) {
+    J.A.alpha = p->alpha;
+    if (ad) {
+        AdamArgs& O = J.A.adam;
+        O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;
+        O.n = ad->n;
+        O.lr = ad->lr; O.b1 = ad->beta1; O.b2 = ad->beta2; O.eps = ad->eps;
+        O.wd = ad->weight_decay; O.gscale = ad->grad_scale; O.step = ad->step; O.on = 1;
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(J.blocks), dim3(kBlock), 0, stream, J.A);
+}
+
 int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream_t stream) {
     const int T = p->n_types, K = p->k_in, C = p->n_classes;
     const bool rs = p->rel_slots != 0;
@@ -1951,6 +1988,11 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
     const regnn_nsm_adam* ad = w->adam;
     if (ad && (!ad->param || !ad->exp_avg || !ad->exp_avg_sq || !ad->grad_base || !ad->step))
         return REGNN_EINVAL;
+    // split_finalize: the gradients final after the gather (head, layer 1, layer 0's LayerNorm and
+    // conv bias) are reduced by a finalize launch at the end of part 1, so a caller can exchange
+    // them while part 2 runs; the fused Adam (its step count advances in bwd0) excludes it
+    const bool split = w->split_finalize != 0;
+    if (split && ad) return REGNN_EINVAL;
     const Slab2 S = slab2(p, w->cap[0]);
     const Drop drop = make_drop(p->p_drop);
     Ptrs lin_w{}, lin_b{}, xt{};
@@ -2040,6 +2082,12 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         G.hub_acc = w->hub_acc; G.hub_ticket = w->hub_ticket; G.hub_terms = w->hub_terms;
         hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kBlock), 0, stream, G);
         REGNN_LAUNCH_CHECK();
+        if (split) {
+            JobList J;
+            add_early_jobs(J, p, w, S);
+            launch_finalize(J, p, nullptr, stream);
+            REGNN_LAUNCH_CHECK();
+        }
     }
     if (!second) return REGNN_OK;
     // 4. layer 0's backward
@@ -2071,42 +2119,20 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         const int rc = regnn_nsm_rel0(p, w, w->slab + S.rel0, stream);
         if (rc != REGNN_OK) return rc;
     }
-    // 6. fixed-order reductions (+ Adam)
+    // 6. fixed-order reductions (+ Adam): the late jobs (bwd0's and rel0's partials), and the early
+    // ones here too unless part 1 reduced them (split_finalize)
     {
         JobList J;
-        J.A.alpha = p->alpha;
-        const float* hp = w->slab + S.head;
-        const int nh = S.head_blocks;
-        const int64_t o_cb = C, o_w1 = head_o_w1(C);
-        J.add_outw(w->slab + S.hg, w->slab + S.hh, nh * kRows, C, p->g_out_w);
-        J.add(hp, hw, nh, C, p->g_out_b);
-        J.add(hp + o_cb, hw, nh, F, p->g_conv_b[1]);
-        J.add(hp + o_cb + F, hw, nh, F, p->g_ln_b[1]);
-        J.add(hp + o_cb + 2 * F, hw, nh, F, p->g_ln_w[1]);
-        J.add(hp + o_cb + 3 * F, hw, nh, 1, p->loss, kOpLoss, w->nvalid, w->hub_terms + 3 * F);
-        J.add(hp + o_w1, hw, nh, F * F, p->g_conv_w[1]);
-        const float* gs = w->slab + S.gath;
-        J.add(gs, kGathW, kGathBlocks, p->n_rel[1], p->g_conv_rw[1], kOpRel, p->conv_rw[1]);
-        J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
+        if (!split) add_early_jobs(J, p, w, S);
         const int64_t pw = int64_t(K + 1) * F;
+        J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
         for (int t = 0; t < T; ++t) {
             const float* src = w->slab + S.proj + int64_t(t) * kBwdBlocks * pw;
             J.add(src, pw, kBwdBlocks, K * F, p->g_lin_w[t]);
             J.add(src + int64_t(K) * F, pw, kBwdBlocks, F, p->g_lin_b[t]);
         }
         J.add(w->slab + S.post0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
-        J.add(gs + F, kGathW, kGathBlocks, F, p->g_conv_b[0], kOpFix, nullptr, w->hub_terms);
-        J.add(gs + 2 * F, kGathW, kGathBlocks, F, p->g_ln_b[0], kOpFix, nullptr, w->hub_terms + F);
-        J.add(gs + 3 * F, kGathW, kGathBlocks, F, p->g_ln_w[0], kOpFix, nullptr,
-              w->hub_terms + 2 * F);
-        if (ad) {
-            AdamArgs& O = J.A.adam;
-            O.p = ad->param; O.m = ad->exp_avg; O.v = ad->exp_avg_sq; O.gbase = ad->grad_base;
-            O.n = ad->n;
-            O.lr = ad->lr; O.b1 = ad->beta1; O.b2 = ad->beta2; O.eps = ad->eps;
-            O.wd = ad->weight_decay; O.gscale = ad->grad_scale; O.step = ad->step; O.on = 1;
-        }
-        hipLaunchKernelGGL(finalize_kernel, dim3(J.blocks), dim3(kBlock), 0, stream, J.A);
+        launch_finalize(J, p, ad, stream);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

@@ -29,6 +29,7 @@ F32 = ctypes.c_float
 _SIG = {
     "regnn_abi_version": ([], ctypes.c_int),
     "regnn_gemm_x6_work_floats": ([I64, I64, I32], I64),
+    "regnn_copy2d_many": ([P, I32, P], ctypes.c_int),
     "regnn_wide_ln_fwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),
     "regnn_wide_ln_slab_rows": ([I64, I32], I64),
     "regnn_wide_ln_bwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),

@@ -492,6 +492,7 @@ class REGNN(torch.nn.Module):
         w_cat = torch.cat([lin.weight.t() for lin in lins], 0)                  # [T K, H]
         b_cat = torch.stack([lin.bias for lin in lins], 0)                      # [T, H]
         # (products on regnn_gemm_x6: fp32-accurate bf16x6 MFMA)
+        # (the T-wide products stay on hipBLASLt: measured faster there than a 128-row MFMA tile)
         w_c, b_c = ops.mm(w_cat, conv.weight), b_cat @ conv.weight
         n = blk.n_dst
         agg = ops.mm(S.view(n, T * K), w_c, torch.mm(w, b_c))

@@ -280,7 +280,7 @@ class _NsmWork(ctypes.Structure):
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
                 ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P),
                 ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML), ("part", ctypes.c_int32),
-                ("hub_acc", _P), ("hub_ticket", _P), ("hub_terms", _P)]
+                ("hub_acc", _P), ("hub_ticket", _P), ("hub_terms", _P), ("split_finalize", ctypes.c_int32)]
 
 # include/regnn_hip.h REGNN_CSC_LONG_*: hub rows of a <= 32768-edge block, their <= 1024-entry
 # pieces, and the csc_long buffer holding ids + piece table
@@ -348,6 +348,10 @@ FUSED_ADAM = {"mode": "on"}
 # "on": the pipelined trainer joins the sampler stream between the step's two parts (before
 # layer 0's backward); "off": after the whole step (A/B)
 SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
+# "on": several ranks all-reduce the gradients the two-layer step has final after layer 1's
+# transposed pass (early_grad_params, the bucket's head) on a comm stream while layer 0's
+# backward runs, the rest after the step; "off": one all-reduce of the whole bucket (A/B)
+SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "on")}
 # "on": the module path (device blocks) samples the next batch on a second stream while the
 # model trains on this one, as the fused step does; "off" (default: at hidden 512, mag-10x the
 # overlapped sampler slowed the dense kernels more than it hid, 1.045 -> 1.09 ms per step)
@@ -602,6 +606,15 @@ def _capturing(g):
     return torch.cuda.graph(g, capture_error_mode="thread_local")
 
 
+def early_grad_params(model):
+    """the parameters whose gradients the two-layer fused step has final after layer 1's
+    transposed pass (regnn_nsm_work.split_finalize: reduced at the end of part 1): out_lin,
+    layer 1 (weight, bias, relation table, LayerNorm) and layer 0's conv bias and LayerNorm."""
+    c0, c1 = model.convs[0], model.convs[1]
+    return [model.out_lin.weight, model.out_lin.bias, c1.weight, c1.bias, c1.relation_weight,
+            c1.norm.weight, c1.norm.bias, c0.bias, c0.norm.weight, c0.norm.bias]
+
+
 def _slab_floats(P, cap0):
     n = int(L._so.regnn_nsm_slab_floats(ctypes.addressof(P), int(cap0)))
     if n <= 0:
@@ -673,11 +686,25 @@ class NSTrainer:
                            getattr(model, "self_loop_type", None) == 2)
         self.params = [p for p in model.parameters() if p.requires_grad]
         # every parameter starts on a 16-byte boundary of the flat buckets (the fused step's
-        # finalize sums and steps 4 aligned elements per thread); the pad elements stay zero
-        self.offsets, o = [], 0
-        for p in self.params:
-            self.offsets.append(o)
+        # finalize sums and steps 4 aligned elements per thread); the pad elements stay zero.
+        # Two-layer fused step: the gradients final after layer 1's transposed pass lead the
+        # bucket ([0, n_early)), so several ranks all-reduce them while layer 0's backward runs.
+        why = fused_unsupported(model, x_dict)
+        early = []
+        if engine != "module" and why is None and len(model.convs) == 2:
+            ids = {id(p) for p in self.params}
+            early = [p for p in early_grad_params(model) if id(p) in ids]
+        eids = {id(p) for p in early}
+        order = early + [p for p in self.params if id(p) not in eids]
+        offs, o = {}, 0
+        for p in order:
+            offs[id(p)] = o
             o += (p.numel() + 3) // 4 * 4
+            if p is (early[-1] if early else None):
+                self.n_early = o
+        if not early:
+            self.n_early = 0
+        self.offsets = [offs[id(p)] for p in self.params]
         self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
         for p, o in zip(self.params, self.offsets):
             p.grad = self.flat[o:o + p.numel()].view_as(p)
@@ -695,7 +722,6 @@ class NSTrainer:
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in eight HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
-        why = fused_unsupported(model, x_dict)
         if engine == "fused" and why is not None:
             raise ValueError(f"fused NS step unavailable: {why}")
         self.fused = None
@@ -736,6 +762,15 @@ class NSTrainer:
         self.exchange_in_graph = False         # capture() sets it: the all-reduce is in the graphs
         # tests: all-reduce the bucket even with one rank (the captured-exchange path on one GPU)
         self._force_exchange = False
+        # several ranks, two-layer fused step: the bucket's early part is all-reduced on a comm
+        # stream between the step's two parts (split_finalize), the rest after the step
+        self._xsplit = False
+        self._comm = None
+        # False while the graphs hold no collective (several ranks, the exchange between graphs):
+        # the whole bucket then goes in one eager all-reduce after each replay
+        self._early_ok = True
+        if self.world > 1:
+            self._set_exchange_split()
         self.epoch = -1
         self.set_epoch(0)
 
@@ -812,14 +847,14 @@ class NSTrainer:
         # (the profiled eager steps of bench.py time the step as one event: unsplit)
         split = (self.ahead == 1 and fs.two_layer and SPLIT_JOIN["mode"] != "off" and
                  not profile_enabled())
-        fs.step(part=1 if split else 0)
+        self._fs_step(fs, part=1 if split else 0)
         with torch.cuda.stream(self._side):
             self._sample(nxt)
         # the join sits between layer 1's transposed pass and layer 0's backward (the sampler is
         # done by then): the next step's first kernel then waits on its own queue only
         cs.wait_stream(self._side)
         if split:
-            fs.step(part=2)
+            self._fs_step(fs, part=2)
 
     def _ahead_group(self, start, m, in_graph):
         """m <= ahead steps from slot `start` as one unit: the model trains slots
@@ -831,7 +866,7 @@ class NSTrainer:
         self._side.wait_stream(cs)
         # the model's launches first (captured first: the graph runs them on the launch queue)
         for i in range(m):
-            self.fused_slots[(start + i) % n].step()
+            self._fs_step(self.fused_slots[(start + i) % n])
             if in_graph:
                 self._exchange()
             self._opt_step()
@@ -863,7 +898,7 @@ class NSTrainer:
                 self._advance()
                 return
             self._sample(0)
-            self.fused.step()
+            self._fs_step(self.fused)
             return
         if self.pipelined:
             self._prime()
@@ -895,21 +930,57 @@ class NSTrainer:
                              self.local_node_idx)
             y = self.y_flat[n_id[:hops[0][2][1]]]
         loss = F.nll_loss(out, y)                     # mean over the batch's targets
-        # the gradients straight into the flat bucket: autograd.grad, then one multi-tensor copy
-        # (backward() would accumulate into the zeroed bucket views, one add kernel per
-        # parameter: ~80 us per step at hidden 512)
+        # the gradients straight into the flat bucket: autograd.grad, then one launch copying
+        # every gradient (some of them transposed views) into its bucket view (backward() would
+        # accumulate with one add kernel per parameter, and _foreach_copy_ / _foreach_add_
+        # lower to a kernel per tensor here: ~90 us per step at hidden 512)
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         with torch.no_grad():
             dst = [p.grad for p, g in zip(self.params, grads) if g is not None]
             src = [g for g in grads if g is not None]
             if dst:
-                torch._foreach_copy_(dst, src)
+                from . import ops
+                ops.copy_many(dst, src)
             self.loss.copy_(loss.detach())
+
+    def _set_exchange_split(self):
+        """the split exchange (two-layer fused step without the fused Adam): every slot's step
+        reduces the early gradients at the end of its part 1 (regnn_nsm_work.split_finalize)."""
+        if (self.fused is None or not self.fused.two_layer or self.adam_fused or
+                self.n_early <= 0 or SPLIT_EXCHANGE["mode"] == "off"):
+            return
+        self._xsplit = True
+        self._comm = torch.cuda.Stream(device=self.device)
+        for fs in (self.fused_slots if self.pipelined else [self.fused]):
+            fs.W.split_finalize = 1
+
+    def _fs_step(self, fs, part=0):
+        """the fused step's launches (part 0: both parts); with the split exchange the early
+        gradients' all-reduce is issued on the comm stream right after part 1."""
+        if not (self._xsplit and self._early_ok):
+            fs.step(part=part)
+            return
+        if part in (0, 1):
+            fs.step(part=1)
+            self._exchange_early()
+        if part in (0, 2):
+            fs.step(part=2)
+
+    def _exchange_early(self):
+        import torch.distributed as dist
+        cs = torch.cuda.current_stream(self.device)
+        self._comm.wait_stream(cs)
+        with torch.cuda.stream(self._comm):
+            dist.all_reduce(self.flat[:self.n_early], op=dist.ReduceOp.SUM)
 
     def _exchange(self):
         if self.world > 1 or self._force_exchange:
             import torch.distributed as dist
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+            if self._xsplit and self._early_ok:  # the early part went out after part 1
+                dist.all_reduce(self.flat[self.n_early:], op=dist.ReduceOp.SUM)
+                torch.cuda.current_stream(self.device).wait_stream(self._comm)
+            else:
+                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             if not isinstance(self.opt, FlatAdam):       # FlatAdam takes the mean itself
                 self.flat.div_(self.world)
 
@@ -1020,6 +1091,7 @@ class NSTrainer:
         """the eager warm-up steps (undone), then the graphs; warm: replay every multi-step
         graph once (_warm_graphs) -- capture() defers that until the ranks agreed."""
         multi = self.world > 1 or self._force_exchange
+        self._early_ok = not multi or bool(exchange_in_graph)
         if self.fused is None and not self._blocks_ok:
             raise ValueError("this model's module path reads exact-size adjs (a host sync per "
                              "step) and cannot be captured; run step() eagerly")
@@ -1170,6 +1242,7 @@ class NSTrainer:
             for fs in (self.fused_slots if self.pipelined else [self.fused]):
                 fs.adam = None
                 fs.W.adam = None
+        self._set_exchange_split()
 
     def param_vector(self):
         """the parameters in model order without the bucket's alignment pads."""

@@ -1545,10 +1545,10 @@ def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
 
 
 def gemm_x6_ok(*ts):
-    """the operands regnn_gemm_x6 takes: 2-D contiguous fp32 device tensors, every dimension a
-    multiple of 4 where it is a contiguous one (checked here for both layouts), 16-byte aligned."""
+    """the operands regnn_gemm_x6 takes: 2-D contiguous fp32 device tensors (rows of a multiple
+    of 4 floats on 16-byte boundaries load as vectors, any others per element)."""
     return all(t is not None and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and
-               t.is_contiguous() and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0 for t in ts)
+               t.is_contiguous() for t in ts)
 
 
 class _MMx6(torch.autograd.Function):
@@ -1576,6 +1576,67 @@ class _MMx6(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             gc = g.sum(0) if len(ctx.c_shape) == 1 else g
         return ga, gb, gc
+
+
+class _LinearX6(torch.autograd.Function):
+    """x @ w^T + bias (nn.Linear: w [N, K]) with regnn_gemm_x6 forward and backward: gx = g w,
+    gw = g^T x (w's own layout), gbias = the column sums of g."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        if bias is None:
+            out = gemm_x6(x, w, trans_b=True)
+        else:
+            out = bias.expand(x.shape[0], w.shape[0]).contiguous()
+            gemm_x6(x, w, trans_b=True, out=out, beta=1.0)
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = g.contiguous()
+        gx = gemm_x6(g, w) if ctx.needs_input_grad[0] else None
+        gw = gemm_x6(g, x, trans_a=True) if ctx.needs_input_grad[1] else None
+        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+class _Copy2d(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int64),
+                ("cols", ctypes.c_int64), ("s0", ctypes.c_int64), ("s1", ctypes.c_int64)]
+
+
+def copy_many(dst, src):
+    """dst[i].copy_(src[i]) for every pair in one launch (regnn_copy2d_many): fp32 device
+    tensors of <= 2 dims, dst contiguous, src any strides (e.g. a transposed weight gradient);
+    other pairs take copy_."""
+    descs = []
+    for d, s_ in zip(dst, src):
+        if (d.is_cuda and s_.is_cuda and d.dtype == s_.dtype == torch.float32 and
+                d.is_contiguous() and d.numel() == s_.numel() and s_.dim() <= 2 and
+                tuple(d.shape) == tuple(s_.shape)):
+            if s_.dim() == 2:
+                rows, cols, s0, s1 = s_.shape[0], s_.shape[1], s_.stride(0), s_.stride(1)
+            elif s_.dim() == 1:
+                rows, cols, s0, s1 = 1, s_.shape[0], 0, s_.stride(0)
+            else:
+                rows, cols, s0, s1 = 1, 1, 0, 0
+            descs.append(_Copy2d(s_.data_ptr(), d.data_ptr(), rows, cols, s0, s1))
+        else:
+            d.copy_(s_)
+    if descs:
+        arr = (_Copy2d * len(descs))(*descs)
+        L.call("regnn_copy2d_many", ctypes.addressof(arr), len(descs), L.stream())
+
+
+def linear(x, w, bias=None):
+    """nn.functional.linear on regnn_gemm_x6 when the operands allow it (else torch)."""
+    if (GEMM_X6["mode"] != "off" and x.dim() == 2 and gemm_x6_ok(x, w) and
+            (bias is None or (bias.is_cuda and bias.dtype == torch.float32 and bias.dim() == 1))):
+        return _LinearX6.apply(x, w, bias)
+    return torch.nn.functional.linear(x, w, bias)
 
 
 def mm(a, b, c=None):

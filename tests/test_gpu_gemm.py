@@ -17,7 +17,9 @@ def _ref(a, b, ta, tb):
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(5606, 512, 512), (100, 68, 36), (512, 512, 13312),
-                                   (64, 64, 32), (1, 4, 4), (333, 132, 1000)])
+                                   (64, 64, 32), (1, 4, 4), (333, 132, 1000),
+                                   (512, 349, 512), (349, 512, 512), (13312, 4, 512),
+                                   (4, 512, 13312)])
 def test_gemm_x6_layouts(ta, tb, M, N, K):
     from regnn_hip import ops
     g = torch.Generator(device=DEV).manual_seed(M + 7 * N + 13 * K)
@@ -102,3 +104,41 @@ def test_wide_ln_act_matches_autograd(H, dropout, res):
     for got, want in pairs:
         scale = max(1.0, float(want.abs().max()))
         assert float((got.double() - want).abs().max()) <= 2e-5 * scale
+
+
+def test_linear_x6_autograd_matches_fp64():
+    """ops.linear (out_lin: 349 classes, rows of 349 floats load per element) forward and
+    backward against fp64."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(512, 512, generator=g, device=DEV, requires_grad=True)
+    w = torch.randn(349, 512, generator=g, device=DEV, requires_grad=True)
+    bias = torch.randn(349, generator=g, device=DEV, requires_grad=True)
+    gout = torch.randn(512, 349, generator=g, device=DEV)
+    y = ops.linear(x, w, bias)
+    y.backward(gout)
+    x64, w64, g64 = x.detach().double(), w.detach().double(), gout.double()
+    checks = [(y, x64 @ w64.t() + bias.detach().double(), x64.abs() @ w64.abs().t()),
+              (x.grad, g64 @ w64, g64.abs() @ w64.abs()),
+              (w.grad, g64.t() @ x64, g64.abs().t() @ x64.abs())]
+    for got, ref, mag in checks:
+        err = (got.detach().double() - ref).abs()
+        assert (err <= 2e-6 * mag + 1e-6).all(), float((err / (mag + 1e-30)).max())
+    assert torch.allclose(bias.grad.double(), g64.sum(0), rtol=1e-5, atol=1e-5)
+
+
+def test_copy_many_strided_sources():
+    """ops.copy_many: one launch copying 2-D (some transposed), 1-D and 0-D sources into
+    contiguous destinations, bitwise."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(1)
+    srcs = [torch.randn(128, 512, generator=g, device=DEV).t(),
+            torch.randn(512, 512, generator=g, device=DEV),
+            torch.randn(349, generator=g, device=DEV),
+            torch.randn(64, 4, generator=g, device=DEV)[:, 1],
+            torch.randn((), device=DEV)]
+    srcs += [torch.randn(3, 5, generator=g, device=DEV) for _ in range(40)]   # > 32: 2 launches
+    dsts = [torch.full(tuple(s_.shape), float("nan"), device=DEV) for s_ in srcs]
+    ops.copy_many(dsts, srcs)
+    for d, s_ in zip(dsts, srcs):
+        assert torch.equal(d, s_)

@@ -102,13 +102,14 @@ def _union_worker(rank, world, port, q):
             s.set_seed(11, 0, 4)
             s.set_targets(targets)
             s.run_hops()
-            tr.fused.step()
+            tr._fs_step(tr.fused)              # (several ranks: the split exchange's first part)
             tr._exchange()
             tr._opt_step()
             torch.cuda.synchronize()
 
         tr = trainer(world, rank)
         assert tr.fused is not None and tr.fused.two_layer and not tr.adam_fused
+        assert tr._xsplit and 0 < tr.n_early < tr.flat.numel()
         assert tr.opt.grad_scale == 0.5
         one_step(tr, union[32 * rank:32 * (rank + 1)])
         out = {"grad_sum": tr.flat.cpu().numpy().copy(),
@@ -183,17 +184,30 @@ def _graph_allreduce_worker(port, q):
                              torch.arange(d["n_paper"], device="cuda"), d["x_dict"],
                              d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=9,
                              adam=dict(lr=1e-2))
-        ta, tb = make(), make()
+        from regnn_hip import ns
+        ta, tb, tc, td = make(), make(), make(), make()
         ta._force_exchange = True              # the RCCL all-reduce inside the captured graph
         ta.capture(warmup=1, exchange_in_graph=True)
         tb.capture(warmup=1)
-        assert ta.graphs[1] is None and ta.graph_groups
+        # the several-rank structure: split finalize, the early all-reduce on the comm stream
+        # between the step's parts, the rest after it, Adam as its own launch; td: the same
+        # without the split (one all-reduce of the whole bucket after the step)
+        tc.rehearse_exchange()
+        assert tc._xsplit and not tc.adam_fused
+        tc.capture(warmup=1, exchange_in_graph=True)
+        ns.SPLIT_EXCHANGE["mode"] = "off"
+        td.rehearse_exchange()
+        ns.SPLIT_EXCHANGE["mode"] = "on"
+        assert not td._xsplit and not td.adam_fused
+        td.capture(warmup=1, exchange_in_graph=True)
+        assert ta.graphs[1] is None and ta.graph_groups and tc.graph_groups
         out = []
         for k in (4, 1, 3):                    # a multi-step graph first, then single replays
-            ta.run_steps(k)
-            tb.run_steps(k)
+            for t in (ta, tb, tc, td):
+                t.run_steps(k)
             torch.cuda.synchronize()
-            out.append((float(ta.loss), float(tb.loss), bool(torch.equal(ta.pflat, tb.pflat))))
+            out.append((float(ta.loss), float(tb.loss), bool(torch.equal(ta.pflat, tb.pflat)),
+                        float(tc.loss) == float(td.loss) and bool(torch.equal(tc.pflat, td.pflat))))
         dist.destroy_process_group()
         q.put(out)
     except Exception as e:
@@ -214,8 +228,8 @@ def test_ns_allreduce_captured_in_step_graph():
     res = q.get(timeout=240)
     p.join(timeout=60)
     assert not isinstance(res, str), res
-    for la, lb, same in res:
-        assert la == lb and same
+    for la, lb, same, same_split in res:
+        assert la == lb and same and same_split
 
 
 def _fallback_worker(rank, world, port, q):
@@ -245,15 +259,17 @@ def _fallback_worker(rank, world, port, q):
         for mode in ("fallback", "eager"):
             tr = make()
             if mode == "fallback":
-                orig = tr._exchange
-
-                def exchange(orig=orig):
-                    if torch.cuda.is_current_stream_capturing():
-                        if rank == 1:
-                            raise RuntimeError("injected: all-reduce capture failed")
-                        return                  # rank 0: a captured collective's stand-in
-                    orig()
-                tr._exchange = exchange
+                def stub(orig):
+                    def exchange():
+                        if torch.cuda.is_current_stream_capturing():
+                            if rank == 1:
+                                raise RuntimeError("injected: all-reduce capture failed")
+                            return              # rank 0: a captured collective's stand-in
+                        orig()
+                    return exchange
+                # (the split exchange's early all-reduce too: the first collective of a step)
+                tr._exchange = stub(tr._exchange)
+                tr._exchange_early = stub(tr._exchange_early)
                 with warnings.catch_warnings(record=True) as wl:
                     warnings.simplefilter("always")
                     tr.capture(warmup=1, exchange_in_graph=True)

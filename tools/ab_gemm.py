@@ -32,7 +32,13 @@ def main():
                                      (512, 512, 13312, True, False, "dWc = S^T dA"),
                                      (512, 512, 512, False, False, "512^3"),
                                      (512, 349, 512, False, True, "out_lin"),
-                                     (5606, 512, 512, False, False, "n1=5606 fwd")]:
+                                     (5606, 512, 512, False, False, "n1=5606 fwd"),
+                                     (512, 512, 349, False, False, "out_lin gx"),
+                                     (349, 512, 512, True, False, "out_lin gw"),
+                                     (13312, 512, 4, False, False, "w @ b_c"),
+                                     (13312, 4, 512, False, True, "g b_c^T"),
+                                     (4, 512, 13312, True, False, "w^T g"),
+                                     (4, 512, 512, False, False, "b_cat @ W")]:
         a = torch.randn(*((K, M) if ta else (M, K)), device=dev)
         b = torch.randn(*((N, K) if tb else (K, N)), device=dev)
         if not (ops.gemm_x6_ok(a) and ops.gemm_x6_ok(b)):
