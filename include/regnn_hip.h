@@ -619,7 +619,8 @@ int regnn_ns_spmm_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel
  *   gx[u] = sum_{entries of u} rel_table[r] out_scale[v] g[v]      (every row u < cap_rows
  *           written once; rows u >= sizes[size_idx] (the batch's sources) get zeros)
  *   slab[b][r] (optional) = block b's partial of sum out_scale[v] <g[v], x[u]> over relation r
- *   (launches slab_rows blocks; reduce with regnn_rel_reduce; LDS float bins).
+ *   (launches slab_rows blocks; reduce with regnn_rel_reduce; LDS bins per row group, added in
+ *   entry order and summed in group order: bitwise reproducible).
  * sizes may be null (then every row < cap_rows is live). F in {64, 128, 256, 512, 1024, 2048}.
  * hub_work (optional, regnn_ns_csc_hub_work_floats(F) floats): the hub rows (csc_long's piece
  * table) are cut into chunks of (256 / min(64, F / 4)) * 8 entries, one workgroup each, and
@@ -648,9 +649,9 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
                        float* S, float* wsum, hipStream_t stream);
 
 /* Relation-table gradient of regnn_ns_typed_agg: slab[b][r] = block b's partial of
- * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (LDS float atomics: the
- * order within a block is run-dependent, as regnn_ns_spmm_bwd). Launches slab_rows blocks; reduce
- * the slab with regnn_rel_reduce. n_rel <= 256. */
+ * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (per row group bins added
+ * in entry order, the groups in a fixed order: bitwise reproducible). Launches slab_rows blocks;
+ * reduce the slab with regnn_rel_reduce. n_rel <= 256. */
 int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                            const int32_t* n_id, const int32_t* ntype, const int64_t* local,
                            const int32_t* e_type, const int64_t* e_off,

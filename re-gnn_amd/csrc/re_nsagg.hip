@@ -131,8 +131,9 @@ typed_agg_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __re
     }
 }
 
-// d tab[r] = sum_e <x_src_e, gS[v, t_e]> + gw[v, t_e]: per-block relation bins in LDS, one slab
-// row [n_rel] per block (the caller reduces the slab in a fixed order)
+// d tab[r] = sum_e <x_src_e, gS[v, t_e]> + gw[v, t_e]: relation bins per row group in LDS (lane 0
+// of the group adds its entries in order; the group rows summed in group order), one slab row
+// [n_rel] per block (the caller reduces the slab in a fixed order): bitwise reproducible
 template <int K, int NT>
 __global__ void __launch_bounds__(kBlock)
 typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __restrict__ rel,
@@ -141,10 +142,12 @@ typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* 
     constexpr int LPR = K / 4;
     constexpr int RPW = 64 / LPR;
     constexpr int UN = 4;
-    __shared__ float bins[256];
-    for (int r = threadIdx.x; r < n_rel; r += kBlock) bins[r] = 0.f;
+    constexpr int NG = kBlock / LPR;
+    __shared__ float gbins[NG][256];
+    for (int i = threadIdx.x; i < NG * 256; i += kBlock) gbins[i >> 8][i & 255] = 0.f;
     __syncthreads();
     const int lane = threadIdx.x & 63, l = lane % LPR, gl = lane - l;
+    float* bins = gbins[threadIdx.x / LPR];
     const int64_t rows_per_block = int64_t(kBlock / 64) * RPW;
     for (int64_t v0 = int64_t(blockIdx.x) * rows_per_block; v0 < n_rows;
          v0 += int64_t(gridDim.x) * rows_per_block) {
@@ -184,13 +187,17 @@ typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* 
                     float d = x[u].x * gg.x + x[u].y * gg.y + x[u].z * gg.z + x[u].w * gg.w;
                     d = group_sum<LPR>(d);
                     const float b = __shfl(gwl, gl + tt[u], 64);
-                    if (l == 0 && j + u < m) atomicAdd(bins + rr[u], d + b);
+                    if (l == 0 && j + u < m) bins[rr[u]] += d + b;
                 }
             }
         }
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < n_rel; r += kBlock) slab[int64_t(blockIdx.x) * n_rel + r] = bins[r];
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) {
+        float sr = 0.f;
+        for (int k = 0; k < NG; ++k) sr += gbins[k][r];
+        slab[int64_t(blockIdx.x) * n_rel + r] = sr;
+    }
 }
 
 }  // namespace nsagg

@@ -349,9 +349,13 @@ FUSED_ADAM = {"mode": "on"}
 # layer 0's backward); "off": after the whole step (A/B)
 SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
 # "on": several ranks all-reduce the gradients the two-layer step has final after layer 1's
-# transposed pass (early_grad_params, the bucket's head) on a comm stream while layer 0's
-# backward runs, the rest after the step; "off": one all-reduce of the whole bucket (A/B)
-SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "on")}
+# transposed pass (early_grad_params, the bucket's head) while layer 0's backward runs on a
+# forked stream, the rest after the step; "off" (default): one all-reduce of the whole bucket
+# after the step. Measured on one rank with the several-rank structure (REGNN_NS_FORCE_EXCHANGE,
+# mag-10x, hidden 64): 127.2 us split against 120.0 unsplit and 115.5 without an exchange -- the
+# extra reduction launch and the fork / join cost more than the overlap hides while a
+# collective's latency, not its bytes, sets its time
+SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
 # "on": the module path (device blocks) samples the next batch on a second stream while the
 # model trains on this one, as the fused step does; "off" (default: at hidden 512, mag-10x the
 # overlapped sampler slowed the dense kernels more than it hid, 1.045 -> 1.09 ms per step)
@@ -762,8 +766,8 @@ class NSTrainer:
         self.exchange_in_graph = False         # capture() sets it: the all-reduce is in the graphs
         # tests: all-reduce the bucket even with one rank (the captured-exchange path on one GPU)
         self._force_exchange = False
-        # several ranks, two-layer fused step: the bucket's early part is all-reduced on a comm
-        # stream between the step's two parts (split_finalize), the rest after the step
+        # several ranks, two-layer fused step: the bucket's early part is all-reduced between the
+        # step's two parts while part 2 runs on a forked stream (split_finalize), the rest after
         self._xsplit = False
         self._comm = None
         # False while the graphs hold no collective (several ranks, the exchange between graphs):
@@ -955,30 +959,32 @@ class NSTrainer:
             fs.W.split_finalize = 1
 
     def _fs_step(self, fs, part=0):
-        """the fused step's launches (part 0: both parts); with the split exchange the early
-        gradients' all-reduce is issued on the comm stream right after part 1."""
+        """the fused step's launches (part 0: both parts); with the split exchange, after part 1
+        the early gradients' all-reduce is issued on the launch stream while part 2 runs on a
+        forked stream (the collectives stay on the capture's origin stream; the next exchange
+        joins the fork)."""
         if not (self._xsplit and self._early_ok):
             fs.step(part=part)
             return
         if part in (0, 1):
             fs.step(part=1)
-            self._exchange_early()
         if part in (0, 2):
-            fs.step(part=2)
+            cs = torch.cuda.current_stream(self.device)
+            self._comm.wait_stream(cs)
+            self._exchange_early()
+            with torch.cuda.stream(self._comm):
+                fs.step(part=2)
 
     def _exchange_early(self):
         import torch.distributed as dist
-        cs = torch.cuda.current_stream(self.device)
-        self._comm.wait_stream(cs)
-        with torch.cuda.stream(self._comm):
-            dist.all_reduce(self.flat[:self.n_early], op=dist.ReduceOp.SUM)
+        dist.all_reduce(self.flat[:self.n_early], op=dist.ReduceOp.SUM)
 
     def _exchange(self):
         if self.world > 1 or self._force_exchange:
             import torch.distributed as dist
             if self._xsplit and self._early_ok:  # the early part went out after part 1
-                dist.all_reduce(self.flat[self.n_early:], op=dist.ReduceOp.SUM)
                 torch.cuda.current_stream(self.device).wait_stream(self._comm)
+                dist.all_reduce(self.flat[self.n_early:], op=dist.ReduceOp.SUM)
             else:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             if not isinstance(self.opt, FlatAdam):       # FlatAdam takes the mean itself

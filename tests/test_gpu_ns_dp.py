@@ -86,7 +86,9 @@ def _union_worker(rank, world, port, q):
         sys.path.insert(0, HERE)
         sys.path.insert(0, os.path.join(os.path.dirname(HERE), "re-gnn_amd"))
         from test_gpu_ns_engine import _mag
+        from regnn_hip import ns
         from regnn_hip.ns import NSTrainer
+        ns.SPLIT_EXCHANGE["mode"] = "on"       # the split exchange's gradients under the contract
         d = _mag(0.002, seed=8, F=128, hidden=64, classes=13, dropout=0.0)
         union = torch.randperm(d["n_paper"], generator=torch.Generator().manual_seed(0))[:64]
         union = union.to("cuda")
@@ -185,29 +187,26 @@ def _graph_allreduce_worker(port, q):
                              d["edge_type"], d["node_type"], d["local"], d["y"], 7, seed=9,
                              adam=dict(lr=1e-2))
         from regnn_hip import ns
-        ta, tb, tc, td = make(), make(), make(), make()
+        ta, tb, tc = make(), make(), make()
         ta._force_exchange = True              # the RCCL all-reduce inside the captured graph
         ta.capture(warmup=1, exchange_in_graph=True)
         tb.capture(warmup=1)
         # the several-rank structure: split finalize, the early all-reduce on the comm stream
-        # between the step's parts, the rest after it, Adam as its own launch; td: the same
-        # without the split (one all-reduce of the whole bucket after the step)
+        # between the step's parts, the rest after it, Adam as its own launch (regnn_adam_flat:
+        # equal to the fused Adam within rounding, test_fused_adam_equals_separate_adam)
+        ns.SPLIT_EXCHANGE["mode"] = "on"
         tc.rehearse_exchange()
         assert tc._xsplit and not tc.adam_fused
         tc.capture(warmup=1, exchange_in_graph=True)
-        ns.SPLIT_EXCHANGE["mode"] = "off"
-        td.rehearse_exchange()
-        ns.SPLIT_EXCHANGE["mode"] = "on"
-        assert not td._xsplit and not td.adam_fused
-        td.capture(warmup=1, exchange_in_graph=True)
         assert ta.graphs[1] is None and ta.graph_groups and tc.graph_groups
         out = []
         for k in (4, 1, 3):                    # a multi-step graph first, then single replays
-            for t in (ta, tb, tc, td):
+            for t in (ta, tb, tc):
                 t.run_steps(k)
             torch.cuda.synchronize()
             out.append((float(ta.loss), float(tb.loss), bool(torch.equal(ta.pflat, tb.pflat)),
-                        float(tc.loss) == float(td.loss) and bool(torch.equal(tc.pflat, td.pflat))))
+                        abs(float(tc.loss) - float(tb.loss)) <= 1e-5 * abs(float(tb.loss)) and
+                        bool(torch.allclose(tc.pflat, tb.pflat, rtol=1e-5, atol=1e-6))))
         dist.destroy_process_group()
         q.put(out)
     except Exception as e:
@@ -225,7 +224,7 @@ def test_ns_allreduce_captured_in_step_graph():
     port = 29500 + ((os.getpid() + 250) % 1000)
     p = ctx.Process(target=_graph_allreduce_worker, args=(port, q))
     p.start()
-    res = q.get(timeout=240)
+    res = q.get(timeout=150)
     p.join(timeout=60)
     assert not isinstance(res, str), res
     for la, lb, same, same_split in res:

@@ -198,3 +198,4 @@ def test_csc_gather_chunked_hubs_match(monkeypatch):
     for n in gb:
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
+
