@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 37). */
+/* ABI version (bumped on any signature or semantics change; currently 38). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -641,12 +641,15 @@ int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const 
  * hop's per-edge source node type and table row, regnn_ns_hop) the edge's type and row are read
  * from them and idx / n_id / ntype / local may be null. The caller projects
  * a = inv (S W_c + wsum b_c) + bias with W_c[t] = W_t^T W_0, b_c[t] = b_t W_0 (linearity).
- * K in {64, 128} fp32 (rows 16-byte aligned), 1 <= n_types <= 8, tables[t] non-null. */
+ * K in {64, 128} fp32 (rows 16-byte aligned), 1 <= n_types <= 8, tables[t] non-null. Row
+ * strides: S row v at S + v ld_s (ld_s >= n_types K, a multiple of 4, S 16-byte aligned), wsum row v
+ * at wsum + v ld_w (ld_w >= n_types): the caller can place wsum as S's last n_types columns
+ * (one [n][T K + T] operand, so the projection is one GEMM against [W_c; b_c]). */
 int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                        const float* rel_table, const int32_t* n_id, const int32_t* ntype,
                        const int64_t* local, const int32_t* e_type, const int64_t* e_off,
                        const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
-                       float* S, float* wsum, hipStream_t stream);
+                       float* S, float* wsum, int64_t ld_s, int64_t ld_w, hipStream_t stream);
 
 /* Relation-table gradient of regnn_ns_typed_agg: slab[b][r] = block b's partial of
  * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (per row group bins added
@@ -656,8 +659,8 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
                            const int32_t* n_id, const int32_t* ntype, const int64_t* local,
                            const int32_t* e_type, const int64_t* e_off,
                            const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
-                           const float* gS, const float* gw, float* slab, int32_t n_rel,
-                           int32_t slab_rows, hipStream_t stream);
+                           const float* gS, const float* gw, int64_t ld_s, int64_t ld_w,
+                           float* slab, int32_t n_rel, int32_t slab_rows, hipStream_t stream);
 
 
 /* ---------------------------------------------------------------------------------------

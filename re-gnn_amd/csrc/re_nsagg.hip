@@ -61,12 +61,13 @@ __device__ __forceinline__ void edge_meta(const EdgeSrc& E, const uint8_t* rel, 
     }
 }
 
-// S [n_rows][T][K], w [n_rows][T]. LPR = K / 4 lanes per row, 64 / LPR rows per wave.
+// S [n_rows][T][K] (row stride lds floats), w [n_rows][T] (row stride ldw). LPR = K / 4 lanes
+// per row, 64 / LPR rows per wave.
 template <int K, int NT>
 __global__ void __launch_bounds__(kBlock)
 typed_agg_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __restrict__ rel,
                  const float* __restrict__ tab, Tabs xt, int T, int64_t n_rows,
-                 float* __restrict__ S, float* __restrict__ wsum) {
+                 float* __restrict__ S, float* __restrict__ wsum, int64_t lds, int64_t ldw) {
     constexpr int LPR = K / 4;
     constexpr int RPW = 64 / LPR;
     constexpr int UN = 4;
@@ -117,7 +118,7 @@ typed_agg_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __re
                 }
             }
         }
-        float4* srow = reinterpret_cast<float4*>(S + v * int64_t(T) * K);
+        float4* srow = reinterpret_cast<float4*>(S + v * lds);
 #pragma unroll
         for (int k = 0; k < NT; ++k)
             if (k < T) srow[k * LPR + l] = acc[k];
@@ -126,7 +127,7 @@ typed_agg_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __re
 #pragma unroll
             for (int k = 1; k < NT; ++k)
                 if (l == k) s = ws[k];
-            wsum[v * T + l] = s;
+            wsum[v * ldw + l] = s;
         }
     }
 }
@@ -138,7 +139,8 @@ template <int K, int NT>
 __global__ void __launch_bounds__(kBlock)
 typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* __restrict__ rel,
                      Tabs xt, int T, int64_t n_rows, const float* __restrict__ gS,
-                     const float* __restrict__ gw, float* __restrict__ slab, int n_rel) {
+                     const float* __restrict__ gw, float* __restrict__ slab, int n_rel,
+                     int64_t lds, int64_t ldw) {
     constexpr int LPR = K / 4;
     constexpr int RPW = 64 / LPR;
     constexpr int UN = 4;
@@ -156,10 +158,10 @@ typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* 
         const int e0 = ptr[v], e1 = ptr[v + 1];
         if (e0 == e1) continue;
         float4 g[NT];
-        const float4* grow = reinterpret_cast<const float4*>(gS + v * int64_t(T) * K);
+        const float4* grow = reinterpret_cast<const float4*>(gS + v * lds);
 #pragma unroll
         for (int k = 0; k < NT; ++k) g[k] = k < T ? grow[k * LPR + l] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float gwl = l < T ? gw[v * T + l] : 0.f;
+        const float gwl = l < T ? gw[v * ldw + l] : 0.f;
         for (int c = e0; c < e1; c += LPR) {
             int mt, mr;
             int64_t mrow;
@@ -220,10 +222,13 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
                        const float* rel_table, const int32_t* n_id, const int32_t* ntype,
                        const int64_t* local, const int32_t* e_type, const int64_t* e_off,
                        const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
-                       float* S, float* wsum, hipStream_t stream) {
+                       float* S, float* wsum, int64_t ld_s, int64_t ld_w, hipStream_t stream) {
     EdgeSrc E;
     if (!ptr || !rel || !rel_table || !tables || !S || !wsum || n_types <= 0 || n_types > kMT ||
         n_rows < 0 || !edge_src(idx, n_id, ntype, local, e_type, e_off, E))
+        return REGNN_EINVAL;
+    if (ld_s < int64_t(n_types) * K || ld_s % 4 || reinterpret_cast<uintptr_t>(S) % 16 ||
+        ld_w < n_types)
         return REGNN_EINVAL;
     Tabs xt{};
     for (int t = 0; t < n_types; ++t) {
@@ -238,7 +243,8 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
 #define AGG_CASE(KK, N)                                                                        \
     if (K == KK && n_types <= N) {                                                             \
         hipLaunchKernelGGL((typed_agg_kernel<KK, N>), dim3((unsigned)grid), dim3(kBlock), 0,   \
-                           stream, ptr, E, rel, rel_table, xt, n_types, n_rows, S, wsum);      \
+                           stream, ptr, E, rel, rel_table, xt, n_types, n_rows, S, wsum, ld_s, \
+                           ld_w);                                                              \
         REGNN_LAUNCH_CHECK();                                                                  \
         return REGNN_OK;                                                                       \
     }
@@ -251,12 +257,15 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
                            const int32_t* n_id, const int32_t* ntype, const int64_t* local,
                            const int32_t* e_type, const int64_t* e_off,
                            const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
-                           const float* gS, const float* gw, float* slab, int32_t n_rel,
-                           int32_t slab_rows, hipStream_t stream) {
+                           const float* gS, const float* gw, int64_t ld_s, int64_t ld_w,
+                           float* slab, int32_t n_rel, int32_t slab_rows, hipStream_t stream) {
     EdgeSrc E;
     if (!ptr || !rel || !tables || !gS || !gw || !slab || n_types <= 0 || n_types > kMT ||
         n_rows < 0 || n_rel <= 0 || n_rel > 256 || slab_rows <= 0 ||
         !edge_src(idx, n_id, ntype, local, e_type, e_off, E))
+        return REGNN_EINVAL;
+    if (ld_s < int64_t(n_types) * K || ld_s % 4 || reinterpret_cast<uintptr_t>(gS) % 16 ||
+        ld_w < n_types)
         return REGNN_EINVAL;
     Tabs xt{};
     for (int t = 0; t < n_types; ++t) {
@@ -267,7 +276,7 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
     if (K == KK && n_types <= N) {                                                             \
         hipLaunchKernelGGL((typed_agg_bwd_kernel<KK, N>), dim3((unsigned)slab_rows),           \
                            dim3(kBlock), 0, stream, ptr, E, rel, xt, n_types, n_rows, gS, gw,  \
-                           slab, n_rel);                                                       \
+                           slab, n_rel, ld_s, ld_w);                                           \
         REGNN_LAUNCH_CHECK();                                                                  \
         return REGNN_OK;                                                                       \
     }

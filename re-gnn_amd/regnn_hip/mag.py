@@ -487,15 +487,16 @@ class REGNN(torch.nn.Module):
             return None
         T, K = len(tabs), int(tabs[0].shape[1])
         tab = F.leaky_relu(conv.relation_weight * conv.scaling_factor)          # :110-111
-        S, w = ops.ns_typed_agg(blk, tab, n_id, tabs, node_type, local_node_idx)
+        # [S | w]: the per-type sums and weight sums as one [n, T K + T] operand, so the
+        # projection S W_c + w b_c is one GEMM against [W_c; b_c] (products on regnn_gemm_x6:
+        # fp32-accurate bf16x6 MFMA; the small composition b_cat W_0 stays on hipBLASLt)
+        Sw = ops.ns_typed_agg(blk, tab, n_id, tabs, node_type, local_node_idx, ext=True)
         lins = [self.lins[str(t)] for t in range(T)]
         w_cat = torch.cat([lin.weight.t() for lin in lins], 0)                  # [T K, H]
         b_cat = torch.stack([lin.bias for lin in lins], 0)                      # [T, H]
-        # (products on regnn_gemm_x6: fp32-accurate bf16x6 MFMA)
-        # (the T-wide products stay on hipBLASLt: measured faster there than a 128-row MFMA tile)
         w_c, b_c = ops.mm(w_cat, conv.weight), b_cat @ conv.weight
         n = blk.n_dst
-        agg = ops.mm(S.view(n, T * K), w_c, torch.mm(w, b_c))
+        agg = ops.mm(Sw, torch.cat([w_c, b_c], 0))
         res = None
         if conv.residual:                                                       # :104,131-132
             x_t = self.group_input(x_dict, node_type, local_node_idx, n_id[:n])

@@ -654,15 +654,21 @@ def ns_spmm(blk, x, tab=None, bias=None):
 
 class _NsTypedAgg(torch.autograd.Function):
     """S[v, t] = sum_{e in v, type(src) = t} tab[rel_e] x_src (raw input rows read through n_id /
-    node type / local row), w[v, t] = sum of the same tab[rel_e] (regnn_ns_typed_agg); backward:
+    node type / local row), w[v, t] = sum of the same tab[rel_e] (regnn_ns_typed_agg), returned
+    as one [n_dst, T K + T] tensor [S | w] (ext) or as (S [n_dst, T, K], w [n_dst, T]); backward:
     the relation-table gradient only (the input tables are data, feats_type 3)."""
 
     @staticmethod
-    def forward(ctx, tab, blk, n_id, tables, node_type, local_idx):
+    def forward(ctx, tab, blk, n_id, tables, node_type, local_idx, ext):
         T, K = len(tables), int(tables[0].shape[1])
         dev = tables[0].device
-        S = torch.empty(blk.n_dst, T, K, dtype=torch.float32, device=dev)
-        w = torch.empty(blk.n_dst, T, dtype=torch.float32, device=dev)
+        if ext:
+            out = torch.empty(blk.n_dst, T * K + T, dtype=torch.float32, device=dev)
+            S_ptr, w_ptr, lds, ldw = L.ptr(out), L.ptr(out) + 4 * T * K, T * K + T, T * K + T
+        else:
+            S = torch.empty(blk.n_dst, T, K, dtype=torch.float32, device=dev)
+            w = torch.empty(blk.n_dst, T, dtype=torch.float32, device=dev)
+            S_ptr, w_ptr, lds, ldw = L.ptr(S), L.ptr(w), T * K, T
         t = tab.detach().float().contiguous()
         meta = getattr(blk, "edge_meta", None)
         if meta is not None:
@@ -678,30 +684,39 @@ class _NsTypedAgg(torch.autograd.Function):
         with timed("ns_typed_agg", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
             L.call("regnn_ns_typed_agg", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx), L.ptr(blk.rel),
                    L.ptr(t), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx), L.ptr(e_type),
-                   L.ptr(e_off), arr, T, K, blk.n_dst, L.ptr(S), L.ptr(w), L.stream())
+                   L.ptr(e_off), arr, T, K, blk.n_dst, S_ptr, w_ptr, lds, ldw, L.stream())
         ctx.blk, ctx.tables, ctx.idx = blk, tables, (n_id, node_type, local_idx, e_type, e_off)
-        ctx.n_rel, ctx.tab_shape = t.numel(), tab.shape
-        return S, w
+        ctx.n_rel, ctx.tab_shape, ctx.ext = t.numel(), tab.shape, bool(ext)
+        return out if ext else (S, w)
 
     @staticmethod
-    def backward(ctx, gS, gw):
+    def backward(ctx, *grads):
         if not ctx.needs_input_grad[0]:
-            return (None,) * 6
+            return (None,) * 7
         blk, tables = ctx.blk, ctx.tables
         n_id, node_type, local_idx, e_type, e_off = ctx.idx
         T, K = len(tables), int(tables[0].shape[1])
         dev = tables[0].device
-        gS = torch.zeros(blk.n_dst, T, K, device=dev) if gS is None else gS.contiguous().float()
-        gw = torch.zeros(blk.n_dst, T, device=dev) if gw is None else gw.contiguous().float()
+        if ctx.ext:
+            g = grads[0]
+            g = (torch.zeros(blk.n_dst, T * K + T, device=dev) if g is None
+                 else g.contiguous().float())
+            gS_ptr, gw_ptr, lds, ldw = L.ptr(g), L.ptr(g) + 4 * T * K, T * K + T, T * K + T
+        else:
+            gS, gw = grads
+            gS = (torch.zeros(blk.n_dst, T, K, device=dev) if gS is None
+                  else gS.contiguous().float())
+            gw = torch.zeros(blk.n_dst, T, device=dev) if gw is None else gw.contiguous().float()
+            gS_ptr, gw_ptr, lds, ldw = L.ptr(gS), L.ptr(gw), T * K, T
         rows = L.slab_rows()
         slab = torch.empty(rows, ctx.n_rel, dtype=torch.float32, device=dev)
         with timed("ns_typed_agg_bwd", blk.E * (4 * K + 13) + blk.n_dst * (T * 4 * K + 4 * T + 8)):
             L.call("regnn_ns_typed_agg_bwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
                    L.ptr(blk.rel), L.ptr(n_id), L.ptr(node_type), L.ptr(local_idx),
                    L.ptr(e_type), L.ptr(e_off),
-                   _ptr_array([L.ptr(x) for x in tables]), T, K, blk.n_dst, L.ptr(gS), L.ptr(gw),
-                   L.ptr(slab), ctx.n_rel, rows, L.stream())
-        return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None, None, None
+                   _ptr_array([L.ptr(x) for x in tables]), T, K, blk.n_dst, gS_ptr, gw_ptr,
+                   lds, ldw, L.ptr(slab), ctx.n_rel, rows, L.stream())
+        return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None, None, None, None
 
 
 _CAST_CACHE = {}
@@ -723,12 +738,13 @@ def _cached_cast(t, dtype):
     return out
 
 
-def ns_typed_agg(blk, tab, n_id, tables, node_type, local_idx):
+def ns_typed_agg(blk, tab, n_id, tables, node_type, local_idx, ext=False):
     """layer 0's sampled-block aggregation of the RAW input rows per source node type (the NS
     REGNN's group_input Linear and first conv weight moved after the mean by linearity,
     mag/regnn_ns.py:300-326 + mag/regnn_layers.py:101-148): returns S [n_dst, T, K] and the
-    per-type weight sums w [n_dst, T]; differentiable in tab."""
-    return _NsTypedAgg.apply(tab, blk, n_id, tables, node_type, local_idx)
+    per-type weight sums w [n_dst, T], or with ext one [n_dst, T K + T] tensor [S | w] (the
+    projection's single GEMM operand against [W_c; b_c]); differentiable in tab."""
+    return _NsTypedAgg.apply(tab, blk, n_id, tables, node_type, local_idx, bool(ext))
 
 
 def ns_typed_agg_ok(tables):

@@ -119,6 +119,16 @@ def test_typed_agg_against_fp64_sums():
     ((S64 * gS[:n_dst].double().cpu()).sum() + (w64 * gw[:n_dst].double().cpu()).sum()).backward()
     ok, err = G.close(rw.grad.cpu().numpy(), rw64.grad.numpy(), 1e-5)
     assert ok, err
+    # the [S | w] form (one strided operand): the same values, the same relation-table gradient
+    g_ref = rw.grad.clone()
+    rw.grad = None
+    tab = torch.nn.functional.leaky_relu(rw * 10.0)
+    Sw = ops.ns_typed_agg(blk, tab, n_id, tables, d["node_type"], d["local"], ext=True)
+    assert Sw.shape == (S.shape[0], 4 * 128 + 4)
+    assert torch.equal(Sw[:, :512], S.detach().reshape(S.shape[0], 512))
+    assert torch.equal(Sw[:, 512:], w.detach())
+    (Sw * torch.cat([gS.reshape(gS.shape[0], 512), gw], 1)).sum().backward()
+    assert torch.equal(rw.grad, g_ref)
 
 
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
