@@ -8,8 +8,13 @@ import numpy as np
 import pytest
 import torch
 
+import os
+
 import _golden as G
 
+if not os.path.exists(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                   "mag_regnn_init.npz")):
+    pytest.skip("fixture tests/golden/mag_regnn_init.npz absent", allow_module_level=True)
 D = G.load("mag_regnn_init")
 
 
