@@ -225,7 +225,10 @@ def test_pipelined_trainer_matches_unpipelined(monkeypatch, graph, engine):
         lp.append(float(tr_p.loss))
         lu.append(float(tr_u.loss))
     assert np.all(np.isfinite(lp))
-    assert np.allclose(lp, lu, rtol=1e-6, atol=1e-7), (lp, lu)
+    # the module path's small products run on hipBLASLt, which may pick another algorithm when
+    # captured than eagerly (ulp-level differences that Adam carries forward): 1e-5 there
+    tol = 1e-6 if fused else 1e-5
+    assert np.allclose(lp, lu, rtol=tol, atol=tol * 0.1), (lp, lu)
 
 
 def test_trainer_epoch_wraps_and_counts():
