@@ -25,7 +25,7 @@ def model_kernel(name):
 
 def per_step(disp):
     tot, per_k = 0.0, defaultdict(float)
-    steps = sum(1 for _, n, _ in disp if "regnn::nsm" in n and "agg0_kernel" in n)
+    steps = sum(1 for _, n, _ in disp if "regnn::nsm" in n and "agg0" in n and "kernel" in n)
     for _, n, v in disp:
         if model_kernel(n):
             tot += v
