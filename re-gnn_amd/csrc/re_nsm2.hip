@@ -775,12 +775,12 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
                 const float w0 = my_r0 < A.n_rel ? (tr0 > 0.f ? tr0 : 0.01f * tr0) : 0.f;
                 const float w1 = my_r1 < A.n_rel ? (tr1 > 0.f ? tr1 : 0.01f * tr1) : 0.f;
 #pragma unroll
-                for (int u = 0; u < UN; ++u) {     // predicated, not a break: a loop with a break
-                    if (u < m) {                   // is left rolled and x[] goes to scratch
-                        const float wt = __shfl(u < 16 ? w0 : w1, gl + (u & 15), 64);
-                        s0 = fmaf(wt, x[u].x, s0); s1 = fmaf(wt, x[u].y, s1);
-                        s2 = fmaf(wt, x[u].z, s2); s3 = fmaf(wt, x[u].w, s3);
-                    }
+                for (int u = 0; u < UN; ++u) {     // branch-free: a padding entry (a clamped
+                    // valid row) gets weight 0, which adds exact zeros
+                    const float ws = __shfl(u < 16 ? w0 : w1, gl + (u & 15), 64);
+                    const float wt = u < m ? ws : 0.f;
+                    s0 = fmaf(wt, x[u].x, s0); s1 = fmaf(wt, x[u].y, s1);
+                    s2 = fmaf(wt, x[u].z, s2); s3 = fmaf(wt, x[u].w, s3);
                 }
             }
         }
@@ -1090,12 +1090,12 @@ __device__ __forceinline__ RowIn row_in(const GathArgs& A, uint32_t key, int u, 
 
 // `m` entries of a segment starting at c (m <= 16, uniform over the group): fixed-point sums of
 // tab[r] GH[v] into acc and the relation dots into the block's bins
+// `my`: lane l's entry word of the chunk (l < m), loaded by the caller
 template <int UN>
-__device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab,
-                                             unsigned long long (&rb)[4], int c, int m, int l,
-                                             int gl, const RowIn& R,
-                                             unsigned long long (&acc)[4], bool& bad) {
-    const int my = l < m ? A.cent[c + l] : 0;
+__device__ __forceinline__ void gather_chunk_my(const GathArgs& A, const float* tab,
+                                                unsigned long long (&rb)[4], int my, int m, int l,
+                                                int gl, const RowIn& R,
+                                                unsigned long long (&acc)[4], bool& bad) {
     for (int j = 0; j < m; j += UN) {
         int pk[UN];
         float4 g[UN];
@@ -1107,7 +1107,9 @@ __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab
 #pragma unroll
         for (int u = 0; u < UN; ++u) {
             if (j + u >= m) continue;          // uniform over the group (continue: the loop
-                                               // unrolls, a break leaves g[] in scratch)
+                                               // unrolls, a break leaves g[] in scratch; a
+                                               // branch-free form computed the short rows'
+                                               // padding too: the gather 4.0 -> 6.2 us p50)
             const float t = tab[pk[u] & 255];
             acc[0] += to_fix_chk(t * g[u].x, bad);
             acc[1] += to_fix_chk(t * g[u].y, bad);
@@ -1126,6 +1128,15 @@ __device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab
             for (int k = 0; k < 4; ++k) rb[k] += mine && (r >> 4) == k ? dq : 0ull;
         }
     }
+}
+
+template <int UN>
+__device__ __forceinline__ void gather_chunk(const GathArgs& A, const float* tab,
+                                             unsigned long long (&rb)[4], int c, int m, int l,
+                                             int gl, const RowIn& R,
+                                             unsigned long long (&acc)[4], bool& bad) {
+    const int my = l < m ? A.cent[c + l] : 0;
+    gather_chunk_my<UN>(A, tab, rb, my, m, l, gl, R, acc, bad);
 }
 
 // the LayerNorm / relu / dropout backward of row u from its sums; G0 row to HBM, row terms
@@ -1216,9 +1227,18 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
             if (g1 > g0) gather_chunk<4>(A, tab, rb, e0 + g0, g1 - g0, l, gl, R, acc, bad);
         } else if (per <= 8) {
             if (g1 > g0) gather_chunk<8>(A, tab, rb, e0 + g0, g1 - g0, l, gl, R, acc, bad);
-        } else {
-            for (int e = g0; e < g1; e += kShort)                  // <= 64 entries: 4 chunks
-                gather_chunk<kShort>(A, tab, rb, e0 + e, min(kShort, g1 - e), l, gl, R, acc, bad);
+        } else {                               // <= 64 entries: up to 4 chunks, whose entry
+            int myk[4];                        // words are all requested first
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int ck = g0 + kShort * k, mk = min(kShort, g1 - ck);
+                myk[k] = mk > 0 && l < mk ? A.cent[e0 + ck + l] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int ck = g0 + kShort * k, mk = min(kShort, g1 - ck);
+                if (mk > 0) gather_chunk_my<kShort>(A, tab, rb, myk[k], mk, l, gl, R, acc, bad);
+            }
         }
         PG(j, 1);
 #pragma unroll
