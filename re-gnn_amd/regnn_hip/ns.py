@@ -285,7 +285,9 @@ class _NsmWork(ctypes.Structure):
 # include/regnn_hip.h REGNN_CSC_LONG_*: hub rows of a <= 32768-edge block, their <= 1024-entry
 # pieces, and the csc_long buffer holding ids + piece table
 _LONG_CAP = 32768 // 17 + 1
-_MAX_PIECE = 32768 // 1024 + _LONG_CAP
+_CSC_PIECE = 1024                     # include/regnn_hip.h REGNN_CSC_PIECE (256: measured no faster,
+#                                       the two-piece rows' ticket path cost what the split saved)
+_MAX_PIECE = 32768 // _CSC_PIECE + _LONG_CAP
 CSC_LONG_INTS = ((_LONG_CAP + 2) + 3) // 4 * 4 + 4 * _MAX_PIECE
 
 

@@ -570,7 +570,7 @@ NS_CSC = {"mode": "auto"}
 # "off": a workgroup per hub row
 NS_CSC_CHUNKED = {"mode": os.environ.get("REGNN_NS_CSC_CHUNKED", "on")}
 # include/regnn_hip.h REGNN_CSC_LONG_INTS (the sampler's csc_long with the hub piece table)
-CSC_LONG_INTS = ((32768 // 17 + 1 + 2) + 3) // 4 * 4 + 4 * (32768 // 1024 + 32768 // 17 + 1)
+CSC_LONG_INTS = ((32768 // 17 + 1 + 2) + 3) // 4 * 4 + 4 * (32768 // 1024 + 32768 // 17 + 1)  # PIECE 1024
 _HUB_WORK = {}
 
 
