@@ -680,7 +680,11 @@ struct GatFusedArgs {
 template <typename T, int LPR, int NV, bool CH>
 __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, LongPlan P) {
     constexpr int EV = Vec<T>::N;
+#ifdef REGNN_GATF_UN
+    constexpr int UN = NV <= 2 ? REGNN_GATF_UN : (NV <= 4 ? 4 : 2);
+#else
     constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);
+#endif
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     const int F = p.H * p.D;
