@@ -23,7 +23,12 @@ namespace gemm {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 128, BN = 128, BK = 32, RS = 40;
+// (BK 64 measured: 256 VGPRs and 3x slower; one LDS stage of BK 32 it is)
+#ifndef GEMM_BK
+#define GEMM_BK 32
+#endif
+constexpr int BM = 128, BN = 128, BK = GEMM_BK, RS = BK + 8;
+constexpr int NQ = BM * BK / 4 / 256;       // quads (row, 4 k) per thread per operand tile
 constexpr int kThreads = 256;
 constexpr int kStage = 3 * (BM + BN) * RS;       // bf16 of the LDS stage: A then B, 3 splits each
 
@@ -42,15 +47,15 @@ __device__ __forceinline__ void split3(float x, uint16_t& a, uint16_t& b, uint16
 template <bool KC>
 __device__ __forceinline__ void quad_rk(int i, int& r, int& k) {
     const int q = threadIdx.x + kThreads * i;
-    if constexpr (KC) { r = q >> 3; k = 4 * (q & 7); }
+    if constexpr (KC) { r = q / (BK / 4); k = 4 * (q % (BK / 4)); }
     else { r = q & 127; k = 4 * (q >> 7); }
 }
 
 template <bool KC, bool VEC>
 __device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t ld, int64_t r0,
-                                          int64_t nr, int64_t k0, int64_t K, float4 (&v)[4]) {
+                                          int64_t nr, int64_t k0, int64_t K, float4 (&v)[NQ]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NQ; ++i) {
         int r, k;
         quad_rk<KC>(i, r, k);
         const int64_t rr = r0 + r, kk = k0 + k;
@@ -86,9 +91,9 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t l
 
 // the tile's three bf16 splits into LDS [3][128][RS] (row = m or n, column = k): 8-byte writes
 template <bool KC>
-__device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float4 (&v)[4]) {
+__device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float4 (&v)[NQ]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NQ; ++i) {
         int r, k;
         quad_rk<KC>(i, r, k);
         const float x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -122,7 +127,7 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 va[4], vb[4];
+    float4 va[NQ], vb[NQ];
     int64_t kt = z;
     if (kt < nk) {
         load_tile<AKC, VEC>(A, lda, m0, M, kt * BK, K, va);
@@ -139,18 +144,20 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
             load_tile<AKC, VEC>(A, lda, m0, M, (kt + S) * BK, K, va);
             load_tile<BKC, VEC>(B, ldb, n0, N, (kt + S) * BK, K, vb);
         }
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks) {
         bf16x8_t b[4][3];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int s = 0; s < 3; ++s)
-                b[j][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * BN + 64 * wc + 16 * j + c) * RS + 8 * q);
+                b[j][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * BN + 64 * wc + 16 * j + c) * RS + 32 * ks + 8 * q);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             bf16x8_t a[3];
 #pragma unroll
             for (int s = 0; s < 3; ++s)
-                a[s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * BM + 64 * wr + 16 * i + c) * RS + 8 * q);
+                a[s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * BM + 64 * wr + 16 * i + c) * RS + 32 * ks + 8 * q);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {              // small products first
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
@@ -160,6 +167,7 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
             }
+        }
         }
     }
     // D lane (q, c): rows 4 q + r of the 16-row tile, column c
