@@ -1586,8 +1586,12 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     for (int a = 0; a < KB; ++a)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
-            *reinterpret_cast<float4*>(o + int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q) =
-                make_float4(acc[a][jb][0], acc[a][jb][1], acc[a][jb][2], acc[a][jb][3]);
+        {
+            const f32x4 v4 = acc[a][jb];
+            // non-temporal: the launch boundary after bwd0 measured 3.3 us instead of 4.6 (the
+            // same for agg0's per-type sums measured nothing)
+            __builtin_nontemporal_store(v4, reinterpret_cast<f32x4*>(o + int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q));
+        }
     if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
     if constexpr (RS) {
         if (threadIdx.x < F) {
