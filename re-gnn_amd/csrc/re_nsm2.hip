@@ -1062,7 +1062,10 @@ struct GathArgs {
     unsigned long long* hub_acc; int32_t* hub_ticket; unsigned long long* hub_terms;
 };
 
-static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 512);
+// 512 threads (32 row groups) per block: a hub piece's entries over 32 groups (a 439-entry row:
+// 14 per group instead of 28); 256 blocks keep the 8192 groups of the short rows
+constexpr int kGathT = 512, kGathG = kGathT / 16;
+static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 256);
 constexpr int kGathW = 4 * F;
 constexpr int kShort = 16;                 // = re_ns.hip kCscShort
 
@@ -1186,19 +1189,15 @@ __device__ __forceinline__ void hub_row_bwd(const GathArgs& A, int u, int l, con
 // in LDS. A row of one piece finishes there; a longer row's pieces store their sums to
 // hub_acc[j] and the piece that completes the row's ticket sums them (exact) and runs the row's
 // backward (device-scope fences: only for rows past 1024 entries).
-__global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
+__global__ void __launch_bounds__(kGathT) gather_kernel(GathArgs A) {
     __shared__ unsigned long long bins[F];
     __shared__ unsigned long long lgh[F];
     __shared__ float tab[F];
-    __shared__ float rt[3][16][F];
+    __shared__ float rt[3][kGathG][F];
     __shared__ int s_last;
     PH(2, 8);
     PE(2, 0);
-    const int j = int(gridDim.x) - 1 - int(blockIdx.x);    // this block's hub piece, if any
     const int n_piece = A.clong[REGNN_CSC_LONG_NPIECE];
-    const int4 pc = j < REGNN_CSC_LONG_MAXPIECE
-                        ? reinterpret_cast<const int4*>(A.clong + REGNN_CSC_LONG_TAB)[j]
-                        : make_int4(0, 0, 0, 0);
     if (threadIdx.x < F) {
         bins[threadIdx.x] = 0ull;
         lgh[threadIdx.x] = 0ull;
@@ -1214,15 +1213,17 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
     float sga[4] = {0.f, 0.f, 0.f, 0.f}, sgy[4] = {0.f, 0.f, 0.f, 0.f}, sgyx[4] = {0.f, 0.f, 0.f, 0.f};
     bool bad = false;                          // a fixed-point term out of range (to_fix_chk)
     unsigned long long rb[4] = {0ull, 0ull, 0ull, 0ull};   // relation bins l + 16 k (exact)
-    if (j < n_piece) {                         // block-uniform
+    // hub pieces j = grid - 1 - block, + grid, ... (block-uniform; usually one per block)
+    for (int j = int(gridDim.x) - 1 - int(blockIdx.x); j < n_piece; j += int(gridDim.x)) {
+        const int4 pc = reinterpret_cast<const int4*>(A.clong + REGNN_CSC_LONG_TAB)[j];
         const int u = pc.x, e0 = pc.y, cnt = pc.z;
         const int li = pc.w >> 16, k = (pc.w >> 8) & 255, npc = pc.w & 255;
         PG(j, 0);
         const RowIn R = row_in(A, key, u, l, lw, lb);
         unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
-        // the piece's entries in even shares over the 16 groups (a 48-entry row: 3 per group,
-        // not 16 on each of three); chunk width by the share (block-uniform)
-        const int per = (cnt + 15) >> 4, g0 = min(cnt, per * grp), g1 = min(cnt, g0 + per);
+        // the piece's entries in even shares over the 32 groups (a 64-entry row: 2 per group,
+        // not 16 on each of four); chunk width by the share (block-uniform)
+        const int per = (cnt + kGathG - 1) / kGathG, g0 = min(cnt, per * grp), g1 = min(cnt, g0 + per);
         if (per <= 4) {
             if (g1 > g0) gather_chunk<4>(A, tab, rb, e0 + g0, g1 - g0, l, gl, R, acc, bad);
         } else if (per <= 8) {
@@ -1278,9 +1279,12 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
                 }
             }
         }
+        __syncthreads();                       // lgh read; cleared for this block's next piece
+        if (threadIdx.x < F) lgh[threadIdx.x] = 0ull;
+        __syncthreads();
     }
     // ---- rows with <= kShort edges: one group each
-    for (int u = blockIdx.x * 16 + grp; u < n; u += gridDim.x * 16) {
+    for (int u = blockIdx.x * kGathG + grp; u < n; u += gridDim.x * kGathG) {
         const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
         if (m > kShort) continue;              // a hub: its pieces above
         const RowIn R = row_in(A, key, u, l, lw, lb);
@@ -1305,7 +1309,7 @@ __global__ void __launch_bounds__(kBlock) gather_kernel(GathArgs A) {
         const int which = threadIdx.x >> 6, f = threadIdx.x & 63;
         float sum = 0.f;
 #pragma unroll
-        for (int g = 0; g < 16; ++g) sum += rt[which][g][f];
+        for (int g = 0; g < kGathG; ++g) sum += rt[which][g][f];
         o[F + threadIdx.x] = sum;
     }
     PH(2, 9);
@@ -2104,7 +2108,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1]; G.alpha = p->alpha;
         G.g0 = w->ga[0]; G.slab = w->slab + S.gath;
         G.hub_acc = w->hub_acc; G.hub_ticket = w->hub_ticket; G.hub_terms = w->hub_terms;
-        hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kBlock), 0, stream, G);
+        hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kGathT), 0, stream, G);
         REGNN_LAUNCH_CHECK();
         if (split) {
             JobList J;
