@@ -1893,7 +1893,10 @@ struct JobList {
                 reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
                 reinterpret_cast<uintptr_t>(dst) % 16 == 0;
         const int cols = j.vec ? width / 4 : width;
-        j.cb = cols <= 8 ? 8 : cols <= 16 ? 16 : 32;
+        // wide jobs over many partial rows (bwd0's 128 per type): 16 columns x 16 groups per
+        // block, twice the blocks and half the partial rows per thread (107.7-108.7 against
+        // 108.5-108.7 us per step with 32 columns)
+        j.cb = cols <= 8 ? 8 : (cols <= 16 || (j.vec && nparts >= 64)) ? 16 : 32;
         blocks += (cols + j.cb - 1) / j.cb;
     }
     // out_lin.weight [C][64] = g^T h: g rows [rows][C], h rows [rows][64]; 4 blocks per 16 classes
