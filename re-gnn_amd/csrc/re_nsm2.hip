@@ -412,6 +412,12 @@ __global__ void __launch_bounds__(kBlock, 2) agg0_kernel(Agg0Args A) {
 // capacity's 832) is resident at once; stage 1's eight waves split the node types in two halves
 // whose partial products meet in LDS in a fixed order. Same outputs as agg0_kernel<128, ..>.
 constexpr int kAggW = 512;
+// rows of a tile (<= 16: the MFMA tiles stay 16 rows, the rest are padding). 12 / 14 rows (more,
+// lighter tiles for the CUs that hold two) measured 109.1-109.8 / 107.4-108.4 against 107.9 us
+#ifndef REGNN_AGG_ROWS
+#define REGNN_AGG_ROWS 16
+#endif
+constexpr int kAggRows = REGNN_AGG_ROWS;
 
 inline size_t agg0w_lds(int T) {          // St [16][T K + 4] | sw [16][MT] | Pt [16][68] |
     return (size_t(16) * (T * 128 + 4) + 16 * MT + 16 * 68 + 16 * F + 16 * F) * sizeof(float);
@@ -449,12 +455,13 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
             *A.nvalid = float(t);
         }
     }
-    const int base = blockIdx.x * 16;
+    const int base = blockIdx.x * kAggRows;
     if (base >= n) return;                 // block-uniform (the grid is capacity-sized)
     // the relation table in registers of every lane (n_rel <= 64), read by shuffles
     const float tabw = rel_tab(A.rw, A.n_rel, A.alpha, lane);
     // ---- gather: per-type register sums of this lane's 4 features of row v
     const int v = base + sub;
+    const bool rv = sub < kAggRows && v < n;   // a row of this tile and of the batch
     float wsum[NT];
     float4 racc[NT];
     int rel_t[NT];
@@ -467,7 +474,7 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
         racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     int e0 = 0, e1 = 0;
-    if (v < n) row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
+    if (rv) row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
     for (int c0 = e0; c0 < e1; c0 += 32) {
         const int m = min(32, e1 - c0);
         int my_t = 0, my_lo = 0, my_r = 0;  // table rows < 2^31 (checked by the host)
@@ -544,11 +551,11 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
                 sv = make_float4(fmaf(ws, xself.x, wr * sv.x), fmaf(ws, xself.y, wr * sv.y),
                                  fmaf(ws, xself.z, wr * sv.z), fmaf(ws, xself.w, wr * sv.w));
             *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l) = sv;
-            if (v < n)
+            if (rv)
                 *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l) = racc[tt];
             if (l == 0) {
                 sw[sub * MT + tt] = RS ? fmaf(wr, wsum[tt], ws) : wsum[tt];
-                if (v < n) {
+                if (rv) {
                     A.s_w[int64_t(v) * T + tt] = wsum[tt];
                     if constexpr (RS) A.u_rel[int64_t(v) * (T + 1) + tt] = rel_t[tt];
                 }
@@ -556,7 +563,7 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
         }
     }
     if constexpr (RS) {
-        if (v < n) {
+        if (rv) {
             *reinterpret_cast<float4*>(A.u_self + int64_t(v) * K + 4 * l) = xself;
             if (l == 0) A.u_rel[int64_t(v) * (T + 1) + T] = r_self;
         }
@@ -570,7 +577,8 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) w0c[4 * b + i] = A.w0[(16 * b + 4 * q + i) * F + 16 * w + c];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) iv4[r] = base + 4 * q + r < n ? A.inv[base + 4 * q + r] : 0.f;
+        for (int r = 0; r < 4; ++r)
+            iv4[r] = 4 * q + r < kAggRows && base + 4 * q + r < n ? A.inv[base + 4 * q + r] : 0.f;
         bj = A.bias[16 * w + c];
     }
     __syncthreads();
@@ -643,7 +651,7 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
     if (threadIdx.x < kBlock) {
         const int l16 = threadIdx.x & 15, s16 = threadIdx.x >> 4;
         const int vv = base + s16;
-        if (vv < n) {
+        if (s16 < kAggRows && vv < n) {
             const float4 gw = reinterpret_cast<const float4*>(A.ln_w)[l16];
             const float4 gb = reinterpret_cast<const float4*>(A.ln_b)[l16];
             *reinterpret_cast<float4*>(A.p + int64_t(vv) * F + 4 * l16) =
@@ -2051,6 +2059,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         A.n_id = w->n_id; A.labels = w->labels; A.nvalid = w->nvalid;
         int grid = (w->cap[h] + 15) / 16;
         if (K == 128 && T <= 4 && !getenv("REGNN_NSM_AGG0_OLD")) {  // every tile its own block
+            grid = (w->cap[h] + kAggRows - 1) / kAggRows;
             const size_t lds = agg0w_lds(T);
 #define AGG0W_CASE(NN, RS)                                                                     \
             if (rs == RS) {                                                                    \
