@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 39). */
+/* ABI version (bumped on any signature or semantics change; currently 40). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -305,8 +305,12 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
 int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                         const float* ee_table, const float* el, const float* er, const void* x,
                         void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
-                        int32_t dtype, const regnn_seg_plan* plan,
+                        int32_t dtype, const float* attn_l, const regnn_seg_plan* plan,
                         hipStream_t stream);  /* partial width H*D + 2H */
+/* attn_l ([H, D] fp32, may be NULL): with fp32 rows, D % 4 == 0 and D / 4 a power of two the
+ * kernel re-forms el[u] from the row it gathers (regnn_attn_dots_fwd's summation order, so
+ * bitwise the el passed) instead of reading el: one random access per edge instead of two.
+ * el must then be regnn_attn_dots_fwd(x, attn_l, ...)'s. */
 
 /* The attention a[e,h] = exp(e[h] - lse[v,h]) (CSR edge order) of regnn_gat_fused_fwd, re-formed
  * for the backward. H a power of two <= 32. */

@@ -670,20 +670,41 @@ struct GatFusedArgs {
     const void* x;
     void* out;
     float* lse;
+    const float* al;    // attn_l [H, D] (ELX kernels: el re-formed from the gathered row)
     int64_t n_seg;
     int H, D;
     float slope;
 };
 
+// el[u,h] as attn_dots_fwd_vec forms it: lane l of the head's D/4 lanes takes x[u,h,4l..4l+3]
+// (an fmaf chain from 0), then an xor butterfly over the D/4 lanes (every lane ends with the same
+// sum). The ELX forward forms it from the row it already holds, so each edge makes one random
+// access (the row) instead of two (the row and el[u], 32 B of another array): bitwise the el the
+// backward re-forms the attention from.
+__device__ __forceinline__ float head_dot4(const float (&v)[4], const float (&a)[4], int dl) {
+    float d = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) d = fmaf(v[t], a[t], d);
+    for (int o = dl >> 1; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    return d;
+}
+
+// attn_dots_fwd in the order head_dot4 uses: D % 4 == 0 and D / 4 a power of two <= 64
+inline bool attn_dots_vec_ok(int D) {
+    const int dl = D / 4;
+    return D > 0 && D % 4 == 0 && dl <= 64 && (dl & (dl - 1)) == 0;
+}
+
 // CH: the units are the chunks of long segments (partial rows [acc | max | sum], unnormalised);
 // otherwise the segments, long ones skipped.
-template <typename T, int LPR, int NV, bool CH>
+template <typename T, int LPR, int NV, bool CH, bool ELX>
 __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, LongPlan P) {
     constexpr int EV = Vec<T>::N;
+    static_assert(!ELX || EV == 4, "ELX: fp32 rows");
 #ifdef REGNN_GATF_UN
     constexpr int UN = NV <= 2 ? REGNN_GATF_UN : (NV <= 4 ? 4 : 2);
 #else
-    constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);
+    constexpr int UN = NV <= 4 ? 4 : 2;    // 8 rows for NV <= 2: 25.5 / 18.2 ms against 24.7 / 17.2
 #endif
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
@@ -704,6 +725,7 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, L
         }
         float acc[NV][EV] = {};
         float m[NV], s[NV], erv[NV];
+        float alv[ELX ? NV : 1][4];
         int head[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -712,6 +734,10 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, L
             erv[q] = p.er[seg * p.H + head[q]];
             m[q] = -INFINITY;
             s[q] = 0.f;
+            if constexpr (ELX) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) alv[q][t] = o < F ? p.al[o + t] : 0.f;
+            }
         }
         for (int e0 = beg; e0 < end; e0 += LPR) {
             const int e = e0 + lane;
@@ -734,9 +760,13 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, L
                         const int o = (q * LPR + lane) * EV;
                         if (o < F) {
                             Vec<T>::load(src + (int64_t)jj * F + o, v[u][q]);
-                            float z = p.el[(int64_t)jj * p.H + head[q]] + erv[q];
-                            if (p.ee) z += p.ee[rr * p.H + head[q]];
-                            sc[u][q] = lrelu(z, p.slope);
+                            if constexpr (ELX) {       // the relation bias; el once the row is in
+                                sc[u][q] = p.ee ? p.ee[rr * p.H + head[q]] : 0.f;
+                            } else {
+                                float z = p.el[(int64_t)jj * p.H + head[q]] + erv[q];
+                                if (p.ee) z += p.ee[rr * p.H + head[q]];
+                                sc[u][q] = lrelu(z, p.slope);
+                            }
                         } else {
 #pragma unroll
                             for (int t = 0; t < EV; ++t) v[u][q][t] = 0.f;
@@ -747,6 +777,14 @@ __global__ void __launch_bounds__(kBlock) gat_fused_fwd_kernel(GatFusedArgs p, L
 #pragma unroll
                 for (int u = 0; u < UN; ++u) {
                     if (k0 + u >= cnt) break;
+                    if constexpr (ELX) {
+#pragma unroll
+                        for (int q = 0; q < NV; ++q) {
+                            float z = head_dot4(v[u][q], alv[q], p.D >> 2) + erv[q];
+                            if (p.ee) z += sc[u][q];
+                            sc[u][q] = lrelu(z, p.slope);
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < NV; ++q) {
                         const float d = sc[u][q] - m[q];
@@ -838,15 +876,31 @@ int dispatch_gat_fused(GatFusedArgs p, const regnn_seg_plan* pl, hipStream_t str
     if (p.D <= 0 || p.D % EV || p.H <= 0) return REGNN_EUNSUPPORTED;
     const int nvec = F / EV;
     const LongPlan P = long_plan(pl);
+#ifdef REGNN_GATF_NO_ELX
+    p.al = nullptr;
+#endif
 #define REGNN_GATF(LPR, NV)                                                                   \
     if (nvec <= (LPR) * (NV)) {                                                               \
-        hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, false>),                         \
-                           dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, p, P); \
+        const bool elx = std::is_same<T, float>::value && p.al && attn_dots_vec_ok(p.D) &&    \
+                         p.D / 4 <= (LPR);                                                    \
+        if (elx)                                                                              \
+            hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, false, EV == 4>),            \
+                               dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, \
+                               p, P);                                                         \
+        else                                                                                  \
+            hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, false, false>),              \
+                               dim3(grid_for(p.n_seg, kBlock / (LPR))), dim3(kBlock), 0, stream, \
+                               p, P);                                                         \
         REGNN_LAUNCH_CHECK();                                                                 \
         if (P.n_chunk > 0) {                                                                  \
-            hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, true>),                      \
-                               dim3(grid_for(P.n_chunk, kBlock / (LPR))), dim3(kBlock), 0, stream, \
-                               p, P);                                                         \
+            if (elx)                                                                          \
+                hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, true, EV == 4>),         \
+                                   dim3(grid_for(P.n_chunk, kBlock / (LPR))), dim3(kBlock), 0, \
+                                   stream, p, P);                                             \
+            else                                                                              \
+                hipLaunchKernelGGL((gat_fused_fwd_kernel<T, LPR, NV, true, false>),           \
+                                   dim3(grid_for(P.n_chunk, kBlock / (LPR))), dim3(kBlock), 0, \
+                                   stream, p, P);                                             \
             const int64_t base = run_tree(pl, 1, F + 2 * p.H, F, p.H, p.D, stream);           \
             hipLaunchKernelGGL(seg_emit_softmax<T>, dim3(long_grid(P.n_long)), dim3(kBlock),  \
                                0, stream, P.part, P.chunk_off, base, pl->n_levels, P.long_ids, \
@@ -892,6 +946,35 @@ attn_dots_fwd_kernel(const float* __restrict__ ft, const float* __restrict__ al,
             sl += __shfl_xor(sl, o, G);
             sr += __shfl_xor(sr, o, G);
         }
+        if (lane == 0) {
+            el[t] = sl;
+            er[t] = sr;
+        }
+    }
+}
+
+// The same dots in head_dot4's order (D % 4 == 0, D / 4 a power of two <= 64): D / 4 lanes per
+// (node, head), lane l the fmaf chain over d = 4l..4l+3, then the xor butterfly. The fused GAT
+// forward re-forms el from its gathered rows in exactly this order.
+__global__ void __launch_bounds__(kBlock)
+attn_dots_fwd_vec_kernel(const float* __restrict__ ft, const float* __restrict__ al,
+                         const float* __restrict__ ar, int64_t N, int H, int D,
+                         float* __restrict__ el, float* __restrict__ er) {
+    const int dl = D >> 2;
+    const int lane = threadIdx.x & (dl - 1);
+    const int64_t total = N * H, per_block = kBlock / dl;
+    for (int64_t t = (int64_t)blockIdx.x * per_block + threadIdx.x / dl; t < total;
+         t += (int64_t)gridDim.x * per_block) {
+        const int h = int(t % H);
+        const float* __restrict__ x = ft + t * D + 4 * lane;
+        float v[4], a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] = x[i];
+            a[i] = al[h * D + 4 * lane + i];
+            b[i] = ar[h * D + 4 * lane + i];
+        }
+        const float sl = head_dot4(v, a, dl), sr = head_dot4(v, b, dl);
         if (lane == 0) {
             el[t] = sl;
             er[t] = sr;
@@ -1090,13 +1173,14 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
 int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* rel,
                         const float* ee_table, const float* el, const float* er, const void* x,
                         void* out, float* lse, int64_t n_seg, int32_t H, int32_t D, float slope,
-                        int32_t dtype, const regnn_seg_plan* plan, hipStream_t stream) {
+                        int32_t dtype, const float* attn_l, const regnn_seg_plan* plan,
+                        hipStream_t stream) {
     if (!ptr || !idx || !el || !er || !x || !out || !lse || n_seg < 0 || (ee_table && !rel))
         return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, int64_t(H) * D + 2 * H)) return rc;
     if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
-    GatFusedArgs p{ptr, idx, rel, ee_table, el, er, x, out, lse, n_seg, H, D, slope};
+    GatFusedArgs p{ptr, idx, rel, ee_table, el, er, x, out, lse, attn_l, n_seg, H, D, slope};
     if (dtype == REGNN_F32) return dispatch_gat_fused<float>(p, plan, stream);
     if (dtype == REGNN_BF16) return dispatch_gat_fused<bf16_t>(p, plan, stream);
     return REGNN_EUNSUPPORTED;
@@ -1186,8 +1270,12 @@ int regnn_attn_dots_fwd(const float* ft, const float* attn_l, const float* attn_
                         int32_t H, int32_t D, float* el, float* er, hipStream_t stream) {
     if (!ft || !attn_l || !attn_r || !el || !er || N < 0 || H <= 0 || D <= 0) return REGNN_EINVAL;
     if (N == 0) return REGNN_OK;
-    hipLaunchKernelGGL(attn_dots_fwd_kernel, dim3(grid_for(N * H, kBlock / kDotGroup)),
-                       dim3(kBlock), 0, stream, ft, attn_l, attn_r, N, H, D, el, er);
+    if (attn_dots_vec_ok(D))
+        hipLaunchKernelGGL(attn_dots_fwd_vec_kernel, dim3(grid_for(N * H, kBlock / (D / 4))),
+                           dim3(kBlock), 0, stream, ft, attn_l, attn_r, N, H, D, el, er);
+    else
+        hipLaunchKernelGGL(attn_dots_fwd_kernel, dim3(grid_for(N * H, kBlock / kDotGroup)),
+                           dim3(kBlock), 0, stream, ft, attn_l, attn_r, N, H, D, el, er);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }

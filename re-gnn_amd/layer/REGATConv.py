@@ -69,7 +69,7 @@ class REGATConv(nn.Module):
             rst = ops.head_spmm(rg, a, ft)                                         # :90-92
         else:
             # no attention dropout: scores, softmax and aggregation in one pass (:80-92)
-            rst = ops.gat_fused(rg, el, er, ft, tab, pack, slope)
+            rst = ops.gat_fused(rg, el, er, ft, tab, pack, slope, attn_l=self.attn_l)
         if self.res_fc is not None:
             resval = self.res_fc(h).view(h.shape[0], -1, self.out_feats)           # :94-96
             rst = rst + resval

@@ -76,7 +76,7 @@ _SIG = {
     "regnn_gat_softmax_bwd": ([P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, I32, P, P],
                               ctypes.c_int),
     "regnn_spmm_heads_fwd": ([P, P, P, P, P, P, I64, I32, I32, I32, P, P], ctypes.c_int),
-    "regnn_gat_fused_fwd": ([P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I32, P, P],
+    "regnn_gat_fused_fwd": ([P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I32, P, P, P],
                             ctypes.c_int),
     "regnn_gat_attn_lse": ([P, P, P, P, P, P, P, I64, I32, F32, P, P, P], ctypes.c_int),
     "regnn_spmm_heads_bwd": ([P, P, P, P, P, P, P, P, I64, I32, I32, I32, P, P], ctypes.c_int),
@@ -123,7 +123,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 39
+ABI_VERSION = 40
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

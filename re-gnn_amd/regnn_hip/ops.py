@@ -1029,9 +1029,10 @@ class _GatFused(torch.autograd.Function):
     (regnn_gat_attn_lse) and runs the unfused backward kernels."""
 
     @staticmethod
-    def forward(ctx, el, er, ee_tab, ft, rg, pack, slope):
+    def forward(ctx, el, er, ee_tab, ft, rg, pack, slope, attn_l):
         N, H, D = ft.shape
         el, er, ft = el.contiguous().float(), er.contiguous().float(), ft.contiguous()
+        al = None if attn_l is None else attn_l.detach().reshape(H, D).float().contiguous()
         t = None if ee_tab is None else ee_tab.detach().float().contiguous()
         rel = pack.rel_csr if t is not None else None
         out = torch.empty(rg.n_dst, H, D, dtype=ft.dtype, device=ft.device)
@@ -1042,7 +1043,7 @@ class _GatFused(torch.autograd.Function):
             gp = _GatPlan(getattr(rg, "csr_plan", None), H * D + 2 * H, ft.device)
             L.call("regnn_gat_fused_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(rel),
                    L.ptr(t), L.ptr(el), L.ptr(er), L.ptr(ft), L.ptr(out), L.ptr(lse), rg.n_dst, H,
-                   D, float(slope), L.dtype_code(ft), gp.ptr, L.stream())
+                   D, float(slope), L.dtype_code(ft), L.ptr(al), gp.ptr, L.stream())
         ctx.rg, ctx.pack, ctx.slope = rg, pack, slope
         ctx.tab_shape = None if ee_tab is None else ee_tab.shape
         ctx.save_for_backward(el, er, t, ft, lse)
@@ -1084,16 +1085,18 @@ class _GatFused(torch.autograd.Function):
         L.call("regnn_segment_sum", L.ptr(rg.csc_ptr), L.ptr(rg.csc2csr), L.ptr(gs), rg.n_src, H,
                L.ptr(gel), gq.ptr, L.stream())
         g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if slab is not None else None
-        return gel, ger, g_tab, gft, None, None, None
+        return gel, ger, g_tab, gft, None, None, None, None
 
 
-def gat_fused(rg, el, er, ft, ee_tab=None, pack=None, slope=0.2):
+def gat_fused(rg, el, er, ft, ee_tab=None, pack=None, slope=0.2, attn_l=None):
     """layer/REGATConv.py:80-92 without attention dropout, as one fused forward pass (H a power of
-    two <= 32; otherwise the unfused gat_attention + head_spmm)."""
+    two <= 32; otherwise the unfused gat_attention + head_spmm). With attn_l (el then being
+    attn_dots(ft, attn_l, ...)'s) the kernel re-forms el from the rows it gathers, bitwise the
+    same, instead of reading it per edge (fp32 rows, D / 4 a power of two)."""
     H = ft.shape[1]
     if H & (H - 1) or H > 32:
         return head_spmm(rg, gat_attention(rg, el, er, ee_tab, pack, slope), ft)
-    return _GatFused.apply(el, er, ee_tab, ft, rg, pack, slope)
+    return _GatFused.apply(el, er, ee_tab, ft, rg, pack, slope, attn_l)
 
 
 def head_spmm(rg, a, ft):

@@ -122,3 +122,46 @@ def test_gat_long_rows_vs_fp64(fused):
     for name, a, b in zip(["out", "g_ft", "g_el", "g_er", "g_tab"], got, want):
         err = (a.double() - b).abs().max().item() / _rel(b)
         assert err <= 1e-5, f"{name}: rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("H,D,hub", [(8, 64, False), (8, 64, True), (4, 16, False), (2, 8, True),
+                                     (8, 32, False), (4, 4, False), (2, 128, False),
+                                     (2, 256, False)])
+def test_gat_fused_el_reformed_bitwise(H, D, hub):
+    """attn_l passed: the forward re-forms el from the gathered rows (regnn_attn_dots_fwd's
+    summation order) instead of reading it; outputs and gradients bitwise those of the el-reading
+    kernel (D = 128 on 16-lane rows: the el-reading kernel runs either way)."""
+    from regnn_hip import ops
+    rg, e_feat = (_hub_graph() if hub else _graph())
+    N = rg.n_dst
+    g = torch.Generator(device=DEV).manual_seed(5)
+    ft0 = torch.randn(N, H, D, generator=g, device=DEV)
+    al0 = torch.randn(1, H, D, generator=g, device=DEV) * 0.3
+    ar0 = torch.randn(1, H, D, generator=g, device=DEV) * 0.3
+    tab0 = torch.randn(7, H, generator=g, device=DEV) * 0.5
+    pack = rg.rel_pack(e_feat, num_rel=7)
+    gy = torch.randn(N, H, D, generator=g, device=DEV)
+    outs = []
+    for pass_al in (False, True):
+        ft, al, ar, tab = (t.clone().requires_grad_(True) for t in (ft0, al0, ar0, tab0))
+        el, er = ops.attn_dots(ft, al, ar)
+        y = ops.gat_fused(rg, el, er, ft, tab, pack, 0.2, attn_l=al if pass_al else None)
+        y.backward(gy)
+        outs.append([y.detach(), ft.grad, al.grad, ar.grad, tab.grad])
+    for name, a, b in zip(["out", "g_ft", "g_al", "g_ar", "g_tab"], outs[0], outs[1]):
+        assert torch.equal(a, b), f"{name}: max diff {(a - b).abs().max().item():.3e}"
+
+
+def test_attn_dots_vec_order_matches_fp64():
+    """regnn_attn_dots_fwd in the lane order the fused forward re-forms el in, against fp64."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(6)
+    for H, D in [(8, 64), (4, 16), (3, 4), (2, 12)]:
+        ft = torch.randn(5000, H, D, generator=g, device=DEV)
+        al = torch.randn(1, H, D, generator=g, device=DEV)
+        ar = torch.randn(1, H, D, generator=g, device=DEV)
+        el, er = ops.attn_dots(ft, al, ar)
+        rl = (ft.double() * al.double()).sum(-1)
+        rr = (ft.double() * ar.double()).sum(-1)
+        assert (el.double() - rl).abs().max().item() <= 1e-5 * max(1.0, rl.abs().max().item())
+        assert (er.double() - rr).abs().max().item() <= 1e-5 * max(1.0, rr.abs().max().item())
