@@ -279,7 +279,11 @@ struct HeadArgs {
 template <typename T, int LPR, int NV, bool BWD, bool CH>
 __global__ void __launch_bounds__(kBlock) spmm_heads_kernel(HeadArgs p, LongPlan P) {
     constexpr int EV = Vec<T>::N;
+#ifdef REGNN_HEADS_UN
+    constexpr int UN = NV <= 2 ? REGNN_HEADS_UN : (NV <= 4 ? 4 : 2);
+#else
     constexpr int UN = NV <= 2 ? 8 : (NV <= 4 ? 4 : 2);   // edge rows in flight per step
+#endif
     constexpr int GPB = kBlock / LPR;
     const int tid = threadIdx.x, lane = tid & (LPR - 1);
     const int F = p.H * p.D;
