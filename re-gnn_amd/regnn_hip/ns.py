@@ -358,10 +358,11 @@ SPLIT_JOIN = {"mode": os.environ.get("REGNN_NS_SPLIT_JOIN", "on")}
 # extra reduction launch and the fork / join cost more than the overlap hides while a
 # collective's latency, not its bytes, sets its time
 SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
-# "on": the module path (device blocks) samples the next batch on a second stream while the
-# model trains on this one, as the fused step does; "off" (default: at hidden 512, mag-10x the
-# overlapped sampler slowed the dense kernels more than it hid, 1.045 -> 1.09 ms per step)
-MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "off")}
+# "on" (default): the module path (device blocks) samples the next batch on a second stream while
+# the model trains on this one, as the fused step does; "off": in order. At hidden 512, mag-10x:
+# round 3 (hipBLASLt GEMMs) 1.045 off / 1.09 on; round 4 (x6 GEMMs, interleaved pairs) 0.771 /
+# 0.761 off against 0.757 / 0.756 on
+MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # the fused engine's sampling lookahead G: 2G sampler slots, each step samples the batch trained
 # G steps later, and a G-step graph trains G slots while the sampler fills the other G on the
 # second queue with one fork (the graph's root) and one join (its end) -- instead of a fork and
