@@ -110,6 +110,46 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ s, const float
 // C[m][n] = sum_k opA[m][k] opB[k][n]; TA: A stored [K][M] (lda >= M), else [M][K]; TB: B
 // stored [N][K], else [K][N]. Wave w: rows 64 (w >> 1) .., columns 64 (w & 1) .. of the 128 x 128
 // tile as 4 x 4 MFMA tiles (96 MFMAs per k-step against 24 fragment reads from LDS).
+// One k-step of wave (wr, wc)'s MFMA tiles: NI x NJ of its 4 x 4 (the rest lie past M / N: an
+// edge tile's waves skip the products nothing reads, e.g. the 4 extra columns of a 516-wide
+// operand cost 1 / 8 of a tile's MFMAs instead of a whole tile's).
+template <int NI, int NJ>
+__device__ __forceinline__ void mma_step(const uint16_t* sa, const uint16_t* sb, int wr, int wc,
+                                         int c, int q, f32x4 (&acc)[4][4]) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8_t b[NJ][3];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                b[j][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * BN + 64 * wc + 16 * j + c) * RS + 32 * ks + 8 * q);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            bf16x8_t a[3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                a[s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * BM + 64 * wr + 16 * i + c) * RS + 32 * ks + 8 * q);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {             // small products first
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// valid 16-wide MFMA tiles of a wave's 64 (rows or columns from b of ext): 0, 1 or 4 (2 / 3 run
+// as 4)
+__device__ __forceinline__ int wave_tiles(int64_t b, int64_t ext) {
+    const int64_t v = ext - b;
+    return v <= 0 ? 0 : (v <= 16 ? 1 : 4);
+}
+
 template <bool TA, bool TB, bool VEC>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
@@ -122,6 +162,7 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
     const int64_t nk = (K + BK - 1) / BK;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
     const int wr = w >> 1, wc = w & 1;
+    const int NI = wave_tiles(m0 + 64 * wr, M), NJ = wave_tiles(n0 + 64 * wc, N);
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -144,31 +185,14 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
             load_tile<AKC, VEC>(A, lda, m0, M, (kt + S) * BK, K, va);
             load_tile<BKC, VEC>(B, ldb, n0, N, (kt + S) * BK, K, vb);
         }
-#pragma unroll
-        for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8_t b[4][3];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-                b[j][s] = *reinterpret_cast<const bf16x8_t*>(sb + (s * BN + 64 * wc + 16 * j + c) * RS + 32 * ks + 8 * q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            bf16x8_t a[3];
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-                a[s] = *reinterpret_cast<const bf16x8_t*>(sa + (s * BM + 64 * wr + 16 * i + c) * RS + 32 * ks + 8 * q);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {              // small products first
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
-            }
-        }
-        }
+#ifdef REGNN_GEMM_NO_EDGE
+        mma_step<4, 4>(sa, sb, wr, wc, c, q, acc);
+#else
+        if (NI == 4 && NJ == 4) mma_step<4, 4>(sa, sb, wr, wc, c, q, acc);
+        else if (NI == 1 && NJ == 4) mma_step<1, 4>(sa, sb, wr, wc, c, q, acc);
+        else if (NI == 4 && NJ == 1) mma_step<4, 1>(sa, sb, wr, wc, c, q, acc);
+        else if (NI == 1 && NJ == 1) mma_step<1, 1>(sa, sb, wr, wc, c, q, acc);
+#endif
     }
     // D lane (q, c): rows 4 q + r of the 16-row tile, column c
 #pragma unroll
