@@ -1,3 +1,8 @@
+# bwd0 grid A/B: REGNN_NSM_BWD_BLOCKS per type 128 (default) / 112 / 144
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out &&
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ns_engine.py tests/test_gpu_ns.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/t.log 2>&1; tail -1 gpurun_out/t.log &&
-bash tools/ab_lib2.sh 2 base cur
+for r in 1 2; do
+  for gb in 128 112 144; do
+    REGNN_NSM_BWD_BLOCKS=$gb timeout -k 10 300 python bench.py --no-full-batch --no-cpu-baseline --steps 300 > gpurun_out/gb_$gb.log 2>&1 || { tail -5 gpurun_out/gb_$gb.log; exit 1; }
+    echo "bwd_blocks=$gb $(grep '^{' gpurun_out/gb_$gb.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"]*1000,1))') us"
+  done
+done
