@@ -1535,6 +1535,10 @@ def typed_linear(tables, weights, biases, node_type, local_idx, n_id=None, wgrou
 GEMM_X6 = {"mode": os.environ.get("REGNN_GEMM_X6", "on")}
 
 
+# split-K target: blocks (tile x split) per launch; env REGNN_GEMM_SPLIT_TARGET for A/B runs
+_SPLIT_TARGET = int(os.environ.get("REGNN_GEMM_SPLIT_TARGET", "512"))
+
+
 def _gemm_splits(M, N, K):
     """split-K factor: about two 128 x 128 tiles per CU for a small output over a long
     reduction (each split keeps >= 4 k-steps of 32)."""
@@ -1542,7 +1546,7 @@ def _gemm_splits(M, N, K):
     nk = -(-K // 32)
     if tiles >= 256 or nk < 8:
         return 1
-    return int(max(1, min(64, 512 // tiles, nk // 4)))
+    return int(max(1, min(64, _SPLIT_TARGET // tiles, nk // 4)))
 
 
 def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
