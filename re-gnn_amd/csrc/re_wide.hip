@@ -219,7 +219,8 @@ int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, con
         (p_drop > 0.f && !state))
         return REGNN_EINVAL;
     if (n == 0) return REGNN_OK;
-    if (!aligned(x) || !aligned(a) || !aligned(y) || (res && !aligned(res)) || (bias && !aligned(bias)))
+    if (!aligned(x) || !aligned(a) || !aligned(y) || (res && !aligned(res)) || (bias && !aligned(bias)) ||
+        !aligned(gamma) || !aligned(beta))
         return REGNN_EUNSUPPORTED;
     LnArgs A{};
     A.n = n; A.H = H; A.x = x; A.rs = rs; A.bias = bias; A.res = res; A.gamma = gamma; A.beta = beta;
@@ -245,7 +246,8 @@ int regnn_wide_ln_bwd(int64_t n, int32_t H, const float* gy, const float* a, con
     if (n < 0 || !gy || !a || !stats || !gamma || !beta || !gx || !slab ||
         !(p_drop >= 0.f && p_drop < 1.f) || (p_drop > 0.f && !state))
         return REGNN_EINVAL;
-    if (!aligned(gy) || !aligned(a) || !aligned(gx) || (gres && !aligned(gres)))
+    if (!aligned(gy) || !aligned(a) || !aligned(gx) || (gres && !aligned(gres)) || !aligned(gamma) ||
+        !aligned(beta))
         return REGNN_EUNSUPPORTED;
     LnArgs A{};
     A.n = n; A.H = H; A.gy = gy; A.a_in = a; A.stats_in = stats; A.rs = rs; A.gamma = gamma; A.beta = beta;

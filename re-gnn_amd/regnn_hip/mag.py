@@ -496,12 +496,15 @@ class REGNN(torch.nn.Module):
         b_cat = torch.stack([lin.bias for lin in lins], 0)                      # [T, H]
         w_c, b_c = ops.mm(w_cat, conv.weight), b_cat @ conv.weight
         n = blk.n_dst
-        agg = ops.mm(Sw, torch.cat([w_c, b_c], 0))
+        wb = [w_c, b_c]
+        if Sw.shape[1] > T * K + T:                 # the zero pad columns of [S | w | 0]
+            wb.append(w_c.new_zeros(Sw.shape[1] - T * K - T, w_c.shape[1]))
+        agg = ops.mm(Sw, torch.cat(wb, 0))
         res = None
         if conv.residual:                                                       # :104,131-132
             x_t = self.group_input(x_dict, node_type, local_node_idx, n_id[:n])
             res = ops.mm(x_t, conv.weight)
-        if epi is not None and ops.wide_ln_ok(agg, conv.norm):
+        if epi is not None and ops.wide_ln_ok(agg, conv.norm, conv.bias):
             # mean + bias + residual, LayerNorm, relu, dropout in one launch (:341-343)
             return ops.wide_ln_act(agg, conv.bias, conv.norm, epi[0], epi[1], 0,
                                    rs=blk.inv[:n], res=res), True
@@ -539,7 +542,7 @@ class REGNN(torch.nn.Module):
             blk = edge_index if getattr(edge_index, "is_ns_block", False) else \
                 getattr(adj, "block", None)
             if (blk is not None and getattr(blk, "is_ns_block", False) and epi is not None and
-                    self.self_loop_type == 2 and ops.wide_ln_ok(x, self.convs[i].norm)):
+                    self.self_loop_type == 2 and ops.wide_ln_ok(x, self.convs[i].norm, self.convs[i].bias)):
                 ep = self._wide_epi(blk) or epi
                 x = self.convs[i].forward_act(x, x_target, blk, ep[0], ep[1], i)
                 continue                       # (relu and dropout applied in the epilogue)

@@ -1003,6 +1003,16 @@ class NSTrainer:
         self._exchange()
         self._opt_step()
 
+    def guarded_step(self, guard=None):
+        """step() with a failure on any rank ending every rank (regnn_hip.guard): a rank whose
+        forward / backward raises still issues the step's gradient all-reduce its peers are in,
+        then all ranks agree on the outcome (one eager flag all-reduce) and, if any failed,
+        raise guard.RankFailure together. One rank: step()."""
+        from .guard import Guard
+        guard = guard or Guard(self.world)
+        guard.stage("NS train step", self._forward_backward, always=self._exchange)
+        self._opt_step()
+
     def _train_state(self):
         """parameters and optimizer state, for capture() to undo its warm-up steps."""
         if isinstance(self.opt, FlatAdam):
@@ -1110,7 +1120,12 @@ class NSTrainer:
         saved = self._train_state()
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                self.step()
+                # several ranks: a warm-up step that fails on one rank ends every rank together
+                # (regnn_hip.guard) instead of leaving its peers in the step's all-reduce
+                if multi:
+                    self.guarded_step()
+                else:
+                    self.step()
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._undo_steps(saved, st0)
         # one rank: the optimizer step joins the step's graph (no graph boundary, no host gap

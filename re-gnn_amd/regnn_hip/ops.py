@@ -663,8 +663,13 @@ class _NsTypedAgg(torch.autograd.Function):
         T, K = len(tables), int(tables[0].shape[1])
         dev = tables[0].device
         if ext:
-            out = torch.empty(blk.n_dst, T * K + T, dtype=torch.float32, device=dev)
-            S_ptr, w_ptr, lds, ldw = L.ptr(out), L.ptr(out) + 4 * T * K, T * K + T, T * K + T
+            # row stride T K + Tp, Tp = T rounded up to 4 (the kernels take 16-byte aligned
+            # rows); the Tp - T pad columns are zeros, so a GEMM against [W_c; b_c; 0] is exact
+            Tp = _ext_pad(T)
+            out = torch.empty(blk.n_dst, T * K + Tp, dtype=torch.float32, device=dev)
+            if Tp != T:
+                out[:, T * K + T:].zero_()
+            S_ptr, w_ptr, lds, ldw = L.ptr(out), L.ptr(out) + 4 * T * K, T * K + Tp, T * K + Tp
         else:
             S = torch.empty(blk.n_dst, T, K, dtype=torch.float32, device=dev)
             w = torch.empty(blk.n_dst, T, dtype=torch.float32, device=dev)
@@ -699,9 +704,10 @@ class _NsTypedAgg(torch.autograd.Function):
         dev = tables[0].device
         if ctx.ext:
             g = grads[0]
-            g = (torch.zeros(blk.n_dst, T * K + T, device=dev) if g is None
+            Tp = _ext_pad(T)
+            g = (torch.zeros(blk.n_dst, T * K + Tp, device=dev) if g is None
                  else g.contiguous().float())
-            gS_ptr, gw_ptr, lds, ldw = L.ptr(g), L.ptr(g) + 4 * T * K, T * K + T, T * K + T
+            gS_ptr, gw_ptr, lds, ldw = L.ptr(g), L.ptr(g) + 4 * T * K, T * K + Tp, T * K + Tp
         else:
             gS, gw = grads
             gS = (torch.zeros(blk.n_dst, T, K, device=dev) if gS is None
@@ -738,12 +744,18 @@ def _cached_cast(t, dtype):
     return out
 
 
+def _ext_pad(T):
+    """columns of w in ns_typed_agg's ext rows: T rounded up to a multiple of 4."""
+    return (int(T) + 3) // 4 * 4
+
+
 def ns_typed_agg(blk, tab, n_id, tables, node_type, local_idx, ext=False):
     """layer 0's sampled-block aggregation of the RAW input rows per source node type (the NS
     REGNN's group_input Linear and first conv weight moved after the mean by linearity,
     mag/regnn_ns.py:300-326 + mag/regnn_layers.py:101-148): returns S [n_dst, T, K] and the
-    per-type weight sums w [n_dst, T], or with ext one [n_dst, T K + T] tensor [S | w] (the
-    projection's single GEMM operand against [W_c; b_c]); differentiable in tab."""
+    per-type weight sums w [n_dst, T], or with ext one [n_dst, T K + Tp] tensor [S | w | 0]
+    (Tp = T rounded up to 4, zero pad columns: the projection's single GEMM operand against
+    [W_c; b_c; 0]); differentiable in tab."""
     return _NsTypedAgg.apply(tab, blk, n_id, tables, node_type, local_idx, bool(ext))
 
 
@@ -1664,8 +1676,12 @@ def linear(x, w, bias=None):
 
 def mm(a, b, c=None):
     """c + a @ b on regnn_gemm_x6 when the operands allow it (else torch)."""
-    if (GEMM_X6["mode"] != "off" and gemm_x6_ok(a, b) and
-            (c is None or (c.is_cuda and c.dtype == torch.float32))):
+    # c: None, a length-N row vector or exactly [M, N] (the x6 epilogue writes M rows with c's
+    # row stride; any other broadcastable shape goes to torch)
+    M, N = (a.shape[0], b.shape[1]) if a.dim() == 2 and b.dim() == 2 else (-1, -1)
+    c_ok = c is None or (c.is_cuda and c.dtype == torch.float32 and
+                         (tuple(c.shape) == (N,) or tuple(c.shape) == (M, N)))
+    if GEMM_X6["mode"] != "off" and gemm_x6_ok(a, b) and c_ok:
         return _MMx6.apply(a, b, c)
     return a @ b if c is None else (torch.addmm(c, a, b) if c.dim() <= 2 else c + a @ b)
 
@@ -1695,6 +1711,8 @@ class _WideLn(torch.autograd.Function):
         a, stats, rs, gamma, beta, state = ctx.saved_tensors
         n, H = a.shape
         gy = gy.contiguous()
+        if gy.data_ptr() % 16:                 # the kernel's float4 rows need 16-byte alignment
+            gy = gy.clone()
         gx = torch.empty_like(a)
         gres = torch.empty_like(a) if ctx.has_res and ctx.needs_input_grad[2] else None
         rows = int(L._so.regnn_wide_ln_slab_rows(n, H))
@@ -1707,10 +1725,17 @@ class _WideLn(torch.autograd.Function):
         return (gx, g_bias, gres, g_gamma, g_beta, None, None, None, None)
 
 
-def wide_ln_ok(x, ln):
+def wide_ln_ok(x, ln, bias=None):
     return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and
             x.shape[1] in WIDE_LN_WIDTHS and isinstance(ln, torch.nn.LayerNorm) and
-            ln.elementwise_affine and abs(ln.eps - 1e-5) < 1e-12 and x.data_ptr() % 16 == 0)
+            ln.elementwise_affine and abs(ln.eps - 1e-5) < 1e-12 and x.data_ptr() % 16 == 0 and
+            # the kernels read gamma / beta / bias as float4 rows too
+            ln.weight.data_ptr() % 16 == 0 and ln.bias.data_ptr() % 16 == 0 and
+            _wide_operands_ok(bias))
+
+
+def _wide_operands_ok(*ts):
+    return all(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in ts)
 
 
 def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None):
@@ -1718,5 +1743,12 @@ def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None):
     dropout mask the fused NS step's spec keyed on the sampler `state` and `layer`."""
     if p > 0 and state is None:
         raise ValueError("wide_ln_act: dropout needs the sampler state (its mask key)")
-    return _WideLn.apply(x, bias, None if res is None else res.contiguous(), ln.weight, ln.bias,
+    if res is not None:
+        res = res.contiguous()
+        if res.data_ptr() % 16:
+            res = res.clone()
+    if not _wide_operands_ok(bias, ln.weight, ln.bias):
+        raise ValueError("wide_ln_act: bias / LayerNorm weight and bias must be contiguous and "
+                         "16-byte aligned (check wide_ln_ok first)")
+    return _WideLn.apply(x, bias, res, ln.weight, ln.bias,
                          rs, state if p > 0 else None, layer, float(p))

@@ -124,3 +124,91 @@ def test_dp_uneven_batch_count_same_steps_per_rank():
     out = mgr.dict()
     mp.spawn(_uneven_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     assert out[0] == [0, 2, 4] and out[1] == [1, 3, 0]
+
+
+_FAIL_WORKER = r"""
+import os, sys, time
+sys.path.insert(0, os.path.join(os.environ["REGNN_ROOT"], "re-gnn_amd"))
+import torch
+import torch.distributed as dist
+from regnn_hip.guard import Guard, pg_timeout
+from regnn_hip.ns import NSTrainer
+
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout())
+
+
+class FakeTrainer:
+    # NSTrainer.guarded_step's contract on the CPU: forward / backward local, the exchange a
+    # collective every rank issues, then the optimizer
+    world = 2
+
+    def __init__(self):
+        self.flat = torch.ones(1000)
+        self.steps = 0
+
+    def _forward_backward(self):
+        self.flat.mul_(1.5)
+        if rank == 1 and self.steps == int(os.environ["FAIL_AT"]):
+            raise RuntimeError("injected failure inside the warm-up step")
+
+    def _exchange(self):
+        dist.all_reduce(self.flat)
+
+    def _opt_step(self):
+        self.steps += 1
+
+
+tr = FakeTrainer()
+guard = Guard(world)
+guard.stage("build", lambda: None)
+for _ in range(3):                                   # the warm-up steps
+    NSTrainer.guarded_step(tr, guard)
+print(f"rank {rank} finished", flush=True)
+dist.destroy_process_group()
+"""
+
+
+def _run_two_ranks(fail_at, timeout_s=20):
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), REGNN_ROOT=root, FAIL_AT=str(fail_at),
+                   REGNN_DIST_TIMEOUT=str(timeout_s))
+        procs.append(subprocess.Popen([sys.executable, "-c", _FAIL_WORKER], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout_s + 60)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a rank hung past the process group timeout")
+        outs.append((p.returncode, o, e))
+    return outs, time.time() - t0
+
+
+def test_rank_failure_in_warmup_ends_every_rank():
+    """rank 1 raises inside a warm-up step (its peer is then in the step's
+    gradient all-reduce); both ranks exit non-zero (guard.EXIT_CODE) well within the process
+    group's timeout, neither hangs, and rank 1 reports the injected error."""
+    from regnn_hip.guard import EXIT_CODE
+    outs, dt = _run_two_ranks(fail_at=1)
+    codes = [rc for rc, _, _ in outs]
+    assert codes == [EXIT_CODE, EXIT_CODE], (codes, [e[-600:] for _, _, e in outs])
+    assert "injected failure" in outs[1][2]
+    assert all("finished" not in o for _, o, _ in outs)
+    assert dt < 20, dt                                 # agreement, not the timeout, ended it
+
+
+def test_no_failure_both_ranks_finish():
+    outs, _ = _run_two_ranks(fail_at=-1)
+    assert [rc for rc, _, _ in outs] == [0, 0], [e[-600:] for _, _, e in outs]
+    assert all("finished" in o for _, o, _ in outs)

@@ -31,7 +31,8 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(
                       use_norm="ln", self_loop_type=2, residual=residual).to(DEV)
         with torch.no_grad():
             for conv in m.convs:
-                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, 11, device=DEV))
+                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, conv.relation_weight.numel(),
+                                                            device=DEV))
                 conv.bias.normal_(0, 0.1)
         m.train()
         opt = torch.optim.SGD(m.parameters(), lr=0.0)
@@ -67,6 +68,35 @@ def test_typed_first_layer_matches_reference_order(K, hidden, residual):
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
     # the relation table of layer 0 has a gradient through the typed aggregation
+    assert np.abs(ga["convs.0.relation_weight"]).max() > 0
+
+
+def _three_types(d):
+    """the same graph with 3 node types (institution and field merged into one type, their
+    feature tables concatenated): T = 3 is not a multiple of 4, so [S | w] rows carry pad
+    columns (ops.ns_typed_agg ext)."""
+    nt = d["node_type"].clone()
+    n2 = int(d["x_dict"][2].shape[0])
+    local = d["local"].clone()
+    f = nt == 3
+    local[f] += n2
+    nt[f] = 2
+    x = {0: d["x_dict"][0], 1: d["x_dict"][1],
+         2: torch.cat([d["x_dict"][2], d["x_dict"][3]], 0).contiguous()}
+    return dict(d, node_type=nt, local=local, x_dict=x)
+
+
+@pytest.mark.parametrize("hidden", [64, 512])
+def test_typed_first_layer_three_types(hidden):
+    """T = 3 node types (row stride T K + 4, not T K + T) through the typed first
+    layer, against the reference-ordered path."""
+    d = _three_types(_mag(0.003, seed=2, F=128))
+    la, ga = _grads_one_step(d, hidden, True, 0.0)
+    lb, gb = _grads_one_step(d, hidden, False, 0.0)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
     assert np.abs(ga["convs.0.relation_weight"]).max() > 0
 
 
@@ -167,7 +197,8 @@ def test_wide_epilogue_and_gemm_match_torch_path(monkeypatch, hidden, residual, 
                       use_norm="ln", self_loop_type=2, residual=residual).to(DEV)
         with torch.no_grad():
             for conv in m.convs:
-                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, 11, device=DEV))
+                conv.relation_weight.copy_(torch.linspace(-0.02, 0.12, conv.relation_weight.numel(),
+                                                            device=DEV))
                 conv.bias.normal_(0, 0.1)
                 conv.norm.weight.normal_(1, 0.1)
         m.train()
