@@ -191,7 +191,8 @@ def run_ns_epoch(args, dev):
                                             "cores, hidden 512, real ogbn-mag"}}
 
 
-def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False, two_layer=True, adam_params=0):
+def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False, two_layer=True, adam_params=0,
+                  pre_sums=False):
     """algorithmic HBM bytes of one fused NS model step (regnn_nsm_step) at the sampled sizes
     sz (regnn_ns_hop sizes: sz[h] = rows after h hops, sz[8 + h] = edges of hop h's block,
     self loops included): every row / index / feature byte a kernel must read or write once
@@ -207,11 +208,15 @@ def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False, two_layer=True, ada
                 4*T counts); relation slots: + n1 x (K*4 self row + 4*(T+1) slots); else
                 + n1 x (T*K*4 Z + 4*T beta) and rel0's E1 x (K*4 + 13) + n1 x (T*K*4 + 4*T)
       Adam      24 B per parameter (p, m, v read and written) when it runs inside the step
+    pre_sums (regnn_nsm_work.pre_sums): the sampler formed layer 0's per-type input sums ahead of
+    the step (regnn_ns_hop_typed_sums); agg0 reads the n1 x (T*K*4 + 4*T + K*4 + 4*(T+1)) bytes of
+    sums / counts / self rows / slots instead of gathering E1 input rows and writing them.
     The L-layer composed-map form (two_layer=False) keeps round 2's model."""
     f = 4 * F
     if two_layer and L == 2:
         n1, E1, n0, E0 = sz[1], sz[9], sz[0], sz[8]
-        b = E1 * (4 * K + 13) + n1 * (T * 4 * K + 4 * T + 3 * f + 2 * f + 16)
+        gather0 = 0 if pre_sums else E1 * (4 * K + 13)
+        b = gather0 + n1 * (T * 4 * K + 4 * T + 3 * f + 2 * f + 16)
         b += E0 * 2 * (f + 5) + E0 * 2 * f + n0 * 24 + 4 * C * F + 4 * F * F
         b += n1 * (2 * f + f + f + 12 + T * 4 * K + 4 * T)
         if rel_slots:
@@ -259,7 +264,8 @@ def run_ns(args, dev):
             nsm_bytes.append(ns_step_bytes(
                 tr.sampler.sizes.cpu().tolist(), 128, 349, rel_slots=bool(tr.fused.P.rel_slots),
                 two_layer=tr.fused.two_layer,
-                adam_params=tr.flat.numel() if tr.adam_fused else 0))
+                adam_params=tr.flat.numel() if tr.adam_fused else 0,
+                pre_sums=bool(tr.fused.W.pre_sums)))
     torch.cuda.synchronize()
     kstats = profile.summary()
     profile.enable(False)
@@ -446,6 +452,31 @@ def build_full(args, dev, wl):
         return dict(step=step, edges_per_step=rg.E, rg=rg, R=gd["R"],
                     kernels=("gat_fused_fwd", "spmm_heads_bwd", "gat_softmax_bwd",
                              "gat_attn_lse"), convs=1, N=rg.n_dst, E=rg.E, train_nodes=0)
+    elif wl == "gatv2":
+        # one REGATv2Conv layer (heads 8, out 64, relation bias, LeakyReLU 0.01) forward +
+        # backward on mag_like(scale): the GATv2 score SDDMM, the per-destination edge softmax
+        # and the per-head aggregation; Zipf hub rows take the long-segment plan
+        from layer import REGATv2Conv
+        gd = synth.mag_like(args.scale, seed=0, device=dev, zipf_s=args.zipf)
+        g, rg, e_feat = _full_graph(gd, dev)
+        conv = REGATv2Conv(gd["R"], 100.0, 64, 64, 8, 0.0, 0.0, 0.01).to(dev).train()
+        x = torch.randn(gd["N"], 64, generator=gen, device=dev)
+        gout = torch.randn(gd["N"], 8, 64, generator=gen, device=dev)
+        params = list(conv.parameters())
+
+        def step():
+            y = conv(g, x, e_feat)
+            y.backward(gout)
+            for p_ in params:
+                p_.grad = None
+
+        torch.cuda.synchronize()
+        log(f"[bench] gatv2: N={gd['N']:,} E={rg.E:,} R={gd['R']} built in {time.time() - t0:.1f}s; "
+            f"long rows csr={rg.csr_plan.n_long} csc={rg.csc_plan.n_long}")
+        return dict(step=step, edges_per_step=rg.E, rg=rg, R=gd["R"],
+                    kernels=("gatv2_score_fwd", "gatv2_score_bwd", "edge_softmax_fwd",
+                             "edge_softmax_bwd", "spmm_heads_fwd", "spmm_heads_bwd"),
+                    convs=1, N=rg.n_dst, E=rg.E, train_nodes=0)
     elif wl == "imdb":
         gd = synth.imdb_like(seed=0, device=dev)
         feats = synth.type_features(gd["counts"], synth.IMDB_DIMS, seed=1, device=dev,
@@ -590,7 +621,10 @@ def run_full(args, dev, wl):
             "acm": "REGAT 2-layer hidden=64 heads [8,8,1] (last layer twice) on acm_like",
             "imdb": "REMixHop 2-layer p=[0,1,2] hidden=64 on imdb_like",
             "gat": f"REGATConv heads 8 x 64, relation bias, fwd (fused scores + softmax + SpMM) "
-                   f"+ bwd on mag_like(scale={args.scale}, zipf_s={args.zipf})"}[wl],
+                   f"+ bwd on mag_like(scale={args.scale}, zipf_s={args.zipf})",
+            "gatv2": f"REGATv2Conv heads 8 x 64, relation bias, fwd (GATv2 score SDDMM, edge "
+                     f"softmax, per-head SpMM) + bwd on mag_like(scale={args.scale}, "
+                     f"zipf_s={args.zipf})"}[wl],
             "nodes": w["N"], "edges": w["E"], "relations": w["R"],
             "conv_applications_per_step": w["convs"], "hidden": 64, "hip_graph": use_graph,
             "label_rows": (f"{w['train_nodes']:,} train rows: a seeded random 85.5 % of the "
@@ -712,7 +746,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "gat",
+    ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "gat", "gatv2",
                                            "ns_infer", "ns_epoch"], default="ns")
     ap.add_argument("--hidden", type=int, default=64, help="ns / ns_epoch: hidden width")
     ap.add_argument("--zipf", type=float, default=1.1,

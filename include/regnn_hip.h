@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 40). */
+/* ABI version (bumped on any signature or semantics change; currently 41). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -460,29 +460,35 @@ int regnn_attn_dots_bwd(const float* ft, const float* attn_l, const float* attn_
 /* ---------------------------------------------------------------------------------------
  * GATv2 scores and the edge softmax over per-edge logits (re_gatv2.hip; H a power of two <= 32
  * for the softmax entry points; D % 4 == 0 with D / 4 a power of two for the score kernels).
+ * plan (may be NULL; ABI 41): the CSR's (CSC's for bwd_src) long-segment plan, as REGATConv's
+ * entry points take it: hub rows run as chunks on groups of their own, their segment sums /
+ * max / dot combined by the plan's fixed-order tree. Partial widths: score_fwd 0,
+ * score_bwd_dst / _src H*D, edge_softmax_fwd 2H, edge_softmax_bwd H.
  * --------------------------------------------------------------------------------------- */
 
 /* GATv2 score SDDMM (layer/REGATv2Conv.py:139-141; mag/regnn_layers.py:399-403), CSR order:
  *   s[e,h] = sum_d att[h*D+d] * LeakyReLU(fs[idx[e], h*D+d] + fd[v, h*D+d], slope). */
 int regnn_gatv2_score_fwd(const int32_t* ptr, const int32_t* idx, const float* fs, const float* fd,
                           const float* att, int64_t n_seg, int32_t H, int32_t D, float slope,
-                          float* s, hipStream_t stream);
+                          float* s, const regnn_seg_plan* plan, hipStream_t stream);
 
 /* Its backward, destination side (CSR): gfd[v] = sum_{e in seg v} gs[e,h] * att * lrelu'(pre),
  * and per-block partials of d att = sum_e gs[e,h] * LeakyReLU(pre) in att_slab
- * [slab_rows, H*D] (every row < the launch grid written; reduce with regnn_rel_reduce over
- * min(slab_rows, grid) rows: the grid is min(slab_rows, segments / groups per block)). */
+ * [slab_rows, H*D] (zero-filled by the caller; the launches write rows < slab_rows: with a
+ * plan's chunks the per-segment pass takes rows < slab_rows / 2, the chunk pass the rest;
+ * reduce every row with regnn_rel_reduce). */
 int regnn_gatv2_score_bwd_dst(const int32_t* ptr, const int32_t* idx, const float* fs,
                               const float* fd, const float* att, const float* gs, int64_t n_seg,
                               int32_t H, int32_t D, float slope, float* gfd, float* att_slab,
-                              int32_t slab_rows, hipStream_t stream);
+                              int32_t slab_rows, const regnn_seg_plan* plan, hipStream_t stream);
 
 /* Its backward, source side (CSC, csc2csr maps a CSC position to the CSR edge position of gs):
  *   gfs[u] = sum_{e: u->v} gs[e,h] * att * lrelu'(fs[u] + fd[v]). */
 int regnn_gatv2_score_bwd_src(const int32_t* csc_ptr, const int32_t* csc_idx,
                               const int32_t* csc2csr, const float* fs, const float* fd,
                               const float* att, const float* gs, int64_t n_src, int32_t H,
-                              int32_t D, float slope, float* gfs, hipStream_t stream);
+                              int32_t D, float slope, float* gfs, const regnn_seg_plan* plan,
+                              hipStream_t stream);
 
 /* Edge softmax over per-edge logits z = s[e,h] + (ee_table ? ee_table[rel[e]*H + h] : 0), per
  * destination (CSR):
@@ -493,13 +499,14 @@ int regnn_gatv2_score_bwd_src(const int32_t* csc_ptr, const int32_t* csc_idx,
  *                 exactly as the reference's). */
 int regnn_edge_softmax_fwd(const int32_t* ptr, const float* s, const uint8_t* rel,
                            const float* ee_table, const float* gmax, float eps, int64_t n_seg,
-                           int32_t H, float* a, hipStream_t stream);
+                           int32_t H, float* a, const regnn_seg_plan* plan, hipStream_t stream);
 
 /* Backward (both forms; the global max's own gradient is exactly 0 up to the eps term):
- *   gz = a * (ga - sum_v a*ga) (CSR order); slab (optional): per-block (rel, h) sums of gz. */
+ *   gz = a * (ga - sum_v a*ga) (CSR order); slab (optional, regnn_slab_rows() rows): per-block
+ *   (rel, h) sums of gz. */
 int regnn_edge_softmax_bwd(const int32_t* ptr, const uint8_t* rel, const float* a,
                            const float* ga, int64_t n_seg, int32_t H, float* gz, float* slab,
-                           int32_t n_rel, hipStream_t stream);
+                           int32_t n_rel, const regnn_seg_plan* plan, hipStream_t stream);
 
 /* GAT v1 scores written per edge (CSR): s = LeakyReLU(el[idx[e],h] + er[v,h] + ee[rel[e],h]),
  * for the global max of the ogbn-mag softmax (mag/regnn_layers.py:297-307). */
@@ -586,9 +593,12 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * strided = 1: the block in the fixed-stride layout instead of the CSR -- row i's edges at
  * [i S, i S + cnt_i) (S = k + 1, cnt_i = scnt[i], sampled positions ascending), its self loop at
  * i S + cnt_i, the other slots empty (blk_idx -1); blk_ptr is not written. Sampling and
- * placement run as one launch (no row-offset scan): 5 launches with de-duplication (4 without
- * the transposed index), 1 meta-only. sizes[8 + hop] must be zero on entry (regnn_ns_batch
- * zeroes sizes[8 ..]); the hop adds its edges to it and to state[5]. */
+ * placement run as one launch (no row-offset scan), the de-duplication as one pass (decoupled
+ * look-back over status), the transposed index by many blocks (per-slot ranks in samp, the
+ * last resolving block scans): 4 launches with de-duplication and the transposed index (3
+ * without it), 1 meta-only. Strided buffer sizes: samp >= cap_e ints, status >= ceil(cap_e /
+ * 1024) int64 (ABI 41). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
+ * the hop adds its edges to it and to state[5]. */
 #define REGNN_CSC_PIECE 1024
 #define REGNN_CSC_LONG_CAP (32768 / 17 + 1)          /* hub rows of a <= 32768-edge block */
 #define REGNN_CSC_LONG_NPIECE (REGNN_CSC_LONG_CAP + 1)
@@ -604,6 +614,25 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                  int32_t* blk_row, float* inv, const int64_t* local, int32_t* edge_type,
                  int64_t* edge_off, int32_t meta_only, int32_t* csc_cnt, int32_t* csc_ptr,
                  int32_t* csc_ent, int32_t* csc_long, int32_t strided, hipStream_t stream);
+
+/* The fused step's outer (meta-only, strided) hop with layer 0's parameter-free input sums
+ * (relation slots: each (target type, source type) pair has one relation). Samples hop `hop` as
+ * regnn_ns_hop(meta_only = 1, strided = 1) does -- the same slots, scnt, inv, blk_rel, edge_type /
+ * edge_off, sizes[hop + 1] = sizes[hop], edge counts into sizes[8 + hop] and state[5] -- and then
+ * sums each row i's sampled raw input rows (tables[t] rows local[u], K = 128 fp32) per source node
+ * type: s_agg[i][t][:] = sum of the rows of type t (unweighted), s_w[i][t] = their count,
+ * u_self[i][:] = the self loop's row, u_rel[i][t] = the relation of type t's edges (-1: none),
+ * u_rel[i][T] = the self loop's relation (regnn_nsm_work's layer-0 buffers, read by
+ * regnn_nsm_step with pre_sums = 1; they depend on the batch only, so the sampler computes them
+ * ahead of the model). T = n_types in [1, 4], k <= 63, tables / s_agg / u_self 16-byte aligned.
+ * One launch. The summation order is fixed (the result is a function of the batch). */
+int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
+                            const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
+                            int64_t* state, int32_t* sizes, const int32_t* n_id, int32_t cap_dst,
+                            int32_t* scnt, uint8_t* blk_rel, float* inv, const int64_t* local,
+                            int32_t* edge_type, int64_t* edge_off, const float* const* tables,
+                            int32_t n_types, int32_t K, float* s_agg, float* s_w, float* u_self,
+                            int32_t* u_rel, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):
@@ -684,12 +713,12 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
  * (state[3] << 8) ^ (layer + 0x51ED27))) (seed, epoch, global batch), row = target row of the
  * layer's block, 4 features per 16-byte vector.
  *
- * L = 2 (the reference's default num_layers; C <= 416): 5 launches (6 without rel_slots), the
+ * L = 2 (the reference's default num_layers; C <= 384): 5 launches (6 without rel_slots), the
  * group_input Linear and each conv's x @ W applied after their layer's aggregation (linearity:
  * mean_e(ew x_e) W = mean_e(ew x_e W)), the transposed aggregation of layer 1 as 2^-40
  * fixed-point integer sums, every other reduction fixed-order: the step is bitwise
  * reproducible; optionally the Adam update of regnn_nsm_work.adam in the last launch.
- * L = 3, 4 (or C > 416): the composed-map form above, 8+ launches, layer >= 1 transposed
+ * L = 3, 4 (or C > 384): the composed-map form above, 8+ launches, layer >= 1 transposed
  * aggregations with float atomics (as regnn_ns_spmm_bwd).
  * --------------------------------------------------------------------------------------- */
 #define REGNN_NSM_MAX_TYPES 8
@@ -729,7 +758,7 @@ typedef struct regnn_nsm_params {
                                  rows per source type unweighted and the relation-table gradient
                                  comes from those sums (no second pass over the edges; needs
                                  u_self / u_rel); 0: the edge pass */
-    int32_t two_layer;        /* 1: the caller set up the two-layer form (L = 2, C <= 416, hop 0's
+    int32_t two_layer;        /* 1: the caller set up the two-layer form (L = 2, C <= 384, hop 0's
                                  edge capacity <= 32768, regnn_nsm_work.p0 / gh1 / csc_* set):
                                  regnn_nsm_step and regnn_nsm_slab_floats take that form only
                                  then, one decision for both; 0: the composed-map form (ABI 36) */
@@ -767,7 +796,7 @@ typedef struct regnn_nsm_work {
     float* slab;              /* regnn_nsm_slab_floats() floats of per-block partials */
     float* u_self;            /* rel_slots: cap[L-1] * k_in, each row's self-loop input row */
     int32_t* u_rel;           /* rel_slots: cap[L-1] * (T + 1), relation of each source-type slot */
-    /* the two-layer step (L = 2, C <= 416, hop 0's edge capacity <= 32768): */
+    /* the two-layer step (L = 2, C <= 384, hop 0's edge capacity <= 32768): */
     float* p0;                /* cap[1] * 64: layer 0's group_input projection, summed per row */
     const struct regnn_nsm_adam* adam;   /* NULL, or the optimizer the last launch applies */
     float* gh1;               /* cap[0] * 64: G W_1^T of layer 1's target rows (its transposed pass) */
@@ -792,6 +821,10 @@ typedef struct regnn_nsm_work {
                                  the gradients final after layer 1's transposed pass (out_lin,
                                  layer 1, layer 0's conv bias and LayerNorm), part 2 reduces the
                                  rest (a caller all-reduces the first set while part 2 runs) */
+    int32_t pre_sums;         /* two-layer step with rel_slots, k_in 128, T <= 4: 1 = s_agg / s_w /
+                                 u_self / u_rel already hold the batch's layer-0 input sums
+                                 (regnn_ns_hop_typed_sums): layer 0 reads them instead of
+                                 gathering its input rows (ABI 41) */
 } regnn_nsm_work;
 
 /* Adam over the flat parameter bucket whose gradient bucket starts at grad_base (every g_*

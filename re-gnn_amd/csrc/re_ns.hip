@@ -291,6 +291,216 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
     }
 }
 
+// The fused step's outer hop with layer 0's parameter-free input sums (relation slots): the
+// meta-only strided hop of ns_sample_strided_kernel (same sampling, same slots, edge meta and
+// counts), and then the row's G lanes gather its sampled raw input rows (K = 128 floats: G = 32
+// lanes x float4 per row, two rows per wave; G = 64: each half of the wave a float4 of alternate
+// rows) and sum them per source node type (mag/regnn_ns.py:300-326 + mag/regnn_layers.py:110-144:
+// with one relation per (target type, source type) pair, sum_{e: type t} tab[r_e] x_e =
+// tab[r_t] sum_{e: type t} x_e, so the sums do not depend on the parameters and run G steps ahead
+// on the sampler's stream). Writes per row i: s_agg[i][t][:] (unweighted sums), s_w[i][t]
+// (counts), u_self[i][:] (the self loop's row), u_rel[i][t] (the slot's relation or -1),
+// u_rel[i][T] (the self loop's relation) -- what agg0's gather phase formed (regnn_nsm_work), in
+// agg0's order: the entries in slot order (ascending CSR position), so G = 32 gives agg0's bits.
+struct NsSumArgs {
+    const int32_t* ptr; const int32_t* idx; const uint8_t* etype; const int32_t* ntype;
+    const int64_t* local; int n_et;
+    const int32_t* n_id; int32_t* sizes; int hop; int cap; int k;
+    int64_t* state;
+    int32_t* scnt; uint8_t* blk_rel; float* inv; int32_t* e_type; int64_t* e_off;
+    const float* xt[8]; int T;
+    float* s_agg; float* s_w; float* u_self; int32_t* u_rel;
+};
+
+template <int NT>
+__device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
+    const float* r = A.xt[0];
+#pragma unroll
+    for (int q = 1; q < NT; ++q)
+        if (t == q) r = A.xt[q];
+    return r;
+}
+
+constexpr int kNsSumK = 128;               // input row width of the sums kernel
+constexpr int kNsSumUN = 11;               // entries' rows in flight per lane
+constexpr int kNsSumWaves = 8;             // waves per block (512 threads)
+
+template <int G, int NT>
+__global__ void __launch_bounds__(64 * kNsSumWaves, 4)
+ns_sample_sums_kernel(NsSumArgs A) {
+    constexpr int K = kNsSumK;
+    constexpr int TPW = 64 / G;                // rows per wave
+    constexpr int H = G == 64 ? 2 : 1;         // lane groups of 32 per row (each a float4 column)
+    __shared__ int wsum[kNsSumWaves * TPW];
+    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = wl % G, tl = wv * TPW + wl / G;
+    const uint64_t gmask = G == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
+    const int i = blockIdx.x * (kNsSumWaves * TPW) + tl;
+    const int n = A.sizes[A.hop];
+    const int k = A.k, S = k + 1;
+    const int64_t base = int64_t(i) * S;
+    int cnt = -1;                              // -1: no row (past the batch)
+    if (i < A.cap && i >= n) {
+        if (lane == 0) {
+            A.scnt[i] = 0;
+            A.inv[i] = 1.f;
+        }
+    } else if (i < n) {
+        const uint64_t seed = ns_hop_seed(A.state, A.hop);
+        const int t = A.n_id[i];
+        const int b = A.ptr[t], d = A.ptr[t + 1] - b;
+        cnt = d < k ? d : k;
+        int slot = lane < d ? lane : -1, rank = lane;  // deg <= k: every position, in order
+        int src = lane;                        // the lane holding slot `lane`'s draw
+        if (d > k) {                               // Floyd (regnn_sample_fill's spec)
+            slot = -1;
+            const int jl = d - k + lane;
+            const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
+                                               uint64_t(jl + 1)) >> 32) : 0;
+            for (int q = 0; q < k; ++q) {
+                const int pos = __shfl(my_pos, q, G);
+                const bool seen = (__ballot(slot == pos) & gmask) != 0;
+                if (lane == q) slot = seen ? d - k + q : pos;
+            }
+            rank = 0;
+            for (int m = 0; m < k; ++m) {
+                const int other = __shfl(slot, m, G);
+                rank += (lane < k && other < slot) ? 1 : 0;
+            }
+            for (int m = 0; m < k; ++m)            // inverse: slot j's draw
+                if (__shfl(rank, m, G) == lane) src = m;
+        }
+        // this lane's draw: a sampled edge (lane < cnt)
+        int my_t = 0, my_lo = 0, my_r = 0;     // table rows < 2^31 (checked by the host)
+        if (lane < cnt) {
+            const int p = b + slot;
+            const int u = A.idx[p];
+            const int64_t bp = base + rank;
+            my_r = A.etype[p];
+            my_t = A.ntype[u];
+            const int64_t lo = A.local[u];
+            my_lo = int(lo);
+            A.blk_rel[bp] = uint8_t(my_r);
+            A.e_type[bp] = my_t;
+            A.e_off[bp] = lo;
+        }
+        // slot order: lane j < cnt takes slot j's entry, lane cnt the self loop
+        int st = __shfl(my_t, src, G), sr = __shfl(my_r, src, G), slo = __shfl(my_lo, src, G);
+        if (lane == cnt) {
+            const int64_t bp = base + cnt;
+            st = A.ntype[t];
+            sr = A.n_et + st;
+            const int64_t lo = A.local[t];
+            slo = int(lo);
+            A.blk_rel[bp] = uint8_t(sr);
+            A.e_type[bp] = st;
+            A.e_off[bp] = lo;
+        }
+        if (lane == 0) {
+            A.scnt[i] = cnt;
+            A.inv[i] = 1.f / float(cnt + 1);
+        }
+        // ---- the row's input sums over its entries j = h, h + H, ..; lane l a float4 column
+        const int h = lane >> 5, l = lane & 31;
+        const int ne = cnt + 1;
+        float4 racc[NT];
+        float ws[NT];
+        int rt[NT];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ws[tt] = 0.f;
+            rt[tt] = -1;
+        }
+        float4 xs = make_float4(0.f, 0.f, 0.f, 0.f);
+        int rs = -1;
+        for (int j0 = 0; j0 < ne; j0 += H * kNsSumUN) {
+            int tj[kNsSumUN], rj[kNsSumUN];
+            float4 x[kNsSumUN];
+#pragma unroll
+            for (int u = 0; u < kNsSumUN; ++u) {
+                const int j = j0 + H * u + h;
+                const int jj = j < ne ? j : ne - 1;  // padding: a valid row, loaded, not added
+                tj[u] = __shfl(st, jj, G);
+                rj[u] = __shfl(sr, jj, G);
+                const int64_t lo = __shfl(slo, jj, G);
+                x[u] = *reinterpret_cast<const float4*>(pick_tab<NT>(A, tj[u]) + lo * K + 4 * l);
+                if (j >= ne) tj[u] = -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kNsSumUN; ++u) {
+                if (tj[u] < 0) continue;
+                if (rj[u] >= A.n_et) {             // the self loop (one per row)
+                    xs = x[u];
+                    rs = rj[u];
+                    continue;
+                }
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    if (tt != tj[u]) continue;
+                    ws[tt] += 1.f;
+                    rt[tt] = rj[u];
+                    racc[tt].x += x[u].x; racc[tt].y += x[u].y;
+                    racc[tt].z += x[u].z; racc[tt].w += x[u].w;
+                }
+            }
+        }
+        if constexpr (H == 2) {
+            // the two halves' sums (even / odd slots): half 0's first, the same bits in both
+            auto both = [&](float v) {
+                const float o = __shfl_xor(v, 32, 64);
+                return h == 0 ? v + o : o + v;
+            };
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                racc[tt] = make_float4(both(racc[tt].x), both(racc[tt].y), both(racc[tt].z),
+                                       both(racc[tt].w));
+                ws[tt] = both(ws[tt]);
+                rt[tt] = max(rt[tt], __shfl_xor(rt[tt], 32, 64));
+            }
+            const int rso = __shfl_xor(rs, 32, 64);
+            const float4 xo = make_float4(__shfl_xor(xs.x, 32, 64), __shfl_xor(xs.y, 32, 64),
+                                          __shfl_xor(xs.z, 32, 64), __shfl_xor(xs.w, 32, 64));
+            if (rs < 0) {
+                xs = xo;
+                rs = rso;
+            }
+        }
+        const int T = A.T;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+            if (tt < T && (H == 1 || (tt & 1) == h))
+                *reinterpret_cast<float4*>(A.s_agg + (int64_t(i) * T + tt) * K + 4 * l) = racc[tt];
+        if (H == 1 || h == 1) *reinterpret_cast<float4*>(A.u_self + int64_t(i) * K + 4 * l) = xs;
+        if (lane < T) {
+            float wv_ = 0.f;
+            int rv_ = -1;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt)
+                if (tt == lane) {
+                    wv_ = ws[tt];
+                    rv_ = rt[tt];
+                }
+            A.s_w[int64_t(i) * T + lane] = wv_;
+            A.u_rel[int64_t(i) * (T + 1) + lane] = rv_;
+        } else if (lane == T) {
+            A.u_rel[int64_t(i) * (T + 1) + T] = rs;
+        }
+    }
+    if (lane == 0) wsum[tl] = cnt + 1;         // edges of the row, self loop included
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int e = 0;
+#pragma unroll
+        for (int q = 0; q < kNsSumWaves * TPW; ++q) e += wsum[q];
+        if (e) {
+            atomicAdd(A.sizes + 8 + A.hop, e);
+            atomicAdd(reinterpret_cast<unsigned long long*>(A.state + 5), (unsigned long long)e);
+        }
+        if (blockIdx.x == 0) A.sizes[A.hop + 1] = n;
+    }
+}
+
 // row offsets (sampled count + the self loop), 1/in-count and the self-loop entries: one tile of
 // kNsRowsTile rows per block, the tiles' exclusive prefix by decoupled look-back (integer sums:
 // exact in any order). status[tile] = stamp << 32 | kind << 30 | value, kind 1 = the tile's own
@@ -512,6 +722,71 @@ ns_finish_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ s
     }
 }
 
+// The strided layout's de-duplication in one pass (ns_flags_kernel + ns_finish_kernel): tile t's
+// first-occurrence flags over its kNsTile slots, their count published in status[t] (stamp <<
+// 32 | kind << 30 | value, kind 1 = the tile's count, 2 = inclusive prefix, as ns_rows_kernel),
+// the exclusive prefix by decoupled look-back over the lower tiles (dispatched before this one),
+// then the tile's new nodes appended to n_id in slot order and their local ids written to g2l.
+// The last tile sets sizes[hop + 1]. A new node's flag is decided by its owning slot before any
+// block writes its g2l entry (only that slot writes it), so the one-pass order is safe.
+__global__ void __launch_bounds__(kBlock)
+ns_flags_finish_kernel(const int32_t* __restrict__ gsrc, int32_t* __restrict__ sizes, int hop,
+                       const int64_t* __restrict__ state, uint64_t* __restrict__ g2l,
+                       const uint64_t* __restrict__ first, uint64_t* __restrict__ status,
+                       int32_t* __restrict__ n_id, int cap_e) {
+    __shared__ int lds[kBlock / 64 + 1];
+    __shared__ int s_prefix;
+    const uint32_t stamp = ns_stamp(state, hop);
+    const int n = sizes[hop];
+    const int tile = blockIdx.x;
+    const int base = tile * kNsTile + threadIdx.x * 4;
+    int u[4], c = 0;
+    bool f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int bp = base + j;
+        u[j] = bp < cap_e ? gsrc[bp] : -2;
+        f[j] = u[j] >= 0 && uint32_t(g2l[u[j]] >> 32) != stamp &&
+               first[u[j]] == first_key(stamp, bp);
+        c += f[j] ? 1 : 0;
+    }
+    int total;
+    const int ex = block_exscan<kBlock>(c, lds, &total);
+    if (threadIdx.x == 0) {
+        int prefix = 0;
+        if (tile == 0) {
+            __hip_atomic_store(status, lb_pack(stamp, 2u, uint32_t(total)), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(status + tile, lb_pack(stamp, 1u, uint32_t(total)),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            for (int p = tile - 1; p >= 0;) {
+                const uint64_t st =
+                    __hip_atomic_load(status + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (uint32_t(st >> 32) != stamp) continue;            // not yet published
+                prefix += int(st & 0x3FFFFFFFu);
+                if (((st >> 30) & 3u) == 2u) break;
+                --p;
+            }
+            __hip_atomic_store(status + tile, lb_pack(stamp, 2u, uint32_t(prefix + total)),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_prefix = prefix;
+        if (tile == int(gridDim.x) - 1) sizes[hop + 1] = n + prefix + total;
+    }
+    __syncthreads();
+    int off = s_prefix + ex;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (f[j]) {
+            const int loc = n + off;
+            n_id[loc] = u[j];
+            g2l[u[j]] = (uint64_t(stamp) << 32) | uint32_t(loc);
+            ++off;
+        }
+    }
+}
+
 // every sampled edge's local source id (and, when asked, its source's node type and row in
 // that type's table, read beside the dedup table)
 __global__ void __launch_bounds__(kBlock)
@@ -612,6 +887,105 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
         const int slot = atomicAdd(cur + u, 1);
         csc_ent[slot] = (blk_row[bp] << 8) | int(blk_rel[bp]);
     }
+}
+
+// The transposed index built by many blocks (replaces the one-workgroup ns_csc_kernel on the
+// strided path): ns_resolve_csc_kernel resolves every slot's local source id (as
+// ns_resolve_kernel), takes the entry's rank in its source's segment from the counter's atomic
+// (crank), and the last block to finish (a ticket) scans the counts into csc_ptr, the hub list and
+// the piece table (ns_csc_kernel's first half); ns_csc_place_kernel then writes every entry at
+// csc_ptr[source] + rank. The order inside a segment follows the counters' atomics (unspecified,
+// as before: the consumer's sums are exact fixed-point).
+constexpr int kCscScanT = 1024;
+
+__device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
+                               int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_long) {
+    __shared__ int lds[kCscScanT / 64 + 1];
+    constexpr int IT = 8;
+    int carry = 0, lcarry = 0, pcarry = 0;
+    int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
+    for (int base = 0; base < n; base += kCscScanT * IT) {
+        const int i0 = base + threadIdx.x * IT;
+        int v[IT], s = 0, nl = 0, np = 0;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            v[j] = i0 + j < n ? __hip_atomic_load(csc_cnt + i0 + j, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) : 0;
+            s += v[j];
+            nl += v[j] > kCscShort ? 1 : 0;
+            np += v[j] > kCscShort ? (v[j] + kCscPiece - 1) / kCscPiece : 0;
+        }
+        int total, ltotal, ptotal;
+        int off = carry + block_exscan<kCscScanT>(s, lds, &total);
+        int loff = lcarry + block_exscan<kCscScanT>(nl, lds, &ltotal);
+        int poff = pcarry + block_exscan<kCscScanT>(np, lds, &ptotal);
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            if (i0 + j < n) {
+                csc_ptr[i0 + j] = off;
+                if (v[j] > kCscShort) {
+                    const int li = loff++;
+                    csc_long[1 + li] = i0 + j;
+                    const int npc = (v[j] + kCscPiece - 1) / kCscPiece;
+                    for (int k = 0; k < npc; ++k, ++poff)
+                        pieces[poff] = make_int4(i0 + j, off + k * kCscPiece,
+                                                 min(kCscPiece, v[j] - k * kCscPiece),
+                                                 (li << 16) | (k << 8) | npc);
+                }
+            }
+            off += v[j];
+        }
+        carry += total;
+        lcarry += ltotal;
+        pcarry += ptotal;
+    }
+    if (threadIdx.x == 0) {
+        csc_ptr[n] = carry;
+        csc_long[0] = lcarry;
+        csc_long[REGNN_CSC_LONG_NPIECE] = pcarry;
+    }
+}
+
+__global__ void __launch_bounds__(kCscScanT)
+ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes,
+                      int hop, const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx,
+                      int cap_e, int32_t* __restrict__ csc_cnt, int32_t* __restrict__ crank,
+                      int32_t* __restrict__ ticket, int32_t* __restrict__ csc_ptr,
+                      int32_t* __restrict__ csc_long) {
+    __shared__ bool last;
+    const int bp = blockIdx.x * kCscScanT + threadIdx.x;
+    if (bp < cap_e) {
+        const int u = gsrc[bp];
+        if (u != -2) {                     // -2: an empty slot of the strided layout
+            int lid;
+            if (u < 0) {                   // the self loop
+                lid = blk_idx[bp];
+            } else {
+                lid = int32_t(uint32_t(g2l[u]));
+                blk_idx[bp] = lid;
+            }
+            crank[bp] = atomicAdd(csc_cnt + lid, 1);     // integer: exact in any order
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == int(gridDim.x) - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    csc_scan_block(csc_cnt, sizes[hop + 1], csc_ptr, csc_long);
+    if (threadIdx.x == 0) *ticket = 0;     // for the next hop / step
+}
+
+__global__ void __launch_bounds__(kBlock)
+ns_csc_place_kernel(const int32_t* __restrict__ blk_idx, const int32_t* __restrict__ blk_row,
+                    const uint8_t* __restrict__ blk_rel, const int32_t* __restrict__ crank,
+                    const int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_ent, int cap_e) {
+    const int bp = blockIdx.x * kBlock + threadIdx.x;
+    if (bp >= cap_e) return;
+    const int u = blk_idx[bp];
+    if (u < 0) return;                     // an empty slot
+    csc_ent[csc_ptr[u] + crank[bp]] = (blk_row[bp] << 8) | int(blk_rel[bp]);
 }
 
 // Backward of the sampled block's mean aggregation y[v] = s[v] sum_e tab[rel_e] x[idx_e] + b
@@ -999,12 +1373,23 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         REGNN_LAUNCH_CHECK();
         if (lean) return REGNN_OK;
         const int ce = int(cap_e);
-        hipLaunchKernelGGL(ns_flags_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes,
-                           hop, state, g2l, first, flag, tiles, n_tiles, ce);
+        // de-duplication in one pass (status: >= n_tiles entries on this path)
+        hipLaunchKernelGGL(ns_flags_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc,
+                           sizes, hop, state, g2l, first, status, n_id, ce);
         REGNN_LAUNCH_CHECK();
-        hipLaunchKernelGGL(ns_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc, sizes,
-                           hop, state, flag, tiles, g2l, n_id, ce);
-        REGNN_LAUNCH_CHECK();
+        if (csc && !edge_type) {
+            // the transposed index by many blocks: resolve + counts + ranks (the last block
+            // scans), then the placement (samp holds each slot's rank: >= cap_e entries)
+            hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
+                               dim3(kCscScanT), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce,
+                               csc_cnt, samp, tiles, csc_ptr, csc_long);
+            REGNN_LAUNCH_CHECK();
+            hipLaunchKernelGGL(ns_csc_place_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
+                               dim3(kBlock), 0, stream, blk_idx, blk_row, blk_rel, samp, csc_ptr,
+                               csc_ent, ce);
+            REGNN_LAUNCH_CHECK();
+            return REGNN_OK;
+        }
         hipLaunchKernelGGL(ns_resolve_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce, ntype,
                            local, edge_type, edge_off, csc_cnt, 1);
@@ -1046,6 +1431,44 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                            blk_row, blk_rel, csc_cnt, csc_ptr, csc_ent, csc_long, 0);
         REGNN_LAUNCH_CHECK();
     }
+    return REGNN_OK;
+}
+
+int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
+                            const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
+                            int64_t* state, int32_t* sizes, const int32_t* n_id, int32_t cap_dst,
+                            int32_t* scnt, uint8_t* blk_rel, float* inv, const int64_t* local,
+                            int32_t* edge_type, int64_t* edge_off, const float* const* tables,
+                            int32_t n_types, int32_t K, float* s_agg, float* s_w, float* u_self,
+                            int32_t* u_rel, hipStream_t stream) {
+    if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !scnt || !blk_rel ||
+        !inv || !local || !edge_type || !edge_off || !tables || !s_agg || !s_w || !u_self ||
+        !u_rel || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
+        return REGNN_EINVAL;
+    if (K != kNsSumK || n_types < 1 || n_types > 4 || k < 1 || k > 63) return REGNN_EUNSUPPORTED;
+    if (int64_t(cap_dst) * (k + 1) >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
+    NsSumArgs A{};
+    A.ptr = ptr; A.idx = idx; A.etype = etype; A.ntype = ntype; A.local = local;
+    A.n_et = num_edge_types; A.n_id = n_id; A.sizes = sizes; A.hop = hop; A.cap = cap_dst;
+    A.k = k; A.state = state; A.scnt = scnt; A.blk_rel = blk_rel; A.inv = inv;
+    A.e_type = edge_type; A.e_off = edge_off; A.T = n_types;
+    for (int t = 0; t < n_types; ++t) {
+        if (!tables[t] || reinterpret_cast<uintptr_t>(tables[t]) % 16) return REGNN_EINVAL;
+        A.xt[t] = tables[t];
+    }
+    for (int t = n_types; t < 8; ++t) A.xt[t] = tables[0];
+    if (reinterpret_cast<uintptr_t>(s_agg) % 16 || reinterpret_cast<uintptr_t>(u_self) % 16)
+        return REGNN_EINVAL;
+    A.s_agg = s_agg; A.s_w = s_w; A.u_self = u_self; A.u_rel = u_rel;
+    if (k + 1 <= 32)                   // two rows per wave (32 lanes each): sums in slot order
+        hipLaunchKernelGGL((ns_sample_sums_kernel<32, 4>),
+                           dim3(unsigned((cap_dst + 2 * kNsSumWaves - 1) / (2 * kNsSumWaves))),
+                           dim3(64 * kNsSumWaves), 0, stream, A);
+    else
+        hipLaunchKernelGGL((ns_sample_sums_kernel<64, 4>),
+                           dim3(unsigned((cap_dst + kNsSumWaves - 1) / kNsSumWaves)),
+                           dim3(64 * kNsSumWaves), 0, stream, A);
+    REGNN_LAUNCH_CHECK();
     return REGNN_OK;
 }
 

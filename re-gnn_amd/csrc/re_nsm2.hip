@@ -43,7 +43,7 @@ inline int env_blocks(const char* name, int dflt) {
     return v >= 16 && v <= 4096 ? v : dflt;
 }
 static const int kBwdBlocks = env_blocks("REGNN_NSM_BWD_BLOCKS", 128);
-constexpr int kMaxCT = 27;                 // class tiles of 16 (the head's LDS holds C <= 416)
+constexpr int kMaxCT = 27;                 // class tiles of 16 (the head's LDS holds C <= 384)
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
 
@@ -423,8 +423,12 @@ inline size_t agg0w_lds(int T) {          // St [16][T K + 4] | sw [16][MT] | Pt
     return (size_t(16) * (T * 128 + 4) + 16 * MT + 16 * 68 + 16 * F + 16 * F) * sizeof(float);
 }                                         // at [16][64] | red [16][64]
 
-template <int NT, bool RS>
+// PRE (relation slots): the row's per-type input sums, counts, self row and slot relations were
+// formed by the sampler (regnn_ns_hop_typed_sums into s_agg / s_w / u_self / u_rel): the gather
+// phase is one round of contiguous loads, and nothing of them is written here
+template <int NT, bool RS, bool PRE = false>
 __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
+    static_assert(!PRE || RS, "the sampler's sums need relation slots");
     constexpr int K = 128, HB = K / 32;    // float4 steps per half type (stage 1)
     extern __shared__ float sm[];
     PH(0, 12);
@@ -474,7 +478,22 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
         racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     int e0 = 0, e1 = 0;
-    if (rv) row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
+    if constexpr (PRE) {
+        if (rv) {
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                if (tt < T) {
+                    racc[tt] = *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l);
+                    wsum[tt] = A.s_w[int64_t(v) * T + tt];
+                    rel_t[tt] = A.u_rel[int64_t(v) * (T + 1) + tt];
+                }
+            }
+            xself = *reinterpret_cast<const float4*>(A.u_self + int64_t(v) * K + 4 * l);
+            r_self = A.u_rel[int64_t(v) * (T + 1) + T];
+        }
+    } else if (rv) {
+        row_range(A.ptr, A.cnt, A.stride, v, e0, e1);
+    }
     for (int c0 = e0; c0 < e1; c0 += 32) {
         const int m = min(32, e1 - c0);
         int my_t = 0, my_lo = 0, my_r = 0;  // table rows < 2^31 (checked by the host)
@@ -551,18 +570,18 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
                 sv = make_float4(fmaf(ws, xself.x, wr * sv.x), fmaf(ws, xself.y, wr * sv.y),
                                  fmaf(ws, xself.z, wr * sv.z), fmaf(ws, xself.w, wr * sv.w));
             *reinterpret_cast<float4*>(St + sub * SR + tt * K + 4 * l) = sv;
-            if (rv)
+            if (rv && !PRE)
                 *reinterpret_cast<float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l) = racc[tt];
             if (l == 0) {
                 sw[sub * MT + tt] = RS ? fmaf(wr, wsum[tt], ws) : wsum[tt];
-                if (rv) {
+                if (rv && !PRE) {
                     A.s_w[int64_t(v) * T + tt] = wsum[tt];
                     if constexpr (RS) A.u_rel[int64_t(v) * (T + 1) + tt] = rel_t[tt];
                 }
             }
         }
     }
-    if constexpr (RS) {
+    if constexpr (RS && !PRE) {
         if (rv) {
             *reinterpret_cast<float4*>(A.u_self + int64_t(v) * K + 4 * l) = xself;
             if (l == 0) A.u_rel[int64_t(v) * (T + 1) + T] = r_self;
@@ -714,14 +733,19 @@ __host__ __device__ inline int head_wl(int C) {
 }
 inline size_t head_lds(int C) {
     return (size_t(head_wl(C)) + 16 * head_cp(C) + 16 * 68 + 16 * 80 + 16 * 68 + 16 * 68 +
-            16 * 68) * sizeof(float);
+            3 * 16 * 68) * sizeof(float);
 }
 
 __device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c & 15) << 2)); }
 
-// 8 waves: the row phases (16 rows x 16 lanes) run on threads 0..255, the class-tile loops (logits,
-// gh, the out_lin partial) on all 8 waves
-constexpr int kHeadThreads = 512;
+// 16 waves: the row phases (16 rows x 16 lanes) run on threads 0..255, the class-tile loops
+// (logits, gh) and the softmax (64 lanes per row) on all 16 waves; out_lin.weight's LDS-DMA
+// staging on waves 4..15 under the aggregation
+constexpr int kHeadThreads = 1024;
+constexpr int kHeadW = kHeadThreads / 64;  // waves
+constexpr int kHeadSL = kHeadThreads / 16; // softmax lanes per row
+constexpr int kHeadNQ = kHeadW / 4;        // gh: class parts (4 feature tiles x kHeadNQ)
+static_assert(kHeadNQ == 4 && kHeadSL == 64, "step 4c / 4d sum four class parts; 4b a wave per row");
 
 __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     extern __shared__ float hl[];
@@ -732,14 +756,14 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     float* hs2 = hs + 16 * 68;             // [16][80]: h (column reads)
     float* ghs = hs2 + 16 * 80;            // [16][68]: a, then gh
     float* hg = ghs + 16 * 68;             // [16][68]: Hagg
-    float* ghp = hg + 16 * 68;             // [16][68]: gh over the second half of the classes
+    float* ghp = hg + 16 * 68;             // [16][68] x 3: gh over class parts 1 .. 3
     float* red = Wl;
     __shared__ float lrow[kRows];
     __shared__ float bo_s[16 * kMaxCT];    // out_lin.bias (classes >= C: 0)
     const bool rowt = threadIdx.x < kBlock;    // the row phases' threads
     const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 15, gl = threadIdx.x & 48;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, q = lane >> 4;
-    const int wq = w & 3, wh = w >> 2;        // feature tile, class half (step 4c)
+    const int wq = w & 3, wh = w >> 2;        // feature tile, class part (step 4c)
     PH(1, 12);
     PE(1, 0);
     const int n = A.sizes[0];
@@ -748,7 +772,7 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     // Order of the global requests: the aggregation's chain first (nothing waits behind the
     // staging), then step 2 / 3's operands, then out_lin's LDS-DMA; the barriers up to step 4a
     // order LDS only (lds_sync), so the DMA lands under steps 1-3.
-    const int r32 = threadIdx.x >> 5, l32 = threadIdx.x & 31;   // step 4b: 32 lanes per row
+    const int r32 = threadIdx.x / kHeadSL, l32 = threadIdx.x % kHeadSL;   // step 4b: a row's lanes
     const int v32 = blockIdx.x * kRows + r32;
     const int nid32 = v32 < n ? A.n_id[v32] : -1;
     PH(1, 0);
@@ -798,7 +822,7 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
         // W[c][4 ((L%16) ^ (c & 15)) ..] (head_sw); pad rows c >= C read row C-1
         // by LDS-DMA: vmcnt is per wave, so only these four waves wait for it (at the barrier)
         const int L64 = threadIdx.x & 63;
-        for (int i = w - 4; i < CT * 4; i += 4) {
+        for (int i = w - 4; i < CT * 4; i += kHeadW - 4) {
             const int c = 4 * i + (L64 >> 4);
             const int cs = c < C ? c : C - 1;
             const float* src = A.w_out + int64_t(cs) * F + 4 * ((L64 & 15) ^ (c & 15));
@@ -883,27 +907,27 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     }
     __syncthreads();
     PH(1, 8);
-    // ---- 4b. log_softmax, nll, g: lane l32 of row r32 holds classes l32 + 32 i (all 8 waves)
+    // ---- 4b. log_softmax, nll, g: lane l32 of row r32 holds classes l32 + SL i (all waves)
     {
-        constexpr int NI = (16 * kMaxCT + 31) / 32;
+        constexpr int NI = (16 * kMaxCT + kHeadSL - 1) / kHeadSL;
         const int CW = 16 * CT;                // classes >= C hold -inf
         float zr[NI];
         float zmax = -INFINITY;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int c = l32 + 32 * i;
+            const int c = l32 + kHeadSL * i;
             zr[i] = c < CW ? zs[r32 * CP + c] : -INFINITY;
             zmax = fmaxf(zmax, zr[i]);
         }
 #pragma unroll
-        for (int o = 16; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
+        for (int o = kHeadSL / 2; o > 0; o >>= 1) zmax = fmaxf(zmax, __shfl_xor(zmax, o, 64));
         float se = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             zr[i] = expf(zr[i] - zmax);        // classes >= C: exp(-inf) = 0
             se += zr[i];
         }
-        se = group_sum<32>(se);
+        se = group_sum<kHeadSL>(se);
         const float lse = zmax + logf(se), rse = 1.f / se;
         const bool ok = v32 < n;
         const float zy = y >= 0 ? zs[r32 * CP + y] : 0.f;
@@ -911,17 +935,17 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
         const float inv_n = y >= 0 && nvalid > 0.f ? 1.f / nvalid : 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int c = l32 + 32 * i;
+            const int c = l32 + kHeadSL * i;
             if (c < CW)
                 zs[r32 * CP + c] = ok && c < C ? (zr[i] * rse - (int64_t(c) == y ? 1.f : 0.f)) * inv_n : 0.f;
         }
     }
     __syncthreads();
     PH(1, 9);
-    // ---- 4c. gh = g W: wave w -> features 16 wq + cc, rows 4 q + r, class tiles of half wh
+    // ---- 4c. gh = g W: wave w -> features 16 wq + cc, rows 4 q + r, class tiles of part wh
     {
         const int k = 16 * wq + cc;
-        const int cth = (CT + 1) / 2, b0 = wh ? cth : 0, b1 = wh ? CT : cth;
+        const int ctp = (CT + kHeadNQ - 1) / kHeadNQ, b0 = min(CT, wh * ctp), b1 = min(CT, b0 + ctp);
         auto step = [&](int b, f32x4 d) {
             const float4 av = *reinterpret_cast<const float4*>(zs + cc * CP + 16 * b + 4 * q);
             const int c0 = 16 * b + 4 * q;
@@ -937,7 +961,7 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
             dg1 = step(b + 1, dg1);
         }
         if (b < b1) dg0 = step(b, dg0);
-        float* gd = wh ? ghp : ghs;
+        float* gd = wh ? ghp + (wh - 1) * 16 * 68 : ghs;
 #pragma unroll
         for (int r = 0; r < 4; ++r) gd[(4 * q + r) * 68 + k] = dg0[r] + dg1[r];
     }
@@ -949,9 +973,13 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     for (int b = 0; b < 4; ++b)
         w1r[b] = *reinterpret_cast<const float4*>(A.w1 + (16 * wq + cc) * F + 16 * b + 4 * q);
     if (rowt) {
+        // the class parts' gh in a fixed order: (0 + 1) + (2 + 3)
         const float4 ga4 = *reinterpret_cast<const float4*>(ghs + sub * 68 + 4 * l);
         const float4 gb4 = *reinterpret_cast<const float4*>(ghp + sub * 68 + 4 * l);
-        const float g[4] = {ga4.x + gb4.x, ga4.y + gb4.y, ga4.z + gb4.z, ga4.w + gb4.w};
+        const float4 gc4 = *reinterpret_cast<const float4*>(ghp + 16 * 68 + sub * 68 + 4 * l);
+        const float4 gd4 = *reinterpret_cast<const float4*>(ghp + 2 * 16 * 68 + sub * 68 + 4 * l);
+        const float g[4] = {(ga4.x + gb4.x) + (gc4.x + gd4.x), (ga4.y + gb4.y) + (gc4.y + gd4.y),
+                            (ga4.z + gb4.z) + (gc4.z + gd4.z), (ga4.w + gb4.w) + (gc4.w + gd4.w)};
         float gy[4], gx[4];
         float p1 = 0.f, p2 = 0.f;
 #pragma unroll
@@ -1291,8 +1319,14 @@ __global__ void __launch_bounds__(kGathT) gather_kernel(GathArgs A) {
         if (threadIdx.x < F) lgh[threadIdx.x] = 0ull;
         __syncthreads();
     }
-    // ---- rows with <= kShort edges: one group each
-    for (int u = blockIdx.x * kGathG + grp; u < n; u += gridDim.x * kGathG) {
+    // ---- rows with <= kShort edges: one group each, on the blocks without a hub piece (piece j
+    // runs on block grid - 1 - j): a hub block's short row would wait behind its piece (the
+    // kernel's tail), so the short rows go to the other blocks while they can hold them all
+    const int hub_blocks = min(n_piece, int(gridDim.x));
+    int sblocks = int(gridDim.x) - hub_blocks;
+    if (sblocks * kGathG < n) sblocks = int(gridDim.x);  // too few: every block takes short rows
+    if (int(blockIdx.x) >= sblocks) sblocks = 0;        // (block-uniform) a hub block: none
+    for (int u = blockIdx.x * kGathG + grp; sblocks && u < n; u += sblocks * kGathG) {
         const int c0 = A.cptr[u], m = A.cptr[u + 1] - c0;
         if (m > kShort) continue;              // a hub: its pieces above
         const RowIn R = row_in(A, key, u, l, lw, lb);
@@ -2041,6 +2075,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         xt.p[t] = p->x_tab[t];
     }
     const bool first = w->part != 2, second = w->part != 1;
+    // layer 0's input sums formed by the sampler (regnn_ns_hop_typed_sums)
+    const bool pre = w->pre_sums != 0;
     // 1. layer 0
     if (first) {
         const int h = 1;
@@ -2058,18 +2094,19 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         A.n_et = p->n_edge_types; A.u_self = w->u_self; A.u_rel = w->u_rel;
         A.n_id = w->n_id; A.labels = w->labels; A.nvalid = w->nvalid;
         int grid = (w->cap[h] + 15) / 16;
-        if (K == 128 && T <= 4 && !getenv("REGNN_NSM_AGG0_OLD")) {  // every tile its own block
+        if (pre && (K != 128 || T > 4 || !rs)) return REGNN_EINVAL;
+        if (K == 128 && T <= 4 && (pre || !getenv("REGNN_NSM_AGG0_OLD"))) {  // every tile its own block
             grid = (w->cap[h] + kAggRows - 1) / kAggRows;
             const size_t lds = agg0w_lds(T);
-#define AGG0W_CASE(NN, RS)                                                                     \
-            if (rs == RS) {                                                                    \
+#define AGG0W_CASE(NN, RS, PRE)                                                                \
+            if (rs == RS && pre == PRE) {                                                      \
                 static size_t done = 0;                                                        \
-                if (!set_lds(reinterpret_cast<const void*>(&agg0w_kernel<NN, RS>), lds, &done)) \
+                if (!set_lds(reinterpret_cast<const void*>(&agg0w_kernel<NN, RS, PRE>), lds, &done)) \
                     return REGNN_EUNSUPPORTED;                                                 \
-                hipLaunchKernelGGL((agg0w_kernel<NN, RS>), dim3(grid), dim3(kAggW), lds, stream, A); \
+                hipLaunchKernelGGL((agg0w_kernel<NN, RS, PRE>), dim3(grid), dim3(kAggW), lds, stream, A); \
                 REGNN_LAUNCH_CHECK();                                                          \
             } else
-            AGG0W_CASE(4, true) AGG0W_CASE(4, false)
+            AGG0W_CASE(4, true, true) AGG0W_CASE(4, true, false) AGG0W_CASE(4, false, false)
                 return REGNN_EUNSUPPORTED;
 #undef AGG0W_CASE
         } else {

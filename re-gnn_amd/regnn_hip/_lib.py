@@ -64,12 +64,13 @@ _SIG = {
     "regnn_head_bwd_z": ([P, I64, I32, I64, I32, P, P, P, P, I64, P, I32, P, P, F32, P, P, P, P,
                           I32, P], ctypes.c_int),
     "regnn_head_argmax": ([P, I64, I32, P, P, I32, P, P], ctypes.c_int),
-    "regnn_gatv2_score_fwd": ([P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
-    "regnn_gatv2_score_bwd_dst": ([P, P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P],
+    "regnn_gatv2_score_fwd": ([P, P, P, P, P, I64, I32, I32, F32, P, P, P], ctypes.c_int),
+    "regnn_gatv2_score_bwd_dst": ([P, P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P, P],
                                   ctypes.c_int),
-    "regnn_gatv2_score_bwd_src": ([P, P, P, P, P, P, P, I64, I32, I32, F32, P, P], ctypes.c_int),
-    "regnn_edge_softmax_fwd": ([P, P, P, P, P, F32, I64, I32, P, P], ctypes.c_int),
-    "regnn_edge_softmax_bwd": ([P, P, P, P, I64, I32, P, P, I32, P], ctypes.c_int),
+    "regnn_gatv2_score_bwd_src": ([P, P, P, P, P, P, P, I64, I32, I32, F32, P, P, P],
+                                  ctypes.c_int),
+    "regnn_edge_softmax_fwd": ([P, P, P, P, P, F32, I64, I32, P, P, P], ctypes.c_int),
+    "regnn_edge_softmax_bwd": ([P, P, P, P, I64, I32, P, P, I32, P, P], ctypes.c_int),
     "regnn_gat_scores": ([P, P, P, P, P, P, I64, I32, F32, P, P], ctypes.c_int),
     "regnn_rel_reduce": ([P, I64, I32, P, I32, P], ctypes.c_int),
     "regnn_gat_softmax_fwd": ([P, P, P, P, P, P, I64, I32, F32, P, P, P], ctypes.c_int),
@@ -95,6 +96,8 @@ _SIG = {
     "regnn_ns_batch": ([P, I64, I32, I32, I32, P, P, P, P, P], ctypes.c_int),
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
+    "regnn_ns_hop_typed_sums": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P,
+                                 I32, I32, P, P, P, P, P], ctypes.c_int),
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_ns_csc_hub_work_floats": ([I32], I64),
     "regnn_ns_spmm_bwd_csc": ([P, P, P, P, P, P, P, P, P, I32, P, I32, I64, I32, I32, P, P],
@@ -123,7 +126,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 40
+ABI_VERSION = 41
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

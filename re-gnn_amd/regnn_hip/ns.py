@@ -119,9 +119,11 @@ class DeviceSampler:
             ce = cd * (k + 1)
             nt = (ce + 1023) // 1024
             z = lambda n, dt=torch.int32: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
-            self.hop_bufs.append(dict(samp=z(cd * k), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
+            # samp: the strided transposed index's per-slot ranks too (>= ce); status: the
+            # strided de-duplication's look-back too (>= ceil(ce / 1024) tiles)
+            self.hop_bufs.append(dict(samp=z(ce), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
                                       flag=z(ce, torch.uint8), tiles=z(nt + 1),
-                                      status=z((cd + 1023) // 1024, torch.int64)))
+                                      status=z(max((cd + 1023) // 1024, nt), torch.int64)))
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
                           torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev,
                           row=z(ce))
@@ -137,6 +139,9 @@ class DeviceSampler:
         # meta_only[h]: hop h writes only the edge meta its consumer reads (regnn_ns_hop
         # meta_only: no de-duplication, n_id not extended, sampled blk_idx unwritten)
         self.meta_only = [False] * len(self.sizes_k)
+        # typed_sums[h]: hop h (meta-only, strided) also forms layer 0's input sums for the
+        # fused step (regnn_ns_hop_typed_sums; FusedStep.enable_pre_sums), or None
+        self.typed_sums = [None] * len(self.sizes_k)
         self._csr_fresh = True
 
     def enable_edge_meta(self, local_node_idx, hop):
@@ -174,6 +179,19 @@ class DeviceSampler:
         rg = self.rg
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
+            ts = self.typed_sums[h]
+            if (ts is not None and strided and meta_only and self.meta_only[h] and
+                    self.edge_meta[h] is not None):
+                et, eo = self.edge_meta[h]
+                L.call("regnn_ns_hop_typed_sums", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                       L.ptr(self.etype_csr), L.ptr(self.ntype), self.num_edge_types, k, h,
+                       L.ptr(self.state), L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h],
+                       L.ptr(b["scnt"]), L.ptr(blk.rel), L.ptr(blk.inv), L.ptr(self.local),
+                       L.ptr(et), L.ptr(eo), ts["tables"], ts["T"], ts["K"],
+                       L.ptr(ts["s_agg"]), L.ptr(ts["s_w"]), L.ptr(ts["u_self"]),
+                       L.ptr(ts["u_rel"]), L.stream())
+                self.meta_fresh[h] = True
+                continue
             L.call("regnn_ns_hop", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(self.etype_csr),
                    L.ptr(self.ntype), self.num_edge_types, k, h, L.ptr(self.state),
                    L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h], L.ptr(self.g2l),
@@ -280,7 +298,8 @@ class _NsmWork(ctypes.Structure):
                 ("u_self", _P), ("u_rel", _P), ("p0", _P), ("adam", _P), ("gh1", _P),
                 ("csc_ptr0", _P), ("csc_ent0", _P), ("csc_long0", _P),
                 ("stride", ctypes.c_int32 * _ML), ("blk_cnt", _P * _ML), ("part", ctypes.c_int32),
-                ("hub_acc", _P), ("hub_ticket", _P), ("hub_terms", _P), ("split_finalize", ctypes.c_int32)]
+                ("hub_acc", _P), ("hub_ticket", _P), ("hub_terms", _P), ("split_finalize", ctypes.c_int32),
+                ("pre_sums", ctypes.c_int32)]
 
 # include/regnn_hip.h REGNN_CSC_LONG_*: hub rows of a <= 32768-edge block, their <= 1024-entry
 # pieces, and the csc_long buffer holding ids + piece table
@@ -300,8 +319,8 @@ class _NsmAdam(ctypes.Structure):
                 ("step", _P), ("ticket", _P)]
 
 
-# regnn_nsm_step's two-layer form (re_nsm2.hip): L = 2 and at most 416 classes (its head's LDS)
-TWO_LAYER_MAX_CLASSES = 416
+# regnn_nsm_step's two-layer form (re_nsm2.hip): L = 2 and at most 384 classes (its head's LDS)
+TWO_LAYER_MAX_CLASSES = 384
 
 
 def fused_unsupported(model, x_dict):
@@ -377,6 +396,10 @@ MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
 # "on": the fused step's last sampler hop runs meta-only (no dedup / n_id append); "off": the
 # full hop (tests that inspect the outermost n_id / local ids)
 LEAN_LAST_HOP = {"mode": "on"}
+# "on": with relation slots (K = 128, T <= 4) the fused step's outer hop also forms layer 0's
+# per-type input sums (regnn_ns_hop_typed_sums) on the sampler's stream, ahead of the model, and
+# agg0 reads them (regnn_nsm_work.pre_sums); "off": agg0 gathers the raw rows itself (A/B, tests)
+PRE_SUMS = {"mode": os.environ.get("REGNN_NS_PRE_SUMS", "on")}
 
 
 def relation_slots_ok(sampler, T):
@@ -516,6 +539,21 @@ class FusedStep:
         self.slab = z(_slab_floats(P, caps[0]))
         W.slab = ptr(self.slab)
         self.model, self.sampler, self.n_layers = model, sampler, nl
+        # layer 0's parameter-free input sums on the sampler (it runs ahead of the model on its
+        # own stream): the outer hop writes them straight into this step's s_agg / s_w / u_self
+        # / u_rel and agg0 reads them instead of gathering the raw input rows
+        if (PRE_SUMS["mode"] != "off" and self.two_layer and P.rel_slots and K == 128 and
+                T <= 4 and sampler.strided and sampler.meta_only[nl - 1] and
+                max(sampler.sizes_k) <= 63):
+            self._tables = (ctypes.c_void_p * T)(*[x_dict[k].data_ptr() for k in keys])
+            sampler.typed_sums[nl - 1] = dict(
+                tables=self._tables, T=T, K=K, s_agg=self._buf(W.s_agg), s_w=self._buf(W.s_w),
+                u_self=self._buf(W.u_self), u_rel=self._buf(W.u_rel))
+            W.pre_sums = 1
+
+    def _buf(self, addr):
+        """the kept tensor whose data starts at addr."""
+        return next(t for t in self.keep if torch.is_tensor(t) and t.data_ptr() == addr)
 
     def attach_adam(self, opt, grad_flat):
         """the optimizer step joins the last launch (two-layer step): Adam on each parameter

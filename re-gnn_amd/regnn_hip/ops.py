@@ -829,8 +829,9 @@ class _GatAttention(torch.autograd.Function):
             L.call("regnn_gat_scores", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), rel, L.ptr(t),
                    L.ptr(el), L.ptr(er), rg.n_dst, H, float(slope), L.ptr(s), L.stream())
             gmax = s.amax().reshape(1) if s.numel() else torch.zeros(1, device=el.device)
+            gp = _GatPlan(getattr(rg, "csr_plan", None), 2 * H, el.device)
             L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), None, None,
-                   L.ptr(gmax), 1e-16, rg.n_dst, H, L.ptr(a), L.stream())
+                   L.ptr(gmax), 1e-16, rg.n_dst, H, L.ptr(a), gp.ptr, L.stream())
         else:
             gp = _GatPlan(getattr(rg, "csr_plan", None), 2 * H, el.device)
             with timed("gat_softmax_fwd", rg.E * (5 + 12 * H) + rg.n_dst * 8 * H):
@@ -884,9 +885,11 @@ class _GatV2Score(torch.autograd.Function):
         fs, fd = fs.contiguous().float(), fd.contiguous().float()
         a = att.detach().reshape(H * D).contiguous().float()
         s = torch.empty(rg.E, H, dtype=torch.float32, device=fs.device)
+        gp = _GatPlan(getattr(rg, "csr_plan", None), 0, fs.device)     # hub rows as chunks
         with timed("gatv2_score_fwd", rg.E * (H * D * 4 + 4 * H + 4) + rg.n_dst * H * D * 4):
             L.call("regnn_gatv2_score_fwd", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(fs),
-                   L.ptr(fd), L.ptr(a), rg.n_dst, H, D, float(slope), L.ptr(s), L.stream())
+                   L.ptr(fd), L.ptr(a), rg.n_dst, H, D, float(slope), L.ptr(s), gp.ptr,
+                   L.stream())
         ctx.rg, ctx.slope, ctx.att_shape = rg, slope, att.shape
         ctx.save_for_backward(fs, fd, a)
         return s
@@ -899,14 +902,18 @@ class _GatV2Score(torch.autograd.Function):
         gs = gs.contiguous().float()
         gfd = torch.empty_like(fd)
         gfs = torch.empty_like(fs)
-        rows = L.slab_rows() // 2
+        gp = _GatPlan(getattr(rg, "csr_plan", None), H * D, fs.device)
+        gq = _GatPlan(getattr(rg, "csc_plan", None), H * D, fs.device)
+        # with hub chunks the per-segment and the chunk pass take half the slab rows each
+        rows = L.slab_rows() // (1 if gp.ptr is not None else 2)
         slab = torch.zeros(rows, H * D, dtype=torch.float32, device=fs.device)
-        L.call("regnn_gatv2_score_bwd_dst", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(fs),
-               L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_dst, H, D, float(slope), L.ptr(gfd),
-               L.ptr(slab), rows, L.stream())
-        L.call("regnn_gatv2_score_bwd_src", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
-               L.ptr(rg.csc2csr), L.ptr(fs), L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_src, H, D,
-               float(slope), L.ptr(gfs), L.stream())
+        with timed("gatv2_score_bwd", 2 * rg.E * (H * D * 4 + 4 * H + 8) + 3 * rg.n_dst * H * D * 4):
+            L.call("regnn_gatv2_score_bwd_dst", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(fs),
+                   L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_dst, H, D, float(slope), L.ptr(gfd),
+                   L.ptr(slab), rows, gp.ptr, L.stream())
+            L.call("regnn_gatv2_score_bwd_src", L.ptr(rg.csc_ptr), L.ptr(rg.csc_idx),
+                   L.ptr(rg.csc2csr), L.ptr(fs), L.ptr(fd), L.ptr(a), L.ptr(gs), rg.n_src, H, D,
+                   float(slope), L.ptr(gfs), gq.ptr, L.stream())
         g_att = _reduce(slab, H * D).view(ctx.att_shape)
         return gfs, gfd, g_att, None, None
 
@@ -931,8 +938,11 @@ class _EdgeSoftmax(torch.autograd.Function):
         if global_max:
             z = s if t is None else s + t[rel.long()]
             gmax = z.amax().reshape(1) if z.numel() else torch.zeros(1, device=s.device)
-        L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), L.ptr(rel), L.ptr(t),
-               L.ptr(gmax), 1e-16 if global_max else 0.0, rg.n_dst, H, L.ptr(a), L.stream())
+        gp = _GatPlan(getattr(rg, "csr_plan", None), 2 * H, s.device)
+        with timed("edge_softmax_fwd", rg.E * (8 * H + 1) + rg.n_dst * 8):
+            L.call("regnn_edge_softmax_fwd", L.ptr(rg.csr_ptr), L.ptr(s), L.ptr(rel), L.ptr(t),
+                   L.ptr(gmax), 1e-16 if global_max else 0.0, rg.n_dst, H, L.ptr(a), gp.ptr,
+                   L.stream())
         ctx.rg, ctx.pack = rg, pack
         ctx.tab_shape = None if ee_tab is None else ee_tab.shape
         ctx.save_for_backward(a)
@@ -946,10 +956,12 @@ class _EdgeSoftmax(torch.autograd.Function):
         need_tab = ctx.tab_shape is not None and ctx.needs_input_grad[1]
         n_rel = ctx.tab_shape[0] if need_tab else 0
         slab = _slab(n_rel * H, a.device) if need_tab else None
-        L.call("regnn_edge_softmax_bwd", L.ptr(rg.csr_ptr),
-               L.ptr(ctx.pack.rel_csr if need_tab else None), L.ptr(a),
-               L.ptr(ga.contiguous().float()), rg.n_dst, H, L.ptr(gz), L.ptr(slab), n_rel,
-               L.stream())
+        gp = _GatPlan(getattr(rg, "csr_plan", None), H, a.device)
+        with timed("edge_softmax_bwd", rg.E * (12 * H + 1) + rg.n_dst * 8):
+            L.call("regnn_edge_softmax_bwd", L.ptr(rg.csr_ptr),
+                   L.ptr(ctx.pack.rel_csr if need_tab else None), L.ptr(a),
+                   L.ptr(ga.contiguous().float()), rg.n_dst, H, L.ptr(gz), L.ptr(slab), n_rel,
+                   gp.ptr, L.stream())
         g_tab = _reduce(slab, n_rel * H).view(ctx.tab_shape) if need_tab else None
         return gz, g_tab, None, None, None
 

@@ -642,6 +642,35 @@ def test_two_layer_step_bitwise_reproducible(monkeypatch, rel_slots):
         assert torch.equal(ga, gb)
 
 
+def test_pre_sums_match_in_kernel_gather(monkeypatch):
+    """layer 0's per-type input sums formed on the sampler stream (regnn_ns_hop_typed_sums,
+    PRE_SUMS on) against agg0's own gather (off) on the same batch: the sampler adds each row's
+    entries in slot order as agg0 does, so sums, counts, self rows, slot relations, the loss and
+    every gradient are bitwise equal."""
+    from regnn_hip import ns
+    d = _mag(0.003, seed=9, F=128, hidden=64, classes=29, dropout=0.5)
+    res = {}
+    for mode in ("on", "off"):
+        monkeypatch.setitem(ns.PRE_SUMS, "mode", mode)
+        m = d["model"](4)
+        m.train()
+        tr, _ = _setup_trainer(d, m, batch=128, sizes=(10, 6))
+        assert bool(tr.fused.W.pre_sums) == (mode == "on")
+        tr._forward_backward()
+        torch.cuda.synchronize()
+        fs = tr.fused_slots[tr._trained] if tr.pipelined else tr.fused
+        n1 = int(tr.sampler.sizes[1])
+        W = fs.W
+        res[mode] = (float(tr.loss), [p.grad.clone() for p in m.parameters()],
+                     [fs._buf(a)[:n1].clone() for a in (W.s_agg, W.s_w, W.u_self, W.u_rel)])
+    (la, ga, ba), (lb, gb, bb) = res["on"], res["off"]
+    for x, y in zip(ba, bb):
+        assert torch.equal(x, y)
+    assert la == lb
+    for x, y in zip(ga, gb):
+        assert torch.equal(x, y)
+
+
 def test_fused_adam_equals_separate_adam(monkeypatch):
     """a one-rank FlatAdam trainer's optimizer inside the step's last launch (FUSED_ADAM on)
     gives the parameters, moments and step count of the separate regnn_adam_flat launch (the

@@ -13,7 +13,7 @@ from regnn_hip import build as B  # noqa: E402
 
 def main():
     name, extra = sys.argv[1], sys.argv[2:]
-    od = os.path.join(ROOT, "ab", f"obj_{name}")
+    od = os.path.join(ROOT, os.environ.get("AB_DIR", "ab"), f"obj_{name}")
     os.makedirs(od, exist_ok=True)
 
     def comp(src):
@@ -25,7 +25,7 @@ def main():
         return obj
     with cf.ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(comp, B._sources()))
-    out = os.path.join(ROOT, "ab", f"libregnn_{name}.so")
+    out = os.path.join(ROOT, os.environ.get("AB_DIR", "ab"), f"libregnn_{name}.so")
     r = subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *objs, "-o", out],
                        capture_output=True, text=True)
     if r.returncode:
