@@ -598,7 +598,10 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * last resolving block scans): 4 launches with de-duplication and the transposed index (3
  * without it), 1 meta-only. Strided buffer sizes: samp >= cap_e ints, status >= ceil(cap_e /
  * 1024) int64 (ABI 41). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
- * the hop adds its edges to it and to state[5]. */
+ * the hop adds its edges to it and to state[5]. strided = 2 (with the transposed index, no
+ * edge meta): everything but the transposed index and the sampled edges' blk_idx, which a
+ * second call with strided = 3 and the same arguments then writes (on another stream if the
+ * caller wants: nothing the next hop reads depends on it). */
 #define REGNN_CSC_PIECE 1024
 #define REGNN_CSC_LONG_CAP (32768 / 17 + 1)          /* hub rows of a <= 32768-edge block */
 #define REGNN_CSC_LONG_NPIECE (REGNN_CSC_LONG_CAP + 1)
@@ -876,7 +879,12 @@ int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_
 int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits);
 int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                  float beta, float* work, int32_t splits, hipStream_t stream);
+                  float beta, float* work, int32_t splits, const int32_t* m_live,
+                  const int32_t* k_live, hipStream_t stream);
+/* m_live / k_live (ABI 41; device int32 counts, may be NULL): op(A)'s rows m >= *m_live, and the
+ * k >= *k_live columns of op(A) / rows of op(B), are zero (the unused rows of a capacity-sized
+ * sampled block): the kernel skips their products (C rows >= *m_live get beta C) -- the same C,
+ * with the work of the live rows only. */
 
 /* Several strided 2-D fp32 copies in one launch: dst[i * cols + j] = src[i * s0 + j * s1] for
  * each descriptor (the module path's parameter gradients, some of them transposed views, into the

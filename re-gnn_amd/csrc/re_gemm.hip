@@ -150,16 +150,22 @@ __device__ __forceinline__ int wave_tiles(int64_t b, int64_t ext) {
     return v <= 0 ? 0 : (v <= 16 ? 1 : 4);
 }
 
+// m_live / k_live (device counts, may be null): the operands' rows past them are zeros (a
+// capacity-sized sampled block's unused rows), so a row tile m0 >= *m_live computes nothing (its
+// C rows get beta C) and the k-steps past *k_live are skipped: the same result, the GEMM's work
+// scaled to the batch's live rows.
 template <bool TA, bool TB, bool VEC>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
-               float beta, float* __restrict__ work) {
+               float beta, float* __restrict__ work, const int32_t* __restrict__ m_live,
+               const int32_t* __restrict__ k_live) {
     extern __shared__ uint16_t lds[];                 // [kStage]
     constexpr bool AKC = !TA, BKC = TB;               // k contiguous in A / B
     const int64_t m0 = int64_t(blockIdx.y) * BM, n0 = int64_t(blockIdx.x) * BN;
     const int z = blockIdx.z, S = gridDim.z;
-    const int64_t nk = (K + BK - 1) / BK;
+    const int64_t Ke = k_live ? min(K, int64_t(*k_live)) : K;
+    const int64_t nk = (m_live && m0 >= int64_t(*m_live)) ? 0 : (Ke + BK - 1) / BK;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
     const int wr = w >> 1, wc = w & 1;
     const int NI = wave_tiles(m0 + 64 * wr, M), NJ = wave_tiles(n0 + 64 * wc, N);
@@ -265,7 +271,8 @@ int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits) {
 
 int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                  float beta, float* work, int32_t splits, hipStream_t stream) {
+                  float beta, float* work, int32_t splits, const int32_t* m_live,
+                  const int32_t* k_live, hipStream_t stream) {
     if (M < 0 || N < 0 || K < 0 || splits < 1 || splits > 64) return REGNN_EINVAL;
     if (M == 0 || N == 0) return REGNN_OK;
     if (!A || !B || !C || (splits > 1 && !work)) return REGNN_EINVAL;
@@ -282,7 +289,7 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
 #define GEMM_CASE(TA_, TB_, V_)                                                                \
     if (bool(trans_a) == TA_ && bool(trans_b) == TB_ && vec == V_) {                           \
         hipLaunchKernelGGL((gemm_x6_kernel<TA_, TB_, V_>), grid, dim3(kThreads), lds, stream, M, N, \
-                           K, A, lda, B, ldb, C, ldc, beta, work);                             \
+                           K, A, lda, B, ldb, C, ldc, beta, work, m_live, k_live);             \
     }
     GEMM_CASE(false, false, true) GEMM_CASE(false, true, true) GEMM_CASE(true, false, true)
     GEMM_CASE(true, true, true) GEMM_CASE(false, false, false) GEMM_CASE(false, true, false)

@@ -323,7 +323,8 @@ __device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
 
 constexpr int kNsSumK = 128;               // input row width of the sums kernel
 constexpr int kNsSumUN = 11;               // entries' rows in flight per lane
-constexpr int kNsSumWaves = 8;             // waves per block (512 threads)
+constexpr int kNsSumWaves = 4;             // waves per block (256 threads: they fit beside the
+                                           // model's kernels on a shared CU)
 
 template <int G, int NT>
 __global__ void __launch_bounds__(64 * kNsSumWaves, 4)
@@ -896,12 +897,12 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
 // the piece table (ns_csc_kernel's first half); ns_csc_place_kernel then writes every entry at
 // csc_ptr[source] + rank. The order inside a segment follows the counters' atomics (unspecified,
 // as before: the consumer's sums are exact fixed-point).
-constexpr int kCscScanT = 1024;
+constexpr int kCscScanT = 256;             // 256-thread blocks: they fit beside the model's kernels
 
 __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
                                int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_long) {
     __shared__ int lds[kCscScanT / 64 + 1];
-    constexpr int IT = 8;
+    constexpr int IT = 16;                 // 4096 sources per pass, every count load in flight
     int carry = 0, lcarry = 0, pcarry = 0;
     int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
     for (int base = 0; base < n; base += kCscScanT * IT) {
@@ -1354,6 +1355,21 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
     if (cap_e >= (int64_t(1) << 31)) return REGNN_EUNSUPPORTED;
     const int n_tiles = int((cap_e + kNsTile - 1) / kNsTile);
     if (csc && cap_e > kCscMax) return REGNN_EUNSUPPORTED;
+    if (strided == 3) {
+        // the transposed index only (the part a strided = 2 call left out), on whatever stream
+        // the caller runs it: resolve + counts + ranks, scan, placement
+        if (!csc || edge_type || lean) return REGNN_EINVAL;
+        const int ce = int(cap_e);
+        hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
+                           dim3(kCscScanT), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce,
+                           csc_cnt, samp, tiles, csc_ptr, csc_long);
+        REGNN_LAUNCH_CHECK();
+        hipLaunchKernelGGL(ns_csc_place_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, stream, blk_idx, blk_row, blk_rel, samp, csc_ptr,
+                           csc_ent, ce);
+        REGNN_LAUNCH_CHECK();
+        return REGNN_OK;
+    }
     if (strided) {
         // sampling + placement in one launch, no row-offset scan (the layout above)
         if (k + 1 <= 32 && ns_half_waves())
@@ -1377,6 +1393,7 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         hipLaunchKernelGGL(ns_flags_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc,
                            sizes, hop, state, g2l, first, status, n_id, ce);
         REGNN_LAUNCH_CHECK();
+        if (csc && !edge_type && strided == 2) return REGNN_OK;   // the index: a strided = 3 call
         if (csc && !edge_type) {
             // the transposed index by many blocks: resolve + counts + ranks (the last block
             // scans), then the placement (samp holds each slot's rank: >= cap_e entries)

@@ -33,7 +33,7 @@ _SIG = {
     "regnn_wide_ln_fwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),
     "regnn_wide_ln_slab_rows": ([I64, I32], I64),
     "regnn_wide_ln_bwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),
-    "regnn_gemm_x6": ([I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, F32, P, I32, P],
+    "regnn_gemm_x6": ([I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, F32, P, I32, P, P, P],
                       ctypes.c_int),
     "regnn_slab_rows": ([I64, I32], I64),
     "regnn_tune": ([I32, I64], I64),

@@ -499,7 +499,9 @@ class REGNN(torch.nn.Module):
         wb = [w_c, b_c]
         if Sw.shape[1] > T * K + T:                 # the zero pad columns of [S | w | 0]
             wb.append(w_c.new_zeros(Sw.shape[1] - T * K - T, w_c.shape[1]))
-        agg = ops.mm(Sw, torch.cat(wb, 0))
+        # the block is capacity-sized: its rows past the batch's live targets are zeros, and the
+        # GEMMs (forward and both backward products) skip them (live: sizes[hop] on the device)
+        agg = ops.mm(Sw, torch.cat(wb, 0), live=getattr(blk, "live_rows", None))
         res = None
         if conv.residual:                                                       # :104,131-132
             x_t = self.group_input(x_dict, node_type, local_node_idx, n_id[:n])

@@ -171,14 +171,19 @@ class DeviceSampler:
                L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes),
                None if self.stamp_src is None else L.ptr(self.stamp_src), L.stream())
 
-    def run_hops(self, meta_only=True, strided=None):
+    def run_hops(self, meta_only=True, strided=None, csc_stream=None):
         """every hop of the current batch; meta_only=False runs hops marked meta_only in full
         (a consumer that reads n_id / the local source ids, e.g. the module path); strided=False
-        writes the CSR blocks whatever self.strided says (None: self.strided)."""
+        writes the CSR blocks whatever self.strided says (None: self.strided). csc_stream
+        (strided): a strided hop's transposed index (and its sampled blk_idx) is built on that
+        stream, forked after the hop's de-duplication, while the next hop samples on this one;
+        the caller joins it."""
         strided = self.strided if strided is None else bool(strided)
         rg = self.rg
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
+            fork = (csc_stream is not None and strided and self.csc[h] is not None and
+                    self.edge_meta[h] is None)
             ts = self.typed_sums[h]
             if (ts is not None and strided and meta_only and self.meta_only[h] and
                     self.edge_meta[h] is not None):
@@ -205,10 +210,30 @@ class DeviceSampler:
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
                      else (None, None, None, None)),
-                   int(strided), L.stream())
+                   2 if fork else int(strided), L.stream())
+            if fork:
+                csc_stream.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(csc_stream):
+                    self._hop_call(h, k, meta_only, 3)
             self.meta_fresh[h] = self.edge_meta[h] is not None
         # the blocks now hold the CSR layout (readable by exact_adjs / model_blocks) or not
         self._csr_fresh = not strided
+
+    def _hop_call(self, h, k, meta_only, mode):
+        rg, b, blk = self.rg, self.hop_bufs[h], self.blocks[h]
+        L.call("regnn_ns_hop", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(self.etype_csr),
+               L.ptr(self.ntype), self.num_edge_types, k, h, L.ptr(self.state),
+               L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h], L.ptr(self.g2l),
+               L.ptr(self.first), L.ptr(b["samp"]), L.ptr(b["spos"]), L.ptr(b["scnt"]),
+               L.ptr(b["gsrc"]), L.ptr(b["flag"]), L.ptr(b["tiles"]), L.ptr(b["status"]),
+               L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx), L.ptr(blk.rel), L.ptr(blk.pos),
+               L.ptr(blk.row), L.ptr(blk.inv),
+               *((L.ptr(self.local), L.ptr(self.edge_meta[h][0]), L.ptr(self.edge_meta[h][1]))
+                 if self.edge_meta[h] is not None else (None, None, None)),
+               int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
+               *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
+                 else (None, None, None, None)),
+               mode, L.stream())
 
     def set_seed(self, base_seed, epoch, batch_idx):
         """host-driven batches (the PyG-style iterator): seed words + a fresh dedup stamp."""
@@ -382,6 +407,9 @@ SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
 # round 3 (hipBLASLt GEMMs) 1.045 off / 1.09 on; round 4 (x6 GEMMs, interleaved pairs) 0.771 /
 # 0.761 off against 0.757 / 0.756 on
 MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
+# "on": the pipelined fused engine builds hop 0's transposed index on a third stream while hop 1
+# samples (regnn_ns_hop strided 2 / 3); "off": in the sampler's own chain (A/B)
+CSC_FORK = {"mode": os.environ.get("REGNN_NS_CSC_FORK", "on")}
 # the fused engine's sampling lookahead G: 2G sampler slots, each step samples the batch trained
 # G steps later, and a G-step graph trains G slots while the sampler fills the other G on the
 # second queue with one fork (the graph's root) and one join (its end) -- instead of a fork and
@@ -795,7 +823,11 @@ class NSTrainer:
                     for s in self.slots[1:]]
             else:
                 self._setup_module_slot(self.slots[1])
-            self._side = torch.cuda.Stream(device=dev)
+            # the sampler's stream; REGNN_NS_SIDE_PRIORITY (-1: high) for A/B runs
+            self._side = torch.cuda.Stream(device=dev,
+                                           priority=int(os.environ.get("REGNN_NS_SIDE_PRIORITY", "0")))
+            if self.fused is not None and CSC_FORK["mode"] != "off":
+                self._csc = torch.cuda.Stream(device=dev)
         # one rank, FlatAdam, two-layer step: the optimizer runs inside the step's last launch
         # (no all-reduce sits between the backward and the update)
         self.adam_fused = (self.fused is not None and self.fused.two_layer and self.world == 1
@@ -831,6 +863,8 @@ class NSTrainer:
             s.meta_only[last] = True
             blk = s.blocks[last]
             blk.edge_meta, blk.meta_only = (et, eo), True
+        for h, blk in enumerate(s.blocks):
+            blk.live_rows = s.sizes[h:h + 1]      # the block's live target rows (device count)
         if s.blocks[0].csr_idx.numel() <= 32768:
             _, cptr, cent, clong = s.csc[0] or s.enable_csc(0)
             b0 = s.blocks[0]
@@ -867,9 +901,15 @@ class NSTrainer:
     def _sample(self, slot):
         n = len(self.slots)
         s = self.slots[slot]
+        if getattr(self, "_csc", None) is not None:
+            # the previous batch's transposed index reads the dedup tables every slot shares
+            # (g2l): it completes before this batch's sampling writes them
+            torch.cuda.current_stream(self.device).wait_stream(self._csc)
         s.batch_from_perm(self.perm, self.rank + slot * self.world, n * self.world)
         if self.fused is not None:
-            s.run_hops()
+            # the pipelined engine builds hop 0's transposed index on a third stream while hop 1
+            # samples (CSC_FORK; joined before the next batch's sampling and at the group's end)
+            s.run_hops(csc_stream=self._csc if getattr(self, "_csc", None) is not None else None)
         else:                                 # the module path reads the CSR blocks
             s.run_hops(meta_only=self._module_lean, strided=False)
 
@@ -898,6 +938,7 @@ class NSTrainer:
         # the join sits between layer 1's transposed pass and layer 0's backward (the sampler is
         # done by then): the next step's first kernel then waits on its own queue only
         cs.wait_stream(self._side)
+        self._join_csc(cs)
         if split:
             self._fs_step(fs, part=2)
 
@@ -919,6 +960,11 @@ class NSTrainer:
             for i in range(m):
                 self._sample((start + G + i) % n)
         cs.wait_stream(self._side)
+        self._join_csc(cs)
+
+    def _join_csc(self, cs):
+        if getattr(self, "_csc", None) is not None:
+            cs.wait_stream(self._csc)
 
     def _group_sizes(self):
         return group_sizes(self.ahead)
@@ -931,6 +977,7 @@ class NSTrainer:
         if not self._primed:
             for i in range(self.ahead):
                 self._sample((self.cur + i) % len(self.slots))
+            self._join_csc(torch.cuda.current_stream(self.device))
             self._primed = True
 
     def _forward_backward(self):

@@ -1573,9 +1573,11 @@ def _gemm_splits(M, N, K):
     return int(max(1, min(64, _SPLIT_TARGET // tiles, nk // 4)))
 
 
-def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
+def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0, m_live=None, k_live=None):
     """op(a) @ op(b) (+ beta * out) in fp32 accuracy: a [M, K] ([K, M] with trans_a), b [K, N]
-    ([N, K] with trans_b), contiguous fp32 device tensors."""
+    ([N, K] with trans_b), contiguous fp32 device tensors. m_live / k_live: one-element int32
+    device tensors, the live rows of op(a) / the live k (the operands are zero past them: a
+    capacity-sized sampled block's unused rows), so the kernel skips those products."""
     M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
     Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
     if K != Kb:
@@ -1587,8 +1589,14 @@ def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
     work = (torch.empty(int(L._so.regnn_gemm_x6_work_floats(M, N, S)), dtype=torch.float32,
                         device=a.device) if S > 1 else None)
     L.call("regnn_gemm_x6", int(trans_a), int(trans_b), M, N, K, L.ptr(a), a.stride(0), L.ptr(b),
-           b.stride(0), L.ptr(out), out.stride(0), float(beta), L.ptr(work), S, L.stream())
+           b.stride(0), L.ptr(out), out.stride(0), float(beta), L.ptr(work), S, L.ptr(m_live),
+           L.ptr(k_live), L.stream())
     return out
+
+
+# "on": ops.mm's live-row hint reaches the GEMMs (the capacity-sized block's unused rows are
+# skipped); "off": every row computed (A/B)
+LIVE_ROWS = {"mode": os.environ.get("REGNN_GEMM_LIVE_ROWS", "on")}
 
 
 def gemm_x6_ok(*ts):
@@ -1600,29 +1608,33 @@ def gemm_x6_ok(*ts):
 
 class _MMx6(torch.autograd.Function):
     """c + a @ b (c optional, broadcast over rows when 1-D) with regnn_gemm_x6 forward and
-    backward (ga = g b^T, gb = a^T g: split-K over the rows)."""
+    backward (ga = g b^T, gb = a^T g: split-K over the rows). live: a's live rows (a one-element
+    int32 device tensor, or None): a's rows past it are zero, the output's rows there are c's
+    (the incoming gradient's rows there are taken as zero: nothing reads them)."""
 
     @staticmethod
-    def forward(ctx, a, b, c):
+    def forward(ctx, a, b, c, live):
         if c is None:
-            out = gemm_x6(a, b)
+            out = gemm_x6(a, b, m_live=live)
         else:
             out = (c.expand(a.shape[0], b.shape[1]) if c.dim() == 1 else c).contiguous().clone()
-            gemm_x6(a, b, out=out, beta=1.0)
+            gemm_x6(a, b, out=out, beta=1.0, m_live=live)
         ctx.save_for_backward(a, b)
         ctx.c_shape = None if c is None else c.shape
+        ctx.live = live
         return out
 
     @staticmethod
     def backward(ctx, g):
         a, b = ctx.saved_tensors
         g = g.contiguous()
-        ga = gemm_x6(g, b, trans_b=True) if ctx.needs_input_grad[0] else None
-        gb = gemm_x6(a, g, trans_a=True) if ctx.needs_input_grad[1] else None
+        live = ctx.live
+        ga = gemm_x6(g, b, trans_b=True, m_live=live) if ctx.needs_input_grad[0] else None
+        gb = gemm_x6(a, g, trans_a=True, k_live=live) if ctx.needs_input_grad[1] else None
         gc = None
         if ctx.needs_input_grad[2]:
             gc = g.sum(0) if len(ctx.c_shape) == 1 else g
-        return ga, gb, gc
+        return ga, gb, gc, None
 
 
 class _LinearX6(torch.autograd.Function):
@@ -1686,15 +1698,18 @@ def linear(x, w, bias=None):
     return torch.nn.functional.linear(x, w, bias)
 
 
-def mm(a, b, c=None):
-    """c + a @ b on regnn_gemm_x6 when the operands allow it (else torch)."""
+def mm(a, b, c=None, live=None):
+    """c + a @ b on regnn_gemm_x6 when the operands allow it (else torch). live: a one-element
+    int32 device tensor with a's live rows (a's rows past it are zero: the GEMMs skip them)."""
     # c: None, a length-N row vector or exactly [M, N] (the x6 epilogue writes M rows with c's
     # row stride; any other broadcastable shape goes to torch)
     M, N = (a.shape[0], b.shape[1]) if a.dim() == 2 and b.dim() == 2 else (-1, -1)
     c_ok = c is None or (c.is_cuda and c.dtype == torch.float32 and
                          (tuple(c.shape) == (N,) or tuple(c.shape) == (M, N)))
     if GEMM_X6["mode"] != "off" and gemm_x6_ok(a, b) and c_ok:
-        return _MMx6.apply(a, b, c)
+        live_ok = (live is not None and live.is_cuda and live.dtype == torch.int32 and
+                   live.numel() == 1 and LIVE_ROWS["mode"] != "off")
+        return _MMx6.apply(a, b, c, live if live_ok else None)
     return a @ b if c is None else (torch.addmm(c, a, b) if c.dim() <= 2 else c + a @ b)
 
 

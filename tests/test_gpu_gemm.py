@@ -142,3 +142,28 @@ def test_copy_many_strided_sources():
     ops.copy_many(dsts, srcs)
     for d, s_ in zip(dsts, srcs):
         assert torch.equal(d, s_)
+
+
+@pytest.mark.parametrize("live", [0, 1, 127, 128, 5606, 13312])
+def test_mm_live_rows_bitwise(live):
+    """ops.mm with a live-row count (the capacity-sized block's rows past it are zero): the
+    forward and both gradients bitwise those of the full GEMMs on the same zero-padded operands
+    (the skipped products are exact zeros), the output's dead rows equal to c's."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(11)
+    M, K, N = 13312, 516, 512
+    a0 = torch.randn(M, K, generator=g, device=DEV)
+    a0[live:] = 0
+    b0 = torch.randn(K, N, generator=g, device=DEV)
+    c0 = torch.randn(N, generator=g, device=DEV)
+    gout = torch.randn(M, N, generator=g, device=DEV)
+    gout[live:] = 0
+    cnt = torch.tensor([live], dtype=torch.int32, device=DEV)
+    outs = []
+    for lv in (None, cnt):
+        a, b, c = (t.clone().requires_grad_(True) for t in (a0, b0, c0))
+        y = ops.mm(a, b, c, live=lv)
+        y.backward(gout)
+        outs.append([y.detach(), a.grad, b.grad, c.grad])
+    for name, x, y in zip(["out", "g_a", "g_b", "g_c"], outs[0], outs[1]):
+        assert torch.equal(x, y), name
