@@ -322,14 +322,18 @@ __device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
 }
 
 constexpr int kNsSumK = 128;               // input row width of the sums kernel
-constexpr int kNsSumUN = 11;               // entries' rows in flight per lane
+// entries' rows in flight per lane: 32 lanes per row take every entry of a fan-out <= 20 row in
+// one round (21 rows); 64 lanes per row (fan-outs > 31), half of them each
+template <int G>
+constexpr int ns_sum_un() { return G == 32 ? 21 : 11; }
 constexpr int kNsSumWaves = 4;             // waves per block (256 threads: they fit beside the
                                            // model's kernels on a shared CU)
 
 template <int G, int NT>
-__global__ void __launch_bounds__(64 * kNsSumWaves, 4)
+__global__ void __launch_bounds__(64 * kNsSumWaves, 3)
 ns_sample_sums_kernel(NsSumArgs A) {
     constexpr int K = kNsSumK;
+    constexpr int kNsSumUN = ns_sum_un<G>();
     constexpr int TPW = 64 / G;                // rows per wave
     constexpr int H = G == 64 ? 2 : 1;         // lane groups of 32 per row (each a float4 column)
     __shared__ int wsum[kNsSumWaves * TPW];
@@ -416,31 +420,33 @@ ns_sample_sums_kernel(NsSumArgs A) {
         float4 xs = make_float4(0.f, 0.f, 0.f, 0.f);
         int rs = -1;
         for (int j0 = 0; j0 < ne; j0 += H * kNsSumUN) {
-            int tj[kNsSumUN], rj[kNsSumUN];
             float4 x[kNsSumUN];
 #pragma unroll
             for (int u = 0; u < kNsSumUN; ++u) {
                 const int j = j0 + H * u + h;
                 const int jj = j < ne ? j : ne - 1;  // padding: a valid row, loaded, not added
-                tj[u] = __shfl(st, jj, G);
-                rj[u] = __shfl(sr, jj, G);
+                const int tj = __shfl(st, jj, G);
                 const int64_t lo = __shfl(slo, jj, G);
-                x[u] = *reinterpret_cast<const float4*>(pick_tab<NT>(A, tj[u]) + lo * K + 4 * l);
-                if (j >= ne) tj[u] = -1;
+                x[u] = *reinterpret_cast<const float4*>(pick_tab<NT>(A, tj) + lo * K + 4 * l);
             }
+            // (each entry's type / relation shuffled again here: arrays of them held across the
+            // loads cost the registers that keep every row in flight)
 #pragma unroll
             for (int u = 0; u < kNsSumUN; ++u) {
-                if (tj[u] < 0) continue;
-                if (rj[u] >= A.n_et) {             // the self loop (one per row)
+                const int j = j0 + H * u + h;
+                const int jj = j < ne ? j : ne - 1;
+                const int tj = __shfl(st, jj, G), rj = __shfl(sr, jj, G);
+                if (j >= ne) continue;
+                if (rj >= A.n_et) {                // the self loop (one per row)
                     xs = x[u];
-                    rs = rj[u];
+                    rs = rj;
                     continue;
                 }
 #pragma unroll
                 for (int tt = 0; tt < NT; ++tt) {
-                    if (tt != tj[u]) continue;
+                    if (tt != tj) continue;
                     ws[tt] += 1.f;
-                    rt[tt] = rj[u];
+                    rt[tt] = rj;
                     racc[tt].x += x[u].x; racc[tt].y += x[u].y;
                     racc[tt].z += x[u].z; racc[tt].w += x[u].w;
                 }
@@ -753,27 +759,32 @@ ns_flags_finish_kernel(const int32_t* __restrict__ gsrc, int32_t* __restrict__ s
     }
     int total;
     const int ex = block_exscan<kBlock>(c, lds, &total);
-    if (threadIdx.x == 0) {
+    // every tile publishes its count, then the first wave reads all lower tiles' counts at once
+    // (one lane per tile, 64 per round) until each carries this hop's stamp: a few round trips
+    // whatever the tile's position (a serial walk cost one round trip per lower tile)
+    if (threadIdx.x == 0)
+        __hip_atomic_store(status + tile, lb_pack(stamp, 1u, uint32_t(total)), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
         int prefix = 0;
-        if (tile == 0) {
-            __hip_atomic_store(status, lb_pack(stamp, 2u, uint32_t(total)), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(status + tile, lb_pack(stamp, 1u, uint32_t(total)),
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            for (int p = tile - 1; p >= 0;) {
-                const uint64_t st =
-                    __hip_atomic_load(status + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if (uint32_t(st >> 32) != stamp) continue;            // not yet published
-                prefix += int(st & 0x3FFFFFFFu);
-                if (((st >> 30) & 3u) == 2u) break;
-                --p;
+        for (int p0 = 0; p0 < tile; p0 += 64) {
+            const int p = p0 + int(threadIdx.x);
+            int v = 0;
+            if (p < tile) {
+                uint64_t st;
+                do {
+                    st = __hip_atomic_load(status + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                } while (uint32_t(st >> 32) != stamp);                // not yet published
+                v = int(st & 0x3FFFFFFFu);
             }
-            __hip_atomic_store(status + tile, lb_pack(stamp, 2u, uint32_t(prefix + total)),
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            prefix += v;
         }
-        s_prefix = prefix;
-        if (tile == int(gridDim.x) - 1) sizes[hop + 1] = n + prefix + total;
+        if (threadIdx.x == 0) {
+            s_prefix = prefix;
+            if (tile == int(gridDim.x) - 1) sizes[hop + 1] = n + prefix + total;
+        }
     }
     __syncthreads();
     int off = s_prefix + ex;
@@ -910,8 +921,7 @@ __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
         int v[IT], s = 0, nl = 0, np = 0;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            v[j] = i0 + j < n ? __hip_atomic_load(csc_cnt + i0 + j, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) : 0;
+            v[j] = i0 + j < n ? csc_cnt[i0 + j] : 0;   // (after the ticket's fence)
             s += v[j];
             nl += v[j] > kCscShort ? 1 : 0;
             np += v[j] > kCscShort ? (v[j] + kCscPiece - 1) / kCscPiece : 0;

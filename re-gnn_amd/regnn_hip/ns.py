@@ -408,8 +408,11 @@ SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
 # 0.761 off against 0.757 / 0.756 on
 MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # "on": the pipelined fused engine builds hop 0's transposed index on a third stream while hop 1
-# samples (regnn_ns_hop strided 2 / 3); "off": in the sampler's own chain (A/B)
-CSC_FORK = {"mode": os.environ.get("REGNN_NS_CSC_FORK", "on")}
+# samples (regnn_ns_hop strided 2 / 3); "off" (default): in the sampler's own chain. Eager runs
+# are fine; capturing the third stream (forked from the sampler's stream, joined back before the
+# next batch) segfaults inside torch.cuda.graph's capture_end on this image (ROCm 7.2, torch
+# 2.10), so the graphed bench cannot use it
+CSC_FORK = {"mode": os.environ.get("REGNN_NS_CSC_FORK", "off")}
 # the fused engine's sampling lookahead G: 2G sampler slots, each step samples the batch trained
 # G steps later, and a G-step graph trains G slots while the sampler fills the other G on the
 # second queue with one fork (the graph's root) and one join (its end) -- instead of a fork and
@@ -901,15 +904,15 @@ class NSTrainer:
     def _sample(self, slot):
         n = len(self.slots)
         s = self.slots[slot]
-        if getattr(self, "_csc", None) is not None:
-            # the previous batch's transposed index reads the dedup tables every slot shares
-            # (g2l): it completes before this batch's sampling writes them
-            torch.cuda.current_stream(self.device).wait_stream(self._csc)
         s.batch_from_perm(self.perm, self.rank + slot * self.world, n * self.world)
         if self.fused is not None:
             # the pipelined engine builds hop 0's transposed index on a third stream while hop 1
-            # samples (CSC_FORK; joined before the next batch's sampling and at the group's end)
-            s.run_hops(csc_stream=self._csc if getattr(self, "_csc", None) is not None else None)
+            # samples (CSC_FORK), joined back right after: the next batch's sampling writes the
+            # dedup tables (g2l) every slot shares, which the index reads
+            csc = getattr(self, "_csc", None)
+            s.run_hops(csc_stream=csc)
+            if csc is not None:
+                torch.cuda.current_stream(self.device).wait_stream(csc)
         else:                                 # the module path reads the CSR blocks
             s.run_hops(meta_only=self._module_lean, strided=False)
 
@@ -938,7 +941,6 @@ class NSTrainer:
         # the join sits between layer 1's transposed pass and layer 0's backward (the sampler is
         # done by then): the next step's first kernel then waits on its own queue only
         cs.wait_stream(self._side)
-        self._join_csc(cs)
         if split:
             self._fs_step(fs, part=2)
 
@@ -960,11 +962,6 @@ class NSTrainer:
             for i in range(m):
                 self._sample((start + G + i) % n)
         cs.wait_stream(self._side)
-        self._join_csc(cs)
-
-    def _join_csc(self, cs):
-        if getattr(self, "_csc", None) is not None:
-            cs.wait_stream(self._csc)
 
     def _group_sizes(self):
         return group_sizes(self.ahead)
@@ -977,7 +974,6 @@ class NSTrainer:
         if not self._primed:
             for i in range(self.ahead):
                 self._sample((self.cur + i) % len(self.slots))
-            self._join_csc(torch.cuda.current_stream(self.device))
             self._primed = True
 
     def _forward_backward(self):
