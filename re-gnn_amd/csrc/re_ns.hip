@@ -322,15 +322,20 @@ __device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
 }
 
 constexpr int kNsSumK = 128;               // input row width of the sums kernel
-// entries' rows in flight per lane: 32 lanes per row take every entry of a fan-out <= 20 row in
-// one round (21 rows); 64 lanes per row (fan-outs > 31), half of them each
+// entries' rows in flight per lane (32 lanes per row: two rounds of 11 for a fan-out of 20). All
+// 21 in one round (REGNN_NS_SUM_UN32=21: 168 VGPRs, 3 waves per SIMD) measured 118.3 against
+// 106.7 us per step: the sampler's kernel then holds more of the GPU beside the model
+#ifndef REGNN_NS_SUM_UN32
+#define REGNN_NS_SUM_UN32 11
+#endif
 template <int G>
-constexpr int ns_sum_un() { return G == 32 ? 21 : 11; }
+constexpr int ns_sum_un() { return G == 32 ? REGNN_NS_SUM_UN32 : 11; }
+constexpr int kNsSumOcc = REGNN_NS_SUM_UN32 > 11 ? 3 : 4;   // waves per SIMD the registers allow
 constexpr int kNsSumWaves = 4;             // waves per block (256 threads: they fit beside the
                                            // model's kernels on a shared CU)
 
 template <int G, int NT>
-__global__ void __launch_bounds__(64 * kNsSumWaves, 3)
+__global__ void __launch_bounds__(64 * kNsSumWaves, kNsSumOcc)
 ns_sample_sums_kernel(NsSumArgs A) {
     constexpr int K = kNsSumK;
     constexpr int kNsSumUN = ns_sum_un<G>();

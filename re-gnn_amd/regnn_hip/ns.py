@@ -811,6 +811,8 @@ class NSTrainer:
                              getattr(model, "typed_first_layer_ok", lambda _x: False)(x_dict))
         if self.fused is None and self._blocks_ok:
             self._setup_module_slot(self.slots[0])
+        # REGNN_NS_PIPELINE=0: no second stream (a profiling aid: every kernel's time alone)
+        pipeline = pipeline and os.environ.get("REGNN_NS_PIPELINE", "1") != "0"
         self.pipelined = bool(pipeline) and (self.fused is not None or
                                              (self._blocks_ok and MODULE_PIPELINE["mode"] != "off"))
         # the sampling lookahead (fused engine; the module path samples one batch ahead)
