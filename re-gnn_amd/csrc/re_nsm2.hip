@@ -418,6 +418,10 @@ constexpr int kAggW = 512;
 #define REGNN_AGG_ROWS 16
 #endif
 constexpr int kAggRows = REGNN_AGG_ROWS;
+// with the sampler's sums (PRE), stage 1's W_t fragments are all requested at the kernel's start
+#ifndef REGNN_AGG0_EARLY_W
+#define REGNN_AGG0_EARLY_W 1
+#endif
 
 inline size_t agg0w_lds(int T) {          // St [16][T K + 4] | sw [16][MT] | Pt [16][68] |
     return (size_t(16) * (T * 128 + 4) + 16 * MT + 16 * 68 + 16 * F + 16 * F) * sizeof(float);
@@ -461,6 +465,23 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
     }
     const int base = blockIdx.x * kAggRows;
     if (base >= n) return;                 // block-uniform (the grid is capacity-sized)
+    // PRE: every W_t fragment stage 1 reads (this wave's types, both halves) requested first,
+    // under the input loads: nothing they depend on is produced in this kernel
+    const int nst = 2 * ((T - kh + 1) / 2);                 // stage-1 steps of this wave's types
+    constexpr bool EW = PRE && REGNN_AGG0_EARLY_W;
+    float4 bq_all[EW ? NT : 1][K / 32];
+    if constexpr (EW) {
+#pragma unroll
+        for (int step = 0; step < NT; ++step) {
+            if (step < nst) {
+                const int tt = kh + 2 * (step >> 1), h0 = (step & 1) * (K / 32);
+                const float* wt = pick(A.lin_w.p, tt) + (16 * ct + c) * K + 4 * q + 16 * h0;
+#pragma unroll
+                for (int b = 0; b < K / 32; ++b)
+                    bq_all[step][b] = *reinterpret_cast<const float4*>(wt + 16 * b);
+            }
+        }
+    }
     // the relation table in registers of every lane (n_rel <= 64), read by shuffles
     const float tabw = rel_tab(A.rw, A.n_rel, A.alpha, lane);
     // ---- gather: per-type register sums of this lane's 4 features of row v
@@ -605,7 +626,21 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
     // ---- stage 1: wave (ct, kh) forms sum over its half's types of S_t W_t^T for columns
     // 16 ct + c; W_t fragments from L2, two in flight
     f32x4 d = {0.f, 0.f, 0.f, 0.f};
-    {
+    if constexpr (EW) {
+#pragma unroll
+        for (int step = 0; step < NT; ++step) {
+            if (step < nst) {
+                const int tt = kh + 2 * (step >> 1);
+                const float* sa = St + c * SR + tt * K + 16 * (step & 1) * HB + 4 * q;
+#pragma unroll
+                for (int b = 0; b < HB; ++b) {
+                    const float4 av = *reinterpret_cast<const float4*>(sa + 16 * b);
+                    const float4 bv = bq_all[step][b];
+                    MFMA4(av, bv.x, bv.y, bv.z, bv.w, d);
+                }
+            }
+        }
+    } else {
         float4 bq[3][HB];
         auto bload = [&](int step, float4 (&dst)[HB]) {     // step: (type tt = kh + 2 (step >> 1), half)
             const int tt = kh + 2 * (step >> 1), h0 = (step & 1) * HB;
@@ -613,7 +648,6 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
 #pragma unroll
             for (int b = 0; b < HB; ++b) dst[b] = *reinterpret_cast<const float4*>(wt + 16 * b);
         };
-        const int nst = 2 * ((T - kh + 1) / 2);             // steps of this half's types
         if (nst > 0) bload(0, bq[0]);
         if (nst > 1) bload(1, bq[1]);
 #pragma unroll

@@ -749,8 +749,8 @@ def test_block_transposed_index():
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
 
 
-@pytest.mark.parametrize("half_waves", ["0", "1"])
-def test_strided_blocks_match_csr(monkeypatch, half_waves):
+@pytest.mark.parametrize("half_waves,dedup_one", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one):
     """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
     launch) against the CSR layout on the same batches: the same n_id, sizes, per-row edges
     (local source, relation, CSR position, target row; the meta-only hop's source type / table
@@ -759,6 +759,9 @@ def test_strided_blocks_match_csr(monkeypatch, half_waves):
     wave (fan-outs 9 and 7 fit 32 lanes)."""
     from regnn_hip import ns
     monkeypatch.setenv("REGNN_NS_HALF_WAVES", half_waves)
+    # "0": the multi-block kernels (one-pass look-back dedup, resolve + ranks + last-block scan,
+    # placement); "1": hop 0's de-duplication and transposed index in one workgroup
+    monkeypatch.setenv("REGNN_NS_DEDUP_ONE", dedup_one)
     d = _mag(0.003, seed=10, F=128, hidden=64, classes=19, dropout=0.5)
     trs, models = [], []
     for mode in ("off", "on"):
