@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 41). */
+/* ABI version (bumped on any signature or semantics change; currently 42). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -594,10 +594,11 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * [i S, i S + cnt_i) (S = k + 1, cnt_i = scnt[i], sampled positions ascending), its self loop at
  * i S + cnt_i, the other slots empty (blk_idx -1); blk_ptr is not written. Sampling and
  * placement run as one launch (no row-offset scan), the de-duplication as one pass (decoupled
- * look-back over status), the transposed index by many blocks (per-slot ranks in samp, the
- * last resolving block scans): 4 launches with de-duplication and the transposed index (3
- * without it), 1 meta-only. Strided buffer sizes: samp >= cap_e ints, status >= ceil(cap_e /
- * 1024) int64 (ABI 41). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
+ * look-back over status), the transposed index by many blocks in one launch (the last block
+ * to resolve scans the counts and publishes csc_ptr, then every block places its entries):
+ * 3 launches with de-duplication and the transposed index, 1 meta-only. Strided buffer sizes:
+ * tiles >= 2 ints (an arrival ticket and a published stamp), status >= ceil(cap_e / 1024)
+ * int64 (ABI 42). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
  * the hop adds its edges to it and to state[5]. strided = 2 (with the transposed index, no
  * edge meta): everything but the transposed index and the sampled edges' blk_idx, which a
  * second call with strided = 3 and the same arguments then writes (on another stream if the

@@ -345,9 +345,13 @@ ns_sample_sums_kernel(NsSumArgs A) {
     const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int lane = wl % G, tl = wv * TPW + wl / G;
     const uint64_t gmask = G == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
-    const int i = blockIdx.x * (kNsSumWaves * TPW) + tl;
     const int n = A.sizes[A.hop];
     const int k = A.k, S = k + 1;
+    int etot = 0;                              // this lane's rows' edges (lane 0 of a row)
+    // grid-stride over row groups (uniform per block): a grid smaller than the rows (the launch's
+    // REGNN_NS_SUM_BLOCKS) keeps the kernel on fewer CUs beside the model's kernels
+    for (int ib = blockIdx.x * (kNsSumWaves * TPW); ib < A.cap; ib += gridDim.x * (kNsSumWaves * TPW)) {
+    const int i = ib + tl;
     const int64_t base = int64_t(i) * S;
     int cnt = -1;                              // -1: no row (past the batch)
     if (i < A.cap && i >= n) {
@@ -499,7 +503,9 @@ ns_sample_sums_kernel(NsSumArgs A) {
             A.u_rel[int64_t(i) * (T + 1) + T] = rs;
         }
     }
-    if (lane == 0) wsum[tl] = cnt + 1;         // edges of the row, self loop included
+    etot += cnt + 1;                           // edges of the row, self loop included
+    }
+    if (lane == 0) wsum[tl] = etot;
     __syncthreads();
     if (threadIdx.x == 0) {
         int e = 0;
@@ -906,54 +912,110 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
     }
 }
 
-// The transposed index built by many blocks (replaces the one-workgroup ns_csc_kernel on the
-// strided path): ns_resolve_csc_kernel resolves every slot's local source id (as
-// ns_resolve_kernel), takes the entry's rank in its source's segment from the counter's atomic
-// (crank), and the last block to finish (a ticket) scans the counts into csc_ptr, the hub list and
-// the piece table (ns_csc_kernel's first half); ns_csc_place_kernel then writes every entry at
-// csc_ptr[source] + rank. The order inside a segment follows the counters' atomics (unspecified,
-// as before: the consumer's sums are exact fixed-point).
+// The transposed index built by many blocks in one launch (replaces the one-workgroup
+// ns_csc_kernel on the strided path). Every block resolves its slots' local source ids (as
+// ns_resolve_kernel) and takes each entry's rank in its source's segment from the counter's
+// returned atomic; the last block to arrive (a ticket) scans the counts into csc_ptr, the hub list
+// and the piece table and publishes them (agent release, a stamped flag); every block then places
+// its own entries at csc_ptr[source] + rank (the others wait on the flag: the last block is
+// running, it took the last ticket). The order inside a segment follows the counters' atomics
+// (unspecified: the consumer's sums are exact fixed-point).
 constexpr int kCscScanT = 256;             // 256-thread blocks: they fit beside the model's kernels
+constexpr int kCscScanQ = 16;              // counts per lane per pass (lane-contiguous)
+constexpr int kCscScanWE = 64 * kCscScanQ; // counts per wave per pass
+constexpr int kCscScanPad = kCscScanWE + kCscScanWE / kCscScanQ;   // LDS words per wave (padded)
 
+// The scan of the per-source counts by one 256-thread block: per pass each wave loads 1,024
+// counts coalesced, transposes them through LDS (index e at e + e / 16: conflict-free both ways)
+// so each lane holds 16 consecutive counts, scans lane-serially and across the wave (shuffles),
+// combines the four waves through LDS, and writes csc_ptr back coalesced through the same LDS.
+// Hub rows (more than kCscShort entries) are listed ascending with their pieces.
 __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
-                               int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_long) {
-    __shared__ int lds[kCscScanT / 64 + 1];
-    constexpr int IT = 16;                 // 4096 sources per pass, every count load in flight
+                               int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_long,
+                               int* __restrict__ sbuf, int* __restrict__ swave) {
+    constexpr int NW = kCscScanT / 64, Q = kCscScanQ;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int* buf = sbuf + w * kCscScanPad;
     int carry = 0, lcarry = 0, pcarry = 0;
     int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
-    for (int base = 0; base < n; base += kCscScanT * IT) {
-        const int i0 = base + threadIdx.x * IT;
-        int v[IT], s = 0, nl = 0, np = 0;
+    for (int base = 0; base < n; base += NW * kCscScanWE) {
+        const int wb = base + w * kCscScanWE;
+        int v[Q];
 #pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            v[j] = i0 + j < n ? csc_cnt[i0 + j] : 0;   // (after the ticket's fence)
-            s += v[j];
-            nl += v[j] > kCscShort ? 1 : 0;
-            np += v[j] > kCscShort ? (v[j] + kCscPiece - 1) / kCscPiece : 0;
+        for (int j = 0; j < Q; ++j) {
+            const int e = j * 64 + lane;
+            v[j] = wb + e < n ? csc_cnt[wb + e] : 0;   // (behind the ticket's acquire)
         }
-        int total, ltotal, ptotal;
-        int off = carry + block_exscan<kCscScanT>(s, lds, &total);
-        int loff = lcarry + block_exscan<kCscScanT>(nl, lds, &ltotal);
-        int poff = pcarry + block_exscan<kCscScanT>(np, lds, &ptotal);
 #pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            if (i0 + j < n) {
-                csc_ptr[i0 + j] = off;
-                if (v[j] > kCscShort) {
-                    const int li = loff++;
-                    csc_long[1 + li] = i0 + j;
-                    const int npc = (v[j] + kCscPiece - 1) / kCscPiece;
-                    for (int k = 0; k < npc; ++k, ++poff)
-                        pieces[poff] = make_int4(i0 + j, off + k * kCscPiece,
-                                                 min(kCscPiece, v[j] - k * kCscPiece),
-                                                 (li << 16) | (k << 8) | npc);
-                }
+        for (int j = 0; j < Q; ++j) {
+            const int e = j * 64 + lane;
+            buf[e + (e >> 4)] = v[j];
+        }
+        __syncthreads();
+        int s = 0, nl = 0, np = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            v[q] = buf[lane * (Q + 1) + q];
+            s += v[q];
+            nl += v[q] > kCscShort ? 1 : 0;
+            np += v[q] > kCscShort ? (v[q] + kCscPiece - 1) / kCscPiece : 0;
+        }
+        int xs = s, xl = nl, xp = np;             // inclusive wave scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int ys = __shfl_up(xs, o, 64), yl = __shfl_up(xl, o, 64),
+                      yp = __shfl_up(xp, o, 64);
+            if (lane >= o) {
+                xs += ys;
+                xl += yl;
+                xp += yp;
             }
-            off += v[j];
         }
-        carry += total;
-        lcarry += ltotal;
-        pcarry += ptotal;
+        if (lane == 63) {
+            swave[w] = xs;
+            swave[NW + w] = xl;
+            swave[2 * NW + w] = xp;
+        }
+        __syncthreads();
+        int ws = carry, wl = lcarry, wp = pcarry, ts = 0, tl = 0, tp = 0;
+#pragma unroll
+        for (int u = 0; u < NW; ++u) {
+            const int a = swave[u], b = swave[NW + u], c = swave[2 * NW + u];
+            if (u < w) {
+                ws += a;
+                wl += b;
+                wp += c;
+            }
+            ts += a;
+            tl += b;
+            tp += c;
+        }
+        int off = ws + xs - s, loff = wl + xl - nl, poff = wp + xp - np;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int i = wb + lane * Q + q;
+            buf[lane * (Q + 1) + q] = off;
+            if (v[q] > kCscShort && i < n) {
+                const int li = loff++;
+                csc_long[1 + li] = i;
+                const int npc = (v[q] + kCscPiece - 1) / kCscPiece;
+                for (int k = 0; k < npc; ++k, ++poff)
+                    pieces[poff] = make_int4(i, off + k * kCscPiece,
+                                             min(kCscPiece, v[q] - k * kCscPiece),
+                                             (li << 16) | (k << 8) | npc);
+            }
+            off += v[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const int e = j * 64 + lane;
+            if (wb + e < n) csc_ptr[wb + e] = buf[e + (e >> 4)];
+        }
+        carry += ts;
+        lcarry += tl;
+        pcarry += tp;
+        __syncthreads();                          // buf / swave reused by the next pass
     }
     if (threadIdx.x == 0) {
         csc_ptr[n] = carry;
@@ -962,46 +1024,73 @@ __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
     }
 }
 
+// tiles[0]: the arrival ticket (reset by the last block), tiles[1]: the published stamp
 __global__ void __launch_bounds__(kCscScanT)
 ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes,
-                      int hop, const uint64_t* __restrict__ g2l, int32_t* __restrict__ blk_idx,
-                      int cap_e, int32_t* __restrict__ csc_cnt, int32_t* __restrict__ crank,
-                      int32_t* __restrict__ ticket, int32_t* __restrict__ csc_ptr,
+                      int hop, const int64_t* __restrict__ state, const uint64_t* __restrict__ g2l,
+                      int32_t* __restrict__ blk_idx, const int32_t* __restrict__ blk_row,
+                      const uint8_t* __restrict__ blk_rel, int cap_e,
+                      int32_t* __restrict__ csc_cnt, int32_t* __restrict__ tiles,
+                      int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_ent,
                       int32_t* __restrict__ csc_long) {
-    __shared__ bool last;
+    __shared__ int sbuf[(kCscScanT / 64) * kCscScanPad];
+    __shared__ int swave[3 * (kCscScanT / 64)];
+    __shared__ int last;
     const int bp = blockIdx.x * kCscScanT + threadIdx.x;
+    int lid = -1, rank = 0, ent = 0;
     if (bp < cap_e) {
         const int u = gsrc[bp];
         if (u != -2) {                     // -2: an empty slot of the strided layout
-            int lid;
+            ent = (blk_row[bp] << 8) | int(blk_rel[bp]);
             if (u < 0) {                   // the self loop
                 lid = blk_idx[bp];
             } else {
                 lid = int32_t(uint32_t(g2l[u]));
                 blk_idx[bp] = lid;
             }
-            crank[bp] = atomicAdd(csc_cnt + lid, 1);     // integer: exact in any order
+            rank = atomicAdd(csc_cnt + lid, 1);          // integer: exact in any order
         }
     }
-    __threadfence();
+    const uint32_t stamp = ns_stamp(state, hop);
+    __syncthreads();                       // every count of this block added (values returned)
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               int(gridDim.x) - 1;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == int(gridDim.x) - 1;
+    if (last) {
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        csc_scan_block(csc_cnt, sizes[hop + 1], csc_ptr, csc_long, sbuf, swave);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(tiles, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(tiles + 1, int(stamp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    } else if (threadIdx.x == 0) {
+        // one lane polls the published stamp (relaxed), then one acquire; bounded (a watchdog:
+        // the last block holds a CU and runs to the publish)
+        for (uint32_t spins = 0; spins < (1u << 26); ++spins) {
+            if (uint32_t(__hip_atomic_load(tiles + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) == stamp)
+                break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    if (!last) return;
-    __threadfence();
-    csc_scan_block(csc_cnt, sizes[hop + 1], csc_ptr, csc_long);
-    if (threadIdx.x == 0) *ticket = 0;     // for the next hop / step
-}
-
-__global__ void __launch_bounds__(kBlock)
-ns_csc_place_kernel(const int32_t* __restrict__ blk_idx, const int32_t* __restrict__ blk_row,
-                    const uint8_t* __restrict__ blk_rel, const int32_t* __restrict__ crank,
-                    const int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_ent, int cap_e) {
-    const int bp = blockIdx.x * kBlock + threadIdx.x;
-    if (bp >= cap_e) return;
-    const int u = blk_idx[bp];
-    if (u < 0) return;                     // an empty slot
-    csc_ent[csc_ptr[u] + crank[bp]] = (blk_row[bp] << 8) | int(blk_rel[bp]);
+    if (lid >= 0) csc_ent[csc_ptr[lid] + rank] = ent;
 }
 
 // The strided hop's de-duplication and transposed index in ONE workgroup (replaces
@@ -1518,12 +1607,8 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         if (!csc || edge_type || lean) return REGNN_EINVAL;
         const int ce = int(cap_e);
         hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
-                           dim3(kCscScanT), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce,
-                           csc_cnt, samp, tiles, csc_ptr, csc_long);
-        REGNN_LAUNCH_CHECK();
-        hipLaunchKernelGGL(ns_csc_place_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, stream, blk_idx, blk_row, blk_rel, samp, csc_ptr,
-                           csc_ent, ce);
+                           dim3(kCscScanT), 0, stream, gsrc, sizes, hop, state, g2l, blk_idx,
+                           blk_row, blk_rel, ce, csc_cnt, tiles, csc_ptr, csc_ent, csc_long);
         REGNN_LAUNCH_CHECK();
         return REGNN_OK;
     }
@@ -1560,15 +1645,11 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         REGNN_LAUNCH_CHECK();
         if (csc && !edge_type && strided == 2) return REGNN_OK;   // the index: a strided = 3 call
         if (csc && !edge_type) {
-            // the transposed index by many blocks: resolve + counts + ranks (the last block
-            // scans), then the placement (samp holds each slot's rank: >= cap_e entries)
+            // the transposed index by many blocks in one launch: resolve + counts + ranks, the
+            // last block's scan, every block's placement
             hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
-                               dim3(kCscScanT), 0, stream, gsrc, sizes, hop, g2l, blk_idx, ce,
-                               csc_cnt, samp, tiles, csc_ptr, csc_long);
-            REGNN_LAUNCH_CHECK();
-            hipLaunchKernelGGL(ns_csc_place_kernel, dim3(unsigned((cap_e + kBlock - 1) / kBlock)),
-                               dim3(kBlock), 0, stream, blk_idx, blk_row, blk_rel, samp, csc_ptr,
-                               csc_ent, ce);
+                               dim3(kCscScanT), 0, stream, gsrc, sizes, hop, state, g2l, blk_idx,
+                               blk_row, blk_rel, ce, csc_cnt, tiles, csc_ptr, csc_ent, csc_long);
             REGNN_LAUNCH_CHECK();
             return REGNN_OK;
         }
@@ -1642,13 +1723,19 @@ int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_
     if (reinterpret_cast<uintptr_t>(s_agg) % 16 || reinterpret_cast<uintptr_t>(u_self) % 16)
         return REGNN_EINVAL;
     A.s_agg = s_agg; A.s_w = s_w; A.u_self = u_self; A.u_rel = u_rel;
+    static const int sum_blocks = [] {     // REGNN_NS_SUM_BLOCKS: cap the grid (0: a row per lane group)
+        const char* v = getenv("REGNN_NS_SUM_BLOCKS");
+        return v ? atoi(v) : 0;
+    }();
+    auto grid = [&](int rows_per_block) {
+        const int g = (cap_dst + rows_per_block - 1) / rows_per_block;
+        return dim3(unsigned(sum_blocks > 0 && sum_blocks < g ? sum_blocks : g));
+    };
     if (k + 1 <= 32)                   // two rows per wave (32 lanes each): sums in slot order
-        hipLaunchKernelGGL((ns_sample_sums_kernel<32, 4>),
-                           dim3(unsigned((cap_dst + 2 * kNsSumWaves - 1) / (2 * kNsSumWaves))),
+        hipLaunchKernelGGL((ns_sample_sums_kernel<32, 4>), grid(2 * kNsSumWaves),
                            dim3(64 * kNsSumWaves), 0, stream, A);
     else
-        hipLaunchKernelGGL((ns_sample_sums_kernel<64, 4>),
-                           dim3(unsigned((cap_dst + kNsSumWaves - 1) / kNsSumWaves)),
+        hipLaunchKernelGGL((ns_sample_sums_kernel<64, 4>), grid(kNsSumWaves),
                            dim3(64 * kNsSumWaves), 0, stream, A);
     REGNN_LAUNCH_CHECK();
     return REGNN_OK;

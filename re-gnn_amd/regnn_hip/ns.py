@@ -119,9 +119,9 @@ class DeviceSampler:
             ce = cd * (k + 1)
             nt = (ce + 1023) // 1024
             z = lambda n, dt=torch.int32: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
-            # samp: the strided transposed index's per-slot ranks too (>= ce); status: the
+            # tiles: the strided transposed index's ticket and stamp too (>= 2); status: the
             # strided de-duplication's look-back too (>= ceil(ce / 1024) tiles)
-            self.hop_bufs.append(dict(samp=z(ce), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
+            self.hop_bufs.append(dict(samp=z(cd * k), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
                                       flag=z(ce, torch.uint8), tiles=z(nt + 1),
                                       status=z(max((cd + 1023) // 1024, nt), torch.int64)))
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
