@@ -629,14 +629,31 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
  * u_rel[i][T] = the self loop's relation (regnn_nsm_work's layer-0 buffers, read by
  * regnn_nsm_step with pre_sums = 1; they depend on the batch only, so the sampler computes them
  * ahead of the model). T = n_types in [1, 4], k <= 63, tables / s_agg / u_self 16-byte aligned.
- * One launch. The summation order is fixed (the result is a function of the batch). */
+ * One launch. The summation order is fixed (the result is a function of the batch).
+ * csc (may be NULL; ABI 42): an earlier hop's transposed index, whose regnn_ns_hop call ran with
+ * strided = 2 (de-duplication done, index left out), built by extra workgroups of the same launch
+ * (regnn_ns_hop strided = 3's work, beside the sums instead of before them; same state / sizes). */
+typedef struct regnn_ns_csc_job {
+    int32_t hop;                /* that hop */
+    int32_t cap_e;              /* its block's slots: cap_dst * (k + 1) <= 32768 */
+    const int32_t* gsrc;        /* its buffers, as passed to regnn_ns_hop */
+    const uint64_t* g2l;
+    int32_t* blk_idx;
+    const int32_t* blk_row;
+    const uint8_t* blk_rel;
+    int32_t* csc_cnt;
+    int32_t* tiles;             /* >= 2 ints */
+    int32_t* csc_ptr;
+    int32_t* csc_ent;
+    int32_t* csc_long;
+} regnn_ns_csc_job;
 int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
                             const int32_t* ntype, int32_t num_edge_types, int32_t k, int32_t hop,
                             int64_t* state, int32_t* sizes, const int32_t* n_id, int32_t cap_dst,
                             int32_t* scnt, uint8_t* blk_rel, float* inv, const int64_t* local,
                             int32_t* edge_type, int64_t* edge_off, const float* const* tables,
                             int32_t n_types, int32_t K, float* s_agg, float* s_w, float* u_self,
-                            int32_t* u_rel, hipStream_t stream);
+                            int32_t* u_rel, const regnn_ns_csc_job* csc, hipStream_t stream);
 
 /* Backward of a sampled block's aggregation y[v] = out_scale[v] sum_e rel_table[rel_e] x[idx_e]
  * (+ bias) over rows v < n_rows (the forward is regnn_spmm_fwd on the block):

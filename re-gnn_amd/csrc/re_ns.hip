@@ -291,234 +291,6 @@ ns_sample_strided_kernel(const int32_t* __restrict__ ptr, const int32_t* __restr
     }
 }
 
-// The fused step's outer hop with layer 0's parameter-free input sums (relation slots): the
-// meta-only strided hop of ns_sample_strided_kernel (same sampling, same slots, edge meta and
-// counts), and then the row's G lanes gather its sampled raw input rows (K = 128 floats: G = 32
-// lanes x float4 per row, two rows per wave; G = 64: each half of the wave a float4 of alternate
-// rows) and sum them per source node type (mag/regnn_ns.py:300-326 + mag/regnn_layers.py:110-144:
-// with one relation per (target type, source type) pair, sum_{e: type t} tab[r_e] x_e =
-// tab[r_t] sum_{e: type t} x_e, so the sums do not depend on the parameters and run G steps ahead
-// on the sampler's stream). Writes per row i: s_agg[i][t][:] (unweighted sums), s_w[i][t]
-// (counts), u_self[i][:] (the self loop's row), u_rel[i][t] (the slot's relation or -1),
-// u_rel[i][T] (the self loop's relation) -- what agg0's gather phase formed (regnn_nsm_work), in
-// agg0's order: the entries in slot order (ascending CSR position), so G = 32 gives agg0's bits.
-struct NsSumArgs {
-    const int32_t* ptr; const int32_t* idx; const uint8_t* etype; const int32_t* ntype;
-    const int64_t* local; int n_et;
-    const int32_t* n_id; int32_t* sizes; int hop; int cap; int k;
-    int64_t* state;
-    int32_t* scnt; uint8_t* blk_rel; float* inv; int32_t* e_type; int64_t* e_off;
-    const float* xt[8]; int T;
-    float* s_agg; float* s_w; float* u_self; int32_t* u_rel;
-};
-
-template <int NT>
-__device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
-    const float* r = A.xt[0];
-#pragma unroll
-    for (int q = 1; q < NT; ++q)
-        if (t == q) r = A.xt[q];
-    return r;
-}
-
-constexpr int kNsSumK = 128;               // input row width of the sums kernel
-// entries' rows in flight per lane (32 lanes per row: two rounds of 11 for a fan-out of 20). All
-// 21 in one round (REGNN_NS_SUM_UN32=21: 168 VGPRs, 3 waves per SIMD) measured 118.3 against
-// 106.7 us per step: the sampler's kernel then holds more of the GPU beside the model
-#ifndef REGNN_NS_SUM_UN32
-#define REGNN_NS_SUM_UN32 11
-#endif
-template <int G>
-constexpr int ns_sum_un() { return G == 32 ? REGNN_NS_SUM_UN32 : 11; }
-constexpr int kNsSumOcc = REGNN_NS_SUM_UN32 > 11 ? 3 : 4;   // waves per SIMD the registers allow
-constexpr int kNsSumWaves = 4;             // waves per block (256 threads: they fit beside the
-                                           // model's kernels on a shared CU)
-
-template <int G, int NT>
-__global__ void __launch_bounds__(64 * kNsSumWaves, kNsSumOcc)
-ns_sample_sums_kernel(NsSumArgs A) {
-    constexpr int K = kNsSumK;
-    constexpr int kNsSumUN = ns_sum_un<G>();
-    constexpr int TPW = 64 / G;                // rows per wave
-    constexpr int H = G == 64 ? 2 : 1;         // lane groups of 32 per row (each a float4 column)
-    __shared__ int wsum[kNsSumWaves * TPW];
-    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int lane = wl % G, tl = wv * TPW + wl / G;
-    const uint64_t gmask = G == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
-    const int n = A.sizes[A.hop];
-    const int k = A.k, S = k + 1;
-    int etot = 0;                              // this lane's rows' edges (lane 0 of a row)
-    // grid-stride over row groups (uniform per block): a grid smaller than the rows (the launch's
-    // REGNN_NS_SUM_BLOCKS) keeps the kernel on fewer CUs beside the model's kernels
-    for (int ib = blockIdx.x * (kNsSumWaves * TPW); ib < A.cap; ib += gridDim.x * (kNsSumWaves * TPW)) {
-    const int i = ib + tl;
-    const int64_t base = int64_t(i) * S;
-    int cnt = -1;                              // -1: no row (past the batch)
-    if (i < A.cap && i >= n) {
-        if (lane == 0) {
-            A.scnt[i] = 0;
-            A.inv[i] = 1.f;
-        }
-    } else if (i < n) {
-        const uint64_t seed = ns_hop_seed(A.state, A.hop);
-        const int t = A.n_id[i];
-        const int b = A.ptr[t], d = A.ptr[t + 1] - b;
-        cnt = d < k ? d : k;
-        int slot = lane < d ? lane : -1, rank = lane;  // deg <= k: every position, in order
-        int src = lane;                        // the lane holding slot `lane`'s draw
-        if (d > k) {                               // Floyd (regnn_sample_fill's spec)
-            slot = -1;
-            const int jl = d - k + lane;
-            const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
-                                               uint64_t(jl + 1)) >> 32) : 0;
-            for (int q = 0; q < k; ++q) {
-                const int pos = __shfl(my_pos, q, G);
-                const bool seen = (__ballot(slot == pos) & gmask) != 0;
-                if (lane == q) slot = seen ? d - k + q : pos;
-            }
-            rank = 0;
-            for (int m = 0; m < k; ++m) {
-                const int other = __shfl(slot, m, G);
-                rank += (lane < k && other < slot) ? 1 : 0;
-            }
-            for (int m = 0; m < k; ++m)            // inverse: slot j's draw
-                if (__shfl(rank, m, G) == lane) src = m;
-        }
-        // this lane's draw: a sampled edge (lane < cnt)
-        int my_t = 0, my_lo = 0, my_r = 0;     // table rows < 2^31 (checked by the host)
-        if (lane < cnt) {
-            const int p = b + slot;
-            const int u = A.idx[p];
-            const int64_t bp = base + rank;
-            my_r = A.etype[p];
-            my_t = A.ntype[u];
-            const int64_t lo = A.local[u];
-            my_lo = int(lo);
-            A.blk_rel[bp] = uint8_t(my_r);
-            A.e_type[bp] = my_t;
-            A.e_off[bp] = lo;
-        }
-        // slot order: lane j < cnt takes slot j's entry, lane cnt the self loop
-        int st = __shfl(my_t, src, G), sr = __shfl(my_r, src, G), slo = __shfl(my_lo, src, G);
-        if (lane == cnt) {
-            const int64_t bp = base + cnt;
-            st = A.ntype[t];
-            sr = A.n_et + st;
-            const int64_t lo = A.local[t];
-            slo = int(lo);
-            A.blk_rel[bp] = uint8_t(sr);
-            A.e_type[bp] = st;
-            A.e_off[bp] = lo;
-        }
-        if (lane == 0) {
-            A.scnt[i] = cnt;
-            A.inv[i] = 1.f / float(cnt + 1);
-        }
-        // ---- the row's input sums over its entries j = h, h + H, ..; lane l a float4 column
-        const int h = lane >> 5, l = lane & 31;
-        const int ne = cnt + 1;
-        float4 racc[NT];
-        float ws[NT];
-        int rt[NT];
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) {
-            racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
-            ws[tt] = 0.f;
-            rt[tt] = -1;
-        }
-        float4 xs = make_float4(0.f, 0.f, 0.f, 0.f);
-        int rs = -1;
-        for (int j0 = 0; j0 < ne; j0 += H * kNsSumUN) {
-            float4 x[kNsSumUN];
-#pragma unroll
-            for (int u = 0; u < kNsSumUN; ++u) {
-                const int j = j0 + H * u + h;
-                const int jj = j < ne ? j : ne - 1;  // padding: a valid row, loaded, not added
-                const int tj = __shfl(st, jj, G);
-                const int64_t lo = __shfl(slo, jj, G);
-                x[u] = *reinterpret_cast<const float4*>(pick_tab<NT>(A, tj) + lo * K + 4 * l);
-            }
-            // (each entry's type / relation shuffled again here: arrays of them held across the
-            // loads cost the registers that keep every row in flight)
-#pragma unroll
-            for (int u = 0; u < kNsSumUN; ++u) {
-                const int j = j0 + H * u + h;
-                const int jj = j < ne ? j : ne - 1;
-                const int tj = __shfl(st, jj, G), rj = __shfl(sr, jj, G);
-                if (j >= ne) continue;
-                if (rj >= A.n_et) {                // the self loop (one per row)
-                    xs = x[u];
-                    rs = rj;
-                    continue;
-                }
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) {
-                    if (tt != tj) continue;
-                    ws[tt] += 1.f;
-                    rt[tt] = rj;
-                    racc[tt].x += x[u].x; racc[tt].y += x[u].y;
-                    racc[tt].z += x[u].z; racc[tt].w += x[u].w;
-                }
-            }
-        }
-        if constexpr (H == 2) {
-            // the two halves' sums (even / odd slots): half 0's first, the same bits in both
-            auto both = [&](float v) {
-                const float o = __shfl_xor(v, 32, 64);
-                return h == 0 ? v + o : o + v;
-            };
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-                racc[tt] = make_float4(both(racc[tt].x), both(racc[tt].y), both(racc[tt].z),
-                                       both(racc[tt].w));
-                ws[tt] = both(ws[tt]);
-                rt[tt] = max(rt[tt], __shfl_xor(rt[tt], 32, 64));
-            }
-            const int rso = __shfl_xor(rs, 32, 64);
-            const float4 xo = make_float4(__shfl_xor(xs.x, 32, 64), __shfl_xor(xs.y, 32, 64),
-                                          __shfl_xor(xs.z, 32, 64), __shfl_xor(xs.w, 32, 64));
-            if (rs < 0) {
-                xs = xo;
-                rs = rso;
-            }
-        }
-        const int T = A.T;
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt)
-            if (tt < T && (H == 1 || (tt & 1) == h))
-                *reinterpret_cast<float4*>(A.s_agg + (int64_t(i) * T + tt) * K + 4 * l) = racc[tt];
-        if (H == 1 || h == 1) *reinterpret_cast<float4*>(A.u_self + int64_t(i) * K + 4 * l) = xs;
-        if (lane < T) {
-            float wv_ = 0.f;
-            int rv_ = -1;
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt)
-                if (tt == lane) {
-                    wv_ = ws[tt];
-                    rv_ = rt[tt];
-                }
-            A.s_w[int64_t(i) * T + lane] = wv_;
-            A.u_rel[int64_t(i) * (T + 1) + lane] = rv_;
-        } else if (lane == T) {
-            A.u_rel[int64_t(i) * (T + 1) + T] = rs;
-        }
-    }
-    etot += cnt + 1;                           // edges of the row, self loop included
-    }
-    if (lane == 0) wsum[tl] = etot;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int e = 0;
-#pragma unroll
-        for (int q = 0; q < kNsSumWaves * TPW; ++q) e += wsum[q];
-        if (e) {
-            atomicAdd(A.sizes + 8 + A.hop, e);
-            atomicAdd(reinterpret_cast<unsigned long long*>(A.state + 5), (unsigned long long)e);
-        }
-        if (blockIdx.x == 0) A.sizes[A.hop + 1] = n;
-    }
-}
-
 // row offsets (sampled count + the self loop), 1/in-count and the self-loop entries: one tile of
 // kNsRowsTile rows per block, the tiles' exclusive prefix by decoupled look-back (integer sums:
 // exact in any order). status[tile] = stamp << 32 | kind << 30 | value, kind 1 = the tile's own
@@ -921,25 +693,27 @@ ns_csc_kernel(const int32_t* __restrict__ sizes, int hop, const int32_t* __restr
 // running, it took the last ticket). The order inside a segment follows the counters' atomics
 // (unspecified: the consumer's sums are exact fixed-point).
 constexpr int kCscScanT = 256;             // 256-thread blocks: they fit beside the model's kernels
-constexpr int kCscScanQ = 16;              // counts per lane per pass (lane-contiguous)
-constexpr int kCscScanWE = 64 * kCscScanQ; // counts per wave per pass
-constexpr int kCscScanPad = kCscScanWE + kCscScanWE / kCscScanQ;   // LDS words per wave (padded)
+// counts per lane per pass (lane-contiguous): 16 in the index's own launch, 4 beside the sums
+// (whose launch would otherwise hold the larger LDS in every block)
+template <int Q>
+constexpr int csc_scan_pad() { return 64 * Q + 64; }   // LDS words per wave (padded)
 
-// The scan of the per-source counts by one 256-thread block: per pass each wave loads 1,024
-// counts coalesced, transposes them through LDS (index e at e + e / 16: conflict-free both ways)
-// so each lane holds 16 consecutive counts, scans lane-serially and across the wave (shuffles),
+// The scan of the per-source counts by one 256-thread block: per pass each wave loads 64 Q
+// counts coalesced, transposes them through LDS (index e at e + e / Q) so each lane holds Q
+// consecutive counts, scans lane-serially and across the wave (shuffles),
 // combines the four waves through LDS, and writes csc_ptr back coalesced through the same LDS.
 // Hub rows (more than kCscShort entries) are listed ascending with their pieces.
+template <int Q>
 __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
                                int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_long,
                                int* __restrict__ sbuf, int* __restrict__ swave) {
-    constexpr int NW = kCscScanT / 64, Q = kCscScanQ;
+    constexpr int NW = kCscScanT / 64, WE = 64 * Q;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int* buf = sbuf + w * kCscScanPad;
+    int* buf = sbuf + w * csc_scan_pad<Q>();
     int carry = 0, lcarry = 0, pcarry = 0;
     int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
-    for (int base = 0; base < n; base += NW * kCscScanWE) {
-        const int wb = base + w * kCscScanWE;
+    for (int base = 0; base < n; base += NW * WE) {
+        const int wb = base + w * WE;
         int v[Q];
 #pragma unroll
         for (int j = 0; j < Q; ++j) {
@@ -949,7 +723,7 @@ __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
 #pragma unroll
         for (int j = 0; j < Q; ++j) {
             const int e = j * 64 + lane;
-            buf[e + (e >> 4)] = v[j];
+            buf[e + e / Q] = v[j];
         }
         __syncthreads();
         int s = 0, nl = 0, np = 0;
@@ -1010,7 +784,7 @@ __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
 #pragma unroll
         for (int j = 0; j < Q; ++j) {
             const int e = j * 64 + lane;
-            if (wb + e < n) csc_ptr[wb + e] = buf[e + (e >> 4)];
+            if (wb + e < n) csc_ptr[wb + e] = buf[e + e / Q];
         }
         carry += ts;
         lcarry += tl;
@@ -1024,40 +798,43 @@ __device__ void csc_scan_block(const int32_t* __restrict__ csc_cnt, int n,
     }
 }
 
-// tiles[0]: the arrival ticket (reset by the last block), tiles[1]: the published stamp
-__global__ void __launch_bounds__(kCscScanT)
-ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restrict__ sizes,
-                      int hop, const int64_t* __restrict__ state, const uint64_t* __restrict__ g2l,
-                      int32_t* __restrict__ blk_idx, const int32_t* __restrict__ blk_row,
-                      const uint8_t* __restrict__ blk_rel, int cap_e,
-                      int32_t* __restrict__ csc_cnt, int32_t* __restrict__ tiles,
-                      int32_t* __restrict__ csc_ptr, int32_t* __restrict__ csc_ent,
-                      int32_t* __restrict__ csc_long) {
-    __shared__ int sbuf[(kCscScanT / 64) * kCscScanPad];
+struct NsCscJob {
+    int hop, cap_e;
+    const int32_t* gsrc; const uint64_t* g2l;
+    int32_t* blk_idx; const int32_t* blk_row; const uint8_t* blk_rel;
+    int32_t* csc_cnt; int32_t* tiles; int32_t* csc_ptr; int32_t* csc_ent; int32_t* csc_long;
+};
+
+// One workgroup (block `bid` of `nb`) of the transposed index's launch. tiles[0]: the arrival
+// ticket (reset by the last block), tiles[1]: the published stamp
+template <int Q>
+__device__ void csc_resolve_place(const NsCscJob& J, const int32_t* __restrict__ sizes,
+                                  const int64_t* __restrict__ state, int bid, int nb) {
+    __shared__ int sbuf[(kCscScanT / 64) * csc_scan_pad<Q>()];
     __shared__ int swave[3 * (kCscScanT / 64)];
     __shared__ int last;
-    const int bp = blockIdx.x * kCscScanT + threadIdx.x;
+    const int bp = bid * kCscScanT + threadIdx.x;
     int lid = -1, rank = 0, ent = 0;
-    if (bp < cap_e) {
-        const int u = gsrc[bp];
+    if (bp < J.cap_e) {
+        const int u = J.gsrc[bp];
         if (u != -2) {                     // -2: an empty slot of the strided layout
-            ent = (blk_row[bp] << 8) | int(blk_rel[bp]);
+            ent = (J.blk_row[bp] << 8) | int(J.blk_rel[bp]);
             if (u < 0) {                   // the self loop
-                lid = blk_idx[bp];
+                lid = J.blk_idx[bp];
             } else {
-                lid = int32_t(uint32_t(g2l[u]));
-                blk_idx[bp] = lid;
+                lid = int32_t(uint32_t(J.g2l[u]));
+                J.blk_idx[bp] = lid;
             }
-            rank = atomicAdd(csc_cnt + lid, 1);          // integer: exact in any order
+            rank = atomicAdd(J.csc_cnt + lid, 1);        // integer: exact in any order
         }
     }
-    const uint32_t stamp = ns_stamp(state, hop);
+    const uint32_t stamp = ns_stamp(state, J.hop);
     __syncthreads();                       // every count of this block added (values returned)
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               int(gridDim.x) - 1;
+        last = __hip_atomic_fetch_add(J.tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               nb - 1;
     }
     __syncthreads();
     if (last) {
@@ -1066,14 +843,14 @@ ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restric
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        csc_scan_block(csc_cnt, sizes[hop + 1], csc_ptr, csc_long, sbuf, swave);
+        csc_scan_block<Q>(J.csc_cnt, sizes[J.hop + 1], J.csc_ptr, J.csc_long, sbuf, swave);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
         __syncthreads();
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(tiles, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(tiles + 1, int(stamp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(J.tiles, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(J.tiles + 1, int(stamp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -1081,7 +858,7 @@ ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restric
         // one lane polls the published stamp (relaxed), then one acquire; bounded (a watchdog:
         // the last block holds a CU and runs to the publish)
         for (uint32_t spins = 0; spins < (1u << 26); ++spins) {
-            if (uint32_t(__hip_atomic_load(tiles + 1, __ATOMIC_RELAXED,
+            if (uint32_t(__hip_atomic_load(J.tiles + 1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT)) == stamp)
                 break;
             __builtin_amdgcn_s_sleep(1);
@@ -1090,7 +867,251 @@ ns_resolve_csc_kernel(const int32_t* __restrict__ gsrc, const int32_t* __restric
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (lid >= 0) csc_ent[csc_ptr[lid] + rank] = ent;
+    if (lid >= 0) J.csc_ent[J.csc_ptr[lid] + rank] = ent;
+}
+
+inline int csc_blocks(int64_t cap_e) { return int((cap_e + kCscScanT - 1) / kCscScanT); }
+
+__global__ void __launch_bounds__(kCscScanT)
+ns_resolve_csc_kernel(NsCscJob J, const int32_t* __restrict__ sizes,
+                      const int64_t* __restrict__ state) {
+    csc_resolve_place<16>(J, sizes, state, blockIdx.x, gridDim.x);
+}
+
+// The fused step's outer hop with layer 0's parameter-free input sums (relation slots): the
+// meta-only strided hop of ns_sample_strided_kernel (same sampling, same slots, edge meta and
+// counts), and then the row's G lanes gather its sampled raw input rows (K = 128 floats: G = 32
+// lanes x float4 per row, two rows per wave; G = 64: each half of the wave a float4 of alternate
+// rows) and sum them per source node type (mag/regnn_ns.py:300-326 + mag/regnn_layers.py:110-144:
+// with one relation per (target type, source type) pair, sum_{e: type t} tab[r_e] x_e =
+// tab[r_t] sum_{e: type t} x_e, so the sums do not depend on the parameters and run G steps ahead
+// on the sampler's stream). Writes per row i: s_agg[i][t][:] (unweighted sums), s_w[i][t]
+// (counts), u_self[i][:] (the self loop's row), u_rel[i][t] (the slot's relation or -1),
+// u_rel[i][T] (the self loop's relation) -- what agg0's gather phase formed (regnn_nsm_work), in
+// agg0's order: the entries in slot order (ascending CSR position), so G = 32 gives agg0's bits.
+struct NsSumArgs {
+    const int32_t* ptr; const int32_t* idx; const uint8_t* etype; const int32_t* ntype;
+    const int64_t* local; int n_et;
+    const int32_t* n_id; int32_t* sizes; int hop; int cap; int k;
+    int64_t* state;
+    int32_t* scnt; uint8_t* blk_rel; float* inv; int32_t* e_type; int64_t* e_off;
+    const float* xt[8]; int T;
+    float* s_agg; float* s_w; float* u_self; int32_t* u_rel;
+    NsCscJob csc; int csc_blocks;          // an earlier hop's transposed index (csc_blocks > 0)
+};
+
+template <int NT>
+__device__ __forceinline__ const float* pick_tab(const NsSumArgs& A, int t) {
+    const float* r = A.xt[0];
+#pragma unroll
+    for (int q = 1; q < NT; ++q)
+        if (t == q) r = A.xt[q];
+    return r;
+}
+
+constexpr int kNsSumK = 128;               // input row width of the sums kernel
+// entries' rows in flight per lane (32 lanes per row: two rounds of 11 for a fan-out of 20). All
+// 21 in one round (REGNN_NS_SUM_UN32=21: 168 VGPRs, 3 waves per SIMD) measured 118.3 against
+// 106.7 us per step: the sampler's kernel then holds more of the GPU beside the model
+#ifndef REGNN_NS_SUM_UN32
+#define REGNN_NS_SUM_UN32 11
+#endif
+template <int G>
+constexpr int ns_sum_un() { return G == 32 ? REGNN_NS_SUM_UN32 : 11; }
+constexpr int kNsSumOcc = REGNN_NS_SUM_UN32 > 11 ? 3 : 4;   // waves per SIMD the registers allow
+constexpr int kNsSumWaves = 4;             // waves per block (256 threads: they fit beside the
+                                           // model's kernels on a shared CU)
+
+template <int G, int NT>
+__global__ void __launch_bounds__(64 * kNsSumWaves, kNsSumOcc)
+ns_sample_sums_kernel(NsSumArgs A) {
+    // the first csc_blocks workgroups build the earlier hop's transposed index (latency-bound:
+    // dispatched first, they run beside the sums instead of ahead of them)
+    if (int(blockIdx.x) < A.csc_blocks) {
+        csc_resolve_place<4>(A.csc, A.sizes, A.state, blockIdx.x, A.csc_blocks);
+        return;
+    }
+    const int bid = blockIdx.x - A.csc_blocks, nbk = gridDim.x - A.csc_blocks;
+    constexpr int K = kNsSumK;
+    constexpr int kNsSumUN = ns_sum_un<G>();
+    constexpr int TPW = 64 / G;                // rows per wave
+    constexpr int H = G == 64 ? 2 : 1;         // lane groups of 32 per row (each a float4 column)
+    __shared__ int wsum[kNsSumWaves * TPW];
+    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = wl % G, tl = wv * TPW + wl / G;
+    const uint64_t gmask = G == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
+    const int n = A.sizes[A.hop];
+    const int k = A.k, S = k + 1;
+    int etot = 0;                              // this lane's rows' edges (lane 0 of a row)
+    // grid-stride over row groups (uniform per block): a grid smaller than the rows (the launch's
+    // REGNN_NS_SUM_BLOCKS) keeps the kernel on fewer CUs beside the model's kernels
+    for (int ib = bid * (kNsSumWaves * TPW); ib < A.cap; ib += nbk * (kNsSumWaves * TPW)) {
+    const int i = ib + tl;
+    const int64_t base = int64_t(i) * S;
+    int cnt = -1;                              // -1: no row (past the batch)
+    if (i < A.cap && i >= n) {
+        if (lane == 0) {
+            A.scnt[i] = 0;
+            A.inv[i] = 1.f;
+        }
+    } else if (i < n) {
+        const uint64_t seed = ns_hop_seed(A.state, A.hop);
+        const int t = A.n_id[i];
+        const int b = A.ptr[t], d = A.ptr[t + 1] - b;
+        cnt = d < k ? d : k;
+        int slot = lane < d ? lane : -1, rank = lane;  // deg <= k: every position, in order
+        int src = lane;                        // the lane holding slot `lane`'s draw
+        if (d > k) {                               // Floyd (regnn_sample_fill's spec)
+            slot = -1;
+            const int jl = d - k + lane;
+            const int my_pos = lane < k ? int((uint64_t(ns_hash(seed, uint64_t(t), uint64_t(jl))) *
+                                               uint64_t(jl + 1)) >> 32) : 0;
+            for (int q = 0; q < k; ++q) {
+                const int pos = __shfl(my_pos, q, G);
+                const bool seen = (__ballot(slot == pos) & gmask) != 0;
+                if (lane == q) slot = seen ? d - k + q : pos;
+            }
+            rank = 0;
+            for (int m = 0; m < k; ++m) {
+                const int other = __shfl(slot, m, G);
+                rank += (lane < k && other < slot) ? 1 : 0;
+            }
+            for (int m = 0; m < k; ++m)            // inverse: slot j's draw
+                if (__shfl(rank, m, G) == lane) src = m;
+        }
+        // this lane's draw: a sampled edge (lane < cnt)
+        int my_t = 0, my_lo = 0, my_r = 0;     // table rows < 2^31 (checked by the host)
+        if (lane < cnt) {
+            const int p = b + slot;
+            const int u = A.idx[p];
+            const int64_t bp = base + rank;
+            my_r = A.etype[p];
+            my_t = A.ntype[u];
+            const int64_t lo = A.local[u];
+            my_lo = int(lo);
+            A.blk_rel[bp] = uint8_t(my_r);
+            A.e_type[bp] = my_t;
+            A.e_off[bp] = lo;
+        }
+        // slot order: lane j < cnt takes slot j's entry, lane cnt the self loop
+        int st = __shfl(my_t, src, G), sr = __shfl(my_r, src, G), slo = __shfl(my_lo, src, G);
+        if (lane == cnt) {
+            const int64_t bp = base + cnt;
+            st = A.ntype[t];
+            sr = A.n_et + st;
+            const int64_t lo = A.local[t];
+            slo = int(lo);
+            A.blk_rel[bp] = uint8_t(sr);
+            A.e_type[bp] = st;
+            A.e_off[bp] = lo;
+        }
+        if (lane == 0) {
+            A.scnt[i] = cnt;
+            A.inv[i] = 1.f / float(cnt + 1);
+        }
+        // ---- the row's input sums over its entries j = h, h + H, ..; lane l a float4 column
+        const int h = lane >> 5, l = lane & 31;
+        const int ne = cnt + 1;
+        float4 racc[NT];
+        float ws[NT];
+        int rt[NT];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            racc[tt] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ws[tt] = 0.f;
+            rt[tt] = -1;
+        }
+        float4 xs = make_float4(0.f, 0.f, 0.f, 0.f);
+        int rs = -1;
+        for (int j0 = 0; j0 < ne; j0 += H * kNsSumUN) {
+            float4 x[kNsSumUN];
+#pragma unroll
+            for (int u = 0; u < kNsSumUN; ++u) {
+                const int j = j0 + H * u + h;
+                const int jj = j < ne ? j : ne - 1;  // padding: a valid row, loaded, not added
+                const int tj = __shfl(st, jj, G);
+                const int64_t lo = __shfl(slo, jj, G);
+                x[u] = *reinterpret_cast<const float4*>(pick_tab<NT>(A, tj) + lo * K + 4 * l);
+            }
+            // (each entry's type / relation shuffled again here: arrays of them held across the
+            // loads cost the registers that keep every row in flight)
+#pragma unroll
+            for (int u = 0; u < kNsSumUN; ++u) {
+                const int j = j0 + H * u + h;
+                const int jj = j < ne ? j : ne - 1;
+                const int tj = __shfl(st, jj, G), rj = __shfl(sr, jj, G);
+                if (j >= ne) continue;
+                if (rj >= A.n_et) {                // the self loop (one per row)
+                    xs = x[u];
+                    rs = rj;
+                    continue;
+                }
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    if (tt != tj) continue;
+                    ws[tt] += 1.f;
+                    rt[tt] = rj;
+                    racc[tt].x += x[u].x; racc[tt].y += x[u].y;
+                    racc[tt].z += x[u].z; racc[tt].w += x[u].w;
+                }
+            }
+        }
+        if constexpr (H == 2) {
+            // the two halves' sums (even / odd slots): half 0's first, the same bits in both
+            auto both = [&](float v) {
+                const float o = __shfl_xor(v, 32, 64);
+                return h == 0 ? v + o : o + v;
+            };
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                racc[tt] = make_float4(both(racc[tt].x), both(racc[tt].y), both(racc[tt].z),
+                                       both(racc[tt].w));
+                ws[tt] = both(ws[tt]);
+                rt[tt] = max(rt[tt], __shfl_xor(rt[tt], 32, 64));
+            }
+            const int rso = __shfl_xor(rs, 32, 64);
+            const float4 xo = make_float4(__shfl_xor(xs.x, 32, 64), __shfl_xor(xs.y, 32, 64),
+                                          __shfl_xor(xs.z, 32, 64), __shfl_xor(xs.w, 32, 64));
+            if (rs < 0) {
+                xs = xo;
+                rs = rso;
+            }
+        }
+        const int T = A.T;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+            if (tt < T && (H == 1 || (tt & 1) == h))
+                *reinterpret_cast<float4*>(A.s_agg + (int64_t(i) * T + tt) * K + 4 * l) = racc[tt];
+        if (H == 1 || h == 1) *reinterpret_cast<float4*>(A.u_self + int64_t(i) * K + 4 * l) = xs;
+        if (lane < T) {
+            float wv_ = 0.f;
+            int rv_ = -1;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt)
+                if (tt == lane) {
+                    wv_ = ws[tt];
+                    rv_ = rt[tt];
+                }
+            A.s_w[int64_t(i) * T + lane] = wv_;
+            A.u_rel[int64_t(i) * (T + 1) + lane] = rv_;
+        } else if (lane == T) {
+            A.u_rel[int64_t(i) * (T + 1) + T] = rs;
+        }
+    }
+    etot += cnt + 1;                           // edges of the row, self loop included
+    }
+    if (lane == 0) wsum[tl] = etot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int e = 0;
+#pragma unroll
+        for (int q = 0; q < kNsSumWaves * TPW; ++q) e += wsum[q];
+        if (e) {
+            atomicAdd(A.sizes + 8 + A.hop, e);
+            atomicAdd(reinterpret_cast<unsigned long long*>(A.state + 5), (unsigned long long)e);
+        }
+        if (bid == 0) A.sizes[A.hop + 1] = n;
+    }
 }
 
 // The strided hop's de-duplication and transposed index in ONE workgroup (replaces
@@ -1606,9 +1627,10 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         // the caller runs it: resolve + counts + ranks, scan, placement
         if (!csc || edge_type || lean) return REGNN_EINVAL;
         const int ce = int(cap_e);
-        hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
-                           dim3(kCscScanT), 0, stream, gsrc, sizes, hop, state, g2l, blk_idx,
-                           blk_row, blk_rel, ce, csc_cnt, tiles, csc_ptr, csc_ent, csc_long);
+        const NsCscJob J{hop, ce, gsrc, g2l, blk_idx, blk_row, blk_rel, csc_cnt, tiles, csc_ptr,
+                         csc_ent, csc_long};
+        hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned(csc_blocks(cap_e))),
+                           dim3(kCscScanT), 0, stream, J, sizes, state);
         REGNN_LAUNCH_CHECK();
         return REGNN_OK;
     }
@@ -1647,9 +1669,10 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         if (csc && !edge_type) {
             // the transposed index by many blocks in one launch: resolve + counts + ranks, the
             // last block's scan, every block's placement
-            hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned((cap_e + kCscScanT - 1) / kCscScanT)),
-                               dim3(kCscScanT), 0, stream, gsrc, sizes, hop, state, g2l, blk_idx,
-                               blk_row, blk_rel, ce, csc_cnt, tiles, csc_ptr, csc_ent, csc_long);
+            const NsCscJob J{hop, ce, gsrc, g2l, blk_idx, blk_row, blk_rel, csc_cnt, tiles,
+                             csc_ptr, csc_ent, csc_long};
+            hipLaunchKernelGGL(ns_resolve_csc_kernel, dim3(unsigned(csc_blocks(cap_e))),
+                               dim3(kCscScanT), 0, stream, J, sizes, state);
             REGNN_LAUNCH_CHECK();
             return REGNN_OK;
         }
@@ -1703,7 +1726,7 @@ int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_
                             int32_t* scnt, uint8_t* blk_rel, float* inv, const int64_t* local,
                             int32_t* edge_type, int64_t* edge_off, const float* const* tables,
                             int32_t n_types, int32_t K, float* s_agg, float* s_w, float* u_self,
-                            int32_t* u_rel, hipStream_t stream) {
+                            int32_t* u_rel, const regnn_ns_csc_job* csc, hipStream_t stream) {
     if (!ptr || !idx || !etype || !ntype || !state || !sizes || !n_id || !scnt || !blk_rel ||
         !inv || !local || !edge_type || !edge_off || !tables || !s_agg || !s_w || !u_self ||
         !u_rel || cap_dst <= 0 || hop < 0 || hop > 6 || num_edge_types < 0)
@@ -1723,13 +1746,24 @@ int regnn_ns_hop_typed_sums(const int32_t* ptr, const int32_t* idx, const uint8_
     if (reinterpret_cast<uintptr_t>(s_agg) % 16 || reinterpret_cast<uintptr_t>(u_self) % 16)
         return REGNN_EINVAL;
     A.s_agg = s_agg; A.s_w = s_w; A.u_self = u_self; A.u_rel = u_rel;
+    if (csc) {
+        if (!csc->gsrc || !csc->g2l || !csc->blk_idx || !csc->blk_row || !csc->blk_rel ||
+            !csc->csc_cnt || !csc->tiles || !csc->csc_ptr || !csc->csc_ent || !csc->csc_long ||
+            csc->hop < 0 || csc->hop >= hop || csc->cap_e <= 0)
+            return REGNN_EINVAL;
+        if (csc->cap_e > kCscMax) return REGNN_EUNSUPPORTED;
+        A.csc = NsCscJob{csc->hop, csc->cap_e, csc->gsrc, csc->g2l, csc->blk_idx, csc->blk_row,
+                         csc->blk_rel, csc->csc_cnt, csc->tiles, csc->csc_ptr, csc->csc_ent,
+                         csc->csc_long};
+        A.csc_blocks = csc_blocks(csc->cap_e);
+    }
     static const int sum_blocks = [] {     // REGNN_NS_SUM_BLOCKS: cap the grid (0: a row per lane group)
         const char* v = getenv("REGNN_NS_SUM_BLOCKS");
         return v ? atoi(v) : 0;
     }();
     auto grid = [&](int rows_per_block) {
         const int g = (cap_dst + rows_per_block - 1) / rows_per_block;
-        return dim3(unsigned(sum_blocks > 0 && sum_blocks < g ? sum_blocks : g));
+        return dim3(unsigned(A.csc_blocks + (sum_blocks > 0 && sum_blocks < g ? sum_blocks : g)));
     };
     if (k + 1 <= 32)                   // two rows per wave (32 lanes each): sums in slot order
         hipLaunchKernelGGL((ns_sample_sums_kernel<32, 4>), grid(2 * kNsSumWaves),

@@ -97,7 +97,7 @@ _SIG = {
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_ns_hop_typed_sums": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P,
-                                 I32, I32, P, P, P, P, P], ctypes.c_int),
+                                 I32, I32, P, P, P, P, P, P], ctypes.c_int),
     "regnn_ns_spmm_bwd": ([P, P, P, P, P, P, P, P, P, I32, I64, I32, P], ctypes.c_int),
     "regnn_ns_csc_hub_work_floats": ([I32], I64),
     "regnn_ns_spmm_bwd_csc": ([P, P, P, P, P, P, P, P, P, I32, P, I32, I64, I32, I32, P, P],

@@ -142,6 +142,7 @@ class DeviceSampler:
         # typed_sums[h]: hop h (meta-only, strided) also forms layer 0's input sums for the
         # fused step (regnn_ns_hop_typed_sums; FusedStep.enable_pre_sums), or None
         self.typed_sums = [None] * len(self.sizes_k)
+        self._csc_jobs = {}
         self._csr_fresh = True
 
     def enable_edge_meta(self, local_node_idx, hop):
@@ -180,13 +181,13 @@ class DeviceSampler:
         the caller joins it."""
         strided = self.strided if strided is None else bool(strided)
         rg = self.rg
+        deferred = -1
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
             fork = (csc_stream is not None and strided and self.csc[h] is not None and
                     self.edge_meta[h] is None)
-            ts = self.typed_sums[h]
-            if (ts is not None and strided and meta_only and self.meta_only[h] and
-                    self.edge_meta[h] is not None):
+            if self._sums_path(h, strided, meta_only):
+                ts = self.typed_sums[h]
                 et, eo = self.edge_meta[h]
                 L.call("regnn_ns_hop_typed_sums", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
                        L.ptr(self.etype_csr), L.ptr(self.ntype), self.num_edge_types, k, h,
@@ -194,9 +195,15 @@ class DeviceSampler:
                        L.ptr(b["scnt"]), L.ptr(blk.rel), L.ptr(blk.inv), L.ptr(self.local),
                        L.ptr(et), L.ptr(eo), ts["tables"], ts["T"], ts["K"],
                        L.ptr(ts["s_agg"]), L.ptr(ts["s_w"]), L.ptr(ts["u_self"]),
-                       L.ptr(ts["u_rel"]), L.stream())
+                       L.ptr(ts["u_rel"]),
+                       ctypes.addressof(self._csc_job(h - 1)) if deferred == h - 1 else None,
+                       L.stream())
                 self.meta_fresh[h] = True
                 continue
+            # the transposed index of this hop built beside the next hop's sums (one launch)
+            defer = (not fork and strided and CSC_FUSE["mode"] != "off" and
+                     self.csc[h] is not None and self.edge_meta[h] is None and
+                     h + 1 < len(self.sizes_k) and self._sums_path(h + 1, strided, meta_only))
             L.call("regnn_ns_hop", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(self.etype_csr),
                    L.ptr(self.ntype), self.num_edge_types, k, h, L.ptr(self.state),
                    L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h], L.ptr(self.g2l),
@@ -210,7 +217,8 @@ class DeviceSampler:
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
                      else (None, None, None, None)),
-                   2 if fork else int(strided), L.stream())
+                   2 if fork or defer else int(strided), L.stream())
+            deferred = h if defer else -1
             if fork:
                 csc_stream.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(csc_stream):
@@ -218,6 +226,23 @@ class DeviceSampler:
             self.meta_fresh[h] = self.edge_meta[h] is not None
         # the blocks now hold the CSR layout (readable by exact_adjs / model_blocks) or not
         self._csr_fresh = not strided
+
+    def _sums_path(self, h, strided, meta_only):
+        """hop h runs as regnn_ns_hop_typed_sums (the fused step's outer hop with layer 0's sums)"""
+        return (self.typed_sums[h] is not None and strided and meta_only and self.meta_only[h]
+                and self.edge_meta[h] is not None)
+
+    def _csc_job(self, h):
+        """regnn_ns_csc_job of hop h's transposed index (its buffers are fixed: built once)"""
+        job = self._csc_jobs.get(h)
+        if job is None:
+            b, blk = self.hop_bufs[h], self.blocks[h]
+            cnt, cptr, cent, clong = self.csc[h]
+            job = self._csc_jobs[h] = _NsCscJob(
+                h, blk.csr_idx.numel(), L.ptr(b["gsrc"]), L.ptr(self.g2l), L.ptr(blk.csr_idx),
+                L.ptr(blk.row), L.ptr(blk.rel), L.ptr(cnt), L.ptr(b["tiles"]), L.ptr(cptr),
+                L.ptr(cent), L.ptr(clong))
+        return job
 
     def _hop_call(self, h, k, meta_only, mode):
         rg, b, blk = self.rg, self.hop_bufs[h], self.blocks[h]
@@ -335,6 +360,13 @@ _MAX_PIECE = 32768 // _CSC_PIECE + _LONG_CAP
 CSC_LONG_INTS = ((_LONG_CAP + 2) + 3) // 4 * 4 + 4 * _MAX_PIECE
 
 
+class _NsCscJob(ctypes.Structure):
+    """regnn_ns_csc_job (include/regnn_hip.h)."""
+    _fields_ = [("hop", ctypes.c_int32), ("cap_e", ctypes.c_int32), ("gsrc", _P), ("g2l", _P),
+                ("blk_idx", _P), ("blk_row", _P), ("blk_rel", _P), ("csc_cnt", _P),
+                ("tiles", _P), ("csc_ptr", _P), ("csc_ent", _P), ("csc_long", _P)]
+
+
 class _NsmAdam(ctypes.Structure):
     """regnn_nsm_adam (include/regnn_hip.h)."""
     _fields_ = [("param", _P), ("exp_avg", _P), ("exp_avg_sq", _P), ("grad_base", _P),
@@ -413,6 +445,12 @@ MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # next batch) segfaults inside torch.cuda.graph's capture_end on this image (ROCm 7.2, torch
 # 2.10), so the graphed bench cannot use it
 CSC_FORK = {"mode": os.environ.get("REGNN_NS_CSC_FORK", "off")}
+# "on": hop 0's transposed index is built by extra workgroups of the outer hop's sums launch
+# (regnn_ns_hop_typed_sums csc), beside the sums instead of ahead of them in the sampler's
+# chain; "off" (default): its own launch after hop 0's de-duplication. Measured (interleaved,
+# 300 steps): 111.1-111.5 us on against 107.7-108.4 off -- the sampler's chain is not what
+# bounds the step; its waiting workgroups beside the model's kernels cost more than they save
+CSC_FUSE = {"mode": os.environ.get("REGNN_NS_CSC_FUSE", "off")}
 # the fused engine's sampling lookahead G: 2G sampler slots, each step samples the batch trained
 # G steps later, and a G-step graph trains G slots while the sampler fills the other G on the
 # second queue with one fork (the graph's root) and one join (its end) -- instead of a fork and

@@ -749,8 +749,9 @@ def test_block_transposed_index():
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
 
 
-@pytest.mark.parametrize("half_waves,dedup_one", [("0", "0"), ("1", "0"), ("0", "1")])
-def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one):
+@pytest.mark.parametrize("half_waves,dedup_one,csc_fuse",
+                         [("0", "0", "on"), ("1", "0", "on"), ("0", "0", "off"), ("0", "1", "off")])
+def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one, csc_fuse):
     """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
     launch) against the CSR layout on the same batches: the same n_id, sizes, per-row edges
     (local source, relation, CSR position, target row; the meta-only hop's source type / table
@@ -762,6 +763,9 @@ def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one):
     # "0": the multi-block kernels (one-pass look-back dedup, resolve + ranks + last-block scan,
     # placement); "1": hop 0's de-duplication and transposed index in one workgroup
     monkeypatch.setenv("REGNN_NS_DEDUP_ONE", dedup_one)
+    # "on": hop 0's transposed index built by extra workgroups of hop 1's sums launch; "off": its
+    # own launch after the de-duplication
+    monkeypatch.setitem(ns.CSC_FUSE, "mode", csc_fuse)
     d = _mag(0.003, seed=10, F=128, hidden=64, classes=19, dropout=0.5)
     trs, models = [], []
     for mode in ("off", "on"):
