@@ -1118,7 +1118,6 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
 // whole workgroup each, the segment's 16-entry chunks over its groups, the partial sums added in
 // LDS. Row terms per group in a fixed row order, summed over the groups in order.
 // Slab row per block: [64 relation dots | 64 sum ga0 | 64 sum gy | 64 sum gy xhat]
-constexpr int kPfMax = 10;                 // prefetch list entries (4 W_t + 4 b_t + W_0 + table)
 struct GathArgs {
     const int32_t* sizes; int hop;
     const int32_t* cptr; const int32_t* cent; const int32_t* clong; const float* gh;
@@ -1131,22 +1130,13 @@ struct GathArgs {
     // backward and adds its row terms to hub_terms [3][64] (all exact 2^-40 integers; hub_acc /
     // hub_ticket zeroed by that group, hub_terms by finalize); hub_terms[192]: the overflow flag
     unsigned long long* hub_acc; int32_t* hub_ticket; unsigned long long* hub_terms;
-    // L2 prefetch of what bwd0 reads first (its W_t / b_t / W_0): pf_blocks extra workgroups
-    // after the gather's, one per XCD (blocks are dealt round-robin), each loading every list
-    const float4* pf[kPfMax]; int pf_n[kPfMax]; int pf_blocks;
 };
 
 // 512 threads (32 row groups) per block: a hub piece's entries over 32 groups (a 439-entry row:
 // 14 per group instead of 28); 256 blocks keep the 8192 groups of the short rows
 constexpr int kGathT = 512, kGathG = kGathT / 16;
 static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 256);
-static bool gath_prefetch() {             // REGNN_NSM_PREFETCH=0: no L2 prefetch blocks (A/B)
-    static const bool on = [] {
-        const char* v = getenv("REGNN_NSM_PREFETCH");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
+
 constexpr int kGathW = 4 * F;
 constexpr int kShort = 16;                 // = re_ns.hip kCscShort
 
@@ -1278,23 +1268,7 @@ __global__ void __launch_bounds__(kGathT) gather_kernel(GathArgs A) {
     __shared__ int s_last;
     PH(2, 8);
     PE(2, 0);
-    const int nblk = int(gridDim.x) - A.pf_blocks;   // the gather's own blocks
-    if (int(blockIdx.x) >= nblk) {             // an L2 prefetch block (block-uniform)
-        float acc = 0.f;
-#pragma unroll
-        for (int e = 0; e < kPfMax; ++e) {
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = int(threadIdx.x) + u * kGathT;
-                v[u] = i < A.pf_n[e] ? A.pf[e][i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc += v[u].x;
-        }
-        if (acc == -1.2345e38f) A.slab[0] = acc;   // never: keeps the loads
-        return;
-    }
+    const int nblk = int(gridDim.x);
     const int n_piece = A.clong[REGNN_CSC_LONG_NPIECE];
     if (threadIdx.x < F) {
         bins[threadIdx.x] = 0ull;
@@ -1630,16 +1604,12 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         for (int a = 0; a < KB; ++a) {
             const int kb = KB * w + a;
             f32x4 zc = {0.f, 0.f, 0.f, 0.f};
-#ifndef REGNN_BWD0_NOZ_PROBE
 #pragma unroll
             for (int b = 0; b < F / 16; ++b) {
                 const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
                 const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
                 MFMA4(av, bw.x, bw.y, bw.z, bw.w, zc);
             }
-#else
-            zc[0] = gs2[c * G2 + 4 * q];
-#endif
             // zc[r] = Z[row 4 q + r][k = 16 kb + c]
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -2223,21 +2193,7 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         G.rw = p->conv_rw[1]; G.n_rel = p->n_rel[1]; G.alpha = p->alpha;
         G.g0 = w->ga[0]; G.slab = w->slab + S.gath;
         G.hub_acc = w->hub_acc; G.hub_ticket = w->hub_ticket; G.hub_terms = w->hub_terms;
-        if (second && gath_prefetch()) {       // bwd0's first reads, into every XCD's L2
-            int e = 0;
-            auto add = [&](const float* ptr, int64_t floats) {
-                if (ptr && e < kPfMax && floats % 4 == 0 && reinterpret_cast<uintptr_t>(ptr) % 16 == 0 &&
-                    floats / 4 <= 4 * kGathT) {
-                    G.pf[e] = reinterpret_cast<const float4*>(ptr);
-                    G.pf_n[e++] = int(floats / 4);
-                }
-            };
-            for (int t = 0; t < T; ++t) add(lin_w.p[t], int64_t(F) * K);
-            for (int t = 0; t < T; ++t) add(lin_b.p[t], F);
-            add(p->conv_w[0], int64_t(F) * F);
-            G.pf_blocks = 8;
-        }
-        hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks + G.pf_blocks), dim3(kGathT), 0, stream, G);
+        hipLaunchKernelGGL(gather_kernel, dim3(kGathBlocks), dim3(kGathT), 0, stream, G);
         REGNN_LAUNCH_CHECK();
         if (split) {
             JobList J;

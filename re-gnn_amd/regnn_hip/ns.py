@@ -172,13 +172,14 @@ class DeviceSampler:
                L.ptr(self.state), L.ptr(self.n_id), L.ptr(self.sizes),
                None if self.stamp_src is None else L.ptr(self.stamp_src), L.stream())
 
-    def run_hops(self, meta_only=True, strided=None, csc_stream=None):
+    def run_hops(self, meta_only=True, strided=None, csc_stream=None, before_sums=None):
         """every hop of the current batch; meta_only=False runs hops marked meta_only in full
         (a consumer that reads n_id / the local source ids, e.g. the module path); strided=False
         writes the CSR blocks whatever self.strided says (None: self.strided). csc_stream
         (strided): a strided hop's transposed index (and its sampled blk_idx) is built on that
         stream, forked after the hop's de-duplication, while the next hop samples on this one;
-        the caller joins it."""
+        the caller joins it. before_sums: called right before the outer hop's sums launch
+        (regnn_ns_hop_typed_sums), e.g. to make it wait on an event."""
         strided = self.strided if strided is None else bool(strided)
         rg = self.rg
         deferred = -1
@@ -187,6 +188,8 @@ class DeviceSampler:
             fork = (csc_stream is not None and strided and self.csc[h] is not None and
                     self.edge_meta[h] is None)
             if self._sums_path(h, strided, meta_only):
+                if before_sums is not None:
+                    before_sums()
                 ts = self.typed_sums[h]
                 et, eo = self.edge_meta[h]
                 L.call("regnn_ns_hop_typed_sums", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
@@ -459,6 +462,10 @@ CSC_FUSE = {"mode": os.environ.get("REGNN_NS_CSC_FUSE", "off")}
 # mag-10x, hidden 64: 134.7 (G=1) / 129.1 (G=4) / 128.1 (G=8) us per step; 16 slots hold
 # 0.9 GiB more HBM than 2.
 AHEAD = {"steps": int(os.environ.get("REGNN_NS_AHEAD", "8"))}
+# "on" (default): inside a lookahead group, the sampler's outer-hop sums launch for the group's
+# batch i waits for the end of model step i - 1 (a model -> sampler edge only: the model never
+# waits), placing it beside step i's agg0 / head; "off": the sampler runs free
+SUMS_ALIGN = {"mode": os.environ.get("REGNN_NS_SUMS_ALIGN", "on")}
 # "on": the module path's last hop runs meta-only when the model's layer 0 is the typed first
 # layer (mag.REGNN.typed_first_layer_ok); "off": the full hop (A/B, tests)
 MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
@@ -941,7 +948,7 @@ class NSTrainer:
         return self.slots[self._trained]
 
     # -- one step --------------------------------------------------------------------------------
-    def _sample(self, slot):
+    def _sample(self, slot, before_sums=None):
         n = len(self.slots)
         s = self.slots[slot]
         s.batch_from_perm(self.perm, self.rank + slot * self.world, n * self.world)
@@ -950,7 +957,7 @@ class NSTrainer:
             # samples (CSC_FORK), joined back right after: the next batch's sampling writes the
             # dedup tables (g2l) every slot shares, which the index reads
             csc = getattr(self, "_csc", None)
-            s.run_hops(csc_stream=csc)
+            s.run_hops(csc_stream=csc, before_sums=before_sums)
             if csc is not None:
                 torch.cuda.current_stream(self.device).wait_stream(csc)
         else:                                 # the module path reads the CSR blocks
@@ -993,14 +1000,24 @@ class NSTrainer:
         G, n = self.ahead, len(self.slots)
         self._side.wait_stream(cs)
         # the model's launches first (captured first: the graph runs them on the launch queue)
+        align = SUMS_ALIGN["mode"] != "off"
+        ends = []
         for i in range(m):
             self._fs_step(self.fused_slots[(start + i) % n])
             if in_graph:
                 self._exchange()
             self._opt_step()
+            if align and i + 1 < m:
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                ends.append(ev)
         with torch.cuda.stream(self._side):
             for i in range(m):
-                self._sample((start + G + i) % n)
+                # batch i's outer-hop sums (the sampler's one heavy launch) wait for the end of
+                # model step i - 1, so they run beside step i's agg0 / head (which they slow
+                # little) instead of its gather / bwd0 / finalize (2-4x slower beside them)
+                wait = (lambda e=ends[i - 1]: self._side.wait_event(e)) if align and i else None
+                self._sample((start + G + i) % n, before_sums=wait)
         cs.wait_stream(self._side)
 
     def _group_sizes(self):
