@@ -42,7 +42,13 @@ inline int env_blocks(const char* name, int dflt) {
     const int v = e ? atoi(e) : 0;
     return v >= 16 && v <= 4096 ? v : dflt;
 }
-static const int kBwdBlocks = env_blocks("REGNN_NSM_BWD_BLOCKS", 128);
+static const int kBwdBlocks = env_blocks("REGNN_NSM_BWD_BLOCKS", 128);   // wave groups per type
+// bwd0's wave groups per block (REGNN_NSM_BWD_GROUPS, 1 or 2): two groups in half the blocks
+// (one 512-thread block per CU) share the W_t image and sum their partials in LDS
+static const int kBwdGroups = [] {
+    const char* e = getenv("REGNN_NSM_BWD_GROUPS");
+    return e && e[0] == '1' ? 1 : 2;
+}();
 constexpr int kMaxCT = 27;                 // class tiles of 16 (the head's LDS holds C <= 384)
 constexpr float kFixScale = 1099511627776.0f;      // 2^40: fixed point of layer 1's scatter
 constexpr float kFixInv = 9.094947017729282e-13f;  // 2^-40
@@ -1419,33 +1425,47 @@ struct Bwd0Args {
 
 constexpr int kPost0W = F * F;
 
+// a wave group's LDS (tile buffers, row meta, relation bins)
 template <int K, bool RS>
+constexpr size_t bwd0_group_floats(int n_rel) {
+    return size_t(16) * (K + 4) * (RS ? 2 : 1) + 16 * (F + 16) + 16 * (F + 4) + 2 * 16 * 68 +
+           16 * 4 + 16 * 2 + 4 * 16 * 2 + size_t(n_rel) * 16;
+}
+template <int K, bool RS, int NG>
 constexpr size_t bwd0_lds_floats(int n_rel) {
-    return size_t(K) * (F + 4) + F + 16 * (K + 4) * (RS ? 2 : 1) + 16 * (F + 16) + 16 * (F + 4) +
-           2 * 16 * 68 + F + 16 * 4 + 16 * 2 + 4 * 16 * 2 + size_t(n_rel) * 16;
+    return size_t(K) * (F + 4) + 2 * F + NG * bwd0_group_floats<K, RS>(n_rel);
 }
 
-template <int K, bool RS>
-__global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
+// NG wave groups of 4 waves per block: group g takes tiles NG b + g, NG (b + grid) + g, ..; the
+// groups' W_t image is shared and their partials meet in LDS (group 0 + group 1, fixed order)
+// before one slab row per block: NG = 2 with half the blocks keeps the waves per CU and halves
+// the split-K slab finalize reads.
+template <int K, bool RS, int NG>
+__global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
+    static_assert(NG == 1 || NG == 2, "one or two wave groups");
     constexpr int XS = K + 4, GS = F + 16, G2 = F + 4, WS = F + 4;
     constexpr int KB = K / 64;                // k blocks per wave
     constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile of a K-wide row
     extern __shared__ float sm[];
     PH(2, 12);
     PE(3, 0);
-    float* Wk = sm;                           // [K][WS]: W_t k-major; at the end the row terms
+    float* Wk = sm;                           // [K][WS]: W_t k-major; after the loop: group 1's
+                                              // W_t partial on its way to group 0
     // the fused Adam's step count advances here, the launch before finalize, which reads it:
     // no completion ticket among finalize's blocks (their contended atomic was its tail)
     if (A.adam_step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) A.adam_step[0] += 1;
     float* bc = Wk + K * WS;                  // [F] b_t
-    float* ush = bc + F;                      // [16][XS] U_t (RS) or S_t
+    float* tabl = bc + F;                     // [F]
+    const int grp = NG == 1 ? 0 : int(threadIdx.x) / kBlock;
+    const int tid = int(threadIdx.x) - grp * kBlock;
+    float* gbase = tabl + F + grp * bwd0_group_floats<K, RS>(A.n_rel);
+    float* ush = gbase;                       // [16][XS] U_t (RS) or S_t
     float* xsh = ush + 16 * XS;               // [16][XS] x_self (RS only)
     float* gsh = xsh + (RS ? 16 * XS : 0);    // [16][GS] gP
     float* gs2 = gsh + 16 * GS;               // [16][G2] gP
     float* g0s = gs2 + 16 * G2;               // [16][68] G0
     float* psh = g0s + 16 * 68;               // [16][68] P (t = 0)
-    float* tabl = psh + 16 * 68;              // [F]
-    float* rm = tabl + F;                     // [16][4]: wr, ws, cnt, beta
+    float* rm = psh + 16 * 68;                // [16][4]: wr, ws, cnt, beta
     int* rr = reinterpret_cast<int*>(rm + 64);  // [16][2]: r_vt (or -1), r_self (or -1)
     float* dred = reinterpret_cast<float*>(rr + 32);   // [4 waves][16][2]
     float* bins = dred + 128;                 // [n_rel][16]
@@ -1455,7 +1475,7 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     // W_t[j][k] -> Wk[k][j]: lane-consecutive j (conflict-free LDS writes), a float4 of row j
     // per element group, every load of the thread in flight at once
 #pragma unroll
-    for (int e = threadIdx.x; e < K / 4 * F; e += kBlock) {
+    for (int e = threadIdx.x; e < K / 4 * F; e += kBlock * NG) {
         const int j = e & (F - 1), k4 = e >> 6;
         const float4 v = *reinterpret_cast<const float4*>(wt + j * K + 4 * k4);
         Wk[(4 * k4 + 0) * WS + j] = v.x;
@@ -1468,10 +1488,10 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         tabl[threadIdx.x] = rel_tab(A.rw, A.n_rel, A.alpha, threadIdx.x);
     }
     if constexpr (RS)
-        for (int i = threadIdx.x; i < A.n_rel * 16; i += kBlock) bins[i] = 0.f;
+        for (int i = tid; i < A.n_rel * 16; i += kBlock) bins[i] = 0.f;
     const int n = A.sizes[A.hop];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-    const int gr = threadIdx.x >> 4, gj = threadIdx.x & 15;
+    const int w = tid >> 6, lane = tid & 63, c = lane & 15, q = lane >> 4;
+    const int gr = tid >> 4, gj = tid & 15;
     float4 w0r[4];                            // W_0[16 w + c][16 b + 4 q ..]: gP's B operand
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -1492,7 +1512,7 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
     auto load = [&](int v0) {
 #pragma unroll
         for (int u = 0; u < XV; ++u) {
-            const int e = threadIdx.x + kBlock * u;
+            const int e = tid + kBlock * u;
             const int r = e / (K / 4), k4 = e - r * (K / 4);
             const bool ok = v0 + r < n;
             ur[u] = ok ? *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
@@ -1508,8 +1528,8 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         if (t0)
             p4 = okv ? *reinterpret_cast<const float4*>(A.p + int64_t(v) * F + 4 * gj)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (threadIdx.x < 16) {
-            const int vv = v0 + threadIdx.x;
+        if (tid < 16) {
+            const int vv = v0 + tid;
             const bool ok = vv < n;
             cntv = ok ? A.s_w[int64_t(vv) * T + t] : 0.f;
             if constexpr (RS) {
@@ -1518,39 +1538,44 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
             }
         }
     };
-    int tile = blockIdx.x;
+    const int stride = int(gridDim.x) * NG;   // tiles per round of the grid
     PH(2, 0);
-    if (tile * 16 < n) load(tile * 16);
+    if ((int(blockIdx.x) * NG + grp) * 16 < n) load((int(blockIdx.x) * NG + grp) * 16);
     __syncthreads();
     PH(2, 1);
-    for (; tile * 16 < n; tile += gridDim.x) {
+    // rounds: block-uniform (every group reaches every barrier); a group past the rows idles
+    for (int base = int(blockIdx.x) * NG; base * 16 < n; base += stride) {
+        const int tile = base + grp;
+        const bool has = tile * 16 < n;       // group-uniform
         const int v0 = tile * 16;
-        *reinterpret_cast<float4*>(g0s + gr * 68 + 4 * gj) = g4;
-        if (t0) *reinterpret_cast<float4*>(psh + gr * 68 + 4 * gj) = p4;
-        if (threadIdx.x < 16) {                // row meta: S = wr U + ws x_self (RS)
-            if constexpr (RS) {
-                const bool self = rsv >= 0 && rsv - A.n_et == t;
-                rm[4 * threadIdx.x] = relv >= 0 ? tabl[relv] : 0.f;
-                rm[4 * threadIdx.x + 1] = self ? tabl[rsv] : 0.f;
-                rr[2 * threadIdx.x] = (relv >= 0 && cntv > 0.f) ? relv : -1;
-                rr[2 * threadIdx.x + 1] = self ? rsv : -1;
-            } else {
-                rm[4 * threadIdx.x] = 1.f;
-                rm[4 * threadIdx.x + 1] = 0.f;
+        if (has) {
+            *reinterpret_cast<float4*>(g0s + gr * 68 + 4 * gj) = g4;
+            if (t0) *reinterpret_cast<float4*>(psh + gr * 68 + 4 * gj) = p4;
+            if (tid < 16) {                    // row meta: S = wr U + ws x_self (RS)
+                if constexpr (RS) {
+                    const bool self = rsv >= 0 && rsv - A.n_et == t;
+                    rm[4 * tid] = relv >= 0 ? tabl[relv] : 0.f;
+                    rm[4 * tid + 1] = self ? tabl[rsv] : 0.f;
+                    rr[2 * tid] = (relv >= 0 && cntv > 0.f) ? relv : -1;
+                    rr[2 * tid + 1] = self ? rsv : -1;
+                } else {
+                    rm[4 * tid] = 1.f;
+                    rm[4 * tid + 1] = 0.f;
+                }
+                rm[4 * tid + 2] = cntv;
             }
-            rm[4 * threadIdx.x + 2] = cntv;
-        }
 #pragma unroll
-        for (int u = 0; u < XV; ++u) {
-            const int e = threadIdx.x + kBlock * u;
-            const int r = e / (K / 4), k4 = e - r * (K / 4);
-            *reinterpret_cast<float4*>(ush + r * XS + 4 * k4) = ur[u];
-            if constexpr (RS) *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[u];
+            for (int u = 0; u < XV; ++u) {
+                const int e = tid + kBlock * u;
+                const int r = e / (K / 4), k4 = e - r * (K / 4);
+                *reinterpret_cast<float4*>(ush + r * XS + 4 * k4) = ur[u];
+                if constexpr (RS) *reinterpret_cast<float4*>(xsh + r * XS + 4 * k4) = xr[u];
+            }
         }
         __syncthreads();
-        if ((tile + gridDim.x) * 16 < n) load((tile + gridDim.x) * 16);
+        if ((tile + stride) * 16 < n) load((tile + stride) * 16);
         // ---- gP = G0 W_0^T -> gsh / gs2; t = 0: W_0 partial D[k][j] = sum_v P[v][k] G0[v][j]
-        {
+        if (has) {
             f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -1574,82 +1599,84 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
             }
         }
         __syncthreads();
-        if (threadIdx.x < F) {                 // g b_t = sum_v w_vt gP_v
+        if (has) {
+            if (tid < F) {                     // g b_t = sum_v w_vt gP_v
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float wv = RS ? fmaf(rm[4 * r], rm[4 * r + 2], rm[4 * r + 1]) : rm[4 * r + 2];
-                bsum = fmaf(wv, gsh[r * GS + threadIdx.x], bsum);
+                for (int r = 0; r < 16; ++r) {
+                    const float wv = RS ? fmaf(rm[4 * r], rm[4 * r + 2], rm[4 * r + 1]) : rm[4 * r + 2];
+                    bsum = fmaf(wv, gsh[r * GS + tid], bsum);
+                }
             }
-        }
-        // g W_t partial D[k][j] = sum_v S_vt[k] gP_v[j] over the tile's (re-formed) S rows
+            // g W_t partial D[k][j] = sum_v S_vt[k] gP_v[j] over the tile's (re-formed) S rows
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            const int r = 4 * st + q;
-            const float wr = rm[4 * r], ws = rm[4 * r + 1];
-            float bv[4];
+            for (int st = 0; st < 4; ++st) {
+                const int r = 4 * st + q;
+                const float wr = rm[4 * r], ws = rm[4 * r + 1];
+                float bv[4];
 #pragma unroll
-            for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+                for (int jb = 0; jb < 4; ++jb) bv[jb] = gsh[r * GS + 16 * jb + c];
+#pragma unroll
+                for (int a = 0; a < KB; ++a) {
+                    const int k = 16 * (KB * w + a) + c;
+                    const float av = RS ? fmaf(ws, xsh[r * XS + k], wr * ush[r * XS + k]) : ush[r * XS + k];
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb)
+                        acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
+                }
+            }
+            // Z_t = gP W_t (wave w -> k blocks KB w ..): relation dots (RS) or Z to HBM
+            float pu[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int a = 0; a < KB; ++a) {
-                const int k = 16 * (KB * w + a) + c;
-                const float av = RS ? fmaf(ws, xsh[r * XS + k], wr * ush[r * XS + k]) : ush[r * XS + k];
+                const int kb = KB * w + a;
+                f32x4 zc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int jb = 0; jb < 4; ++jb)
-                    acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
-            }
-        }
-        // Z_t = gP W_t (wave w -> k blocks KB w ..): relation dots (RS) or Z to HBM
-        float pu[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int a = 0; a < KB; ++a) {
-            const int kb = KB * w + a;
-            f32x4 zc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int b = 0; b < F / 16; ++b) {
-                const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
-                const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
-                MFMA4(av, bw.x, bw.y, bw.z, bw.w, zc);
-            }
-            // zc[r] = Z[row 4 q + r][k = 16 kb + c]
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if constexpr (RS) {
-                    pu[r] = fmaf(zc[r], ush[(4 * q + r) * XS + 16 * kb + c], pu[r]);
-                    ps[r] = fmaf(zc[r], xsh[(4 * q + r) * XS + 16 * kb + c], ps[r]);
-                } else {
-                    const int v = v0 + 4 * q + r;
-                    if (v < n) A.z[(int64_t(v) * T + t) * K + 16 * kb + c] = zc[r];
+                for (int b = 0; b < F / 16; ++b) {
+                    const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
+                    const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
+                    MFMA4(av, bw.x, bw.y, bw.z, bw.w, zc);
                 }
-            }
-        }
-        if constexpr (RS) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                pu[r] = group_sum<16>(pu[r]);
-                ps[r] = group_sum<16>(ps[r]);
-            }
-            if (c == 0) {
+                // zc[r] = Z[row 4 q + r][k = 16 kb + c]
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    dred[(w * 16 + 4 * q + r) * 2] = pu[r];
-                    dred[(w * 16 + 4 * q + r) * 2 + 1] = ps[r];
+                    if constexpr (RS) {
+                        pu[r] = fmaf(zc[r], ush[(4 * q + r) * XS + 16 * kb + c], pu[r]);
+                        ps[r] = fmaf(zc[r], xsh[(4 * q + r) * XS + 16 * kb + c], ps[r]);
+                    } else {
+                        const int v = v0 + 4 * q + r;
+                        if (v < n) A.z[(int64_t(v) * T + t) * K + 16 * kb + c] = zc[r];
+                    }
                 }
             }
-        }
-        {                                      // beta_vt = <b_t, gP_v>
-            const float4 g4 = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
-            float bt = bc[4 * gj] * g4.x + bc[4 * gj + 1] * g4.y + bc[4 * gj + 2] * g4.z +
-                       bc[4 * gj + 3] * g4.w;
-            bt = group_sum<16>(bt);
-            if (gj == 0) {
-                if constexpr (RS) rm[4 * gr + 3] = bt;
-                else if (v0 + gr < n) A.beta[int64_t(v0 + gr) * T + t] = bt;
+            if constexpr (RS) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pu[r] = group_sum<16>(pu[r]);
+                    ps[r] = group_sum<16>(ps[r]);
+                }
+                if (c == 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        dred[(w * 16 + 4 * q + r) * 2] = pu[r];
+                        dred[(w * 16 + 4 * q + r) * 2 + 1] = ps[r];
+                    }
+                }
+            }
+            {                                  // beta_vt = <b_t, gP_v>
+                const float4 g4v = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
+                float bt = bc[4 * gj] * g4v.x + bc[4 * gj + 1] * g4v.y + bc[4 * gj + 2] * g4v.z +
+                           bc[4 * gj + 3] * g4v.w;
+                bt = group_sum<16>(bt);
+                if (gj == 0) {
+                    if constexpr (RS) rm[4 * gr + 3] = bt;
+                    else if (v0 + gr < n) A.beta[int64_t(v0 + gr) * T + t] = bt;
+                }
             }
         }
         __syncthreads();
         if constexpr (RS) {
-            if (threadIdx.x < 16) {            // row r's relation dots into its bin column
-                const int r = threadIdx.x;
+            if (has && tid < 16) {             // row r's relation dots into its bin column
+                const int r = tid;
                 const float du = ((dred[(0 * 16 + r) * 2] + dred[(1 * 16 + r) * 2]) +
                                   dred[(2 * 16 + r) * 2]) + dred[(3 * 16 + r) * 2];
                 const float ds = ((dred[(0 * 16 + r) * 2 + 1] + dred[(1 * 16 + r) * 2 + 1]) +
@@ -1662,6 +1689,39 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
         }
     }
     PH(2, 2);
+    if constexpr (NG == 2) {
+        // group 1's partials into LDS (W_t partial over Wk, the rest over its tile buffers),
+        // group 0 adds them to its own: one slab row per block
+        float* xg = tabl + F + bwd0_group_floats<K, RS>(A.n_rel);   // group 1's region
+        float* x0 = xg + 4 * 64 * 16;          // after its W_0 partial: the bias partial
+        __syncthreads();                       // every group done with Wk
+        if (grp == 1) {
+#pragma unroll
+            for (int a = 0; a < KB; ++a)
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    *reinterpret_cast<f32x4*>(Wk + ((w * KB + a) * 4 + jb) * 256 + 4 * lane) = acc[a][jb];
+            if (t0) {
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    *reinterpret_cast<f32x4*>(xg + (w * 4 + jb) * 256 + 4 * lane) = acc0[jb];
+            }
+            if (tid < F) x0[tid] = bsum;
+        }
+        __syncthreads();
+        if (grp == 1) return;                  // (no barrier follows)
+#pragma unroll
+        for (int a = 0; a < KB; ++a)
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+                acc[a][jb] += *reinterpret_cast<const f32x4*>(Wk + ((w * KB + a) * 4 + jb) * 256 + 4 * lane);
+        if (t0) {
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+                acc0[jb] += *reinterpret_cast<const f32x4*>(xg + (w * 4 + jb) * 256 + 4 * lane);
+        }
+        if (tid < F) bsum += x0[tid];
+    }
     // ---- partials: g W_t as [64][K] (lins[t].weight's layout), g b_t
     float* o = A.slab + (int64_t(t) * gridDim.x + blockIdx.x) * int64_t((K + 1) * F);
 #pragma unroll
@@ -1674,14 +1734,22 @@ __global__ void __launch_bounds__(kBlock) bwd0_kernel(Bwd0Args A) {
             // same for agg0's per-type sums measured nothing)
             __builtin_nontemporal_store(v4, reinterpret_cast<f32x4*>(o + int64_t(16 * jb + c) * K + 16 * (KB * w + a) + 4 * q));
         }
-    if (threadIdx.x < F) o[K * F + threadIdx.x] = bsum;
+    if (tid < F) o[K * F + tid] = bsum;
     if constexpr (RS) {
-        if (threadIdx.x < F) {
+        if (tid < F) {
             float sr = 0.f;
-            if (threadIdx.x < A.n_rel)
+            if (tid < A.n_rel) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sr += bins[threadIdx.x * 16 + r];
-            A.rslab[(int64_t(t) * gridDim.x + blockIdx.x) * F + threadIdx.x] = sr;
+                for (int r = 0; r < 16; ++r) sr += bins[tid * 16 + r];
+                if constexpr (NG == 2) {       // group 1's bins, added after group 0's
+                    const float* bins1 = bins + bwd0_group_floats<K, RS>(A.n_rel);
+                    float s1 = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s1 += bins1[tid * 16 + r];
+                    sr += s1;
+                }
+            }
+            A.rslab[(int64_t(t) * gridDim.x + blockIdx.x) * F + tid] = sr;
         }
     }
     if (t0) {
@@ -2203,7 +2271,8 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         }
     }
     if (!second) return REGNN_OK;
-    // 4. layer 0's backward
+    // 4. layer 0's backward (nb0 blocks per type: one slab row each)
+    const int nb0 = kBwdBlocks / kBwdGroups;
     {
         Bwd0Args B{};
         B.sizes = w->sizes; B.hop = 1; B.T = T;
@@ -2213,17 +2282,18 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         B.u_self = w->u_self; B.u_rel = w->u_rel; B.z = w->z; B.beta = w->beta;
         B.slab = w->slab + S.proj; B.rslab = w->slab + S.rel0; B.slab0 = w->slab + S.post0;
         B.adam_step = ad ? ad->step : nullptr;
-        const dim3 grid(kBwdBlocks, T);
-#define BWD0_CASE(KK, RS)                                                                      \
-        if (K == KK && rs == RS) {                                                             \
+        const dim3 grid(nb0, T);
+#define BWD0_CASE(KK, RS, NG)                                                                  \
+        if (K == KK && rs == RS && kBwdGroups == NG) {                                         \
             static size_t done = 0;                                                            \
-            const size_t lds = bwd0_lds_floats<KK, RS>(p->n_rel[0]) * sizeof(float);           \
-            if (!set_lds(reinterpret_cast<const void*>(&bwd0_kernel<KK, RS>), lds, &done))     \
+            const size_t lds = bwd0_lds_floats<KK, RS, NG>(p->n_rel[0]) * sizeof(float);       \
+            if (!set_lds(reinterpret_cast<const void*>(&bwd0_kernel<KK, RS, NG>), lds, &done)) \
                 return REGNN_EUNSUPPORTED;                                                     \
-            hipLaunchKernelGGL((bwd0_kernel<KK, RS>), grid, dim3(kBlock), lds, stream, B);     \
+            hipLaunchKernelGGL((bwd0_kernel<KK, RS, NG>), grid, dim3(kBlock * NG), lds, stream, B); \
             REGNN_LAUNCH_CHECK();                                                              \
         } else
-        BWD0_CASE(128, true) BWD0_CASE(64, true) BWD0_CASE(128, false) BWD0_CASE(64, false)
+        BWD0_CASE(128, true, 2) BWD0_CASE(64, true, 2) BWD0_CASE(128, false, 2) BWD0_CASE(64, false, 2)
+        BWD0_CASE(128, true, 1) BWD0_CASE(64, true, 1) BWD0_CASE(128, false, 1) BWD0_CASE(64, false, 1)
             return REGNN_EUNSUPPORTED;
 #undef BWD0_CASE
     }
@@ -2238,13 +2308,14 @@ int regnn_nsm2_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStrea
         JobList J;
         if (!split) add_early_jobs(J, p, w, S);
         const int64_t pw = int64_t(K + 1) * F;
-        J.add(w->slab + S.rel0, F, S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel, p->conv_rw[0]);
+        J.add(w->slab + S.rel0, F, rs ? T * nb0 : S.rel0_rows, p->n_rel[0], p->g_conv_rw[0], kOpRel,
+              p->conv_rw[0]);
         for (int t = 0; t < T; ++t) {
-            const float* src = w->slab + S.proj + int64_t(t) * kBwdBlocks * pw;
-            J.add(src, pw, kBwdBlocks, K * F, p->g_lin_w[t]);
-            J.add(src + int64_t(K) * F, pw, kBwdBlocks, F, p->g_lin_b[t]);
+            const float* src = w->slab + S.proj + int64_t(t) * nb0 * pw;
+            J.add(src, pw, nb0, K * F, p->g_lin_w[t]);
+            J.add(src + int64_t(K) * F, pw, nb0, F, p->g_lin_b[t]);
         }
-        J.add(w->slab + S.post0, kPost0W, kBwdBlocks, F * F, p->g_conv_w[0]);
+        J.add(w->slab + S.post0, kPost0W, nb0, F * F, p->g_conv_w[0]);
         launch_finalize(J, p, ad, stream);
         REGNN_LAUNCH_CHECK();
     }
