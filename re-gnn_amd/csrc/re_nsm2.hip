@@ -111,24 +111,6 @@ __device__ unsigned long long g_nsm2_gp[64][8];
 #define PG(j, k) do {} while (0)
 #endif
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-// x = x0 + x1 + x2 in bf16 (re_gemm.hip's split): the "bf16x6" products sum x_i y_j, i + j <= 2
-__device__ __forceinline__ void split3(float x, uint16_t& a, uint16_t& b, uint16_t& c) {
-    a = f2bf(x);
-    const float r = x - bf2f(a);
-    b = f2bf(r);
-    c = f2bf(r - bf2f(b));
-}
-// d += A B over one 32-deep k-step from the operands' three bf16 images (small products first)
-__device__ __forceinline__ f32x4 mfma_x6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 d) {
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], d, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], d, 0, 0, 0);
-}
-
 #define MFMA4(av, b0, b1, b2, b3, d)                                 \
     d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).x, (b0), d, 0, 0, 0); \
     d = __builtin_amdgcn_mfma_f32_16x16x4f32((av).y, (b1), d, 0, 0, 0); \
@@ -799,9 +781,6 @@ __device__ __forceinline__ int head_sw(int c, int k) { return c * F + (k ^ ((c &
 // 16 waves: the row phases (16 rows x 16 lanes) run on threads 0..255, the class-tile loops
 // (logits, gh) and the softmax (64 lanes per row) on all 16 waves; out_lin.weight's LDS-DMA
 // staging on waves 4..15 under the aggregation
-#ifndef REGNN_HEAD_SLOTS
-#define REGNN_HEAD_SLOTS 1                 // strided rows: slot loads beside the count's (A/B)
-#endif
 constexpr int kHeadThreads = 1024;
 constexpr int kHeadW = kHeadThreads / 64;  // waves
 constexpr int kHeadSL = kHeadThreads / 16; // softmax lanes per row
@@ -844,36 +823,7 @@ __global__ void __launch_bounds__(kHeadThreads, 1) head_kernel(HeadArgs A) {
     if (rowt) {
         const int vr = blockIdx.x * kRows + sub;
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        if (REGNN_HEAD_SLOTS && vr < n && A.stride > 0 && A.stride <= 32) {
-            // strided block: the row's slots are known without its count, so the slot loads
-            // (clamped to the row's S slots) go out beside the count's, and every slot's h row
-            // is requested (an empty slot's id -1 reads row 0, weighted 0): one dependent round
-            // trip fewer than count -> slots -> rows
-            const int S = A.stride, e0 = vr * S;
-            const int my_u0 = A.idx[e0 + min(l, S - 1)];
-            const int my_r0 = int(A.rel[e0 + min(l, S - 1)]);
-            const int my_u1 = A.idx[e0 + min(l + 16, S - 1)];
-            const int my_r1 = int(A.rel[e0 + min(l + 16, S - 1)]);
-            const int m = A.cnt[vr] + 1;
-            constexpr int UN = 32;
-            float4 x[UN];
-#pragma unroll
-            for (int u = 0; u < UN; ++u) {
-                const int uu = max(__shfl(u < 16 ? my_u0 : my_u1, gl + (u & 15), 64), 0);
-                x[u] = *reinterpret_cast<const float4*>(A.h + int64_t(uu) * F + 4 * l);
-            }
-            const float tr0 = A.rw[min(my_r0, A.n_rel - 1)] * A.alpha;
-            const float tr1 = A.rw[min(my_r1, A.n_rel - 1)] * A.alpha;
-            const float w0 = my_r0 < A.n_rel ? (tr0 > 0.f ? tr0 : 0.01f * tr0) : 0.f;
-            const float w1 = my_r1 < A.n_rel ? (tr1 > 0.f ? tr1 : 0.01f * tr1) : 0.f;
-#pragma unroll
-            for (int u = 0; u < UN; ++u) {
-                const float ws = __shfl(u < 16 ? w0 : w1, gl + (u & 15), 64);
-                const float wt = u < m ? ws : 0.f;
-                s0 = fmaf(wt, x[u].x, s0); s1 = fmaf(wt, x[u].y, s1);
-                s2 = fmaf(wt, x[u].z, s2); s3 = fmaf(wt, x[u].w, s3);
-            }
-        } else if (vr < n) {
+        if (vr < n) {
             int e0, e1;
             row_range(A.ptr, A.cnt, A.stride, vr, e0, e1);
             for (int c0 = e0; c0 < e1; c0 += 32) {
@@ -1476,20 +1426,14 @@ struct Bwd0Args {
 constexpr int kPost0W = F * F;
 
 // a wave group's LDS (tile buffers, row meta, relation bins)
-constexpr int kB0P = F + 8;                // bf16 row pitch of bwd0's split images (144 B)
 template <int K, bool RS>
 constexpr size_t bwd0_group_floats(int n_rel) {
-    return size_t(16) * (K + 4) * (RS ? 2 : 1) + 16 * (F + 16) + 3 * 16 * kB0P / 2 + 2 * 16 * 68 +
+    return size_t(16) * (K + 4) * (RS ? 2 : 1) + 16 * (F + 16) + 16 * (F + 4) + 2 * 16 * 68 +
            16 * 4 + 16 * 2 + 4 * 16 * 2 + size_t(n_rel) * 16;
-}
-template <int K>
-constexpr size_t bwd0_wk_floats() {        // W_t's three bf16 images, later group 1's W_t partial
-    return size_t(3) * K * kB0P / 2 > size_t(K / 64) * 4096 ? size_t(3) * K * kB0P / 2
-                                                              : size_t(K / 64) * 4096;
 }
 template <int K, bool RS, int NG>
 constexpr size_t bwd0_lds_floats(int n_rel) {
-    return bwd0_wk_floats<K>() + 2 * F + NG * bwd0_group_floats<K, RS>(n_rel);
+    return size_t(K) * (F + 4) + 2 * F + NG * bwd0_group_floats<K, RS>(n_rel);
 }
 
 // NG wave groups of 4 waves per block: group g takes tiles NG b + g, NG (b + grid) + g, ..; the
@@ -1499,19 +1443,18 @@ constexpr size_t bwd0_lds_floats(int n_rel) {
 template <int K, bool RS, int NG>
 __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
     static_assert(NG == 1 || NG == 2, "one or two wave groups");
-    constexpr int XS = K + 4, GS = F + 16;
+    constexpr int XS = K + 4, GS = F + 16, G2 = F + 4, WS = F + 4;
     constexpr int KB = K / 64;                // k blocks per wave
     constexpr int XV = K / 4 * 16 / kBlock;   // float4 per thread per 16-row tile of a K-wide row
     extern __shared__ float sm[];
     PH(2, 12);
     PE(3, 0);
-    float* Wk = sm;                           // W_t's bf16 images [3][K][kB0P] (k-major); after
-                                              // the loop: group 1's W_t partial on its way to group 0
-    uint16_t* wkb = reinterpret_cast<uint16_t*>(sm);
+    float* Wk = sm;                           // [K][WS]: W_t k-major; after the loop: group 1's
+                                              // W_t partial on its way to group 0
     // the fused Adam's step count advances here, the launch before finalize, which reads it:
     // no completion ticket among finalize's blocks (their contended atomic was its tail)
     if (A.adam_step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) A.adam_step[0] += 1;
-    float* bc = Wk + bwd0_wk_floats<K>();     // [F] b_t
+    float* bc = Wk + K * WS;                  // [F] b_t
     float* tabl = bc + F;                     // [F]
     const int grp = NG == 1 ? 0 : int(threadIdx.x) / kBlock;
     const int tid = int(threadIdx.x) - grp * kBlock;
@@ -1519,8 +1462,8 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
     float* ush = gbase;                       // [16][XS] U_t (RS) or S_t
     float* xsh = ush + 16 * XS;               // [16][XS] x_self (RS only)
     float* gsh = xsh + (RS ? 16 * XS : 0);    // [16][GS] gP
-    uint16_t* gpb = reinterpret_cast<uint16_t*>(gsh + 16 * GS);   // gP's bf16 images [3][16][kB0P]
-    float* g0s = gsh + 16 * GS + 3 * 16 * kB0P / 2;                 // [16][68] G0
+    float* gs2 = gsh + 16 * GS;               // [16][G2] gP
+    float* g0s = gs2 + 16 * G2;               // [16][68] G0
     float* psh = g0s + 16 * 68;               // [16][68] P (t = 0)
     float* rm = psh + 16 * 68;                // [16][4]: wr, ws, cnt, beta
     int* rr = reinterpret_cast<int*>(rm + 64);  // [16][2]: r_vt (or -1), r_self (or -1)
@@ -1529,25 +1472,16 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
     const int t = blockIdx.y, T = A.T;
     const bool t0 = t == 0;
     const float* wt = pick(A.lin_w.p, t);
-    // W_t[j][k] -> its bf16 images [s][k][j] (Z's B operand, j contiguous): rows j, j + 1 of
-    // a float4 of k per element pair (a packed 32-bit write per k and image), every load of the
-    // thread in flight at once
+    // W_t[j][k] -> Wk[k][j]: lane-consecutive j (conflict-free LDS writes), a float4 of row j
+    // per element group, every load of the thread in flight at once
 #pragma unroll
-    for (int e = threadIdx.x; e < K / 4 * F / 2; e += kBlock * NG) {
-        const int jp = e & (F / 2 - 1), k4 = e / (F / 2), j = 2 * jp;
-        const float4 v0 = *reinterpret_cast<const float4*>(wt + j * K + 4 * k4);
-        const float4 v1 = *reinterpret_cast<const float4*>(wt + (j + 1) * K + 4 * k4);
-        const float x0[4] = {v0.x, v0.y, v0.z, v0.w}, x1[4] = {v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint16_t a0, b0, c0, a1, b1, c1;
-            split3(x0[i], a0, b0, c0);
-            split3(x1[i], a1, b1, c1);
-            uint32_t* d = reinterpret_cast<uint32_t*>(wkb + (4 * k4 + i) * kB0P + j);
-            d[0] = a0 | (uint32_t(a1) << 16);
-            d[K * kB0P / 2] = b0 | (uint32_t(b1) << 16);
-            d[K * kB0P] = c0 | (uint32_t(c1) << 16);
-        }
+    for (int e = threadIdx.x; e < K / 4 * F; e += kBlock * NG) {
+        const int j = e & (F - 1), k4 = e >> 6;
+        const float4 v = *reinterpret_cast<const float4*>(wt + j * K + 4 * k4);
+        Wk[(4 * k4 + 0) * WS + j] = v.x;
+        Wk[(4 * k4 + 1) * WS + j] = v.y;
+        Wk[(4 * k4 + 2) * WS + j] = v.z;
+        Wk[(4 * k4 + 3) * WS + j] = v.w;
     }
     if (threadIdx.x < F) {
         bc[threadIdx.x] = pick(A.lin_b.p, t)[threadIdx.x];
@@ -1651,12 +1585,7 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 gsh[(4 * q + r) * GS + 16 * w + c] = d[r];
-                uint16_t x0, x1, x2;
-                split3(d[r], x0, x1, x2);
-                uint16_t* gp = gpb + (4 * q + r) * kB0P + 16 * w + c;
-                gp[0] = x0;
-                gp[16 * kB0P] = x1;
-                gp[2 * 16 * kB0P] = x2;
+                gs2[(4 * q + r) * G2 + 16 * w + c] = d[r];
             }
             if (t0) {
 #pragma unroll
@@ -1695,26 +1624,17 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
                         acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[jb], acc[a][jb], 0, 0, 0);
                 }
             }
-            // Z_t = gP W_t (wave w -> k blocks KB w ..) on bf16x6 MFMA: relation dots (RS) or Z
-            // to HBM
+            // Z_t = gP W_t (wave w -> k blocks KB w ..): relation dots (RS) or Z to HBM
             float pu[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
-            bf16x8_t ga[F / 32][3];            // gP row c, j = 32 ks + 8 q ..: the A operand
-#pragma unroll
-            for (int ks = 0; ks < F / 32; ++ks)
-#pragma unroll
-                for (int sp = 0; sp < 3; ++sp)
-                    ga[ks][sp] = *reinterpret_cast<const bf16x8_t*>(gpb + (sp * 16 + c) * kB0P + 32 * ks + 8 * q);
 #pragma unroll
             for (int a = 0; a < KB; ++a) {
                 const int kb = KB * w + a;
                 f32x4 zc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < F / 32; ++ks) {
-                    bf16x8_t wb[3];
-#pragma unroll
-                    for (int sp = 0; sp < 3; ++sp)
-                        wb[sp] = *reinterpret_cast<const bf16x8_t*>(wkb + (sp * K + 16 * kb + c) * kB0P + 32 * ks + 8 * q);
-                    zc = mfma_x6(ga[ks], wb, zc);
+                for (int b = 0; b < F / 16; ++b) {
+                    const float4 av = *reinterpret_cast<const float4*>(gs2 + c * G2 + 16 * b + 4 * q);
+                    const float4 bw = *reinterpret_cast<const float4*>(Wk + (16 * kb + c) * WS + 16 * b + 4 * q);
+                    MFMA4(av, bw.x, bw.y, bw.z, bw.w, zc);
                 }
                 // zc[r] = Z[row 4 q + r][k = 16 kb + c]
 #pragma unroll
@@ -1743,7 +1663,7 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
                 }
             }
             {                                  // beta_vt = <b_t, gP_v>
-                const float4 g4v = *reinterpret_cast<const float4*>(gsh + gr * GS + 4 * gj);
+                const float4 g4v = *reinterpret_cast<const float4*>(gs2 + gr * G2 + 4 * gj);
                 float bt = bc[4 * gj] * g4v.x + bc[4 * gj + 1] * g4v.y + bc[4 * gj + 2] * g4v.z +
                            bc[4 * gj + 3] * g4v.w;
                 bt = group_sum<16>(bt);
