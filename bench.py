@@ -666,7 +666,7 @@ def _gather_ceiling(wl, dtype, hbm):
     row = 64 * (2 if dtype == "bf16" else 4)
     c = GATHER_CEILING_GBS[row]
     return {"row_bytes": row, "GB/s": c, "source": "profiles/r02_gather_probe.txt",
-            "frac_hbm_of_ceiling": None if hbm is None else hbm / c}
+            "hbm_over_ceiling": None if hbm is None else hbm / c}
 
 
 def build_ns_infer(args, dev):
@@ -744,7 +744,9 @@ def cpu_baseline(scale=1.0, reps=10, warm=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # default: 160 timed steps for the NS step (20 lookahead groups of 8: a steadier figure than
+    # 2.5 groups), 20 for the full-graph workloads and the full_batch leg
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["ns", "mag", "dblp", "acm", "imdb", "gat", "gatv2",
                                            "ns_infer", "ns_epoch"], default="ns")
@@ -769,10 +771,15 @@ def main():
         sys.exit(self_launch(args.gpus))
 
     rank, world, dev = setup_dist(args.gpus)
+    explicit_steps = args.steps is not None
+    if not explicit_steps:
+        args.steps = 160 if args.workload == "ns" else 20
     if args.workload == "ns":
         result = run_ns(args, dev)
         if world == 1 and not args.no_full_batch:
             # the full-graph REGraphConv step: north_star's SpMM roofline gate, under its own key
+            if not explicit_steps:
+                args.steps = 20
             result["full_batch"] = run_full(args, dev, "mag")
     elif args.workload == "ns_infer":
         result = run_other_ns_infer(args, dev)
