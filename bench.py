@@ -244,6 +244,32 @@ def ns_step_bytes(sz, K, C, L=2, F=64, T=4, rel_slots=False, two_layer=True, ada
     return b
 
 
+def ns_sums_bytes(sz, K, T):
+    """Algorithmic HBM bytes of the sampler's outer-hop sums launch (regnn_ns_hop_typed_sums,
+    hop 1 of the two-layer step; n1 = sizes[1] rows, E1 = sizes[9] slots incl. self loops):
+      per row    n_id + ptr pair 12, scnt + inv 8, and its outputs: T*K*4 sums, 4*T counts,
+                 K*4 self row, 4*(T+1) slot relations
+      per slot   idx 4 + etype 1 + node type 4 + table row 8 read, the raw input row K*4
+                 gathered, and the edge meta 13 (relation 1, source type 4, table row 8) written"""
+    n1, E1 = sz[1], sz[9]
+    return E1 * (4 + 1 + 4 + 8 + 4 * K + 13) + n1 * (12 + 8 + T * 4 * K + 4 * T + 4 * K + 4 * (T + 1))
+
+
+def pmc_traffic_sums():
+    """HBM bytes per sums launch from the same committed PMC summary, or (None, reason)."""
+    from regnn_hip.build import NS_SUMS_SOURCES, kernel_hash
+    path = os.path.join(ROOT, "profiles", "pmc_ns_fp32.json")
+    if not os.path.exists(path):
+        return None, "no PMC summary committed"
+    with open(path) as f:
+        rec = json.load(f)
+    if "ns_sums" not in rec:
+        return None, "PMC summary has no sums record"
+    if rec.get("sums_code_hash") != kernel_hash(NS_SUMS_SOURCES):
+        return None, "PMC summary is for other kernel code (stale: re-run tools/gpu_pmc_ns.sh)"
+    return rec["ns_sums"]["bytes_per_launch"], "ok"
+
+
 def run_ns(args, dev):
     from regnn_hip import profile
     from regnn_hip.guard import Guard
@@ -363,6 +389,23 @@ def run_ns(args, dev):
                            "profiled_launches": launches, "algorithmic_bytes_per_launch": b,
                            "note": "algorithmic bytes: bench.ns_step_bytes (DESIGN.md §4b); the "
                                    "step is latency-bound (dependent phases), not byte-bound"}
+    if "ns_typed_sums" in kstats and tr.fused is not None:
+        # the sampler's one heavy launch (layer 0's input gather, G steps ahead on the second
+        # stream): its own roofline, bytes at the mean of every sampled slot's sizes
+        launches, mean_ms, _, _ = kstats["ns_typed_sums"]
+        b = statistics.mean(ns_sums_bytes(sl.sizes.cpu().tolist(), 128, tr.fused.P.n_types)
+                            for sl in tr.slots)
+        ach = b / (mean_ms / 1e3) / 1e9
+        traffic, pmc_status = pmc_traffic_sums()
+        hbm = None if traffic is None else traffic / (mean_ms / 1e3) / 1e9
+        res["sampler_roofline"] = {
+            "bound": "hbm", "kernel": "regnn_ns_hop_typed_sums (ns_sample_sums_kernel)",
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": traffic, "achieved_hbm": hbm,
+            "frac_hbm": None if hbm is None else hbm / HBM_PEAK_GBS, "pmc": pmc_status,
+            "launch_ms": mean_ms, "profiled_launches": launches, "algorithmic_bytes_per_launch": b,
+            "note": "eager profiled steps: the launch shares the GPU with the model step; "
+                    "algorithmic bytes: bench.ns_sums_bytes (every slot's raw row gathered once)"}
     cand = {k: v for k, v in kstats.items() if k in ("ns_spmm_fwd", "ns_spmm_bwd")}
     if cand:
         dom = max(cand, key=lambda k: cand[k][2])

@@ -62,6 +62,7 @@ def source_hash():
 PMC_SOURCES = ("re_spmm.hip", "re_dense.hip", "regnn_common.h")
 # the fused NS model step's kernels (profiles/pmc_ns_fp32.json)
 NS_PMC_SOURCES = ("re_nsm.hip", "re_nsm2.hip", "re_nsm_common.h", "regnn_common.h")
+NS_SUMS_SOURCES = ("re_ns.hip", "regnn_common.h")             # the sampler's sums launch
 
 
 def kernel_hash(names=PMC_SOURCES):

@@ -192,15 +192,16 @@ class DeviceSampler:
                     before_sums()
                 ts = self.typed_sums[h]
                 et, eo = self.edge_meta[h]
-                L.call("regnn_ns_hop_typed_sums", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
-                       L.ptr(self.etype_csr), L.ptr(self.ntype), self.num_edge_types, k, h,
-                       L.ptr(self.state), L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h],
-                       L.ptr(b["scnt"]), L.ptr(blk.rel), L.ptr(blk.inv), L.ptr(self.local),
-                       L.ptr(et), L.ptr(eo), ts["tables"], ts["T"], ts["K"],
-                       L.ptr(ts["s_agg"]), L.ptr(ts["s_w"]), L.ptr(ts["u_self"]),
-                       L.ptr(ts["u_rel"]),
-                       ctypes.addressof(self._csc_job(h - 1)) if deferred == h - 1 else None,
-                       L.stream())
+                with timed("ns_typed_sums"):
+                    L.call("regnn_ns_hop_typed_sums", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx),
+                           L.ptr(self.etype_csr), L.ptr(self.ntype), self.num_edge_types, k, h,
+                           L.ptr(self.state), L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h],
+                           L.ptr(b["scnt"]), L.ptr(blk.rel), L.ptr(blk.inv), L.ptr(self.local),
+                           L.ptr(et), L.ptr(eo), ts["tables"], ts["T"], ts["K"],
+                           L.ptr(ts["s_agg"]), L.ptr(ts["s_w"]), L.ptr(ts["u_self"]),
+                           L.ptr(ts["u_rel"]),
+                           ctypes.addressof(self._csc_job(h - 1)) if deferred == h - 1 else None,
+                           L.stream())
                 self.meta_fresh[h] = True
                 continue
             # the transposed index of this hop built beside the next hop's sums (one launch)

@@ -51,6 +51,15 @@ def main():
         "steps": fs,
         "per_kernel_bytes": {k: (fk[k] * 1024 * f_scale + wk.get(k, 0.0) * 1024 * w_scale) / fs
                              for k in sorted(fk)}}}
+    # the sampler's outer-hop sums launch (regnn_ns_hop_typed_sums), per dispatch
+    def sums(path, scale_):
+        v = [x for _, n, x in load(path) if "ns_sample_sums_kernel" in n]
+        return (sum(v) * 1024 * scale_ / len(v), len(v)) if v else (None, 0)
+    sf, sn = sums(fd, f_scale)
+    sw, _ = sums(wd, w_scale)
+    if sn:
+        res["ns_sums"] = {"bytes_per_launch": sf + sw, "fetch_bytes_per_launch": sf,
+                          "write_bytes_per_launch": sw, "launches": sn}
     res["calibration"] = {"copy_bytes": true_bytes, "FETCH_SIZE_bytes": cal_f,
                           "WRITE_SIZE_bytes": cal_w}
     res["config"] = {"scale": float(scale), "batch": int(batch), "fanout": [25, 20],
@@ -58,6 +67,8 @@ def main():
     sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/re-gnn_amd")
     from regnn_hip.build import NS_PMC_SOURCES, kernel_hash
     res["code_hash"] = kernel_hash(NS_PMC_SOURCES)
+    from regnn_hip.build import NS_SUMS_SOURCES
+    res["sums_code_hash"] = kernel_hash(NS_SUMS_SOURCES)
     json.dump(res, open(out_json, "w"), indent=1)
     print(json.dumps(res["nsm_step"], indent=1))
 
