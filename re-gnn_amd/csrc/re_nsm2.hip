@@ -428,9 +428,6 @@ constexpr int kAggRows = REGNN_AGG_ROWS;
 #ifndef REGNN_AGG0_EARLY_W
 #define REGNN_AGG0_EARLY_W 1
 #endif
-#ifndef REGNN_AGG0_SKIP_EMPTY
-#define REGNN_AGG0_SKIP_EMPTY 0                // PRE: sums of types with no edges not fetched (A/B)
-#endif
 
 inline size_t agg0w_lds(int T) {          // St [16][T K + 4] | sw [16][MT] | Pt [16][68] |
     return (size_t(16) * (T * 128 + 4) + 16 * MT + 16 * 68 + 16 * F + 16 * F) * sizeof(float);
@@ -513,21 +510,11 @@ __global__ void __launch_bounds__(kAggW, 4) agg0w_kernel(Agg0Args A) {
 #pragma unroll
             for (int tt = 0; tt < NT; ++tt) {
                 if (tt < T) {
+                    racc[tt] = *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l);
                     wsum[tt] = A.s_w[int64_t(v) * T + tt];
                     rel_t[tt] = A.u_rel[int64_t(v) * (T + 1) + tt];
-#if !REGNN_AGG0_SKIP_EMPTY
-                    racc[tt] = *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l);
-#endif
                 }
             }
-#if REGNN_AGG0_SKIP_EMPTY
-            // a type without edges into the row has exact-zero sums: not fetched (~40 % of the
-            // (row, type) pairs at mag)
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt)
-                if (tt < T && wsum[tt] > 0.f)
-                    racc[tt] = *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v) * T + tt) * K + 4 * l);
-#endif
             xself = *reinterpret_cast<const float4*>(A.u_self + int64_t(v) * K + 4 * l);
             r_self = A.u_rel[int64_t(v) * (T + 1) + T];
         }
@@ -1523,28 +1510,16 @@ __global__ void __launch_bounds__(kBlock * NG) bwd0_kernel(Bwd0Args A) {
     float cntv = 0.f;
     int relv = -1, rsv = -1;
     auto load = [&](int v0) {
-        // a row's type-t sums only when it has type-t edges, its self row only in the block of
-        // its own node type (the only one whose S and relation dots read it): the others are
-        // exact zeros, never fetched (the self rows were read T times, 3 of them for nothing)
-        int rc[XV], rself[XV];
-#pragma unroll
-        for (int u = 0; u < XV; ++u) {
-            const int r = (tid + kBlock * u) / (K / 4);
-            const bool ok = v0 + r < n;
-            // (relation slots: s_w holds counts; weighted sums without them may cancel to 0)
-            rc[u] = ok ? (RS ? int(A.s_w[int64_t(v0 + r) * T + t]) : 1) : 0;
-            rself[u] = RS && ok ? A.u_rel[int64_t(v0 + r) * (T + 1) + T] : -1;
-        }
 #pragma unroll
         for (int u = 0; u < XV; ++u) {
             const int e = tid + kBlock * u;
             const int r = e / (K / 4), k4 = e - r * (K / 4);
-            ur[u] = rc[u] > 0 ? *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            const bool ok = v0 + r < n;
+            ur[u] = ok ? *reinterpret_cast<const float4*>(A.s_agg + (int64_t(v0 + r) * T + t) * K + 4 * k4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
             if constexpr (RS)
-                xr[u] = rself[u] >= 0 && rself[u] - A.n_et == t
-                            ? *reinterpret_cast<const float4*>(A.u_self + int64_t(v0 + r) * K + 4 * k4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                xr[u] = ok ? *reinterpret_cast<const float4*>(A.u_self + int64_t(v0 + r) * K + 4 * k4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const int v = v0 + gr;
         const bool okv = v < n;
