@@ -462,7 +462,14 @@ CSC_FUSE = {"mode": os.environ.get("REGNN_NS_CSC_FUSE", "off")}
 # next batch sampled during this step and joined before layer 0's backward. Measured at
 # mag-10x, hidden 64: 134.7 (G=1) / 129.1 (G=4) / 128.1 (G=8) us per step; 16 slots hold
 # 0.9 GiB more HBM than 2.
-AHEAD = {"steps": int(os.environ.get("REGNN_NS_AHEAD", "8"))}
+# Round 5 (one rank, 300-step runs): G = 8 107.4-108.4, 16 106.5-108.3, 32 105.6-106.0 us (a
+# fork / join per group). Default: 32 with one rank; 8 with several (every captured group holds
+# one RCCL all-reduce per step, and that capture was only rehearsed at 8); REGNN_NS_AHEAD wins
+AHEAD = {"steps": int(os.environ["REGNN_NS_AHEAD"]) if "REGNN_NS_AHEAD" in os.environ else None}
+
+
+def default_ahead(world):
+    return AHEAD["steps"] if AHEAD["steps"] is not None else (32 if world == 1 else 8)
 # "on" (default): inside a lookahead group, the sampler's outer-hop sums launch for the group's
 # batch i waits for the end of model step i - 1 (a model -> sampler edge only: the model never
 # waits), placing it beside step i's agg0 / head; "off": the sampler runs free
@@ -862,7 +869,8 @@ class NSTrainer:
         self.pipelined = bool(pipeline) and (self.fused is not None or
                                              (self._blocks_ok and MODULE_PIPELINE["mode"] != "off"))
         # the sampling lookahead (fused engine; the module path samples one batch ahead)
-        self.ahead = max(1, int(AHEAD["steps"])) if self.pipelined and self.fused is not None else 1
+        self.ahead = (max(1, int(default_ahead(self.world))) if self.pipelined and
+                      self.fused is not None else 1)
         if self.pipelined:
             for _ in range(2 * self.ahead - 1):
                 self.slots.append(DeviceSampler(rg, sizes, batch_size,
