@@ -1141,7 +1141,9 @@ struct GathArgs {
 // 512 threads (32 row groups) per block: a hub piece's entries over 32 groups (a 439-entry row:
 // 14 per group instead of 28); 256 blocks keep the 8192 groups of the short rows
 constexpr int kGathT = 512, kGathG = kGathT / 16;
-static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 256);
+// 192 blocks: 104.3-104.9 us per step against 105.7-106.2 at 256, 106.0-106.7 at 160, 106.6-107.0
+// at 128 (round 5, lookahead 32: fewer gather blocks beside the sampler's launches)
+static const int kGathBlocks = env_blocks("REGNN_NSM_GATH_BLOCKS", 192);
 
 constexpr int kGathW = 4 * F;
 constexpr int kShort = 16;                 // = re_ns.hip kCscShort
