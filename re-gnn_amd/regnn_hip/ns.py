@@ -441,7 +441,8 @@ SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
 # "on" (default): the module path (device blocks) samples the next batch on a second stream while
 # the model trains on this one, as the fused step does; "off": in order. At hidden 512, mag-10x:
 # round 3 (hipBLASLt GEMMs) 1.045 off / 1.09 on; round 4 (x6 GEMMs, interleaved pairs) 0.771 /
-# 0.761 off against 0.757 / 0.756 on
+# 0.761 off against 0.757 / 0.756 on; round 5 (three interleaved 300-step pairs) 0.683-0.684
+# off against 0.667-0.673 on
 MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # "on": the pipelined fused engine builds hop 0's transposed index on a third stream while hop 1
 # samples (regnn_ns_hop strided 2 / 3); "off" (default): in the sampler's own chain. Eager runs
