@@ -567,6 +567,17 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
  * state[3] = g, and advances state[2] and the dedup stamp state[4] (by one, or, with stamp_src
  * non-null, to ++*stamp_src: one int64 counter shared by samplers that use the same dedup
  * tables one after another, so their stamps stay increasing). */
+/* The wide NS model's small per-step ops, one launch each (ABI 42):
+ * regnn_ns_labels: y[i] = labels[n_id[i]] for i < sizes[0] (the batch's live targets), else
+ *   `ignore` (nll_loss's ignore_index), i < B -- replaces mag/regnn_ns.py:404's y gather plus the
+ *   mask of a capacity-sized batch;
+ * regnn_rel_tab: out = leaky_relu(alpha rw, slope) (gtab NULL; mag/regnn_layers.py:110-111) or,
+ *   with gtab, its backward out = d rw = gtab alpha (alpha rw > 0 ? 1 : slope), n entries. */
+int regnn_ns_labels(const int32_t* n_id, const int32_t* sizes, const int64_t* labels, int32_t B,
+                    int64_t ignore, int64_t* y, hipStream_t stream);
+int regnn_rel_tab(const float* rw, const float* gtab, int32_t n, float alpha, float slope,
+                  float* out, hipStream_t stream);
+
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
                    int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,
                    int64_t* stamp_src, hipStream_t stream);

@@ -1526,6 +1526,28 @@ ns_csc_hub_sum_kernel(const int32_t* __restrict__ clong, int chunk,
     }
 }
 
+
+// ---- module-path helpers (the wide NS model's small per-step ops in one launch each)
+// y[i] = labels[n_id[i]] for the batch's live targets i < sizes[0], else `ignore`
+// (mag/regnn_ns.py:404: y = data.y[n_id[:batch_size]], nll_loss over the targets)
+__global__ void __launch_bounds__(kBlock)
+ns_labels_kernel(const int32_t* __restrict__ n_id, const int32_t* __restrict__ sizes,
+                 const int64_t* __restrict__ labels, int B, int64_t ignore, int64_t* __restrict__ y) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < B) y[i] = i < sizes[0] ? labels[n_id[i]] : ignore;
+}
+
+// the relation table tab = leaky_relu(alpha rw) (mag/regnn_layers.py:110-111) and its backward
+// grw = gtab * alpha * (alpha rw > 0 ? 1 : slope)
+__global__ void __launch_bounds__(kBlock)
+rel_tab_kernel(const float* __restrict__ rw, const float* __restrict__ gtab, int n, float alpha,
+               float slope, float* __restrict__ out) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float x = alpha * rw[i];
+    out[i] = gtab ? gtab[i] * (x > 0.f ? alpha : slope * alpha) : (x > 0.f ? x : slope * x);
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -1583,6 +1605,26 @@ int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const 
     NSC_CASE(64, 8)
 #undef NSC_CASE
     return REGNN_EUNSUPPORTED;
+}
+
+int regnn_ns_labels(const int32_t* n_id, const int32_t* sizes, const int64_t* labels, int32_t B,
+                    int64_t ignore, int64_t* y, hipStream_t stream) {
+    if (!n_id || !sizes || !labels || !y || B < 0) return REGNN_EINVAL;
+    if (B == 0) return REGNN_OK;
+    hipLaunchKernelGGL(ns_labels_kernel, dim3(unsigned((B + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, n_id, sizes, labels, B, ignore, y);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_rel_tab(const float* rw, const float* gtab, int32_t n, float alpha, float slope,
+                  float* out, hipStream_t stream) {
+    if (!rw || !out || n < 0) return REGNN_EINVAL;
+    if (n == 0) return REGNN_OK;
+    hipLaunchKernelGGL(rel_tab_kernel, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, rw, gtab, n, alpha, slope, out);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,

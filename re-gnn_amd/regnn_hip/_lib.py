@@ -94,6 +94,8 @@ _SIG = {
     "regnn_sample_count": ([P, P, I64, I32, P, P], ctypes.c_int),
     "regnn_sample_fill": ([P, P, P, I64, I32, U64, P, P, P, P], ctypes.c_int),
     "regnn_ns_batch": ([P, I64, I32, I32, I32, P, P, P, P, P], ctypes.c_int),
+    "regnn_ns_labels": ([P, P, P, I32, I64, P, P], ctypes.c_int),
+    "regnn_rel_tab": ([P, P, I32, ctypes.c_float, ctypes.c_float, P, P], ctypes.c_int),
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_ns_hop_typed_sums": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P,

@@ -110,7 +110,7 @@ class REGCNConv(torch.nn.Module):
     def forward_act(self, x_src, x_target, blk, p, state, layer):
         """forward() on a device-sampled block followed by the model's relu and dropout, the
         bias / LayerNorm / relu / dropout as one launch (ops.wide_ln_act)."""
-        tab = F.leaky_relu(self.relation_weight * self.scaling_factor)           # :110-111
+        tab = ops.rel_tab(self.relation_weight, self.scaling_factor)            # :110-111
         agg = ops.ns_spmm(blk, x_src, tab)
         if self.residual:
             agg = agg + x_target
@@ -486,22 +486,22 @@ class REGNN(torch.nn.Module):
         if conv.relation_weight.numel() > 256:
             return None
         T, K = len(tabs), int(tabs[0].shape[1])
-        tab = F.leaky_relu(conv.relation_weight * conv.scaling_factor)          # :110-111
+        tab = ops.rel_tab(conv.relation_weight, conv.scaling_factor)           # :110-111
         # [S | w]: the per-type sums and weight sums as one [n, T K + T] operand, so the
         # projection S W_c + w b_c is one GEMM against [W_c; b_c] (products on regnn_gemm_x6:
         # fp32-accurate bf16x6 MFMA; the small composition b_cat W_0 stays on hipBLASLt)
         Sw = ops.ns_typed_agg(blk, tab, n_id, tabs, node_type, local_node_idx, ext=True)
         lins = [self.lins[str(t)] for t in range(T)]
-        w_cat = torch.cat([lin.weight.t() for lin in lins], 0)                  # [T K, H]
-        b_cat = torch.stack([lin.bias for lin in lins], 0)                      # [T, H]
-        w_c, b_c = ops.mm(w_cat, conv.weight), b_cat @ conv.weight
         n = blk.n_dst
-        wb = [w_c, b_c]
-        if Sw.shape[1] > T * K + T:                 # the zero pad columns of [S | w | 0]
-            wb.append(w_c.new_zeros(Sw.shape[1] - T * K - T, w_c.shape[1]))
+        # [W_c; b_c; 0] = [W_1ᵀ; ..; W_Tᵀ; b_1; ..; b_T; 0] @ W_0: one concatenation and one x6
+        # GEMM (the zero rows of the pad a cached constant), forward and backward
+        pad = Sw.shape[1] - T * K - T
+        zpad = self._zero_rows(pad, conv.weight.shape[0], conv.weight)
+        wb_in = torch.cat([lin.weight.t() for lin in lins] +
+                          [lin.bias.view(1, -1) for lin in lins] + ([zpad] if pad else []), 0)
         # the block is capacity-sized: its rows past the batch's live targets are zeros, and the
         # GEMMs (forward and both backward products) skip them (live: sizes[hop] on the device)
-        agg = ops.mm(Sw, torch.cat(wb, 0), live=getattr(blk, "live_rows", None))
+        agg = ops.mm(Sw, ops.mm(wb_in, conv.weight), live=getattr(blk, "live_rows", None))
         res = None
         if conv.residual:                                                       # :104,131-132
             x_t = self.group_input(x_dict, node_type, local_node_idx, n_id[:n])
@@ -517,8 +517,14 @@ class REGNN(torch.nn.Module):
             out = conv.norm(out)                                                # :134-135
         return out, False
 
+    def _zero_rows(self, rows, cols, like):
+        """a cached [rows, cols] zero block (no fill launch per step)"""
+        z = getattr(self, "_zrows", None)
+        if z is None or z.shape != (rows, cols) or z.device != like.device:
+            z = self._zrows = like.new_zeros(rows, cols)
+        return z
+
     def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
-        ntype = node_type[n_id]
         blk0 = tuple(adjs[0])[0] if adjs else None
         epi = self._wide_epi(blk0) if getattr(blk0, "is_ns_block", False) else None
         r = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx, epi)
@@ -528,7 +534,6 @@ class REGNN(torch.nn.Module):
                                "only the typed first layer (TYPED_AGG) can read it")
         start = 0
         if x is not None:                      # layer 0 done (group_input folded in)
-            ntype = ntype[:tuple(adjs[0])[2][1]]
             if not acted:
                 x = F.relu(x)
                 x = F.dropout(x, p=self.dropout, training=self.training)
@@ -540,7 +545,6 @@ class REGNN(torch.nn.Module):
                 continue
             edge_index, e_id, size = adj
             x_target = x[:size[1]]
-            ntype = ntype[:size[1]]
             blk = edge_index if getattr(edge_index, "is_ns_block", False) else \
                 getattr(adj, "block", None)
             if (blk is not None and getattr(blk, "is_ns_block", False) and epi is not None and
@@ -550,8 +554,13 @@ class REGNN(torch.nn.Module):
                 continue                       # (relu and dropout applied in the epilogue)
             if blk is not None and self.model == 'regcn' and self.self_loop_type == 2:
                 x = self.convs[i]((x, x_target), blk)          # relation ids formed on device
-            elif (self.model == 'regcn' and self.self_loop_type == 2 and
-                  getattr(adj, "counts", None) is not None):
+                x = F.relu(x)
+                x = F.dropout(x, p=self.dropout, training=self.training)
+                continue
+            # the targets' node types (only these paths read them: no gather launch otherwise)
+            ntype = node_type[n_id[:size[1]]]
+            if (self.model == 'regcn' and self.self_loop_type == 2 and
+                    getattr(adj, "counts", None) is not None):
                 x = self.convs[i]((x, x_target), _typed_block(adj, edge_type, ntype, n_id, size,
                                                               self.num_edge_types))
             else:

@@ -1072,9 +1072,9 @@ class NSTrainer:
             n_id = s.n_id.to(torch.int64)
             out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
                              self.local_node_idx)
-            y = self.y_flat[n_id[:B]]
-            valid = torch.arange(B, device=self.device) < s.sizes[0]
-            y = torch.where(valid, y, torch.full_like(y, -100))
+            # the targets' labels, -100 (ignored) past the batch's live rows: one launch
+            from . import ops
+            y = ops.ns_labels(s.n_id, s.sizes, self.y_flat, B)
         else:
             # exact sizes (host sync) and the reference's (edge_index, e_id, size) adjs,
             # outermost hop first (mag/regnn_ns.py:399-403)

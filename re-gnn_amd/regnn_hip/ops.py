@@ -770,6 +770,49 @@ def ns_typed_agg_ok(tables):
         t.is_contiguous() and t.data_ptr() % 16 == 0 for t in tables)
 
 
+class _RelTab(torch.autograd.Function):
+    """tab = leaky_relu(alpha rw, slope) in one launch, its backward in one (regnn_rel_tab)."""
+
+    @staticmethod
+    def forward(ctx, rw, alpha, slope):
+        rw = rw.contiguous()
+        out = torch.empty_like(rw)
+        L.call("regnn_rel_tab", L.ptr(rw), None, rw.numel(), float(alpha), float(slope),
+               L.ptr(out), L.stream())
+        ctx.save_for_backward(rw)
+        ctx.alpha, ctx.slope = alpha, slope
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (rw,) = ctx.saved_tensors
+        g = g.contiguous()
+        out = torch.empty_like(rw)
+        L.call("regnn_rel_tab", L.ptr(rw), L.ptr(g), rw.numel(), float(ctx.alpha),
+               float(ctx.slope), L.ptr(out), L.stream())
+        return out, None, None
+
+
+def rel_tab(rw, alpha, slope=0.01):
+    """leaky_relu(alpha * rw, slope) (mag/regnn_layers.py:110-111): the relation table of an
+    fp32 device relation_weight in one launch instead of a multiply and an activation (and two
+    in the backward)."""
+    if not (rw.is_cuda and rw.dtype == torch.float32):
+        raise ValueError("rel_tab: an fp32 device tensor")
+    return _RelTab.apply(rw, alpha, slope)
+
+
+def ns_labels(n_id, sizes, labels, B, ignore=-100):
+    """y[i] = labels[n_id[i]] for the batch's live targets i < sizes[0], else `ignore`
+    (mag/regnn_ns.py:404 over a capacity-sized batch) in one launch; n_id int32, labels int64."""
+    if n_id.dtype != torch.int32 or labels.dtype != torch.int64 or not n_id.is_cuda:
+        raise ValueError("ns_labels: int32 n_id, int64 labels, device tensors")
+    y = torch.empty(B, dtype=torch.int64, device=n_id.device)
+    L.call("regnn_ns_labels", L.ptr(n_id), L.ptr(sizes), L.ptr(labels.contiguous()), int(B),
+           int(ignore), L.ptr(y), L.stream())
+    return y
+
+
 # ---------------------------------------------------------------------------------------------
 class _EdgeSpmm(torch.autograd.Function):
     """y[v] = sum_{e: u->v} ew[e] * x[u]; ew per edge in the caller's edge order."""

@@ -240,3 +240,30 @@ def test_csc_gather_chunked_hubs_match(monkeypatch):
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
 
+
+
+def test_rel_tab_and_labels_match_torch():
+    """the module path's one-launch helpers against the torch ops they replace: the relation
+    table leaky_relu(alpha rw) (mag/regnn_layers.py:110-111, forward bitwise, backward to 1e-6)
+    and the batch's labels with -100 past the live targets (mag/regnn_ns.py:404)."""
+    import torch.nn.functional as F
+    from regnn_hip import ops
+    g0 = torch.Generator(device=DEV)
+    g0.manual_seed(7)
+    rw = (torch.randn(23, device=DEV, generator=g0) * 0.02).requires_grad_(True)
+    ref_rw = rw.detach().clone().requires_grad_(True)
+    tab = ops.rel_tab(rw, 100.0)
+    ref = F.leaky_relu(ref_rw * 100.0)
+    assert torch.equal(tab, ref)
+    g = torch.randn(23, device=DEV, generator=g0)
+    tab.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(rw.grad, ref_rw.grad, rtol=1e-6, atol=0)
+    n_id = torch.randint(0, 1000, (64,), device=DEV, dtype=torch.int32, generator=g0)
+    labels = torch.randint(0, 349, (1000,), device=DEV, generator=g0)
+    for live in (0, 50, 64):
+        sizes = torch.tensor([live], device=DEV, dtype=torch.int32)
+        y = ops.ns_labels(n_id, sizes, labels, 64)
+        want = torch.where(torch.arange(64, device=DEV) < live, labels[n_id.long()],
+                           torch.full((64,), -100, device=DEV))
+        assert torch.equal(y, want)
