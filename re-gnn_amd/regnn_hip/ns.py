@@ -1066,7 +1066,11 @@ class NSTrainer:
 
     def _module_step(self, s):
         """the mag.REGNN autograd forward / nll / backward on sampler slot s's batch."""
-        self.flat.zero_()                     # (parameters the forward never reads stay zero)
+        # the bucket zeroed once: every step overwrites each gradient the forward produces, and
+        # a parameter the forward never reads (allow_unused) keeps the zeros (no fill per step)
+        if not getattr(self, "_flat_zeroed", False):
+            self.flat.zero_()
+            self._flat_zeroed = True
         if self._blocks_ok:
             B = s.B
             n_id = s.n_id.to(torch.int64)
