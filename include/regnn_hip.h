@@ -575,6 +575,16 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
  *   with gtab, its backward out = d rw = gtab alpha (alpha rw > 0 ? 1 : slope), n entries. */
 int regnn_ns_labels(const int32_t* n_id, const int32_t* sizes, const int64_t* labels, int32_t B,
                     int64_t ignore, int64_t* y, hipStream_t stream);
+/* log_softmax + nll_loss over B rows of C fp32 logits z (row-major), labels y (`ignore` rows
+ * skipped): forward (a wave per row, then a fixed-order sum: deterministic) writes lse[B], the
+ * scratch rowloss[2 B] and out[2] = {mean loss over the valid rows, their count}; backward gz =
+ * g[0] / out[1] * (softmax(z) - onehot(y)), zero rows for ignored labels (ABI 42;
+ * mag/regnn_ns.py:404-405's log_softmax / nll pair). */
+int regnn_softmax_xent_fwd(const float* z, const int64_t* y, int32_t B, int32_t C, int64_t ignore,
+                           float* lse, float* rowloss, float* out, hipStream_t stream);
+int regnn_softmax_xent_bwd(const float* z, const int64_t* y, const float* lse, const float* stat,
+                           const float* g, int32_t B, int32_t C, int64_t ignore, float* gz,
+                           hipStream_t stream);
 int regnn_rel_tab(const float* rw, const float* gtab, int32_t n, float alpha, float slope,
                   float* out, hipStream_t stream);
 

@@ -1548,6 +1548,75 @@ rel_tab_kernel(const float* __restrict__ rw, const float* __restrict__ gtab, int
     out[i] = gtab ? gtab[i] * (x > 0.f ? alpha : slope * alpha) : (x > 0.f ? x : slope * x);
 }
 
+
+// log_softmax + nll_loss (mean over rows whose label != ignore; mag/regnn_ns.py:404-405 over the
+// model's out_lin logits): a wave per row writes lse[r] and the row's loss (0 on an ignored row)
+// and validity; one workgroup then sums them in a fixed order (deterministic) into out = {mean
+// loss, valid count}; backward: gz[r][c] = g / count * (exp(z[r][c] - lse[r]) - [c == y_r]), 0 on
+// ignored rows (a wave per row)
+__global__ void __launch_bounds__(kBlock)
+xent_rows_kernel(const float* __restrict__ z, const int64_t* __restrict__ y, int B, int C,
+                 int64_t ignore, float* __restrict__ lse, float* __restrict__ rowloss) {
+    const int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= B) return;
+    const float* zr = z + int64_t(r) * C;
+    const int64_t yr = y[r];
+    float m = -INFINITY;
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, zr[c]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) se += expf(zr[c] - m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    const float l = m + logf(se);
+    if (lane == 0) {
+        lse[r] = l;
+        rowloss[r] = yr != ignore ? l - zr[yr] : 0.f;
+        rowloss[B + r] = yr != ignore ? 1.f : 0.f;
+    }
+}
+
+constexpr int kXentT = 1024;
+__global__ void __launch_bounds__(kXentT)
+xent_sum_kernel(const float* __restrict__ rowloss, int B, float* __restrict__ out) {
+    __shared__ float ls[kXentT], lc[kXentT];
+    float s = 0.f, n = 0.f;                  // thread t: rows t, t + 1024, .. in order
+    for (int r = threadIdx.x; r < B; r += kXentT) {
+        s += rowloss[r];
+        n += rowloss[B + r];
+    }
+    ls[threadIdx.x] = s;
+    lc[threadIdx.x] = n;
+    __syncthreads();
+    for (int h = kXentT / 2; h > 0; h >>= 1) {   // a fixed-shape tree
+        if (int(threadIdx.x) < h) {
+            ls[threadIdx.x] += ls[threadIdx.x + h];
+            lc[threadIdx.x] += lc[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = ls[0] / lc[0];              // (0 / 0 = nan with no valid row, as nll_loss)
+        out[1] = lc[0];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+xent_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ y,
+                const float* __restrict__ lse, const float* __restrict__ stat,
+                const float* __restrict__ g, int B, int C, int64_t ignore, float* __restrict__ gz) {
+    const int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= B) return;
+    const int64_t yr = y[r];
+    const float scale = yr != ignore ? g[0] / stat[1] : 0.f;
+    const float l = lse[r];
+    const float* zr = z + int64_t(r) * C;
+    float* gr = gz + int64_t(r) * C;
+    for (int c = lane; c < C; c += 64)
+        gr[c] = scale * (expf(zr[c] - l) - (int64_t(c) == yr ? 1.f : 0.f));
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -1605,6 +1674,30 @@ int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const 
     NSC_CASE(64, 8)
 #undef NSC_CASE
     return REGNN_EUNSUPPORTED;
+}
+
+int regnn_softmax_xent_fwd(const float* z, const int64_t* y, int32_t B, int32_t C, int64_t ignore,
+                           float* lse, float* rowloss, float* out, hipStream_t stream) {
+    if (!z || !y || !lse || !rowloss || !out || B < 0 || C <= 0) return REGNN_EINVAL;
+    if (B > 0) {
+        hipLaunchKernelGGL(xent_rows_kernel, dim3(unsigned((B + 3) / 4)), dim3(kBlock), 0, stream,
+                           z, y, B, C, ignore, lse, rowloss);
+        REGNN_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(kXentT), 0, stream, rowloss, B, out);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_softmax_xent_bwd(const float* z, const int64_t* y, const float* lse, const float* stat,
+                           const float* g, int32_t B, int32_t C, int64_t ignore, float* gz,
+                           hipStream_t stream) {
+    if (!z || !y || !lse || !stat || !g || !gz || B < 0 || C <= 0) return REGNN_EINVAL;
+    if (B == 0) return REGNN_OK;
+    hipLaunchKernelGGL(xent_bwd_kernel, dim3(unsigned((B + 3) / 4)), dim3(kBlock), 0, stream, z, y,
+                       lse, stat, g, B, C, ignore, gz);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 int regnn_ns_labels(const int32_t* n_id, const int32_t* sizes, const int64_t* labels, int32_t B,

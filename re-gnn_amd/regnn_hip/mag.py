@@ -524,7 +524,9 @@ class REGNN(torch.nn.Module):
             z = self._zrows = like.new_zeros(rows, cols)
         return z
 
-    def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx):
+    def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx, logits=False):
+        """-> log_softmax of out_lin (mag/regnn_ns.py:346); logits=True: out_lin's raw output
+        (a caller that forms the loss itself, e.g. NSTrainer with ops.softmax_xent)."""
         blk0 = tuple(adjs[0])[0] if adjs else None
         epi = self._wide_epi(blk0) if getattr(blk0, "is_ns_block", False) else None
         r = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx, epi)
@@ -567,7 +569,8 @@ class REGNN(torch.nn.Module):
                 x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
             x = F.relu(x)
             x = F.dropout(x, p=self.dropout, training=self.training)
-        return self.out_lin(x).log_softmax(dim=-1)
+        out = self.out_lin(x)
+        return out if logits else out.log_softmax(dim=-1)
 
     @torch.no_grad()
     def inference(self, x_dict, subgraph_loader, edge_type, node_type, local_node_idx,

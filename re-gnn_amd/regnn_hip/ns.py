@@ -1074,10 +1074,12 @@ class NSTrainer:
         if self._blocks_ok:
             B = s.B
             n_id = s.n_id.to(torch.int64)
+            from . import mag, ops
+            fused_loss = (isinstance(self.model, mag.REGNN) and
+                          os.environ.get("REGNN_NS_FUSED_LOSS", "on") != "off")
             out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
-                             self.local_node_idx)
+                             self.local_node_idx, **({"logits": True} if fused_loss else {}))
             # the targets' labels, -100 (ignored) past the batch's live rows: one launch
-            from . import ops
             y = ops.ns_labels(s.n_id, s.sizes, self.y_flat, B)
         else:
             # exact sizes (host sync) and the reference's (edge_index, e_id, size) adjs,
@@ -1088,7 +1090,11 @@ class NSTrainer:
             out = self.model(n_id, self.x_dict, adjs, self.edge_type, self.node_type,
                              self.local_node_idx)
             y = self.y_flat[n_id[:hops[0][2][1]]]
-        loss = F.nll_loss(out, y)                     # mean over the batch's targets
+            fused_loss = False
+        if fused_loss:                                # log_softmax + nll in one launch each way
+            loss = ops.softmax_xent(out, y)
+        else:
+            loss = F.nll_loss(out, y)                 # mean over the batch's targets
         # the gradients straight into the flat bucket: autograd.grad, then one launch copying
         # every gradient (some of them transposed views) into its bucket view (backward() would
         # accumulate with one add kernel per parameter, and _foreach_copy_ / _foreach_add_

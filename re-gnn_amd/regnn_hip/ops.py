@@ -802,6 +802,40 @@ def rel_tab(rw, alpha, slope=0.01):
     return _RelTab.apply(rw, alpha, slope)
 
 
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, y, ignore):
+        z = z.contiguous().float()
+        y = y.contiguous()
+        B, C = z.shape
+        lse = torch.empty(B, dtype=torch.float32, device=z.device)
+        rowloss = torch.empty(2 * B, dtype=torch.float32, device=z.device)
+        out = torch.empty(2, dtype=torch.float32, device=z.device)
+        L.call("regnn_softmax_xent_fwd", L.ptr(z), L.ptr(y), B, C, int(ignore), L.ptr(lse),
+               L.ptr(rowloss), L.ptr(out), L.stream())
+        ctx.save_for_backward(z, y, lse, out)
+        ctx.ignore = int(ignore)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        z, y, lse, out = ctx.saved_tensors
+        B, C = z.shape
+        gz = torch.empty_like(z)
+        g = g.reshape(1).contiguous().float()
+        L.call("regnn_softmax_xent_bwd", L.ptr(z), L.ptr(y), L.ptr(lse), L.ptr(out), L.ptr(g), B,
+               C, ctx.ignore, L.ptr(gz), L.stream())
+        return gz, None, None
+
+
+def softmax_xent(z, y, ignore=-100):
+    """nll_loss(log_softmax(z), y, ignore_index) (mean over the non-ignored rows) from fp32 logits
+    in one launch forward and one backward (regnn_softmax_xent_*); y int64."""
+    if not (z.is_cuda and z.dim() == 2 and y.dtype == torch.int64):
+        raise ValueError("softmax_xent: [B, C] device logits, int64 labels")
+    return _SoftmaxXent.apply(z, y, ignore)
+
+
 def ns_labels(n_id, sizes, labels, B, ignore=-100):
     """y[i] = labels[n_id[i]] for the batch's live targets i < sizes[0], else `ignore`
     (mag/regnn_ns.py:404 over a capacity-sized batch) in one launch; n_id int32, labels int64."""

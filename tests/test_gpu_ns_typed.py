@@ -267,3 +267,27 @@ def test_rel_tab_and_labels_match_torch():
         want = torch.where(torch.arange(64, device=DEV) < live, labels[n_id.long()],
                            torch.full((64,), -100, device=DEV))
         assert torch.equal(y, want)
+
+
+def test_softmax_xent_matches_torch():
+    """ops.softmax_xent (one launch each way) against log_softmax + nll_loss with ignored rows,
+    loss and logits gradient to 1e-6, and the all-ignored batch (nan, as torch)."""
+    import torch.nn.functional as F
+    from regnn_hip import ops
+    g0 = torch.Generator(device=DEV)
+    g0.manual_seed(3)
+    for B, C in ((512, 349), (37, 5), (1, 64)):
+        z = (torch.randn(B, C, device=DEV, generator=g0) * 3).requires_grad_(True)
+        y = torch.randint(0, C, (B,), device=DEV, generator=g0)
+        y[::7] = -100
+        if B == 1:
+            y[0] = 3
+        zr = z.detach().clone().requires_grad_(True)
+        loss = ops.softmax_xent(z, y)
+        ref = F.nll_loss(zr.log_softmax(-1), y)
+        torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-6)
+        loss.backward()
+        ref.backward()
+        torch.testing.assert_close(z.grad, zr.grad, rtol=1e-5, atol=1e-7)
+    z = torch.randn(4, 6, device=DEV)
+    assert torch.isnan(ops.softmax_xent(z, torch.full((4,), -100, device=DEV)))
