@@ -296,8 +296,12 @@ def run_ns(args, dev):
     kstats = profile.summary()
     profile.enable(False)
     use_graph = args.graph != "off"
+    capture_s = None
     if use_graph:
+        t_cap = time.time()
         guard.stage("capture the step graphs", lambda: tr.capture(warmup=2))
+        capture_s = time.time() - t_cap
+        log(f"[bench] ns: captured the step graphs in {capture_s:.1f}s (lookahead {tr.ahead})")
         run_k = tr.run_steps               # step pairs as one graph replay where they fit
     else:
         def run_k(k):
@@ -363,7 +367,8 @@ def run_ns(args, dev):
             "fanout": [25, 20], "parallelism": f"dp{world}",
             "grad_exchange": exchange,
             "lookahead": tr.ahead,
-            "hip_graph": use_graph, "aggregated_edges_per_step_per_rank": edges / world / args.steps,
+            "hip_graph": use_graph, "lookahead": tr.ahead, "capture_s": capture_s,
+            "aggregated_edges_per_step_per_rank": edges / world / args.steps,
             "final_loss": loss,
         },
         "ns_kernels_ms": {k: round(v[1], 4) for k, v in kstats.items()},
