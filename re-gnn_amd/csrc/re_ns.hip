@@ -1114,140 +1114,6 @@ ns_sample_sums_kernel(NsSumArgs A) {
     }
 }
 
-// The strided hop's de-duplication and transposed index in ONE workgroup (replaces
-// ns_flags_finish + ns_resolve_csc + ns_csc_place for blocks of <= kDedupMaxE slots, the fused
-// step's hop 0: 512 targets x 26 slots). Each thread owns kDedupIT consecutive slots; every
-// global load it needs (sources, their dedup entries, relation ids) is issued up front, and the
-// rest runs in LDS: first-occurrence flags -> block scan -> new local ids (n_id, g2l) -> every
-// slot's local id (a target's from g2l, a new source's from its first occurrence's slot) ->
-// per-source counts and entry ranks (LDS atomics) -> the counts' scan (csc_ptr, the hub list and
-// its piece table) -> every entry placed. Two global round trips and one CU, instead of three
-// launches that each waited on several (and held the GPU beside the model meanwhile).
-constexpr int kDedupT = 1024;
-constexpr int kDedupIT = 13;               // slots per thread (registers: every load in flight)
-constexpr int kDedupMaxE = kDedupT * kDedupIT;   // 13312 = 512 targets x 26 slots
-
-__global__ void __launch_bounds__(kDedupT)
-ns_dedup_csc_block_kernel(const int32_t* __restrict__ gsrc, int32_t* __restrict__ sizes, int hop,
-                          const int64_t* __restrict__ state, uint64_t* __restrict__ g2l,
-                          const uint64_t* __restrict__ first, int32_t* __restrict__ n_id,
-                          int32_t* __restrict__ blk_idx, const uint8_t* __restrict__ blk_rel,
-                          int S, int cap_e, int32_t* __restrict__ csc_ptr,
-                          int32_t* __restrict__ csc_ent, int32_t* __restrict__ csc_long) {
-    __shared__ int slot_lid[kDedupMaxE];   // a flagged slot's new local id
-    __shared__ int cnt[kDedupMaxE];        // per local source: entry count, then segment start
-    __shared__ int lds[kDedupT / 64 + 1];
-    const uint32_t stamp = ns_stamp(state, hop);
-    const int n = sizes[hop];
-    const int b0 = threadIdx.x * kDedupIT;
-    int u[kDedupIT];
-#pragma unroll
-    for (int j = 0; j < kDedupIT; ++j) u[j] = b0 + j < cap_e ? gsrc[b0 + j] : -2;
-    // key: a target's local id | 1 << 30, else its first occurrence's slot (flag: that slot is
-    // this one); both dedup words of every slot requested at once
-    int key[kDedupIT], c = 0;
-    uint32_t fmask = 0;
-    {
-        uint64_t gl[kDedupIT], fs[kDedupIT];
-#pragma unroll
-        for (int j = 0; j < kDedupIT; ++j) {
-            gl[j] = u[j] >= 0 ? g2l[u[j]] : 0ull;
-            fs[j] = u[j] >= 0 ? first[u[j]] : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < kDedupIT; ++j) {
-            const bool tgt = u[j] >= 0 && uint32_t(gl[j] >> 32) == stamp;
-            const bool f = u[j] >= 0 && !tgt && fs[j] == first_key(stamp, b0 + j);
-            key[j] = tgt ? (int(uint32_t(gl[j])) | (1 << 30)) : int(uint32_t(fs[j]));
-            fmask |= f ? 1u << j : 0u;
-            c += f ? 1 : 0;
-        }
-    }
-    for (int i = threadIdx.x; i < kDedupMaxE; i += kDedupT) cnt[i] = 0;
-    // ---- first occurrences of non-target sources: new local ids in slot order
-    int total;
-    int loc = n + block_exscan<kDedupT>(c, lds, &total);
-#pragma unroll
-    for (int j = 0; j < kDedupIT; ++j) {
-        if (fmask >> j & 1u) {
-            n_id[loc] = u[j];
-            g2l[u[j]] = (uint64_t(stamp) << 32) | uint32_t(loc);
-            slot_lid[b0 + j] = loc;
-            ++loc;
-        }
-    }
-    const int n1 = n + total;
-    if (threadIdx.x == 0) sizes[hop + 1] = n1;
-    __syncthreads();
-    // ---- every slot's local source id and its rank in that source's segment, packed as
-    // lid << 16 | rank (both < 2^15), -1 for an empty slot
-    int lr[kDedupIT];
-#pragma unroll
-    for (int j = 0; j < kDedupIT; ++j) {
-        const int bp = b0 + j;
-        int lid = -1;
-        if (u[j] == -1) {
-            lid = bp / S;                      // the self loop: the row itself
-        } else if (u[j] >= 0) {
-            lid = (key[j] >> 30) ? (key[j] & ((1 << 30) - 1)) : slot_lid[key[j]];
-            blk_idx[bp] = lid;
-        }
-        lr[j] = lid >= 0 ? (lid << 16) | atomicAdd(&cnt[lid], 1) : -1;
-    }
-    __syncthreads();
-    // ---- the counts' scan over the n1 sources: csc_ptr, the hub list, the piece table
-    {
-        int4* pieces = reinterpret_cast<int4*>(csc_long + REGNN_CSC_LONG_TAB);
-        int carry = 0, lcarry = 0, pcarry = 0;
-        for (int base = 0; base < n1; base += kDedupT * kDedupIT) {
-            const int i0 = base + threadIdx.x * kDedupIT;
-            int v[kDedupIT], sm = 0, nl = 0, np = 0;
-#pragma unroll
-            for (int j = 0; j < kDedupIT; ++j) {
-                v[j] = i0 + j < n1 ? cnt[i0 + j] : 0;
-                sm += v[j];
-                nl += v[j] > kCscShort ? 1 : 0;
-                np += v[j] > kCscShort ? (v[j] + kCscPiece - 1) / kCscPiece : 0;
-            }
-            int t0, t1, t2;
-            int off = carry + block_exscan<kDedupT>(sm, lds, &t0);
-            int loff = lcarry + block_exscan<kDedupT>(nl, lds, &t1);
-            int poff = pcarry + block_exscan<kDedupT>(np, lds, &t2);
-#pragma unroll
-            for (int j = 0; j < kDedupIT; ++j) {
-                if (i0 + j < n1) {
-                    csc_ptr[i0 + j] = off;
-                    cnt[i0 + j] = off;         // (this thread's own entries: read above)
-                    if (v[j] > kCscShort) {
-                        const int li = loff++;
-                        csc_long[1 + li] = i0 + j;
-                        const int npc = (v[j] + kCscPiece - 1) / kCscPiece;
-                        for (int k = 0; k < npc; ++k, ++poff)
-                            pieces[poff] = make_int4(i0 + j, off + k * kCscPiece,
-                                                     min(kCscPiece, v[j] - k * kCscPiece),
-                                                     (li << 16) | (k << 8) | npc);
-                    }
-                }
-                off += v[j];
-            }
-            carry += t0;
-            lcarry += t1;
-            pcarry += t2;
-        }
-        if (threadIdx.x == 0) {
-            csc_ptr[n1] = carry;
-            csc_long[0] = lcarry;
-            csc_long[REGNN_CSC_LONG_NPIECE] = pcarry;
-        }
-    }
-    __syncthreads();
-    // ---- every entry (target row << 8 | relation) at its segment start + rank
-#pragma unroll
-    for (int j = 0; j < kDedupIT; ++j)
-        if (lr[j] >= 0)
-            csc_ent[cnt[lr[j] >> 16] + (lr[j] & 0xFFFF)] = (((b0 + j) / S) << 8) | int(blk_rel[b0 + j]);
-}
-
 // Backward of the sampled block's mean aggregation y[v] = s[v] sum_e tab[rel_e] x[idx_e] + b
 // (mag/regnn_layers.py:129,142-148 through torch_scatter's mean): per target row v the scaled
 // gradient s[v] g[v] is scattered to the gathered rows with hardware float atomics (the block's
@@ -1629,13 +1495,6 @@ static bool ns_half_waves() {
     return v && v[0] == '1';
 }
 
-// REGNN_NS_DEDUP_ONE=1: the strided hop's de-duplication + transposed index in one workgroup
-// (measured 60 us on the sampler stream against ~30 us for the multi-block kernels, and the step
-// 112.6-113.4 against 106.8 us; kept off, read per launch)
-static bool ns_dedup_one() {
-    const char* v = getenv("REGNN_NS_DEDUP_ONE");
-    return v && v[0] == '1';
-}
 
 extern "C" {
 
@@ -1788,14 +1647,6 @@ int regnn_ns_hop(const int32_t* ptr, const int32_t* idx, const uint8_t* etype,
         REGNN_LAUNCH_CHECK();
         if (lean) return REGNN_OK;
         const int ce = int(cap_e);
-        if (csc && !edge_type && strided != 2 && cap_e <= kDedupMaxE && ns_dedup_one()) {
-            // de-duplication and the transposed index in one workgroup
-            hipLaunchKernelGGL(ns_dedup_csc_block_kernel, dim3(1), dim3(kDedupT), 0, stream, gsrc,
-                               sizes, hop, state, g2l, first, n_id, blk_idx, blk_rel, k + 1, ce,
-                               csc_ptr, csc_ent, csc_long);
-            REGNN_LAUNCH_CHECK();
-            return REGNN_OK;
-        }
         // de-duplication in one pass (status: >= n_tiles entries on this path)
         hipLaunchKernelGGL(ns_flags_finish_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, gsrc,
                            sizes, hop, state, g2l, first, status, n_id, ce);

@@ -749,9 +749,8 @@ def test_block_transposed_index():
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
 
 
-@pytest.mark.parametrize("half_waves,dedup_one,csc_fuse",
-                         [("0", "0", "on"), ("1", "0", "on"), ("0", "0", "off"), ("0", "1", "off")])
-def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one, csc_fuse):
+@pytest.mark.parametrize("half_waves,csc_fuse", [("0", "on"), ("1", "on"), ("0", "off")])
+def test_strided_blocks_match_csr(monkeypatch, half_waves, csc_fuse):
     """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
     launch) against the CSR layout on the same batches: the same n_id, sizes, per-row edges
     (local source, relation, CSR position, target row; the meta-only hop's source type / table
@@ -760,9 +759,6 @@ def test_strided_blocks_match_csr(monkeypatch, half_waves, dedup_one, csc_fuse):
     wave (fan-outs 9 and 7 fit 32 lanes)."""
     from regnn_hip import ns
     monkeypatch.setenv("REGNN_NS_HALF_WAVES", half_waves)
-    # "0": the multi-block kernels (one-pass look-back dedup, resolve + ranks + last-block scan,
-    # placement); "1": hop 0's de-duplication and transposed index in one workgroup
-    monkeypatch.setenv("REGNN_NS_DEDUP_ONE", dedup_one)
     # "on": hop 0's transposed index built by extra workgroups of hop 1's sums launch; "off": its
     # own launch after the de-duplication
     monkeypatch.setitem(ns.CSC_FUSE, "mode", csc_fuse)
