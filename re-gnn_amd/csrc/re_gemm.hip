@@ -27,9 +27,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #ifndef GEMM_BK
 #define GEMM_BK 32
 #endif
-#ifndef GEMM_XCD_REMAP
-#define GEMM_XCD_REMAP 1              // XCD-aware tile order (A/B: 0)
-#endif
 constexpr int BM = 128, BN = 128, BK = GEMM_BK, RS = BK + 8;
 constexpr int NQ = BM * BK / 4 / 256;       // quads (row, 4 k) per thread per operand tile
 constexpr int kThreads = 256;
@@ -165,22 +162,7 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
                const int32_t* __restrict__ k_live) {
     extern __shared__ uint16_t lds[];                 // [kStage]
     constexpr bool AKC = !TA, BKC = TB;               // k contiguous in A / B
-#if GEMM_XCD_REMAP
-    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin by linear id, so map
-    // consecutive linear ids of one XCD to consecutive tiles (a row panel's column tiles share
-    // that XCD's L2 instead of fetching the panel on up to four XCDs); bijective for any count
-    int bx, by;
-    {
-        const int nwg = int(gridDim.x * gridDim.y), orig = int(blockIdx.x + gridDim.x * blockIdx.y);
-        const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8, k = orig / 8;
-        const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + k;
-        bx = lin % int(gridDim.x);
-        by = lin / int(gridDim.x);
-    }
-#else
-    const int bx = blockIdx.x, by = blockIdx.y;
-#endif
-    const int64_t m0 = int64_t(by) * BM, n0 = int64_t(bx) * BN;
+    const int64_t m0 = int64_t(blockIdx.y) * BM, n0 = int64_t(blockIdx.x) * BN;
     const int z = blockIdx.z, S = gridDim.z;
     const int64_t Ke = k_live ? min(K, int64_t(*k_live)) : K;
     const int64_t nk = (m_live && m0 >= int64_t(*m_live)) ? 0 : (Ke + BK - 1) / BK;
