@@ -1073,7 +1073,9 @@ class NSTrainer:
             self._flat_zeroed = True
         if self._blocks_ok:
             B = s.B
-            n_id = s.n_id.to(torch.int64)
+            # the sampler's int32 ids as they are (torch indexes with int32; the HIP ops convert
+            # where they need to): no int64 copy per step
+            n_id = s.n_id
             from . import mag, ops
             fused_loss = (isinstance(self.model, mag.REGNN) and
                           os.environ.get("REGNN_NS_FUSED_LOSS", "on") != "off")
