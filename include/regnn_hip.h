@@ -587,6 +587,10 @@ int regnn_softmax_xent_bwd(const float* z, const int64_t* y, const float* lse, c
                            hipStream_t stream);
 int regnn_rel_tab(const float* rw, const float* gtab, int32_t n, float alpha, float slope,
                   float* out, hipStream_t stream);
+/* regnn_rel_tab over `count` <= 4 tables (rw[t] of n[t] entries; gtab NULL: forward, else every
+ * gtab[t] set: backward) in one launch: every conv layer's relation table at once. */
+int regnn_rel_tabs(const float* const* rw, const float* const* gtab, float* const* out,
+                   const int32_t* n, int32_t count, float alpha, float slope, hipStream_t stream);
 
 int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t rank,
                    int32_t world, int64_t* state, int32_t* n_id, int32_t* sizes,

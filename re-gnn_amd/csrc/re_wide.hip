@@ -176,6 +176,27 @@ __global__ void __launch_bounds__(kBlock) ln_bwd_kernel(LnArgs A) {
     }
 }
 
+
+// Several relation tables at once (every conv layer's leaky_relu(alpha rw), mag/regnn_layers.py:
+// 110-111), or their backward d rw = g alpha (alpha rw > 0 ? 1 : slope): one launch for all
+constexpr int kTabsMax = 4;
+struct TabsArgs {
+    const float* rw[kTabsMax]; const float* g[kTabsMax]; float* out[kTabsMax];
+    int start[kTabsMax + 1]; int count; float alpha, slope;
+};
+
+__global__ void __launch_bounds__(kBlock) rel_tabs_kernel(TabsArgs A) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.start[A.count]) return;
+    int t = 0;
+#pragma unroll
+    for (int q = 1; q < kTabsMax; ++q) t += (q < A.count && i >= A.start[q]) ? 1 : 0;
+    const int e = i - A.start[t];
+    const float x = A.alpha * A.rw[t][e];
+    A.out[t][e] = A.g[t] ? A.g[t][e] * (x > 0.f ? A.alpha : A.slope * A.alpha)
+                         : (x > 0.f ? x : A.slope * x);
+}
+
 }  // namespace wide
 }  // namespace regnn
 
@@ -210,6 +231,31 @@ bool aligned(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 }  // namespace
 
 extern "C" {
+
+int regnn_rel_tabs(const float* const* rw, const float* const* gtab, float* const* out,
+                   const int32_t* n, int32_t count, float alpha, float slope, hipStream_t stream) {
+    using namespace regnn::wide;
+    if (!rw || !out || !n || count < 1 || count > kTabsMax) return REGNN_EINVAL;
+    TabsArgs A{};
+    A.count = count;
+    A.alpha = alpha;
+    A.slope = slope;
+    A.start[0] = 0;
+    for (int t = 0; t < count; ++t) {
+        if (!rw[t] || !out[t] || n[t] < 0) return REGNN_EINVAL;
+        A.rw[t] = rw[t];
+        A.g[t] = gtab ? gtab[t] : nullptr;
+        if (gtab && !gtab[t]) return REGNN_EINVAL;
+        A.out[t] = out[t];
+        A.start[t + 1] = A.start[t] + n[t];
+    }
+    const int total = A.start[count];
+    if (total == 0) return REGNN_OK;
+    hipLaunchKernelGGL(rel_tabs_kernel, dim3(unsigned((total + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, stream, A);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
 
 int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, const float* bias,
                       const float* res, const float* gamma, const float* beta,

@@ -96,6 +96,7 @@ _SIG = {
     "regnn_ns_batch": ([P, I64, I32, I32, I32, P, P, P, P, P], ctypes.c_int),
     "regnn_ns_labels": ([P, P, P, I32, I64, P, P], ctypes.c_int),
     "regnn_rel_tab": ([P, P, I32, ctypes.c_float, ctypes.c_float, P, P], ctypes.c_int),
+    "regnn_rel_tabs": ([P, P, P, P, I32, ctypes.c_float, ctypes.c_float, P], ctypes.c_int),
     "regnn_softmax_xent_fwd": ([P, P, I32, I32, I64, P, P, P, P], ctypes.c_int),
     "regnn_softmax_xent_bwd": ([P, P, P, P, P, I32, I32, I64, P, P], ctypes.c_int),
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,

@@ -107,10 +107,12 @@ class REGCNConv(torch.nn.Module):
                                            x_target.shape[0]), tab
         return out
 
-    def forward_act(self, x_src, x_target, blk, p, state, layer):
+    def forward_act(self, x_src, x_target, blk, p, state, layer, tab=None):
         """forward() on a device-sampled block followed by the model's relu and dropout, the
-        bias / LayerNorm / relu / dropout as one launch (ops.wide_ln_act)."""
-        tab = ops.rel_tab(self.relation_weight, self.scaling_factor)            # :110-111
+        bias / LayerNorm / relu / dropout as one launch (ops.wide_ln_act). tab: this layer's
+        relation table when the caller formed it (ops.rel_tabs)."""
+        if tab is None:
+            tab = ops.rel_tab(self.relation_weight, self.scaling_factor)        # :110-111
         agg = ops.ns_spmm(blk, x_src, tab)
         if self.residual:
             agg = agg + x_target
@@ -286,6 +288,8 @@ TYPED_AGG = {"mode": "auto"}
 # relu / dropout as one launch each way (ops.wide_ln_act: regnn_wide_ln_fwd / _bwd); "off":
 # torch's kernels (A/B, tests)
 WIDE_EPI = {"mode": os.environ.get("REGNN_WIDE_EPI", "on")}
+# all layers' relation tables from one launch (ops.rel_tabs) on device-sampled blocks
+REL_TABS = os.environ.get("REGNN_REL_TABS", "1") != "0"
 
 
 class REGNN(torch.nn.Module):
@@ -461,7 +465,8 @@ class REGNN(torch.nn.Module):
             return None
         return p, state
 
-    def _typed_first_layer(self, n_id, x_dict, adjs, node_type, local_node_idx, epi=None):
+    def _typed_first_layer(self, n_id, x_dict, adjs, node_type, local_node_idx, epi=None,
+                           tab=None):
         """layer 0 over a device block with group_input folded in (None: not applicable).
 
         The reference runs every sampled node's raw row through its type's Linear
@@ -486,7 +491,8 @@ class REGNN(torch.nn.Module):
         if conv.relation_weight.numel() > 256:
             return None
         T, K = len(tabs), int(tabs[0].shape[1])
-        tab = ops.rel_tab(conv.relation_weight, conv.scaling_factor)           # :110-111
+        if tab is None:
+            tab = ops.rel_tab(conv.relation_weight, conv.scaling_factor)       # :110-111
         # [S | w]: the per-type sums and weight sums as one [n, T K + T] operand, so the
         # projection S W_c + w b_c is one GEMM against [W_c; b_c] (products on regnn_gemm_x6:
         # fp32-accurate bf16x6 MFMA; the small composition b_cat W_0 stays on hipBLASLt)
@@ -529,7 +535,16 @@ class REGNN(torch.nn.Module):
         (a caller that forms the loss itself, e.g. NSTrainer with ops.softmax_xent)."""
         blk0 = tuple(adjs[0])[0] if adjs else None
         epi = self._wide_epi(blk0) if getattr(blk0, "is_ns_block", False) else None
-        r = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx, epi)
+        # every layer's relation table in one launch (and one in the backward) on device blocks
+        tabs = None
+        if REL_TABS and epi is not None and self.model == 'regcn' and 1 <= len(self.convs) <= 4:
+            rws = [getattr(c, "relation_weight", None) for c in self.convs]
+            alphas = {getattr(c, "scaling_factor", None) for c in self.convs}
+            if (all(r is not None and r.is_cuda and r.dtype == torch.float32 and r.dim() == 1
+                    for r in rws) and len(alphas) == 1 and None not in alphas):
+                tabs = ops.rel_tabs(rws, alphas.pop())
+        r = self._typed_first_layer(n_id, x_dict, adjs, node_type, local_node_idx, epi,
+                                    tab=None if tabs is None else tabs[0])
         x, acted = (None, False) if r is None else r
         if x is None and adjs and getattr(tuple(adjs[0])[0], "meta_only", False):
             raise RuntimeError("layer 0's block was sampled meta-only (no local source ids): "
@@ -552,7 +567,8 @@ class REGNN(torch.nn.Module):
             if (blk is not None and getattr(blk, "is_ns_block", False) and epi is not None and
                     self.self_loop_type == 2 and ops.wide_ln_ok(x, self.convs[i].norm, self.convs[i].bias)):
                 ep = self._wide_epi(blk) or epi
-                x = self.convs[i].forward_act(x, x_target, blk, ep[0], ep[1], i)
+                x = self.convs[i].forward_act(x, x_target, blk, ep[0], ep[1], i,
+                                              tab=None if tabs is None else tabs[i])
                 continue                       # (relu and dropout applied in the epilogue)
             if blk is not None and self.model == 'regcn' and self.self_loop_type == 2:
                 x = self.convs[i]((x, x_target), blk)          # relation ids formed on device

@@ -793,6 +793,41 @@ class _RelTab(torch.autograd.Function):
         return out, None, None
 
 
+class _RelTabs(torch.autograd.Function):
+    """every layer's relation table in one launch, their backward in one (regnn_rel_tabs)."""
+
+    @staticmethod
+    def forward(ctx, alpha, slope, *rws):
+        rws = [r.contiguous() for r in rws]
+        outs = [torch.empty_like(r) for r in rws]
+        n = (ctypes.c_int32 * len(rws))(*[r.numel() for r in rws])
+        L.call("regnn_rel_tabs", _ptr_array([L.ptr(r) for r in rws]), None,
+               _ptr_array([L.ptr(o) for o in outs]), n, len(rws), float(alpha), float(slope),
+               L.stream())
+        ctx.save_for_backward(*rws)
+        ctx.alpha, ctx.slope = alpha, slope
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        rws = ctx.saved_tensors
+        gs = [torch.zeros_like(r) if g is None else g.contiguous() for r, g in zip(rws, gs)]
+        outs = [torch.empty_like(r) for r in rws]
+        n = (ctypes.c_int32 * len(rws))(*[r.numel() for r in rws])
+        L.call("regnn_rel_tabs", _ptr_array([L.ptr(r) for r in rws]),
+               _ptr_array([L.ptr(g) for g in gs]), _ptr_array([L.ptr(o) for o in outs]), n,
+               len(rws), float(ctx.alpha), float(ctx.slope), L.stream())
+        return (None, None) + tuple(outs)
+
+
+def rel_tabs(rws, alpha, slope=0.01):
+    """[leaky_relu(alpha * rw, slope) for rw in rws] (<= 4 fp32 device tensors) in one launch
+    forward and one backward."""
+    if not (1 <= len(rws) <= 4 and all(r.is_cuda and r.dtype == torch.float32 for r in rws)):
+        raise ValueError("rel_tabs: 1..4 fp32 device tensors")
+    return list(_RelTabs.apply(alpha, slope, *rws))
+
+
 def rel_tab(rw, alpha, slope=0.01):
     """leaky_relu(alpha * rw, slope) (mag/regnn_layers.py:110-111): the relation table of an
     fp32 device relation_weight in one launch instead of a multiply and an activation (and two

@@ -269,6 +269,33 @@ def test_rel_tab_and_labels_match_torch():
         assert torch.equal(y, want)
 
 
+def test_rel_tabs_match_torch():
+    """ops.rel_tabs: every layer's relation table from one launch, forward bitwise against
+    leaky_relu(alpha rw) per table (mag/regnn_layers.py:110-111), backward per table to 1e-6,
+    a table the loss does not reach getting a zero gradient."""
+    import torch.nn.functional as F
+    from regnn_hip import ops
+    g0 = torch.Generator(device=DEV)
+    g0.manual_seed(11)
+    for sizes in ((23,), (23, 23, 23), (5, 300, 1, 17)):
+        rws = [(torch.randn(n, device=DEV, generator=g0) * 0.02).requires_grad_(True)
+               for n in sizes]
+        refs = [r.detach().clone().requires_grad_(True) for r in rws]
+        tabs = ops.rel_tabs(rws, 100.0)
+        want = [F.leaky_relu(r * 100.0) for r in refs]
+        for t, w in zip(tabs, want):
+            assert torch.equal(t, w)
+        gs = [torch.randn(n, device=DEV, generator=g0) for n in sizes]
+        used = range(len(sizes) - 1) if len(sizes) > 1 else range(1)
+        sum((tabs[i] * gs[i]).sum() for i in used).backward()
+        sum((want[i] * gs[i]).sum() for i in used).backward()
+        for i, (r, rr) in enumerate(zip(rws, refs)):
+            if i in used:
+                torch.testing.assert_close(r.grad, rr.grad, rtol=1e-6, atol=0)
+            else:
+                assert r.grad is None or not r.grad.any()
+
+
 def test_softmax_xent_matches_torch():
     """ops.softmax_xent (one launch each way) against log_softmax + nll_loss with ignored rows,
     loss and logits gradient to 1e-6, and the all-ignored batch (nan, as torch)."""
