@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 43). */
+/* ABI version (bumped on any signature or semantics change; currently 42). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -923,15 +923,11 @@ int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits);
 int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                   float beta, float* work, int32_t splits, const int32_t* m_live,
-                  const int32_t* k_live, int32_t* tickets, hipStream_t stream);
+                  const int32_t* k_live, hipStream_t stream);
 /* m_live / k_live (ABI 41; device int32 counts, may be NULL): op(A)'s rows m >= *m_live, and the
  * k >= *k_live columns of op(A) / rows of op(B), are zero (the unused rows of a capacity-sized
  * sampled block): the kernel skips their products (C rows >= *m_live get beta C) -- the same C,
- * with the work of the live rows only.
- * tickets (ABI 43; may be NULL): with splits > 1, ceil(M / 128) * ceil(N / 128) device int32
- * zeros (left zero again): the last split block of each 128 x 128 tile to finish adds the tile's
- * partials (same split order, same bits) instead of a second reduce launch. The launches that
- * share a ticket array must be stream-ordered. NULL: the reduce launch. */
+ * with the work of the live rows only. */
 
 /* Several strided 2-D fp32 copies in one launch: dst[i * cols + j] = src[i * s0 + j * s1] for
  * each descriptor (the module path's parameter gradients, some of them transposed views, into the

@@ -14,11 +14,7 @@
 //
 // Split-K (splits > 1): block z of the grid's third dimension sums k-steps z, z + splits, ...
 // into its own partial C (work [splits][M][N]); regnn_gemm_x6 then adds the partials in split
-// order (fixed: bitwise reproducible). With a ticket array the adding needs no second launch:
-// each block publishes its partial (agent release) and takes its tile's ticket; the last of the
-// tile's splits to arrive (acquire) adds the tile's partials in the same split order and resets
-// the ticket (the same bits as the reduce launch, its tile's partials read while the other
-// tiles still compute).
+// order (fixed: bitwise reproducible).
 #include "regnn_common.h"
 
 namespace regnn {
@@ -163,7 +159,7 @@ __global__ void __launch_bounds__(kThreads, 2)
 gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
                float beta, float* __restrict__ work, const int32_t* __restrict__ m_live,
-               const int32_t* __restrict__ k_live, int32_t* __restrict__ tickets) {
+               const int32_t* __restrict__ k_live) {
     extern __shared__ uint16_t lds[];                 // [kStage]
     constexpr bool AKC = !TA, BKC = TB;               // k contiguous in A / B
     const int64_t m0 = int64_t(blockIdx.y) * BM, n0 = int64_t(blockIdx.x) * BN;
@@ -223,40 +219,6 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
                 }
             }
         }
-    if (S == 1 || !tickets) return;
-    // the flag in the (dynamic, 16-byte aligned) stage: a static __shared__ variable would shift
-    // the stage by 4 bytes and misalign every 8- / 16-byte LDS access of the main loop
-    int& s_last = *reinterpret_cast<int*>(lds);
-    const int tile = int(blockIdx.y) * int(gridDim.x) + int(blockIdx.x);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's partial stores done
-    __syncthreads();                                    // (and every wave's stage reads)
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = __hip_atomic_fetch_add(tickets + tile, 1, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    // the tile's elements, 128 consecutive columns per half block; each summed over the splits
-    // in split order (gemm_reduce_kernel's order)
-    const int64_t total = M * N;
-    const int nr = int(min(int64_t(BM), M - m0)), ncol = int(min(int64_t(BN), N - n0));
-    for (int e = threadIdx.x; e < nr * BN; e += kThreads) {
-        const int r = e >> 7, cc = e & (BN - 1);
-        if (cc >= ncol) continue;
-        const int64_t m = m0 + r, n = n0 + cc, x = m * N + n;
-        float sum = work[x];
-        for (int zz = 1; zz < S; ++zz) sum += work[int64_t(zz) * total + x];
-        float* o = C + m * ldc + n;
-        *o = beta != 0.f ? sum + beta * *o : sum;
-    }
 }
 
 // C = sum_z work[z] (in split order) + beta C
@@ -310,7 +272,7 @@ int64_t regnn_gemm_x6_work_floats(int64_t M, int64_t N, int32_t splits) {
 int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                   float beta, float* work, int32_t splits, const int32_t* m_live,
-                  const int32_t* k_live, int32_t* tickets, hipStream_t stream) {
+                  const int32_t* k_live, hipStream_t stream) {
     if (M < 0 || N < 0 || K < 0 || splits < 1 || splits > 64) return REGNN_EINVAL;
     if (M == 0 || N == 0) return REGNN_OK;
     if (!A || !B || !C || (splits > 1 && !work)) return REGNN_EINVAL;
@@ -327,14 +289,14 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
 #define GEMM_CASE(TA_, TB_, V_)                                                                \
     if (bool(trans_a) == TA_ && bool(trans_b) == TB_ && vec == V_) {                           \
         hipLaunchKernelGGL((gemm_x6_kernel<TA_, TB_, V_>), grid, dim3(kThreads), lds, stream, M, N, \
-                           K, A, lda, B, ldb, C, ldc, beta, work, m_live, k_live, tickets);    \
+                           K, A, lda, B, ldb, C, ldc, beta, work, m_live, k_live);             \
     }
     GEMM_CASE(false, false, true) GEMM_CASE(false, true, true) GEMM_CASE(true, false, true)
     GEMM_CASE(true, true, true) GEMM_CASE(false, false, false) GEMM_CASE(false, true, false)
     GEMM_CASE(true, false, false) GEMM_CASE(true, true, false)
 #undef GEMM_CASE
     REGNN_LAUNCH_CHECK();
-    if (splits > 1 && !tickets) {
+    if (splits > 1) {
         int64_t blocks = (M * N + kThreads - 1) / kThreads;
         if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, stream, M,

@@ -1685,28 +1685,6 @@ def _gemm_splits(M, N, K):
     return int(max(1, min(64, _SPLIT_TARGET // tiles, nk // 4)))
 
 
-# split-K partials added inside the GEMM by each tile's last split block (regnn_gemm_x6's tickets:
-# no reduce launch) for splits <= this; larger splits keep the reduce launch (one block reading a
-# tile's many partials is slower than the spread-out reduce). env REGNN_GEMM_FIXUP_MAX, 0: off
-_FIXUP_MAX = int(os.environ.get("REGNN_GEMM_FIXUP_MAX", "8"))
-_TICKETS = {}
-_TICKETS_N = 1 << 16
-
-
-def _gemm_tickets(dev, tiles):
-    """the device's ticket array (zeros, left zero by every launch): allocated on first use, which
-    is eager (a captured step has run warm-up steps first); every x6 GEMM is issued on L.stream()
-    in stream order"""
-    if tiles > _TICKETS_N:
-        return None
-    t = _TICKETS.get(dev)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        t = _TICKETS[dev] = torch.zeros(_TICKETS_N, dtype=torch.int32, device=dev)
-    return t
-
-
 def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0, m_live=None, k_live=None):
     """op(a) @ op(b) (+ beta * out) in fp32 accuracy: a [M, K] ([K, M] with trans_a), b [K, N]
     ([N, K] with trans_b), contiguous fp32 device tensors. m_live / k_live: one-element int32
@@ -1722,11 +1700,9 @@ def gemm_x6(a, b, trans_a=False, trans_b=False, out=None, beta=0.0, m_live=None,
     S = _gemm_splits(M, N, K)
     work = (torch.empty(int(L._so.regnn_gemm_x6_work_floats(M, N, S)), dtype=torch.float32,
                         device=a.device) if S > 1 else None)
-    tickets = (_gemm_tickets(a.device, -(-M // 128) * -(-N // 128))
-               if 1 < S <= _FIXUP_MAX else None)
     L.call("regnn_gemm_x6", int(trans_a), int(trans_b), M, N, K, L.ptr(a), a.stride(0), L.ptr(b),
            b.stride(0), L.ptr(out), out.stride(0), float(beta), L.ptr(work), S, L.ptr(m_live),
-           L.ptr(k_live), L.ptr(tickets), L.stream())
+           L.ptr(k_live), L.stream())
     return out
 
 

@@ -51,35 +51,6 @@ def test_gemm_x6_beta_and_splits_deterministic():
     assert ((outs[0].double() - ref).abs() <= 2e-6 * mag).all()
 
 
-@pytest.mark.parametrize("M,N,K,ta", [(1024, 512, 512, False), (520, 128, 512, False),
-                                      (512, 512, 1024, True), (333, 132, 1000, True),
-                                      (128, 512, 520, True)])
-def test_gemm_x6_ticket_fixup_bitwise(M, N, K, ta, monkeypatch):
-    """split-K partials added by each tile's last split block (tickets) against the reduce launch:
-    the same bits (split order), with beta, ragged edge tiles and every split count up to 8, the
-    ticket array left zero for the next launch"""
-    from regnn_hip import ops
-    g = torch.Generator(device=DEV).manual_seed(M + N + K)
-    a = torch.randn(*((K, M) if ta else (M, K)), generator=g, device=DEV)
-    b = torch.randn(K, N, generator=g, device=DEV)
-    c0 = torch.randn(M, N, generator=g, device=DEV)
-    tiles = -(-M // 128) * -(-N // 128)
-    for S in (2, 3, 5, 8):
-        monkeypatch.setattr(ops, "_gemm_splits", lambda *_a, S=S: S)
-        outs = []
-        for fix in (0, 8):
-            monkeypatch.setattr(ops, "_FIXUP_MAX", fix)
-            for beta in (0.0, 1.0):
-                c = c0.clone()
-                ops.gemm_x6(a, b, trans_a=ta, out=c, beta=beta)
-                outs.append(c)
-        torch.cuda.synchronize()
-        assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3]), S
-        assert not ops._TICKETS[torch.device(DEV, torch.cuda.current_device())][:tiles].any()
-    ref, mag = _ref(a, b, ta, False)
-    assert ((outs[2].double() - ref).abs() <= 2e-6 * mag + 1e-30).all()
-
-
 def test_mm_autograd_matches_fp64():
     from regnn_hip import ops
     g = torch.Generator(device=DEV).manual_seed(5)
