@@ -1103,12 +1103,11 @@ class NSTrainer:
         # lower to a kernel per tensor here: ~90 us per step at hidden 512)
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         with torch.no_grad():
-            dst = [p.grad for p, g in zip(self.params, grads) if g is not None]
-            src = [g for g in grads if g is not None]
-            if dst:
-                from . import ops
-                ops.copy_many(dst, src)
-            self.loss.copy_(loss.detach())
+            # (the loss rides in the same launch: no copy of its own)
+            dst = [p.grad for p, g in zip(self.params, grads) if g is not None] + [self.loss]
+            src = [g for g in grads if g is not None] + [loss.detach()]
+            from . import ops
+            ops.copy_many(dst, src)
 
     def _set_exchange_split(self):
         """the split exchange (two-layer fused step without the fused Adam): every slot's step
