@@ -228,8 +228,17 @@ gemm_reduce_kernel(int64_t M, int64_t N, const float* __restrict__ work, int S, 
     const int64_t total = M * N;
     for (int64_t e = int64_t(blockIdx.x) * kThreads + threadIdx.x; e < total;
          e += int64_t(gridDim.x) * kThreads) {
+        // the splits' loads 8 at a time in flight (clamped addresses, unconditional), added in
+        // split order (the same bits as one load and add per split)
         float s = work[e];
-        for (int z = 1; z < S; ++z) s += work[int64_t(z) * total + e];
+        for (int z = 1; z < S; z += 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = work[int64_t(z + j < S ? z + j : 0) * total + e];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (z + j < S) s += v[j];
+        }
         const int64_t m = e / N, n = e - m * N;
         float* o = C + m * ldc + n;
         *o = beta != 0.f ? s + beta * *o : s;
