@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 42). */
+/* ABI version (bumped on any signature or semantics change; currently 43). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -550,7 +550,7 @@ int regnn_sample_fill(const int32_t* ptr, const int32_t* idx, const int32_t* tar
  *  g2l, first  uint64 [num_nodes] dedup tables: g2l zero-filled, first all-ones, once.
  *  Per-hop scratch (cap_dst = capacity of the hop's targets, k = fan-out, cap_e = cap_dst*(k+1)):
  *  samp, spos [cap_dst*k] int32; scnt [cap_dst] int32; gsrc [cap_e] int32; flag [cap_e] uint8;
- *  tiles [ceil(cap_e/1024) + 1] int32, zero-filled once; status [ceil(cap_dst/1024)] uint64
+ *  tiles [ceil(cap_e/1024) + 4] int32, zero-filled once; status [ceil(cap_dst/1024)] uint64
  *  (row-offset look-back, zero-filled once).
  *  Block output (mag/regnn_layers.py:90-99 with self_loop_type 2): blk_ptr [cap_dst+1],
  *  blk_idx [cap_e] (local source ids; row i's self loop last), blk_rel [cap_e] uint8 (edge type
@@ -622,8 +622,10 @@ int regnn_ns_batch(const int64_t* perm, int64_t n_perm, int32_t batch, int32_t r
  * look-back over status), the transposed index by many blocks in one launch (the last block
  * to resolve scans the counts and publishes csc_ptr, then every block places its entries):
  * 3 launches with de-duplication and the transposed index, 1 meta-only. Strided buffer sizes:
- * tiles >= 2 ints (an arrival ticket and a published stamp), status >= ceil(cap_e / 1024)
- * int64 (ABI 42). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
+ * tiles >= ceil(cap_e / 1024) + 4 ints (the CSR path's tile words, then the index's own arrival
+ * ticket, published stamp and sticky error word at tiles[ceil(cap_e / 1024) + 3]: 1 when a block
+ * gave up waiting for the publish and placed nothing -- the caller checks it), status >=
+ * ceil(cap_e / 1024) int64 (ABI 43). sizes[8 + hop] must be zero on entry (regnn_ns_batch zeroes sizes[8 ..]);
  * the hop adds its edges to it and to state[5]. strided = 2 (with the transposed index, no
  * edge meta): everything but the transposed index and the sampled edges' blk_idx, which a
  * second call with strided = 3 and the same arguments then writes (on another stream if the
@@ -667,7 +669,7 @@ typedef struct regnn_ns_csc_job {
     const int32_t* blk_row;
     const uint8_t* blk_rel;
     int32_t* csc_cnt;
-    int32_t* tiles;             /* >= 2 ints */
+    int32_t* tiles;             /* >= ceil(cap_e / 1024) + 4 ints (as regnn_ns_hop) */
     int32_t* csc_ptr;
     int32_t* csc_ent;
     int32_t* csc_long;

@@ -936,7 +936,6 @@ int regnn_gat_softmax_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
         return REGNN_OK;
     }
     if (const int rc = check_plan(plan, 2 * H)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     const LongPlan P = long_plan(plan);
     hipLaunchKernelGGL(gat_softmax_fwd_group<0>, dim3(grid_for(n_seg, kBlock / kGatGroup)),
                        dim3(kBlock), 0, stream, ptr, idx, rel, ee_table, el, er, n_seg, H, lg,
@@ -975,7 +974,6 @@ int regnn_gat_softmax_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t*
         return REGNN_OK;
     }
     if (const int rc = check_plan(plan, H)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     const LongPlan P = long_plan(plan);
     const int g0 = grid_for(n_seg, kBlock / kGatGroup);
     hipLaunchKernelGGL(gat_softmax_bwd_group<0>, dim3(g0), dim3(kBlock), lds, stream, ptr, idx,
@@ -1012,7 +1010,6 @@ int regnn_gat_fused_fwd(const int32_t* ptr, const int32_t* idx, const uint8_t* r
         return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, int64_t(H) * D + 2 * H)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     GatFusedArgs p{ptr, idx, rel, ee_table, el, er, x, out, lse, attn_l, n_seg, H, D, slope};
     if (dtype == REGNN_F32) return dispatch_gat_fused<float>(p, plan, stream);
     if (dtype == REGNN_BF16) return dispatch_gat_fused<bf16_t>(p, plan, stream);
@@ -1049,7 +1046,6 @@ int regnn_spmm_heads_fwd(const int32_t* ptr, const int32_t* idx, const int32_t* 
     if (!ptr || !idx || !a || !x || !y || n_seg < 0) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, int64_t(H) * D)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     HeadArgs p{ptr, idx, perm, a, x, nullptr, y, nullptr, n_seg, H, D};
     if (dtype == REGNN_F32) return dispatch_heads<float, false>(p, plan, stream);
     if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, false>(p, plan, stream);
@@ -1063,7 +1059,6 @@ int regnn_spmm_heads_bwd(const int32_t* ptr, const int32_t* idx, const int32_t* 
     if (!ptr || !idx || !a || !g || !x || !gx || !ga || n_seg < 0) return REGNN_EINVAL;
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, int64_t(H) * D)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     HeadArgs p{ptr, idx, perm, a, g, x, gx, ga, n_seg, H, D};
     if (dtype == REGNN_F32) return dispatch_heads<float, true>(p, plan, stream);
     if (dtype == REGNN_BF16) return dispatch_heads<bf16_t, true>(p, plan, stream);
@@ -1082,7 +1077,6 @@ int regnn_segment_sum(const int32_t* ptr, const int32_t* perm, const float* vals
         return REGNN_OK;
     }
     if (const int rc = check_plan(plan, H)) return rc;
-    if (plan && plan->n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     const LongPlan P = long_plan(plan);
     hipLaunchKernelGGL(segment_sum_group<false>, dim3(grid_for(n_seg, kBlock / kGatGroup)),
                        dim3(kBlock), 0, stream, ptr, perm, vals, n_seg, H, lg, out, P);

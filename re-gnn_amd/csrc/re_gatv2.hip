@@ -180,7 +180,6 @@ int launch_gatv2(V2Args p, int grid, const regnn_seg_plan* pl, int grid2, hipStr
     const int nvec = F / 4;
     if (const int rc = check_plan(pl, MODE == 0 ? 0 : F)) return rc;
     const LongPlan P = long_plan(pl);
-    if (MODE != 0 && P.n_chunk > 0 && pl->n_levels == 0) return REGNN_EUNSUPPORTED;
 #define REGNN_V2(LPR, NV)                                                                        \
     if (nvec <= (LPR) * (NV) && vph <= (LPR)) {                                                  \
         const size_t lds = MODE == 1 ? size_t(kBlock / (LPR)) * F * sizeof(float) : 0;           \
@@ -469,7 +468,6 @@ int regnn_edge_softmax_fwd(const int32_t* ptr, const float* s, const uint8_t* re
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, 2 * H)) return rc;
     const LongPlan P = long_plan(plan);
-    if (P.n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     hipLaunchKernelGGL(edge_softmax_fwd_kernel<0>, dim3(grid_for(n_seg, kBlock / kSmG)),
                        dim3(kBlock), 0, stream, ptr, s, rel, ee_table, gmax, eps, n_seg, H, lg, a,
                        P, nullptr, 0, 0);
@@ -497,7 +495,6 @@ int regnn_edge_softmax_bwd(const int32_t* ptr, const uint8_t* rel, const float* 
     if (n_seg == 0) return REGNN_OK;
     if (const int rc = check_plan(plan, H)) return rc;
     const LongPlan P = long_plan(plan);
-    if (P.n_chunk > 0 && plan->n_levels == 0) return REGNN_EUNSUPPORTED;
     const size_t lds = slab ? size_t(n_rel) * kBlock * sizeof(float) : 0;
     // the slab's rows: the per-segment pass's blocks, then the chunk pass's (regnn_slab_rows()
     // = 2 kMaxGrid holds both grids)

@@ -805,14 +805,23 @@ struct NsCscJob {
     int32_t* csc_cnt; int32_t* tiles; int32_t* csc_ptr; int32_t* csc_ent; int32_t* csc_long;
 };
 
-// One workgroup (block `bid` of `nb`) of the transposed index's launch. tiles[0]: the arrival
-// ticket (reset by the last block), tiles[1]: the published stamp
+// The strided transposed index's control words, past everything the CSR path's flag tiles use
+// (tiles[0 .. n_tiles]: the tile counts / prefixes and their ticket): ctl[0] the arrival ticket
+// (reset by the last block), ctl[1] the published stamp (no other kernel writes it, so a leftover
+// value never equals this hop's stamp), ctl[2] a sticky error word (1: a waiting block's bounded
+// spin ran out before the publish; its entries were not placed). tiles >= n_tiles + 4 ints.
+__device__ __forceinline__ int32_t* csc_ctl(const NsCscJob& J) {
+    return J.tiles + (J.cap_e + kNsTile - 1) / kNsTile + 1;
+}
+
+// One workgroup (block `bid` of `nb`) of the transposed index's launch (control words: csc_ctl)
 template <int Q>
 __device__ void csc_resolve_place(const NsCscJob& J, const int32_t* __restrict__ sizes,
                                   const int64_t* __restrict__ state, int bid, int nb) {
     __shared__ int sbuf[(kCscScanT / 64) * csc_scan_pad<Q>()];
     __shared__ int swave[3 * (kCscScanT / 64)];
-    __shared__ int last;
+    __shared__ int last, ok;
+    int32_t* ctl = csc_ctl(J);
     const int bp = bid * kCscScanT + threadIdx.x;
     int lid = -1, rank = 0, ent = 0;
     if (bp < J.cap_e) {
@@ -833,8 +842,9 @@ __device__ void csc_resolve_place(const NsCscJob& J, const int32_t* __restrict__
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(J.tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        last = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                nb - 1;
+        ok = 1;
     }
     __syncthreads();
     if (last) {
@@ -849,25 +859,31 @@ __device__ void csc_resolve_place(const NsCscJob& J, const int32_t* __restrict__
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(J.tiles, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(J.tiles + 1, int(stamp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl + 1, int(stamp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     } else if (threadIdx.x == 0) {
         // one lane polls the published stamp (relaxed), then one acquire; bounded (a watchdog:
-        // the last block holds a CU and runs to the publish)
-        for (uint32_t spins = 0; spins < (1u << 26); ++spins) {
-            if (uint32_t(__hip_atomic_load(J.tiles + 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)) == stamp)
-                break;
-            __builtin_amdgcn_s_sleep(1);
+        // the last block holds a CU and runs to the publish). A spin that runs out places
+        // nothing (csc_ptr may be stale) and raises the sticky error word the host checks
+        // (DeviceSampler.check_index)
+        int seen = 0;
+        for (uint32_t spins = 0; spins < (1u << 26) && !seen; ++spins) {
+            seen = uint32_t(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)) == stamp;
+            if (!seen) __builtin_amdgcn_s_sleep(1);
+        }
+        if (!seen) {
+            __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = 0;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (lid >= 0) J.csc_ent[J.csc_ptr[lid] + rank] = ent;
+    if (lid >= 0 && ok) J.csc_ent[J.csc_ptr[lid] + rank] = ent;
 }
 
 inline int csc_blocks(int64_t cap_e) { return int((cap_e + kCscScanT - 1) / kCscScanT); }

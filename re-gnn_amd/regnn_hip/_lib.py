@@ -131,7 +131,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 42
+ABI_VERSION = 43
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

@@ -7,11 +7,17 @@ blocked until the process group's timeout. The rules here:
 
 * every stage that can fail on one rank is run by ``Guard.stage``: the exception is caught, the
   collectives the peers are issuing in that stage (``always``: e.g. the step's gradient
-  exchange) are still issued, and all ranks then agree on the outcome with one eager MAX
-  all-reduce of the failure flags;
+  exchange) are still issued, and all ranks then agree on the outcome with one eager SUM
+  all-reduce of the failure flags (the number of ranks that failed);
 * if any rank failed, every rank raises ``RankFailure`` (a SystemExit with a non-zero code), so
   the whole job ends with a non-zero exit on every rank instead of hanging; the failing rank's
   own traceback is printed first;
+* the agreement itself is guarded: if its all-reduce (or reading its result) raises -- a peer
+  that died, a device left in a faulted state -- this rank raises ``RankFailure`` too, so it
+  exits with ``EXIT_CODE`` rather than a plain RuntimeError;
+* a rank whose device faults hard (the process is killed, or it hangs inside a HIP call) never
+  reaches the agreement: its peers' agreement all-reduce then fails at the process group's
+  timeout (``pg_timeout``), which ends them through the rule above;
 * nothing here re-executes a process (no exec of any kind after the GPU was touched).
 
 One rank: ``stage`` runs fn and lets its exception propagate unchanged.
@@ -33,6 +39,8 @@ class RankFailure(SystemExit):
         self.what, self.ranks_failed, self.local_exc = what, ranks_failed, local_exc
 
     def __str__(self):
+        if self.ranks_failed < 0:
+            return f"stage '{self.what}': the ranks could not agree (collective failed)"
         return f"stage '{self.what}' failed on {self.ranks_failed} rank(s)"
 
 
@@ -64,9 +72,15 @@ class Guard:
         """True on every rank when ok holds on every rank; else RankFailure on every rank."""
         if self.world <= 1:
             return True
-        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=self.device)
-        self.dist.all_reduce(flag, op=self.dist.ReduceOp.SUM)
-        n_bad = int(flag.item())
+        try:
+            flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=self.device)
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.SUM)
+            n_bad = int(flag.item())
+        except Exception as e:               # noqa: BLE001 (a dead peer, a faulted device)
+            rank = self.dist.get_rank() if self.dist.is_initialized() else -1
+            print(f"[rank {rank}] the agreement after '{what}' failed: {e}", file=sys.stderr,
+                  flush=True)
+            raise RankFailure(what, -1, e) from e
         if n_bad:
             raise RankFailure(what, n_bad)
         return True

@@ -119,10 +119,11 @@ class DeviceSampler:
             ce = cd * (k + 1)
             nt = (ce + 1023) // 1024
             z = lambda n, dt=torch.int32: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
-            # tiles: the strided transposed index's ticket and stamp too (>= 2); status: the
-            # strided de-duplication's look-back too (>= ceil(ce / 1024) tiles)
+            # tiles: the CSR de-duplication's nt tile counts and their ticket, then the strided
+            # transposed index's own ticket, published stamp and error word (nt + 4); status:
+            # the strided de-duplication's look-back too (>= ceil(ce / 1024) tiles)
             self.hop_bufs.append(dict(samp=z(cd * k), spos=z(cd * k), scnt=z(cd), gsrc=z(ce),
-                                      flag=z(ce, torch.uint8), tiles=z(nt + 1),
+                                      flag=z(ce, torch.uint8), tiles=z(nt + 4),
                                       status=z(max((cd + 1023) // 1024, nt), torch.int64)))
             blk = NSBlock(z(cd + 1), z(ce), z(ce, torch.uint8), z(ce),
                           torch.ones(cd, dtype=torch.float32, device=dev), cd, caps[h + 1], ce, dev,
@@ -131,6 +132,8 @@ class DeviceSampler:
             self.blocks.append(blk)
         self.local, self.edge_meta = None, [None] * len(self.sizes_k)
         self.meta_fresh = [False] * len(self.sizes_k)
+        # sums_fresh[h]: the latest run_hops wrote hop h's layer-0 input sums (typed_sums path)
+        self.sums_fresh = [False] * len(self.sizes_k)
         self.csc = [None] * len(self.sizes_k)      # per hop: (cnt, ptr, ent, long) or None
         # strided: every hop's block in the fixed-stride layout (row i at i (k + 1), regnn_ns_hop
         # strided) -- the two-layer fused step's layout; False: the CSR layout the module path,
@@ -154,6 +157,19 @@ class DeviceSampler:
                                torch.zeros(ce, dtype=torch.int64, device=self.device))
         self.meta_fresh[hop] = False          # written by the next run_hops
         return self.edge_meta[hop]
+
+    def index_errors(self):
+        """device int32 tensor: per hop the strided transposed index's sticky error word (1: a
+        block of regnn_ns_hop's index launch gave up waiting for the publish and placed nothing;
+        the index of that batch is incomplete). Reading it is one host sync (check_index)."""
+        return torch.stack([b["tiles"][-1] for b in self.hop_bufs])
+
+    def check_index(self):
+        """raise if any hop's transposed index reported a failed build (index_errors)."""
+        bad = self.index_errors().cpu().tolist()
+        if any(bad):
+            raise RuntimeError(f"regnn_ns_hop: the transposed index build timed out waiting for "
+                               f"its publish (hops {[h for h, v in enumerate(bad) if v]})")
 
     def enable_csc(self, hop):
         """also build hop `hop`'s transposed index (regnn_ns_hop csc_*: per local source, its
@@ -203,7 +219,9 @@ class DeviceSampler:
                            ctypes.addressof(self._csc_job(h - 1)) if deferred == h - 1 else None,
                            L.stream())
                 self.meta_fresh[h] = True
+                self.sums_fresh[h] = True
                 continue
+            self.sums_fresh[h] = False
             # the transposed index of this hop built beside the next hop's sums (one launch)
             defer = (not fork and strided and CSC_FUSE["mode"] != "off" and
                      self.csc[h] is not None and self.edge_meta[h] is None and
@@ -485,6 +503,11 @@ LEAN_LAST_HOP = {"mode": "on"}
 # per-type input sums (regnn_ns_hop_typed_sums) on the sampler's stream, ahead of the model, and
 # agg0 reads them (regnn_nsm_work.pre_sums); "off": agg0 gathers the raw rows itself (A/B, tests)
 PRE_SUMS = {"mode": os.environ.get("REGNN_NS_PRE_SUMS", "on")}
+# capture order of a lookahead group's launches: "model" (every model step, then every sampler
+# batch) or "interleave" (model step i, then sampler batch i): the same dependency edges, but the
+# runtime enqueues a replay's nodes in capture order, so with "model" the sampler's first launch
+# reaches its queue only after the host has enqueued the whole model chain
+GROUP_ORDER = {"mode": os.environ.get("REGNN_NS_GROUP_ORDER", "model")}
 
 
 def relation_slots_ok(sampler, T):
@@ -683,6 +706,12 @@ class FusedStep:
         if not self.sampler.meta_fresh[self.n_layers - 1]:
             raise RuntimeError("run the sampler's hops after building FusedStep: layer 0 reads the "
                                "per-edge source type / table row they write")
+        if self.W.pre_sums and not self.sampler.sums_fresh[self.n_layers - 1]:
+            # run_hops(meta_only=False) or run_hops(strided=False) samples the outer hop without
+            # its input sums: agg0 / bwd0 would read an earlier batch's
+            raise RuntimeError("the sampler's latest batch did not form layer 0's input sums "
+                               "(run_hops with meta_only=True and the strided layout, as the "
+                               "fused step's sampling does)")
         # train / eval decides the dropout (a captured graph keeps the value it was captured with)
         self.P.p_drop = float(self.model.dropout) if self.model.training else 0.0
         with torch.cuda.device(self.device), timed("nsm_step"):
@@ -1009,10 +1038,10 @@ class NSTrainer:
         cs = torch.cuda.current_stream(self.device)
         G, n = self.ahead, len(self.slots)
         self._side.wait_stream(cs)
-        # the model's launches first (captured first: the graph runs them on the launch queue)
         align = SUMS_ALIGN["mode"] != "off"
         ends = []
-        for i in range(m):
+
+        def model(i):
             self._fs_step(self.fused_slots[(start + i) % n])
             if in_graph:
                 self._exchange()
@@ -1021,13 +1050,25 @@ class NSTrainer:
                 ev = torch.cuda.Event()
                 ev.record(cs)
                 ends.append(ev)
-        with torch.cuda.stream(self._side):
-            for i in range(m):
+
+        def sampler(i):
+            with torch.cuda.stream(self._side):
                 # batch i's outer-hop sums (the sampler's one heavy launch) wait for the end of
                 # model step i - 1, so they run beside step i's agg0 / head (which they slow
                 # little) instead of its gather / bwd0 / finalize (2-4x slower beside them)
                 wait = (lambda e=ends[i - 1]: self._side.wait_event(e)) if align and i else None
                 self._sample((start + G + i) % n, before_sums=wait)
+
+        if GROUP_ORDER["mode"] == "interleave":
+            for i in range(m):
+                model(i)
+                sampler(i)
+        else:
+            # the model's launches first (captured first: the graph runs them on the launch queue)
+            for i in range(m):
+                model(i)
+            for i in range(m):
+                sampler(i)
         cs.wait_stream(self._side)
 
     def _group_sizes(self):
@@ -1102,6 +1143,16 @@ class NSTrainer:
         # accumulate with one add kernel per parameter, and _foreach_copy_ / _foreach_add_
         # lower to a kernel per tensor here: ~90 us per step at hidden 512)
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        # the bucket is zeroed once (above), so a parameter that had a gradient on an earlier
+        # step and has none now would keep the stale one: zero exactly those views (the set is
+        # the same every step for a fixed model, so this is a host-side set compare only)
+        had = getattr(self, "_had_grad", None)
+        now = frozenset(i for i, g in enumerate(grads) if g is not None)
+        if had is not None and not had <= now:
+            with torch.no_grad():
+                for i in had - now:
+                    self.params[i].grad.zero_()
+        self._had_grad = now                  # the views holding a (possibly) non-zero gradient
         with torch.no_grad():
             # (the loss rides in the same launch: no copy of its own)
             dst = [p.grad for p, g in zip(self.params, grads) if g is not None] + [self.loss]
@@ -1434,4 +1485,12 @@ class NSTrainer:
     def edges_total(self):
         """aggregated edges of every batch sampled so far (device counters: one host sync;
         pipelined, that includes the batch sampled ahead)."""
-        return int(sum(int(s.state[5].item()) for s in self.slots))
+        # one host sync: the slots' edge counters and (the sampler's own failure report riding
+        # on it) every slot's transposed-index error words
+        words = torch.cat([torch.stack([s.state[5] for s in self.slots]).sum().reshape(1)] +
+                          [s.index_errors().to(torch.int64) for s in self.slots]).cpu().tolist()
+        if any(words[1:]):
+            bad = [i for i, s in enumerate(self.slots) if any(s.index_errors().cpu().tolist())]
+            raise RuntimeError(f"regnn_ns_hop: a transposed index build timed out waiting for its "
+                               f"publish (sampler slots {bad}): those batches are incomplete")
+        return int(words[0])

@@ -150,6 +150,8 @@ class FakeTrainer:
     def _forward_backward(self):
         self.flat.mul_(1.5)
         if rank == 1 and self.steps == int(os.environ["FAIL_AT"]):
+            if os.environ.get("FAIL_MODE") == "die":
+                os._exit(9)                              # a hard death: no agreement from it
             raise RuntimeError("injected failure inside the warm-up step")
 
     def _exchange(self):
@@ -169,7 +171,7 @@ dist.destroy_process_group()
 """
 
 
-def _run_two_ranks(fail_at, timeout_s=20):
+def _run_two_ranks(fail_at, timeout_s=20, mode="raise"):
     import subprocess
     import sys
     import time
@@ -179,7 +181,7 @@ def _run_two_ranks(fail_at, timeout_s=20):
     t0 = time.time()
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), REGNN_ROOT=root, FAIL_AT=str(fail_at),
+                   MASTER_PORT=str(port), REGNN_ROOT=root, FAIL_AT=str(fail_at), FAIL_MODE=mode,
                    REGNN_DIST_TIMEOUT=str(timeout_s))
         procs.append(subprocess.Popen([sys.executable, "-c", _FAIL_WORKER], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -206,6 +208,18 @@ def test_rank_failure_in_warmup_ends_every_rank():
     assert "injected failure" in outs[1][2]
     assert all("finished" not in o for _, o, _ in outs)
     assert dt < 20, dt                                 # agreement, not the timeout, ended it
+
+
+def test_peer_death_ends_the_survivor_with_exit_code():
+    """rank 1 dies without reaching the agreement (os._exit inside the step); rank 0's
+    exchange and then its agreement all-reduce fail, and the guarded agreement turns that into
+    RankFailure: rank 0 exits guard.EXIT_CODE (not a plain RuntimeError traceback), in time."""
+    from regnn_hip.guard import EXIT_CODE
+    outs, dt = _run_two_ranks(fail_at=1, mode="die")
+    codes = [rc for rc, _, _ in outs]
+    assert codes == [EXIT_CODE, 9], (codes, [e[-600:] for _, _, e in outs])
+    assert "finished" not in outs[0][1]
+    assert dt < 60, dt
 
 
 def test_no_failure_both_ranks_finish():

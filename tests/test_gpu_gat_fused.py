@@ -222,3 +222,76 @@ def test_gatv2_long_rows_vs_fp64(global_max):
     for name, x, w in zip(["out", "g_fs", "g_fd", "g_att", "g_tab", "g_ft"], got, want):
         err = (x.double() - w).abs().max().item() / _rel(w)
         assert err <= 1e-5, f"{name}: rel err {err:.3e}"
+
+
+def _single_chunk_graph(N=3000, E=30000, R=7, seed=4):
+    """long rows that are each ONE chunk on both sides (split 32 < degree <= chunk 256): the plan
+    has chunks but no tree levels (n_levels == 0), its final rows the chunk rows themselves."""
+    from regnn_hip.graph import RelGraph
+    rng = np.random.default_rng(seed)
+    dst = rng.integers(0, N, E)
+    src = rng.integers(0, N, E)
+    hubs = rng.choice(N, 40, replace=False)
+    hd = np.repeat(hubs[:20], 150)                      # 20 destinations with 150+ in-edges
+    hs = np.repeat(hubs[20:], 170)                      # 20 sources with 170+ out-edges
+    src = np.concatenate([src, rng.integers(0, N, hd.size), hs])
+    dst = np.concatenate([dst, hd, rng.integers(0, N, hs.size)])
+    rel = rng.integers(1, R + 1, src.size)
+    keep = np.arange(N)
+    src = np.concatenate([src, keep]); dst = np.concatenate([dst, keep])
+    rel = np.concatenate([rel, np.full(N, R)])
+    rg = RelGraph(src, dst, N, DEV, split=32, chunk=256)
+    return rg, torch.from_numpy(rel).to(DEV)
+
+
+@pytest.mark.parametrize("kind", ["gat_fused", "gat", "gatv2"])
+def test_attention_single_chunk_long_rows_vs_fp64(kind):
+    """a plan whose long segments are one chunk each (n_levels == 0) runs -- the GAT /
+    GATv2 score, softmax and aggregation kernels read the chunk rows as the final rows -- and
+    matches the fp64 restatement at 1e-5, forward and every gradient."""
+    from regnn_hip import ops
+    rg, e_feat = _single_chunk_graph()
+    for plan in (rg.csr_plan, rg.csc_plan):
+        assert plan.n_long > 0 and plan.n_chunk == plan.n_long and plan.n_levels == 0
+    N = rg.n_dst
+    g = torch.Generator(device=DEV).manual_seed(9)
+    pack = rg.rel_pack(e_feat, num_rel=7)
+    if kind.startswith("gat") and kind != "gatv2":
+        H, D = 4, 16
+        ft0 = torch.randn(N, H, D, generator=g, device=DEV)
+        el0 = torch.randn(N, H, generator=g, device=DEV)
+        er0 = torch.randn(N, H, generator=g, device=DEV)
+        tab0 = torch.randn(7, H, generator=g, device=DEV) * 0.5
+        gy = torch.randn(N, H, D, generator=g, device=DEV)
+        ft, el, er, tab = (t.clone().requires_grad_(True) for t in (ft0, el0, er0, tab0))
+        if kind == "gat_fused":
+            y = ops.gat_fused(rg, el, er, ft, tab, pack, 0.2)
+        else:
+            y = ops.head_spmm(rg, ops.gat_attention(rg, el, er, tab, pack, 0.2), ft)
+        y.backward(gy)
+        got = [y.detach(), ft.grad, el.grad, er.grad, tab.grad]
+        ref_in = [t.double().clone().requires_grad_(True) for t in (el0, er0, tab0, ft0)]
+        yr = _gat_reference(rg, pack.rel_csr, *ref_in, 0.2)
+        yr.backward(gy.double())
+        want = [yr.detach(), ref_in[3].grad, ref_in[0].grad, ref_in[1].grad, ref_in[2].grad]
+    else:
+        H, D = 4, 16
+        fs0 = torch.randn(N, H, D, generator=g, device=DEV) * 0.5
+        fd0 = torch.randn(N, H, D, generator=g, device=DEV) * 0.5
+        att0 = torch.randn(1, H, D, generator=g, device=DEV) * 0.3
+        tab0 = torch.randn(7, H, generator=g, device=DEV) * 0.5
+        ft0 = torch.randn(N, H, D, generator=g, device=DEV)
+        gy = torch.randn(N, H, D, generator=g, device=DEV)
+        fs, fd, att, tab, ft = (t.clone().requires_grad_(True)
+                                for t in (fs0, fd0, att0, tab0, ft0))
+        s = ops.gatv2_scores(rg, fs, fd, att, 0.2)
+        y = ops.head_spmm(rg, ops.edge_softmax_logits(rg, s, tab, pack, False), ft)
+        y.backward(gy)
+        got = [y.detach(), fs.grad, fd.grad, att.grad, tab.grad, ft.grad]
+        ref_in = [t.double().clone().requires_grad_(True) for t in (fs0, fd0, att0, tab0, ft0)]
+        yr = _gatv2_reference(rg, pack.rel_csr, *ref_in, 0.2, False)
+        yr.backward(gy.double())
+        want = [yr.detach()] + [t.grad for t in ref_in]
+    for i, (x, w) in enumerate(zip(got, want)):
+        err = (x.double() - w).abs().max().item() / _rel(w)
+        assert err <= 1e-5, f"{kind} output {i}: rel err {err:.3e}"

@@ -749,6 +749,57 @@ def test_block_transposed_index():
     assert cl[0] == longs.size and longs.size > 0 and np.array_equal(cl[1:1 + cl[0]], longs)
 
 
+def test_transposed_index_after_csr_batches():
+    """batches in the CSR layout (exact_adjs, the module path) and in the
+    strided layout alternating on one sampler. The strided index's control words (ticket,
+    published stamp, error word) lie past the CSR de-duplication's tile words, so a tile count a
+    CSR batch leaves behind cannot pass for the publish: here the old publish word (tiles[1]) is
+    even set to the coming hop's stamp before each strided batch. Every batch's index equals the
+    block's transposed multiset and the error word stays 0."""
+    from regnn_hip.graph import RelGraph
+    from regnn_hip.ns import DeviceSampler
+    rng = np.random.default_rng(13)
+    N, E = 5000, 80000
+    dst = np.minimum((rng.pareto(1.1, E) * 4).astype(np.int64), N - 1)
+    src = np.where(rng.random(E) < 0.6, rng.integers(0, 3, E), rng.integers(0, N, E))
+    rg = RelGraph(src, dst, N, DEV)
+    ds = DeviceSampler(rg, [12, 5], 150, etype=torch.from_numpy(rng.integers(0, 7, E)),
+                       ntype=torch.from_numpy(rng.integers(0, 4, N)), num_edge_types=7)
+    _, cptr, cent, clong = ds.enable_csc(0)
+    assert ds.hop_bufs[0]["tiles"].numel() >= 2 + 4     # two flag tiles: tiles[1] a tile word
+    for it, strided in enumerate([False, True, False, True, True]):
+        ds.set_seed(5, 0, it)
+        ds.set_targets(torch.from_numpy(rng.permutation(N)[:150]).to(DEV))
+        if strided:
+            ds.hop_bufs[0]["tiles"][1] = int(ds.state[4].item()) * 8 + 1   # hop 0's stamp
+        ds.run_hops(strided=strided)
+        sz = ds.sizes.cpu().tolist()
+        n_dst, n_src = sz[0], sz[1]
+        blk = ds.blocks[0]
+        if strided:
+            S = ds.sizes_k[0] + 1
+            cnt = ds.hop_bufs[0]["scnt"][:n_dst].cpu().numpy()
+            pos = np.concatenate([np.arange(i * S, i * S + cnt[i] + 1) for i in range(n_dst)])
+        else:
+            pos = np.arange(int(blk.csr_ptr[n_dst].item()))
+        pos_t = torch.from_numpy(pos).to(DEV)
+        idx = blk.csr_idx[pos_t].cpu().numpy()
+        rel = blk.rel[pos_t].cpu().numpy().astype(np.int64)
+        row = blk.row[pos_t].cpu().numpy()
+        Eb = pos.size
+        assert sz[8] == Eb
+        cp = cptr[:n_src + 1].cpu().numpy()
+        ce = cent[:Eb].cpu().numpy().astype(np.int64)
+        assert cp[0] == 0 and cp[-1] == Eb and np.all(np.diff(cp) >= 1), (it, strided)
+        want = [[] for _ in range(n_src)]
+        for bp in range(Eb):
+            want[idx[bp]].append((int(row[bp]) << 8) | int(rel[bp]))
+        for u in range(n_src):
+            assert sorted(ce[cp[u]:cp[u + 1]].tolist()) == sorted(want[u]), (it, strided, u)
+        assert not any(ds.index_errors().cpu().tolist())
+    ds.check_index()
+
+
 @pytest.mark.parametrize("half_waves,csc_fuse", [("0", "on"), ("1", "on"), ("0", "off")])
 def test_strided_blocks_match_csr(monkeypatch, half_waves, csc_fuse):
     """regnn_ns_hop strided (the fused engine's fixed-stride blocks: sampling and placement in one
