@@ -483,12 +483,19 @@ CSC_FUSE = {"mode": os.environ.get("REGNN_NS_CSC_FUSE", "off")}
 # 0.9 GiB more HBM than 2.
 # Round 5 (one rank, 300-step runs): G = 8 107.4-108.4, 16 106.5-108.3, 32 105.6-106.0 us (a
 # fork / join per group). Default: 32 with one rank; 8 with several (every captured group holds
-# one RCCL all-reduce per step, and that capture was only rehearsed at 8); REGNN_NS_AHEAD wins
+# one RCCL all-reduce per step, and that capture was only rehearsed at 8); REGNN_NS_AHEAD wins.
+# Round 6: a timed run starts from an idle GPU (after a synchronisation), and a replay's nodes
+# reach the queues only as fast as the host enqueues them, so the first group of a run sets how
+# late the sampler's queue starts. With a 4-step lead group (PLAN_ORDER "lead4") the 20-step run
+# the driver times measured (6 x 20 steps, medians): G = 32 desc 117.8, G = 32 lead4 114.2,
+# G = 8 desc 114.0, G = 16 lead4 109.2-110.4 us per step; 160-step runs 106.0 / 105.4 (G = 32
+# desc / lead4) against 106.4 (G = 16 lead4). Default: 16 with one rank (32 slots: half the
+# lookahead memory of 32)
 AHEAD = {"steps": int(os.environ["REGNN_NS_AHEAD"]) if "REGNN_NS_AHEAD" in os.environ else None}
 
 
 def default_ahead(world):
-    return AHEAD["steps"] if AHEAD["steps"] is not None else (32 if world == 1 else 8)
+    return AHEAD["steps"] if AHEAD["steps"] is not None else (16 if world == 1 else 8)
 # "on" (default): inside a lookahead group, the sampler's outer-hop sums launch for the group's
 # batch i waits for the end of model step i - 1 (a model -> sampler edge only: the model never
 # waits), placing it beside step i's agg0 / head; "off": the sampler runs free
@@ -504,9 +511,8 @@ LEAN_LAST_HOP = {"mode": "on"}
 # agg0 reads them (regnn_nsm_work.pre_sums); "off": agg0 gathers the raw rows itself (A/B, tests)
 PRE_SUMS = {"mode": os.environ.get("REGNN_NS_PRE_SUMS", "on")}
 # capture order of a lookahead group's launches: "model" (every model step, then every sampler
-# batch) or "interleave" (model step i, then sampler batch i): the same dependency edges, but the
-# runtime enqueues a replay's nodes in capture order, so with "model" the sampler's first launch
-# reaches its queue only after the host has enqueued the whole model chain
+# batch) or "interleave" (model step i, then sampler batch i): the same dependency edges; measured
+# (round 6, 20-step runs) within run-to-run spread of each other, so "model" stays
 GROUP_ORDER = {"mode": os.environ.get("REGNN_NS_GROUP_ORDER", "model")}
 
 
@@ -728,18 +734,51 @@ def group_sizes(ahead):
     return out
 
 
-def plan_run(cur, k, ahead, n_slots, have=lambda m, start: True):
-    """the replays NSTrainer.run_steps issues for k steps from slot `cur` at lookahead `ahead`
-    > 1: [(m, start)], m = 1 for a one-step graph; the longest captured group (`have`) that
-    fits the remaining steps, from wherever cur stands."""
+# the order of a run's replays (plan_run): "desc" (the longest group first, as the greedy split
+# finds them), "asc" (shortest first) or "leadL" (a group of L first, then the rest longest
+# first). A replay's nodes reach the GPU queues while the host enqueues them; after an idle GPU
+# (every timed run starts after a synchronisation) a short first group starts the sampler's
+# queue early while the host enqueues the long groups behind it
+PLAN_ORDER = {"mode": os.environ.get("REGNN_NS_PLAN", "lead4")}
+
+
+def _split(k, ahead):
+    """k steps as group lengths, longest first (group_sizes(ahead), ones for the rest)."""
     out = []
     while k > 0:
         m = next((m for m in group_sizes(ahead) if m <= k), 1)
+        out.append(m)
+        k -= m
+    return out
+
+
+def plan_sizes(k, ahead, order=None):
+    """the group lengths plan_run replays for k steps, in order (PLAN_ORDER)."""
+    order = order or PLAN_ORDER["mode"]
+    sizes = _split(k, ahead)
+    if order == "asc":
+        return sorted(sizes)
+    if order.startswith("lead"):
+        lead = int(order[4:])
+        if lead in group_sizes(ahead) and k > lead and sizes[0] > lead:
+            return [lead] + _split(k - lead, ahead)
+    return sizes
+
+
+def plan_run(cur, k, ahead, n_slots, have=lambda m, start: True, order=None):
+    """the replays NSTrainer.run_steps issues for k steps from slot `cur` at lookahead `ahead`
+    > 1: [(m, start)], m = 1 for a one-step graph; the captured groups (`have`) of the greedy
+    split of k into group lengths, in PLAN_ORDER's order, from wherever cur stands (a group
+    without a captured graph runs as one-step graphs)."""
+    out = []
+    for m in plan_sizes(k, ahead, order):
         if m > 1 and not have(m, cur):
-            m = 1
+            for _ in range(m):
+                out.append((1, cur))
+                cur = (cur + 1) % n_slots
+            continue
         out.append((m, cur))
         cur = (cur + m) % n_slots
-        k -= m
     return out
 
 

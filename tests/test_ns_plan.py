@@ -37,21 +37,31 @@ def _simulate(ahead, plan, cur):
     return cur
 
 
+@pytest.mark.parametrize("order", ["desc", "asc", "lead4", "lead2"])
 @pytest.mark.parametrize("ahead", [2, 4, 8])
-def test_plan_run_keeps_the_sampled_window(ahead):
+def test_plan_run_keeps_the_sampled_window(ahead, order):
     n = 2 * ahead
     for cur, k in itertools.product(range(n), range(1, 3 * n + 2)):
-        plan = plan_run(cur, k, ahead, n)
+        plan = plan_run(cur, k, ahead, n, order=order)
         assert sum(m for m, _ in plan) == k
         assert all(m == 1 or m in group_sizes(ahead) for m, _ in plan)
-        assert len(plan) <= k // ahead + len(group_sizes(ahead)) + 1
+        assert len(plan) <= k // ahead + len(group_sizes(ahead)) + 2
         end = _simulate(ahead, plan, cur)
         assert end == (cur + k) % n
 
 
 def test_plan_run_without_a_group_falls_back_to_single_steps():
-    plan = plan_run(3, 8, 8, 16, have=lambda m, c: c != 3)
+    plan = plan_run(3, 8, 8, 16, have=lambda m, c: c != 3, order="desc")
     assert plan[0] == (1, 3) and plan[1][1] == 4 and sum(m for m, _ in plan) == 8
+
+
+def test_plan_orders():
+    from regnn_hip.ns import plan_sizes
+    assert plan_sizes(20, 32, "desc") == [16, 4]
+    assert plan_sizes(20, 32, "asc") == [4, 16]
+    assert plan_sizes(20, 32, "lead4") == [4, 16]
+    assert plan_sizes(160, 32, "lead4") == [4, 32, 32, 32, 32, 16, 8, 4]
+    assert plan_sizes(3, 32, "lead4") == [2, 1]
 
 
 @pytest.mark.parametrize("ahead", [2, 4, 8])

@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seq", default="20,20,20,160,20")
     ap.add_argument("--sweep", default="", help="group lengths m: T(m) median/min of 7 runs")
-    ap.add_argument("--pre", default="none", help="sweep preambles: none,spin,spin_sync")
+    ap.add_argument("--pre", default="none", help="sweep preambles: none,spin,spin_sync,sleep,self")
     a0 = ap.parse_args()
     args = argparse.Namespace(scale=10.0, zipf=1.1, hidden=64, dropout=0.5, batch=512)
     dev = torch.device("cuda", 0)
@@ -46,6 +46,10 @@ def main():
                     spin()
                 if pre == "spin_sync":
                     torch.cuda.synchronize()
+                if pre == "sleep":             # 20 ms of GPU idle before the run
+                    time.sleep(0.02)
+                if pre == "self":               # our own steps in flight (no sync) before it
+                    tr.run_steps(16)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
                 tr.run_steps(m)
