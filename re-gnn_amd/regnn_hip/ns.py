@@ -63,10 +63,12 @@ class DeviceSampler:
     ntype: node type per global node (self-loop relation num_edge_types + ntype), or None."""
 
     def __init__(self, rg, sizes, batch_size, etype=None, ntype=None, num_edge_types=0,
-                 share=None):
+                 share=None, share_dedup=None):
         """share: another DeviceSampler over the same graph whose read-only tables (edge and
         node types) and dedup tables are reused (a second pipeline slot: the two never sample
-        at the same time, and their dedup stamps never coincide)."""
+        at the same time, and their dedup stamps never coincide). share_dedup: the sampler whose
+        dedup tables to reuse instead (default: share); False: tables of its own (a slot that
+        may sample at the same time as share, on another stream)."""
         dev = rg.device
         self.rg, self.device = rg, dev
         self.sizes_k = [int(k) for k in sizes]
@@ -103,12 +105,13 @@ class DeviceSampler:
         self.state = torch.zeros(8, dtype=torch.int64, device=dev)
         self.sizes = torch.zeros(16, dtype=torch.int32, device=dev)
         self.n_id = torch.zeros(caps[-1], dtype=torch.int32, device=dev)
-        if share is not None:
+        dd = share if share_dedup is None else share_dedup
+        if dd:
             # one stamp counter for both: the dedup tables need increasing stamps
-            self.g2l, self.first = share.g2l, share.first
-            if share.stamp_src is None:
-                share.stamp_src = share.state[4:5].clone()
-            self.stamp_src = share.stamp_src
+            self.g2l, self.first = dd.g2l, dd.first
+            if dd.stamp_src is None:
+                dd.stamp_src = dd.state[4:5].clone()
+            self.stamp_src = dd.stamp_src
         else:
             self.g2l = torch.zeros(n_nodes, dtype=torch.int64, device=dev)
             self.first = torch.full((n_nodes,), -1, dtype=torch.int64, device=dev)
@@ -496,10 +499,18 @@ AHEAD = {"steps": int(os.environ["REGNN_NS_AHEAD"]) if "REGNN_NS_AHEAD" in os.en
 
 def default_ahead(world):
     return AHEAD["steps"] if AHEAD["steps"] is not None else (16 if world == 1 else 8)
-# "on" (default): inside a lookahead group, the sampler's outer-hop sums launch for the group's
-# batch i waits for the end of model step i - 1 (a model -> sampler edge only: the model never
-# waits), placing it beside step i's agg0 / head; "off": the sampler runs free
-SUMS_ALIGN = {"mode": os.environ.get("REGNN_NS_SUMS_ALIGN", "on")}
+# "on": inside a lookahead group, the sampler's outer-hop sums launch for the group's batch i
+# waits for the end of model step i - 1 (a model -> sampler edge only: the model never waits),
+# placing it beside step i's agg0 / head; N (default 2): only every N-th batch (each edge costs a
+# marker on the model's queue, ~4 us of idle before the next agg0; 6 x 20-step runs: on 111.0,
+# 2 110.1, 4 110.2 us; 160 steps 106.2 / 105.5 / 105.5); "off": the sampler runs free
+SUMS_ALIGN = {"mode": os.environ.get("REGNN_NS_SUMS_ALIGN", "2")}
+# parallel sampler lanes inside a lookahead group (REGNN_NS_SAMPLER_LANES): L streams, slot s on
+# lane s mod L with dedup tables of its own lane (L x 16 B per node of HBM). Measured (round 6):
+# L = 1 / 2 / 4 at 20 steps 110.6 / 116.0 / 133.0, at 160 steps 105.3 / 112.4 / 137.9 us per step
+# -- more sampler work at once slows the model's kernels more than the shorter sampler chain
+# saves; 1 stays
+SAMPLER_LANES = {"n": int(os.environ.get("REGNN_NS_SAMPLER_LANES", "1"))}
 # "on": the module path's last hop runs meta-only when the model's layer 0 is the typed first
 # layer (mag.REGNN.typed_first_layer_ok); "off": the full hop (A/B, tests)
 MODULE_LEAN_HOP = {"mode": os.environ.get("REGNN_NS_MODULE_LEAN", "on")}
@@ -940,11 +951,19 @@ class NSTrainer:
         # the sampling lookahead (fused engine; the module path samples one batch ahead)
         self.ahead = (max(1, int(default_ahead(self.world))) if self.pipelined and
                       self.fused is not None else 1)
+        # parallel sampler lanes (lookahead groups): slot s samples on lane s mod L with that
+        # lane's own dedup tables, so L batches of a group sample at the same time on L streams
+        self.lanes = (max(1, int(SAMPLER_LANES["n"])) if self.pipelined and self.fused is not None
+                      and self.ahead > 1 else 1)
+        if self.lanes > 1 and (2 * self.ahead) % self.lanes:
+            raise ValueError(f"{self.lanes} sampler lanes must divide the {2 * self.ahead} slots")
         if self.pipelined:
-            for _ in range(2 * self.ahead - 1):
-                self.slots.append(DeviceSampler(rg, sizes, batch_size,
-                                                num_edge_types=num_edge_types,
-                                                share=self.slots[0]))
+            for j in range(1, 2 * self.ahead):
+                lane = j % self.lanes
+                self.slots.append(DeviceSampler(
+                    rg, sizes, batch_size, num_edge_types=num_edge_types, share=self.slots[0],
+                    share_dedup=(False if j == lane else self.slots[lane]) if self.lanes > 1
+                    else None))
             if self.fused is not None:
                 self.fused_slots = [self.fused] + [
                     FusedStep(model, s, x_dict, node_type, local_node_idx, self.y_flat, self.loss)
@@ -954,6 +973,8 @@ class NSTrainer:
             # the sampler's stream; REGNN_NS_SIDE_PRIORITY (-1: high) for A/B runs
             self._side = torch.cuda.Stream(device=dev,
                                            priority=int(os.environ.get("REGNN_NS_SIDE_PRIORITY", "0")))
+            self._sides = [self._side] + [torch.cuda.Stream(device=dev)
+                                          for _ in range(self.lanes - 1)]
             if self.fused is not None and CSC_FORK["mode"] != "off":
                 self._csc = torch.cuda.Stream(device=dev)
         # one rank, FlatAdam, two-layer step: the optimizer runs inside the step's last launch
@@ -1076,27 +1097,36 @@ class NSTrainer:
         trained last) on the second one; one fork before, one join after."""
         cs = torch.cuda.current_stream(self.device)
         G, n = self.ahead, len(self.slots)
-        self._side.wait_stream(cs)
-        align = SUMS_ALIGN["mode"] != "off"
-        ends = []
+        for sd in self._sides:
+            sd.wait_stream(cs)
+        # "on": every step; an integer N: the sums of batches i = N, 2N, .. only (each event
+        # record is a marker on the model's queue: ~4 us of queue idle between finalize and the
+        # next agg0, measured in a kernel trace); "off": never
+        mode = SUMS_ALIGN["mode"]
+        every = 0 if mode == "off" else (1 if mode == "on" else int(mode))
+        align = every > 0
+        ends = {}
 
         def model(i):
             self._fs_step(self.fused_slots[(start + i) % n])
             if in_graph:
                 self._exchange()
             self._opt_step()
-            if align and i + 1 < m:
+            if align and i + 1 < m and (i + 1) % every == 0:
                 ev = torch.cuda.Event()
                 ev.record(cs)
-                ends.append(ev)
+                ends[i] = ev
 
         def sampler(i):
-            with torch.cuda.stream(self._side):
+            slot = (start + G + i) % n
+            sd = self._sides[slot % self.lanes]
+            with torch.cuda.stream(sd):
                 # batch i's outer-hop sums (the sampler's one heavy launch) wait for the end of
                 # model step i - 1, so they run beside step i's agg0 / head (which they slow
                 # little) instead of its gather / bwd0 / finalize (2-4x slower beside them)
-                wait = (lambda e=ends[i - 1]: self._side.wait_event(e)) if align and i else None
-                self._sample((start + G + i) % n, before_sums=wait)
+                wait = ((lambda e=ends[i - 1], sd=sd: sd.wait_event(e))
+                        if align and i and (i - 1) in ends else None)
+                self._sample(slot, before_sums=wait)
 
         if GROUP_ORDER["mode"] == "interleave":
             for i in range(m):
@@ -1108,7 +1138,8 @@ class NSTrainer:
                 model(i)
             for i in range(m):
                 sampler(i)
-        cs.wait_stream(self._side)
+        for sd in self._sides:
+            cs.wait_stream(sd)
 
     def _group_sizes(self):
         return group_sizes(self.ahead)
