@@ -165,7 +165,10 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
     const int64_t m0 = int64_t(blockIdx.y) * BM, n0 = int64_t(blockIdx.x) * BN;
     const int z = blockIdx.z, S = gridDim.z;
     const int64_t Ke = k_live ? min(K, int64_t(*k_live)) : K;
-    const int64_t nk = (m_live && m0 >= int64_t(*m_live)) ? 0 : (Ke + BK - 1) / BK;
+    const bool dead = m_live && m0 >= int64_t(*m_live);
+    // split-K: a dead row tile writes no partial (gemm_reduce_kernel skips the rows past m_live)
+    if (dead && gridDim.z > 1) return;
+    const int64_t nk = dead ? 0 : (Ke + BK - 1) / BK;
     const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
     const int wr = w >> 1, wc = w & 1;
     const int NI = wave_tiles(m0 + 64 * wr, M), NJ = wave_tiles(n0 + 64 * wc, N);
@@ -221,13 +224,21 @@ gemm_x6_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int
         }
 }
 
-// C = sum_z work[z] (in split order) + beta C
+// C = sum_z work[z] (in split order) + beta C; rows past m_live (may be null) are beta C (the
+// partials hold nothing there)
 __global__ void __launch_bounds__(kThreads)
 gemm_reduce_kernel(int64_t M, int64_t N, const float* __restrict__ work, int S, float* __restrict__ C,
-                   int64_t ldc, float beta) {
+                   int64_t ldc, float beta, const int32_t* __restrict__ m_live) {
     const int64_t total = M * N;
+    const int64_t live = m_live ? min(M, int64_t(*m_live)) * N : total;
     for (int64_t e = int64_t(blockIdx.x) * kThreads + threadIdx.x; e < total;
          e += int64_t(gridDim.x) * kThreads) {
+        if (e >= live) {
+            const int64_t m = e / N, n = e - m * N;
+            float* o = C + m * ldc + n;
+            *o = beta != 0.f ? beta * *o : 0.f;
+            continue;
+        }
         // the splits' loads 8 at a time in flight (clamped addresses, unconditional), added in
         // split order (the same bits as one load and add per split)
         float s = work[e];
@@ -309,7 +320,7 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
         int64_t blocks = (M * N + kThreads - 1) / kThreads;
         if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, stream, M,
-                           N, work, splits, C, ldc, beta);
+                           N, work, splits, C, ldc, beta, m_live);
         REGNN_LAUNCH_CHECK();
     }
     return REGNN_OK;

@@ -505,6 +505,11 @@ def default_ahead(world):
 # marker on the model's queue, ~4 us of idle before the next agg0; 6 x 20-step runs: on 111.0,
 # 2 110.1, 4 110.2 us; 160 steps 106.2 / 105.5 / 105.5); "off": the sampler runs free
 SUMS_ALIGN = {"mode": os.environ.get("REGNN_NS_SUMS_ALIGN", "2")}
+# "on": the module path sizes its GEMMs' split-K for the first batch's live rows (ops.LIVE_HINT:
+# ~6 k of the 13312-row capacity at mag-10x, split 2 with a reduce); measured at hidden 512 (3 x
+# 20 steps): 578.2 against 563.0 us per step without -- the reduce costs more than the shorter
+# k-chains save; off by default (REGNN_NS_GEMM_LIVE_HINT=on)
+GEMM_LIVE_HINT = {"mode": os.environ.get("REGNN_NS_GEMM_LIVE_HINT", "off")}
 # parallel sampler lanes inside a lookahead group (REGNN_NS_SAMPLER_LANES): L streams, slot s on
 # lane s mod L with dedup tables of its own lane (L x 16 B per node of HBM). Measured (round 6):
 # L = 1 / 2 / 4 at 20 steps 110.6 / 116.0 / 133.0, at 160 steps 105.3 / 112.4 / 137.9 us per step
@@ -1177,6 +1182,17 @@ class NSTrainer:
 
     def _module_step(self, s):
         """the mag.REGNN autograd forward / nll / backward on sampler slot s's batch."""
+        if (self._blocks_ok and GEMM_LIVE_HINT["mode"] == "on" and
+                not getattr(self, "_live_hinted", False) and
+                not torch.cuda.is_current_stream_capturing()):
+            # the GEMMs' split-K sized for the live rows of a typical block (one host read of
+            # the first batch's sizes, eager, before any capture): ops.LIVE_HINT
+            from . import ops
+            torch.cuda.current_stream(self.device).synchronize()
+            sz = s.sizes.cpu().tolist()
+            for h in range(1, len(s.caps) - 1):
+                ops.set_live_hint(s.caps[h], sz[h])
+            self._live_hinted = True
         # the bucket zeroed once: every step overwrites each gradient the forward produces, and
         # a parameter the forward never reads (allow_unused) keeps the zeros (no fill per step)
         if not getattr(self, "_flat_zeroed", False):

@@ -1675,9 +1675,23 @@ GEMM_X6 = {"mode": os.environ.get("REGNN_GEMM_X6", "on")}
 _SPLIT_TARGET = int(os.environ.get("REGNN_GEMM_SPLIT_TARGET", "512"))
 
 
+# typical live rows of a capacity-sized operand: LIVE_HINT[M] = rows (set_live_hint; the NS
+# trainer's module path sets it from its first batch when ns.GEMM_LIVE_HINT is on -- measured
+# slower, off by default). The split-K factor of every GEMM with M rows is chosen for that many
+# rows (the dead row tiles the kernel skips leave much of the chip idle: 13312-row capacity, ~6 k
+# live rows at mag-10x), whether or not the call passes m_live, so a product's summation order
+# depends on M alone; with split-K the dead row tiles write no partial and the reduce skips them
+LIVE_HINT = {}
+
+
+def set_live_hint(capacity_rows, rows):
+    LIVE_HINT[int(capacity_rows)] = max(1, min(int(capacity_rows), int(rows)))
+
+
 def _gemm_splits(M, N, K):
     """split-K factor: about two 128 x 128 tiles per CU for a small output over a long
-    reduction (each split keeps >= 4 k-steps of 32)."""
+    reduction (each split keeps >= 4 k-steps of 32); M at its live-row hint (LIVE_HINT)."""
+    M = LIVE_HINT.get(M, M)
     tiles = -(-M // 128) * -(-N // 128)
     nk = -(-K // 32)
     if tiles >= 256 or nk < 8:

@@ -144,12 +144,19 @@ def test_copy_many_strided_sources():
         assert torch.equal(d, s_)
 
 
+@pytest.mark.parametrize("hint", [None, 6100])
 @pytest.mark.parametrize("live", [0, 1, 127, 128, 5606, 13312])
-def test_mm_live_rows_bitwise(live):
+def test_mm_live_rows_bitwise(live, hint, monkeypatch):
     """ops.mm with a live-row count (the capacity-sized block's rows past it are zero): the
     forward and both gradients bitwise those of the full GEMMs on the same zero-padded operands
-    (the skipped products are exact zeros), the output's dead rows equal to c's."""
+    (the skipped products are exact zeros), the output's dead rows equal to c's. hint: the
+    trainer's typical live rows for this capacity (ops.LIVE_HINT): the 13312-row products split
+    K in two (the dead row tiles write no partial, the reduce skips their rows) with and without
+    the live count alike; against fp64 at 1e-5 too."""
     from regnn_hip import ops
+    monkeypatch.setattr(ops, "LIVE_HINT", {} if hint is None else {13312: hint})
+    if hint is not None:
+        assert ops._gemm_splits(13312, 512, 516) == 2
     g = torch.Generator(device=DEV).manual_seed(11)
     M, K, N = 13312, 516, 512
     a0 = torch.randn(M, K, generator=g, device=DEV)
@@ -167,3 +174,9 @@ def test_mm_live_rows_bitwise(live):
         outs.append([y.detach(), a.grad, b.grad, c.grad])
     for name, x, y in zip(["out", "g_a", "g_b", "g_c"], outs[0], outs[1]):
         assert torch.equal(x, y), name
+    ref = c0.double() + a0.double() @ b0.double()
+    err = (outs[1][0].double() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert err <= 1e-5, err
+    ga = gout.double() @ b0.double().t()
+    err = (outs[1][1].double() - ga).abs().max().item() / max(1.0, ga.abs().max().item())
+    assert err <= 1e-5, err
