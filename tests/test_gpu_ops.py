@@ -110,11 +110,14 @@ def test_col_sum(rows, cols):
 
 
 @pytest.mark.parametrize("rows,width", [(2048, 22880), (300, 8256), (255, 5000), (2048, 4096),
-                                        (1000, 4095), (33, 9000)])
+                                        (1000, 4095), (33, 9000),
+                                        # narrow: relation tables over 4096 rows
+                                        (4096, 11), (4096, 16), (4096, 17), (4096, 32), (5000, 1),
+                                        (3, 14), (4096, 33)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_rel_reduce_wide(rows, width, accumulate):
-    """regnn_rel_reduce on wide slabs (the in-place two-stage split for tall ones): fixed-order
-    column sums, deterministic."""
+    """regnn_rel_reduce on wide slabs (the in-place two-stage split for tall ones) and narrow ones
+    (relation tables): fixed-order column sums, deterministic."""
     from regnn_hip import _lib as L
     g = torch.Generator(device=DEV).manual_seed(rows + width)
     slab = torch.randn(rows, width, device=DEV, generator=g)
