@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 43). */
+/* ABI version (bumped on any signature or semantics change; currently 44). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -731,6 +731,26 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
                        const int64_t* local, const int32_t* e_type, const int64_t* e_off,
                        const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
                        float* S, float* wsum, int64_t ld_s, int64_t ld_w, hipStream_t stream);
+
+/* Layer 0's [S | w | 0] operand from the sampler's per-type input sums (relation slots; ABI 44):
+ * the outputs of regnn_ns_hop_typed_sums for hop `hop` (U [cap][T][K] unweighted sums, cnt
+ * [cap][T] counts, x_self [cap][K], u_rel [cap][T + 1]: each slot's relation or -1, then the self
+ * loop's relation n_et + node type) and the relation table tab give, for rows v < sizes[hop],
+ *   out[v][t K ..] = tab[u_rel[v][t]] U[v][t] + [t = u_rel[v][T] - n_et] tab[u_rel[v][T]] x_self[v]
+ *   out[v][T K + t] = tab[u_rel[v][t]] cnt[v][t] + [same] tab[u_rel[v][T]]     (0 past T, < Tp)
+ * what regnn_ns_typed_agg forms from the sampled edges (mag/regnn_layers.py:110-129), with Tp = T
+ * rounded up to 4; rows [sizes[hop], next multiple of 128) are zeros, later rows untouched.
+ * K = 128, T <= 4, ld >= T K + Tp. The backward writes slab[b][r] (slab_rows blocks; reduce with
+ * regnn_rel_reduce) of d tab[r] = sum over r's slots of <U, gS> + cnt gw and over r's self loops
+ * of <x_self, gS_t_self> + gw_t_self: fixed order, bitwise reproducible. */
+int regnn_ns_slot_agg(const int32_t* sizes, int32_t hop, const float* U, const float* cnt,
+                      const float* x_self, const int32_t* u_rel, const float* rel_table,
+                      int32_t n_et, int32_t n_types, int32_t K, int64_t cap, float* out,
+                      int64_t ld, hipStream_t stream);
+int regnn_ns_slot_agg_bwd(const int32_t* sizes, int32_t hop, const float* U, const float* cnt,
+                          const float* x_self, const int32_t* u_rel, const float* g, int64_t ld,
+                          int32_t n_et, int32_t n_types, int32_t K, float* slab, int32_t n_rel,
+                          int32_t slab_rows, hipStream_t stream);
 
 /* Relation-table gradient of regnn_ns_typed_agg: slab[b][r] = block b's partial of
  * sum_{e: rel_e = r} (<tables[t_e][row_e], gS[v][t_e]> + gw[v][t_e]) (per row group bins added

@@ -202,6 +202,108 @@ typed_agg_bwd_kernel(const int32_t* __restrict__ ptr, EdgeSrc E, const uint8_t* 
     }
 }
 
+// ---- layer 0 from the sampler's per-type input sums (relation slots) -------------------------
+// With one relation per (target type, source type) pair (ogbn-mag's schema), the outer hop's
+// sampler (regnn_ns_hop_typed_sums, on its own stream ahead of the model) forms the parameter-free
+// parts: U[v][t] = the unweighted sum of row v's sampled input rows of source type t, cnt[v][t]
+// their count, x_self[v] the self loop's row and the slots' relations u_rel[v][t] (-1: none),
+// u_rel[v][T] = the self loop's. Layer 0's operand [S | w | 0] is then
+//     S_vt = tab[r_vt] U_vt + [t = t_self(v)] tab[r_self] x_self(v),
+//     w_vt = tab[r_vt] cnt_vt + [t = t_self(v)] tab[r_self]
+// (agg0's formula, re_nsm2.hip) -- one read of contiguous sums per row instead of a gather of
+// every sampled row on the model's critical path. 32 lanes per row (K = 128: a float4 each), two
+// rows per wave. Rows in [n, the next multiple of 128) are written as zeros (the GEMMs' live-row
+// tiles read them), rows past that are left alone (nothing reads them).
+constexpr int kSlotK = 128;
+
+template <int NT>
+__global__ void __launch_bounds__(kBlock)
+slot_agg_kernel(const int32_t* __restrict__ sizes, int hop, const float* __restrict__ U,
+                const float* __restrict__ cnt, const float* __restrict__ xself,
+                const int32_t* __restrict__ urel, const float* __restrict__ tab, int n_et, int T,
+                int Tp, int64_t cap, float* __restrict__ out, int64_t ld) {
+    const int n = sizes[hop];
+    const int64_t lim = min(cap, (int64_t(n) + 127) / 128 * 128);
+    const int l = threadIdx.x & 31;
+    for (int64_t v = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / 32; v < lim;
+         v += int64_t(gridDim.x) * (kBlock / 32)) {
+        float* o = out + v * ld;
+        if (v >= n) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                if (t < T) *reinterpret_cast<float4*>(o + t * kSlotK + 4 * l) = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (l < Tp) o[T * kSlotK + l] = 0.f;
+            continue;
+        }
+        const int32_t* ur = urel + v * (T + 1);
+        const int rs = ur[T], ts = rs >= 0 ? rs - n_et : -1;
+        const float ws = rs >= 0 ? tab[rs] : 0.f;
+        const float4 xs = *reinterpret_cast<const float4*>(xself + v * kSlotK + 4 * l);
+        float wl = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (t >= T) continue;
+            const int r = ur[t];
+            const float wr = r >= 0 ? tab[r] : 0.f, wst = t == ts ? ws : 0.f;
+            const float4 u = *reinterpret_cast<const float4*>(U + (v * T + t) * kSlotK + 4 * l);
+            *reinterpret_cast<float4*>(o + t * kSlotK + 4 * l) =
+                make_float4(fmaf(wst, xs.x, wr * u.x), fmaf(wst, xs.y, wr * u.y),
+                            fmaf(wst, xs.z, wr * u.z), fmaf(wst, xs.w, wr * u.w));
+            if (l == t) wl = fmaf(wr, cnt[v * T + t], wst);
+        }
+        if (l < Tp) o[T * kSlotK + l] = l < T ? wl : 0.f;
+    }
+}
+
+// its relation-table gradient: d tab[r] = sum over (v, t) with r_vt = r of <U_vt, gS_vt> +
+// cnt_vt gw_vt, and over v with r_self(v) = r of <x_self, gS_v,t_self> + gw_v,t_self. One slab
+// row [n_rel] per block (launched with slab_rows blocks, 8 row groups each): each group adds its
+// rows' terms into its own LDS bins in (t, then self) order, the groups summed in group order --
+// bitwise reproducible; reduce the slab with regnn_rel_reduce.
+template <int NT>
+__global__ void __launch_bounds__(kBlock)
+slot_agg_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const float* __restrict__ U,
+                    const float* __restrict__ cnt, const float* __restrict__ xself,
+                    const int32_t* __restrict__ urel, const float* __restrict__ g, int64_t ld,
+                    int n_et, int T, float* __restrict__ slab, int n_rel) {
+    constexpr int NG = kBlock / 32;
+    __shared__ float gbins[NG][256];
+    for (int i = threadIdx.x; i < NG * 256; i += kBlock) gbins[i >> 8][i & 255] = 0.f;
+    __syncthreads();
+    const int n = sizes[hop];
+    const int l = threadIdx.x & 31, grp = threadIdx.x / 32;
+    float* bins = gbins[grp];
+    for (int64_t v = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / 32; v < n;
+         v += int64_t(gridDim.x) * NG) {
+        const int32_t* ur = urel + v * (T + 1);
+        const int rs = ur[T], ts = rs >= 0 ? rs - n_et : -1;
+        const float* gr = g + v * ld;
+        const float4 xs = *reinterpret_cast<const float4*>(xself + v * kSlotK + 4 * l);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (t >= T) continue;
+            const int r = ur[t];
+            const float4 gs = *reinterpret_cast<const float4*>(gr + t * kSlotK + 4 * l);
+            const float4 u = *reinterpret_cast<const float4*>(U + (v * T + t) * kSlotK + 4 * l);
+            const float gw = gr[T * kSlotK + t];
+            if (r >= 0) {
+                const float d = group_sum<32>(u.x * gs.x + u.y * gs.y + u.z * gs.z + u.w * gs.w);
+                if (l == 0) bins[r] += fmaf(cnt[v * T + t], gw, d);
+            }
+            if (t == ts) {
+                const float d = group_sum<32>(xs.x * gs.x + xs.y * gs.y + xs.z * gs.z + xs.w * gs.w);
+                if (l == 0) bins[rs] += d + gw;
+            }
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < n_rel; r += kBlock) {
+        float sr = 0.f;
+        for (int k = 0; k < NG; ++k) sr += gbins[k][r];
+        slab[int64_t(blockIdx.x) * n_rel + r] = sr;
+    }
+}
+
 }  // namespace nsagg
 }  // namespace regnn
 
@@ -283,6 +385,45 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
     BWD_CASE(64, 4) BWD_CASE(64, 8) BWD_CASE(128, 4) BWD_CASE(128, 8)
 #undef BWD_CASE
     return REGNN_EUNSUPPORTED;
+}
+
+int regnn_ns_slot_agg(const int32_t* sizes, int32_t hop, const float* U, const float* cnt,
+                      const float* x_self, const int32_t* u_rel, const float* rel_table,
+                      int32_t n_et, int32_t n_types, int32_t K, int64_t cap, float* out,
+                      int64_t ld, hipStream_t stream) {
+    if (!sizes || !U || !cnt || !x_self || !u_rel || !rel_table || !out || hop < 0 || hop > 7 ||
+        n_et < 0 || n_types < 1 || cap < 0)
+        return REGNN_EINVAL;
+    if (K != kSlotK || n_types > 4) return REGNN_EUNSUPPORTED;
+    const int Tp = (n_types + 3) & ~3;
+    if (ld < int64_t(n_types) * K + Tp || ld % 4 || reinterpret_cast<uintptr_t>(out) % 16 ||
+        reinterpret_cast<uintptr_t>(U) % 16 || reinterpret_cast<uintptr_t>(x_self) % 16)
+        return REGNN_EINVAL;
+    if (cap == 0) return REGNN_OK;
+    int64_t grid = (cap + kBlock / 32 - 1) / (kBlock / 32);
+    if (grid > kMaxGrid) grid = kMaxGrid;
+    hipLaunchKernelGGL((slot_agg_kernel<4>), dim3(unsigned(grid)), dim3(kBlock), 0, stream, sizes,
+                       hop, U, cnt, x_self, u_rel, rel_table, n_et, n_types, Tp, cap, out, ld);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_ns_slot_agg_bwd(const int32_t* sizes, int32_t hop, const float* U, const float* cnt,
+                          const float* x_self, const int32_t* u_rel, const float* g, int64_t ld,
+                          int32_t n_et, int32_t n_types, int32_t K, float* slab, int32_t n_rel,
+                          int32_t slab_rows, hipStream_t stream) {
+    if (!sizes || !U || !cnt || !x_self || !u_rel || !g || !slab || hop < 0 || hop > 7 ||
+        n_et < 0 || n_types < 1 || n_rel <= 0 || n_rel > 256 || slab_rows <= 0)
+        return REGNN_EINVAL;
+    if (K != kSlotK || n_types > 4) return REGNN_EUNSUPPORTED;
+    if (ld < int64_t(n_types) * K + n_types || ld % 4 || reinterpret_cast<uintptr_t>(g) % 16 ||
+        reinterpret_cast<uintptr_t>(U) % 16 || reinterpret_cast<uintptr_t>(x_self) % 16)
+        return REGNN_EINVAL;
+    hipLaunchKernelGGL((slot_agg_bwd_kernel<4>), dim3(unsigned(slab_rows)), dim3(kBlock), 0,
+                       stream, sizes, hop, U, cnt, x_self, u_rel, g, ld, n_et, n_types, slab,
+                       n_rel);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 }  // extern "C"

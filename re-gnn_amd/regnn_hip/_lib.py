@@ -111,6 +111,9 @@ _SIG = {
                            ctypes.c_int),
     "regnn_ns_typed_agg_bwd": ([P, P, P, P, P, P, P, P, P, I32, I32, I64, P, P, I64, I64, P, I32,
                                 I32, P], ctypes.c_int),
+    "regnn_ns_slot_agg": ([P, I32, P, P, P, P, P, I32, I32, I32, I64, P, I64, P], ctypes.c_int),
+    "regnn_ns_slot_agg_bwd": ([P, I32, P, P, P, P, P, I64, I32, I32, I32, P, I32, I32, P],
+                              ctypes.c_int),
     "regnn_nsm_slab_floats": ([P, I32], I64),
     "regnn_nsm_step": ([P, P, P], ctypes.c_int),
     "regnn_adam_flat": ([P, P, P, P, I64, F32, F32, F32, F32, F32, F32, P, P, P], ctypes.c_int),
@@ -131,7 +134,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 43
+ABI_VERSION = 44
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

@@ -496,7 +496,12 @@ class REGNN(torch.nn.Module):
         # [S | w]: the per-type sums and weight sums as one [n, T K + T] operand, so the
         # projection S W_c + w b_c is one GEMM against [W_c; b_c] (products on regnn_gemm_x6:
         # fp32-accurate bf16x6 MFMA; the small composition b_cat W_0 stays on hipBLASLt)
-        Sw = ops.ns_typed_agg(blk, tab, n_id, tabs, node_type, local_node_idx, ext=True)
+        if getattr(blk, "pre_sums", None) is not None:
+            # the sampler formed the per-type input sums ahead (relation slots): [S | w | 0] from
+            # one read of them, no gather of the sampled raw rows here
+            Sw = ops.ns_slot_agg(blk, tab, self.num_edge_types)
+        else:
+            Sw = ops.ns_typed_agg(blk, tab, n_id, tabs, node_type, local_node_idx, ext=True)
         lins = [self.lins[str(t)] for t in range(T)]
         n = blk.n_dst
         # [W_c; b_c; 0] = [W_1ᵀ; ..; W_Tᵀ; b_1; ..; b_T; 0] @ W_0: one concatenation and one x6

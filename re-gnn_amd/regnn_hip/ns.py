@@ -148,6 +148,7 @@ class DeviceSampler:
         # typed_sums[h]: hop h (meta-only, strided) also forms layer 0's input sums for the
         # fused step (regnn_ns_hop_typed_sums; FusedStep.enable_pre_sums), or None
         self.typed_sums = [None] * len(self.sizes_k)
+        self.hop_strided = [None] * len(self.sizes_k)   # per-hop layout override (run_hops)
         self._csc_jobs = {}
         self._csr_fresh = True
 
@@ -200,13 +201,17 @@ class DeviceSampler:
         the caller joins it. before_sums: called right before the outer hop's sums launch
         (regnn_ns_hop_typed_sums), e.g. to make it wait on an event."""
         strided = self.strided if strided is None else bool(strided)
+        # a hop's own layout (hop_strided[h] not None) wins over the call's: the module path
+        # samples its outer hop strided with the input sums while hop 0 stays CSR
+        hs = lambda h: strided if self.hop_strided[h] is None else self.hop_strided[h]  # noqa: E731
         rg = self.rg
         deferred = -1
         for h, k in enumerate(self.sizes_k):
             b, blk = self.hop_bufs[h], self.blocks[h]
-            fork = (csc_stream is not None and strided and self.csc[h] is not None and
+            sh = hs(h)
+            fork = (csc_stream is not None and sh and self.csc[h] is not None and
                     self.edge_meta[h] is None)
-            if self._sums_path(h, strided, meta_only):
+            if self._sums_path(h, sh, meta_only):
                 if before_sums is not None:
                     before_sums()
                 ts = self.typed_sums[h]
@@ -226,9 +231,9 @@ class DeviceSampler:
                 continue
             self.sums_fresh[h] = False
             # the transposed index of this hop built beside the next hop's sums (one launch)
-            defer = (not fork and strided and CSC_FUSE["mode"] != "off" and
+            defer = (not fork and sh and CSC_FUSE["mode"] != "off" and
                      self.csc[h] is not None and self.edge_meta[h] is None and
-                     h + 1 < len(self.sizes_k) and self._sums_path(h + 1, strided, meta_only))
+                     h + 1 < len(self.sizes_k) and self._sums_path(h + 1, hs(h + 1), meta_only))
             L.call("regnn_ns_hop", L.ptr(rg.csr_ptr), L.ptr(rg.csr_idx), L.ptr(self.etype_csr),
                    L.ptr(self.ntype), self.num_edge_types, k, h, L.ptr(self.state),
                    L.ptr(self.sizes), L.ptr(self.n_id), self.caps[h], L.ptr(self.g2l),
@@ -242,7 +247,7 @@ class DeviceSampler:
                    int(meta_only and self.meta_only[h] and self.edge_meta[h] is not None),
                    *((L.ptr(t) for t in self.csc[h]) if self.csc[h] is not None
                      else (None, None, None, None)),
-                   2 if fork or defer else int(strided), L.stream())
+                   2 if fork or defer else int(sh), L.stream())
             deferred = h if defer else -1
             if fork:
                 csc_stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -510,6 +515,10 @@ SUMS_ALIGN = {"mode": os.environ.get("REGNN_NS_SUMS_ALIGN", "2")}
 # 20 steps): 578.2 against 563.0 us per step without -- the reduce costs more than the shorter
 # k-chains save; off by default (REGNN_NS_GEMM_LIVE_HINT=on)
 GEMM_LIVE_HINT = {"mode": os.environ.get("REGNN_NS_GEMM_LIVE_HINT", "off")}
+# "on": the module path's outer hop forms layer 0's per-type input sums on the sampler's stream
+# (relation slots; NSTrainer._module_pre_sums) and layer 0 reads them; "off": layer 0 gathers the
+# sampled raw rows itself (regnn_ns_typed_agg, A/B)
+MODULE_PRE_SUMS = {"mode": os.environ.get("REGNN_NS_MODULE_PRESUMS", "on")}
 # parallel sampler lanes inside a lookahead group (REGNN_NS_SAMPLER_LANES): L streams, slot s on
 # lane s mod L with dedup tables of its own lane (L x 16 B per node of HBM). Measured (round 6):
 # L = 1 / 2 / 4 at 20 steps 110.6 / 116.0 / 133.0, at 160 steps 105.3 / 112.4 / 137.9 us per step
@@ -1017,12 +1026,35 @@ class NSTrainer:
             s.meta_only[last] = True
             blk = s.blocks[last]
             blk.edge_meta, blk.meta_only = (et, eo), True
+            self._module_pre_sums(s, last)
         for h, blk in enumerate(s.blocks):
             blk.live_rows = s.sizes[h:h + 1]      # the block's live target rows (device count)
         if s.blocks[0].csr_idx.numel() <= 32768:
             _, cptr, cent, clong = s.csc[0] or s.enable_csc(0)
             b0 = s.blocks[0]
             b0.csc, b0.csc_cap = (cptr, cent, clong, s.sizes, 1), s.caps[1]
+
+    def _module_pre_sums(self, s, last):
+        """relation slots, 128-wide inputs, <= 4 node types: the module path's outer hop runs as
+        the sampler's sums launch (regnn_ns_hop_typed_sums, strided, on the sampler's stream) and
+        layer 0 reads the per-type sums (ops.ns_slot_agg) instead of gathering the sampled raw
+        rows on the model's stream (mag.REGNN._typed_first_layer); hop 0 stays CSR."""
+        tabs = getattr(self.model, "_type_tables", lambda _x: None)(self.x_dict)
+        T = len(tabs) if tabs else 0
+        if (MODULE_PRE_SUMS["mode"] == "off" or not tabs or T > 4 or
+                any(t is None or t.dim() != 2 or t.shape[1] != 128 or not t.is_contiguous() or
+                    t.data_ptr() % 16 for t in tabs) or max(s.sizes_k) > 63 or
+                not relation_slots_ok(s, T)):
+            return
+        cap, K, dev = s.caps[last], 128, self.device
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=dev)  # noqa: E731
+        U, cnt, xself = z(cap, T, K), z(cap, T), z(cap, K)
+        urel = torch.full((cap, T + 1), -1, dtype=torch.int32, device=dev)
+        ptrs = (ctypes.c_void_p * T)(*[t.data_ptr() for t in tabs])
+        s.typed_sums[last] = dict(tables=ptrs, T=T, K=K, s_agg=U, s_w=cnt, u_self=xself,
+                                  u_rel=urel, keep=tabs)
+        s.hop_strided[last] = True
+        s.blocks[last].pre_sums = (U, cnt, xself, urel)
 
     # -- epochs ----------------------------------------------------------------------------------
     def steps_per_epoch(self):

@@ -725,6 +725,51 @@ class _NsTypedAgg(torch.autograd.Function):
         return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None, None, None, None
 
 
+class _NsSlotAgg(torch.autograd.Function):
+    """[S | w | 0] of regnn_ns_typed_agg (ext) from the sampler's per-type input sums (relation
+    slots; regnn_ns_slot_agg): pre = the slot's U [cap, T, K], counts [cap, T], self rows [cap, K]
+    and slot relations [cap, T + 1] the outer hop's sums launch wrote; backward: the relation
+    table's gradient (regnn_ns_slot_agg_bwd + the fixed-order slab reduce)."""
+
+    @staticmethod
+    def forward(ctx, tab, blk, pre, n_et):
+        U, cnt, xself, urel = pre
+        cap, T, K = U.shape
+        Tp = _ext_pad(T)
+        ld = T * K + Tp
+        out = torch.empty(cap, ld, dtype=torch.float32, device=U.device)
+        t = tab.detach().float().contiguous()
+        with timed("ns_slot_agg"):
+            L.call("regnn_ns_slot_agg", L.ptr(blk.live_rows), 0, L.ptr(U), L.ptr(cnt),
+                   L.ptr(xself), L.ptr(urel), L.ptr(t), int(n_et), T, K, cap, L.ptr(out), ld,
+                   L.stream())
+        ctx.blk, ctx.pre, ctx.n_et = blk, pre, int(n_et)
+        ctx.n_rel, ctx.tab_shape = t.numel(), tab.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        U, cnt, xself, urel = ctx.pre
+        cap, T, K = U.shape
+        g = g.contiguous().float()
+        rows = int(min(L.slab_rows(), max(1, -(-cap // 8))))   # 8 row groups per block
+        slab = torch.empty(rows, ctx.n_rel, dtype=torch.float32, device=U.device)
+        with timed("ns_slot_agg_bwd"):
+            L.call("regnn_ns_slot_agg_bwd", L.ptr(ctx.blk.live_rows), 0, L.ptr(U), L.ptr(cnt),
+                   L.ptr(xself), L.ptr(urel), L.ptr(g), g.stride(0), ctx.n_et, T, K, L.ptr(slab),
+                   ctx.n_rel, rows, L.stream())
+        return _reduce(slab, ctx.n_rel).view(ctx.tab_shape), None, None, None
+
+
+def ns_slot_agg(blk, tab, n_et):
+    """ns_typed_agg(..., ext=True) for a block whose sampler formed layer 0's per-type input sums
+    (blk.pre_sums: relation slots, regnn_ns_hop_typed_sums): the same [S | w | 0] operand from one
+    read of contiguous sums per row; differentiable in tab."""
+    return _NsSlotAgg.apply(tab, blk, blk.pre_sums, int(n_et))
+
+
 _CAST_CACHE = {}
 
 

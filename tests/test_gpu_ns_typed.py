@@ -18,10 +18,14 @@ import _golden as G  # noqa: E402
 from test_gpu_ns_engine import _mag, DEV  # noqa: E402
 
 
-def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(6, 4)):
-    from regnn_hip import mag, ops
+def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(6, 4),
+                    pre=None):
+    from regnn_hip import mag, ns, ops
     from regnn_hip.ns import NSTrainer
     old, old_csc = mag.TYPED_AGG["mode"], ops.NS_CSC["mode"]
+    old_pre = ns.MODULE_PRE_SUMS["mode"]
+    if pre is not None:
+        ns.MODULE_PRE_SUMS["mode"] = "on" if pre else "off"
     # the reference-ordered run also takes the atomic scatter backward of the last layer
     mag.TYPED_AGG["mode"] = ops.NS_CSC["mode"] = "auto" if typed else "off"
     try:
@@ -51,10 +55,14 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(
         tr._forward_backward()
         torch.cuda.synchronize()
         assert seen == [typed]
+        if pre is not None:                    # the outer hop's sums path ran (or not)
+            assert all((s.typed_sums[-1] is not None) == pre for s in tr.slots)
+            assert all(s.sums_fresh[-1] == pre for s in tr.slots[:1])
         return float(tr.loss), {n: p.grad.detach().double().cpu().numpy().copy()
                                 for n, p in m.named_parameters()}
     finally:
         mag.TYPED_AGG["mode"], ops.NS_CSC["mode"] = old, old_csc
+        ns.MODULE_PRE_SUMS["mode"] = old_pre
 
 
 @pytest.mark.parametrize("K,hidden,residual", [(128, 512, False), (128, 64, False),
@@ -68,6 +76,21 @@ def test_typed_first_layer_matches_reference_order(K, hidden, residual):
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
     # the relation table of layer 0 has a gradient through the typed aggregation
+    assert np.abs(ga["convs.0.relation_weight"]).max() > 0
+
+
+@pytest.mark.parametrize("hidden,dropout", [(512, 0.0), (64, 0.0), (256, 0.5)])
+def test_module_pre_sums_match_typed_agg(hidden, dropout):
+    """the module path's layer 0 from the sampler's per-type input sums (relation slots: the outer
+    hop as regnn_ns_hop_typed_sums, ops.ns_slot_agg) against the same layer gathering the sampled
+    raw rows itself (regnn_ns_typed_agg): the same batch, loss and every gradient at 1e-5."""
+    d = _mag(0.003, seed=4, F=128)
+    la, ga = _grads_one_step(d, hidden, True, dropout, pre=True)
+    lb, gb = _grads_one_step(d, hidden, True, dropout, pre=False)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
     assert np.abs(ga["convs.0.relation_weight"]).max() > 0
 
 
