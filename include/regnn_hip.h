@@ -732,6 +732,17 @@ int regnn_ns_typed_agg(const int32_t* ptr, const int32_t* idx, const uint8_t* re
                        const float* const* tables, int32_t n_types, int32_t K, int64_t n_rows,
                        float* S, float* wsum, int64_t ld_s, int64_t ld_w, hipStream_t stream);
 
+/* The mean aggregation of a sampled block in the strided layout (regnn_ns_hop strided = 1: row
+ * i's edges at slots [i S, i S + cnt[i]], the self loop last; ABI 44): y[i] = inv[i] sum_e
+ * tab[rel_e] x[idx_e] + bias for i < live[0], bias (or 0) past it, over n_rows (the capacity)
+ * rows of F fp32 features (F % 4 == 0, F <= 1024; x, y, bias 16-byte aligned); rel_table may be
+ * NULL (weight 1). What regnn_spmm_fwd computes over the same block in the CSR layout, summed
+ * in the same slot order (mag/regnn_layers.py:110-148). */
+int regnn_ns_spmm_strided_fwd(const int32_t* live, const int32_t* cnt, int32_t stride,
+                              const int32_t* idx, const uint8_t* rel, const float* rel_table,
+                              const float* inv, const float* bias, const float* x, float* y,
+                              int64_t n_rows, int32_t F, hipStream_t stream);
+
 /* Layer 0's [S | w | 0] operand from the sampler's per-type input sums (relation slots; ABI 44):
  * the outputs of regnn_ns_hop_typed_sums for hop `hop` (U [cap][T][K] unweighted sums, cnt
  * [cap][T] counts, x_self [cap][K], u_rel [cap][T + 1]: each slot's relation or -1, then the self

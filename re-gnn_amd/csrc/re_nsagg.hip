@@ -304,6 +304,71 @@ slot_agg_bwd_kernel(const int32_t* __restrict__ sizes, int hop, const float* __r
     }
 }
 
+// ---- the mean aggregation of a block in the strided layout (regnn_ns_hop strided = 1) --------
+// row i's edges at slots [i S, i S + cnt[i]] (sampled ones in CSR order, the self loop last), the
+// slot order the CSR layout keeps: y[i] = inv[i] sum_e tab[rel_e] x[idx_e] + bias for live rows
+// i < sizes[0], bias for the others. One wave per row, LPR lanes x VPL float4 per lane, the
+// row's entries loaded lane-parallel and its source rows UN at a time in flight.
+template <int VPL>
+__global__ void __launch_bounds__(kBlock)
+strided_spmm_kernel(const int32_t* __restrict__ live, const int32_t* __restrict__ cnt, int S,
+                    const int32_t* __restrict__ idx, const uint8_t* __restrict__ rel,
+                    const float* __restrict__ tab, const float* __restrict__ inv,
+                    const float* __restrict__ bias, const float* __restrict__ x,
+                    float* __restrict__ y, int64_t n_rows, int F) {
+    constexpr int UN = 8;
+    const int lane = threadIdx.x & 63;
+    const int n = live[0];
+    const int nv = F / 4;
+    for (int64_t i = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / 64; i < n_rows;
+         i += int64_t(gridDim.x) * (kBlock / 64)) {
+        float4 acc[VPL];
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int m = i < n ? cnt[i] + 1 : 0;
+        const int64_t base = i * S;
+        const int my_u = lane < m ? idx[base + lane] : 0;
+        const float my_w = lane < m ? (tab ? tab[rel[base + lane]] : 1.f) : 0.f;
+        for (int j = 0; j < m; j += UN) {
+            float4 xv[UN][VPL];
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                const int uu = __shfl(my_u, min(j + u, m - 1), 64);
+#pragma unroll
+                for (int q = 0; q < VPL; ++q) {
+                    const int c = lane + 64 * q;
+                    xv[u][q] = c < nv ? reinterpret_cast<const float4*>(x + int64_t(uu) * F)[c]
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                if (j + u >= m) continue;
+                const float w = __shfl(my_w, j + u, 64);
+#pragma unroll
+                for (int q = 0; q < VPL; ++q) {
+                    acc[q].x = fmaf(w, xv[u][q].x, acc[q].x);
+                    acc[q].y = fmaf(w, xv[u][q].y, acc[q].y);
+                    acc[q].z = fmaf(w, xv[u][q].z, acc[q].z);
+                    acc[q].w = fmaf(w, xv[u][q].w, acc[q].w);
+                }
+            }
+        }
+        const float iv = i < n ? inv[i] : 0.f;
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+            const int c = lane + 64 * q;
+            if (c >= nv) continue;
+            float4 b = bias ? reinterpret_cast<const float4*>(bias)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            b.x = fmaf(iv, acc[q].x, b.x);
+            b.y = fmaf(iv, acc[q].y, b.y);
+            b.z = fmaf(iv, acc[q].z, b.z);
+            b.w = fmaf(iv, acc[q].w, b.w);
+            reinterpret_cast<float4*>(y + i * F)[c] = b;
+        }
+    }
+}
+
 }  // namespace nsagg
 }  // namespace regnn
 
@@ -384,6 +449,33 @@ int regnn_ns_typed_agg_bwd(const int32_t* ptr, const int32_t* idx, const uint8_t
     }
     BWD_CASE(64, 4) BWD_CASE(64, 8) BWD_CASE(128, 4) BWD_CASE(128, 8)
 #undef BWD_CASE
+    return REGNN_EUNSUPPORTED;
+}
+
+int regnn_ns_spmm_strided_fwd(const int32_t* live, const int32_t* cnt, int32_t stride,
+                              const int32_t* idx, const uint8_t* rel, const float* rel_table,
+                              const float* inv, const float* bias, const float* x, float* y,
+                              int64_t n_rows, int32_t F, hipStream_t stream) {
+    if (!live || !cnt || !idx || !inv || !x || !y || (rel_table && !rel) || n_rows < 0 ||
+        stride < 1 || stride > 64 || F <= 0 || F % 4)
+        return REGNN_EINVAL;
+    if (reinterpret_cast<uintptr_t>(x) % 16 || reinterpret_cast<uintptr_t>(y) % 16 ||
+        (bias && reinterpret_cast<uintptr_t>(bias) % 16))
+        return REGNN_EINVAL;
+    if (n_rows == 0) return REGNN_OK;
+    int64_t grid = (n_rows + kBlock / 64 - 1) / (kBlock / 64);
+    if (grid > kMaxGrid) grid = kMaxGrid;
+    const int vpl = (F / 4 + 63) / 64;
+#define SSP_CASE(V)                                                                             \
+    if (vpl <= V) {                                                                             \
+        hipLaunchKernelGGL((strided_spmm_kernel<V>), dim3(unsigned(grid)), dim3(kBlock), 0,     \
+                           stream, live, cnt, stride, idx, rel, rel_table, inv, bias, x, y,     \
+                           n_rows, F);                                                          \
+        REGNN_LAUNCH_CHECK();                                                                   \
+        return REGNN_OK;                                                                        \
+    }
+    SSP_CASE(1) SSP_CASE(2) SSP_CASE(4)
+#undef SSP_CASE
     return REGNN_EUNSUPPORTED;
 }
 

@@ -111,6 +111,7 @@ _SIG = {
                            ctypes.c_int),
     "regnn_ns_typed_agg_bwd": ([P, P, P, P, P, P, P, P, P, I32, I32, I64, P, P, I64, I64, P, I32,
                                 I32, P], ctypes.c_int),
+    "regnn_ns_spmm_strided_fwd": ([P, P, I32, P, P, P, P, P, P, P, I64, I32, P], ctypes.c_int),
     "regnn_ns_slot_agg": ([P, I32, P, P, P, P, P, I32, I32, I32, I64, P, I64, P], ctypes.c_int),
     "regnn_ns_slot_agg_bwd": ([P, I32, P, P, P, P, P, I64, I32, I32, I32, P, I32, I32, P],
                               ctypes.c_int),

@@ -519,6 +519,9 @@ GEMM_LIVE_HINT = {"mode": os.environ.get("REGNN_NS_GEMM_LIVE_HINT", "off")}
 # (relation slots; NSTrainer._module_pre_sums) and layer 0 reads them; "off": layer 0 gathers the
 # sampled raw rows itself (regnn_ns_typed_agg, A/B)
 MODULE_PRE_SUMS = {"mode": os.environ.get("REGNN_NS_MODULE_PRESUMS", "on")}
+# "on": the module path samples hop 0 in the strided layout too (its last layer's forward reads
+# the strided rows, its backward the transposed index); "off": hop 0 in the CSR layout (A/B)
+MODULE_STRIDED = {"mode": os.environ.get("REGNN_NS_MODULE_STRIDED", "on")}
 # parallel sampler lanes inside a lookahead group (REGNN_NS_SAMPLER_LANES): L streams, slot s on
 # lane s mod L with dedup tables of its own lane (L x 16 B per node of HBM). Measured (round 6):
 # L = 1 / 2 / 4 at 20 steps 110.6 / 116.0 / 133.0, at 160 steps 105.3 / 112.4 / 137.9 us per step
@@ -1033,6 +1036,16 @@ class NSTrainer:
             _, cptr, cent, clong = s.csc[0] or s.enable_csc(0)
             b0 = s.blocks[0]
             b0.csc, b0.csc_cap = (cptr, cent, clong, s.sizes, 1), s.caps[1]
+            from . import ops as _ops
+            # (the layer's backward must take the transposed-index gather: ops._NsSpmm)
+            if (MODULE_STRIDED["mode"] != "off" and _ops.NS_CSC["mode"] != "off" and
+                    len(s.sizes_k) > 1 and
+                    getattr(self.model, "hidden_dim", 0) in _ops._CSC_WIDTHS):
+                # hop 0 in the strided layout (sampling + placement in one launch, the one-pass
+                # de-duplication, the multi-block transposed index): its forward aggregation
+                # reads rows at i S (regnn_ns_spmm_strided_fwd), its backward the index
+                s.hop_strided[0] = True
+                b0.strided_rows = (s.hop_bufs[0]["scnt"], s.sizes_k[0] + 1)
 
     def _module_pre_sums(self, s, last):
         """relation slots, 128-wide inputs, <= 4 node types: the module path's outer hop runs as

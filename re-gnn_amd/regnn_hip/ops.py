@@ -594,6 +594,18 @@ class _NsSpmm(torch.autograd.Function):
         F = x.shape[1]
         y = torch.empty(blk.n_dst, F, dtype=x.dtype, device=x.device)
         t = _flat_table(tab)
+        strided = getattr(blk, "strided_rows", None)
+        if strided is not None:
+            # the sampler wrote this block in the strided layout: row i at slots i S ..
+            cnt, S = strided
+            b = None if bias is None else bias.detach().float().contiguous()
+            with timed("ns_spmm_fwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_fwd")):
+                L.call("regnn_ns_spmm_strided_fwd", L.ptr(blk.live_rows), L.ptr(cnt), S,
+                       L.ptr(blk.csr_idx), L.ptr(blk.rel if t is not None else None), L.ptr(t),
+                       L.ptr(blk.inv), L.ptr(b), L.ptr(x), L.ptr(y), blk.n_dst, F, L.stream())
+            ctx.blk, ctx.tab_shape = blk, None if tab is None else tab.shape
+            ctx.save_for_backward(x, t)
+            return y
         with timed("ns_spmm_fwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_fwd")):
             L.call("regnn_spmm_fwd", L.ptr(blk.csr_ptr), L.ptr(blk.csr_idx),
                    L.ptr(blk.rel if t is not None else None), L.ptr(t), None, None,
@@ -633,6 +645,9 @@ class _NsSpmm(torch.autograd.Function):
             g_tab = _reduce(slab, n_rel).view(ctx.tab_shape) if slab is not None else None
             g_bias = gy.sum(0) if ctx.needs_input_grad[2] else None
             return (gx if need_x else None), g_tab, g_bias, None
+        if getattr(blk, "strided_rows", None) is not None:
+            raise RuntimeError("ns_spmm: a strided block differentiates through its transposed "
+                               "index only (NS_CSC on, F in %s)" % (_CSC_WIDTHS,))
         gx = torch.zeros_like(x)
         slab = _slab(n_rel, x.device) if (need_tab and t is not None) else None
         with timed("ns_spmm_bwd", spmm_bytes(blk.E, blk.n_dst, blk.n_src, F, 4, "spmm_bwd")):

@@ -19,13 +19,15 @@ from test_gpu_ns_engine import _mag, DEV  # noqa: E402
 
 
 def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(6, 4),
-                    pre=None):
+                    pre=None, strided=None):
     from regnn_hip import mag, ns, ops
     from regnn_hip.ns import NSTrainer
     old, old_csc = mag.TYPED_AGG["mode"], ops.NS_CSC["mode"]
-    old_pre = ns.MODULE_PRE_SUMS["mode"]
+    old_pre, old_str = ns.MODULE_PRE_SUMS["mode"], ns.MODULE_STRIDED["mode"]
     if pre is not None:
         ns.MODULE_PRE_SUMS["mode"] = "on" if pre else "off"
+    if strided is not None:
+        ns.MODULE_STRIDED["mode"] = "on" if strided else "off"
     # the reference-ordered run also takes the atomic scatter backward of the last layer
     mag.TYPED_AGG["mode"] = ops.NS_CSC["mode"] = "auto" if typed else "off"
     try:
@@ -55,6 +57,9 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(
         tr._forward_backward()
         torch.cuda.synchronize()
         assert seen == [typed]
+        if strided is not None:                # hop 0's layout
+            assert all((getattr(s.blocks[0], "strided_rows", None) is not None) == strided
+                       for s in tr.slots)
         if pre is not None:                    # the outer hop's sums path ran (or not)
             assert all((s.typed_sums[-1] is not None) == pre for s in tr.slots)
             assert all(s.sums_fresh[-1] == pre for s in tr.slots[:1])
@@ -62,7 +67,7 @@ def _grads_one_step(d, hidden, typed, dropout, residual=False, batch=96, sizes=(
                                 for n, p in m.named_parameters()}
     finally:
         mag.TYPED_AGG["mode"], ops.NS_CSC["mode"] = old, old_csc
-        ns.MODULE_PRE_SUMS["mode"] = old_pre
+        ns.MODULE_PRE_SUMS["mode"], ns.MODULE_STRIDED["mode"] = old_pre, old_str
 
 
 @pytest.mark.parametrize("K,hidden,residual", [(128, 512, False), (128, 64, False),
@@ -92,6 +97,20 @@ def test_module_pre_sums_match_typed_agg(hidden, dropout):
         ok, err = G.close(ga[n], gb[n], 1e-5)
         assert ok, f"{n}: rel err {err:.3e}"
     assert np.abs(ga["convs.0.relation_weight"]).max() > 0
+
+
+@pytest.mark.parametrize("hidden,typed", [(512, True), (64, True), (128, True)])
+def test_module_strided_hop0_matches_csr(hidden, typed):
+    """the module path's hop 0 in the strided layout (the last layer's forward over rows at i S,
+    regnn_ns_spmm_strided_fwd; its backward over the transposed index the strided hop builds)
+    against hop 0 in the CSR layout: the same batch, loss and every gradient at 1e-5."""
+    d = _mag(0.003, seed=5, F=128)
+    la, ga = _grads_one_step(d, hidden, typed, 0.0, strided=True)
+    lb, gb = _grads_one_step(d, hidden, typed, 0.0, strided=False)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for n in gb:
+        ok, err = G.close(ga[n], gb[n], 1e-5)
+        assert ok, f"{n}: rel err {err:.3e}"
 
 
 def _three_types(d):
