@@ -938,7 +938,9 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
  * data-parallel mean needs no separate pass), t = *step + 1, m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
  * p -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps). *step (int64) and *ticket
  * (uint32, zero-filled once) live on the device; the launch advances *step itself, so a
- * captured graph needs no host update. */
+ * captured graph needs no host update. ticket NULL (ABI 44): *step was already advanced by the
+ * caller (t = *step, nothing written): no end-of-launch ticket, whose one contended atomic per
+ * workgroup serialises the tail of a large bucket's launch. */
 int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, float weight_decay,
                     float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream);

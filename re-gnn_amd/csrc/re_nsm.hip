@@ -1451,7 +1451,8 @@ adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __re
         g0 = reinterpret_cast<const VT*>(g)[i0]; p0 = reinterpret_cast<const VT*>(p)[i0];
         m0 = reinterpret_cast<const VT*>(m)[i0]; v0 = reinterpret_cast<const VT*>(v)[i0];
     }
-    const int64_t t = step[0] + 1;
+    // ticket null: the step count was advanced before this launch (read only, no ticket)
+    const int64_t t = ticket ? step[0] + 1 : step[0];
     const double bc1 = 1.0 - pow(double(b1), double(t));
     const double bc2 = 1.0 - pow(double(b2), double(t));
     const float step_size = float(double(lr) / bc1);
@@ -1478,6 +1479,7 @@ adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __re
     }
     // the ticket only orders every block's read of step[0] (its value is consumed above) before
     // the last block's store of it; the parameter stores need no fence before it
+    if (!ticket) return;                   // (block-uniform)
     __syncthreads();
     if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     __syncthreads();
@@ -1782,7 +1784,7 @@ int regnn_nsm_step(const regnn_nsm_params* p, const regnn_nsm_work* w, hipStream
 int regnn_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, float weight_decay,
                     float grad_scale, int64_t* step, uint32_t* ticket, hipStream_t stream) {
-    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !ticket || n < 0) return REGNN_EINVAL;
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0) return REGNN_EINVAL;
     if (n == 0) return REGNN_OK;
     auto al = [](const void* q) { return reinterpret_cast<uintptr_t>(q) % 16 == 0; };
     const bool vec = n % 4 == 0 && al(param) && al(grad) && al(exp_avg) && al(exp_avg_sq);

@@ -522,6 +522,9 @@ MODULE_PRE_SUMS = {"mode": os.environ.get("REGNN_NS_MODULE_PRESUMS", "on")}
 # "on": the module path samples hop 0 in the strided layout too (its last layer's forward reads
 # the strided rows, its backward the transposed index); "off": hop 0 in the CSR layout (A/B)
 MODULE_STRIDED = {"mode": os.environ.get("REGNN_NS_MODULE_STRIDED", "on")}
+# "on": FlatAdam advances its step count with a one-element add and launches regnn_adam_flat
+# without its end-of-grid ticket (ticket NULL); "off": the launch advances it behind the ticket
+ADAM_PRE_STEP = {"mode": os.environ.get("REGNN_ADAM_PRE_STEP", "on")}
 # parallel sampler lanes inside a lookahead group (REGNN_NS_SAMPLER_LANES): L streams, slot s on
 # lane s mod L with dedup tables of its own lane (L x 16 B per node of HBM). Measured (round 6):
 # L = 1 / 2 / 4 at 20 steps 110.6 / 116.0 / 133.0, at 160 steps 105.3 / 112.4 / 137.9 us per step
@@ -868,10 +871,15 @@ class FlatAdam:
         self.grad_scale = 1.0
 
     def step(self):
+        pre = ADAM_PRE_STEP["mode"] != "off"
+        if pre:
+            # the step count advanced by a one-element add before the launch (capturable),
+            # instead of the launch's end-of-grid ticket (regnn_adam_flat with ticket NULL)
+            self.step_count.add_(1)
         L.call("regnn_adam_flat", L.ptr(self.p), L.ptr(self.g), L.ptr(self.m), L.ptr(self.v),
                self.p.numel(), self.lr, float(self.betas[0]), float(self.betas[1]), self.eps,
-               self.weight_decay, self.grad_scale, L.ptr(self.step_count), L.ptr(self.ticket),
-               L.stream())
+               self.weight_decay, self.grad_scale, L.ptr(self.step_count),
+               None if pre else L.ptr(self.ticket), L.stream())
 
 
 class NSTrainer:

@@ -510,14 +510,18 @@ def test_fused_step_graph_replay_tracks_eager(flat_adam):
     assert np.allclose(le, lg, rtol=1e-4, atol=1e-5), (le, lg)
 
 
+@pytest.mark.parametrize("pre", ["on", "off"])
 @pytest.mark.parametrize("odd", [True, False])
 @pytest.mark.parametrize("wd,gs", [(0.0, 1.0), (1e-3, 1.0), (0.0, 0.125)])
-def test_flat_adam_matches_torch_adam(wd, gs, odd):
+def test_flat_adam_matches_torch_adam(wd, gs, odd, pre, monkeypatch):
     """regnn_adam_flat (the NS trainer's one-launch optimizer) against torch.optim.Adam over
     the same gradients for 4 steps, with and without weight decay; grad_scale 1/8 (the mean of
     an 8-rank SUM all-reduce) against torch's Adam on the divided gradient. odd: a bucket of
-    30603 elements (the scalar kernel); else 30604 (the float4 kernel)."""
+    30603 elements (the scalar kernel); else 30604 (the float4 kernel). pre: the step count
+    advanced by a stream op before the launch (no ticket) or by the kernel's last block."""
+    from regnn_hip import ns
     from regnn_hip.ns import FlatAdam
+    monkeypatch.setitem(ns.ADAM_PRE_STEP, "mode", pre)
     g = torch.Generator(device=DEV).manual_seed(5)
     shapes = [(64, 128), (64,), (11,) if odd else (12,), (349, 64)]
     ref = [torch.randn(s, generator=g, device=DEV).requires_grad_(True) for s in shapes]
