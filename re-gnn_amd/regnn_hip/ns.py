@@ -470,6 +470,11 @@ SPLIT_EXCHANGE = {"mode": os.environ.get("REGNN_NS_SPLIT_EXCHANGE", "off")}
 # 0.761 off against 0.757 / 0.756 on; round 5 (three interleaved 300-step pairs) 0.683-0.684
 # off against 0.667-0.673 on
 MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
+# the module path's sampling lookahead (REGNN_NS_MODULE_AHEAD): 1 -- the next batch sampled beside
+# each step, a fork and a join per step (each a marker on the model's queue: ~5 us of queue idle
+# apiece in a kernel trace at hidden 512); G > 1 -- the fused engine's lookahead groups (2G slots,
+# one fork and one join per group of up to G steps)
+MODULE_AHEAD = {"n": int(os.environ.get("REGNN_NS_MODULE_AHEAD", "4"))}
 # "on": the pipelined fused engine builds hop 0's transposed index on a third stream while hop 1
 # samples (regnn_ns_hop strided 2 / 3); "off" (default): in the sampler's own chain. Eager runs
 # are fine; capturing the third stream (forked from the sampler's stream, joined back before the
@@ -891,7 +896,7 @@ class NSTrainer:
     The gradients live in one flat fp32 bucket (p.grad are views of it): one RCCL all-reduce
     per step for world > 1 (mag.flat_grad_allreduce's exchange), outside the captured graph.
 
-    pipeline: 2 * ahead sampler slots (AHEAD; the module path: ahead 1); while the model trains
+    pipeline: 2 * ahead sampler slots (AHEAD; the module path: MODULE_AHEAD); while the model trains
     on one slot's batch, the batch `ahead` steps later is sampled into another on a second
     stream (the reference's NeighborSampler prefetches batches with DataLoader workers,
     mag/regnn_ns.py:206-208). Slot s deals global batches as rank + s * world of
@@ -973,9 +978,11 @@ class NSTrainer:
         pipeline = pipeline and os.environ.get("REGNN_NS_PIPELINE", "1") != "0"
         self.pipelined = bool(pipeline) and (self.fused is not None or
                                              (self._blocks_ok and MODULE_PIPELINE["mode"] != "off"))
-        # the sampling lookahead (fused engine; the module path samples one batch ahead)
-        self.ahead = (max(1, int(default_ahead(self.world))) if self.pipelined and
-                      self.fused is not None else 1)
+        # the sampling lookahead (fused engine: default_ahead; the module path: MODULE_AHEAD)
+        self.ahead = 1
+        if self.pipelined:
+            self.ahead = max(1, int(default_ahead(self.world) if self.fused is not None
+                                    else MODULE_AHEAD["n"]))
         # parallel sampler lanes (lookahead groups): slot s samples on lane s mod L with that
         # lane's own dedup tables, so L batches of a group sample at the same time on L streams
         self.lanes = (max(1, int(SAMPLER_LANES["n"])) if self.pipelined and self.fused is not None
@@ -994,7 +1001,8 @@ class NSTrainer:
                     FusedStep(model, s, x_dict, node_type, local_node_idx, self.y_flat, self.loss)
                     for s in self.slots[1:]]
             else:
-                self._setup_module_slot(self.slots[1])
+                for s in self.slots[1:]:
+                    self._setup_module_slot(s)
             # the sampler's stream; REGNN_NS_SIDE_PRIORITY (-1: high) for A/B runs
             self._side = torch.cuda.Stream(device=dev,
                                            priority=int(os.environ.get("REGNN_NS_SIDE_PRIORITY", "0")))
@@ -1161,12 +1169,15 @@ class NSTrainer:
         # record is a marker on the model's queue: ~4 us of queue idle between finalize and the
         # next agg0, measured in a kernel trace); "off": never
         mode = SUMS_ALIGN["mode"]
-        every = 0 if mode == "off" else (1 if mode == "on" else int(mode))
+        every = 0 if mode == "off" or self.fused is None else (1 if mode == "on" else int(mode))
         align = every > 0
         ends = {}
 
         def model(i):
-            self._fs_step(self.fused_slots[(start + i) % n])
+            if self.fused is None:             # the module path (autograd forward / backward)
+                self._module_step(self.slots[(start + i) % n])
+            else:
+                self._fs_step(self.fused_slots[(start + i) % n])
             if in_graph:
                 self._exchange()
             self._opt_step()

@@ -189,15 +189,18 @@ def test_trainer_graph_replay_tracks_eager():
 
 
 @pytest.mark.parametrize("graph,engine", [(False, "fused"), (True, "fused"), (False, "module"),
-                                          (True, "module")])
+                                          (True, "module"), (True, "module1")])
 def test_pipelined_trainer_matches_unpipelined(monkeypatch, graph, engine):
-    """two sampler slots (the next batch sampled on a second stream while the model trains)
-    give the unpipelined batch sequence, dropout masks and losses, across an epoch change; for
-    the fused step and for the module path at hidden 128 (the typed first layer, meta-only last
-    hop; dropout off: the module path draws torch's RNG)."""
+    """sampler slots filled ahead on a second stream while the model trains give the
+    unpipelined batch sequence, dropout masks and losses, across an epoch change; for the fused
+    step and for the module path at hidden 128 (the typed first layer, meta-only last hop;
+    dropout off: the module path draws torch's RNG) at its default lookahead and at 1
+    ("module1": the next batch only)."""
     from regnn_hip import ns
     from regnn_hip.ns import NSTrainer
     monkeypatch.setitem(ns.MODULE_PIPELINE, "mode", "on")
+    if engine == "module1":
+        monkeypatch.setitem(ns.MODULE_AHEAD, "n", 1)
     fused = engine == "fused"
     d = _mag(0.002, seed=8, F=128, hidden=64 if fused else 128, classes=13,
              dropout=0.4 if fused else 0.0)
@@ -229,6 +232,53 @@ def test_pipelined_trainer_matches_unpipelined(monkeypatch, graph, engine):
     # captured than eagerly (ulp-level differences that Adam carries forward): 1e-5 there
     tol = 1e-6 if fused else 5e-5
     assert np.allclose(lp, lu, rtol=tol, atol=tol * 0.1), (lp, lu)
+
+
+def test_module_run_steps_groups_match_single_replays(monkeypatch):
+    """the module path's lookahead groups (MODULE_AHEAD 4: 8 slots, 4- and 2-step graphs whose
+    sampler fills the other slots, one fork and one join per group) train the same batches to
+    the same losses and parameters as one-step replays, across an epoch boundary."""
+    d = _mag(0.002, seed=8, F=128, hidden=128, classes=13, dropout=0.0)
+    from regnn_hip import ns
+    from regnn_hip.ns import NSTrainer
+    monkeypatch.setitem(ns.MODULE_PIPELINE, "mode", "on")
+    monkeypatch.setitem(ns.MODULE_AHEAD, "n", 4)
+
+    def make():
+        return NSTrainer(d["model"](5), None, d["rg"], [6, 4], 100,
+                         torch.arange(d["n_paper"], device=DEV), d["x_dict"], d["edge_type"],
+                         d["node_type"], d["local"], d["y"], 7, seed=9, adam=dict(lr=1e-2),
+                         engine="module")
+    ta, tb = make(), make()
+    assert ta.fused is None and ta._module_lean
+    ta.capture(warmup=1)
+    tb.capture(warmup=1)
+    assert ta.ahead == 4 and len(ta.slots) == 8
+    assert sorted(ta.graph_groups) == [(m, c) for m in (2, 4) for c in range(8)]
+    # (hipBLASLt's small products may differ by ulps between graphs, and Adam's m / sqrt(v)
+    # turns an ulp in a near-zero gradient into up to a fraction of its step lr = 1e-2: a few
+    # parameters differ by ~5e-5 after 4 steps, the losses stay bitwise equal; 1e-3 = lr / 10)
+    for k in (4, 3, 2, 7):
+        ta.run_steps(k)
+        for _ in range(k):
+            tb.replay()
+        torch.cuda.synchronize()
+        assert ta.cur == tb.cur and ta._trained == tb._trained
+        assert torch.equal(ta.sampler.n_id[:int(ta.sampler.sizes[0])],
+                           tb.sampler.n_id[:int(tb.sampler.sizes[0])])
+        assert abs(float(ta.loss) - float(tb.loss)) <= 5e-5 * abs(float(tb.loss))
+        dd = (ta.pflat - tb.pflat).abs()
+        assert float(dd.max()) <= 1e-3, \
+            (k, float(dd.max()), int((dd > 1e-6).sum()), ta.pflat.numel(), float(ta.loss),
+             float(tb.loss))
+    ta.set_epoch(1)
+    tb.set_epoch(1)
+    ta.run_steps(2)
+    tb.replay(); tb.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(ta.sampler.n_id[:int(ta.sampler.sizes[0])],
+                       tb.sampler.n_id[:int(tb.sampler.sizes[0])])
+    assert float((ta.pflat - tb.pflat).abs().max()) <= 1e-3
 
 
 def test_trainer_epoch_wraps_and_counts():
