@@ -959,6 +959,8 @@ class NSTrainer:
             # pass between the exchange and the update (p.grad holds the rank sum)
             opt.grad_scale = 1.0 / self.world
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        # the module path's backward seed d loss / d loss = 1 (autograd would fill one per step)
+        self._loss_seed = torch.ones((), dtype=torch.float32, device=dev)
         # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in eight HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
         if engine == "fused" and why is not None:
@@ -1292,7 +1294,8 @@ class NSTrainer:
         # every gradient (some of them transposed views) into its bucket view (backward() would
         # accumulate with one add kernel per parameter, and _foreach_copy_ / _foreach_add_
         # lower to a kernel per tensor here: ~90 us per step at hidden 512)
-        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        seed = self._loss_seed if loss.shape == self._loss_seed.shape else None
+        grads = torch.autograd.grad(loss, self.params, grad_outputs=seed, allow_unused=True)
         # the bucket is zeroed once (above), so a parameter that had a gradient on an earlier
         # step and has none now would keep the stale one: zero exactly those views (the set is
         # the same every step for a fixed model, so this is a host-side set compare only)
