@@ -1292,7 +1292,10 @@ ns_spmm_bwd_csc_kernel(const int32_t* __restrict__ cptr, const int32_t* __restri
     const int l = threadIdx.x % LPR, grp = threadIdx.x / LPR, gl = (threadIdx.x & 63) - l;
     float* bins = gbins[grp];
     const int64_t n_rows = sizes ? min(cap_rows, int64_t(sizes[size_idx])) : cap_rows;
-    if (hub_work) {                            // ---- hub chunks (block-uniform)
+    // ---- hub chunks (block-uniform): chunk j runs on block grid - 1 - j (+ grid, ..); at most
+    // 32768 / CH + MAXPIECE chunks (the hub_work bound), so the blocks below that range skip the
+    // piece table's scan
+    if (hub_work && int(gridDim.x) - 1 - int(blockIdx.x) < 32768 / CH + REGNN_CSC_LONG_MAXPIECE) {
         __shared__ int cpre[REGNN_CSC_LONG_MAXPIECE + 1];
         __shared__ int wsum[kBlock / 64];
         const int total = csc_chunk_scan(clong, CH, cpre, wsum);
@@ -1401,8 +1404,18 @@ ns_csc_hub_sum_kernel(const int32_t* __restrict__ clong, int chunk,
         const int npc = pc.w & 255;
         const int c0 = cpre[p], c1 = cpre[p + npc];
         for (int f = threadIdx.x; f < F; f += kBlock) {
+            // the chunk partials in chunk order; 8 loads in flight per round (the adds in the
+            // same order: one dependent load per chunk measured ~10 us per launch at F = 512)
             float sacc = 0.f;
-            for (int c = c0; c < c1; ++c) sacc += hub_work[int64_t(c) * F + f];
+            int c = c0;
+            for (; c + 8 <= c1; c += 8) {
+                float v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = hub_work[int64_t(c + k) * F + f];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sacc += v[k];
+            }
+            for (; c < c1; ++c) sacc += hub_work[int64_t(c) * F + f];
             gx[int64_t(pc.x) * F + f] = sacc;
         }
     }

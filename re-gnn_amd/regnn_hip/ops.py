@@ -1884,10 +1884,10 @@ def linear(x, w, bias=None):
     return torch.nn.functional.linear(x, w, bias)
 
 
-# products of at most SMALL_BLAS["macs"] multiply-adds (the wide NS model's layer-1 projection
-# and the [W_c; b_c; 0] W_0 composition: 512-516 x 512 x 512) run on hipBLASLt fp32 instead of the
-# x6 GEMM: a few 128 x 128 tiles over a long reduction are latency-bound there (split-K partials
-# and a reduce launch); "off": every eligible product on x6
+# products of at most SMALL_BLAS["macs"] multiply-adds without a live-row bound (the wide NS
+# model's layer-1 projection and the [W_c; b_c; 0] W_0 composition: 512-516 x 512 x 512) run on
+# hipBLASLt fp32 instead of the x6 GEMM: a few 128 x 128 tiles over a long reduction are
+# latency-bound there (split-K partials and a reduce launch); "off": every eligible product on x6
 SMALL_BLAS = {"mode": os.environ.get("REGNN_GEMM_SMALL_BLAS", "on"),
               "macs": int(os.environ.get("REGNN_GEMM_SMALL_MACS", str(1 << 28)))}
 
@@ -1900,7 +1900,9 @@ def mm(a, b, c=None, live=None):
     M, N = (a.shape[0], b.shape[1]) if a.dim() == 2 and b.dim() == 2 else (-1, -1)
     c_ok = c is None or (c.is_cuda and c.dtype == torch.float32 and
                          (tuple(c.shape) == (N,) or tuple(c.shape) == (M, N)))
-    small = (SMALL_BLAS["mode"] != "off" and M > 0 and
+    # (not with `live`: a capacity-sized operand's rows past the live count are unspecified, which
+    # the x6 kernel skips and hipBLASLt would read)
+    small = (SMALL_BLAS["mode"] != "off" and live is None and M > 0 and
              M * N * a.shape[1] <= SMALL_BLAS["macs"])
     if GEMM_X6["mode"] != "off" and gemm_x6_ok(a, b) and c_ok and not small:
         live_ok = (live is not None and live.is_cuda and live.dtype == torch.int32 and
