@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 44). */
+/* ABI version (bumped on any signature or semantics change; currently 45). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -585,6 +585,19 @@ int regnn_softmax_xent_fwd(const float* z, const int64_t* y, int32_t B, int32_t 
 int regnn_softmax_xent_bwd(const float* z, const int64_t* y, const float* lse, const float* stat,
                            const float* g, int32_t B, int32_t C, int64_t ignore, float* gz,
                            hipStream_t stream);
+/* The same loss for a capacity-sized sampled batch in one launch (ABI 45): y[i] = labels[n_id[i]]
+ * for i < sizes[0], else `ignore` (written to y[B], as regnn_ns_labels), lse / rowloss as
+ * regnn_softmax_xent_fwd, and out[2] from the last workgroup to finish (ticket: one int32, zero
+ * on entry and on return; rows summed in a fixed order). regnn_xent_bwd_colsum: gz as
+ * regnn_softmax_xent_bwd, plus gb[c] = sum over rows of gz[r][c] (fixed order) -- out_lin's bias
+ * gradient (mag/regnn_ns.py:346 out_lin + :404-405 log_softmax / nll) without a reduction of
+ * its own. */
+int regnn_ns_xent_fwd(const float* z, const int32_t* n_id, const int32_t* sizes,
+                      const int64_t* labels, int32_t B, int32_t C, int64_t ignore, int64_t* y,
+                      float* lse, float* rowloss, float* out, int32_t* ticket, hipStream_t stream);
+int regnn_xent_bwd_colsum(const float* z, const int64_t* y, const float* lse, const float* stat,
+                          const float* g, int32_t B, int32_t C, int64_t ignore, float* gz,
+                          float* gb, hipStream_t stream);
 int regnn_rel_tab(const float* rw, const float* gtab, int32_t n, float alpha, float slope,
                   float* out, hipStream_t stream);
 /* regnn_rel_tab over `count` <= 4 tables (rw[t] of n[t] entries; gtab NULL: forward, else every

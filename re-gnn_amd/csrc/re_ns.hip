@@ -1512,6 +1512,108 @@ xent_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ y,
         gr[c] = scale * (expf(zr[c] - l) - (int64_t(c) == yr ? 1.f : 0.f));
 }
 
+// The module path's loss in one launch: the labels of a capacity-sized batch (regnn_ns_labels),
+// log_softmax + nll per row (xent_rows_kernel) and, in the last workgroup to finish (an agent-scope
+// ticket, reset by that workgroup), the fixed-order mean (thread t sums rows t, t + 256, .. in
+// order, then a fixed-shape tree): mag/regnn_ns.py:404-405 over out_lin's logits.
+__global__ void __launch_bounds__(kBlock)
+ns_xent_fwd_kernel(const float* __restrict__ z, const int32_t* __restrict__ n_id,
+                   const int32_t* __restrict__ sizes, const int64_t* __restrict__ labels, int B,
+                   int C, int64_t ignore, int64_t* __restrict__ y, float* __restrict__ lse,
+                   float* __restrict__ rowloss, float* __restrict__ out, int32_t* ticket) {
+    __shared__ float ls[kBlock], lc[kBlock];
+    __shared__ int last;
+    const int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r < B) {
+        const int64_t yr = r < sizes[0] ? labels[n_id[r]] : ignore;
+        const float* zr = z + int64_t(r) * C;
+        float m = -INFINITY;
+        for (int c = lane; c < C; c += 64) m = fmaxf(m, zr[c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        float se = 0.f;
+        for (int c = lane; c < C; c += 64) se += expf(zr[c] - m);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+        const float l = m + logf(se);
+        if (lane == 0) {
+            y[r] = yr;
+            lse[r] = l;
+            rowloss[r] = yr != ignore ? l - zr[yr] : 0.f;
+            rowloss[B + r] = yr != ignore ? 1.f : 0.f;
+        }
+    }
+    // every wave releases its own rows' stores at agent scope (the barrier is workgroup scope),
+    // then one ticket per workgroup
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               int(gridDim.x) - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    float s = 0.f, n = 0.f;
+    for (int i = threadIdx.x; i < B; i += kBlock) {
+        s += rowloss[i];
+        n += rowloss[B + i];
+    }
+    ls[threadIdx.x] = s;
+    lc[threadIdx.x] = n;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if (int(threadIdx.x) < h) {
+            ls[threadIdx.x] += ls[threadIdx.x + h];
+            lc[threadIdx.x] += lc[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = ls[0] / lc[0];                // (0 / 0 = nan with no valid row, as nll_loss)
+        out[1] = lc[0];
+        __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Its backward with out_lin's bias gradient: a workgroup per 16 classes over every row (16 row
+// lanes x 16 classes), gz = g[0] / out[1] (softmax(z) - onehot(y)) (xent_bwd_kernel's value) and
+// gb[c] = sum_r gz[r][c]: row lane j sums rows j, j + 16, .. in order, the 16 lanes in order.
+__global__ void __launch_bounds__(kBlock)
+xent_bwd_colsum_kernel(const float* __restrict__ z, const int64_t* __restrict__ y,
+                       const float* __restrict__ lse, const float* __restrict__ stat,
+                       const float* __restrict__ g, int B, int C, int64_t ignore,
+                       float* __restrict__ gz, float* __restrict__ gb) {
+    __shared__ float part[16][17];
+    const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
+    const float gs = g[0] / stat[1];
+    float acc = 0.f;
+    if (c < C) {
+#pragma unroll 4
+        for (int r = rl; r < B; r += 16) {
+            const int64_t yr = y[r];
+            const float scale = yr != ignore ? gs : 0.f;
+            const float v = scale * (expf(z[int64_t(r) * C + c] - lse[r]) - (int64_t(c) == yr ? 1.f : 0.f));
+            gz[int64_t(r) * C + c] = v;
+            acc += v;
+        }
+    }
+    part[rl][cl] = acc;
+    __syncthreads();
+    if (threadIdx.x < 16 && c < C) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += part[j][threadIdx.x];
+        gb[c] = t;
+    }
+}
+
 }  // namespace regnn
 
 using namespace regnn;
@@ -1562,6 +1664,28 @@ int regnn_ns_spmm_bwd_csc(const int32_t* csc_ptr, const int32_t* csc_ent, const 
     NSC_CASE(64, 8)
 #undef NSC_CASE
     return REGNN_EUNSUPPORTED;
+}
+
+int regnn_ns_xent_fwd(const float* z, const int32_t* n_id, const int32_t* sizes,
+                      const int64_t* labels, int32_t B, int32_t C, int64_t ignore, int64_t* y,
+                      float* lse, float* rowloss, float* out, int32_t* ticket, hipStream_t stream) {
+    if (!z || !n_id || !sizes || !labels || !y || !lse || !rowloss || !out || !ticket || B <= 0 ||
+        C <= 0)
+        return REGNN_EINVAL;
+    hipLaunchKernelGGL(ns_xent_fwd_kernel, dim3(unsigned((B + 3) / 4)), dim3(kBlock), 0, stream, z,
+                       n_id, sizes, labels, B, C, ignore, y, lse, rowloss, out, ticket);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
+}
+
+int regnn_xent_bwd_colsum(const float* z, const int64_t* y, const float* lse, const float* stat,
+                          const float* g, int32_t B, int32_t C, int64_t ignore, float* gz,
+                          float* gb, hipStream_t stream) {
+    if (!z || !y || !lse || !stat || !g || !gz || !gb || B < 0 || C <= 0) return REGNN_EINVAL;
+    hipLaunchKernelGGL(xent_bwd_colsum_kernel, dim3(unsigned((C + 15) / 16)), dim3(kBlock), 0,
+                       stream, z, y, lse, stat, g, B, C, ignore, gz, gb);
+    REGNN_LAUNCH_CHECK();
+    return REGNN_OK;
 }
 
 int regnn_softmax_xent_fwd(const float* z, const int64_t* y, int32_t B, int32_t C, int64_t ignore,

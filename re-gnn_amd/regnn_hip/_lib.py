@@ -99,6 +99,8 @@ _SIG = {
     "regnn_rel_tabs": ([P, P, P, P, I32, ctypes.c_float, ctypes.c_float, P], ctypes.c_int),
     "regnn_softmax_xent_fwd": ([P, P, I32, I32, I64, P, P, P, P], ctypes.c_int),
     "regnn_softmax_xent_bwd": ([P, P, P, P, P, I32, I32, I64, P, P], ctypes.c_int),
+    "regnn_ns_xent_fwd": ([P, P, P, P, I32, I32, I64, P, P, P, P, P, P], ctypes.c_int),
+    "regnn_xent_bwd_colsum": ([P, P, P, P, P, I32, I32, I64, P, P, P], ctypes.c_int),
     "regnn_ns_hop": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                       P, P, P, P, P, P, I32, P, P, P, P, I32, P], ctypes.c_int),
     "regnn_ns_hop_typed_sums": ([P, P, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P, P, P,
@@ -135,7 +137,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 44
+ABI_VERSION = 45
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

@@ -535,9 +535,11 @@ class REGNN(torch.nn.Module):
             z = self._zrows = like.new_zeros(rows, cols)
         return z
 
-    def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx, logits=False):
+    def forward(self, n_id, x_dict, adjs, edge_type, node_type, local_node_idx, logits=False,
+                features=False):
         """-> log_softmax of out_lin (mag/regnn_ns.py:346); logits=True: out_lin's raw output
-        (a caller that forms the loss itself, e.g. NSTrainer with ops.softmax_xent)."""
+        (a caller that forms the loss itself, e.g. NSTrainer with ops.softmax_xent);
+        features=True: the last layer's output, before out_lin (NSTrainer with ops.ns_lin_xent)."""
         blk0 = tuple(adjs[0])[0] if adjs else None
         epi = self._wide_epi(blk0) if getattr(blk0, "is_ns_block", False) else None
         # every layer's relation table in one launch (and one in the backward) on device blocks
@@ -590,6 +592,8 @@ class REGNN(torch.nn.Module):
                 x = self.convs[i]((x, x_target), edge_index, edge_type[e_id], ntype)
             x = F.relu(x)
             x = F.dropout(x, p=self.dropout, training=self.training)
+        if features:
+            return x
         out = self.out_lin(x)
         return out if logits else out.log_softmax(dim=-1)
 

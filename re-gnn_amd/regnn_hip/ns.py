@@ -475,6 +475,10 @@ MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # apiece in a kernel trace at hidden 512); G > 1 -- the fused engine's lookahead groups (2G slots,
 # one fork and one join per group of up to G steps)
 MODULE_AHEAD = {"n": int(os.environ.get("REGNN_NS_MODULE_AHEAD", "4"))}
+# "on": the module path's out_lin + loss as ops.ns_lin_xent (labels, per-row loss and the mean in
+# one launch; the loss backward with out_lin's bias gradient in one); "off": out_lin, ns_labels
+# and ops.softmax_xent (A/B)
+LIN_XENT = {"mode": os.environ.get("REGNN_NS_LIN_XENT", "on")}
 # "on": the pipelined fused engine builds hop 0's transposed index on a third stream while hop 1
 # samples (regnn_ns_hop strided 2 / 3); "off" (default): in the sampler's own chain. Eager runs
 # are fine; capturing the third stream (forked from the sampler's stream, joined back before the
@@ -961,6 +965,8 @@ class NSTrainer:
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         # the module path's backward seed d loss / d loss = 1 (autograd would fill one per step)
         self._loss_seed = torch.ones((), dtype=torch.float32, device=dev)
+        # ops.ns_lin_xent's last-workgroup ticket (zero between launches)
+        self._xent_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         # engine: "fused" = regnn_nsm_step (the model's forward / loss / backward in eight HIP
         # launches), "module" = the mag.REGNN autograd path, "auto" = fused where it applies
         if engine == "fused" and why is not None:
@@ -1272,10 +1278,23 @@ class NSTrainer:
             from . import mag, ops
             fused_loss = (isinstance(self.model, mag.REGNN) and
                           os.environ.get("REGNN_NS_FUSED_LOSS", "on") != "off")
-            out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
-                             self.local_node_idx, **({"logits": True} if fused_loss else {}))
-            # the targets' labels, -100 (ignored) past the batch's live rows: one launch
-            y = ops.ns_labels(s.n_id, s.sizes, self.y_flat, B)
+            ol = getattr(self.model, "out_lin", None)
+            lin_xent = (fused_loss and LIN_XENT["mode"] != "off" and ol is not None and
+                        getattr(ol, "bias", None) is not None)
+            if lin_xent:
+                # out_lin, the labels and the loss: ops.ns_lin_xent (forward: the GEMM and one
+                # launch; backward: one launch with out_lin's bias gradient, two GEMMs)
+                h = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
+                               self.local_node_idx, features=True)
+                if h.shape[0] != B:
+                    raise RuntimeError(f"the last layer has {h.shape[0]} rows, the batch {B}")
+                loss = ops.ns_lin_xent(h, ol.weight, ol.bias, s.n_id, s.sizes, self.y_flat,
+                                       self._xent_ticket)
+            else:
+                out = self.model(n_id, self.x_dict, s.model_blocks(), None, self.node_type,
+                                 self.local_node_idx, **({"logits": True} if fused_loss else {}))
+                # the targets' labels, -100 (ignored) past the batch's live rows: one launch
+                y = ops.ns_labels(s.n_id, s.sizes, self.y_flat, B)
         else:
             # exact sizes (host sync) and the reference's (edge_index, e_id, size) adjs,
             # outermost hop first (mag/regnn_ns.py:399-403)
@@ -1285,11 +1304,11 @@ class NSTrainer:
             out = self.model(n_id, self.x_dict, adjs, self.edge_type, self.node_type,
                              self.local_node_idx)
             y = self.y_flat[n_id[:hops[0][2][1]]]
-            fused_loss = False
-        if fused_loss:                                # log_softmax + nll in one launch each way
-            loss = ops.softmax_xent(out, y)
-        else:
-            loss = F.nll_loss(out, y)                 # mean over the batch's targets
+            fused_loss = lin_xent = False
+        if not lin_xent:
+            # log_softmax + nll in one launch each way, or the reference's pair (the mean over
+            # the batch's targets)
+            loss = ops.softmax_xent(out, y) if fused_loss else F.nll_loss(out, y)
         # the gradients straight into the flat bucket: autograd.grad, then one launch copying
         # every gradient (some of them transposed views) into its bucket view (backward() would
         # accumulate with one add kernel per parameter, and _foreach_copy_ / _foreach_add_

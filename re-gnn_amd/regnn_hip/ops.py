@@ -931,6 +931,55 @@ def softmax_xent(z, y, ignore=-100):
     return _SoftmaxXent.apply(z, y, ignore)
 
 
+class _NsLinXent(torch.autograd.Function):
+    """out_lin + log_softmax + nll over a capacity-sized sampled batch: z = x W^T + b on hipBLASLt,
+    then the labels, the per-row loss and the fixed-order mean in one launch
+    (regnn_ns_xent_fwd); backward: gz and out_lin's bias gradient in one launch
+    (regnn_xent_bwd_colsum), gx = gz W and gW = gz^T x on hipBLASLt."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, n_id, sizes, labels, ticket, ignore):
+        z = torch.addmm(b, x, w.t())
+        B, C = z.shape
+        y = torch.empty(B, dtype=torch.int64, device=z.device)
+        lse = torch.empty(B, dtype=torch.float32, device=z.device)
+        rowloss = torch.empty(2 * B, dtype=torch.float32, device=z.device)
+        out = torch.empty(2, dtype=torch.float32, device=z.device)
+        L.call("regnn_ns_xent_fwd", L.ptr(z), L.ptr(n_id), L.ptr(sizes), L.ptr(labels), B, C,
+               int(ignore), L.ptr(y), L.ptr(lse), L.ptr(rowloss), L.ptr(out), L.ptr(ticket),
+               L.stream())
+        ctx.save_for_backward(x, w, z, y, lse, out)
+        ctx.ignore = int(ignore)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, z, y, lse, out = ctx.saved_tensors
+        B, C = z.shape
+        gz = torch.empty_like(z)
+        gb = torch.empty(C, dtype=torch.float32, device=z.device)
+        g = g.reshape(1).contiguous().float()
+        L.call("regnn_xent_bwd_colsum", L.ptr(z), L.ptr(y), L.ptr(lse), L.ptr(out), L.ptr(g), B, C,
+               ctx.ignore, L.ptr(gz), L.ptr(gb), L.stream())
+        gx = gz @ w if ctx.needs_input_grad[0] else None
+        gw = gz.t() @ x if ctx.needs_input_grad[1] else None
+        return gx, gw, gb, None, None, None, None, None
+
+
+def ns_lin_xent(x, w, b, n_id, sizes, labels, ticket, ignore=-100):
+    """nll_loss(log_softmax(x W^T + b), y) with y[i] = labels[n_id[i]] for i < sizes[0] and
+    `ignore` past the batch's live targets (mag/regnn_ns.py:346,404-405 over a capacity-sized
+    batch): 3 launches forward (GEMM, loss) and 3 backward (loss + bias gradient, two GEMMs).
+    x [B, K] fp32, w [C, K], b [C]; n_id / sizes int32, labels int64 device tensors; ticket: one
+    zeroed int32 device word, reused call after call."""
+    if not (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and w.dtype == torch.float32
+            and b is not None and n_id.dtype == torch.int32 and labels.dtype == torch.int64 and
+            ticket.dtype == torch.int32 and ticket.numel() >= 1):
+        raise ValueError("ns_lin_xent: fp32 [B, K] rows / weight / bias, int32 n_id, int64 "
+                         "labels, an int32 ticket")
+    return _NsLinXent.apply(x.contiguous(), w, b, n_id, sizes, labels.contiguous(), ticket, ignore)
+
+
 def ns_labels(n_id, sizes, labels, B, ignore=-100):
     """y[i] = labels[n_id[i]] for the batch's live targets i < sizes[0], else `ignore`
     (mag/regnn_ns.py:404 over a capacity-sized batch) in one launch; n_id int32, labels int64."""

@@ -360,3 +360,45 @@ def test_softmax_xent_matches_torch():
         torch.testing.assert_close(z.grad, zr.grad, rtol=1e-5, atol=1e-7)
     z = torch.randn(4, 6, device=DEV)
     assert torch.isnan(ops.softmax_xent(z, torch.full((4,), -100, device=DEV)))
+
+
+@pytest.mark.parametrize("B,K,C,live", [(512, 512, 349, 300), (512, 64, 349, 512), (37, 128, 5, 0),
+                                        (1, 64, 64, 1), (1030, 64, 17, 1000)])
+def test_ns_lin_xent_matches_torch(B, K, C, live):
+    """ops.ns_lin_xent (out_lin GEMM, then labels + per-row loss + the fixed-order mean in one
+    launch; backward: gz and out_lin's bias gradient in one launch) against F.linear +
+    log_softmax + nll_loss over labels[n_id[:B]] with the rows past sizes[0] ignored (and the
+    labelled -100 rows): loss, x / W / b gradients to 1e-5; the ticket is back at zero after each
+    call (repeat calls agree bitwise); live 0: every row ignored -> nan, as torch."""
+    import torch.nn.functional as F
+    from regnn_hip import ops
+    g0 = torch.Generator(device=DEV)
+    g0.manual_seed(11)
+    n_lab = 5000
+    labels = torch.randint(0, C, (n_lab,), device=DEV, generator=g0)
+    labels[::13] = -100
+    n_id = torch.randint(0, n_lab, (B,), device=DEV, generator=g0).to(torch.int32)
+    sizes = torch.tensor([live, 0, 0, 0], dtype=torch.int32, device=DEV)
+    x = torch.randn(B, K, device=DEV, generator=g0).requires_grad_(True)
+    lin = torch.nn.Linear(K, C).to(DEV)
+    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    y = labels[n_id.long()].clone()
+    y[live:] = -100
+    xr = x.detach().clone().requires_grad_(True)
+    wr = lin.weight.detach().clone().requires_grad_(True)
+    br = lin.bias.detach().clone().requires_grad_(True)
+    ref = F.nll_loss(F.linear(xr, wr, br).log_softmax(-1), y)
+    loss = ops.ns_lin_xent(x, lin.weight, lin.bias, n_id, sizes, labels, ticket)
+    if live == 0 or bool((y == -100).all()):
+        assert torch.isnan(loss) and torch.isnan(ref)
+        return
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    loss.backward()
+    ref.backward()
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lin.weight.grad, wr.grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lin.bias.grad, br.grad, rtol=1e-5, atol=1e-6)
+    torch.cuda.synchronize()
+    assert int(ticket.item()) == 0
+    again = ops.ns_lin_xent(x, lin.weight, lin.bias, n_id, sizes, labels, ticket)
+    assert float(again) == float(loss) and int(ticket.item()) == 0
