@@ -17,4 +17,4 @@ python tools/trace_window.py gpurun_out/ev_prof_ns/run_kernel_trace.csv agg0w_ke
 tools/gpu_step.sh 400 gpurun_out/ev_b_h512.log python bench.py --workload ns --hidden 512 --no-full-batch --no-cpu-baseline || exit 1
 grep '^{' gpurun_out/ev_b_h512.log > gpurun_out/ev_b_h512.json; cut -c1-200 gpurun_out/ev_b_h512.json
 tools/gpu_step.sh 400 gpurun_out/ev_prof_h512.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ev_prof_h512 -o run -- python bench.py --workload ns --hidden 512 --no-full-batch --no-cpu-baseline --steps 30 || exit 1
-python tools/trace_window.py gpurun_out/ev_prof_h512/run_kernel_trace.csv nsagg::slot_agg_kernel 24 > gpurun_out/ev_h512_window.txt; head -3 gpurun_out/ev_h512_window.txt
+python tools/trace_window.py gpurun_out/ev_prof_h512/run_kernel_trace.csv nsagg::slot_agg_kernel 24 --between > gpurun_out/ev_h512_window.txt; head -3 gpurun_out/ev_h512_window.txt
