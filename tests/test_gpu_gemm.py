@@ -180,3 +180,35 @@ def test_mm_live_rows_bitwise(live, hint, monkeypatch):
     ga = gout.double() @ b0.double().t()
     err = (outs[1][1].double() - ga).abs().max().item() / max(1.0, ga.abs().max().item())
     assert err <= 1e-5, err
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K,live", [(13312, 512, 516, 4900), (13312, 516, 512, 4900),
+                                        (333, 132, 100, 333), (65, 4, 36, 40), (64, 512, 32, 1),
+                                        (200, 349, 512, 129)])
+def test_gemm_x6_row_tilings_bitwise(ta, tb, M, N, K, live, monkeypatch):
+    """a product with a live-row count runs on 64-row tiles (REGNN_GEMM_BM64, no split-K), every
+    other on 128-row tiles: each C element sums the same k-steps and products in the same order,
+    so the two tilings give the same bits (rows past the live count: beta C either way)."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * N + 5 * K + live)
+    a = torch.randn(*((K, M) if ta else (M, K)), generator=g, device=DEV)
+    b = torch.randn(*((N, K) if tb else (K, N)), generator=g, device=DEV)
+    if ta:
+        a[:, live:] = 0
+    else:
+        a[live:] = 0
+    if not (ops.gemm_x6_ok(a) and ops.gemm_x6_ok(b)):
+        pytest.skip("contiguous dimension not a multiple of 4")
+    monkeypatch.setattr(ops, "_gemm_splits", lambda *_: 1)
+    cnt = torch.tensor([live], dtype=torch.int32, device=DEV)
+    outs = {}
+    for mode in ("on", "off"):
+        monkeypatch.setenv("REGNN_GEMM_BM64", mode)
+        outs[mode] = ops.gemm_x6(a, b, trans_a=ta, trans_b=tb, m_live=cnt)
+    full = ops.gemm_x6(a, b, trans_a=ta, trans_b=tb)
+    assert torch.equal(outs["on"], outs["off"])
+    assert torch.equal(outs["on"], full)
+    ref, mag = _ref(a, b, ta, tb)
+    err = (outs["on"].double() - ref).abs()
+    assert (err <= 2e-6 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
