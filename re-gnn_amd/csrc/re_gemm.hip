@@ -6,8 +6,9 @@
 // (mag/regnn_layers.py:101-107 by linearity), the other convs' x @ W, out_lin, and their
 // backward products.
 //
-// Block tile 128 x 128, k-step 32, 256 threads: wave w computes rows 64 (w >> 1) .., columns
-// 64 (w & 1) .. as 4 x 4 MFMA tiles (96 MFMAs per k-step). The next k-step's operands are
+// Block tile 128 x 128 (or 64 x 128 for a live-row-bounded product: gemm_x6_kernel's TBM), k-step
+// 32, 256 threads: wave w computes rows 64 (w >> 1) .., columns 64 (w & 1) .. as 4 x 4 MFMA tiles
+// (96 MFMAs per k-step; 2 x 4 at 64 rows). The next k-step's operands are
 // requested before this step's MFMAs (registers) and split into the three bf16 parts on their
 // way into LDS. LDS rows of 32 bf16 padded to 40 (80 bytes: the 16 rows of an 8-element
 // fragment read fall on distinct banks).
