@@ -975,7 +975,9 @@ int regnn_gemm_x6(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
 /* m_live / k_live (ABI 41; device int32 counts, may be NULL): op(A)'s rows m >= *m_live, and the
  * k >= *k_live columns of op(A) / rows of op(B), are zero (the unused rows of a capacity-sized
  * sampled block): the kernel skips their products (C rows >= *m_live get beta C) -- the same C,
- * with the work of the live rows only. */
+ * with the work of the live rows only. With m_live and splits == 1 the launch uses 64-row tiles
+ * (twice the live tiles; env REGNN_GEMM_BM64=off: 128): every C element sums the same k-steps and
+ * products in the same order, so the bits are those of the 128-row tiling. */
 
 /* Several strided 2-D fp32 copies in one launch: dst[i * cols + j] = src[i * s0 + j * s1] for
  * each descriptor (the module path's parameter gradients, some of them transposed views, into the
