@@ -41,7 +41,7 @@ enum { REGNN_F32 = 0, REGNN_BF16 = 1 };
  * <rows, gx_raw> / out_scale (out_scale > 0). Not combinable with edge_grad or the _next call. */
 enum { REGNN_SELF_PRESCALED = 0x100 };
 
-/* ABI version (bumped on any signature or semantics change; currently 45). */
+/* ABI version (bumped on any signature or semantics change; currently 46). */
 int regnn_abi_version(void);
 
 /* Tuning knob (process-wide, for A/B measurements; defaults are the shipped configuration).
@@ -996,16 +996,20 @@ int regnn_copy2d_many(const regnn_copy2d* d, int32_t n, hipStream_t stream);
  * y. Dropout (p_drop > 0): the fused NS step's mask spec (regnn_nsm_step) keyed on the sampler
  * state and `layer`. Backward from gy: gx = rs[v] d a (rs NULL: 1), gres = d a (optional), and
  * slab [regnn_wide_ln_slab_rows(n, H)][3 H] of per-block partials [sum d a | sum gy' xhat | sum
- * gy'] (the bias, LN weight and LN bias gradients after regnn_rel_reduce). 16-byte aligned rows. */
+ * gy'] (the bias, LN weight and LN bias gradients after regnn_rel_reduce). 16-byte aligned rows.
+ * live (ABI 46; device int32 count, may be NULL): only rows v < *live are read (a capacity-sized
+ * sampled block whose later rows nothing reads): the forward leaves a / stats / y past it as they
+ * were, the backward writes zeros to gx (and gres) there and skips those rows' partials (exact
+ * zeros for zero gy). */
 int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, const float* bias,
                       const float* res, const float* gamma, const float* beta,
                       const int64_t* state, int32_t layer, float p_drop, float* a, float* stats,
-                      float* y, hipStream_t stream);
+                      float* y, const int32_t* live, hipStream_t stream);
 int64_t regnn_wide_ln_slab_rows(int64_t n, int32_t H);
 int regnn_wide_ln_bwd(int64_t n, int32_t H, const float* gy, const float* a, const float* stats,
                       const float* rs, const float* gamma, const float* beta,
                       const int64_t* state, int32_t layer, float p_drop, float* gx, float* gres,
-                      float* slab, hipStream_t stream);
+                      float* slab, const int32_t* live, hipStream_t stream);
 
 /* ---- Per-node-type input rows of the ogbn-mag path (mag/regnn_ns.py:300-326, group_input) ----
  * The reference builds the batch's input matrix with one boolean mask per node type (a host

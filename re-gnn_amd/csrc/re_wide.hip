@@ -26,7 +26,14 @@ struct LnArgs {
     float* a; float* stats; float* y;                  // forward outputs
     const float* a_in; const float* stats_in;          // backward inputs
     const float* gy; float* gx; float* gres; float* slab;   // backward
+    const int32_t* live;                               // rows >= *live skipped (may be null)
 };
+
+// the rows a launch covers: n, or the device count of live rows (a capacity-sized block whose
+// rows past it nothing reads; a skipped row would only add exact zeros to the backward partials)
+__device__ __forceinline__ int64_t ln_rows(const LnArgs& A) {
+    return A.live ? min(A.n, int64_t(*A.live)) : A.n;
+}
 
 template <int LPR>
 __device__ __forceinline__ float row_sum(float v) {
@@ -57,7 +64,8 @@ __global__ void __launch_bounds__(kBlock) ln_fwd_kernel(LnArgs A) {
         gb[j] = *reinterpret_cast<const float4*>(A.beta + c);
         bs[j] = A.bias ? *reinterpret_cast<const float4*>(A.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int64_t v = int64_t(blockIdx.x) * RPB + g; v < A.n; v += int64_t(gridDim.x) * RPB) {
+    const int64_t n = ln_rows(A);
+    for (int64_t v = int64_t(blockIdx.x) * RPB + g; v < n; v += int64_t(gridDim.x) * RPB) {
         const float s = A.rs ? A.rs[v] : 1.f;
         float a[VPL][4];
         float sum = 0.f;
@@ -116,7 +124,8 @@ __global__ void __launch_bounds__(kBlock) ln_bwd_kernel(LnArgs A) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) pa[j][k] = pw[j][k] = pb[j][k] = 0.f;
     }
-    for (int64_t v = int64_t(blockIdx.x) * RPB + g; v < A.n; v += int64_t(gridDim.x) * RPB) {
+    const int64_t n = ln_rows(A);
+    for (int64_t v = int64_t(blockIdx.x) * RPB + g; v < n; v += int64_t(gridDim.x) * RPB) {
         const float2 st = reinterpret_cast<const float2*>(A.stats_in)[v];
         const float s = A.rs ? A.rs[v] : 1.f;
         float xh[VPL][4], gx[VPL][4];
@@ -155,6 +164,16 @@ __global__ void __launch_bounds__(kBlock) ln_bwd_kernel(LnArgs A) {
             }
             *reinterpret_cast<float4*>(A.gx + v * H + c) = make_float4(s * ga[0], s * ga[1], s * ga[2], s * ga[3]);
             if (A.gres) *reinterpret_cast<float4*>(A.gres + v * H + c) = make_float4(ga[0], ga[1], ga[2], ga[3]);
+        }
+    }
+    // rows past the live count: zero gradients (the x6 GEMM that reads gx takes rows past its
+    // m_live / k_live as zeros: its last k-step spans a few of them)
+    for (int64_t v = n + int64_t(blockIdx.x) * RPB + g; v < A.n; v += int64_t(gridDim.x) * RPB) {
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int c = 4 * (l + LPR * j);
+            *reinterpret_cast<float4*>(A.gx + v * H + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (A.gres) *reinterpret_cast<float4*>(A.gres + v * H + c) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
     // the row groups' partials in LDS, summed in group order
@@ -260,7 +279,7 @@ int regnn_rel_tabs(const float* const* rw, const float* const* gtab, float* cons
 int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, const float* bias,
                       const float* res, const float* gamma, const float* beta,
                       const int64_t* state, int32_t layer, float p_drop, float* a, float* stats,
-                      float* y, hipStream_t stream) {
+                      float* y, const int32_t* live, hipStream_t stream) {
     if (n < 0 || !x || !gamma || !beta || !a || !stats || !y || !(p_drop >= 0.f && p_drop < 1.f) ||
         (p_drop > 0.f && !state))
         return REGNN_EINVAL;
@@ -271,7 +290,7 @@ int regnn_wide_ln_fwd(int64_t n, int32_t H, const float* x, const float* rs, con
     LnArgs A{};
     A.n = n; A.H = H; A.x = x; A.rs = rs; A.bias = bias; A.res = res; A.gamma = gamma; A.beta = beta;
     A.state = state; A.layer = layer; A.drop = make_drop(p_drop);
-    A.a = a; A.stats = stats; A.y = y;
+    A.a = a; A.stats = stats; A.y = y; A.live = live;
     const int rpb = kBlock / (H >= 256 ? 64 : H / 4);
     int64_t blocks = (n + rpb - 1) / rpb;
     if (blocks > kMaxGrid) blocks = kMaxGrid;
@@ -288,7 +307,7 @@ int64_t regnn_wide_ln_slab_rows(int64_t n, int32_t H) {
 int regnn_wide_ln_bwd(int64_t n, int32_t H, const float* gy, const float* a, const float* stats,
                       const float* rs, const float* gamma, const float* beta,
                       const int64_t* state, int32_t layer, float p_drop, float* gx, float* gres,
-                      float* slab, hipStream_t stream) {
+                      float* slab, const int32_t* live, hipStream_t stream) {
     if (n < 0 || !gy || !a || !stats || !gamma || !beta || !gx || !slab ||
         !(p_drop >= 0.f && p_drop < 1.f) || (p_drop > 0.f && !state))
         return REGNN_EINVAL;
@@ -298,7 +317,7 @@ int regnn_wide_ln_bwd(int64_t n, int32_t H, const float* gy, const float* a, con
     LnArgs A{};
     A.n = n; A.H = H; A.gy = gy; A.a_in = a; A.stats_in = stats; A.rs = rs; A.gamma = gamma; A.beta = beta;
     A.state = state; A.layer = layer; A.drop = make_drop(p_drop);
-    A.gx = gx; A.gres = gres; A.slab = slab;
+    A.gx = gx; A.gres = gres; A.slab = slab; A.live = live;
     return ln_launch(A, true, int(regnn_wide_ln_slab_rows(n, H)), stream);
 }
 

@@ -3,4 +3,4 @@
 // summaries, build.kernel_hash) unchanged.
 #include "regnn_common.h"
 
-extern "C" int regnn_abi_version(void) { return 45; }
+extern "C" int regnn_abi_version(void) { return 46; }

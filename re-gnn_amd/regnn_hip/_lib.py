@@ -30,9 +30,9 @@ _SIG = {
     "regnn_abi_version": ([], ctypes.c_int),
     "regnn_gemm_x6_work_floats": ([I64, I64, I32], I64),
     "regnn_copy2d_many": ([P, I32, P], ctypes.c_int),
-    "regnn_wide_ln_fwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),
+    "regnn_wide_ln_fwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P, P], ctypes.c_int),
     "regnn_wide_ln_slab_rows": ([I64, I32], I64),
-    "regnn_wide_ln_bwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P], ctypes.c_int),
+    "regnn_wide_ln_bwd": ([I64, I32, P, P, P, P, P, P, P, I32, F32, P, P, P, P, P], ctypes.c_int),
     "regnn_gemm_x6": ([I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, F32, P, I32, P, P, P],
                       ctypes.c_int),
     "regnn_slab_rows": ([I64, I32], I64),
@@ -137,7 +137,7 @@ for _name, (_args, _ret) in _SIG.items():
     _f.restype = _ret
 
 EXPORTED = tuple(_SIG)
-ABI_VERSION = 45
+ABI_VERSION = 46
 # (an A/B build of an older tree through REGNN_LIB may trail the ABI: a timing run only)
 if _so.regnn_abi_version() != ABI_VERSION and not os.environ.get("REGNN_LIB"):
     raise ImportError(f"regnn_hip: ABI mismatch ({_so.regnn_abi_version()} != {ABI_VERSION}); "

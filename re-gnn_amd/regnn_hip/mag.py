@@ -519,8 +519,13 @@ class REGNN(torch.nn.Module):
             res = ops.mm(x_t, conv.weight)
         if epi is not None and ops.wide_ln_ok(agg, conv.norm, conv.bias):
             # mean + bias + residual, LayerNorm, relu, dropout in one launch (:341-343)
+            # (only the block's live rows: without residuals every consumer of layer 0's rows is
+            # live-bounded -- layer 1 aggregates sampled rows, the GEMMs take m_live / k_live; a
+            # residual reads the first B rows, which a short last batch may leave unformed)
+            live = (getattr(blk, "live_rows", None)
+                    if not any(getattr(c, "residual", False) for c in self.convs) else None)
             return ops.wide_ln_act(agg, conv.bias, conv.norm, epi[0], epi[1], 0,
-                                   rs=blk.inv[:n], res=res), True
+                                   rs=blk.inv[:n], res=res, live=live), True
         out = torch.addcmul(conv.bias, agg, blk.inv[:n].view(n, 1))           # mean + bias
         if res is not None:
             out = out + res

@@ -1966,23 +1966,28 @@ def mm(a, b, c=None, live=None):
 WIDE_LN_WIDTHS = (64, 128, 256, 512, 1024)
 
 
+# "on": a live-row count reaches regnn_wide_ln_fwd / _bwd (layer 0 of the wide NS model: ~4.9 k
+# live rows of a 13 312-row block at mag-10x); "off": every row formed (A/B)
+WIDE_LN_LIVE = {"mode": os.environ.get("REGNN_WIDE_LN_LIVE", "on")}
+
+
 class _WideLn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, res, gamma, beta, rs, state, layer, p):
+    def forward(ctx, x, bias, res, gamma, beta, rs, state, layer, p, live):
         n, H = x.shape
         a = torch.empty_like(x)
         y = torch.empty_like(x)
         stats = torch.empty(n, 2, dtype=torch.float32, device=x.device)
         L.call("regnn_wide_ln_fwd", n, H, L.ptr(x), L.ptr(rs), L.ptr(bias), L.ptr(res),
                L.ptr(gamma), L.ptr(beta), L.ptr(state), int(layer), float(p), L.ptr(a),
-               L.ptr(stats), L.ptr(y), L.stream())
-        ctx.save_for_backward(a, stats, rs, gamma, beta, state)
+               L.ptr(stats), L.ptr(y), L.ptr(live), L.stream())
+        ctx.save_for_backward(a, stats, rs, gamma, beta, state, live)
         ctx.layer, ctx.p, ctx.has_res = int(layer), float(p), res is not None
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        a, stats, rs, gamma, beta, state = ctx.saved_tensors
+        a, stats, rs, gamma, beta, state, live = ctx.saved_tensors
         n, H = a.shape
         gy = gy.contiguous()
         if gy.data_ptr() % 16:                 # the kernel's float4 rows need 16-byte alignment
@@ -1993,10 +1998,10 @@ class _WideLn(torch.autograd.Function):
         slab = torch.empty(rows, 3 * H, dtype=torch.float32, device=a.device)
         L.call("regnn_wide_ln_bwd", n, H, L.ptr(gy), L.ptr(a), L.ptr(stats), L.ptr(rs),
                L.ptr(gamma), L.ptr(beta), L.ptr(state), ctx.layer, ctx.p, L.ptr(gx), L.ptr(gres),
-               L.ptr(slab), L.stream())
+               L.ptr(slab), L.ptr(live), L.stream())
         sums = _reduce(slab, 3 * H)
         g_bias, g_gamma, g_beta = sums[:H], sums[H:2 * H], sums[2 * H:]
-        return (gx, g_bias, gres, g_gamma, g_beta, None, None, None, None)
+        return (gx, g_bias, gres, g_gamma, g_beta, None, None, None, None, None)
 
 
 def wide_ln_ok(x, ln, bias=None):
@@ -2012,9 +2017,12 @@ def _wide_operands_ok(*ts):
     return all(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in ts)
 
 
-def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None):
+def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None, live=None):
     """dropout(relu(LayerNorm(rs * x + bias + res))) in one launch (regnn_wide_ln_fwd), the
-    dropout mask the fused NS step's spec keyed on the sampler `state` and `layer`."""
+    dropout mask the fused NS step's spec keyed on the sampler `state` and `layer`. live: a
+    one-element int32 device count; only rows below it are formed (forward) and differentiated
+    (backward) -- for a capacity-sized block whose later rows no consumer reads (their outputs
+    and gradients are left unspecified). Not with `res` (its gradient rows would be read)."""
     if p > 0 and state is None:
         raise ValueError("wide_ln_act: dropout needs the sampler state (its mask key)")
     if res is not None:
@@ -2024,5 +2032,8 @@ def wide_ln_act(x, bias, ln, p=0.0, state=None, layer=0, rs=None, res=None):
     if not _wide_operands_ok(bias, ln.weight, ln.bias):
         raise ValueError("wide_ln_act: bias / LayerNorm weight and bias must be contiguous and "
                          "16-byte aligned (check wide_ln_ok first)")
+    if live is not None and (res is not None or not live.is_cuda or live.dtype != torch.int32 or
+                             live.numel() != 1 or WIDE_LN_LIVE["mode"] == "off"):
+        live = None
     return _WideLn.apply(x, bias, res, ln.weight, ln.bias,
-                         rs, state if p > 0 else None, layer, float(p))
+                         rs, state if p > 0 else None, layer, float(p), live)

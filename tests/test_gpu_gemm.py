@@ -212,3 +212,36 @@ def test_gemm_x6_row_tilings_bitwise(ta, tb, M, N, K, live, monkeypatch):
     ref, mag = _ref(a, b, ta, tb)
     err = (outs["on"].double() - ref).abs()
     assert (err <= 2e-6 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+
+
+@pytest.mark.parametrize("H,dropout", [(512, 0.5), (128, 0.0)])
+def test_wide_ln_act_live_rows_bitwise(H, dropout):
+    """ops.wide_ln_act with a live-row count (layer 0 of the wide NS model): the live rows'
+    outputs and input gradients, and the bias / LayerNorm gradients, bitwise those of the
+    all-rows launch when the incoming gradient is zero past the live rows (the skipped rows only
+    added exact zeros to the partials)."""
+    from regnn_hip import ops
+    g = torch.Generator(device=DEV).manual_seed(H)
+    n, live = 13312, 4900
+    x0 = torch.randn(n, H, generator=g, device=DEV)
+    x0[live:] = 0
+    rs = torch.rand(n, generator=g, device=DEV) + 0.5
+    gy = torch.randn(n, H, generator=g, device=DEV)
+    gy[live:] = 0
+    state = torch.tensor([3, 5, 7, 9, 11, 0, 0, 0], dtype=torch.int64, device=DEV)
+    cnt = torch.tensor([live], dtype=torch.int32, device=DEV)
+    outs = []
+    for lv in (None, cnt):
+        ln = torch.nn.LayerNorm(H).to(DEV)
+        with torch.no_grad():
+            ln.weight.copy_(torch.linspace(0.5, 1.5, H, device=DEV))
+            ln.bias.copy_(torch.linspace(-0.2, 0.2, H, device=DEV))
+        bias = torch.linspace(-0.1, 0.1, H, device=DEV).requires_grad_(True)
+        x = x0.clone().requires_grad_(True)
+        y = ops.wide_ln_act(x, bias, ln, p=dropout, state=state, layer=0, rs=rs, live=lv)
+        y.backward(gy)
+        outs.append((y[:live].detach().clone(), x.grad.clone(), bias.grad.clone(),
+                     ln.weight.grad.clone(), ln.bias.grad.clone()))
+    for name, a, b in zip(["y", "gx", "g_bias", "g_gamma", "g_beta"], outs[0], outs[1]):
+        assert torch.equal(a, b), name
+    assert not outs[1][1][live:].any()             # the dead rows' gradient: zeros
