@@ -569,6 +569,11 @@ NS_CSC = {"mode": "auto"}
 # "on": the CSC gather's hub rows in chunks over the grid (regnn_ns_spmm_bwd_csc hub_work);
 # "off": a workgroup per hub row
 NS_CSC_CHUNKED = {"mode": os.environ.get("REGNN_NS_CSC_CHUNKED", "on")}
+# workgroups of regnn_ns_spmm_bwd_csc with relation dots (one relation-slab row each; 0:
+# L.slab_rows() = 4096). 1024: each row group takes ~3 of a 13 312-row block's rows instead of
+# one, and the slab reduce reads a quarter of the rows -- hidden 512, mag-10x: 416.2-418.7 against
+# 424.5-425.4 us per step (512: 418.3-420.3, 2048: 420.8-420.9)
+CSC_BWD_ROWS = {"n": int(os.environ.get("REGNN_NS_CSC_BWD_ROWS", "1024"))}
 # include/regnn_hip.h REGNN_CSC_LONG_INTS (the sampler's csc_long with the hub piece table)
 CSC_LONG_INTS = ((32768 // 17 + 1 + 2) + 3) // 4 * 4 + 4 * (32768 // 1024 + 32768 // 17 + 1)  # PIECE 1024
 _HUB_WORK = {}
@@ -629,7 +634,9 @@ class _NsSpmm(torch.autograd.Function):
             # a gather over the sampler's transposed index: every row written once, no atomics
             cptr, cent, clong, sizes, size_idx = csc
             gx = torch.empty_like(x)
-            rows = L.slab_rows()
+            # the launch's workgroups = its relation-slab rows (grid-stride over the rows and the
+            # hub chunks); REGNN_NS_CSC_BWD_ROWS caps them (A/B)
+            rows = min(L.slab_rows(), CSC_BWD_ROWS["n"]) if CSC_BWD_ROWS["n"] > 0 else L.slab_rows()
             slab = (torch.empty(rows, n_rel, dtype=torch.float32, device=x.device)
                     if (need_tab and t is not None) else None)
             # the hub rows chunked over the grid (a workgroup per 8 entries per row group
