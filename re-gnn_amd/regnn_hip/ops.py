@@ -574,6 +574,10 @@ NS_CSC_CHUNKED = {"mode": os.environ.get("REGNN_NS_CSC_CHUNKED", "on")}
 # one, and the slab reduce reads a quarter of the rows -- hidden 512, mag-10x: 416.2-418.7 against
 # 424.5-425.4 us per step (512: 418.3-420.3, 2048: 420.8-420.9)
 CSC_BWD_ROWS = {"n": int(os.environ.get("REGNN_NS_CSC_BWD_ROWS", "1024"))}
+# workgroups of regnn_ns_slot_agg_bwd (one relation-slab row each; 0: a row per 8 of the block's
+# capacity rows, at most L.slab_rows(): 1664 at mag-10x, 414.2-414.6 us per step at hidden 512
+# against 417.6 with 1024 and 419.1-419.7 with 512)
+SLOT_BWD_ROWS = {"n": int(os.environ.get("REGNN_NS_SLOT_BWD_ROWS", "0"))}
 # include/regnn_hip.h REGNN_CSC_LONG_INTS (the sampler's csc_long with the hub piece table)
 CSC_LONG_INTS = ((32768 // 17 + 1 + 2) + 3) // 4 * 4 + 4 * (32768 // 1024 + 32768 // 17 + 1)  # PIECE 1024
 _HUB_WORK = {}
@@ -777,6 +781,8 @@ class _NsSlotAgg(torch.autograd.Function):
         cap, T, K = U.shape
         g = g.contiguous().float()
         rows = int(min(L.slab_rows(), max(1, -(-cap // 8))))   # 8 row groups per block
+        if SLOT_BWD_ROWS["n"] > 0:
+            rows = min(rows, SLOT_BWD_ROWS["n"])
         slab = torch.empty(rows, ctx.n_rel, dtype=torch.float32, device=U.device)
         with timed("ns_slot_agg_bwd"):
             L.call("regnn_ns_slot_agg_bwd", L.ptr(ctx.blk.live_rows), 0, L.ptr(U), L.ptr(cnt),
