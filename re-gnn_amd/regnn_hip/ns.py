@@ -473,8 +473,9 @@ MODULE_PIPELINE = {"mode": os.environ.get("REGNN_NS_MODULE_PIPELINE", "on")}
 # the module path's sampling lookahead (REGNN_NS_MODULE_AHEAD): 1 -- the next batch sampled beside
 # each step, a fork and a join per step (each a marker on the model's queue: ~5 us of queue idle
 # apiece in a kernel trace at hidden 512); G > 1 -- the fused engine's lookahead groups (2G slots,
-# one fork and one join per group of up to G steps)
-MODULE_AHEAD = {"n": int(os.environ.get("REGNN_NS_MODULE_AHEAD", "4"))}
+# one fork and one join per group of up to G steps); 8 measured 412.3-412.5 against 416.7-416.8
+# us per step for 4 at hidden 512, mag-10x (after this round's other module-path changes)
+MODULE_AHEAD = {"n": int(os.environ.get("REGNN_NS_MODULE_AHEAD", "8"))}
 # "on": the module path's out_lin + loss as ops.ns_lin_xent (labels, per-row loss and the mean in
 # one launch; the loss backward with out_lin's bias gradient in one); "off": out_lin, ns_labels
 # and ops.softmax_xent (A/B)
